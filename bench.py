@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""hipzap headline benchmark: ResNet-50 bs=1 serving throughput (whole node) + cold start.
+
+Metric (BASELINE.json): inferences/sec (whole node) + p50 cold-start ms, ResNet-50 bs=1 at
+1/2/4/8 GPU. One process per GPU (torchrun); every rank is a serving replica:
+  cold start  rank 0 torch.load()s a standard state_dict checkpoint (random-init weights of
+              the real ResNet-50 architecture, written untimed beforehand) -> packs/folds BN
+              on its GPU -> RCCL-broadcasts the packed blob to the other ranks -> every rank
+              plans its arena, binds native programs, captures hipGraphs -> first inference.
+  warm step   every rank serves ``--streams`` independent bs=1 requests concurrently: each is
+              one hipGraph replay that includes the pinned H2D of the fp32 image, preprocess,
+              53 fused conv kernels, pools, FC and the D2H of the logits.
+Timed region: K steps bracketed by barrier + cuda.synchronize on both sides; the slowest
+rank's time is used. value = world * streams * K / t  (weak scaling: fixed work per GPU).
+"""
+import time
+
+T_PROC0 = time.time()
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import statistics  # noqa: E402
+import sys  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "inferences/sec (whole node) + p50 cold-start ms, ResNet-50 bs=1 at 1/2/4/8 GPU"
+BASELINE_INF_S = 27.2  # reference execution model (CPU PyTorch in a WSGI handler), ResNet-50 bs=1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 4)),
+                    help="concurrent bs=1 request contexts per GPU")
+    ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
+    ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds for p50")
+    ap.add_argument("--compare-torch", action="store_true", help="also time PyTorch/MIOpen bf16 + CUDA graph")
+    ap.add_argument("--no-capture", action="store_true")
+    ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
+    return ap.parse_args()
+
+
+def write_checkpoint(path, model):
+    from hipzap.models import registry
+    from hipzap.models.resnet import randomize_bn
+    torch.manual_seed(0)
+    m = randomize_bn(registry.get(model).make_model()).eval()
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + f".tmp{os.getpid()}"
+    torch.save(m.state_dict(), tmp)
+    os.replace(tmp, path)
+
+
+def torch_reference_throughput(model, device, iters=200):
+    """Stock PyTorch path on the same GPU: bf16 channels_last + CUDA(HIP) graph, bs=1."""
+    from hipzap.models import registry
+    m = registry.get(model).make_model().eval().to(device=device, dtype=torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = torch.randn(1, 3, 224, 224, device=device, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    s = torch.cuda.Stream(device)
+    with torch.no_grad(), torch.cuda.stream(s):
+        for _ in range(5):
+            m(x)
+    torch.cuda.synchronize(device)
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        y = m(x)
+    torch.cuda.synchronize(device)
+    for _ in range(20):
+        g.replay()
+    torch.cuda.synchronize(device)
+    t = time.perf_counter()
+    for _ in range(iters):
+        g.replay()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t
+    del y
+    return iters / dt
+
+
+def main():
+    args = parse()
+    from hipzap.engine.engine import Engine
+    from hipzap.models import registry
+    from hipzap.parallel.comm import broadcast_params, env_rank, init_distributed, is_dist
+
+    rank, world, local = env_rank()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    init_distributed(device=device)
+    adapter = registry.get(args.model)
+    ckpt = os.path.join(args.ckpt_dir, f"{args.model}_seed0.pth")
+    if rank == 0 and not os.path.exists(ckpt):
+        write_checkpoint(ckpt, args.model)
+    tuned = None
+    tpath = args.tuned or os.path.join(os.path.dirname(os.path.abspath(__file__)), "hipzap", "tuning",
+                                       f"{args.model}_bs{args.batch}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tuned = json.load(f)
+    if is_dist():
+        dist.barrier()
+
+    def cold_start():
+        t0 = time.perf_counter()
+        timings = {}
+        if rank == 0:
+            ta = time.perf_counter()
+            sd = torch.load(ckpt, map_location="cpu", weights_only=True)
+            timings["load_ms"] = (time.perf_counter() - ta) * 1e3
+            ta = time.perf_counter()
+            sd = {k: v.to(device, non_blocking=True) for k, v in sd.items()}
+            params, arch_kw = adapter.pack(sd, device)
+            torch.cuda.synchronize(device)
+            timings["pack_ms"] = (time.perf_counter() - ta) * 1e3
+        else:
+            params, arch_kw = None, None
+        meta, meta_kw = adapter.meta_params()
+        arch_kw = arch_kw or meta_kw
+        ta = time.perf_counter()
+        params = broadcast_params(params, meta, device)
+        torch.cuda.synchronize(device)
+        timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
+        eng = Engine(args.model, params, device, batch=args.batch, num_contexts=args.streams,
+                     capture=not args.no_capture, tuned=tuned, arch_kw=arch_kw, timings=timings, host_io=True)
+        x = adapter.example_input(args.batch)
+        out = eng.infer(x)
+        cold_ms = (time.perf_counter() - t0) * 1e3
+        eng.timings["first_infer_total_ms"] = cold_ms
+        return eng, out, cold_ms
+
+    eng, out, cold_first = cold_start()
+    cold_process_ms = (time.time() - T_PROC0) * 1e3
+    colds = [cold_first]
+    for _ in range(args.cold_runs):
+        del eng
+        torch.cuda.synchronize(device)
+        eng, out, c = cold_start()
+        colds.append(c)
+    assert torch.isfinite(out).all(), "non-finite logits"
+
+    # single-request latency (one context, full round trip incl. host copies), p50
+    x = adapter.example_input(args.batch)
+    lat = []
+    for i in range(60):
+        t = time.perf_counter()
+        eng.infer(x)
+        lat.append((time.perf_counter() - t) * 1e3)
+    lat_p50 = statistics.median(lat[10:])
+
+    # throughput: warmup then K timed steps, each step = `streams` concurrent bs=1 requests
+    if args.warmup:
+        eng.bench(args.warmup)
+    if is_dist():
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    eng.bench(args.steps)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    if is_dist():
+        dist.barrier()
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    inf = world * args.streams * args.batch * args.steps
+    value = inf / dt
+    torch_ref = None
+    if args.compare_torch and rank == 0:
+        try:
+            torch_ref = torch_reference_throughput(args.model, device)
+        except Exception as e:  # comparison only
+            print(f"torch reference failed: {e}", file=sys.stderr)
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 2), "unit": "inferences/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_INF_S, 2), "dtype": "bf16",
+            "data": "synthetic (random-init ResNet-50 weights via torch.save/torch.load, random fp32 images)",
+            "config": {"model": "ResNet-50", "global_batch": args.batch * world, "seq_len": None,
+                       "parallelism": f"dp{world}", "request_batch": args.batch,
+                       "streams_per_gpu": args.streams, "hipgraph": not args.no_capture},
+            "cold_start_ms_p50": round(statistics.median(colds), 2),
+            "cold_start_ms_first": round(cold_first, 2),
+            "cold_start_process_ms": round(cold_process_ms, 2),
+            "cold_start_breakdown_ms": {k: round(v, 2) for k, v in eng.timings.items()},
+            "latency_ms_p50_single": round(lat_p50, 4),
+            "baseline_note": "vs_baseline against BASELINE.md sandbox-CPU ResNet-50 bs=1 (27.2 inf/s); "
+                             "no published numbers exist",
+        }
+        if torch_ref is not None:
+            res["torch_miopen_graph_inf_s_1gpu_1stream"] = round(torch_ref, 2)
+        print(json.dumps(res), flush=True)
+    if is_dist():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

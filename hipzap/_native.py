@@ -1,0 +1,114 @@
+"""ctypes binding of the hipzap native library (``hipzap/_lib/libhipzap.so``).
+
+The library is the in-tree build of ``hipzap/csrc`` (see :mod:`hipzap.build`). On a GPU host
+every hipzap op goes through it; there is deliberately no silent eager-PyTorch fallback for
+the hot ops — if the library is missing on a GPU host, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libhipzap.so"
+_lock = threading.Lock()
+_lib = None
+
+c_void_p, c_int, c_long, c_double = C.c_void_p, C.c_int, C.c_long, C.c_double
+c_float_p = C.POINTER(C.c_float)
+
+
+class ConvParams(C.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("res", c_void_p), ("out", c_void_p),
+        ("ws", c_void_p), ("cnt", c_void_p),
+        ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int),
+        ("Cout", c_int), ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int), ("P", c_int), ("Q", c_int),
+        ("M", c_int), ("K", c_int), ("ldw", c_int), ("ldo", c_int), ("ldr", c_int),
+        ("act", c_int), ("out_f32", c_int),
+        ("splitk", c_int), ("kslice", c_int),
+        ("tiles_n", c_int),
+    ]
+
+
+class PoolParams(C.Structure):
+    _fields_ = [("x", c_void_p), ("out", c_void_p),
+                ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("P", c_int), ("Q", c_int),
+                ("k", c_int), ("stride", c_int), ("pad", c_int)]
+
+
+def _sig(lib, name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+def _load():
+    lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+    P = c_void_p
+    _sig(lib, "hz_conv_launch", c_int, C.POINTER(ConvParams), c_int, P)
+    _sig(lib, "hz_maxpool_launch", c_int, C.POINTER(PoolParams), P)
+    _sig(lib, "hz_avgpool_launch", c_int, P, P, c_int, c_int, c_int, P)
+    _sig(lib, "hz_preprocess_launch", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P)
+    _sig(lib, "hz_cast_f32_bf16", c_int, P, P, c_long, P)
+    _sig(lib, "hz_cast_bf16_f32", c_int, P, P, c_long, P)
+    _sig(lib, "hz_prog_create", P)
+    _sig(lib, "hz_prog_destroy", None, P)
+    _sig(lib, "hz_prog_num_ops", c_int, P)
+    _sig(lib, "hz_prog_add_conv", c_int, P, C.POINTER(ConvParams), c_int, c_int)
+    _sig(lib, "hz_prog_add_maxpool", c_int, P, C.POINTER(PoolParams), c_int)
+    _sig(lib, "hz_prog_add_avgpool", c_int, P, P, P, c_int, c_int, c_int, c_int)
+    _sig(lib, "hz_prog_add_preprocess", c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int)
+    _sig(lib, "hz_prog_add_memcpy", c_int, P, P, P, C.c_size_t, c_int)
+    _sig(lib, "hz_prog_add_fork", c_int, P, c_int)
+    _sig(lib, "hz_prog_add_join", c_int, P, c_int)
+    _sig(lib, "hz_prog_run", c_int, P, P)
+    _sig(lib, "hz_prog_capture", c_int, P, P)
+    _sig(lib, "hz_prog_replay", c_int, P, P)
+    _sig(lib, "hz_prog_is_captured", c_int, P)
+    _sig(lib, "hz_prog_bench", c_double, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int)
+    for extra in _EXTRA_SIGS:
+        extra(lib)
+    return lib
+
+
+# other modules register additional prototypes here before first load
+_EXTRA_SIGS: list = []
+
+
+def available() -> bool:
+    return _LIB_PATH.exists()
+
+
+def lib():
+    """Return the loaded native library, building it first if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not _LIB_PATH.exists():
+                if os.environ.get("HIPZAP_NO_AUTOBUILD"):
+                    raise RuntimeError(f"hipzap native library missing: {_LIB_PATH} (run python -m hipzap.build)")
+                from . import build as _b
+                _b.build(verbose=False)
+            _lib = _load()
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"hipzap native call {what} failed with code {rc}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

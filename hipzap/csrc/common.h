@@ -1,0 +1,73 @@
+// hipzap common device helpers — gfx950 (CDNA4) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short bf16_t;                                   // storage type
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));       // MFMA A/B fragment (4 VGPR)
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));         // 16x16 MFMA accumulator
+typedef float f32x16 __attribute__((ext_vector_type(16)));       // 32x32 MFMA accumulator
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+#define HZ_WAVE 64
+
+#define HZ_CHECK(x)                                                              \
+  do {                                                                           \
+    hipError_t e__ = (x);                                                        \
+    if (e__ != hipSuccess) {                                                     \
+      fprintf(stderr, "hipzap: %s failed: %s (%s:%d)\n", #x,                     \
+              hipGetErrorString(e__), __FILE__, __LINE__);                       \
+      return (int)e__;                                                           \
+    }                                                                            \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+// 8 bf16 packed in a uint4 <-> floats
+__device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2(f[2 * i], f[2 * i + 1]);
+  return r;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks b and b+8 share an XCD under round-robin dispatch; give each XCD a contiguous
+// chunk of the logical id space. Pure speed choice, never a correctness assumption.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}

@@ -1,0 +1,71 @@
+// hipzap native C ABI (consumed from Python through ctypes: hipzap/_native.py).
+// Every struct here is mirrored field-for-field by a ctypes.Structure; keep them in sync.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { HZ_ACT_NONE = 0, HZ_ACT_RELU = 1, HZ_ACT_GELU = 2, HZ_ACT_TANH = 3 };
+
+typedef struct HzConvParams {
+  const unsigned short* x;   // NHWC bf16 input [N,H,W,C]
+  const unsigned short* w;   // bf16 weights [Cout_pad][ldw]; k = (r*S + s)*C + c
+  const float* bias;         // fp32 [Cout] or NULL
+  const unsigned short* res; // bf16 residual [M][ldr] or NULL
+  void* out;                 // bf16 or fp32 [M][ldo]
+  float* ws;                 // split-K slabs (splitk > 1)
+  int* cnt;                  // split-K tile tickets, zeroed once; self-resetting
+  int N, H, W, C;
+  int Cout, R, S, stride, pad, P, Q;
+  int M, K, ldw, ldo, ldr;
+  int act, out_f32;
+  int splitk, kslice;
+  int tiles_n;               // filled by the launcher
+} HzConvParams;
+
+int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t st);
+
+typedef struct HzPoolParams {
+  const unsigned short* x;  // NHWC bf16
+  unsigned short* out;      // NHWC bf16
+  int N, H, W, C, P, Q, k, stride, pad;
+} HzPoolParams;
+int hz_maxpool_launch(const HzPoolParams* p, hipStream_t st);
+// global average pool NHWC [N,H,W,C] -> [N,C] bf16
+int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, hipStream_t st);
+
+// image pre-processing: src NCHW fp32 (mode 0) or NHWC uint8 (mode 1) -> NHWC bf16 with Cpad channels
+int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
+                         int mode, const float* mean, const float* inv_std, hipStream_t st);
+
+// elementwise helpers
+int hz_cast_f32_bf16(const float* x, unsigned short* y, long n, hipStream_t st);
+int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipStream_t st);
+
+// ---- runtime: static op programs, graph capture / replay ----
+typedef void* HzProgram;
+HzProgram hz_prog_create(void);
+void hz_prog_destroy(HzProgram p);
+int hz_prog_num_ops(HzProgram p);
+int hz_prog_add_conv(HzProgram p, const HzConvParams* cp, int cfg, int slot);
+int hz_prog_add_maxpool(HzProgram p, const HzPoolParams* pp, int slot);
+int hz_prog_add_avgpool(HzProgram p, const unsigned short* x, unsigned short* out, int N, int HW, int C, int slot);
+int hz_prog_add_preprocess(HzProgram p, const void* src, unsigned short* dst, int N, int Cin, int H, int W,
+                           int Cpad, int mode, const float* mean, const float* inv_std, int slot);
+int hz_prog_add_memcpy(HzProgram p, void* dst, const void* src, size_t bytes, int slot);  // any direction (UVA)
+int hz_prog_add_fork(HzProgram p, int slot);   // side stream `slot` waits for main
+int hz_prog_add_join(HzProgram p, int slot);   // main waits for side stream `slot`
+int hz_prog_run(HzProgram p, hipStream_t st);  // eager launch of every op
+int hz_prog_capture(HzProgram p, hipStream_t st);
+int hz_prog_replay(HzProgram p, hipStream_t st);
+int hz_prog_is_captured(HzProgram p);
+// replay `n` programs round-robin on `n` streams `iters` times from C++ and synchronize;
+// returns elapsed microseconds (host wall, includes the final sync) or negative on error.
+double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters);
+
+#ifdef __cplusplus
+}
+#endif

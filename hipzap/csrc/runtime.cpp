@@ -1,0 +1,175 @@
+// hipzap native runtime: static op programs with hipGraph capture/replay.
+//
+// A model is lowered once (at cold start) into a Program: an ordered list of fully bound
+// kernel launches (all pointers fixed into a static activation arena, weights packed), plus
+// fork/join markers that put independent branches (e.g. a ResNet downsample conv) on side
+// streams. The warm path is the Program captured as ONE hipGraph and replayed per request,
+// so per-request host cost is a single hipGraphLaunch (north star "warm-path
+// invocation captured as a hipGraph"). Nothing here allocates or synchronises inside the
+// launch sequence, so capture is always legal (cdna_hip_programming.md §6 Guideline 9).
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <functional>
+#include <vector>
+
+#include "hipzap.h"
+
+namespace {
+
+struct Op {
+  int slot;  // 0 = main stream, k>0 = side stream k
+  enum Kind { LAUNCH, FORK, JOIN } kind;
+  std::function<int(hipStream_t)> fn;
+};
+
+struct Program {
+  std::vector<Op> ops;
+  std::vector<hipStream_t> side;     // side[k-1]
+  std::vector<hipEvent_t> fork_ev;   // one per fork/join op (indexed by op)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  int max_slot = 0;
+
+  ~Program() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (auto s : side) (void)hipStreamDestroy(s);
+    for (auto e : fork_ev) (void)hipEventDestroy(e);
+  }
+
+  int ensure_streams() {
+    while ((int)side.size() < max_slot) {
+      hipStream_t s;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1;
+      side.push_back(s);
+    }
+    while (fork_ev.size() < ops.size()) {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -1;
+      fork_ev.push_back(e);
+    }
+    return 0;
+  }
+
+  int run(hipStream_t main) {
+    if (ensure_streams()) return -1;
+    for (size_t i = 0; i < ops.size(); ++i) {
+      Op& op = ops[i];
+      hipStream_t s = op.slot == 0 ? main : side[op.slot - 1];
+      int rc = 0;
+      switch (op.kind) {
+        case Op::LAUNCH: rc = op.fn(s); break;
+        case Op::FORK:  // side waits for main
+          rc = (int)hipEventRecord(fork_ev[i], main);
+          if (!rc) rc = (int)hipStreamWaitEvent(side[op.slot - 1], fork_ev[i], 0);
+          break;
+        case Op::JOIN:  // main waits for side
+          rc = (int)hipEventRecord(fork_ev[i], side[op.slot - 1]);
+          if (!rc) rc = (int)hipStreamWaitEvent(main, fork_ev[i], 0);
+          break;
+      }
+      if (rc) {
+        fprintf(stderr, "hipzap: program op %zu failed rc=%d\n", i, rc);
+        return rc;
+      }
+    }
+    return 0;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+HzProgram hz_prog_create(void) { return new Program(); }
+void hz_prog_destroy(HzProgram p) { delete static_cast<Program*>(p); }
+int hz_prog_num_ops(HzProgram p) { return (int)static_cast<Program*>(p)->ops.size(); }
+
+static int add_op(Program* P, int slot, Op::Kind kind, std::function<int(hipStream_t)> fn) {
+  if (P->exec) return -3;  // frozen after capture
+  if (slot < 0 || slot > 8) return -4;
+  if (slot > P->max_slot) P->max_slot = slot;
+  P->ops.push_back(Op{slot, kind, std::move(fn)});
+  return 0;
+}
+
+int hz_prog_add_conv(HzProgram h, const HzConvParams* cp, int cfg, int slot) {
+  HzConvParams c = *cp;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [c, cfg](hipStream_t s) { return hz_conv_launch(&c, cfg, s); });
+}
+int hz_prog_add_maxpool(HzProgram h, const HzPoolParams* pp, int slot) {
+  HzPoolParams c = *pp;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_maxpool_launch(&c, s); });
+}
+int hz_prog_add_avgpool(HzProgram h, const unsigned short* x, unsigned short* out, int N, int HW, int C, int slot) {
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [=](hipStream_t s) { return hz_avgpool_launch(x, out, N, HW, C, s); });
+}
+int hz_prog_add_preprocess(HzProgram h, const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
+                           int mode, const float* mean, const float* inv_std, int slot) {
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [=](hipStream_t s) {
+    return hz_preprocess_launch(src, dst, N, Cin, H, W, Cpad, mode, mean, inv_std, s);
+  });
+}
+int hz_prog_add_memcpy(HzProgram h, void* dst, const void* src, size_t bytes, int slot) {
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [=](hipStream_t s) { return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s); });
+}
+int hz_prog_add_fork(HzProgram h, int slot) {
+  if (slot < 1) return -4;
+  return add_op(static_cast<Program*>(h), slot, Op::FORK, nullptr);
+}
+int hz_prog_add_join(HzProgram h, int slot) {
+  if (slot < 1) return -4;
+  return add_op(static_cast<Program*>(h), slot, Op::JOIN, nullptr);
+}
+
+int hz_prog_run(HzProgram h, hipStream_t st) { return static_cast<Program*>(h)->run(st); }
+
+int hz_prog_capture(HzProgram h, hipStream_t st) {
+  Program* P = static_cast<Program*>(h);
+  if (P->exec) return 0;
+  if (P->ensure_streams()) return -1;
+  hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) return (int)e;
+  int rc = P->run(st);
+  hipGraph_t g = nullptr;
+  e = hipStreamEndCapture(st, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return (int)e;
+  P->graph = g;
+  e = hipGraphInstantiate(&P->exec, g, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    P->exec = nullptr;
+    return (int)e;
+  }
+  // upload once so the first replay does not pay for it
+  (void)hipGraphUpload(P->exec, st);
+  return 0;
+}
+
+int hz_prog_is_captured(HzProgram h) { return static_cast<Program*>(h)->exec != nullptr; }
+
+int hz_prog_replay(HzProgram h, hipStream_t st) {
+  Program* P = static_cast<Program*>(h);
+  if (!P->exec) return P->run(st);
+  return (int)hipGraphLaunch(P->exec, st);
+}
+
+double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (int it = 0; it < iters; ++it)
+    for (int i = 0; i < n; ++i)
+      if (hz_prog_replay(progs[i], streams[i])) return -1.0;
+  for (int i = 0; i < n; ++i)
+    if (hipStreamSynchronize(streams[i]) != hipSuccess) return -2.0;
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double, std::micro>(t1 - t0).count();
+}
+
+}  // extern "C"

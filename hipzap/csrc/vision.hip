@@ -1,0 +1,132 @@
+// Vision helper kernels: NHWC max-pool, global average pool, image pre-processing.
+//  All are HBM/latency bound: 16-B vector loads (8 bf16
+// channels per lane), one output vector per lane, grid sized to the output.
+#include "common.h"
+#include "hipzap.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void maxpool_kernel(const HzPoolParams p) {
+  const int C8 = p.C >> 3;
+  const long total = (long)p.N * p.P * p.Q * C8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c8 = i % C8;
+  long t = i / C8;
+  const int q = t % p.Q;
+  t /= p.Q;
+  const int pp = t % p.P;
+  const int n = t / p.P;
+  float m[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+  const int h0 = pp * p.stride - p.pad, w0 = q * p.stride - p.pad;
+  for (int r = 0; r < p.k; ++r) {
+    const int ih = h0 + r;
+    if ((unsigned)ih >= (unsigned)p.H) continue;
+    for (int s = 0; s < p.k; ++s) {
+      const int iw = w0 + s;
+      if ((unsigned)iw >= (unsigned)p.W) continue;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(p.x + (((long)n * p.H + ih) * p.W + iw) * p.C + c8 * 8);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+    }
+  }
+  *reinterpret_cast<u32x4*>(p.out + i * 8) = pack8(m);
+}
+
+// [N, HW, C] -> [N, C]; one lane per 8 channels, HW loop (49 for ResNet).
+__global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
+                                                      int N, int HW, int C) {
+  const int C8 = C >> 3;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C8) return;
+  const int n = i / C8, c8 = i - n * C8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16_t* base = x + (long)n * HW * C + c8 * 8;
+  for (int j = 0; j < HW; ++j) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(base + (long)j * C), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += f[e];
+  }
+  const float inv = 1.0f / HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] *= inv;
+  *reinterpret_cast<u32x4*>(out + (long)n * C + c8 * 8) = pack8(s);
+}
+
+// mode 0: src fp32 NCHW (already normalised unless mean/inv_std given)
+// mode 1: src uint8 NHWC (raw image bytes, normalised with mean/inv_std in 0..1 scale)
+__global__ __launch_bounds__(256) void preprocess_kernel(const void* __restrict__ src, bf16_t* __restrict__ dst,
+                                                         int N, int Cin, int H, int W, int Cpad, int mode,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ inv_std) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel index
+  const long HWl = (long)H * W;
+  if (i >= N * HWl) return;
+  const long n = i / HWl, hw = i - n * HWl;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int c = 0; c < Cin && c < 8; ++c) {
+    float f;
+    if (mode == 0) f = reinterpret_cast<const float*>(src)[(n * Cin + c) * HWl + hw];
+    else f = (float)reinterpret_cast<const unsigned char*>(src)[i * Cin + c] * (1.0f / 255.0f);
+    if (mean) f = (f - mean[c]) * inv_std[c];
+    v[c] = f;
+  }
+  bf16_t* o = dst + i * Cpad;
+  *reinterpret_cast<u32x4*>(o) = pack8(v);
+  for (int c = 8; c < Cpad; c += 8) *reinterpret_cast<u32x4*>(o + c) = u32x4{0, 0, 0, 0};
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+    *reinterpret_cast<u32x2*>(y + i) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  } else {
+    for (long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = bf2f(x[i]);
+}
+
+}  // namespace
+
+extern "C" int hz_maxpool_launch(const HzPoolParams* pp, hipStream_t st) {
+  const HzPoolParams& p = *pp;
+  if (p.C % 8) return -1;
+  const long total = (long)p.N * p.P * p.Q * (p.C / 8);
+  hipLaunchKernelGGL(maxpool_kernel, dim3((total + 255) / 256), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  const int total = N * (C / 8);
+  hipLaunchKernelGGL(avgpool_kernel, dim3((total + 255) / 256), dim3(256), 0, st, x, out, N, HW, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
+                                    int mode, const float* mean, const float* inv_std, hipStream_t st) {
+  if (Cpad % 8 || Cin > 8) return -1;
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(preprocess_kernel, dim3((total + 255) / 256), dim3(256), 0, st, src, dst, N, Cin, H, W, Cpad,
+                     mode, mean, inv_std);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_cast_f32_bf16(const float* x, unsigned short* y, long n, hipStream_t st) {
+  const long threads = (n + 3) / 4;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, x, y, n);
+  return (int)hipGetLastError();
+}
+extern "C" int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, y, n);
+  return (int)hipGetLastError();
+}

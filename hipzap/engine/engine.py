@@ -1,0 +1,114 @@
+"""Serving engine: one model on one GPU with a hipGraph-captured warm path.
+
+Cold start: ``torch.load(weights_only=True)`` of a standard state_dict ->
+pack/fold on the GPU -> plan a static activation arena -> bind native Programs -> capture
+one hipGraph per execution context -> first inference. Warm request: copy the input into a
+context's static input buffer, ``hipGraphLaunch``, copy the logits out. Several contexts per
+GPU (``num_contexts``) let independent bs=1 requests run concurrently on separate streams
+sharing one packed weight set — the GPU analogue of Lambda's per-request container fan-out.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import torch
+
+from ..models import registry
+from .program import ExecContext, bench_contexts
+
+
+class Engine:
+    def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
+                 capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
+                 host_io: bool = True):
+        self.model = model
+        self.adapter = registry.get(model)
+        self.device = torch.device(device)
+        self.batch = batch
+        self.params = params
+        self.arch_kw = arch_kw or {}
+        self.timings = dict(timings or {})
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.device):
+            self.graph = self.adapter.build_graph(batch=batch, **self.arch_kw)
+            self.host_io = host_io
+            self.contexts = [ExecContext(self.graph, params, self.device, tuned, host_io=host_io)
+                             for _ in range(num_contexts)]
+            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(num_contexts)]
+            torch.cuda.synchronize(self.device)
+            self.timings["plan_ms"] = (time.perf_counter() - t0) * 1e3
+            t0 = time.perf_counter()
+            if capture:
+                for c, s in zip(self.contexts, self.streams):
+                    c.capture(s)
+                torch.cuda.synchronize(self.device)
+            self.timings["capture_ms"] = (time.perf_counter() - t0) * 1e3
+        self._rr = 0
+        self._locks = [threading.Lock() for _ in self.contexts]
+        self._rr_lock = threading.Lock()
+
+    # -------------------------------------------------------------- construction
+    @classmethod
+    def from_state_dict(cls, model: str, sd: dict, device="cuda:0", **kw) -> "Engine":
+        t0 = time.perf_counter()
+        adapter = registry.get(model)
+        dev = torch.device(device)
+        with torch.cuda.device(dev):
+            sd_dev = {k: v.to(dev, non_blocking=True) for k, v in sd.items() if torch.is_tensor(v)}
+            params, arch_kw = adapter.pack(sd_dev, dev)
+            torch.cuda.synchronize(dev)
+        timings = dict(kw.pop("timings", {}) or {})
+        timings["pack_ms"] = (time.perf_counter() - t0) * 1e3
+        return cls(model, params, device, arch_kw=arch_kw, timings=timings, **kw)
+
+    @classmethod
+    def from_checkpoint(cls, model: str, path: str, device="cuda:0", **kw) -> "Engine":
+        t0 = time.perf_counter()
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+            sd = sd["state_dict"]
+        timings = {"load_ms": (time.perf_counter() - t0) * 1e3}
+        return cls.from_state_dict(model, sd, device, timings=timings, **kw)
+
+    # -------------------------------------------------------------- warm path
+    def _pick(self) -> int:
+        with self._rr_lock:
+            i = self._rr
+            self._rr = (self._rr + 1) % len(self.contexts)
+        return i
+
+    def infer(self, x: torch.Tensor) -> torch.Tensor:
+        """Run one request (shape = the graph input shape); returns output on the host."""
+        i = self._pick()
+        ctx, s = self.contexts[i], self.streams[i]
+        with self._locks[i], torch.cuda.device(self.device), torch.cuda.stream(s):
+            if self.host_io:  # transfers are inside the captured graph
+                ctx.host_input.copy_(x.reshape(ctx.host_input.shape))
+                ctx.replay(s)
+                s.synchronize()
+                out = ctx.host_output.clone()
+            else:
+                ctx.input.copy_(x.reshape(ctx.input.shape), non_blocking=True)
+                ctx.replay(s)
+                out = ctx.output.to("cpu", non_blocking=False)
+        return self.adapter.postprocess_output(out)
+
+    def infer_device(self, x: torch.Tensor, ctx_index: int = 0) -> torch.Tensor:
+        """Device-resident variant (no host copies); output aliases the static buffer."""
+        ctx, s = self.contexts[ctx_index], self.streams[ctx_index]
+        with torch.cuda.device(self.device), torch.cuda.stream(s):
+            if x is not None:
+                ctx.input.copy_(x.reshape(ctx.input.shape), non_blocking=True)
+            ctx.replay(s)
+        return ctx.output
+
+    def bench(self, iters: int) -> float:
+        """Replay all contexts concurrently ``iters`` times (C++ loop); returns seconds."""
+        return bench_contexts(self.contexts, self.streams, iters)
+
+    def describe(self) -> dict:
+        c = self.contexts[0]
+        return {"model": self.model, "batch": self.batch, "contexts": len(self.contexts),
+                "ops": c.num_ops(), "arena_MB": round(c.arena_bytes / 2**20, 2),
+                "captured": c.captured, "timings_ms": {k: round(v, 2) for k, v in self.timings.items()}}

@@ -1,0 +1,183 @@
+"""Bind a planned :class:`~hipzap.engine.graph.Graph` to device memory as a native Program.
+
+An :class:`ExecContext` owns one activation arena, static input/output buffers, split-K
+workspaces and a native ``HzProgram`` whose ops are fully bound launches. It is the unit of
+concurrency: a serving engine keeps several contexts per GPU (one per in-flight request
+stream), all sharing one packed weight set. ``capture()`` records the program into a
+hipGraph; ``replay()`` is the warm path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from .. import _native as N
+from ..ops import conv as conv_ops
+from .graph import Graph, plan_memory
+
+
+class ExecContext:
+    def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
+                 host_io: bool = False):
+        self.graph = g
+        self.device = torch.device(device)
+        self.params = params
+        self._keep: list = []
+        lib = N.lib()
+        offsets, arena_bytes = plan_memory(g)
+        self.arena_bytes = arena_bytes
+        self.arena = torch.empty(max(arena_bytes, 256), dtype=torch.uint8, device=self.device)
+        base = self.arena.data_ptr()
+        self.ext: dict[int, torch.Tensor] = {}
+        for tid, spec in enumerate(g.tensors):
+            if spec.external:
+                self.ext[tid] = torch.zeros(spec.shape, dtype=spec.dtype, device=self.device)
+
+        def addr(tid):
+            if tid is None:
+                return 0
+            if tid in self.ext:
+                return self.ext[tid].data_ptr()
+            return base + offsets[tid]
+
+        self._addr = addr
+        self.tensor_offsets = offsets
+        self.prog = lib.hz_prog_create()
+        self.configs: list = []
+        # split-K workspace sizing pass
+        ws_total, cnt_total, conv_plans = 0, 0, []
+        for n in g.nodes:
+            if n.kind != "conv":
+                conv_plans.append(None)
+                continue
+            pc = params[n.attrs["w"]]
+            nb, h, w, _ = g.shape(n.inputs[0])
+            p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
+            q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
+            M = nb * p_out * q_out
+            key = f"{M}x{pc.cout}x{pc.K}x{pc.r}{pc.s}s{pc.stride}"
+            cfg, splitk = n.attrs.get("cfg"), n.attrs.get("splitk")
+            if cfg is None or splitk is None:
+                c2, s2 = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
+                cfg = c2 if cfg is None else cfg
+                splitk = s2 if splitk is None else splitk
+            wsb, ncnt = conv_ops.workspace_bytes(M, pc.cout, cfg, splitk)
+            conv_plans.append((cfg, splitk, ws_total, cnt_total, key))
+            ws_total += (wsb + 255) // 256 * 256
+            cnt_total += (ncnt + 63) // 64 * 64
+        self.ws = torch.empty(max(ws_total, 256), dtype=torch.uint8, device=self.device)
+        self.cnt = torch.zeros(max(cnt_total, 64), dtype=torch.int32, device=self.device)
+        # host_io: the request's PCIe transfers are part of the program (and of the graph):
+        # pinned host input -> device input ... device output -> pinned host output.
+        self.host_io = host_io
+        if host_io:
+            self.host_input = torch.zeros(self.input.shape, dtype=self.input.dtype).pin_memory()
+            self.host_output = torch.zeros(self.output.shape, dtype=self.output.dtype).pin_memory()
+            N.check(lib.hz_prog_add_memcpy(self.prog, self.input.data_ptr(), self.host_input.data_ptr(),
+                                           self.input.numel() * self.input.element_size(), 0), "h2d")
+        for i, n in enumerate(g.nodes):
+            self._add_node(lib, n, conv_plans[i])
+        if host_io:
+            N.check(lib.hz_prog_add_memcpy(self.prog, self.host_output.data_ptr(), self.output.data_ptr(),
+                                           self.output.numel() * self.output.element_size(), 0), "d2h")
+
+    # ------------------------------------------------------------------
+    def _add_node(self, lib, n, plan):
+        g, addr = self.graph, self._addr
+        if n.kind == "conv":
+            pc = self.params[n.attrs["w"]]
+            cfg, splitk, ws_off, cnt_off, key = plan
+            nb, h, w, _ = g.shape(n.inputs[0])
+            res = n.inputs[1] if len(n.inputs) > 1 else None
+            prm, _, _ = conv_ops.make_params(
+                addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
+                n.attrs.get("out_f32", False), cfg, splitk,
+                self.ws.data_ptr() + ws_off, self.cnt.data_ptr() + 4 * cnt_off)
+            self.configs.append((n.attrs.get("name", ""), key, cfg, splitk))
+            N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_conv")
+        elif n.kind == "maxpool":
+            nb, h, w, c = g.shape(n.inputs[0])
+            _, p, q, _ = g.shape(n.outputs[0])
+            a = n.attrs
+            prm = N.PoolParams(addr(n.inputs[0]), addr(n.outputs[0]), nb, h, w, c, p, q, a["k"], a["stride"], a["pad"])
+            N.check(lib.hz_prog_add_maxpool(self.prog, C.byref(prm), n.slot), "add_maxpool")
+        elif n.kind == "avgpool":
+            nb, h, w, c = g.shape(n.inputs[0])
+            N.check(lib.hz_prog_add_avgpool(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, h * w, c, n.slot),
+                    "add_avgpool")
+        elif n.kind == "preprocess":
+            src = g.tensors[n.inputs[0]]
+            if src.dtype == torch.uint8:
+                nb, h, w, cin = src.shape
+                mode = 1
+            else:
+                nb, cin, h, w = src.shape
+                mode = 0
+            cpad = g.shape(n.outputs[0])[-1]
+            mean = std = None
+            if n.attrs.get("mean") is not None:
+                mean = torch.tensor(n.attrs["mean"], dtype=torch.float32, device=self.device)
+                std = 1.0 / torch.tensor(n.attrs["std"], dtype=torch.float32, device=self.device)
+                self._keep += [mean, std]
+            N.check(lib.hz_prog_add_preprocess(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, cin, h, w,
+                                               cpad, mode, N.ptr(mean), N.ptr(std), n.slot), "add_preprocess")
+        elif n.kind == "fork":
+            N.check(lib.hz_prog_add_fork(self.prog, n.slot), "fork")
+        elif n.kind == "join":
+            N.check(lib.hz_prog_add_join(self.prog, n.slot), "join")
+        else:
+            raise NotImplementedError(f"node kind {n.kind}")
+
+    # ------------------------------------------------------------------
+    @property
+    def input(self) -> torch.Tensor:
+        return self.ext[self.graph.inputs[0]]
+
+    @property
+    def output(self) -> torch.Tensor:
+        return self.ext[self.graph.outputs[0]]
+
+    def view(self, tid: int) -> torch.Tensor:
+        """Debug view of any tensor of the graph (arena-backed)."""
+        if tid in self.ext:
+            return self.ext[tid]
+        spec = self.graph.tensors[tid]
+        off = self.tensor_offsets[tid]
+        return self.arena[off: off + spec.nbytes].view(spec.dtype).view(spec.shape)
+
+    def run(self, stream=None):
+        N.check(N.lib().hz_prog_run(self.prog, N.stream_ptr(stream)), "prog_run")
+
+    def capture(self, stream=None):
+        N.check(N.lib().hz_prog_capture(self.prog, N.stream_ptr(stream)), "prog_capture")
+
+    @property
+    def captured(self) -> bool:
+        return bool(N.lib().hz_prog_is_captured(self.prog))
+
+    def replay(self, stream=None):
+        N.check(N.lib().hz_prog_replay(self.prog, N.stream_ptr(stream)), "prog_replay")
+
+    def num_ops(self) -> int:
+        return N.lib().hz_prog_num_ops(self.prog)
+
+    def __del__(self):
+        try:
+            if getattr(self, "prog", None):
+                N.lib().hz_prog_destroy(self.prog)
+                self.prog = None
+        except Exception:
+            pass
+
+
+def bench_contexts(ctxs: list, streams: list, iters: int) -> float:
+    """Replay every context on its own stream ``iters`` times from C++; returns seconds."""
+    n = len(ctxs)
+    progs = (C.c_void_p * n)(*[c.prog for c in ctxs])
+    strs = (C.c_void_p * n)(*[s.cuda_stream for s in streams])
+    us = N.lib().hz_prog_bench(progs, strs, n, iters)
+    if us < 0:
+        raise RuntimeError(f"hz_prog_bench failed ({us})")
+    return us * 1e-6

@@ -1,0 +1,71 @@
+"""Pure-PyTorch interpreter of a lowered :class:`Graph` (fp32 oracle of the native program).
+
+It executes exactly the nodes/packed weights the native program will run, with torch ops,
+so the lowering (BN folding, weight packing/padding, NHWC layout, residual wiring, fork/join
+ordering) is checked on CPU against the eager model, and the GPU kernels are checked against
+this node-by-node. ``bf16_acts=True`` rounds every stored activation to bf16 like the device
+does, which isolates accumulation-order error from storage rounding.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .graph import Graph
+
+
+def _conv_ref(x_nhwc, pc, res=None, act="relu", out_f32=False):
+    w = pc.w[: pc.cout, : pc.K].float().reshape(pc.cout, pc.r, pc.s, pc.cin).permute(0, 3, 1, 2)
+    y = F.conv2d(x_nhwc.permute(0, 3, 1, 2).float(), w, pc.bias.float(), stride=pc.stride, padding=pc.pad)
+    y = y.permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + res.float()
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "gelu":
+        y = F.gelu(y)
+    elif act == "tanh":
+        y = torch.tanh(y)
+    return y
+
+
+def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = True) -> dict:
+    vals: dict[int, torch.Tensor] = {}
+    for tid, x in zip(g.inputs, inputs):
+        vals[tid] = x
+
+    def store(tid, v):
+        spec = g.tensors[tid]
+        if bf16_acts and spec.dtype == torch.bfloat16:
+            v = v.to(torch.bfloat16).float()
+        vals[tid] = v.reshape(spec.shape)
+
+    for n in g.nodes:
+        k = n.kind
+        if k in ("fork", "join"):
+            continue
+        if k == "preprocess":
+            src = vals[n.inputs[0]]
+            cpad = g.shape(n.outputs[0])[-1]
+            if src.dtype == torch.uint8:
+                x = src.float() / 255.0
+            else:
+                x = src.float().permute(0, 2, 3, 1)
+            if n.attrs.get("mean") is not None:
+                x = (x - torch.tensor(n.attrs["mean"])) / torch.tensor(n.attrs["std"])
+            store(n.outputs[0], F.pad(x, (0, cpad - x.shape[-1])))
+        elif k == "conv":
+            pc = params[n.attrs["w"]]
+            res = vals[n.inputs[1]] if len(n.inputs) > 1 else None
+            store(n.outputs[0], _conv_ref(vals[n.inputs[0]], pc, res, n.attrs.get("act", "relu")))
+        elif k == "maxpool":
+            a = n.attrs
+            x = vals[n.inputs[0]].permute(0, 3, 1, 2)
+            y = F.max_pool2d(x, a["k"], a["stride"], a["pad"]).permute(0, 2, 3, 1)
+            store(n.outputs[0], y)
+        elif k == "avgpool":
+            x = vals[n.inputs[0]]
+            store(n.outputs[0], x.float().mean(dim=(1, 2), keepdim=True))
+        else:
+            raise NotImplementedError(k)
+    return vals

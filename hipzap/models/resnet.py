@@ -1,0 +1,246 @@
+"""ResNet-18 / ResNet-50 (torchvision-compatible state_dict keys).
+
+Two halves:
+* ``ResNet`` — a plain eager ``nn.Module`` with torchvision's exact parameter names
+  (``conv1``, ``bn1``, ``layer{1..4}.{i}.conv{1,2,3}``, ``downsample.{0,1}``, ``fc``). It is
+  the checkpoint schema (``torch.save(model.state_dict())`` files load unchanged) and the
+  fp32 numerics oracle. torchvision is not installed in this image, so it is written here.
+* ``pack_resnet`` + ``build_graph`` — the MI355X lowering: BN folded into every conv at load
+  time, weights packed for the MFMA implicit-GEMM kernel, and the network lowered to a
+  static kernel graph (preprocess -> stem conv -> maxpool -> bottlenecks with the residual
+  add + ReLU fused into the last conv's epilogue -> avgpool -> FC). The downsample conv runs
+  on a side stream, concurrently with the block's main branch.
+
+The reference repo has no vision model at all (north-star configs 1-3);
+this is the model behind ``POST /predict`` and the headline benchmark.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..engine.graph import Graph
+from ..ops.conv import PackedConv, pack_conv, pack_linear
+from ..ops.vision import IMAGENET_MEAN, IMAGENET_STD
+
+
+def _conv3x3(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+
+
+def _conv1x1(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 1, stride, 0, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = _conv3x3(cin, planes, stride)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = _conv3x3(planes, planes)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = _conv1x1(cin, planes)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = _conv3x3(planes, planes, stride)  # torchvision v1.5: stride on the 3x3
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = _conv1x1(planes, planes * 4)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return self.relu(out + idt)
+
+
+ARCHS = {
+    "resnet18": (BasicBlock, [2, 2, 2, 2]),
+    "resnet34": (BasicBlock, [3, 4, 6, 3]),
+    "resnet50": (Bottleneck, [3, 4, 6, 3]),
+    "resnet101": (Bottleneck, [3, 4, 23, 3]),
+}
+
+
+class ResNet(nn.Module):
+    def __init__(self, arch="resnet50", num_classes=1000):
+        super().__init__()
+        block, layers = ARCHS[arch]
+        self.arch = arch
+        self.block = block
+        self.layers_cfg = layers
+        self.num_classes = num_classes
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._make(block, 64, layers[0])
+        self.layer2 = self._make(block, 128, layers[1], 2)
+        self.layer3 = self._make(block, 256, layers[2], 2)
+        self.layer4 = self._make(block, 512, layers[3], 2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make(self, block, planes, blocks, stride=1):
+        ds = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            ds = nn.Sequential(_conv1x1(self.inplanes, planes * block.expansion, stride),
+                               nn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, ds)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def resnet18(num_classes=1000) -> ResNet:
+    return ResNet("resnet18", num_classes)
+
+
+def resnet50(num_classes=1000) -> ResNet:
+    return ResNet("resnet50", num_classes)
+
+
+def randomize_bn(model: nn.Module, seed: int = 0) -> nn.Module:
+    """Give BN layers non-trivial random statistics (random-init weights, as the bench uses)."""
+    g = torch.Generator().manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            c = m.num_features
+            m.weight.data = 0.5 + torch.rand(c, generator=g)
+            m.bias.data = 0.1 * torch.randn(c, generator=g)
+            m.running_mean.data = 0.1 * torch.randn(c, generator=g)
+            m.running_var.data = 0.5 + torch.rand(c, generator=g)
+    return model
+
+
+def infer_arch(sd: dict) -> tuple[str, int]:
+    nblk = [len({k.split(".")[1] for k in sd if k.startswith(f"layer{i}.")}) for i in range(1, 5)]
+    bottleneck = any(k.endswith("conv3.weight") for k in sd)
+    for name, (blk, layers) in ARCHS.items():
+        if layers == nblk and (blk is Bottleneck) == bottleneck:
+            return name, sd["fc.weight"].shape[0]
+    raise ValueError(f"unrecognised ResNet state_dict (blocks {nblk})")
+
+
+# ---------------------------------------------------------------------------- lowering
+def _bn(sd, prefix):
+    return {k: sd[f"{prefix}.{k}"] for k in ("weight", "bias", "running_mean", "running_var")}
+
+
+def pack_resnet(sd: dict, device="cpu") -> dict[str, PackedConv]:
+    """state_dict -> {name: PackedConv} with BN folded (runs once at cold start)."""
+    sd = {k: v.to(device) for k, v in sd.items()}
+    arch, _ = infer_arch(sd)
+    block, layers = ARCHS[arch]
+    P = {"conv1": pack_conv(sd["conv1.weight"], None, _bn(sd, "bn1"), stride=2, pad=3, cin_pad=8)}
+    for li, nb in enumerate(layers, start=1):
+        for b in range(nb):
+            pre = f"layer{li}.{b}"
+            stride = 2 if (b == 0 and li > 1) else 1
+            if block is Bottleneck:
+                P[f"{pre}.conv1"] = pack_conv(sd[f"{pre}.conv1.weight"], None, _bn(sd, f"{pre}.bn1"))
+                P[f"{pre}.conv2"] = pack_conv(sd[f"{pre}.conv2.weight"], None, _bn(sd, f"{pre}.bn2"), stride, 1)
+                P[f"{pre}.conv3"] = pack_conv(sd[f"{pre}.conv3.weight"], None, _bn(sd, f"{pre}.bn3"))
+            else:
+                P[f"{pre}.conv1"] = pack_conv(sd[f"{pre}.conv1.weight"], None, _bn(sd, f"{pre}.bn1"), stride, 1)
+                P[f"{pre}.conv2"] = pack_conv(sd[f"{pre}.conv2.weight"], None, _bn(sd, f"{pre}.bn2"), 1, 1)
+            if f"{pre}.downsample.0.weight" in sd:
+                P[f"{pre}.downsample"] = pack_conv(sd[f"{pre}.downsample.0.weight"], None,
+                                                   _bn(sd, f"{pre}.downsample.1"), stride, 0)
+    P["fc"] = pack_linear(sd["fc.weight"], sd["fc.bias"])
+    return P
+
+
+def build_graph(arch: str, batch: int, num_classes: int = 1000, image: int = 224,
+                input_uint8: bool = False, side_stream: bool = True) -> Graph:
+    """Lower ResNet to a static kernel graph for a fixed batch size."""
+    block, layers = ARCHS[arch]
+    g = Graph(f"{arch}_bs{batch}")
+    if input_uint8:
+        x_in = g.tensor((batch, image, image, 3), torch.uint8, "image", external=True)
+        mean, std = IMAGENET_MEAN, IMAGENET_STD
+    else:
+        x_in = g.tensor((batch, 3, image, image), torch.float32, "input", external=True)
+        mean = std = None
+    g.inputs.append(x_in)
+    x = g.tensor((batch, image, image, 8), name="nhwc")
+    g.add("preprocess", [x_in], [x], mean=mean, std=std)
+
+    def conv(src, name, cout, k, stride, pad, act="relu", res=None, slot=0, out_f32=False, ext=False):
+        nb, h, w, _ = g.shape(src)
+        p = (h + 2 * pad - k) // stride + 1
+        q = (w + 2 * pad - k) // stride + 1
+        dt = torch.float32 if out_f32 else torch.bfloat16
+        out = g.tensor((nb, p, q, cout), dt, name, external=ext)
+        ins = [src] if res is None else [src, res]
+        g.add("conv", ins, [out], slot=slot, w=name, act=act, out_f32=out_f32, name=name)
+        return out
+
+    x = conv(x, "conv1", 64, 7, 2, 3)
+    nb, h, w, c = g.shape(x)
+    mp = g.tensor((nb, (h + 1) // 2, (w + 1) // 2, c), name="maxpool")
+    g.add("maxpool", [x], [mp], k=3, stride=2, pad=1)
+    x = mp
+    cin = 64
+    for li, nblk in enumerate(layers, start=1):
+        planes = 64 * 2 ** (li - 1)
+        for b in range(nblk):
+            pre = f"layer{li}.{b}"
+            stride = 2 if (b == 0 and li > 1) else 1
+            cout = planes * block.expansion
+            has_ds = b == 0 and (stride != 1 or cin != cout)
+            idt = x
+            if has_ds:
+                slot = 1 if side_stream else 0
+                if side_stream:
+                    g.add("fork", [], [], slot=1)
+                idt = conv(x, f"{pre}.downsample", cout, 1, stride, 0, act="none", slot=slot)
+            if block is Bottleneck:
+                y = conv(x, f"{pre}.conv1", planes, 1, 1, 0)
+                y = conv(y, f"{pre}.conv2", planes, 3, stride, 1)
+                if has_ds and side_stream:
+                    g.add("join", [], [], slot=1)
+                x = conv(y, f"{pre}.conv3", cout, 1, 1, 0, res=idt)
+            else:
+                y = conv(x, f"{pre}.conv1", planes, 3, stride, 1)
+                if has_ds and side_stream:
+                    g.add("join", [], [], slot=1)
+                x = conv(y, f"{pre}.conv2", cout, 3, 1, 1, res=idt)
+            cin = cout
+    nb, h, w, c = g.shape(x)
+    pooled = g.tensor((nb, 1, 1, c), name="avgpool")
+    g.add("avgpool", [x], [pooled])
+    logits = conv(pooled, "fc", num_classes, 1, 1, 0, act="none", out_f32=True, ext=True)
+    g.outputs.append(logits)
+    return g

@@ -1,0 +1,54 @@
+"""Eager wrappers + fp32 oracles for the vision helper kernels (csrc/vision.hip)."""
+from __future__ import annotations
+
+import torch
+
+from .. import _native as N
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def maxpool_nhwc(x: torch.Tensor, k=3, stride=2, pad=1) -> torch.Tensor:
+    n, h, w, c = x.shape
+    p = (h + 2 * pad - k) // stride + 1
+    q = (w + 2 * pad - k) // stride + 1
+    out = torch.empty(n, p, q, c, device=x.device, dtype=torch.bfloat16)
+    prm = N.PoolParams(x.data_ptr(), out.data_ptr(), n, h, w, c, p, q, k, stride, pad)
+    N.check(N.lib().hz_maxpool_launch(prm, N.stream_ptr()), "maxpool")
+    return out
+
+
+def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
+    n, h, w, c = x.shape
+    out = torch.empty(n, c, device=x.device, dtype=torch.bfloat16)
+    N.check(N.lib().hz_avgpool_launch(x.data_ptr(), out.data_ptr(), n, h * w, c, N.stream_ptr()), "avgpool")
+    return out
+
+
+def preprocess(src: torch.Tensor, cpad: int = 8, mean=None, std=None) -> torch.Tensor:
+    """fp32 NCHW (mode 0) or uint8 NHWC (mode 1) -> bf16 NHWC with ``cpad`` channels."""
+    if src.dtype == torch.uint8:
+        n, h, w, cin = src.shape
+        mode = 1
+    else:
+        n, cin, h, w = src.shape
+        mode = 0
+    out = torch.empty(n, h, w, cpad, device=src.device, dtype=torch.bfloat16)
+    mean_t = inv_t = None
+    if mean is not None:
+        mean_t = torch.tensor(mean, dtype=torch.float32, device=src.device)
+        inv_t = 1.0 / torch.tensor(std, dtype=torch.float32, device=src.device)
+    N.check(N.lib().hz_preprocess_launch(src.data_ptr(), out.data_ptr(), n, cin, h, w, cpad, mode,
+                                         N.ptr(mean_t), N.ptr(inv_t), N.stream_ptr()), "preprocess")
+    return out
+
+
+def preprocess_reference(src: torch.Tensor, cpad: int = 8, mean=None, std=None) -> torch.Tensor:
+    if src.dtype == torch.uint8:
+        x = src.float() / 255.0
+    else:
+        x = src.float().permute(0, 2, 3, 1)
+    if mean is not None:
+        x = (x - torch.tensor(mean, device=x.device)) / torch.tensor(std, device=x.device)
+    return torch.nn.functional.pad(x, (0, cpad - x.shape[-1]))

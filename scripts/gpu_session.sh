@@ -1,0 +1,31 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench variants, rocprof kernel stats.
+# Continues past ordinary test failures (rc 1) but stops at any crash/timeout/fault.
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-all}
+python -c "import torch; print(torch.cuda.get_device_name(0))"
+[[ $STEPS == *tests* || $STEPS == all ]] && step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *smoke* || $STEPS == all ]] && step smoke 300 python __graft_entry__.py smoke
+[[ $STEPS == *bench* || $STEPS == all ]] && {
+  for s in ${BENCH_STREAMS:-1 4 8}; do
+    step bench_s$s 300 python bench.py --streams $s --steps 300 --warmup 30 --cold-runs 2 ${BENCH_EXTRA:-}
+    grep '^{' $OUT/bench_s$s.log > $OUT/bench_s$s.json || true
+  done
+}
+[[ $STEPS == *prof* || $STEPS == all ]] && {
+  step rocprof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --streams 1 --steps 50 --warmup 5 --cold-runs 0
+}
+echo "=== done"

@@ -1,0 +1,87 @@
+"""Native vision kernels vs fp32 PyTorch oracles (MI355X only)."""
+import pytest
+import torch
+
+from hipzap.ops import conv as C
+from hipzap.ops import vision as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rand_bn(c, g):
+    return {"weight": 0.5 + torch.rand(c, generator=g), "bias": 0.1 * torch.randn(c, generator=g),
+            "running_mean": 0.1 * torch.randn(c, generator=g), "running_var": 0.5 + torch.rand(c, generator=g)}
+
+
+def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None, splitk=None, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, cin, h, h, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    bn = _rand_bn(cout, g)
+    pc = C.pack_conv(w, None, bn, stride, pad)
+    p = (h + 2 * pad - k) // stride + 1
+    res = torch.randn(n, cout, p, p, generator=g) if residual else None
+    # bf16-rounded inputs for the oracle so only accumulation/epilogue error remains
+    xb = x.to(torch.bfloat16).float()
+    pc_cpu = pc
+    wref = pc_cpu.w[:cout, :pc.K].float().reshape(cout, k, k, pc.cin)[..., :cin].permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xb, wref, pc.bias, stride=stride, padding=pad)
+    if res is not None:
+        ref = ref + res.to(torch.bfloat16).float()
+    if act == "relu":
+        ref = torch.relu(ref)
+    x_nhwc = torch.nn.functional.pad(xb.permute(0, 2, 3, 1), (0, pc.cin - cin)).to(torch.bfloat16)
+    r_nhwc = None if res is None else res.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+    out = C.conv2d_nhwc(x_nhwc.contiguous().to(DEV), pc.to(DEV), r_nhwc, act=act, cfg=cfg, splitk=splitk)
+    torch.cuda.synchronize()
+    got = out.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    return err / scale
+
+
+SHAPES = [
+    # n, cin, h, cout, k, stride, pad
+    (1, 64, 56, 64, 1, 1, 0),
+    (1, 64, 56, 64, 3, 1, 1),
+    (1, 128, 56, 128, 3, 2, 1),
+    (1, 256, 14, 1024, 1, 1, 0),
+    (1, 512, 7, 512, 3, 1, 1),
+    (1, 1024, 14, 2048, 1, 2, 0),
+    (2, 3, 32, 64, 7, 2, 3),     # stem-like, generic K path (cin padded to 8)
+    (1, 48, 9, 40, 3, 1, 1),     # odd: C%32 != 0, Cout not multiple of 16
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_heuristic(shape):
+    assert _case(*shape) < 2e-2
+
+
+@pytest.mark.parametrize("cfg", range(len(C.CONV_CONFIGS)))
+@pytest.mark.parametrize("splitk", [1, 3])
+def test_conv_every_config(cfg, splitk):
+    assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, splitk=splitk) < 2e-2
+
+
+def test_conv_splitk_deep():
+    # layer4-like: M=49, K=4608, heavy split; run twice to check ticket self-reset
+    for _ in range(2):
+        assert _case(1, 512, 7, 512, 3, 1, 1, residual=True, cfg=1, splitk=16) < 2e-2
+
+
+def test_maxpool_avgpool_preprocess():
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 9, 11, 64, generator=g).to(torch.bfloat16)
+    y = V.maxpool_nhwc(x.to(DEV)).cpu().float()
+    ref = torch.nn.functional.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+    a = V.avgpool_nhwc(x.to(DEV)).cpu().float()
+    assert (a - x.float().mean(dim=(1, 2))).abs().max() < 1e-2
+    img = torch.randn(2, 3, 20, 24, generator=g)
+    p = V.preprocess(img.to(DEV)).cpu().float()
+    assert (p - V.preprocess_reference(img)).abs().max() < 1e-2
+    u8 = torch.randint(0, 256, (2, 20, 24, 3), dtype=torch.uint8, generator=g)
+    p = V.preprocess(u8.to(DEV), mean=V.IMAGENET_MEAN, std=V.IMAGENET_STD).cpu().float()
+    assert (p - V.preprocess_reference(u8, mean=V.IMAGENET_MEAN, std=V.IMAGENET_STD)).abs().max() < 2e-2
