@@ -28,7 +28,7 @@ class ConvParams(C.Structure):
         ("M", c_int), ("K", c_int), ("ldw", c_int), ("ldo", c_int), ("ldr", c_int),
         ("act", c_int), ("out_f32", c_int),
         ("splitk", c_int), ("kslice", c_int),
-        ("tiles_n", c_int),
+        ("tiles_n", c_int), ("kw", c_int),
     ]
 
 

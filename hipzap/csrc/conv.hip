@@ -259,6 +259,7 @@ int launch_cfg(const HzConvParams& p, hipStream_t st) {
 extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
   if (p.Cout % 4 != 0 || p.C % 8 != 0 || p.ldw % 32 != 0 || p.splitk < 1) return -1;
+  if (cfg >= 100) return hz_conv_kw_launch(pp, cfg, st);
   switch (cfg) {
     case 0: return launch_cfg<2, 2, 2, 2>(p, st);  //  64ch x  64px
     case 1: return launch_cfg<4, 1, 1, 1>(p, st);  //  64ch x  16px

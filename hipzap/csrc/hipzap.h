@@ -24,9 +24,11 @@ typedef struct HzConvParams {
   int act, out_f32;
   int splitk, kslice;
   int tiles_n;               // filled by the launcher
+  int kw;                    // v2 (cfg >= 100): waves per workgroup splitting K
 } HzConvParams;
 
 int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t st);
+int hz_conv_kw_launch(const HzConvParams* p, int cfg, hipStream_t st);
 
 typedef struct HzPoolParams {
   const unsigned short* x;  // NHWC bf16

@@ -18,6 +18,17 @@ from ..models import registry
 from .program import ExecContext, bench_contexts
 
 
+def load_tuning(model: str, batch: int) -> dict | None:
+    """Measured launch-config table written by ``python -m hipzap.engine.tune`` (if any)."""
+    import json
+    from .tune import table_path
+    p = table_path(model, batch)
+    if p.exists():
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
 class Engine:
     def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
                  capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
@@ -29,6 +40,9 @@ class Engine:
         self.params = params
         self.arch_kw = arch_kw or {}
         self.timings = dict(timings or {})
+        if tuned is None:
+            tuned = load_tuning(model, batch)
+        self.tuned = tuned
         t0 = time.perf_counter()
         with torch.cuda.device(self.device):
             self.graph = self.adapter.build_graph(batch=batch, **self.arch_kw)

@@ -58,13 +58,12 @@ class ExecContext:
             q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
             M = nb * p_out * q_out
             key = f"{M}x{pc.cout}x{pc.K}x{pc.r}{pc.s}s{pc.stride}"
-            cfg, splitk = n.attrs.get("cfg"), n.attrs.get("splitk")
-            if cfg is None or splitk is None:
-                c2, s2 = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
-                cfg = c2 if cfg is None else cfg
-                splitk = s2 if splitk is None else splitk
+            if n.attrs.get("cfg") is not None:
+                cfg, splitk, kw = n.attrs["cfg"], n.attrs.get("splitk", 1), n.attrs.get("kw", 1)
+            else:
+                cfg, splitk, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
             wsb, ncnt = conv_ops.workspace_bytes(M, pc.cout, cfg, splitk)
-            conv_plans.append((cfg, splitk, ws_total, cnt_total, key))
+            conv_plans.append((cfg, splitk, kw, ws_total, cnt_total, key))
             ws_total += (wsb + 255) // 256 * 256
             cnt_total += (ncnt + 63) // 64 * 64
         self.ws = torch.empty(max(ws_total, 256), dtype=torch.uint8, device=self.device)
@@ -88,14 +87,14 @@ class ExecContext:
         g, addr = self.graph, self._addr
         if n.kind == "conv":
             pc = self.params[n.attrs["w"]]
-            cfg, splitk, ws_off, cnt_off, key = plan
+            cfg, splitk, kw, ws_off, cnt_off, key = plan
             nb, h, w, _ = g.shape(n.inputs[0])
             res = n.inputs[1] if len(n.inputs) > 1 else None
             prm, _, _ = conv_ops.make_params(
                 addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
                 n.attrs.get("out_f32", False), cfg, splitk,
-                self.ws.data_ptr() + ws_off, self.cnt.data_ptr() + 4 * cnt_off)
-            self.configs.append((n.attrs.get("name", ""), key, cfg, splitk))
+                self.ws.data_ptr() + ws_off, self.cnt.data_ptr() + 4 * cnt_off, kw=kw)
+            self.configs.append((n.attrs.get("name", ""), key, cfg, splitk, kw))
             N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_conv")
         elif n.kind == "maxpool":
             nb, h, w, c = g.shape(n.inputs[0])

@@ -83,35 +83,77 @@ def pack_linear(weight, bias=None) -> PackedConv:
     return pack_conv(weight[:, :, None, None], bias)
 
 
-def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str | None = None):
-    """Pick (cfg, splitk) for an implicit GEMM of M pixels x cout channels x K.
+KW_TILES = [(fc, fp) for fc in (1, 2, 4) for fp in (1, 2, 4)]  # cfg = 100 + index
 
-    Latency model for the bs=1 regime: prefer the config whose padded work is smallest while
-    the grid still reaches ~the CU count; then split K until the grid has >= ~1 workgroup
-    per CU with >= 4 K-steps per slice. A measured table (``tuned``) overrides this.
+
+def kw_max_threads(nf: int) -> int:
+    return 256 if nf >= 16 else 512 if nf >= 8 else 1024
+
+
+def kw_cfg(fc: int, fp: int) -> int:
+    return 100 + KW_TILES.index((fc, fp))
+
+
+def tile_of(cfg: int) -> tuple[int, int]:
+    """(channels, pixels) per workgroup for any cfg."""
+    if cfg >= 100:
+        fc, fp = KW_TILES[cfg - 100]
+        return fc * 16, fp * 16
+    return tile_dims(cfg)
+
+
+def candidates(M: int, cout: int, K: int) -> list[tuple[int, int, int]]:
+    """All legal (cfg, splitk, kw) launch choices worth timing for one conv shape."""
+    steps = max(1, math.ceil(K / 32))
+    out = []
+    for (fc, fp) in KW_TILES:
+        if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
+            continue
+        for kw in (1, 2, 4, 8, 16):
+            if kw * fc * fp > 64 or 64 * kw > kw_max_threads(fc * fp):
+                continue
+            if kw > 1 and steps / kw < 2:
+                continue
+            out.append((kw_cfg(fc, fp), 1, kw))
+    for cfg in range(len(CONV_CONFIGS)):  # v1 (cross-workgroup split-K) kept as candidates
+        c, sk = _v1_choice(M, cout, K, cfg)
+        out.append((cfg, sk, 1))
+    return out
+
+
+def _v1_choice(M, cout, K, cfg):
+    steps = max(1, math.ceil(K / 32))
+    bnc, bmp = tile_dims(cfg)
+    tiles = math.ceil(cout / bnc) * math.ceil(M / bmp)
+    want = max(1, math.ceil(NUM_CUS / tiles))
+    return cfg, max(1, min(want, steps // 4, 32))
+
+
+def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str | None = None):
+    """Pick (cfg, splitk, kw) for an implicit GEMM of M pixels x cout channels x K.
+
+    A measured table (``tuned``, produced on the GPU by ``hipzap.engine.tune``) wins. The
+    fallback heuristic uses the K-across-waves kernel: the smallest output tile that still
+    yields >= 1 workgroup per CU, then enough waves per workgroup that each wave streams
+    ~6 K-steps.
     """
     if tuned is not None and key is not None and key in tuned:
-        cfg, splitk = tuned[key]
-        return int(cfg), int(splitk)
+        v = tuned[key]
+        return int(v[0]), int(v[1]), int(v[2]) if len(v) > 2 else 1
     steps = max(1, math.ceil(K / 32))
-    best = None
-    for cfg in range(len(CONV_CONFIGS)):
-        if cfg == 5 and M * cout < 512 * 512:  # 128x128 only for big problems
-            continue
-        bnc, bmp = tile_dims(cfg)
-        tiles = math.ceil(cout / bnc) * math.ceil(M / bmp)
-        padded = tiles * bnc * bmp
-        want = max(1, math.ceil(NUM_CUS / tiles))
-        splitk = max(1, min(want, steps // 4, 32))
-        nblk = tiles * splitk
-        kps = math.ceil(steps / splitk)
-        # time ~ waves of blocks x per-block (fixed + per-step cost growing with tile area)
-        waves = math.ceil(nblk / (NUM_CUS * 2))
-        per_step = 1.0 + 0.12 * (bnc * bmp) / 1024.0
-        t = waves * (6.0 + kps * per_step) + (2.0 if splitk > 1 else 0.0) + 1e-6 * padded
-        if best is None or t < best[0]:
-            best = (t, cfg, splitk)
-    return best[1], best[2]
+    fc, fp = 1, 1
+    full = []
+    for (a, b) in KW_TILES:
+        tiles = math.ceil(cout / (16 * a)) * math.ceil(M / (16 * b))
+        waste = tiles * 256 * a * b / max(1, M * cout)
+        if tiles >= NUM_CUS and waste < 1.3:
+            full.append((a * b, -waste, a, b))
+    if full:
+        _, _, fc, fp = max(full)
+    kw = 1
+    while kw * 2 <= 16 and steps / (kw * 2) >= 6 and kw * 2 * fc * fp <= 64 and 128 * kw <= kw_max_threads(fc * fp):
+        kw *= 2
+    return kw_cfg(fc, fp), 1, kw
 
 
 def split_k_slice(K: int, splitk: int) -> int:
@@ -121,7 +163,7 @@ def split_k_slice(K: int, splitk: int) -> int:
 
 def workspace_bytes(M: int, cout: int, cfg: int, splitk: int) -> tuple[int, int]:
     """(slab bytes, counter ints) for a split-K launch."""
-    if splitk <= 1:
+    if splitk <= 1 or cfg >= 100:
         return 0, 0
     wc, wp, fc, fp = CONV_CONFIGS[cfg]
     bnc, bmp = tile_dims(cfg)
@@ -130,7 +172,7 @@ def workspace_bytes(M: int, cout: int, cfg: int, splitk: int) -> tuple[int, int]
 
 
 def make_params(x_ptr, pc: PackedConv, n, h, w, out_ptr, res_ptr=0, act="relu", out_f32=False,
-                cfg=0, splitk=1, ws_ptr=0, cnt_ptr=0, ldo=None, ldr=None) -> tuple[N.ConvParams, int, int]:
+                cfg=0, splitk=1, ws_ptr=0, cnt_ptr=0, ldo=None, ldr=None, kw=1) -> tuple[N.ConvParams, int, int]:
     p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
     M = n * p_out * q_out
@@ -145,21 +187,23 @@ def make_params(x_ptr, pc: PackedConv, n, h, w, out_ptr, res_ptr=0, act="relu", 
     prm.act, prm.out_f32 = ACT[act], int(out_f32)
     prm.splitk, prm.kslice = splitk, split_k_slice(pc.K, splitk)
     prm.tiles_n = 0
+    prm.kw = kw
     return prm, p_out, q_out
 
 
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None = None, act: str = "relu",
-                out_f32: bool = False, cfg: int | None = None, splitk: int | None = None) -> torch.Tensor:
+                out_f32: bool = False, cfg: int | None = None, splitk: int | None = None,
+                kw: int | None = None) -> torch.Tensor:
     """Eager launch: x NHWC bf16 [N,H,W,Cin_pad] -> NHWC [N,P,Q,Cout] (bf16 or fp32)."""
     assert x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[-1] == pc.cin
     n, h, w, _ = x.shape
     p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
     M = n * p_out * q_out
-    if cfg is None or splitk is None:
-        c2, s2 = choose_config(M, pc.cout, pc.K)
-        cfg = c2 if cfg is None else cfg
-        splitk = s2 if splitk is None else splitk
+    if cfg is None:
+        cfg, splitk, kw = choose_config(M, pc.cout, pc.K)
+    splitk = 1 if splitk is None else splitk
+    kw = 1 if kw is None else kw
     out = torch.empty(n, p_out, q_out, pc.cout, device=x.device,
                       dtype=torch.float32 if out_f32 else torch.bfloat16)
     ws_b, n_cnt = workspace_bytes(M, pc.cout, cfg, splitk)
@@ -169,7 +213,7 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None =
         assert residual.dtype == torch.bfloat16 and residual.is_contiguous()
         assert residual.numel() == M * pc.cout
     prm, _, _ = make_params(x.data_ptr(), pc, n, h, w, out.data_ptr(), N.ptr(residual), act, out_f32,
-                            cfg, splitk, ws.data_ptr(), cnt.data_ptr())
+                            cfg, splitk, ws.data_ptr(), cnt.data_ptr(), kw=kw)
     N.check(N.lib().hz_conv_launch(prm, cfg, N.stream_ptr()), "hz_conv_launch")
     return out
 

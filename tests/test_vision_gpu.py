@@ -14,7 +14,7 @@ def _rand_bn(c, g):
             "running_mean": 0.1 * torch.randn(c, generator=g), "running_var": 0.5 + torch.rand(c, generator=g)}
 
 
-def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None, splitk=None, seed=0):
+def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None, splitk=None, seed=0, kw=None):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, cin, h, h, generator=g)
     w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
@@ -33,7 +33,7 @@ def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None,
         ref = torch.relu(ref)
     x_nhwc = torch.nn.functional.pad(xb.permute(0, 2, 3, 1), (0, pc.cin - cin)).to(torch.bfloat16)
     r_nhwc = None if res is None else res.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
-    out = C.conv2d_nhwc(x_nhwc.contiguous().to(DEV), pc.to(DEV), r_nhwc, act=act, cfg=cfg, splitk=splitk)
+    out = C.conv2d_nhwc(x_nhwc.contiguous().to(DEV), pc.to(DEV), r_nhwc, act=act, cfg=cfg, splitk=splitk, kw=kw)
     torch.cuda.synchronize()
     got = out.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs().max().item()
@@ -63,6 +63,24 @@ def test_conv_heuristic(shape):
 @pytest.mark.parametrize("splitk", [1, 3])
 def test_conv_every_config(cfg, splitk):
     assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, splitk=splitk) < 2e-2
+
+
+@pytest.mark.parametrize("tile", C.KW_TILES)
+@pytest.mark.parametrize("kw", [1, 2, 4, 16])
+def test_conv_kw_every_tile(tile, kw):
+    fc, fp = tile
+    if kw * fc * fp > 64 or 64 * kw > C.kw_max_threads(fc * fp):
+        pytest.skip("illegal combo")
+    cfg = C.kw_cfg(fc, fp)
+    assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, splitk=1, kw=kw) < 2e-2
+    assert _case(2, 3, 20, 64, 7, 2, 3, cfg=cfg, splitk=1, kw=kw) < 2e-2  # generic-K path
+    assert _case(1, 64, 9, 128, 1, 1, 0, residual=True, cfg=cfg, splitk=1, kw=kw) < 2e-2  # 1x1 path
+
+
+def test_conv_candidates_all_launch():
+    for cand in C.candidates(49, 512, 4608):
+        cfg, sk, kw = cand
+        assert _case(1, 512, 7, 512, 3, 1, 1, residual=True, cfg=cfg, splitk=sk, kw=kw) < 2e-2, cand
 
 
 def test_conv_splitk_deep():
