@@ -69,6 +69,10 @@ def _load():
     _sig(lib, "hz_prog_replay", c_int, P, P)
     _sig(lib, "hz_prog_is_captured", c_int, P)
     _sig(lib, "hz_prog_bench", c_double, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int)
+    _sig(lib, "hz_prog_bench2", c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int, c_int,
+         C.POINTER(c_double))
+    _sig(lib, "hz_diag_launch", c_int, c_int, c_int, c_int, P, P, c_long, P)
+    _sig(lib, "hz_prog_add_diag", c_int, P, c_int, c_int, c_int, P, P, c_long, c_int)
     for extra in _EXTRA_SIGS:
         extra(lib)
     return lib

@@ -67,6 +67,10 @@ int hz_prog_is_captured(HzProgram p);
 // replay `n` programs round-robin on `n` streams `iters` times from C++ and synchronize;
 // returns elapsed microseconds (host wall, includes the final sync) or negative on error.
 double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters);
+int hz_prog_bench2(HzProgram* progs, hipStream_t* streams, int n, int iters, int threads, double* out);
+// diagnostics (csrc/diag.hip): kind 0 = no-op kernel, 1 = copy `bytes` from a to b
+int hz_diag_launch(int kind, int blocks, int threads, void* a, void* b, long bytes, hipStream_t st);
+int hz_prog_add_diag(HzProgram p, int kind, int blocks, int threads, void* a, void* b, long bytes, int slot);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "hipzap.h"
@@ -170,6 +171,38 @@ double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters) {
     if (hipStreamSynchronize(streams[i]) != hipSuccess) return -2.0;
   auto t1 = std::chrono::steady_clock::now();
   return std::chrono::duration<double, std::micro>(t1 - t0).count();
+}
+
+int hz_prog_add_diag(HzProgram h, int kind, int blocks, int threads, void* a, void* b, long bytes, int slot) {
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [=](hipStream_t s) { return hz_diag_launch(kind, blocks, threads, a, b, bytes, s); });
+}
+
+// out[0] = host submission time (us), out[1] = submission + drain (us).
+// threads != 0: one host thread per stream submits its own replays concurrently.
+int hz_prog_bench2(HzProgram* progs, hipStream_t* streams, int n, int iters, int threads, double* out) {
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = 0;
+  if (!threads) {
+    for (int it = 0; it < iters && !rc; ++it)
+      for (int i = 0; i < n && !rc; ++i) rc = hz_prog_replay(progs[i], streams[i]);
+  } else {
+    std::vector<std::thread> th;
+    std::vector<int> rcs(n, 0);
+    for (int i = 0; i < n; ++i)
+      th.emplace_back([&, i] {
+        for (int it = 0; it < iters && !rcs[i]; ++it) rcs[i] = hz_prog_replay(progs[i], streams[i]);
+      });
+    for (auto& t : th) t.join();
+    for (int r : rcs) rc |= r;
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i)
+    if (hipStreamSynchronize(streams[i]) != hipSuccess) rc = -2;
+  auto t2 = std::chrono::steady_clock::now();
+  out[0] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+  out[1] = std::chrono::duration<double, std::micro>(t2 - t0).count();
+  return rc;
 }
 
 }  // extern "C"
