@@ -1,0 +1,172 @@
+"""Model server: lazily cold-loads models once per process and keeps them warm.
+
+The reference rebuilt and reloaded the AWD-LSTM on EVERY request (main.py:84-103, measured
+8.9 s per GET /inference in SURVEY.md §6). Here a model is loaded on first use (the "cold
+start" of a Lambda container) and every later request reuses the packed weights and the
+captured hipGraphs (the warm path). Backends:
+  * ``gpu``: the native hipzap Engine (HIP kernels, hipGraph replay) — default whenever a GPU
+    is visible; the native library is REQUIRED there (no silent eager fallback);
+  * ``cpu``: eager PyTorch on the host — the BASELINE config-1 "CPU plumbing" path and the
+    development path in GPU-less containers.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+
+import torch
+
+from ..models import registry
+from .artifacts import ArtifactStore
+from .settings import ModelSpec, Settings
+from .text import generate_text, load_itos, make_stoi
+
+log = logging.getLogger("hipzap.server")
+
+
+def _random_state_dict(name: str, seed: int = 0) -> dict:
+    from ..models.resnet import randomize_bn
+    torch.manual_seed(seed)
+    m = registry.get(name).make_model()
+    if hasattr(m, "layer1"):
+        randomize_bn(m, seed)
+    return m.eval().state_dict()
+
+
+class VisionBackend:
+    def __init__(self, name: str, sd: dict, backend: str, device: str, spec: ModelSpec, capture: bool):
+        self.name, self.backend = name, backend
+        t0 = time.perf_counter()
+        self.adapter = registry.get(name)
+        if backend == "gpu":
+            from ..engine.engine import Engine
+            self.engine = Engine.from_state_dict(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
+                                                 capture=capture)
+            self.model = None
+        else:
+            from ..models.resnet import infer_arch
+            _, ncls = infer_arch(sd)
+            self.model = self.adapter.make_model(ncls)
+            self.model.load_state_dict(sd)
+            self.model.eval()
+            self.engine = None
+        self.batch = spec.batch
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if self.engine is not None:
+            outs = []
+            for i in range(0, x.shape[0], self.batch):
+                chunk = x[i: i + self.batch]
+                n = chunk.shape[0]
+                if n < self.batch:  # pad the remainder to the captured batch size
+                    chunk = torch.cat([chunk, chunk.new_zeros((self.batch - n,) + tuple(chunk.shape[1:]))])
+                outs.append(self.engine.infer(chunk)[:n])
+            return torch.cat(outs)
+        with torch.no_grad():
+            return self.model(x.float())
+
+
+class LMBackend:
+    """AWD-LSTM text generation (GET /inference)."""
+
+    def __init__(self, sd: dict, itos: list, backend: str, device: str):
+        from ..models.awd_lstm import reference_lm
+        t0 = time.perf_counter()
+        self.itos, self.stoi = itos, make_stoi(itos)
+        self.backend = backend
+        if backend == "gpu":
+            from ..engine.lm import LMEngine
+            self.engine = LMEngine.from_state_dict(sd, device)
+            self.model = None
+        else:
+            self.model = reference_lm(len(itos))
+            self.model.load_state_dict(sd)
+            self.model.eval()
+            self.engine = None
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+        self._lock = threading.Lock()
+
+    def generate(self, prompt_words, n_words, seed=None) -> str:
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        with self._lock:  # the recurrent state makes one model non-reentrant
+            if self.engine is not None:
+                return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)
+            with torch.no_grad():
+                def step(tok):
+                    res, *_ = self.model(torch.tensor([[tok]]))
+                    return res[-1]
+                return generate_text(step, self.model.reset, self.itos, self.stoi, prompt_words, n_words, gen)
+
+
+class ModelServer:
+    def __init__(self, settings: Settings, backend: str | None = None):
+        self.settings = settings
+        self.store = ArtifactStore(settings.models_bucket, settings.artifact_root)
+        if backend is None:
+            backend = os.environ.get("HIPZAP_BACKEND") or ("gpu" if torch.cuda.is_available() else "cpu")
+        self.backend = backend
+        self.device = f"cuda:{settings.devices[0]}" if backend == "gpu" else "cpu"
+        self._models: dict = {}
+        self._lock = threading.Lock()
+        self.stats = {"requests": 0, "errors": 0, "cold_loads": 0}
+
+    def spec(self, name: str) -> ModelSpec:
+        return self.settings.models.get(name) or ModelSpec(name=name)
+
+    def _load_sd(self, spec: ModelSpec) -> dict:
+        if spec.key in (None, "random") or os.environ.get("HIPZAP_RANDOM_WEIGHTS"):
+            log.warning("model %s: no checkpoint key configured, using random-init weights", spec.name)
+            return _random_state_dict(spec.name)
+        path = self.store.fetch(spec.key)
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and isinstance(sd.get("state_dict"), dict):
+            sd = sd["state_dict"]
+        return sd
+
+    def vision(self, name: str) -> VisionBackend:
+        with self._lock:
+            if name not in self._models:
+                spec = self.spec(name)
+                sd = self._load_sd(spec)
+                self._models[name] = VisionBackend(spec.name, sd, self.backend, self.device, spec,
+                                                   self.settings.capture_graphs)
+                self.stats["cold_loads"] += 1
+            return self._models[name]
+
+    def lm(self) -> LMBackend:
+        key = "__lm__"
+        with self._lock:
+            if key not in self._models:
+                st = self.settings
+                if os.environ.get("HIPZAP_RANDOM_WEIGHTS") or st.models_bucket is None:
+                    from ..models.awd_lstm import reference_lm
+                    itos = synthetic_vocab(int(os.environ.get("HIPZAP_LM_VOCAB", 2000)))
+                    torch.manual_seed(0)
+                    sd = reference_lm(len(itos)).state_dict()
+                else:
+                    itos = load_itos(self.store.fetch(st.lm_vocab_key))
+                    sd = torch.load(self.store.fetch(st.lm_model_key), map_location="cpu", weights_only=True)
+                self._models[key] = LMBackend(sd, itos, self.backend, self.device)
+                self.stats["cold_loads"] += 1
+            return self._models[key]
+
+    def loaded(self) -> dict:
+        return {k: {"backend": getattr(v, "backend", "?"), "cold_ms": round(getattr(v, "cold_ms", 0), 1)}
+                for k, v in self._models.items()}
+
+
+def synthetic_vocab(n: int) -> list[str]:
+    """fastai-style vocabulary for random-weight demos: specials first, then pseudo-words."""
+    specials = ["xxunk", "xxpad", "xxbos", "xxfld", "xxmaj", "xxup", "xxrep", "xxwrep", ".", ",", "!", "?", "'s",
+                "\n", "the", "a", "and", "to", "of", "i", "you", "it", "is", "that", "what", "why", "did"]
+    words = list(specials)
+    syll = ["ka", "lo", "mi", "ne", "ru", "ta", "bo", "shi", "en", "po", "di", "ga"]
+    i = 0
+    while len(words) < n:
+        a, b = divmod(i, len(syll))
+        words.append(syll[a % len(syll)] + syll[b] + ("" if i % 3 else "s"))
+        i += 1
+    return words[:n]
