@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 4)),
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 8)),
                     help="concurrent bs=1 request contexts per GPU")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
     ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds for p50")
@@ -99,11 +99,9 @@ def main():
     ckpt = os.path.join(args.ckpt_dir, f"{args.model}_seed0.pth")
     if rank == 0 and not os.path.exists(ckpt):
         write_checkpoint(ckpt, args.model)
-    tuned = None
-    tpath = args.tuned or os.path.join(os.path.dirname(os.path.abspath(__file__)), "hipzap", "tuning",
-                                       f"{args.model}_bs{args.batch}.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
+    tuned = None  # Engine picks hipzap/tuning/<model>_bs<B>[_c<streams>].json
+    if args.tuned:
+        with open(args.tuned) as f:
             tuned = json.load(f)
     if is_dist():
         dist.barrier()

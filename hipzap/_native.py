@@ -22,12 +22,10 @@ c_float_p = C.POINTER(C.c_float)
 class ConvParams(C.Structure):
     _fields_ = [
         ("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("res", c_void_p), ("out", c_void_p),
-        ("ws", c_void_p), ("cnt", c_void_p),
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int),
         ("Cout", c_int), ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int), ("P", c_int), ("Q", c_int),
-        ("M", c_int), ("K", c_int), ("ldw", c_int), ("ldo", c_int), ("ldr", c_int),
-        ("act", c_int), ("out_f32", c_int),
-        ("splitk", c_int), ("kslice", c_int),
+        ("M", c_int), ("K", c_int), ("ksteps", c_int),
+        ("act", c_int), ("out_f32", c_int), ("out_rowmajor", c_int), ("ldo", c_int),
         ("tiles_n", c_int), ("kw", c_int),
     ]
 
@@ -50,7 +48,7 @@ def _load():
     P = c_void_p
     _sig(lib, "hz_conv_launch", c_int, C.POINTER(ConvParams), c_int, P)
     _sig(lib, "hz_maxpool_launch", c_int, C.POINTER(PoolParams), P)
-    _sig(lib, "hz_avgpool_launch", c_int, P, P, c_int, c_int, c_int, P)
+    _sig(lib, "hz_avgpool_launch", c_int, P, P, c_int, c_int, c_int, c_int, P)
     _sig(lib, "hz_preprocess_launch", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P)
     _sig(lib, "hz_cast_f32_bf16", c_int, P, P, c_long, P)
     _sig(lib, "hz_cast_bf16_f32", c_int, P, P, c_long, P)
@@ -59,7 +57,7 @@ def _load():
     _sig(lib, "hz_prog_num_ops", c_int, P)
     _sig(lib, "hz_prog_add_conv", c_int, P, C.POINTER(ConvParams), c_int, c_int)
     _sig(lib, "hz_prog_add_maxpool", c_int, P, C.POINTER(PoolParams), c_int)
-    _sig(lib, "hz_prog_add_avgpool", c_int, P, P, P, c_int, c_int, c_int, c_int)
+    _sig(lib, "hz_prog_add_avgpool", c_int, P, P, P, c_int, c_int, c_int, c_int, c_int)
     _sig(lib, "hz_prog_add_preprocess", c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int)
     _sig(lib, "hz_prog_add_memcpy", c_int, P, P, P, C.c_size_t, c_int)
     _sig(lib, "hz_prog_add_fork", c_int, P, c_int)

@@ -1,85 +1,88 @@
-// Implicit-GEMM convolution (and plain GEMM/Linear as the 1x1 case) on CDNA4 MFMA.
+// Implicit-GEMM convolution / Linear on CDNA4 MFMA (mfma_f32_16x16x32_bf16) with a fused
+// epilogue (folded-BN bias, residual add, ReLU/GELU/tanh, bf16 or fp32 out).
 //
 //   out[m][n] = act( sum_k W[n][k] * im2col(X)[m][k] + bias[n] (+ res[m][n]) )
 //
-// * Activations are NHWC bf16, so an 8-element K chunk of one im2col row is 16 contiguous
-//   bytes of one input pixel: every MFMA fragment is one 16-B global load straight into
-//   VGPRs (no LDS round trip — the latency-bound bs=1 regime of cdna_hip_programming.md §5,
-//   'GEMV / M <= 16' row; operands are L2/MALL resident, ResNet-50 bf16 is 51 MB).
-// * "Swapped" orientation: the MFMA A operand is the weight (rows = output channels), B is
-//   the activation (cols = output pixels). With mfma_f32_16x16x32_bf16's C/D map
-//   (col = lane&15, row = 4*(lane>>4)+i) each lane then owns 4 CONSECUTIVE output channels
-//   of one pixel, so the fused epilogue (folded-BN bias, residual add, ReLU) does one 16-B
-//   bias load, one 8-B residual load and one 8-B store per accumulator.
-// * bs=1 late stages have tiny M (49 px) and huge K (4608): split-K across workgroups with
-//   an in-launch last-arriver reduction (agent-scope release/acquire ticket protocol of
-//   cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2), so a split conv is
-//   still ONE launch and the partial slabs never leave L2 for long.
-// * Register-ring software pipeline: fragments of step t+DEPTH are in flight while step t
-//   computes (hipcc emits counted vmcnt waits for plain loads).
-//
-// Reference parity: this replaces the conv/BN/ReLU stack the north star asks for
-// (SURVEY.md §2e N1, N3-FC, N4); the reference itself only runs aten::addmm/lstm on CPU
-// (SURVEY.md §2d).
+// Design (bs=1 serving on MI355X; see DESIGN.md "conv kernel"):
+// * K across waves: a workgroup of KW waves owns one (FC*16 channels x FP*16 pixels)
+//   output tile; wave w streams 1/KW of K and the partial accumulators are summed through
+//   LDS in wave order (deterministic). No cross-workgroup split-K: the first MI355X profile
+//   showed the last-arriver slab reduction (agent release/acquire + serial slab reads)
+//   costing 5-25 us per layer.
+// * "Swapped" orientation: MFMA A = weights (rows = output channels), B = activations
+//   (cols = output pixels); with the 16x16 C/D map (col = lane&15, row = 4*(lane>>4)+i) a
+//   lane owns 4 consecutive channels of one pixel: one 16-B bias load, one 8-B residual
+//   load, one 8-B store per accumulator.
+// * Fragment-major weights: packed once at load time as [Cout/16][K/32][64 lanes][8], so
+//   every A-fragment load of a wave is ONE contiguous, aligned 1 KiB (8 cache lines)
+//   instead of 16 rows x 64 B (16 half-used lines).
+// * Channel-blocked activations [N][C/32][H][W][32]: the B fragment of 16 neighbouring
+//   pixels x 32 channels is one contiguous 1 KiB as well (1x1 convs; 3x3 convs get 1 KiB
+//   runs along an image row). Inputs with C < 32 (the 8-channel stem) are plain NHWC.
+// * Each wave streams straight to VGPRs through a DEPTH-deep register ring (every operand
+//   byte is used by exactly one wave at bs=1, so an LDS round trip would be pure cost:
+//   cdna_hip_programming.md §5 'GEMV / M <= 16' row).
 #include "common.h"
 #include "hipzap.h"
 
 namespace {
 
-constexpr int THREADS = 256;
-constexpr int DEPTH = 2;  // loads in flight ahead of the MFMA step
+template <int FC, int FP>
+struct Depth {
+  static constexpr int value = (FC + FP <= 2) ? 6 : (FC + FP <= 3) ? 4 : (FC + FP <= 4) ? 3 : 2;
+};
 
-template <int WC, int WP, int FC, int FP, bool FAST, bool IS1X1>
-__global__ __launch_bounds__(THREADS) void conv_igemm_kernel(const HzConvParams p) {
-  static_assert(WC * WP == 4, "4 waves");
-  constexpr int BNC = WC * FC * 16;  // output channels per block
-  constexpr int BMP = WP * FP * 16;  // output pixels per block
+// keep the register ring out of scratch: 1024 threads cap a wave at 128 VGPRs
+constexpr int conv_max_threads(int nf) { return nf >= 16 ? 256 : nf >= 8 ? 512 : 1024; }
+
+template <int FC, int FP, bool FAST, bool IS1X1>
+__global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const HzConvParams p) {
+  constexpr int DEPTH = Depth<FC, FP>::value;
+  constexpr int NF = FC * FP;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave % WC, wp = wave / WC;
+  const int KW = blockDim.x >> 6;
   const int lrow = lane & 15, lk = (lane >> 4) * 8;
 
-  const int nwg = gridDim.x;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  const int tile = lid / p.splitk;
-  const int slice = lid - tile * p.splitk;
-  const int tile_n = tile % p.tiles_n;
-  const int tile_m = tile / p.tiles_n;
-  const int n0 = tile_n * BNC + wc * FC * 16;
-  const int m0 = tile_m * BMP + wp * FP * 16;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lid % p.tiles_n;
+  const int tile_m = lid / p.tiles_n;
+  const int n0 = tile_n * FC * 16;
+  const int m0 = tile_m * FP * 16;
 
-  const int K = p.K, C = p.C;
-  const int k_begin = slice * p.kslice;
-  const int k_end = min(K, k_begin + p.kslice);
-  const int nsteps = (k_end - k_begin + 31) >> 5;
+  const int C = p.C, HW = p.H * p.W;
+  const int steps = p.ksteps;
+  const int spw = (steps + KW - 1) / KW;
+  const int s_begin = wave * spw;
+  const int nsteps = max(0, min(steps, s_begin + spw) - s_begin);
 
-  // ---- per-pixel precompute (B operand rows = output pixels) ----
-  int pbase[FP], pih[FP], piw[FP];
+  // ---- per-pixel precompute (B operand columns = output pixels) ----
+  int pb[FP], pih[FP], piw[FP];
   bool pval[FP];
+  const int PQ = p.P * p.Q;
 #pragma unroll
   for (int f = 0; f < FP; ++f) {
     const int m = m0 + f * 16 + lrow;
     pval[f] = m < p.M;
     const int mm = pval[f] ? m : 0;
+    const int ni = mm / PQ;
+    const int hw = mm - ni * PQ;
+    const int nbase = FAST ? ni * (C >> 5) * HW : ni * HW;
     if constexpr (IS1X1) {
-      pbase[f] = mm * C;
-      pih[f] = 0;
-      piw[f] = 0;
+      pb[f] = nbase + hw;
+      pih[f] = piw[f] = 0;
     } else {
-      const int PQ = p.P * p.Q;
-      const int ni = mm / PQ;
-      const int rem = mm - ni * PQ;
-      const int oh = rem / p.Q;
-      const int ow = rem - oh * p.Q;
+      const int oh = hw / p.Q;
+      const int ow = hw - oh * p.Q;
       pih[f] = oh * p.stride - p.pad;
       piw[f] = ow * p.stride - p.pad;
-      pbase[f] = ni * p.H * p.W;
+      pb[f] = nbase;
     }
   }
   const bf16_t* __restrict__ X = p.x;
-  const bf16_t* __restrict__ Wt = p.w;
-  const long ldw = p.ldw;
+  // fragment-major weights: fragment (row group g, k-step s) at ((g*ksteps + s)*64 + lane)*8
+  const bf16_t* __restrict__ Wf = p.w + ((long)(n0 >> 4) * steps) * 512 + lane * 8;
 
   bf16x8 fa[DEPTH + 1][FC], fb[DEPTH + 1][FP];
   f32x4 acc[FC][FP];
@@ -89,49 +92,51 @@ __global__ __launch_bounds__(THREADS) void conv_igemm_kernel(const HzConvParams 
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP]) {
-    const int k = k_begin + t * 32;  // wave-uniform
-    const int kk = k + lk;           // this lane's 8-chunk
+    const int s_idx = s_begin + t;
+    const int k = s_idx * 32;
 #pragma unroll
-    for (int i = 0; i < FC; ++i) {
-      const bf16_t* src = Wt + (long)(n0 + i * 16 + lrow) * ldw + kk;
-      a[i] = *reinterpret_cast<const bf16x8*>(src);
-    }
-    if constexpr (IS1X1) {
+    for (int i = 0; i < FC; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(Wf + ((long)i * steps + s_idx) * 512);
+    if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
+      const int rs = k / C;
+      const int cb = (k - rs * C) >> 5;
+      if constexpr (IS1X1) {
 #pragma unroll
-      for (int j = 0; j < FP; ++j) {
-        if (pval[j]) b[j] = *reinterpret_cast<const bf16x8*>(X + (long)pbase[j] + kk);
-        else b[j] = bf16x8{};
-      }
-    } else {
-      int r, s, c;
-      bool kval = true;
-      if constexpr (FAST) {  // C % 32 == 0: (r,s) uniform over the 32-wide step
-        const int rs = k / C;
-        c = k - rs * C + lk;
-        r = rs / p.S;
-        s = rs - r * p.S;
+        for (int j = 0; j < FP; ++j) {
+          if (pval[j]) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + cb * HW) << 5) + lk);
+          else b[j] = bf16x8{};
+        }
       } else {
-        kval = kk < K;
-        const int rs = kk / C;
-        c = kk - rs * C;
-        r = rs / p.S;
-        s = rs - r * p.S;
+        const int r = rs / p.S;
+        const int s = rs - r * p.S;
+#pragma unroll
+        for (int j = 0; j < FP; ++j) {
+          const int ih = pih[j] + r, iw = piw[j] + s;
+          const bool v = pval[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+          if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + cb * HW + ih * p.W + iw) << 5) + lk);
+          else b[j] = bf16x8{};
+        }
       }
+    } else {  // plain NHWC input with C in {8, 16}: per-lane (r, s, c) decomposition
+      const int kk = k + lk;
+      const bool kval = kk < p.K;
+      const int rs = kk / C;
+      const int c = kk - rs * C;
+      const int r = rs / p.S;
+      const int s = rs - r * p.S;
 #pragma unroll
       for (int j = 0; j < FP; ++j) {
         const int ih = pih[j] + r, iw = piw[j] + s;
         const bool v = kval && pval[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pbase[j] + ih * p.W + iw)) * C + c);
+        if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + ih * p.W + iw)) * C + c);
         else b[j] = bf16x8{};
       }
     }
   };
 
-  // prologue
 #pragma unroll
   for (int u = 0; u < DEPTH; ++u)
     if (u < nsteps) load_step(u, fa[u], fb[u]);
-
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
@@ -147,132 +152,107 @@ __global__ __launch_bounds__(THREADS) void conv_igemm_kernel(const HzConvParams 
     }
   }
 
-  // ---- split-K: in-launch last-arriver reduction ----
-  if (p.splitk > 1) {
-    __shared__ int s_last;
-    f32x4* slab = reinterpret_cast<f32x4*>(p.ws) + (long)(tile * p.splitk) * (FC * FP * THREADS);
-    f32x4* mine = slab + (long)slice * (FC * FP * THREADS);
-#pragma unroll
-    for (int i = 0; i < FC; ++i)
-#pragma unroll
-      for (int j = 0; j < FP; ++j) mine[(i * FP + j) * THREADS + tid] = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = (old == p.splitk - 1);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // deterministic: sum the slices in slice order whoever arrives last
-    f32x4 tot[FC][FP];
-#pragma unroll
-    for (int i = 0; i < FC; ++i)
-#pragma unroll
-      for (int j = 0; j < FP; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < p.splitk; ++sl) {
-      const f32x4* other = slab + (long)sl * (FC * FP * THREADS);
-#pragma unroll
-      for (int i = 0; i < FC; ++i)
-#pragma unroll
-        for (int j = 0; j < FP; ++j) tot[i][j] += (sl == slice) ? acc[i][j] : other[(i * FP + j) * THREADS + tid];
-    }
-#pragma unroll
-    for (int i = 0; i < FC; ++i)
-#pragma unroll
-      for (int j = 0; j < FP; ++j) acc[i][j] = tot[i][j];
-    if (tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-
-  // ---- fused epilogue: bias (folded BN) + residual + ReLU, 4 consecutive channels/lane ----
-#pragma unroll
-  for (int j = 0; j < FP; ++j) {
+  auto epilogue = [&](int i, int j, f32x4 a) {
     const int m = m0 + j * 16 + lrow;
-    if (m >= p.M) continue;
+    const int n = n0 + i * 16 + (lane >> 4) * 4;
+    if (m >= p.M || n >= p.Cout) return;
+    float v[4] = {a[0], a[1], a[2], a[3]};
+    if (p.bias) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
 #pragma unroll
-    for (int i = 0; i < FC; ++i) {
-      const int n = n0 + i * 16 + (lane >> 4) * 4;
-      if (n >= p.Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bb[e];
-      }
-      const long o = (long)m * p.ldo + n;
-      if (p.res) {
-        const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + (long)m * p.ldr + n);
-        v[0] += __uint_as_float(rr[0] << 16);
-        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-        v[2] += __uint_as_float(rr[1] << 16);
-        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
-      }
-      if (p.act == HZ_ACT_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      } else if (p.act == HZ_ACT_GELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-      } else if (p.act == HZ_ACT_TANH) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-      }
-      if (p.out_f32) {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
-      } else {
-        *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-      }
+      for (int e = 0; e < 4; ++e) v[e] += bb[e];
     }
+    long o;
+    if (p.out_rowmajor) {
+      o = (long)m * p.ldo + n;
+    } else {  // channel-blocked [N][Cout/32][P*Q][32]
+      const int ni = m / PQ;
+      const int hw = m - ni * PQ;
+      o = (((long)ni * (p.Cout >> 5) + (n >> 5)) * PQ + hw) * 32 + (n & 31);
+    }
+    if (p.res) {
+      const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
+      v[0] += __uint_as_float(rr[0] << 16);
+      v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+      v[2] += __uint_as_float(rr[1] << 16);
+      v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+    }
+    if (p.act == HZ_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (p.act == HZ_ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+    } else if (p.act == HZ_ACT_TANH) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+    }
+    if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+    else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  };
+
+  if (KW == 1) {
+#pragma unroll
+    for (int i = 0; i < FC; ++i)
+#pragma unroll
+      for (int j = 0; j < FP; ++j) epilogue(i, j, acc[i][j]);
+    return;
   }
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  f32x4* red = reinterpret_cast<f32x4*>(smem_raw);  // [KW][NF][64], lane-linear: conflict-free
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) red[(wave * NF + i * FP + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) {
+      const int ij = i * FP + j;
+      if ((ij % KW) != wave) continue;
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < KW; ++w) s += red[(w * NF + ij) * 64 + lane];
+      epilogue(i, j, s);
+    }
 }
 
-template <int WC, int WP, int FC, int FP>
-int launch_cfg(const HzConvParams& p, hipStream_t st) {
-  constexpr int BNC = WC * FC * 16, BMP = WP * FP * 16;
+template <int FC, int FP>
+int launch(const HzConvParams& p, hipStream_t st) {
   HzConvParams q = p;
-  q.tiles_n = (p.Cout + BNC - 1) / BNC;
-  const int tiles_m = (p.M + BMP - 1) / BMP;
-  const int nblk = q.tiles_n * tiles_m * q.splitk;
+  const int kw = p.kw < 1 ? 1 : p.kw;
+  if (kw > 16 || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP)) return -5;
+  q.tiles_n = (p.Cout + FC * 16 - 1) / (FC * 16);
+  const int tiles_m = (p.M + FP * 16 - 1) / (FP * 16);
   const bool is1x1 = p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0;
   const bool fast = (p.C % 32) == 0;
-  dim3 grid(nblk), block(THREADS);
-  if (is1x1 && fast)
-    hipLaunchKernelGGL((conv_igemm_kernel<WC, WP, FC, FP, true, true>), grid, block, 0, st, q);
-  else if (fast)
-    hipLaunchKernelGGL((conv_igemm_kernel<WC, WP, FC, FP, true, false>), grid, block, 0, st, q);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<WC, WP, FC, FP, false, false>), grid, block, 0, st, q);
+  dim3 grid(q.tiles_n * tiles_m), block(64 * kw);
+  const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
+  if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true>), grid, block, lds, st, q);
+  else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false>), grid, block, lds, st, q);
+  else hipLaunchKernelGGL((conv_kernel<FC, FP, false, false>), grid, block, lds, st, q);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// Config table: (WC, WP, FC, FP). Block tile = (WC*FC*16 channels) x (WP*FP*16 pixels).
-// Index order is part of the ABI with hipzap/ops/conv.py (CONV_CONFIGS).
+// cfg = fci*3 + fpi with FC = 1<<fci, FP = 1<<fpi (1, 2, 4); waves per workgroup = p->kw.
+// Mirrored by hipzap/ops/conv.py (TILES).
 extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
-  if (p.Cout % 4 != 0 || p.C % 8 != 0 || p.ldw % 32 != 0 || p.splitk < 1) return -1;
-  if (cfg >= 100) return hz_conv_kw_launch(pp, cfg, st);
+  if (p.Cout % 4 != 0 || p.C % 8 != 0 || (p.C % 32 != 0 && p.C > 16)) return -1;
+  if (!p.out_rowmajor && p.Cout % 32 != 0) return -1;
+  if (p.ksteps * 32 < p.K) return -1;
   switch (cfg) {
-    case 0: return launch_cfg<2, 2, 2, 2>(p, st);  //  64ch x  64px
-    case 1: return launch_cfg<4, 1, 1, 1>(p, st);  //  64ch x  16px
-    case 2: return launch_cfg<4, 1, 2, 1>(p, st);  // 128ch x  16px
-    case 3: return launch_cfg<1, 4, 1, 1>(p, st);  //  16ch x  64px
-    case 4: return launch_cfg<2, 2, 1, 1>(p, st);  //  32ch x  32px
-    case 5: return launch_cfg<2, 2, 4, 4>(p, st);  // 128ch x 128px
-    case 6: return launch_cfg<2, 2, 2, 4>(p, st);  //  64ch x 128px
-    case 7: return launch_cfg<2, 2, 4, 2>(p, st);  // 128ch x  64px
-    case 8: return launch_cfg<4, 1, 1, 2>(p, st);  //  64ch x  32px
-    case 9: return launch_cfg<1, 4, 2, 1>(p, st);  //  32ch x  64px
-    case 10: return launch_cfg<4, 1, 2, 2>(p, st); // 128ch x  32px
-    case 11: return launch_cfg<1, 4, 1, 2>(p, st); //  16ch x 128px
+    case 0: return launch<1, 1>(p, st);
+    case 1: return launch<1, 2>(p, st);
+    case 2: return launch<1, 4>(p, st);
+    case 3: return launch<2, 1>(p, st);
+    case 4: return launch<2, 2>(p, st);
+    case 5: return launch<2, 4>(p, st);
+    case 6: return launch<4, 1>(p, st);
+    case 7: return launch<4, 2>(p, st);
+    case 8: return launch<4, 4>(p, st);
     default: return -2;
   }
 }

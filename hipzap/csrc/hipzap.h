@@ -11,24 +11,21 @@ extern "C" {
 enum { HZ_ACT_NONE = 0, HZ_ACT_RELU = 1, HZ_ACT_GELU = 2, HZ_ACT_TANH = 3 };
 
 typedef struct HzConvParams {
-  const unsigned short* x;   // NHWC bf16 input [N,H,W,C]
-  const unsigned short* w;   // bf16 weights [Cout_pad][ldw]; k = (r*S + s)*C + c
+  const unsigned short* x;   // input: channel-blocked [N][C/32][H][W][32] (C%32==0) or NHWC (C in {8,16})
+  const unsigned short* w;   // fragment-major bf16 weights [Cout_pad/16][ksteps][64][8]; k = (r*S + s)*C + c
   const float* bias;         // fp32 [Cout] or NULL
-  const unsigned short* res; // bf16 residual [M][ldr] or NULL
-  void* out;                 // bf16 or fp32 [M][ldo]
-  float* ws;                 // split-K slabs (splitk > 1)
-  int* cnt;                  // split-K tile tickets, zeroed once; self-resetting
+  const unsigned short* res; // bf16 residual, same layout as out, or NULL
+  void* out;                 // bf16 or fp32; channel-blocked, or row-major [M][ldo] if out_rowmajor
   int N, H, W, C;
   int Cout, R, S, stride, pad, P, Q;
-  int M, K, ldw, ldo, ldr;
-  int act, out_f32;
-  int splitk, kslice;
+  int M, K, ksteps;          // M = N*P*Q; ksteps = ceil(K/32)
+  int act, out_f32, out_rowmajor, ldo;
   int tiles_n;               // filled by the launcher
-  int kw;                    // v2 (cfg >= 100): waves per workgroup splitting K
+  int kw;                    // waves per workgroup splitting K
 } HzConvParams;
 
+// cfg: output tile (FC*16 channels x FP*16 pixels), cfg = log2(FC)*3 + log2(FP)
 int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t st);
-int hz_conv_kw_launch(const HzConvParams* p, int cfg, hipStream_t st);
 
 typedef struct HzPoolParams {
   const unsigned short* x;  // NHWC bf16
@@ -37,7 +34,8 @@ typedef struct HzPoolParams {
 } HzPoolParams;
 int hz_maxpool_launch(const HzPoolParams* p, hipStream_t st);
 // global average pool NHWC [N,H,W,C] -> [N,C] bf16
-int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, hipStream_t st);
+// blocked: x is [N][C/32][HW][32] instead of NHWC
+int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked, hipStream_t st);
 
 // image pre-processing: src NCHW fp32 (mode 0) or NHWC uint8 (mode 1) -> NHWC bf16 with Cpad channels
 int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
@@ -54,7 +52,8 @@ void hz_prog_destroy(HzProgram p);
 int hz_prog_num_ops(HzProgram p);
 int hz_prog_add_conv(HzProgram p, const HzConvParams* cp, int cfg, int slot);
 int hz_prog_add_maxpool(HzProgram p, const HzPoolParams* pp, int slot);
-int hz_prog_add_avgpool(HzProgram p, const unsigned short* x, unsigned short* out, int N, int HW, int C, int slot);
+int hz_prog_add_avgpool(HzProgram p, const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked,
+                        int slot);
 int hz_prog_add_preprocess(HzProgram p, const void* src, unsigned short* dst, int N, int Cin, int H, int W,
                            int Cpad, int mode, const float* mean, const float* inv_std, int slot);
 int hz_prog_add_memcpy(HzProgram p, void* dst, const void* src, size_t bytes, int slot);  // any direction (UVA)

@@ -104,9 +104,10 @@ int hz_prog_add_maxpool(HzProgram h, const HzPoolParams* pp, int slot) {
   HzPoolParams c = *pp;
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_maxpool_launch(&c, s); });
 }
-int hz_prog_add_avgpool(HzProgram h, const unsigned short* x, unsigned short* out, int N, int HW, int C, int slot) {
+int hz_prog_add_avgpool(HzProgram h, const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked,
+                        int slot) {
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
-                [=](hipStream_t s) { return hz_avgpool_launch(x, out, N, HW, C, s); });
+                [=](hipStream_t s) { return hz_avgpool_launch(x, out, N, HW, C, blocked, s); });
 }
 int hz_prog_add_preprocess(HzProgram h, const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
                            int mode, const float* mean, const float* inv_std, int slot) {

@@ -41,16 +41,19 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const HzPoolParams p) {
 // lanes, so every lane issues only ceil(HW/32) independent 16-B loads (a serial HW loop per
 // lane was a 49-deep dependent load chain: 15.7 us on MI355X), then an LDS reduction.
 __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
-                                                      int N, int HW, int C) {
+                                                      int N, int HW, int C, int blocked) {
   __shared__ float red[32][65];
   const int t = threadIdx.x, cg = t & 7, pl = t >> 3;
   const int cblk = C >> 6;
   const int n = blockIdx.x / cblk, c0 = (blockIdx.x - n * cblk) * 64;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bf16_t* base = x + (long)n * HW * C + c0 + cg * 8;
+  const int c = c0 + cg * 8;
+  // blocked: [N][C/32][HW][32]; else NHWC [N][HW][C]
+  const bf16_t* base = blocked ? x + (((long)n * (C >> 5) + (c >> 5)) * HW) * 32 + (c & 31) : x + (long)n * HW * C + c;
+  const long pstride = blocked ? 32 : C;
   for (int j = pl; j < HW; j += 32) {
     float f[8];
-    unpack8(*reinterpret_cast<const u32x4*>(base + (long)j * C), f);
+    unpack8(*reinterpret_cast<const u32x4*>(base + (long)j * pstride), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] += f[e];
   }
@@ -112,9 +115,10 @@ extern "C" int hz_maxpool_launch(const HzPoolParams* pp, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-extern "C" int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, hipStream_t st) {
+extern "C" int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked,
+                                 hipStream_t st) {
   if (C % 64) return -1;
-  hipLaunchKernelGGL(avgpool_kernel, dim3(N * (C / 64)), dim3(256), 0, st, x, out, N, HW, C);
+  hipLaunchKernelGGL(avgpool_kernel, dim3(N * (C / 64)), dim3(256), 0, st, x, out, N, HW, C, blocked);
   return (int)hipGetLastError();
 }
 

@@ -18,14 +18,18 @@ from ..models import registry
 from .program import ExecContext, bench_contexts
 
 
-def load_tuning(model: str, batch: int) -> dict | None:
-    """Measured launch-config table written by ``python -m hipzap.engine.tune`` (if any)."""
+def load_tuning(model: str, batch: int, contexts: int = 1) -> dict | None:
+    """Measured launch-config table written by ``python -m hipzap.engine.tune`` (if any).
+
+    Prefers the table tuned for the same request concurrency (``_c<contexts>``), falling back
+    to the single-stream (latency) table.
+    """
     import json
     from .tune import table_path
-    p = table_path(model, batch)
-    if p.exists():
-        with open(p) as f:
-            return json.load(f)
+    for p in (table_path(model, batch, contexts), table_path(model, batch, 1)):
+        if p.exists():
+            with open(p) as f:
+                return json.load(f)
     return None
 
 
@@ -41,7 +45,7 @@ class Engine:
         self.arch_kw = arch_kw or {}
         self.timings = dict(timings or {})
         if tuned is None:
-            tuned = load_tuning(model, batch)
+            tuned = load_tuning(model, batch, num_contexts)
         self.tuned = tuned
         t0 = time.perf_counter()
         with torch.cuda.device(self.device):

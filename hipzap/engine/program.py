@@ -9,8 +9,6 @@ hipGraph; ``replay()`` is the warm path.
 from __future__ import annotations
 
 import ctypes as C
-import math
-
 import torch
 
 from .. import _native as N
@@ -46,8 +44,7 @@ class ExecContext:
         self.tensor_offsets = offsets
         self.prog = lib.hz_prog_create()
         self.configs: list = []
-        # split-K workspace sizing pass
-        ws_total, cnt_total, conv_plans = 0, 0, []
+        conv_plans = []
         for n in g.nodes:
             if n.kind != "conv":
                 conv_plans.append(None)
@@ -56,18 +53,12 @@ class ExecContext:
             nb, h, w, _ = g.shape(n.inputs[0])
             p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
             q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
-            M = nb * p_out * q_out
-            key = f"{M}x{pc.cout}x{pc.K}x{pc.r}{pc.s}s{pc.stride}"
+            key = conv_ops.conv_key(nb * p_out * q_out, pc)
             if n.attrs.get("cfg") is not None:
-                cfg, splitk, kw = n.attrs["cfg"], n.attrs.get("splitk", 1), n.attrs.get("kw", 1)
+                cfg, kw = n.attrs["cfg"], n.attrs.get("kw", 1)
             else:
-                cfg, splitk, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
-            wsb, ncnt = conv_ops.workspace_bytes(M, pc.cout, cfg, splitk)
-            conv_plans.append((cfg, splitk, kw, ws_total, cnt_total, key))
-            ws_total += (wsb + 255) // 256 * 256
-            cnt_total += (ncnt + 63) // 64 * 64
-        self.ws = torch.empty(max(ws_total, 256), dtype=torch.uint8, device=self.device)
-        self.cnt = torch.zeros(max(cnt_total, 64), dtype=torch.int32, device=self.device)
+                cfg, kw = conv_ops.choose_config(nb * p_out * q_out, pc.cout, pc.K, tuned, key)
+            conv_plans.append((cfg, kw, key))
         # host_io: the request's PCIe transfers are part of the program (and of the graph):
         # pinned host input -> device input ... device output -> pinned host output.
         self.host_io = host_io
@@ -87,25 +78,26 @@ class ExecContext:
         g, addr = self.graph, self._addr
         if n.kind == "conv":
             pc = self.params[n.attrs["w"]]
-            cfg, splitk, kw, ws_off, cnt_off, key = plan
+            cfg, kw, key = plan
             nb, h, w, _ = g.shape(n.inputs[0])
             res = n.inputs[1] if len(n.inputs) > 1 else None
             prm, _, _ = conv_ops.make_params(
                 addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
-                n.attrs.get("out_f32", False), cfg, splitk,
-                self.ws.data_ptr() + ws_off, self.cnt.data_ptr() + 4 * cnt_off, kw=kw)
-            self.configs.append((n.attrs.get("name", ""), key, cfg, splitk, kw))
+                n.attrs.get("out_f32", False), cfg, kw, out_rowmajor=n.attrs.get("rowmajor", False))
+            self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
             N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_conv")
         elif n.kind == "maxpool":
             nb, h, w, c = g.shape(n.inputs[0])
             _, p, q, _ = g.shape(n.outputs[0])
             a = n.attrs
+            if conv_ops.is_blocked(c):  # [N][C/32][H][W][32] == NHWC with N*C/32 images of 32 ch
+                nb, c = nb * c // 32, 32
             prm = N.PoolParams(addr(n.inputs[0]), addr(n.outputs[0]), nb, h, w, c, p, q, a["k"], a["stride"], a["pad"])
             N.check(lib.hz_prog_add_maxpool(self.prog, C.byref(prm), n.slot), "add_maxpool")
         elif n.kind == "avgpool":
             nb, h, w, c = g.shape(n.inputs[0])
-            N.check(lib.hz_prog_add_avgpool(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, h * w, c, n.slot),
-                    "add_avgpool")
+            N.check(lib.hz_prog_add_avgpool(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, h * w, c,
+                                            int(conv_ops.is_blocked(c)), n.slot), "add_avgpool")
         elif n.kind == "preprocess":
             src = g.tensors[n.inputs[0]]
             if src.dtype == torch.uint8:

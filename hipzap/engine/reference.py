@@ -15,7 +15,7 @@ from .graph import Graph
 
 
 def _conv_ref(x_nhwc, pc, res=None, act="relu", out_f32=False):
-    w = pc.w[: pc.cout, : pc.K].float().reshape(pc.cout, pc.r, pc.s, pc.cin).permute(0, 3, 1, 2)
+    w = pc.dense().reshape(pc.cout, pc.r, pc.s, pc.cin).permute(0, 3, 1, 2)
     y = F.conv2d(x_nhwc.permute(0, 3, 1, 2).float(), w, pc.bias.float(), stride=pc.stride, padding=pc.pad)
     y = y.permute(0, 2, 3, 1)
     if res is not None:

@@ -29,7 +29,7 @@ REPS = 16
 
 
 def conv_shapes(graph, params) -> dict:
-    """key -> (node, PackedConv, (n,h,w), M) for each distinct conv shape."""
+    """key -> (PackedConv, (n,h,w), M, has_residual, act, out_f32) per distinct conv shape."""
     out = {}
     for n in graph.nodes:
         if n.kind != "conv":
@@ -39,64 +39,66 @@ def conv_shapes(graph, params) -> dict:
         p = (h + 2 * pc.pad - pc.r) // pc.stride + 1
         q = (w + 2 * pc.pad - pc.s) // pc.stride + 1
         M = nb * p * q
-        key = f"{M}x{pc.cout}x{pc.K}x{pc.r}{pc.s}s{pc.stride}"
-        res = len(n.inputs) > 1
-        out.setdefault(key, (n, pc, (nb, h, w), M, res, n.attrs.get("act", "relu"), n.attrs.get("out_f32", False)))
+        out.setdefault(conv_ops.conv_key(M, pc), (pc, (nb, h, w), M, len(n.inputs) > 1, n.attrs.get("act", "relu"),
+                                                  n.attrs.get("out_f32", False)))
     return out
 
 
-def _time_candidate(lib, pc, nhw, M, res, act, out_f32, cand, bufs, stream) -> float:
-    cfg, splitk, kw = cand
-    nb, h, w = nhw
-    x, r, o = bufs
-    wsb, ncnt = conv_ops.workspace_bytes(M, pc.cout, cfg, splitk)
-    ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=x.device)
-    cnt = torch.zeros(max(ncnt, 64), dtype=torch.int32, device=x.device)
-    prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0, act,
-                                     out_f32, cfg, splitk, ws.data_ptr(), cnt.data_ptr(), kw=kw)
-    rc = lib.hz_conv_launch(C.byref(prm), cfg, stream.cuda_stream)
-    if rc != 0:
-        return float("inf")
+def _capture(lib, prm, cfg, stream):
     prog = lib.hz_prog_create()
+    for _ in range(REPS):
+        N.check(lib.hz_prog_add_conv(prog, C.byref(prm), cfg, 0), "add_conv")
+    N.check(lib.hz_prog_capture(prog, stream.cuda_stream), "capture")
+    return prog
+
+
+def _time_candidate(lib, shape, cand, bufs, streams, concurrent: int) -> float:
+    """Median-of-3 us per launch; with ``concurrent`` > 1, that many independent copies run
+    on separate streams (throughput under request concurrency)."""
+    pc, (nb, h, w), M, res, act, out_f32 = shape
+    cfg, kw = cand
+    progs = []
     try:
-        for _ in range(REPS):
-            N.check(lib.hz_prog_add_conv(prog, C.byref(prm), cfg, 0), "add_conv")
-        N.check(lib.hz_prog_capture(prog, stream.cuda_stream), "capture")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(stream):
-            lib.hz_prog_replay(prog, stream.cuda_stream)
-            best = float("inf")
-            for _ in range(3):
-                e0.record(stream)
-                lib.hz_prog_replay(prog, stream.cuda_stream)
-                e1.record(stream)
-                e1.synchronize()
-                best = min(best, e0.elapsed_time(e1) * 1e3 / REPS)
+        for c in range(concurrent):
+            x, r, o = bufs[c]
+            prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0,
+                                             act, out_f32, cfg, kw)
+            if lib.hz_conv_launch(C.byref(prm), cfg, streams[c].cuda_stream) != 0:
+                return float("inf")
+            progs.append(_capture(lib, prm, cfg, streams[c]))
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for c in range(concurrent):
+                lib.hz_prog_replay(progs[c], streams[c].cuda_stream)
+            for c in range(concurrent):
+                streams[c].synchronize()
+            best = min(best, (time.perf_counter() - t0) * 1e6 / (REPS * concurrent))
         return best
     finally:
-        lib.hz_prog_destroy(prog)
-        del ws, cnt
+        for pg in progs:
+            lib.hz_prog_destroy(pg)
 
 
-def tune_graph(graph, params, device, verbose=False, max_candidates=None) -> tuple[dict, dict]:
+def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tuple[dict, dict]:
     lib = N.lib()
     dev = torch.device(device)
-    stream = torch.cuda.Stream(dev)
     table, report = {}, {}
     g = torch.Generator(device=dev).manual_seed(0)
     with torch.cuda.device(dev):
-        for key, (node, pc, nhw, M, res, act, out_f32) in conv_shapes(graph, params).items():
-            nb, h, w = nhw
-            x = (torch.randn(nb, h, w, pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
-            r = (torch.randn(M, pc.cout, device=dev, generator=g) * 0.5).to(torch.bfloat16)
-            o = torch.empty(M, pc.cout, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
-            cands = conv_ops.candidates(M, pc.cout, pc.K)
-            if max_candidates:
-                cands = cands[:max_candidates]
+        streams = [torch.cuda.Stream(dev) for _ in range(concurrent)]
+        for key, shape in conv_shapes(graph, params).items():
+            pc, (nb, h, w), M, res, act, out_f32 = shape
+            bufs = []
+            for _ in range(concurrent):
+                x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+                r = (torch.randn(M * pc.cout, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+                o = torch.empty(M * pc.cout, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+                bufs.append((x, r, o))
             times = []
-            for cand in cands:
-                t = _time_candidate(lib, pc, nhw, M, res, act, out_f32, cand, (x, r, o), stream)
-                times.append((t, cand))
+            for cand in conv_ops.candidates(M, pc.cout, pc.K):
+                times.append((_time_candidate(lib, shape, cand, bufs, streams, concurrent), cand))
             times.sort()
             best_t, best = times[0]
             heur = conv_ops.choose_config(M, pc.cout, pc.K)
@@ -110,8 +112,9 @@ def tune_graph(graph, params, device, verbose=False, max_candidates=None) -> tup
     return table, report
 
 
-def table_path(model: str, batch: int) -> Path:
-    return TUNING_DIR / f"{model}_bs{batch}.json"
+def table_path(model: str, batch: int, concurrent: int = 1) -> Path:
+    suffix = "" if concurrent <= 1 else f"_c{concurrent}"
+    return TUNING_DIR / f"{model}_bs{batch}{suffix}.json"
 
 
 def main():
@@ -119,6 +122,8 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, nargs="+", default=[1])
     ap.add_argument("--report", default=None)
+    ap.add_argument("--concurrent", type=int, nargs="+", default=[1],
+                    help="tune for throughput with this many concurrent request streams")
     args = ap.parse_args()
     from ..models import registry
     a = registry.get(args.model)
@@ -127,19 +132,21 @@ def main():
     # random weights of the real shapes are enough for timing
     params = {}
     for k, v in meta.items():
-        params[k] = conv_ops.PackedConv((torch.randn(v.w.shape, device=dev) * 0.02).to(torch.bfloat16),
+        params[k] = conv_ops.PackedConv((torch.randn(v.wf.shape, device=dev) * 0.02).to(torch.bfloat16),
                                         torch.zeros(v.bias.shape, device=dev), v.cin, v.cout, v.r, v.s, v.stride,
                                         v.pad)
     full_report = {}
     for b in args.batch:
-        t0 = time.time()
-        graph = a.build_graph(batch=b, **kw)
-        table, report = tune_graph(graph, params, dev, verbose=True)
-        TUNING_DIR.mkdir(exist_ok=True)
-        with open(table_path(args.model, b), "w") as f:
-            json.dump(table, f, indent=1, sort_keys=True)
-        full_report[f"bs{b}"] = report
-        print(f"tuned {args.model} bs{b}: {len(table)} shapes in {time.time() - t0:.1f}s -> {table_path(args.model, b)}")
+        for conc in args.concurrent:
+            t0 = time.time()
+            graph = a.build_graph(batch=b, **kw)
+            table, report = tune_graph(graph, params, dev, verbose=True, concurrent=conc)
+            TUNING_DIR.mkdir(exist_ok=True)
+            path = table_path(args.model, b, conc)
+            with open(path, "w") as f:
+                json.dump(table, f, indent=1, sort_keys=True)
+            full_report[f"bs{b}_c{conc}"] = report
+            print(f"tuned {args.model} bs{b} concurrent={conc}: {len(table)} shapes in {time.time() - t0:.1f}s -> {path}")
     if args.report:
         os.makedirs(os.path.dirname(args.report) or ".", exist_ok=True)
         with open(args.report, "w") as f:

@@ -78,8 +78,8 @@ class DropConnectLSTM(nn.Module):
     def forward(self, x, hc):
         w_hh = F.dropout(self.weight_hh_l0_raw, self.p, self.training) if self.training else self.module.weight_hh_l0
         m = self.module
-        out, (h, c) = torch._VF.lstm(x, hc, [m.weight_ih_l0, w_hh, m.bias_ih_l0, m.bias_hh_l0], True, 1, 0.0,
-                                     self.training, False, False)
+        out, h, c = torch._VF.lstm(x, hc, [m.weight_ih_l0, w_hh, m.bias_ih_l0, m.bias_hh_l0], True, 1, 0.0,
+                                   self.training, False, False)
         return out, (h, c)
 
 

@@ -183,8 +183,13 @@ def pack_resnet(sd: dict, device="cpu") -> dict[str, PackedConv]:
 
 
 def build_graph(arch: str, batch: int, num_classes: int = 1000, image: int = 224,
-                input_uint8: bool = False, side_stream: bool = True) -> Graph:
-    """Lower ResNet to a static kernel graph for a fixed batch size."""
+                input_uint8: bool = False, side_stream: bool = False) -> Graph:
+    """Lower ResNet to a static kernel graph for a fixed batch size.
+
+    ``side_stream`` puts the downsample conv on a forked stream. Off by default: measured on
+    MI355X (scripts/diag_runtime.py), a multi-stream hipGraph costs ~370 us of host
+    submission per replay vs ~30 us single-stream, which dwarfs the overlap it buys.
+    """
     block, layers = ARCHS[arch]
     g = Graph(f"{arch}_bs{batch}")
     if input_uint8:

@@ -1,9 +1,13 @@
 """Conv2d + folded BatchNorm + residual + activation on the native MFMA implicit-GEMM kernel.
 
 Weights are packed ONCE at load time (``pack_conv``): BN folded in fp32, OIHW -> O,R,S,C
-(K contiguous, NHWC-matching), input channels padded to a multiple of 8, K padded to a
-multiple of 32 and output-channel rows padded to 128 so that every tile config reads in
-bounds. A Linear layer is the 1x1 case on a 1x1 image (``pack_linear``).
+(K contiguous), input channels padded to a multiple of 8, K padded to a multiple of 32,
+output rows padded to a multiple of 64, then re-ordered fragment-major
+``[Cout_pad/16][K/32][64 lanes][8]`` so each wave's MFMA A-fragment load is one contiguous
+1 KiB (csrc/conv.hip). A Linear layer is the 1x1 case on a 1x1 image (``pack_linear``).
+
+Activation layout on device: channel-blocked ``[N][C/32][H][W][32]`` when C % 32 == 0,
+plain NHWC otherwise (the 8-channel stem input). ``to_blocked``/``from_blocked`` convert.
 """
 from __future__ import annotations
 
@@ -14,24 +18,15 @@ import torch
 
 from .. import _native as N
 
-# Mirrors the switch in csrc/conv.hip: (WC, WP, FC, FP); tile = WC*FC*16 ch x WP*FP*16 px
-CONV_CONFIGS = [
-    (2, 2, 2, 2), (4, 1, 1, 1), (4, 1, 2, 1), (1, 4, 1, 1), (2, 2, 1, 1), (2, 2, 4, 4),
-    (2, 2, 2, 4), (2, 2, 4, 2), (4, 1, 1, 2), (1, 4, 2, 1), (4, 1, 2, 2), (1, 4, 1, 2),
-]
-ROW_PAD = 128
+TILES = [(fc, fp) for fc in (1, 2, 4) for fp in (1, 2, 4)]  # cfg index -> (FC, FP)
+ROW_PAD = 64
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
 
 
-def tile_dims(cfg: int) -> tuple[int, int]:
-    wc, wp, fc, fp = CONV_CONFIGS[cfg]
-    return wc * fc * 16, wp * fp * 16
-
-
 @dataclass
 class PackedConv:
-    w: torch.Tensor          # bf16 [Cout_pad, ldw]
+    wf: torch.Tensor         # bf16 fragment-major [rows_pad/16, ksteps, 64, 8]
     bias: torch.Tensor       # fp32 [Cout]
     cin: int                 # padded input channels (multiple of 8)
     cout: int
@@ -45,11 +40,17 @@ class PackedConv:
         return self.r * self.s * self.cin
 
     @property
-    def ldw(self) -> int:
-        return self.w.shape[1]
+    def ksteps(self) -> int:
+        return self.wf.shape[1]
+
+    def dense(self) -> torch.Tensor:
+        """Row-major [cout, K] view of the packed weights (fp32; for oracles/tests)."""
+        g, ks = self.wf.shape[0], self.wf.shape[1]
+        w = self.wf.float().reshape(g, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(g * 16, ks * 32)
+        return w[: self.cout, : self.K]
 
     def to(self, device) -> "PackedConv":
-        return PackedConv(self.w.to(device), self.bias.to(device), self.cin, self.cout, self.r, self.s,
+        return PackedConv(self.wf.to(device), self.bias.to(device), self.cin, self.cout, self.r, self.s,
                           self.stride, self.pad)
 
 
@@ -64,6 +65,22 @@ def fold_bn(weight: torch.Tensor, bias: torch.Tensor | None, bn: dict | None, ep
     return w, b
 
 
+def fragment_major(w2d: torch.Tensor) -> torch.Tensor:
+    """[rows, K] (rows % 16 == 0, K % 32 == 0) -> [rows/16, K/32, 64, 8]; lane = kc*16 + row."""
+    rows, K = w2d.shape
+    return w2d.reshape(rows // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(rows // 16, K // 32, 64, 8)
+
+
+def pack_matrix(w2d: torch.Tensor, bias: torch.Tensor, cin: int, r: int = 1, s: int = 1, stride: int = 1,
+                pad: int = 0) -> PackedConv:
+    cout, K = w2d.shape
+    ksteps = int(math.ceil(K / 32))
+    rows = int(math.ceil(cout / ROW_PAD) * ROW_PAD)
+    wp = torch.zeros(rows, ksteps * 32, dtype=torch.bfloat16, device=w2d.device)
+    wp[:cout, :K] = w2d.to(torch.bfloat16)
+    return PackedConv(fragment_major(wp).contiguous(), bias.float().contiguous(), cin, cout, r, s, stride, pad)
+
+
 def pack_conv(weight, bias=None, bn=None, stride=1, pad=0, eps=1e-5, cin_pad: int | None = None) -> PackedConv:
     w, b = fold_bn(weight, bias, bn, eps)
     cout, cin, r, s = w.shape
@@ -71,151 +88,141 @@ def pack_conv(weight, bias=None, bn=None, stride=1, pad=0, eps=1e-5, cin_pad: in
     w = w.permute(0, 2, 3, 1)  # O,R,S,C
     if cin_p != cin:
         w = torch.nn.functional.pad(w, (0, cin_p - cin))
-    K = r * s * cin_p
-    ldw = int(math.ceil(K / 32) * 32)
-    rows = int(math.ceil(cout / ROW_PAD) * ROW_PAD)
-    wp = torch.zeros(rows, ldw, dtype=torch.bfloat16, device=w.device)
-    wp[:cout, :K] = w.reshape(cout, K).to(torch.bfloat16)
-    return PackedConv(wp, b.contiguous(), cin_p, cout, r, s, stride, pad)
+    return pack_matrix(w.reshape(cout, r * s * cin_p), b, cin_p, r, s, stride, pad)
 
 
 def pack_linear(weight, bias=None) -> PackedConv:
-    return pack_conv(weight[:, :, None, None], bias)
+    b = bias if bias is not None else torch.zeros(weight.shape[0], device=weight.device)
+    cin = weight.shape[1]
+    assert cin % 8 == 0
+    return pack_matrix(weight.detach().float(), b.detach().float(), cin)
 
 
-KW_TILES = [(fc, fp) for fc in (1, 2, 4) for fp in (1, 2, 4)]  # cfg = 100 + index
+# ----------------------------------------------------------------------------- layouts
+def is_blocked(c: int) -> bool:
+    return c % 32 == 0
 
 
-def kw_max_threads(nf: int) -> int:
+def to_blocked(x_nhwc: torch.Tensor) -> torch.Tensor:
+    """[N,H,W,C] -> [N, C/32, H, W, 32] (contiguous) when C % 32 == 0, else unchanged."""
+    n, h, w, c = x_nhwc.shape
+    if not is_blocked(c):
+        return x_nhwc.contiguous()
+    return x_nhwc.reshape(n, h, w, c // 32, 32).permute(0, 3, 1, 2, 4).contiguous()
+
+
+def from_blocked(t: torch.Tensor, shape) -> torch.Tensor:
+    """Inverse of :func:`to_blocked` for a logical NHWC ``shape``."""
+    n, h, w, c = shape
+    if not is_blocked(c):
+        return t.reshape(n, h, w, c)
+    return t.reshape(n, c // 32, h, w, 32).permute(0, 2, 3, 1, 4).reshape(n, h, w, c)
+
+
+# ----------------------------------------------------------------------------- configs
+def max_threads(nf: int) -> int:
     return 256 if nf >= 16 else 512 if nf >= 8 else 1024
 
 
-def kw_cfg(fc: int, fp: int) -> int:
-    return 100 + KW_TILES.index((fc, fp))
+def cfg_of(fc: int, fp: int) -> int:
+    return TILES.index((fc, fp))
 
 
 def tile_of(cfg: int) -> tuple[int, int]:
-    """(channels, pixels) per workgroup for any cfg."""
-    if cfg >= 100:
-        fc, fp = KW_TILES[cfg - 100]
-        return fc * 16, fp * 16
-    return tile_dims(cfg)
+    fc, fp = TILES[cfg]
+    return fc * 16, fp * 16
 
 
-def candidates(M: int, cout: int, K: int) -> list[tuple[int, int, int]]:
-    """All legal (cfg, splitk, kw) launch choices worth timing for one conv shape."""
+def legal(cfg: int, kw: int) -> bool:
+    fc, fp = TILES[cfg]
+    return 1 <= kw <= 16 and kw * fc * fp <= 64 and 64 * kw <= max_threads(fc * fp)
+
+
+def candidates(M: int, cout: int, K: int) -> list[tuple[int, int]]:
+    """All legal (cfg, kw) launch choices worth timing for one conv shape."""
     steps = max(1, math.ceil(K / 32))
     out = []
-    for (fc, fp) in KW_TILES:
+    for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue
         for kw in (1, 2, 4, 8, 16):
-            if kw * fc * fp > 64 or 64 * kw > kw_max_threads(fc * fp):
+            if not legal(cfg, kw) or (kw > 1 and steps / kw < 2):
                 continue
-            if kw > 1 and steps / kw < 2:
-                continue
-            out.append((kw_cfg(fc, fp), 1, kw))
-    for cfg in range(len(CONV_CONFIGS)):  # v1 (cross-workgroup split-K) kept as candidates
-        c, sk = _v1_choice(M, cout, K, cfg)
-        out.append((cfg, sk, 1))
+            out.append((cfg, kw))
     return out
 
 
-def _v1_choice(M, cout, K, cfg):
-    steps = max(1, math.ceil(K / 32))
-    bnc, bmp = tile_dims(cfg)
-    tiles = math.ceil(cout / bnc) * math.ceil(M / bmp)
-    want = max(1, math.ceil(NUM_CUS / tiles))
-    return cfg, max(1, min(want, steps // 4, 32))
-
-
 def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str | None = None):
-    """Pick (cfg, splitk, kw) for an implicit GEMM of M pixels x cout channels x K.
+    """Pick (cfg, kw) for an implicit GEMM of M pixels x cout channels x K.
 
     A measured table (``tuned``, produced on the GPU by ``hipzap.engine.tune``) wins. The
-    fallback heuristic uses the K-across-waves kernel: the smallest output tile that still
-    yields >= 1 workgroup per CU, then enough waves per workgroup that each wave streams
-    ~6 K-steps.
+    fallback heuristic: the largest output tile that still yields >= 1 workgroup per CU
+    with < 30 % padding waste (else 16x16 tiles), then enough waves per workgroup that each
+    wave streams ~6 K-steps.
     """
     if tuned is not None and key is not None and key in tuned:
         v = tuned[key]
-        return int(v[0]), int(v[1]), int(v[2]) if len(v) > 2 else 1
+        return int(v[0]), int(v[1])
     steps = max(1, math.ceil(K / 32))
     fc, fp = 1, 1
     full = []
-    for (a, b) in KW_TILES:
+    for (a, b) in TILES:
         tiles = math.ceil(cout / (16 * a)) * math.ceil(M / (16 * b))
         waste = tiles * 256 * a * b / max(1, M * cout)
         if tiles >= NUM_CUS and waste < 1.3:
             full.append((a * b, -waste, a, b))
     if full:
         _, _, fc, fp = max(full)
+    cfg = cfg_of(fc, fp)
     kw = 1
-    while kw * 2 <= 16 and steps / (kw * 2) >= 6 and kw * 2 * fc * fp <= 64 and 128 * kw <= kw_max_threads(fc * fp):
+    while steps / (kw * 2) >= 6 and legal(cfg, kw * 2):
         kw *= 2
-    return kw_cfg(fc, fp), 1, kw
+    return cfg, kw
 
 
-def split_k_slice(K: int, splitk: int) -> int:
-    steps = math.ceil(K / 32)
-    return int(math.ceil(steps / splitk) * 32)
-
-
-def workspace_bytes(M: int, cout: int, cfg: int, splitk: int) -> tuple[int, int]:
-    """(slab bytes, counter ints) for a split-K launch."""
-    if splitk <= 1 or cfg >= 100:
-        return 0, 0
-    wc, wp, fc, fp = CONV_CONFIGS[cfg]
-    bnc, bmp = tile_dims(cfg)
-    tiles = math.ceil(cout / bnc) * math.ceil(M / bmp)
-    return tiles * splitk * fc * fp * 256 * 16, tiles
+def conv_key(M: int, pc: PackedConv) -> str:
+    return f"{M}x{pc.cout}x{pc.K}x{pc.r}{pc.s}s{pc.stride}"
 
 
 def make_params(x_ptr, pc: PackedConv, n, h, w, out_ptr, res_ptr=0, act="relu", out_f32=False,
-                cfg=0, splitk=1, ws_ptr=0, cnt_ptr=0, ldo=None, ldr=None, kw=1) -> tuple[N.ConvParams, int, int]:
+                cfg=0, kw=1, out_rowmajor=False, ldo=None) -> tuple[N.ConvParams, int, int]:
     p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
-    M = n * p_out * q_out
     prm = N.ConvParams()
-    prm.x, prm.w, prm.bias, prm.res, prm.out = x_ptr, pc.w.data_ptr(), pc.bias.data_ptr(), res_ptr, out_ptr
-    prm.ws, prm.cnt = ws_ptr, cnt_ptr
+    prm.x, prm.w, prm.bias, prm.res, prm.out = x_ptr, pc.wf.data_ptr(), pc.bias.data_ptr(), res_ptr, out_ptr
     prm.N, prm.H, prm.W, prm.C = n, h, w, pc.cin
     prm.Cout, prm.R, prm.S, prm.stride, prm.pad, prm.P, prm.Q = pc.cout, pc.r, pc.s, pc.stride, pc.pad, p_out, q_out
-    prm.M, prm.K, prm.ldw = M, pc.K, pc.ldw
-    prm.ldo = ldo if ldo is not None else pc.cout
-    prm.ldr = ldr if ldr is not None else pc.cout
+    prm.M, prm.K, prm.ksteps = n * p_out * q_out, pc.K, pc.ksteps
     prm.act, prm.out_f32 = ACT[act], int(out_f32)
-    prm.splitk, prm.kslice = splitk, split_k_slice(pc.K, splitk)
-    prm.tiles_n = 0
-    prm.kw = kw
+    rowmajor = out_rowmajor or not is_blocked(pc.cout)
+    prm.out_rowmajor, prm.ldo = int(rowmajor), ldo if ldo is not None else pc.cout
+    prm.tiles_n, prm.kw = 0, kw
     return prm, p_out, q_out
 
 
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None = None, act: str = "relu",
-                out_f32: bool = False, cfg: int | None = None, splitk: int | None = None,
-                kw: int | None = None) -> torch.Tensor:
-    """Eager launch: x NHWC bf16 [N,H,W,Cin_pad] -> NHWC [N,P,Q,Cout] (bf16 or fp32)."""
-    assert x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[-1] == pc.cin
+                out_f32: bool = False, cfg: int | None = None, kw: int | None = None) -> torch.Tensor:
+    """Eager launch on logical NHWC tensors (converted to/from the device layout)."""
+    assert x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] == pc.cin
     n, h, w, _ = x.shape
     p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
     M = n * p_out * q_out
     if cfg is None:
-        cfg, splitk, kw = choose_config(M, pc.cout, pc.K)
-    splitk = 1 if splitk is None else splitk
-    kw = 1 if kw is None else kw
-    out = torch.empty(n, p_out, q_out, pc.cout, device=x.device,
-                      dtype=torch.float32 if out_f32 else torch.bfloat16)
-    ws_b, n_cnt = workspace_bytes(M, pc.cout, cfg, splitk)
-    ws = torch.empty(max(ws_b, 16), dtype=torch.uint8, device=x.device)
-    cnt = torch.zeros(max(n_cnt, 1), dtype=torch.int32, device=x.device)
+        cfg, kw = choose_config(M, pc.cout, pc.K)
+    kw = kw or 1
+    xb = to_blocked(x)
+    oshape = (n, p_out, q_out, pc.cout)
+    out = torch.empty(M * pc.cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    rb = None
     if residual is not None:
-        assert residual.dtype == torch.bfloat16 and residual.is_contiguous()
-        assert residual.numel() == M * pc.cout
-    prm, _, _ = make_params(x.data_ptr(), pc, n, h, w, out.data_ptr(), N.ptr(residual), act, out_f32,
-                            cfg, splitk, ws.data_ptr(), cnt.data_ptr(), kw=kw)
+        assert residual.dtype == torch.bfloat16 and tuple(residual.shape) == oshape
+        rb = to_blocked(residual) if is_blocked(pc.cout) else residual.contiguous()
+    prm, _, _ = make_params(xb.data_ptr(), pc, n, h, w, out.data_ptr(), N.ptr(rb), act, out_f32, cfg, kw)
     N.check(N.lib().hz_conv_launch(prm, cfg, N.stream_ptr()), "hz_conv_launch")
-    return out
+    if prm.out_rowmajor:
+        return out.reshape(oshape)
+    return from_blocked(out, oshape)
 
 
 def conv2d_reference(x_nchw: torch.Tensor, weight, bias=None, bn=None, stride=1, pad=0, residual=None,

@@ -19,10 +19,14 @@ def maxpool_nhwc(x: torch.Tensor, k=3, stride=2, pad=1) -> torch.Tensor:
     return out
 
 
-def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
+def avgpool_nhwc(x: torch.Tensor, blocked: bool = False) -> torch.Tensor:
+    """x: logical [N,H,W,C]; ``blocked`` stores it channel-blocked on device first."""
+    from .conv import to_blocked
     n, h, w, c = x.shape
+    src = to_blocked(x) if blocked else x.contiguous()
     out = torch.empty(n, c, device=x.device, dtype=torch.bfloat16)
-    N.check(N.lib().hz_avgpool_launch(x.data_ptr(), out.data_ptr(), n, h * w, c, N.stream_ptr()), "avgpool")
+    N.check(N.lib().hz_avgpool_launch(src.data_ptr(), out.data_ptr(), n, h * w, c, int(blocked), N.stream_ptr()),
+            "avgpool")
     return out
 
 

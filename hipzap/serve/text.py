@@ -68,7 +68,7 @@ def gumbel_topk(logits: torch.Tensor, k: int, generator: torch.Generator | None 
     lg = logits.float().reshape(-1)
     u = torch.rand(lg.shape, generator=generator, device=lg.device).clamp_(1e-20, 1.0)
     g = -torch.log(-torch.log(u))
-    return torch.topk(lg + g, k).indices
+    return torch.topk(lg + g, min(k, lg.numel())).indices
 
 
 def select_token(draws: Sequence[int], exclude: set[int]) -> int:

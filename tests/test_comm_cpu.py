@@ -1,0 +1,58 @@
+"""Weight-blob broadcast (C1) and DP helpers over gloo with world_size 2 (CPU)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hipzap.parallel.comm import broadcast_params, flat_layout, pack_blob, unpack_blob
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipzap.models import registry
+    a = registry.get("resnet18")
+    meta, _ = a.meta_params()
+    params = None
+    if rank == 0:
+        torch.manual_seed(0)
+        params = a.pack(a.make_model().state_dict(), "cpu")[0]
+    got = broadcast_params(params, meta, "cpu")
+    digest = sum(float(p.wf.float().sum() + p.bias.sum()) for p in got.values())
+    q.put((rank, digest, got["fc"].cout))
+    dist.destroy_process_group()
+
+
+def test_blob_roundtrip():
+    from hipzap.models import registry
+    a = registry.get("resnet18")
+    params = a.pack(a.make_model().state_dict(), "cpu")[0]
+    blob = pack_blob(params, "cpu")
+    _, total = flat_layout(params)
+    assert blob.numel() == total
+    back = unpack_blob(blob, params)
+    for k in params:
+        assert torch.equal(back[k].wf, params[k].wf) and torch.equal(back[k].bias, params[k].bias)
+
+
+def test_broadcast_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2] == 1000

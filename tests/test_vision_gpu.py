@@ -14,7 +14,7 @@ def _rand_bn(c, g):
             "running_mean": 0.1 * torch.randn(c, generator=g), "running_var": 0.5 + torch.rand(c, generator=g)}
 
 
-def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None, splitk=None, seed=0, kw=None):
+def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None, kw=None, seed=0):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, cin, h, h, generator=g)
     w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
@@ -24,8 +24,7 @@ def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None,
     res = torch.randn(n, cout, p, p, generator=g) if residual else None
     # bf16-rounded inputs for the oracle so only accumulation/epilogue error remains
     xb = x.to(torch.bfloat16).float()
-    pc_cpu = pc
-    wref = pc_cpu.w[:cout, :pc.K].float().reshape(cout, k, k, pc.cin)[..., :cin].permute(0, 3, 1, 2)
+    wref = pc.dense().reshape(cout, k, k, pc.cin)[..., :cin].permute(0, 3, 1, 2)
     ref = torch.nn.functional.conv2d(xb, wref, pc.bias, stride=stride, padding=pad)
     if res is not None:
         ref = ref + res.to(torch.bfloat16).float()
@@ -33,7 +32,7 @@ def _case(n, cin, h, cout, k, stride, pad, act="relu", residual=False, cfg=None,
         ref = torch.relu(ref)
     x_nhwc = torch.nn.functional.pad(xb.permute(0, 2, 3, 1), (0, pc.cin - cin)).to(torch.bfloat16)
     r_nhwc = None if res is None else res.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
-    out = C.conv2d_nhwc(x_nhwc.contiguous().to(DEV), pc.to(DEV), r_nhwc, act=act, cfg=cfg, splitk=splitk, kw=kw)
+    out = C.conv2d_nhwc(x_nhwc.contiguous().to(DEV), pc.to(DEV), r_nhwc, act=act, cfg=cfg, kw=kw)
     torch.cuda.synchronize()
     got = out.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs().max().item()
@@ -50,7 +49,8 @@ SHAPES = [
     (1, 512, 7, 512, 3, 1, 1),
     (1, 1024, 14, 2048, 1, 2, 0),
     (2, 3, 32, 64, 7, 2, 3),     # stem-like, generic K path (cin padded to 8)
-    (1, 48, 9, 40, 3, 1, 1),     # odd: C%32 != 0, Cout not multiple of 16
+    (2, 64, 9, 96, 3, 1, 1),     # batch 2, odd spatial
+    (1, 64, 5, 40, 1, 1, 0),     # Cout not a multiple of 32 -> row-major output
 ]
 
 
@@ -59,34 +59,31 @@ def test_conv_heuristic(shape):
     assert _case(*shape) < 2e-2
 
 
-@pytest.mark.parametrize("cfg", range(len(C.CONV_CONFIGS)))
-@pytest.mark.parametrize("splitk", [1, 3])
-def test_conv_every_config(cfg, splitk):
-    assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, splitk=splitk) < 2e-2
-
-
-@pytest.mark.parametrize("tile", C.KW_TILES)
+@pytest.mark.parametrize("cfg", range(len(C.TILES)))
 @pytest.mark.parametrize("kw", [1, 2, 4, 16])
-def test_conv_kw_every_tile(tile, kw):
-    fc, fp = tile
-    if kw * fc * fp > 64 or 64 * kw > C.kw_max_threads(fc * fp):
+def test_conv_every_tile(cfg, kw):
+    if not C.legal(cfg, kw):
         pytest.skip("illegal combo")
-    cfg = C.kw_cfg(fc, fp)
-    assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, splitk=1, kw=kw) < 2e-2
-    assert _case(2, 3, 20, 64, 7, 2, 3, cfg=cfg, splitk=1, kw=kw) < 2e-2  # generic-K path
-    assert _case(1, 64, 9, 128, 1, 1, 0, residual=True, cfg=cfg, splitk=1, kw=kw) < 2e-2  # 1x1 path
+    assert _case(1, 64, 14, 96, 3, 1, 1, residual=True, cfg=cfg, kw=kw) < 2e-2
+    assert _case(2, 3, 20, 64, 7, 2, 3, cfg=cfg, kw=kw) < 2e-2  # generic-K path
+    assert _case(1, 64, 9, 128, 1, 1, 0, residual=True, cfg=cfg, kw=kw) < 2e-2  # 1x1 path
+    assert _case(2, 128, 8, 64, 1, 2, 0, cfg=cfg, kw=kw) < 2e-2  # strided 1x1 (downsample)
 
 
 def test_conv_candidates_all_launch():
-    for cand in C.candidates(49, 512, 4608):
-        cfg, sk, kw = cand
-        assert _case(1, 512, 7, 512, 3, 1, 1, residual=True, cfg=cfg, splitk=sk, kw=kw) < 2e-2, cand
+    for cfg, kw in C.candidates(49, 512, 4608):
+        assert _case(1, 512, 7, 512, 3, 1, 1, residual=True, cfg=cfg, kw=kw) < 2e-2, (cfg, kw)
 
 
-def test_conv_splitk_deep():
-    # layer4-like: M=49, K=4608, heavy split; run twice to check ticket self-reset
-    for _ in range(2):
-        assert _case(1, 512, 7, 512, 3, 1, 1, residual=True, cfg=1, splitk=16) < 2e-2
+def test_linear_rowmajor_fp32():
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(1000, 2048, generator=g) * 0.02
+    b = torch.randn(1000, generator=g)
+    pc = C.pack_linear(w, b).to(DEV)
+    x = torch.randn(3, 2048, generator=g).to(torch.bfloat16)
+    out = C.conv2d_nhwc(x.reshape(3, 1, 1, 2048).to(DEV), pc, act="none", out_f32=True).reshape(3, 1000).cpu()
+    ref = x.float() @ w.to(torch.bfloat16).float().T + b
+    assert (out - ref).abs().max() / ref.abs().max() < 1e-2
 
 
 def test_maxpool_avgpool_preprocess():
@@ -95,8 +92,9 @@ def test_maxpool_avgpool_preprocess():
     y = V.maxpool_nhwc(x.to(DEV)).cpu().float()
     ref = torch.nn.functional.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     assert torch.equal(y, ref)
-    a = V.avgpool_nhwc(x.to(DEV)).cpu().float()
-    assert (a - x.float().mean(dim=(1, 2))).abs().max() < 1e-2
+    for blocked in (False, True):
+        a = V.avgpool_nhwc(x.to(DEV), blocked=blocked).cpu().float()
+        assert (a - x.float().mean(dim=(1, 2))).abs().max() < 1e-2
     img = torch.randn(2, 3, 20, 24, generator=g)
     p = V.preprocess(img.to(DEV)).cpu().float()
     assert (p - V.preprocess_reference(img)).abs().max() < 1e-2
