@@ -45,6 +45,40 @@ int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, i
 int hz_cast_f32_bf16(const float* x, unsigned short* y, long n, hipStream_t st);
 int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipStream_t st);
 
+// ---- AWD-LSTM decode (csrc/lstm.hip) ----
+typedef struct HzLstmParams {
+  const unsigned short* w;    // [4H][ldk] bf16, gate-interleaved rows (4j+q = gate q of unit j; i,f,g,o)
+  const float* bias;          // [4H] fp32 (b_ih + b_hh, same interleave)
+  const unsigned short* emb;  // layer 0: embedding [V][lde] bf16 (input gathered by token); else NULL
+  int lde;
+  const int* tok_seq;         // token sequence; step t consumes tok_seq[t]
+  const float* x_state;       // layers > 0: previous layer's h_state [2][In]
+  float* h_state;             // [2][H] fp32, ping-pong by step parity
+  float* c_state;             // [2][H] fp32
+  const int* step;            // device step counter t
+  int In, H, ldk;             // ldk = padded In + H (multiple of 512)
+} HzLstmParams;
+typedef struct HzDecoderParams {
+  const unsigned short* w;    // [V][ldk] bf16 (tied embedding, K padded)
+  const float* bias;          // [V] or NULL
+  const float* h_state;       // last layer [2][H]
+  const int* step;
+  float* logits;              // [V]
+  int V, H, ldk;
+} HzDecoderParams;
+typedef struct HzSamplerParams {
+  const float* logits;        // [V]
+  int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
+  int* step;                  // increments
+  int* draws;                 // optional [steps][10] record of the draws
+  unsigned long long seed;
+  int V, n_forced, n_exclude;
+  int exclude[8];
+} HzSamplerParams;
+int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
+int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);
+int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);
+
 // ---- runtime: static op programs, graph capture / replay ----
 typedef void* HzProgram;
 HzProgram hz_prog_create(void);
@@ -57,6 +91,9 @@ int hz_prog_add_avgpool(HzProgram p, const unsigned short* x, unsigned short* ou
 int hz_prog_add_preprocess(HzProgram p, const void* src, unsigned short* dst, int N, int Cin, int H, int W,
                            int Cpad, int mode, const float* mean, const float* inv_std, int slot);
 int hz_prog_add_memcpy(HzProgram p, void* dst, const void* src, size_t bytes, int slot);  // any direction (UVA)
+int hz_prog_add_lstm(HzProgram p, const HzLstmParams* lp, int slot);
+int hz_prog_add_decoder(HzProgram p, const HzDecoderParams* dp, int slot);
+int hz_prog_add_sampler(HzProgram p, const HzSamplerParams* sp, int slot);
 int hz_prog_add_fork(HzProgram p, int slot);   // side stream `slot` waits for main
 int hz_prog_add_join(HzProgram p, int slot);   // main waits for side stream `slot`
 int hz_prog_run(HzProgram p, hipStream_t st);  // eager launch of every op

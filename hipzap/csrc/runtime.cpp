@@ -119,6 +119,18 @@ int hz_prog_add_memcpy(HzProgram h, void* dst, const void* src, size_t bytes, in
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
                 [=](hipStream_t s) { return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s); });
 }
+int hz_prog_add_lstm(HzProgram h, const HzLstmParams* lp, int slot) {
+  HzLstmParams c = *lp;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_lstm_cell_launch(&c, s); });
+}
+int hz_prog_add_decoder(HzProgram h, const HzDecoderParams* dp, int slot) {
+  HzDecoderParams c = *dp;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_decoder_launch(&c, s); });
+}
+int hz_prog_add_sampler(HzProgram h, const HzSamplerParams* sp, int slot) {
+  HzSamplerParams c = *sp;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_sampler_launch(&c, s); });
+}
 int hz_prog_add_fork(HzProgram h, int slot) {
   if (slot < 1) return -4;
   return add_op(static_cast<Program*>(h), slot, Op::FORK, nullptr);
