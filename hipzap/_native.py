@@ -36,6 +36,23 @@ class PoolParams(C.Structure):
                 ("k", c_int), ("stride", c_int), ("pad", c_int)]
 
 
+class LstmParams(C.Structure):
+    _fields_ = [("w", c_void_p), ("bias", c_void_p), ("emb", c_void_p), ("lde", c_int), ("tok_seq", c_void_p),
+                ("x_state", c_void_p), ("h_state", c_void_p), ("c_state", c_void_p), ("step", c_void_p),
+                ("In", c_int), ("H", c_int), ("ldk", c_int)]
+
+
+class DecoderParams(C.Structure):
+    _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h_state", c_void_p), ("step", c_void_p),
+                ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int)]
+
+
+class SamplerParams(C.Structure):
+    _fields_ = [("logits", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
+                ("seed", c_void_p), ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int),
+                ("exclude", c_int * 8)]
+
+
 def _sig(lib, name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -71,6 +88,13 @@ def _load():
          C.POINTER(c_double))
     _sig(lib, "hz_diag_launch", c_int, c_int, c_int, c_int, P, P, c_long, P)
     _sig(lib, "hz_prog_add_diag", c_int, P, c_int, c_int, c_int, P, P, c_long, c_int)
+    _sig(lib, "hz_prog_replay_n", c_int, P, P, c_int)
+    _sig(lib, "hz_lstm_cell_launch", c_int, C.POINTER(LstmParams), P)
+    _sig(lib, "hz_decoder_launch", c_int, C.POINTER(DecoderParams), P)
+    _sig(lib, "hz_sampler_launch", c_int, C.POINTER(SamplerParams), P)
+    _sig(lib, "hz_prog_add_lstm", c_int, P, C.POINTER(LstmParams), c_int)
+    _sig(lib, "hz_prog_add_decoder", c_int, P, C.POINTER(DecoderParams), c_int)
+    _sig(lib, "hz_prog_add_sampler", c_int, P, C.POINTER(SamplerParams), c_int)
     for extra in _EXTRA_SIGS:
         extra(lib)
     return lib

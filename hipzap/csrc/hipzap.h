@@ -71,8 +71,9 @@ typedef struct HzSamplerParams {
   int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
   int* step;                  // increments
   int* draws;                 // optional [steps][10] record of the draws
-  unsigned long long seed;
-  int V, n_forced, n_exclude;
+  const unsigned long long* seed;  // device: per-request RNG seed
+  const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
+  int V, n_exclude;
   int exclude[8];
 } HzSamplerParams;
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
@@ -100,6 +101,7 @@ int hz_prog_run(HzProgram p, hipStream_t st);  // eager launch of every op
 int hz_prog_capture(HzProgram p, hipStream_t st);
 int hz_prog_replay(HzProgram p, hipStream_t st);
 int hz_prog_is_captured(HzProgram p);
+int hz_prog_replay_n(HzProgram p, hipStream_t st, int n);  // n back-to-back replays, no sync
 // replay `n` programs round-robin on `n` streams `iters` times from C++ and synchronize;
 // returns elapsed microseconds (host wall, includes the final sync) or negative on error.
 double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters);

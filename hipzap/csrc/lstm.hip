@@ -149,7 +149,8 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
   __shared__ int s_draw[TOPK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int t = *p.step;
-  const bool forced = (t + 1) < p.n_forced;
+  const bool forced = (t + 1) < *p.n_forced;
+  const unsigned long long seed = *p.seed;
   if (!forced) {
     // local top-K of perturbed logits (sorted descending, insertion)
     float v[TOPK];
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
       id[q] = -1;
     }
     for (int j = tid; j < p.V; j += blockDim.x) {
-      const float key = p.logits[j] + gumbel(p.seed, t, j);
+      const float key = p.logits[j] + gumbel(seed, t, j);
       if (key > v[TOPK - 1]) {
         float cv = key;
         int ci = j;

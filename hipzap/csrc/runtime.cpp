@@ -219,3 +219,11 @@ int hz_prog_bench2(HzProgram* progs, hipStream_t* streams, int n, int iters, int
 }
 
 }  // extern "C"
+
+extern "C" int hz_prog_replay_n(HzProgram h, hipStream_t st, int n) {
+  for (int i = 0; i < n; ++i) {
+    const int rc = hz_prog_replay(h, st);
+    if (rc) return rc;
+  }
+  return 0;
+}

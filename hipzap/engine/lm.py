@@ -1,0 +1,176 @@
+"""AWD-LSTM text generation engine on MI355X (GET /inference on the GPU backend).
+
+The reference rebuilds the model and runs 201 CPU forwards per request with autograd on
+(main.py:84-103; 8.9 s measured). Here:
+  * cold start packs the state_dict once: per layer ``[W_ih | W_hh]`` concatenated,
+    gate rows interleaved (unit j -> rows 4j..4j+3), ``b_ih + b_hh`` folded, K padded to a
+    multiple of 512, bf16; the tied embedding/decoder matrix is stored once (bf16, padded);
+  * one decode step = ``L`` fused LSTM-cell kernels + decoder GEMV + device sampler
+    (csrc/lstm.hip), captured ONCE as a hipGraph; the recurrent state, the step counter, the
+    prompt length, the RNG seed and the token sequence all live on the device, so a request
+    is ``P + n - 1`` back-to-back graph replays and a single device->host copy at the end.
+  * the SURVEY §5.4 checkpoint rule applies: effective W_hh = ``module.weight_hh_l0`` when
+    present, else ``weight_hh_l0_raw``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import threading
+
+import torch
+
+from .. import _native as N
+from ..serve.text import EXCLUDE_TOKENS, NUM_DRAWS, Detokenizer
+
+
+def _pad_to(n: int, m: int) -> int:
+    return int(math.ceil(n / m) * m)
+
+
+def pack_awd_lstm(sd: dict, device) -> dict:
+    """state_dict (reference key layout) -> device-ready packed tensors."""
+    dev = torch.device(device)
+    layers = []
+    l = 0
+    while f"0.rnns.{l}.module.weight_ih_l0" in sd:
+        pre = f"0.rnns.{l}"
+        w_ih = sd[f"{pre}.module.weight_ih_l0"].float()
+        w_hh = sd.get(f"{pre}.module.weight_hh_l0", sd.get(f"{pre}.weight_hh_l0_raw")).float()
+        b = sd[f"{pre}.module.bias_ih_l0"].float() + sd[f"{pre}.module.bias_hh_l0"].float()
+        four_h, n_in = w_ih.shape
+        H = four_h // 4
+        w = torch.cat([w_ih, w_hh], dim=1)  # [4H, In+H]
+        # interleave gates: new row 4j+q = old row q*H + j
+        w = w.reshape(4, H, n_in + H).permute(1, 0, 2).reshape(4 * H, n_in + H)
+        b = b.reshape(4, H).t().reshape(4 * H)
+        ldk = _pad_to(n_in + H, 512)
+        wp = torch.zeros(4 * H, ldk, dtype=torch.bfloat16, device=dev)
+        wp[:, : n_in + H] = w.to(dev, torch.bfloat16)
+        layers.append({"w": wp, "bias": b.to(dev).contiguous(), "In": n_in, "H": H, "ldk": ldk})
+        l += 1
+    if not layers:
+        raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
+    emb = sd["0.encoder.weight"].float()
+    V, E = emb.shape
+    lde = _pad_to(max(E, layers[-1]["H"]), 512)
+    embp = torch.zeros(V, lde, dtype=torch.bfloat16, device=dev)
+    embp[:, :E] = emb.to(dev, torch.bfloat16)
+    dec_w = sd.get("1.decoder.weight")
+    if dec_w is not None and not torch.equal(dec_w.float(), emb):
+        decp = torch.zeros(V, lde, dtype=torch.bfloat16, device=dev)
+        decp[:, : dec_w.shape[1]] = dec_w.to(dev, torch.bfloat16)
+    else:
+        decp = embp  # tied (awd_lstm.py:40)
+    dec_b = sd.get("1.decoder.bias")
+    dec_b = dec_b.float().to(dev) if dec_b is not None else None
+    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": dec_b, "V": V, "E": E, "lde": lde}
+
+
+class LMEngine:
+    def __init__(self, packed: dict, device="cuda:0", max_steps: int = 1024, exclude_ids=(), record_draws=False,
+                 capture: bool = True):
+        self.p = packed
+        self.device = torch.device(device)
+        self.max_steps = max_steps
+        lib = N.lib()
+        dev = self.device
+        with torch.cuda.device(dev):
+            self.stream = torch.cuda.Stream(dev)
+            L = packed["layers"]
+            self.h = [torch.zeros(2, ly["H"], device=dev) for ly in L]
+            self.c = [torch.zeros(2, ly["H"], device=dev) for ly in L]
+            self.tok_seq = torch.zeros(max_steps + 1, dtype=torch.int32, device=dev)
+            self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.n_forced = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.logits = torch.zeros(packed["V"], device=dev)
+            self.draws = torch.full((max_steps, NUM_DRAWS), -1, dtype=torch.int32, device=dev) if record_draws else None
+            self.prog = lib.hz_prog_create()
+            for i, ly in enumerate(L):
+                prm = N.LstmParams()
+                prm.w, prm.bias = ly["w"].data_ptr(), ly["bias"].data_ptr()
+                prm.emb = packed["emb"].data_ptr() if i == 0 else 0
+                prm.lde = packed["lde"]
+                prm.tok_seq = self.tok_seq.data_ptr()
+                prm.x_state = 0 if i == 0 else self.h[i - 1].data_ptr()
+                prm.h_state, prm.c_state = self.h[i].data_ptr(), self.c[i].data_ptr()
+                prm.step = self.step.data_ptr()
+                prm.In, prm.H, prm.ldk = ly["In"], ly["H"], ly["ldk"]
+                if i == 0 and prm.In > packed["lde"]:
+                    raise ValueError("embedding width mismatch")
+                N.check(lib.hz_prog_add_lstm(self.prog, C.byref(prm), 0), "add_lstm")
+            d = N.DecoderParams()
+            d.w = packed["dec"].data_ptr()
+            d.bias = N.ptr(packed["dec_bias"])
+            d.h_state, d.step, d.logits = self.h[-1].data_ptr(), self.step.data_ptr(), self.logits.data_ptr()
+            d.V, d.H, d.ldk = packed["V"], L[-1]["H"], packed["lde"]
+            N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
+            s = N.SamplerParams()
+            s.logits, s.tok_seq, s.step = self.logits.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
+            s.draws = N.ptr(self.draws)
+            s.seed, s.n_forced = self.seed.data_ptr(), self.n_forced.data_ptr()
+            s.V = packed["V"]
+            ex = [int(e) for e in exclude_ids][:8]
+            s.n_exclude = len(ex)
+            for i, e in enumerate(ex):
+                s.exclude[i] = e
+            N.check(lib.hz_prog_add_sampler(self.prog, C.byref(s), 0), "add_sampler")
+            if capture:
+                N.check(lib.hz_prog_capture(self.prog, self.stream.cuda_stream), "capture")
+            torch.cuda.synchronize(dev)
+        self._lock = threading.Lock()
+
+    @classmethod
+    def from_state_dict(cls, sd: dict, device="cuda:0", **kw) -> "LMEngine":
+        return cls(pack_awd_lstm(sd, device), device, **kw)
+
+    @classmethod
+    def for_vocab(cls, sd: dict, stoi: dict, device="cuda:0", **kw) -> "LMEngine":
+        ex = [stoi[w] for w in EXCLUDE_TOKENS if w in stoi]
+        return cls(pack_awd_lstm(sd, device), device, exclude_ids=ex, **kw)
+
+    def run_tokens(self, prompt_ids: list, n_words: int, seed: int = 0) -> list:
+        """Feed ``prompt_ids``, sample ``n_words`` tokens on device; returns sampled ids."""
+        P = len(prompt_ids)
+        if P < 1:
+            raise ValueError("need at least one prompt token")
+        total = P + n_words - 1
+        if P + n_words > self.max_steps:
+            raise ValueError(f"prompt + words ({P + n_words}) exceeds max_steps {self.max_steps}")
+        with self._lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+            for t in self.h + self.c:
+                t.zero_()
+            self.step.zero_()
+            self.n_forced.fill_(P)
+            self.seed.fill_(int(seed) & ((1 << 62) - 1))
+            self.tok_seq[:P].copy_(torch.tensor(prompt_ids, dtype=torch.int32), non_blocking=False)
+            if total > 0:
+                N.check(N.lib().hz_prog_replay_n(self.prog, self.stream.cuda_stream, total), "replay_n")
+            out = self.tok_seq[P: P + n_words].to("cpu")
+        return out.tolist()
+
+    def generate(self, prompt_words, n_words, itos, stoi, seed=None) -> str:
+        ids = [stoi.get(w, 0) for w in prompt_words]
+        if seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+        toks = self.run_tokens(ids, n_words, seed)
+        det = Detokenizer()
+        for w in prompt_words:
+            det.add_prompt(w)
+        for t in toks:
+            det.add(itos[t])
+        return det.text
+
+    def step_logits(self, prompt_ids: list) -> torch.Tensor:
+        """Teacher-forced logits after feeding ``prompt_ids`` (for numerics tests)."""
+        self.run_tokens(prompt_ids, 1, 0)
+        return self.logits.detach().cpu().clone()
+
+    def __del__(self):
+        try:
+            if getattr(self, "prog", None):
+                N.lib().hz_prog_destroy(self.prog)
+                self.prog = None
+        except Exception:
+            pass

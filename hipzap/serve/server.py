@@ -79,7 +79,7 @@ class LMBackend:
         self.backend = backend
         if backend == "gpu":
             from ..engine.lm import LMEngine
-            self.engine = LMEngine.from_state_dict(sd, device)
+            self.engine = LMEngine.for_vocab(sd, self.stoi, device)
             self.model = None
         else:
             self.model = reference_lm(len(itos))

@@ -1,0 +1,90 @@
+"""AWD-LSTM device decode vs the eager model; sampler distribution and selection rule."""
+import math
+
+import pytest
+import torch
+
+from hipzap.engine.lm import LMEngine
+from hipzap.models.awd_lstm import get_language_model, reference_lm
+from hipzap.serve.text import select_token
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def model():
+    torch.manual_seed(0)
+    m = reference_lm(3000).eval()  # the reference's dims (emb 1000, hidden 1150, 3 layers), small vocab
+    return m
+
+
+def _eager_logits(m, ids):
+    m.reset()
+    with torch.no_grad():
+        for t in ids:
+            res, *_ = m(torch.tensor([[t]]))
+    return res[-1]
+
+
+def test_teacher_forced_logits_match_eager(model):
+    eng = LMEngine.from_state_dict(model.state_dict(), DEV)
+    for ids in ([5], [5, 17, 200, 3, 2999]):
+        got = eng.step_logits(ids)
+        ref = _eager_logits(model, ids)
+        rel = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert rel < 3e-2, rel
+        assert torch.topk(got, 5).indices.tolist()[:1] == torch.topk(ref, 5).indices.tolist()[:1]
+
+
+def test_untied_small_model():
+    torch.manual_seed(1)
+    m = get_language_model(vocab_sz=700, emb_sz=96, n_hid=160, n_layers=2, pad_token=1, tie_weights=False).eval()
+    eng = LMEngine.from_state_dict(m.state_dict(), DEV)
+    ids = [3, 9, 650]
+    got, ref = eng.step_logits(ids), _eager_logits(m, ids)
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 3e-2
+
+
+def test_sampler_distribution_first_draw(model):
+    eng = LMEngine.from_state_dict(model.state_dict(), DEV, record_draws=True)
+    ids = [11, 12]
+    logits = eng.step_logits(ids)
+    p = torch.softmax(logits.double(), 0)
+    top = torch.topk(p, 6).indices.tolist()
+    counts = {t: 0 for t in top}
+    other = 0
+    n = 3000
+    for s in range(n):
+        eng.run_tokens(ids, 1, seed=1000 + s)
+        d0 = int(eng.draws[len(ids) - 1, 0].item())
+        if d0 in counts:
+            counts[d0] += 1
+        else:
+            other += 1
+    exp = [n * p[t].item() for t in top] + [n * (1 - sum(p[t].item() for t in top))]
+    obs = [counts[t] for t in top] + [other]
+    chi2 = sum((o - e) ** 2 / e for o, e in zip(obs, exp) if e > 5)
+    assert chi2 < 25.0, (obs, exp)  # 6 dof
+
+
+def test_draws_distinct_and_selection_rule(model):
+    excl = [int(torch.topk(_eager_logits(model, [11, 12]), 1).indices)]  # exclude the likeliest token
+    eng = LMEngine(LMEngine.from_state_dict(model.state_dict(), DEV).p, DEV, exclude_ids=excl, record_draws=True)
+    ids = [11, 12]
+    for s in range(50):
+        toks = eng.run_tokens(ids, 4, seed=s)
+        for step in range(4):
+            row = eng.draws[len(ids) - 1 + step].tolist()
+            assert len(set(row)) == 10
+            assert toks[step] == select_token(row, set(excl))
+
+
+def test_generate_text_reference_config(model):
+    itos = [f"w{i}" for i in range(3000)]
+    itos[0], itos[1], itos[2] = "xxunk", "xxpad", "."
+    stoi = {w: i for i, w in enumerate(itos)}
+    eng = LMEngine.for_vocab(model.state_dict(), stoi, DEV)
+    a = eng.generate([""], 200, itos, stoi, seed=7)
+    b = eng.generate([""], 200, itos, stoi, seed=7)
+    assert a == b and len(a.split()) >= 150
