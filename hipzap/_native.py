@@ -26,6 +26,7 @@ class ConvParams(C.Structure):
         ("Cout", c_int), ("R", c_int), ("S", c_int), ("stride", c_int), ("pad", c_int), ("P", c_int), ("Q", c_int),
         ("M", c_int), ("K", c_int), ("ksteps", c_int),
         ("act", c_int), ("out_f32", c_int), ("out_rowmajor", c_int), ("ldo", c_int),
+        ("x_rowmajor", c_int), ("ldx", c_int),
         ("tiles_n", c_int), ("kw", c_int),
     ]
 

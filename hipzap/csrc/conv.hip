@@ -35,7 +35,7 @@ struct Depth {
 // keep the register ring out of scratch: 1024 threads cap a wave at 128 VGPRs
 constexpr int conv_max_threads(int nf) { return nf >= 16 ? 256 : nf >= 8 ? 512 : 1024; }
 
-template <int FC, int FP, bool FAST, bool IS1X1>
+template <int FC, int FP, bool FAST, bool IS1X1, bool XROW>
 __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const HzConvParams p) {
   constexpr int DEPTH = Depth<FC, FP>::value;
   constexpr int NF = FC * FP;
@@ -97,7 +97,14 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const H
 #pragma unroll
     for (int i = 0; i < FC; ++i)
       a[i] = *reinterpret_cast<const bf16x8*>(Wf + ((long)i * steps + s_idx) * 512);
-    if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
+    if constexpr (XROW) {  // plain GEMM: row-major activations [M][ldx] (transformers)
+#pragma unroll
+      for (int j = 0; j < FP; ++j) {
+        const int kk = k + lk;
+        if (pval[j] && kk < p.K) b[j] = *reinterpret_cast<const bf16x8*>(X + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
+        else b[j] = bf16x8{};
+      }
+    } else if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
       const int rs = k / C;
       const int cb = (k - rs * C) >> 5;
       if constexpr (IS1X1) {
@@ -228,9 +235,10 @@ int launch(const HzConvParams& p, hipStream_t st) {
   const bool fast = (p.C % 32) == 0;
   dim3 grid(q.tiles_n * tiles_m), block(64 * kw);
   const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
-  if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true>), grid, block, lds, st, q);
-  else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false>), grid, block, lds, st, q);
-  else hipLaunchKernelGGL((conv_kernel<FC, FP, false, false>), grid, block, lds, st, q);
+  if (p.x_rowmajor) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
+  else if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false>), grid, block, lds, st, q);
+  else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false>), grid, block, lds, st, q);
+  else hipLaunchKernelGGL((conv_kernel<FC, FP, false, false, false>), grid, block, lds, st, q);
   return (int)hipGetLastError();
 }
 
@@ -240,7 +248,9 @@ int launch(const HzConvParams& p, hipStream_t st) {
 // Mirrored by hipzap/ops/conv.py (TILES).
 extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
-  if (p.Cout % 4 != 0 || p.C % 8 != 0 || (p.C % 32 != 0 && p.C > 16)) return -1;
+  if (p.Cout % 4 != 0 || p.C % 8 != 0) return -1;
+  if (!p.x_rowmajor && p.C % 32 != 0 && p.C > 16) return -1;
+  if (p.x_rowmajor && (p.ldx % 8 != 0 || p.R != 1 || p.S != 1)) return -1;
   if (!p.out_rowmajor && p.Cout % 32 != 0) return -1;
   if (p.ksteps * 32 < p.K) return -1;
   switch (cfg) {

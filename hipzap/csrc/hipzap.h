@@ -20,6 +20,7 @@ typedef struct HzConvParams {
   int Cout, R, S, stride, pad, P, Q;
   int M, K, ksteps;          // M = N*P*Q; ksteps = ceil(K/32)
   int act, out_f32, out_rowmajor, ldo;
+  int x_rowmajor, ldx;        // GEMM mode: activations row-major [M][ldx] (M = N*H*W, 1x1 only)
   int tiles_n;               // filled by the launcher
   int kw;                    // waves per workgroup splitting K
 } HzConvParams;
@@ -44,6 +45,8 @@ int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, i
 // elementwise helpers
 int hz_cast_f32_bf16(const float* x, unsigned short* y, long n, hipStream_t st);
 int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipStream_t st);
+
+typedef void* HzProgram;
 
 // ---- AWD-LSTM decode (csrc/lstm.hip) ----
 typedef struct HzLstmParams {
@@ -80,8 +83,54 @@ int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);
 int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);
 
+// ---- transformer kernels (csrc/transformer.hip) ----
+typedef struct HzLayerNormParams {
+  const unsigned short* x;    // [rows][ldx] bf16
+  const unsigned short* res;  // optional residual [rows][ldr] (added before the norm)
+  unsigned short* out;        // [rows][ldo] bf16
+  const float* gamma;
+  const float* beta;
+  int rows, D, ldx, ldr, ldo;
+  float eps;
+} HzLayerNormParams;
+typedef struct HzEmbedParams {
+  const int* ids;             // [rows] token ids (rows = B*L)
+  const int* types;           // [rows] token-type ids or NULL
+  const unsigned short* word; // [V][D]
+  const unsigned short* pos;  // [Lmax][D]
+  const unsigned short* type; // [2][D]
+  const float* gamma;
+  const float* beta;
+  unsigned short* out;        // [rows][D]
+  int rows, L, D;
+  float eps;
+} HzEmbedParams;
+typedef struct HzAttentionParams {
+  const unsigned short* qkv;  // [B*L][ldqkv]: Q at col h*64, K at +k_off, V at +v_off
+  const float* mask;          // additive per-key mask [B][L] or NULL
+  unsigned short* out;        // [B*L][ldo], head h at col h*64
+  int B, L, heads, head_dim, ldqkv, k_off, v_off, ldo;
+  float scale;
+} HzAttentionParams;
+typedef struct HzVitTokensParams {
+  const unsigned short* patches;  // [B*np][D]
+  const unsigned short* cls;      // [D]
+  const unsigned short* pos;      // [np+1][D]
+  unsigned short* out;            // [B][np+1][D]
+  int B, np, D;
+} HzVitTokensParams;
+int hz_layernorm_launch(const HzLayerNormParams* p, hipStream_t st);
+int hz_embed_ln_launch(const HzEmbedParams* p, hipStream_t st);
+int hz_attention_launch(const HzAttentionParams* p, hipStream_t st);
+int hz_vit_tokens_launch(const HzVitTokensParams* p, hipStream_t st);
+
+// generic program op: kind selects the launcher, params are copied into the program
+enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
+       HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10 };
+int hz_launch_kernel(int kind, const void* params, hipStream_t st);
+int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
+
 // ---- runtime: static op programs, graph capture / replay ----
-typedef void* HzProgram;
 HzProgram hz_prog_create(void);
 void hz_prog_destroy(HzProgram p);
 int hz_prog_num_ops(HzProgram p);

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -226,4 +227,24 @@ extern "C" int hz_prog_replay_n(HzProgram h, hipStream_t st, int n) {
     if (rc) return rc;
   }
   return 0;
+}
+
+extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
+  switch (kind) {
+    case HZ_K_LAYERNORM: return hz_layernorm_launch(static_cast<const HzLayerNormParams*>(prm), st);
+    case HZ_K_EMBED: return hz_embed_ln_launch(static_cast<const HzEmbedParams*>(prm), st);
+    case HZ_K_ATTENTION: return hz_attention_launch(static_cast<const HzAttentionParams*>(prm), st);
+    case HZ_K_VIT_TOKENS: return hz_vit_tokens_launch(static_cast<const HzVitTokensParams*>(prm), st);
+    case HZ_K_LSTM: return hz_lstm_cell_launch(static_cast<const HzLstmParams*>(prm), st);
+    case HZ_K_DECODER: return hz_decoder_launch(static_cast<const HzDecoderParams*>(prm), st);
+    case HZ_K_SAMPLER: return hz_sampler_launch(static_cast<const HzSamplerParams*>(prm), st);
+    case HZ_K_MAXPOOL: return hz_maxpool_launch(static_cast<const HzPoolParams*>(prm), st);
+    default: return -100;
+  }
+}
+
+extern "C" int hz_prog_add_kernel(HzProgram h, int kind, const void* params, size_t size, int slot) {
+  auto buf = std::make_shared<std::vector<char>>(static_cast<const char*>(params), static_cast<const char*>(params) + size);
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [buf, kind](hipStream_t s) { return hz_launch_kernel(kind, buf->data(), s); });
 }

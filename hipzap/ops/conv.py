@@ -185,7 +185,7 @@ def conv_key(M: int, pc: PackedConv) -> str:
 
 
 def make_params(x_ptr, pc: PackedConv, n, h, w, out_ptr, res_ptr=0, act="relu", out_f32=False,
-                cfg=0, kw=1, out_rowmajor=False, ldo=None) -> tuple[N.ConvParams, int, int]:
+                cfg=0, kw=1, out_rowmajor=False, ldo=None, x_rowmajor=False, ldx=None) -> tuple[N.ConvParams, int, int]:
     p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
     prm = N.ConvParams()
@@ -196,8 +196,26 @@ def make_params(x_ptr, pc: PackedConv, n, h, w, out_ptr, res_ptr=0, act="relu", 
     prm.act, prm.out_f32 = ACT[act], int(out_f32)
     rowmajor = out_rowmajor or not is_blocked(pc.cout)
     prm.out_rowmajor, prm.ldo = int(rowmajor), ldo if ldo is not None else pc.cout
+    prm.x_rowmajor, prm.ldx = int(x_rowmajor), ldx if ldx is not None else pc.cin
     prm.tiles_n, prm.kw = 0, kw
     return prm, p_out, q_out
+
+
+def linear(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None = None, act: str = "none",
+           out_f32: bool = False, cfg: int | None = None, kw: int | None = None, out: torch.Tensor | None = None,
+           ldx: int | None = None, rows: int | None = None) -> torch.Tensor:
+    """Eager GEMM: y[M,N] = act(x[M,K] @ W^T + b (+ residual)); x row-major (stride ``ldx``)."""
+    M = rows if rows is not None else x.shape[0]
+    if cfg is None:
+        cfg, kw = choose_config(M, pc.cout, pc.K)
+    kw = kw or 1
+    if out is None:
+        out = torch.empty(M, pc.cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    prm, _, _ = make_params(x.data_ptr(), pc, M, 1, 1, out.data_ptr(), N.ptr(residual), act, out_f32, cfg, kw,
+                            out_rowmajor=True, ldo=out.stride(0), x_rowmajor=True,
+                            ldx=ldx if ldx is not None else x.stride(0))
+    N.check(N.lib().hz_conv_launch(prm, cfg, N.stream_ptr()), "hz_conv_launch(linear)")
+    return out
 
 
 def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None = None, act: str = "relu",
