@@ -90,6 +90,8 @@ def _load():
     _sig(lib, "hz_diag_launch", c_int, c_int, c_int, c_int, P, P, c_long, P)
     _sig(lib, "hz_prog_add_diag", c_int, P, c_int, c_int, c_int, P, P, c_long, c_int)
     _sig(lib, "hz_prog_replay_n", c_int, P, P, c_int)
+    _sig(lib, "hz_launch_kernel", c_int, c_int, P, P)
+    _sig(lib, "hz_prog_add_kernel", c_int, P, c_int, P, C.c_size_t, c_int)
     _sig(lib, "hz_lstm_cell_launch", c_int, C.POINTER(LstmParams), P)
     _sig(lib, "hz_decoder_launch", c_int, C.POINTER(DecoderParams), P)
     _sig(lib, "hz_sampler_launch", c_int, C.POINTER(SamplerParams), P)

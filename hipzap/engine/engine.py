@@ -96,21 +96,31 @@ class Engine:
             self._rr = (self._rr + 1) % len(self.contexts)
         return i
 
-    def infer(self, x: torch.Tensor) -> torch.Tensor:
-        """Run one request (shape = the graph input shape); returns output on the host."""
+    def infer(self, x) -> torch.Tensor:
+        """Run one request; ``x`` is the graph input tensor, or a list of tensors for
+        multi-input graphs (BERT: ids, token types, additive mask). Returns host output."""
+        xs = list(x) if isinstance(x, (list, tuple)) else [x]
         i = self._pick()
         ctx, s = self.contexts[i], self.streams[i]
         with self._locks[i], torch.cuda.device(self.device), torch.cuda.stream(s):
             if self.host_io:  # transfers are inside the captured graph
-                ctx.host_input.copy_(x.reshape(ctx.host_input.shape))
+                for hb, xi in zip(ctx.host_inputs, xs):
+                    hb.copy_(xi.reshape(hb.shape))
                 ctx.replay(s)
                 s.synchronize()
                 out = ctx.host_output.clone()
             else:
-                ctx.input.copy_(x.reshape(ctx.input.shape), non_blocking=True)
+                for d, xi in zip(ctx.inputs, xs):
+                    d.copy_(xi.reshape(d.shape), non_blocking=True)
                 ctx.replay(s)
                 out = ctx.output.to("cpu", non_blocking=False)
-        return self.adapter.postprocess_output(out)
+        return self._post(out)
+
+    def _post(self, out):
+        try:
+            return self.adapter.postprocess_output(out, getattr(self.graph, "meta", None))
+        except TypeError:
+            return self.adapter.postprocess_output(out)
 
     def infer_device(self, x: torch.Tensor, ctx_index: int = 0) -> torch.Tensor:
         """Device-resident variant (no host copies); output aliases the static buffer."""

@@ -13,6 +13,7 @@ import torch
 
 from .. import _native as N
 from ..ops import conv as conv_ops
+from ..ops import transformer as tx
 from .graph import Graph, plan_memory
 
 
@@ -46,27 +47,36 @@ class ExecContext:
         self.configs: list = []
         conv_plans = []
         for n in g.nodes:
-            if n.kind != "conv":
+            if n.kind not in ("conv", "gemm"):
                 conv_plans.append(None)
                 continue
             pc = params[n.attrs["w"]]
-            nb, h, w, _ = g.shape(n.inputs[0])
-            p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
-            q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
-            key = conv_ops.conv_key(nb * p_out * q_out, pc)
+            if n.kind == "conv":
+                nb, h, w, _ = g.shape(n.inputs[0])
+                p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
+                q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
+                M = nb * p_out * q_out
+                key = conv_ops.conv_key(M, pc)
+            else:
+                M = n.attrs["rows"]
+                key = "r" + conv_ops.conv_key(M, pc)
             if n.attrs.get("cfg") is not None:
                 cfg, kw = n.attrs["cfg"], n.attrs.get("kw", 1)
             else:
-                cfg, kw = conv_ops.choose_config(nb * p_out * q_out, pc.cout, pc.K, tuned, key)
+                cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
             conv_plans.append((cfg, kw, key))
         # host_io: the request's PCIe transfers are part of the program (and of the graph):
-        # pinned host input -> device input ... device output -> pinned host output.
+        # pinned host inputs -> device inputs ... device output -> pinned host output.
         self.host_io = host_io
         if host_io:
-            self.host_input = torch.zeros(self.input.shape, dtype=self.input.dtype).pin_memory()
+            self.host_inputs = [torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype).pin_memory()
+                                for t in g.inputs]
+            self.host_input = self.host_inputs[0]
             self.host_output = torch.zeros(self.output.shape, dtype=self.output.dtype).pin_memory()
-            N.check(lib.hz_prog_add_memcpy(self.prog, self.input.data_ptr(), self.host_input.data_ptr(),
-                                           self.input.numel() * self.input.element_size(), 0), "h2d")
+            for t, hbuf in zip(g.inputs, self.host_inputs):
+                d = self.ext[t]
+                N.check(lib.hz_prog_add_memcpy(self.prog, d.data_ptr(), hbuf.data_ptr(), d.numel() * d.element_size(),
+                                               0), "h2d")
         for i, n in enumerate(g.nodes):
             self._add_node(lib, n, conv_plans[i])
         if host_io:
@@ -114,6 +124,47 @@ class ExecContext:
                 self._keep += [mean, std]
             N.check(lib.hz_prog_add_preprocess(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, cin, h, w,
                                                cpad, mode, N.ptr(mean), N.ptr(std), n.slot), "add_preprocess")
+        elif n.kind == "gemm":
+            pc = self.params[n.attrs["w"]]
+            cfg, kw, key = plan
+            M = n.attrs["rows"]
+            res = n.inputs[1] if len(n.inputs) > 1 else None
+            out_spec = g.tensors[n.outputs[0]]
+            ldx = n.attrs.get("ldx") or g.shape(n.inputs[0])[-1]
+            prm, _, _ = conv_ops.make_params(addr(n.inputs[0]), pc, M, 1, 1, addr(n.outputs[0]), addr(res),
+                                             n.attrs.get("act", "none"), n.attrs.get("out_f32", False), cfg, kw,
+                                             out_rowmajor=True, ldo=out_spec.shape[-1], x_rowmajor=True, ldx=ldx)
+            self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
+            N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_gemm")
+        elif n.kind == "layernorm":
+            npar = self.params[n.attrs["p"]]
+            res = n.inputs[1] if len(n.inputs) > 1 else None
+            D = g.shape(n.outputs[0])[-1]
+            prm = tx.LayerNormParams(addr(n.inputs[0]), addr(res), addr(n.outputs[0]), npar.gamma.data_ptr(),
+                                     npar.beta.data_ptr(), n.attrs["rows"], D, n.attrs.get("ldx") or D, D, D,
+                                     npar.eps)
+            tx.prog_add(self.prog, tx.K_LAYERNORM, prm, n.slot)
+        elif n.kind == "attention":
+            a = n.attrs
+            qkv = n.inputs[0]
+            mask = n.inputs[1] if len(n.inputs) > 1 else None
+            D = a["heads"] * 64
+            prm = tx.AttentionParams(addr(qkv), addr(mask), addr(n.outputs[0]), a["B"], a["L"], a["heads"], 64,
+                                     g.shape(qkv)[-1], D, 2 * D, D, 0.125)
+            tx.prog_add(self.prog, tx.K_ATTENTION, prm, n.slot)
+        elif n.kind == "embed_ln":
+            tab, ln = self.params[n.attrs["emb"]], self.params[n.attrs["ln"]]
+            rows, D = g.shape(n.outputs[0])
+            prm = tx.EmbedParams(addr(n.inputs[0]), addr(n.inputs[1]), tab.word.data_ptr(), tab.pos.data_ptr(),
+                                 tab.type.data_ptr(), ln.gamma.data_ptr(), ln.beta.data_ptr(), addr(n.outputs[0]),
+                                 rows, n.attrs["L"], D, ln.eps)
+            tx.prog_add(self.prog, tx.K_EMBED, prm, n.slot)
+        elif n.kind == "vit_tokens":
+            a = n.attrs
+            D = g.shape(n.outputs[0])[-1]
+            prm = tx.VitTokensParams(addr(n.inputs[0]), self.params[a["cls"]].data_ptr(),
+                                     self.params[a["pos"]].data_ptr(), addr(n.outputs[0]), a["B"], a["np"], D)
+            tx.prog_add(self.prog, tx.K_VIT_TOKENS, prm, n.slot)
         elif n.kind == "fork":
             N.check(lib.hz_prog_add_fork(self.prog, n.slot), "fork")
         elif n.kind == "join":
@@ -125,6 +176,10 @@ class ExecContext:
     @property
     def input(self) -> torch.Tensor:
         return self.ext[self.graph.inputs[0]]
+
+    @property
+    def inputs(self) -> list:
+        return [self.ext[t] for t in self.graph.inputs]
 
     @property
     def output(self) -> torch.Tensor:

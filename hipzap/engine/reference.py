@@ -57,7 +57,8 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
         elif k == "conv":
             pc = params[n.attrs["w"]]
             res = vals[n.inputs[1]] if len(n.inputs) > 1 else None
-            store(n.outputs[0], _conv_ref(vals[n.inputs[0]], pc, res, n.attrs.get("act", "relu")))
+            y = _conv_ref(vals[n.inputs[0]], pc, res, n.attrs.get("act", "relu"))
+            store(n.outputs[0], y.reshape(g.shape(n.outputs[0])))
         elif k == "maxpool":
             a = n.attrs
             x = vals[n.inputs[0]].permute(0, 3, 1, 2)
@@ -66,6 +67,43 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
         elif k == "avgpool":
             x = vals[n.inputs[0]]
             store(n.outputs[0], x.float().mean(dim=(1, 2), keepdim=True))
+        elif k == "gemm":
+            pc = params[n.attrs["w"]]
+            x = vals[n.inputs[0]].float().reshape(-1)
+            rows, ldx = n.attrs["rows"], n.attrs.get("ldx") or g.shape(n.inputs[0])[-1]
+            xm = torch.stack([x[r * ldx: r * ldx + pc.K] for r in range(rows)])
+            w = pc.dense() if not hasattr(pc, "dequant") else pc.dequant()
+            y = xm @ w.t() + pc.bias.float()
+            if len(n.inputs) > 1:
+                y = y + vals[n.inputs[1]].float().reshape(rows, -1)
+            act = n.attrs.get("act", "none")
+            y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
+            store(n.outputs[0], y)
+        elif k == "layernorm":
+            npar = params[n.attrs["p"]]
+            rows = n.attrs["rows"]
+            D = g.shape(n.outputs[0])[-1]
+            ldx = n.attrs.get("ldx") or D
+            x = vals[n.inputs[0]].float().reshape(-1)
+            xm = torch.stack([x[r * ldx: r * ldx + D] for r in range(rows)])
+            if len(n.inputs) > 1:
+                xm = xm + vals[n.inputs[1]].float().reshape(rows, D)
+            store(n.outputs[0], F.layer_norm(xm, (D,), npar.gamma.float(), npar.beta.float(), npar.eps))
+        elif k == "attention":
+            a = n.attrs
+            mask = vals[n.inputs[1]] if len(n.inputs) > 1 else None
+            from ..ops.transformer import attention_ref
+            store(n.outputs[0], attention_ref(vals[n.inputs[0]], a["B"], a["L"], a["heads"], mask))
+        elif k == "embed_ln":
+            from ..ops.transformer import embed_ref
+            tab, ln = params[n.attrs["emb"]], params[n.attrs["ln"]]
+            store(n.outputs[0], embed_ref(vals[n.inputs[0]], vals[n.inputs[1]], tab, ln, n.attrs["L"]))
+        elif k == "vit_tokens":
+            a = n.attrs
+            D = g.shape(n.outputs[0])[-1]
+            pt = vals[n.inputs[0]].float().reshape(a["B"], a["np"], D)
+            cls = params[a["cls"]].float().reshape(1, 1, D).expand(a["B"], 1, D)
+            store(n.outputs[0], torch.cat([cls, pt], 1) + params[a["pos"]].float().reshape(1, a["np"] + 1, D))
         else:
             raise NotImplementedError(k)
     return vals

@@ -1,0 +1,60 @@
+"""Shared helpers for lowering transformer encoders (BERT, ViT) to hipzap graphs."""
+from __future__ import annotations
+
+import torch
+
+from ..engine.graph import Graph
+from ..ops.conv import pack_matrix
+from ..ops.transformer import NormParams
+
+
+def pack_linear_padded(weight: torch.Tensor, bias: torch.Tensor | None, out_multiple: int = 4):
+    """Pack a Linear for the GEMM kernel; output rows padded to ``out_multiple`` (the epilogue
+    stores 4 channels per lane) — logical width kept by the caller."""
+    w = weight.detach().float()
+    b = bias.detach().float() if bias is not None else torch.zeros(w.shape[0], device=w.device)
+    n = w.shape[0]
+    npad = (n + out_multiple - 1) // out_multiple * out_multiple
+    if npad != n:
+        w = torch.cat([w, w.new_zeros(npad - n, w.shape[1])])
+        b = torch.cat([b, b.new_zeros(npad - n)])
+    return pack_matrix(w, b, w.shape[1])
+
+
+def pack_qkv(q_w, q_b, k_w, k_b, v_w, v_b):
+    return pack_linear_padded(torch.cat([q_w, k_w, v_w]), torch.cat([q_b, k_b, v_b]))
+
+
+def norm(sd, prefix, eps):
+    return NormParams(sd[f"{prefix}.weight"].float().contiguous(), sd[f"{prefix}.bias"].float().contiguous(), eps)
+
+
+class TxBuilder:
+    """Adds transformer nodes to a Graph (row-major [rows, cols] bf16 activations)."""
+
+    def __init__(self, g: Graph):
+        self.g = g
+
+    def gemm(self, x, w: str, cols: int, act="none", res=None, rows=None, ldx=None, out_f32=False, ext=False,
+             name=None):
+        g = self.g
+        r = rows if rows is not None else g.shape(x)[0]
+        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
+        ins = [x] if res is None else [x, res]
+        g.add("gemm", ins, [out], w=w, act=act, rows=r, ldx=ldx, out_f32=out_f32, name=name or w)
+        return out
+
+    def layernorm(self, x, p: str, res=None, rows=None, ldx=None, name=None):
+        g = self.g
+        r = rows if rows is not None else g.shape(x)[0]
+        out = g.tensor((r, g.shape(x)[1]), torch.bfloat16, name or p)
+        ins = [x] if res is None else [x, res]
+        g.add("layernorm", ins, [out], p=p, rows=r, ldx=ldx)
+        return out
+
+    def attention(self, qkv, B, L, heads, mask=None):
+        g = self.g
+        out = g.tensor((B * L, heads * 64), torch.bfloat16, "ctx")
+        ins = [qkv] if mask is None else [qkv, mask]
+        g.add("attention", ins, [out], B=B, L=L, heads=heads)
+        return out

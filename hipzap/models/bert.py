@@ -1,0 +1,101 @@
+"""BERT-base sequence classification (HF ``BertForSequenceClassification`` checkpoint layout).
+
+North-star config 4 (BASELINE.json): BERT-base seq-cls bs=16 on one MI355X through the
+Linear/LayerNorm/Softmax HIP path. Not in the reference.
+
+* Checkpoint schema + fp32 oracle: ``transformers.BertForSequenceClassification`` (installed,
+  random init from ``BertConfig`` — no network), keys ``bert.embeddings.*``,
+  ``bert.encoder.layer.{i}.attention.self.{query,key,value}``, ``...attention.output.dense``,
+  ``...intermediate.dense``, ``...output.dense``, ``bert.pooler.dense``, ``classifier``.
+* Lowering per encoder layer (post-LN, 7 kernels): QKV GEMM (Q|K|V packed as one 2304-row
+  matrix, bias fused) -> fused attention (softmax(QK^T/8 + mask)V) -> O-proj GEMM with the
+  residual add fused in the epilogue -> LayerNorm -> FFN1 GEMM + GELU(erf) -> FFN2 GEMM +
+  residual -> LayerNorm. Embeddings gather-sum + LN is one kernel; pooler = GEMM over the
+  CLS rows (row stride L*768) + tanh; classifier GEMM writes fp32 logits.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..engine.graph import Graph
+from ..ops.transformer import EmbedTables
+from ._tx import TxBuilder, norm, pack_linear_padded, pack_qkv
+
+
+def make_model(num_labels: int = 2, **cfg):
+    from transformers import BertConfig, BertForSequenceClassification
+    m = BertForSequenceClassification(BertConfig(num_labels=num_labels, **cfg))
+    return m.eval()
+
+
+def config_from_sd(sd: dict) -> dict:
+    layers = 0
+    while f"bert.encoder.layer.{layers}.attention.self.query.weight" in sd:
+        layers += 1
+    hidden = sd["bert.embeddings.word_embeddings.weight"].shape[1]
+    return {"layers": layers, "hidden": hidden, "heads": hidden // 64,
+            "ffn": sd["bert.encoder.layer.0.intermediate.dense.weight"].shape[0],
+            "num_labels": sd["classifier.weight"].shape[0],
+            "max_pos": sd["bert.embeddings.position_embeddings.weight"].shape[0]}
+
+
+def pack_bert(sd: dict, device="cpu", eps: float = 1e-12) -> tuple[dict, dict]:
+    sd = {k: v.to(device) for k, v in sd.items()}
+    cfg = config_from_sd(sd)
+    P = {
+        "emb": EmbedTables(sd["bert.embeddings.word_embeddings.weight"].to(torch.bfloat16).contiguous(),
+                           sd["bert.embeddings.position_embeddings.weight"].to(torch.bfloat16).contiguous(),
+                           sd["bert.embeddings.token_type_embeddings.weight"].to(torch.bfloat16).contiguous()),
+        "emb_ln": norm(sd, "bert.embeddings.LayerNorm", eps),
+    }
+    for i in range(cfg["layers"]):
+        pre = f"bert.encoder.layer.{i}"
+        a = f"{pre}.attention.self"
+        P[f"l{i}.qkv"] = pack_qkv(sd[f"{a}.query.weight"], sd[f"{a}.query.bias"], sd[f"{a}.key.weight"],
+                                  sd[f"{a}.key.bias"], sd[f"{a}.value.weight"], sd[f"{a}.value.bias"])
+        P[f"l{i}.o"] = pack_linear_padded(sd[f"{pre}.attention.output.dense.weight"],
+                                          sd[f"{pre}.attention.output.dense.bias"])
+        P[f"l{i}.ln1"] = norm(sd, f"{pre}.attention.output.LayerNorm", eps)
+        P[f"l{i}.ffn1"] = pack_linear_padded(sd[f"{pre}.intermediate.dense.weight"], sd[f"{pre}.intermediate.dense.bias"])
+        P[f"l{i}.ffn2"] = pack_linear_padded(sd[f"{pre}.output.dense.weight"], sd[f"{pre}.output.dense.bias"])
+        P[f"l{i}.ln2"] = norm(sd, f"{pre}.output.LayerNorm", eps)
+    P["pooler"] = pack_linear_padded(sd["bert.pooler.dense.weight"], sd["bert.pooler.dense.bias"])
+    P["cls"] = pack_linear_padded(sd["classifier.weight"], sd["classifier.bias"])
+    return P, cfg
+
+
+def build_graph(batch: int, seq_len: int = 128, layers: int = 12, hidden: int = 768, heads: int = 12,
+                ffn: int = 3072, num_labels: int = 2, **_) -> Graph:
+    B, L, D = batch, seq_len, hidden
+    T = B * L
+    g = Graph(f"bert_bs{B}_L{L}")
+    ids = g.tensor((T,), torch.int32, "input_ids", external=True)
+    types = g.tensor((T,), torch.int32, "token_type_ids", external=True)
+    mask = g.tensor((T,), torch.float32, "mask_add", external=True)
+    g.inputs += [ids, types, mask]
+    tb = TxBuilder(g)
+    x = g.tensor((T, D), torch.bfloat16, "emb")
+    g.add("embed_ln", [ids, types], [x], emb="emb", ln="emb_ln", L=L)
+    for i in range(layers):
+        qkv = tb.gemm(x, f"l{i}.qkv", 3 * D)
+        ctx = tb.attention(qkv, B, L, heads, mask)
+        y = tb.gemm(ctx, f"l{i}.o", D, res=x)
+        x1 = tb.layernorm(y, f"l{i}.ln1")
+        h = tb.gemm(x1, f"l{i}.ffn1", ffn, act="gelu")
+        y2 = tb.gemm(h, f"l{i}.ffn2", D, res=x1)
+        x = tb.layernorm(y2, f"l{i}.ln2")
+    pooled = tb.gemm(x, "pooler", D, act="tanh", rows=B, ldx=L * D)
+    npad = (num_labels + 3) // 4 * 4
+    logits = tb.gemm(pooled, "cls", npad, out_f32=True, ext=True)
+    g.outputs.append(logits)
+    g.meta = {"num_labels": num_labels}
+    return g
+
+
+def encode_inputs(input_ids: torch.Tensor, token_type_ids=None, attention_mask=None):
+    """HF-style request tensors -> the graph's three int32/fp32 inputs."""
+    ids = input_ids.to(torch.int32).reshape(-1)
+    tt = (token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)).to(torch.int32).reshape(-1)
+    am = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
+    madd = (1.0 - am.float()).reshape(-1) * -1e9
+    return [ids, tt, madd]

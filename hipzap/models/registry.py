@@ -66,3 +66,82 @@ class ResNet50(VisionAdapter):
 @register("resnet18")
 class ResNet18(VisionAdapter):
     arch = "resnet18"
+
+
+class TextClassifierAdapter:
+    """BERT-base sequence classification (north-star config 4)."""
+    seq_len = 128
+
+    def make_model(self, num_labels=2):
+        from .bert import make_model
+        return make_model(num_labels)
+
+    def pack(self, sd: dict, device):
+        from .bert import pack_bert
+        params, cfg = pack_bert(sd, device)
+        cfg["seq_len"] = self.seq_len
+        return params, cfg
+
+    def meta_params(self, num_labels=2):
+        from .bert import pack_bert
+        with torch.device("meta"):
+            m = self.make_model(num_labels)
+        params, cfg = pack_bert(m.state_dict(), "meta")
+        cfg["seq_len"] = self.seq_len
+        return params, cfg
+
+    def build_graph(self, batch=1, **kw):
+        from .bert import build_graph
+        return build_graph(batch, **kw)
+
+    def example_input(self, batch=1, generator=None, seq_len=None):
+        L = seq_len or self.seq_len
+        ids = torch.randint(1000, 30000, (batch, L), generator=generator)
+        from .bert import encode_inputs
+        return encode_inputs(ids)
+
+    def postprocess_output(self, out: torch.Tensor, meta=None) -> torch.Tensor:
+        n = (meta or {}).get("num_labels", out.shape[-1])
+        return out.reshape(out.shape[0], -1)[:, :n]
+
+
+@register("bert-base")
+class BertBase(TextClassifierAdapter):
+    pass
+
+
+class ImageTransformerAdapter(VisionAdapter):
+    """ViT-B/16 (north-star config 5); ``weights`` = bf16 or fp8 (e4m3 + per-channel scale)."""
+    weights = "bf16"
+
+    def make_model(self, num_classes=None):
+        from .vit import make_model
+        return make_model(num_classes or self.num_classes)
+
+    def pack(self, sd: dict, device):
+        from .vit import pack_vit
+        return pack_vit(sd, device, weights=self.weights)
+
+    def meta_params(self, num_classes=None):
+        from .vit import pack_vit
+        with torch.device("meta"):
+            m = self.make_model(num_classes)
+        return pack_vit(m.state_dict(), "meta", weights=self.weights)
+
+    def build_graph(self, batch=1, **kw):
+        from .vit import build_graph
+        return build_graph(batch, **kw)
+
+    def postprocess_output(self, out: torch.Tensor, meta=None) -> torch.Tensor:
+        n = (meta or {}).get("num_labels", out.shape[-1])
+        return out.reshape(out.shape[0], -1)[:, :n]
+
+
+@register("vit-b16")
+class ViTB16(ImageTransformerAdapter):
+    weights = "bf16"
+
+
+@register("vit-b16-fp8")
+class ViTB16Fp8(ImageTransformerAdapter):
+    weights = "fp8"

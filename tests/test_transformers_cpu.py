@@ -1,0 +1,75 @@
+"""BERT-base / ViT-B/16 lowering vs the HF eager models (CPU, fp32 graph oracle)."""
+import pytest
+import torch
+
+from hipzap.engine.graph import plan_memory
+from hipzap.engine.reference import run_graph_reference
+from hipzap.models import bert, registry, vit
+
+
+def _small_bert():
+    torch.manual_seed(0)
+    return bert.make_model(num_labels=3, num_hidden_layers=2, vocab_size=500, max_position_embeddings=64)
+
+
+def test_bert_graph_oracle_matches_hf():
+    m = _small_bert()
+    P, cfg = bert.pack_bert(m.state_dict())
+    assert cfg["layers"] == 2 and cfg["num_labels"] == 3
+    B, L = 2, 16
+    g = bert.build_graph(B, L, layers=2, num_labels=3)
+    ids = torch.randint(0, 500, (B, L))
+    tt = torch.randint(0, 2, (B, L))
+    am = torch.ones(B, L, dtype=torch.long)
+    am[1, 12:] = 0
+    with torch.no_grad():
+        ref = m(input_ids=ids, token_type_ids=tt, attention_mask=am).logits
+    vals = run_graph_reference(g, P, bert.encode_inputs(ids, tt, am), bf16_acts=False)
+    out = vals[g.outputs[0]][:, :3]
+    assert (out - ref).abs().max() / ref.abs().max() < 3e-2, (out, ref)
+    _, arena = plan_memory(g)
+    assert arena > 0
+
+
+def test_bert_base_shapes_meta():
+    a = registry.get("bert-base")
+    meta, cfg = a.meta_params()
+    assert cfg["layers"] == 12 and cfg["hidden"] == 768 and cfg["ffn"] == 3072
+    assert meta["l0.qkv"].cout == 2304 and meta["cls"].cout == 4  # 2 labels padded to 4
+    g = a.build_graph(batch=16, **cfg)
+    kinds = [n.kind for n in g.nodes]
+    assert kinds.count("gemm") == 12 * 4 + 2 and kinds.count("attention") == 12 and kinds.count("layernorm") == 24
+
+
+@pytest.mark.parametrize("legacy_keys", [False, True])
+def test_vit_graph_oracle_matches_hf(legacy_keys):
+    torch.manual_seed(0)
+    m = vit.make_model(num_labels=10, num_hidden_layers=2, image_size=64, patch_size=16)
+    sd = m.state_dict()
+    if legacy_keys:  # classic HF names (vit.encoder.layer.N.attention.attention.query ...)
+        ren = {"attention.q_proj": "attention.attention.query", "attention.k_proj": "attention.attention.key",
+               "attention.v_proj": "attention.attention.value", "attention.o_proj": "attention.output.dense",
+               "mlp.fc1": "intermediate.dense", "mlp.fc2": "output.dense"}
+        sd2 = {}
+        for k, v in sd.items():
+            nk = k.replace("vit.layers.", "vit.encoder.layer.")
+            for a, b in ren.items():
+                nk = nk.replace(a, b)
+            sd2[nk] = v
+        sd = sd2
+    P, cfg = vit.pack_vit(sd)
+    assert cfg["image"] == 64 and cfg["layers"] == 2
+    g = vit.build_graph(2, **{k: cfg[k] for k in ("layers", "hidden", "heads", "ffn", "patch", "image", "num_labels")})
+    x = torch.randn(2, 3, 64, 64)
+    with torch.no_grad():
+        ref = m(pixel_values=x).logits
+    out = run_graph_reference(g, P, [x], bf16_acts=False)[g.outputs[0]][:, :10]
+    assert (out - ref).abs().max() / ref.abs().max() < 3e-2
+
+
+def test_vit_b16_meta():
+    a = registry.get("vit-b16")
+    meta, cfg = a.meta_params()
+    assert cfg["image"] == 224 and cfg["patch"] == 16 and cfg["layers"] == 12
+    g = a.build_graph(batch=8, **{k: cfg[k] for k in ("layers", "hidden", "heads", "ffn", "patch", "image", "num_labels")})
+    assert g.shape(g.outputs[0]) == (8, 1000)
