@@ -1,0 +1,217 @@
+// FP8 (OCP e4m3fn) inference GEMM path for gfx950 (north-star config 5
+// "ViT-B/16 fp8 weights ... CDNA4 fp8 MFMA GEMM").
+//   * quant_rows: per-row dynamic activation quantisation, x_fp8 = cvt(x / s_m) with
+//     s_m = amax_m / 448 (one wave per row, 16-B loads), scale kept in fp32;
+//   * gemm_fp8:   y[m][n] = s_m * s_n * sum_k x8[m][k] w8[n][k] (+ bias, act, residual) on
+//     v_mfma_f32_16x16x32_fp8_fp8. Same K-across-waves / fragment-major design as the bf16
+//     conv kernel (csrc/conv.hip), but every fragment is 8 B per lane (half the bytes of bf16):
+//     at bs<=64 these GEMMs are operand-streaming bound, so bytes — not the MFMA rate — are
+//     what fp8 buys. Weights: per-output-channel scales s_n, packed [N/16][K/32][64][8] bytes.
+// gfx950 converts with v_cvt_pk_fp8_f32, which on CDNA4 is the OCP e4m3fn encoding (NOT the
+// MI300 FNUZ variant) — checked against torch.float8_e4m3fn in tests/test_fp8_gpu.py.
+#include "common.h"
+#include "hipzap.h"
+
+namespace {
+
+constexpr float FP8_MAX = 448.f;
+
+__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (unsigned)w;
+}
+
+__global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const bf16_t* x = p.x + (long)row * p.ldx;
+  const int nch = p.D >> 3;
+  float v[4][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = c * 64 + lane;
+    if (ch < nch) {
+      unpack8(*reinterpret_cast<const u32x4*>(x + ch * 8), v[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
+    }
+  }
+  amax = warp_max(amax);
+  const float scale = fmaxf(amax, 1e-12f) / FP8_MAX;
+  const float inv = 1.f / scale;
+  unsigned char* o = p.out + (long)row * p.ldo;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = c * 64 + lane;
+    if (ch < nch) {
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = fminf(fmaxf(v[c][e] * inv, -FP8_MAX), FP8_MAX);
+      *reinterpret_cast<u32x2*>(o + ch * 8) = u32x2{pack4_fp8(q[0], q[1], q[2], q[3]), pack4_fp8(q[4], q[5], q[6], q[7])};
+    }
+  }
+  if (lane == 0) p.scale[row] = scale;
+}
+
+template <int FC, int FP>
+struct Depth8 {
+  static constexpr int value = (FC + FP <= 2) ? 8 : (FC + FP <= 3) ? 6 : (FC + FP <= 4) ? 4 : 3;
+};
+constexpr int fp8_max_threads(int nf) { return nf >= 16 ? 256 : nf >= 8 ? 512 : 1024; }
+
+template <int FC, int FP>
+__global__ __launch_bounds__(fp8_max_threads(FC * FP)) void gemm_fp8_kernel(const HzGemmFp8Params p) {
+  constexpr int DEPTH = Depth8<FC, FP>::value;
+  constexpr int NF = FC * FP;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KW = blockDim.x >> 6;
+  const int lrow = lane & 15, lk = (lane >> 4) * 8;
+  const int tiles_n = (p.N + FC * 16 - 1) / (FC * 16);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lid % tiles_n, tile_m = lid / tiles_n;
+  const int n0 = tile_n * FC * 16, m0 = tile_m * FP * 16;
+  const int steps = p.ksteps;
+  const int spw = (steps + KW - 1) / KW;
+  const int s_begin = wave * spw;
+  const int nsteps = max(0, min(steps, s_begin + spw) - s_begin);
+  const unsigned char* __restrict__ Wf = p.w + ((long)(n0 >> 4) * steps) * 512 + lane * 8;
+  bool pval[FP];
+#pragma unroll
+  for (int j = 0; j < FP; ++j) pval[j] = (m0 + j * 16 + lrow) < p.M;
+
+  long fa[DEPTH + 1][FC], fb[DEPTH + 1][FP];
+  f32x4 acc[FC][FP];
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_step = [&](int t, long(&a)[FC], long(&b)[FP]) {
+    const int s_idx = s_begin + t;
+    const int kk = s_idx * 32 + lk;
+#pragma unroll
+    for (int i = 0; i < FC; ++i) a[i] = *reinterpret_cast<const long*>(Wf + ((long)i * steps + s_idx) * 512);
+#pragma unroll
+    for (int j = 0; j < FP; ++j) {
+      if (pval[j] && kk < p.K) b[j] = *reinterpret_cast<const long*>(p.x + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
+      else b[j] = 0;
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < DEPTH; ++u)
+    if (u < nsteps) load_step(u, fa[u], fb[u]);
+  for (int t = 0; t < nsteps; t += DEPTH + 1) {
+#pragma unroll
+    for (int u = 0; u <= DEPTH; ++u) {
+      const int tt = t + u;
+      if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
+      if (tt < nsteps) {
+#pragma unroll
+        for (int i = 0; i < FC; ++i)
+#pragma unroll
+          for (int j = 0; j < FP; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fa[u][i], fb[u][j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  auto epilogue = [&](int i, int j, f32x4 a) {
+    const int m = m0 + j * 16 + lrow;
+    const int n = n0 + i * 16 + (lane >> 4) * 4;
+    if (m >= p.M || n >= p.N) return;
+    const float sx = p.sx[m];
+    const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e] * sx * sw[e];
+    if (p.bias) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bb[e];
+    }
+    const long o = (long)m * p.ldo + n;
+    if (p.res) {
+      const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
+      v[0] += __uint_as_float(rr[0] << 16);
+      v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+      v[2] += __uint_as_float(rr[1] << 16);
+      v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+    }
+    if (p.act == HZ_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (p.act == HZ_ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+    } else if (p.act == HZ_ACT_TANH) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+    }
+    if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+    else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  };
+  if (KW == 1) {
+#pragma unroll
+    for (int i = 0; i < FC; ++i)
+#pragma unroll
+      for (int j = 0; j < FP; ++j) epilogue(i, j, acc[i][j]);
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  f32x4* red = reinterpret_cast<f32x4*>(smem_raw);
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) red[(wave * NF + i * FP + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < FC; ++i)
+#pragma unroll
+    for (int j = 0; j < FP; ++j) {
+      const int ij = i * FP + j;
+      if ((ij % KW) != wave) continue;
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < KW; ++w) s += red[(w * NF + ij) * 64 + lane];
+      epilogue(i, j, s);
+    }
+}
+
+template <int FC, int FP>
+int launch8(const HzGemmFp8Params& p, hipStream_t st) {
+  const int kw = p.kw < 1 ? 1 : p.kw;
+  if (kw > 16 || kw * FC * FP > 64 || 64 * kw > fp8_max_threads(FC * FP)) return -5;
+  const int tiles = ((p.N + FC * 16 - 1) / (FC * 16)) * ((p.M + FP * 16 - 1) / (FP * 16));
+  const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
+  hipLaunchKernelGGL((gemm_fp8_kernel<FC, FP>), dim3(tiles), dim3(64 * kw), lds, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int hz_quant_launch(const HzQuantParams* pp, hipStream_t st) {
+  const HzQuantParams& p = *pp;
+  if (p.D % 8 || p.D > 2048 || p.ldo % 8) return -1;
+  hipLaunchKernelGGL(quant_rows_kernel, dim3((p.rows + 3) / 4), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
+  const HzGemmFp8Params& p = *pp;
+  if (p.N % 4 || p.ldx % 8 || p.ksteps * 32 < p.K) return -1;
+  switch (p.cfg) {
+    case 0: return launch8<1, 1>(p, st);
+    case 1: return launch8<1, 2>(p, st);
+    case 2: return launch8<1, 4>(p, st);
+    case 3: return launch8<2, 1>(p, st);
+    case 4: return launch8<2, 2>(p, st);
+    case 5: return launch8<2, 4>(p, st);
+    case 6: return launch8<4, 1>(p, st);
+    case 7: return launch8<4, 2>(p, st);
+    case 8: return launch8<4, 4>(p, st);
+    default: return -2;
+  }
+}

@@ -83,6 +83,27 @@ int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);
 int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);
 
+// ---- FP8 (OCP e4m3fn) path (csrc/fp8.hip) ----
+typedef struct HzQuantParams {
+  const unsigned short* x;    // [rows][ldx] bf16
+  unsigned char* out;         // [rows][ldo] fp8 e4m3fn
+  float* scale;               // [rows] fp32 (amax/448)
+  int rows, D, ldx, ldo;
+} HzQuantParams;
+typedef struct HzGemmFp8Params {
+  const unsigned char* x;     // [M][ldx] fp8
+  const float* sx;            // [M] row scales
+  const unsigned char* w;     // fragment-major fp8 [N_pad/16][ksteps][64][8]
+  const float* sw;            // [N_pad] per-channel scales
+  const float* bias;          // [N] or NULL
+  const unsigned short* res;  // [M][ldo] bf16 or NULL
+  void* out;                  // [M][ldo] bf16 or fp32
+  int M, N, K, ksteps, ldx, ldo;
+  int act, out_f32, cfg, kw;
+} HzGemmFp8Params;
+int hz_quant_launch(const HzQuantParams* p, hipStream_t st);
+int hz_gemm_fp8_launch(const HzGemmFp8Params* p, hipStream_t st);
+
 // ---- transformer kernels (csrc/transformer.hip) ----
 typedef struct HzLayerNormParams {
   const unsigned short* x;    // [rows][ldx] bf16
@@ -126,7 +147,7 @@ int hz_vit_tokens_launch(const HzVitTokensParams* p, hipStream_t st);
 
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
-       HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10 };
+       HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
 

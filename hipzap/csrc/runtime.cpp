@@ -239,6 +239,8 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_DECODER: return hz_decoder_launch(static_cast<const HzDecoderParams*>(prm), st);
     case HZ_K_SAMPLER: return hz_sampler_launch(static_cast<const HzSamplerParams*>(prm), st);
     case HZ_K_MAXPOOL: return hz_maxpool_launch(static_cast<const HzPoolParams*>(prm), st);
+    case HZ_K_QUANT: return hz_quant_launch(static_cast<const HzQuantParams*>(prm), st);
+    case HZ_K_GEMM_FP8: return hz_gemm_fp8_launch(static_cast<const HzGemmFp8Params*>(prm), st);
     default: return -100;
   }
 }

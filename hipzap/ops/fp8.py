@@ -1,0 +1,123 @@
+"""FP8 (OCP e4m3fn) weight packing, activation quantisation and the fp8 MFMA GEMM.
+
+Weights: per-output-channel scale ``s_n = amax_n / 448``, ``w8 = e4m3(w / s_n)``, packed
+fragment-major ``[N_pad/16][K/32][64][8]`` bytes (csrc/fp8.hip). Activations: per-row dynamic
+scale computed on device by ``quant_rows`` right before each GEMM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native as N
+from .conv import PackedConv, choose_config, fragment_major
+
+K_QUANT, K_GEMM_FP8 = 10, 11
+FP8_MAX = 448.0
+
+
+class QuantParams(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("out", C.c_void_p), ("scale", C.c_void_p), ("rows", C.c_int), ("D", C.c_int),
+                ("ldx", C.c_int), ("ldo", C.c_int)]
+
+
+class GemmFp8Params(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("sx", C.c_void_p), ("w", C.c_void_p), ("sw", C.c_void_p), ("bias", C.c_void_p),
+                ("res", C.c_void_p), ("out", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
+                ("ksteps", C.c_int), ("ldx", C.c_int), ("ldo", C.c_int), ("act", C.c_int), ("out_f32", C.c_int),
+                ("cfg", C.c_int), ("kw", C.c_int)]
+
+
+@dataclass
+class PackedFp8:
+    w8: torch.Tensor     # uint8 (e4m3fn bits) fragment-major [rows_pad/16, ksteps, 64, 8]
+    sw: torch.Tensor     # fp32 [rows_pad] per-output-channel scales
+    bias: torch.Tensor   # fp32 [cout]
+    cin: int             # K
+    cout: int
+
+    @property
+    def K(self) -> int:
+        return self.cin
+
+    @property
+    def ksteps(self) -> int:
+        return self.w8.shape[1]
+
+    def dequant(self) -> torch.Tensor:
+        g, ks = self.w8.shape[0], self.w8.shape[1]
+        w = self.w8.view(torch.float8_e4m3fn).float()
+        w = w.reshape(g, ks, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(g * 16, ks * 32)
+        w = w * self.sw.float().reshape(-1, 1)
+        return w[: self.cout, : self.K]
+
+
+def quantize_weight(w2d: torch.Tensor, rows_pad: int | None = None):
+    """[N, K] float -> (e4m3fn bits [N_pad, K_pad] uint8, scales [N_pad])."""
+    n, k = w2d.shape
+    rows = rows_pad or n
+    kp = int(math.ceil(k / 32) * 32)
+    amax = w2d.float().abs().amax(dim=1).clamp_min(1e-12)
+    s = amax / FP8_MAX
+    q = torch.zeros(rows, kp, dtype=torch.float8_e4m3fn, device=w2d.device)
+    q[:n, :k] = (w2d.float() / s.reshape(-1, 1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    sw = torch.ones(rows, device=w2d.device)
+    sw[:n] = s
+    return q.view(torch.uint8), sw
+
+
+def quantize_linear(pc: PackedConv) -> PackedFp8:
+    if pc.r != 1 or pc.s != 1:
+        raise ValueError("fp8 path is for Linear layers")
+    rows = pc.wf.shape[0] * 16
+    q, sw = quantize_weight(pc.dense(), rows)
+    return PackedFp8(fragment_major(q).contiguous(), sw.contiguous(), pc.bias.float().contiguous(), pc.K, pc.cout)
+
+
+def quantize_params(P: dict, names) -> dict:
+    out = dict(P)
+    for n in names:
+        if isinstance(P[n], PackedConv):
+            out[n] = quantize_linear(P[n])
+    return out
+
+
+def quant_rows_ref(x: torch.Tensor):
+    """fp32 oracle of quant_rows: returns (dequantised x, scales)."""
+    x = x.float()
+    s = x.abs().amax(dim=-1).clamp_min(1e-12) / FP8_MAX
+    q = (x / s.unsqueeze(-1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float()
+    return q * s.unsqueeze(-1), s
+
+
+# ----------------------------------------------------------------------------- eager
+def quant_rows(x: torch.Tensor):
+    rows, D = x.shape
+    out = torch.empty(rows, D, dtype=torch.uint8, device=x.device)
+    sc = torch.empty(rows, dtype=torch.float32, device=x.device)
+    prm = QuantParams(x.data_ptr(), out.data_ptr(), sc.data_ptr(), rows, D, x.stride(0), out.stride(0))
+    N.check(N.lib().hz_launch_kernel(K_QUANT, C.byref(prm), N.stream_ptr()), "quant_rows")
+    return out, sc
+
+
+def gemm_params(x8_ptr, sx_ptr, pw: PackedFp8, M, out_ptr, res_ptr=0, act="none", out_f32=False, cfg=0, kw=1,
+                ldx=None, ldo=None) -> GemmFp8Params:
+    from .conv import ACT
+    return GemmFp8Params(x8_ptr, sx_ptr, pw.w8.data_ptr(), pw.sw.data_ptr(), pw.bias.data_ptr(), res_ptr, out_ptr, M,
+                         pw.cout, pw.K, pw.ksteps, ldx if ldx is not None else pw.K,
+                         ldo if ldo is not None else pw.cout, ACT[act], int(out_f32), cfg, kw)
+
+
+def gemm_fp8(x8: torch.Tensor, sx: torch.Tensor, pw: PackedFp8, residual=None, act="none", out_f32=False,
+             cfg=None, kw=None) -> torch.Tensor:
+    M = x8.shape[0]
+    if cfg is None:
+        cfg, kw = choose_config(M, pw.cout, pw.K)
+    out = torch.empty(M, pw.cout, device=x8.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    prm = gemm_params(x8.data_ptr(), sx.data_ptr(), pw, M, out.data_ptr(), N.ptr(residual), act, out_f32, cfg,
+                      kw or 1, x8.stride(0), out.stride(0))
+    N.check(N.lib().hz_launch_kernel(K_GEMM_FP8, C.byref(prm), N.stream_ptr()), "gemm_fp8")
+    return out
