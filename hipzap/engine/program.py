@@ -13,6 +13,7 @@ import torch
 
 from .. import _native as N
 from ..ops import conv as conv_ops
+from ..ops import fp8
 from ..ops import transformer as tx
 from .graph import Graph, plan_memory
 
@@ -47,11 +48,14 @@ class ExecContext:
         self.configs: list = []
         conv_plans = []
         for n in g.nodes:
-            if n.kind not in ("conv", "gemm"):
+            if n.kind not in ("conv", "gemm", "gemm_fp8"):
                 conv_plans.append(None)
                 continue
             pc = params[n.attrs["w"]]
-            if n.kind == "conv":
+            if n.kind == "gemm_fp8":
+                M = n.attrs["rows"]
+                key = f"f8r{M}x{pc.cout}x{pc.K}"
+            elif n.kind == "conv":
                 nb, h, w, _ = g.shape(n.inputs[0])
                 p_out = (h + 2 * pc.pad - pc.r) // pc.stride + 1
                 q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
@@ -136,6 +140,19 @@ class ExecContext:
                                              out_rowmajor=True, ldo=out_spec.shape[-1], x_rowmajor=True, ldx=ldx)
             self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
             N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_gemm")
+        elif n.kind == "quant":
+            rows, D = g.shape(n.inputs[0])
+            prm = fp8.QuantParams(addr(n.inputs[0]), addr(n.outputs[0]), addr(n.outputs[1]), rows, D, D, D)
+            tx.prog_add(self.prog, fp8.K_QUANT, prm, n.slot)
+        elif n.kind == "gemm_fp8":
+            pw = self.params[n.attrs["w"]]
+            cfg, kw, key = plan
+            res = n.inputs[2] if len(n.inputs) > 2 else None
+            prm = fp8.gemm_params(addr(n.inputs[0]), addr(n.inputs[1]), pw, n.attrs["rows"], addr(n.outputs[0]),
+                                  addr(res), n.attrs.get("act", "none"), n.attrs.get("out_f32", False), cfg, kw,
+                                  ldx=g.shape(n.inputs[0])[-1], ldo=g.shape(n.outputs[0])[-1])
+            self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
+            tx.prog_add(self.prog, fp8.K_GEMM_FP8, prm, n.slot)
         elif n.kind == "layernorm":
             npar = self.params[n.attrs["p"]]
             res = n.inputs[1] if len(n.inputs) > 1 else None

@@ -79,6 +79,19 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             act = n.attrs.get("act", "none")
             y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
             store(n.outputs[0], y)
+        elif k == "quant":
+            from ..ops.fp8 import quant_rows_ref
+            deq, s = quant_rows_ref(vals[n.inputs[0]])
+            vals[n.outputs[0]] = deq  # the oracle carries the dequantised values
+            vals[n.outputs[1]] = s
+        elif k == "gemm_fp8":
+            pw = params[n.attrs["w"]]
+            y = vals[n.inputs[0]].float() @ pw.dequant().t() + pw.bias.float()
+            if len(n.inputs) > 2:
+                y = y + vals[n.inputs[2]].float()
+            act = n.attrs.get("act", "none")
+            y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
+            store(n.outputs[0], y)
         elif k == "layernorm":
             npar = params[n.attrs["p"]]
             rows = n.attrs["rows"]

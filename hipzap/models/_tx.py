@@ -44,6 +44,21 @@ class TxBuilder:
         g.add("gemm", ins, [out], w=w, act=act, rows=r, ldx=ldx, out_f32=out_f32, name=name or w)
         return out
 
+    def gemm8(self, x, w: str, cols: int, act="none", res=None, out_f32=False, ext=False, name=None):
+        """fp8 GEMM: per-row dynamic quantisation of ``x`` then the fp8 MFMA GEMM."""
+        g = self.g
+        r, k = g.shape(x)
+        x8 = g.tensor((r, k), torch.uint8, f"{w}.x8")
+        sx = g.tensor((r,), torch.float32, f"{w}.sx")
+        g.add("quant", [x], [x8, sx])
+        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
+        ins = [x8, sx] if res is None else [x8, sx, res]
+        g.add("gemm_fp8", ins, [out], w=w, act=act, rows=r, out_f32=out_f32, name=name or w)
+        return out
+
+    def linear(self, x, w: str, cols: int, fp8: bool = False, **kw):
+        return self.gemm8(x, w, cols, **kw) if fp8 else self.gemm(x, w, cols, **kw)
+
     def layernorm(self, x, p: str, res=None, rows=None, ldx=None, name=None):
         g = self.g
         r = rows if rows is not None else g.shape(x)[0]

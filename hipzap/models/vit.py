@@ -97,18 +97,19 @@ def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12
     tok = g.tensor((B * T, D), torch.bfloat16, "tokens")
     g.add("vit_tokens", [patches], [tok], cls="cls_token", pos="pos", B=B, np=npch)
     tb = TxBuilder(g)
+    f8 = weights == "fp8"
     x = tok
     for i in range(layers):
         h = tb.layernorm(x, f"l{i}.ln1")
-        qkv = tb.gemm(h, f"l{i}.qkv", 3 * D)
+        qkv = tb.linear(h, f"l{i}.qkv", 3 * D, fp8=f8)
         ctx = tb.attention(qkv, B, T, heads)
-        x2 = tb.gemm(ctx, f"l{i}.o", D, res=x)
+        x2 = tb.linear(ctx, f"l{i}.o", D, fp8=f8, res=x)
         h2 = tb.layernorm(x2, f"l{i}.ln2")
-        f = tb.gemm(h2, f"l{i}.fc1", ffn, act="gelu")
-        x = tb.gemm(f, f"l{i}.fc2", D, res=x2)
+        f = tb.linear(h2, f"l{i}.fc1", ffn, fp8=f8, act="gelu")
+        x = tb.linear(f, f"l{i}.fc2", D, fp8=f8, res=x2)
     cls = tb.layernorm(x, "final_ln", rows=B, ldx=T * D, name="cls_ln")
     npad = (num_labels + 3) // 4 * 4
-    logits = tb.gemm(cls, "head", npad, out_f32=True, ext=True)
+    logits = tb.linear(cls, "head", npad, fp8=f8, out_f32=True, ext=True)
     g.outputs.append(logits)
     g.meta = {"num_labels": num_labels}
     return g

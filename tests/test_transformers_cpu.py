@@ -73,3 +73,28 @@ def test_vit_b16_meta():
     assert cfg["image"] == 224 and cfg["patch"] == 16 and cfg["layers"] == 12
     g = a.build_graph(batch=8, **{k: cfg[k] for k in ("layers", "hidden", "heads", "ffn", "patch", "image", "num_labels")})
     assert g.shape(g.outputs[0]) == (8, 1000)
+
+
+def test_vit_fp8_oracle_close_to_bf16():
+    torch.manual_seed(0)
+    m = vit.make_model(num_labels=10, num_hidden_layers=2, image_size=64, patch_size=16)
+    sd = m.state_dict()
+    kw = lambda cfg: {k: cfg[k] for k in ("layers", "hidden", "heads", "ffn", "patch", "image", "num_labels")}
+    P16, cfg = vit.pack_vit(sd)
+    P8, cfg8 = vit.pack_vit(sd, weights="fp8")
+    g16 = vit.build_graph(2, **kw(cfg))
+    g8 = vit.build_graph(2, **kw(cfg), weights="fp8")
+    assert any(n.kind == "gemm_fp8" for n in g8.nodes) and any(n.kind == "quant" for n in g8.nodes)
+    x = torch.randn(2, 3, 64, 64)
+    a = run_graph_reference(g16, P16, [x], bf16_acts=False)[g16.outputs[0]][:, :10]
+    b = run_graph_reference(g8, P8, [x], bf16_acts=False)[g8.outputs[0]][:, :10]
+    assert (a - b).abs().max() / a.abs().max() < 0.15  # e4m3 has a 3-bit mantissa
+
+
+def test_fp8_weight_roundtrip():
+    from hipzap.ops.conv import pack_linear
+    from hipzap.ops.fp8 import quantize_linear
+    w = torch.randn(100, 96)
+    pw = quantize_linear(pack_linear(w, torch.zeros(100)))
+    err = (pw.dequant() - w).abs() / w.abs().amax(dim=1, keepdim=True)
+    assert err.max() < 0.07 and pw.w8.dtype == torch.uint8 and pw.sw.shape[0] % 64 == 0
