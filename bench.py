@@ -44,7 +44,65 @@ def parse():
     ap.add_argument("--compare-torch", action="store_true", help="also time PyTorch/MIOpen bf16 + CUDA graph")
     ap.add_argument("--no-capture", action="store_true")
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
+    ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
+                    help="replica: independent bs=1 request streams per GPU (headline); scatter: rank 0 scatters "
+                         "a global batch over ranks and gathers the logits (configs 3/5)")
+    ap.add_argument("--global-batch", type=int, default=32, help="scatter mode: global batch over all ranks")
     return ap.parse_args()
+
+
+def run_scatter(args, rank, world, device, adapter, ckpt):
+    """BASELINE configs 3/5: global batch scattered over ranks (RCCL), per-rank hipGraph, logits
+    gathered to rank 0. Step = scatter + per-rank forward + gather."""
+    from hipzap.engine.engine import Engine
+    from hipzap.parallel.comm import broadcast_params, is_dist
+    from hipzap.parallel.dp import DPExecutor
+    shard = args.global_batch // world
+    assert shard * world == args.global_batch, "global batch must divide over ranks"
+    t0 = time.perf_counter()
+    params, arch_kw = (None, None)
+    if rank == 0:
+        sd = torch.load(ckpt, map_location="cpu", weights_only=True)
+        params, arch_kw = adapter.pack({k: v.to(device) for k, v in sd.items()}, device)
+    meta, meta_kw = adapter.meta_params()
+    params = broadcast_params(params, meta, device)
+    eng = Engine(args.model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw or meta_kw,
+                 host_io=False)
+    x_in = adapter.example_input(shard)
+    in_shape = tuple(eng.contexts[0].input.shape[1:])
+    out_shape = tuple(eng.contexts[0].output.shape[1:])
+    ex = DPExecutor(lambda xs: eng.infer_device(xs), shard, in_shape, out_shape, device)
+    xg = adapter.example_input(args.global_batch).to(device) if rank == 0 else None
+    ex.step(xg)
+    torch.cuda.synchronize(device)
+    cold = (time.perf_counter() - t0) * 1e3
+    for _ in range(args.warmup):
+        ex.step(xg)
+    if is_dist():
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        ex.step(xg)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t1
+    if is_dist():
+        dist.barrier()
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    del x_in
+    if rank == 0:
+        value = args.global_batch * args.steps / dt
+        print(json.dumps({
+            "metric": f"{args.model} images/s, global batch {args.global_batch} scattered over {world} GPU(s)",
+            "value": round(value, 2), "unit": "inferences/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "fp8" if "fp8" in args.model else "bf16",
+            "data": "synthetic (random-init weights, random inputs)",
+            "config": {"model": args.model, "global_batch": args.global_batch, "seq_len": None,
+                       "parallelism": f"dp{world}-scatter-gather"},
+            "cold_start_ms": round(cold, 2)}), flush=True)
 
 
 def write_checkpoint(path, model):
@@ -105,6 +163,12 @@ def main():
             tuned = json.load(f)
     if is_dist():
         dist.barrier()
+    if args.mode == "scatter":
+        run_scatter(args, rank, world, device, adapter, ckpt)
+        if is_dist():
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     def cold_start():
         t0 = time.perf_counter()

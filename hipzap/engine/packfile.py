@@ -1,0 +1,65 @@
+"""Pre-packed weight files: the cold-start fast path (SURVEY.md §5 checkpoint/resume).
+
+``torch.load`` of a standard state_dict stays the public format (reference parity:
+main.py:99). ``hipzap pack`` additionally writes the *packed* device layout (BN folded,
+fragment-major bf16/fp8, padded) as a safetensors file + JSON metadata next to the .pth, keyed
+by the checkpoint's sha256, so a cold start can skip folding/packing and stream the blob
+straight into device memory (safetensors: no pickle, nothing executed on load).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+
+import torch
+
+from ..parallel.comm import _rebuild, _tensor_fields
+
+
+def _classes():
+    from ..ops.conv import PackedConv
+    from ..ops.fp8 import PackedFp8
+    from ..ops.transformer import EmbedTables, NormParams
+    return {c.__name__: c for c in (PackedConv, PackedFp8, NormParams, EmbedTables)}
+
+
+def save_packed(params: dict, cfg: dict, path: str, source_sha256: str | None = None) -> None:
+    from safetensors.torch import save_file
+    tensors, meta = {}, {"cfg": cfg, "source_sha256": source_sha256, "entries": {}}
+    for key, obj in params.items():
+        if torch.is_tensor(obj):
+            tensors[key] = obj.detach().contiguous().cpu()
+            meta["entries"][key] = {"type": "tensor"}
+            continue
+        fields = {}
+        for f in dataclasses.fields(obj):
+            v = getattr(obj, f.name)
+            if torch.is_tensor(v):
+                tensors[f"{key}::{f.name}"] = v.detach().contiguous().cpu()
+            else:
+                fields[f.name] = v
+        meta["entries"][key] = {"type": type(obj).__name__, "fields": fields}
+    tmp = path + ".tmp"
+    save_file(tensors, tmp, metadata={"hipzap": json.dumps(meta)})
+    os.replace(tmp, path)
+
+
+def load_packed(path: str, device="cpu") -> tuple[dict, dict]:
+    from safetensors import safe_open
+    classes = _classes()
+    out = {}
+    with safe_open(path, framework="pt", device=str(device)) as f:
+        meta = json.loads(f.metadata()["hipzap"])
+        for key, ent in meta["entries"].items():
+            if ent["type"] == "tensor":
+                out[key] = f.get_tensor(key)
+                continue
+            cls = classes[ent["type"]]
+            kw = dict(ent["fields"])
+            for fl in dataclasses.fields(cls):
+                name = f"{key}::{fl.name}"
+                if fl.name not in kw:
+                    kw[fl.name] = f.get_tensor(name)
+            out[key] = cls(**kw)
+    return out, meta["cfg"]

@@ -56,3 +56,39 @@ def test_broadcast_world2_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2] == 1000
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipzap.parallel.dp import DPExecutor
+    seen = []
+
+    def runner(x):  # per-rank "model": tag rows with the rank that computed them
+        seen.append(x.clone())
+        return x.sum(dim=(1, 2)) + 1000 * rank
+
+    ex = DPExecutor(runner, shard_batch=3, in_shape=(2, 4), out_shape=(), device="cpu")
+    x = torch.arange(5 * 8, dtype=torch.float32).reshape(5, 2, 4) if rank == 0 else None  # uneven: 5 of 6
+    y = ex.step(x)
+    if rank == 0:
+        q.put(("y", y.tolist()))
+    q.put(("shard", rank, seen[0].shape[0]))
+    dist.destroy_process_group()
+
+
+def test_dp_scatter_gather_world2_uneven():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=60)
+    y = next(m[1] for m in msgs if m[0] == "y")
+    x = torch.arange(5 * 8, dtype=torch.float32).reshape(5, 2, 4)
+    expect = (x.sum(dim=(1, 2)) + torch.tensor([0, 0, 0, 1000, 1000])).tolist()
+    assert y == expect
+    assert sorted(m[2] for m in msgs if m[0] == "shard") == [3, 3]
