@@ -1,0 +1,71 @@
+"""CLI, settings, artifact store and packed-weight files (CPU)."""
+import json
+import os
+
+import torch
+
+from hipzap.__main__ import main
+from hipzap.engine.packfile import load_packed, save_packed
+from hipzap.models import registry
+from hipzap.serve.artifacts import ArtifactStore
+from hipzap.serve.settings import apply_environment, load_settings
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_settings_template_and_env(tmp_path):
+    cfg = json.load(open(os.path.join(ROOT, "zappa_settings.rename.json")))
+    assert cfg["dev"]["app_function"] == "main.app"
+    env = {}
+    apply_environment(cfg, "dev", env)
+    assert env["models_bucket"] == "models-bucket-name"
+    p = tmp_path / "zs.json"
+    p.write_text(json.dumps(cfg))
+    env2 = {"HIPZAP_PORT": "9999"}
+    st = load_settings(str(p), "dev", env2)
+    assert st.models_bucket == "models-bucket-name" and st.port == 9999
+    assert st.models["vit-b16"].name == "vit-b16-fp8" and st.models["resnet50"].contexts == 8
+    assert st.lm_model_key == "models/rjokes/rjokes.model.pth"
+
+
+def test_artifact_store_atomic_cache(tmp_path):
+    bucket = tmp_path / "bucket"
+    (bucket / "models" / "m").mkdir(parents=True)
+    (bucket / "models" / "m" / "m.model.pth").write_bytes(b"abc")
+    store = ArtifactStore(f"file://{bucket}", str(tmp_path / "cache"))
+    p = store.fetch("models/m/m.model.pth")  # parent dirs created (main.py:33 bug fixed)
+    assert open(p, "rb").read() == b"abc"
+    (bucket / "models" / "m" / "m.model.pth").write_bytes(b"zzz")
+    assert open(store.fetch("models/m/m.model.pth"), "rb").read() == b"abc"  # cached
+    assert not [f for f in os.listdir(os.path.dirname(p)) if f.startswith(".part-")]
+
+
+def test_upload_dir_local(tmp_path):
+    src = tmp_path / "models" / "x"
+    src.mkdir(parents=True)
+    (src / "x.model.pth").write_bytes(b"1")
+    bucket = tmp_path / "b"
+    bucket.mkdir()
+    copied = ArtifactStore(str(bucket)).upload_dir(str(tmp_path / "models"))
+    assert copied == ["x/x.model.pth"] and (bucket / "models" / "x" / "x.model.pth").exists()
+
+
+def test_packfile_roundtrip(tmp_path):
+    a = registry.get("resnet18")
+    params, cfg = a.pack(a.make_model().state_dict(), "cpu")
+    path = str(tmp_path / "r18.hzpack")
+    save_packed(params, cfg, path, "deadbeef")
+    back, cfg2 = load_packed(path)
+    assert cfg2 == cfg and set(back) == set(params)
+    assert torch.equal(back["fc"].wf, params["fc"].wf) and back["fc"].cout == 1000
+
+
+def test_cli_pack_and_info(tmp_path, capsys):
+    a = registry.get("resnet18")
+    ck = tmp_path / "r.pth"
+    torch.save(a.make_model().state_dict(), ck)
+    main(["pack", "--model", "resnet18", "--ckpt", str(ck), "--out", str(tmp_path / "r.hzpack")])
+    out = json.loads(capsys.readouterr().out)
+    assert out["entries"] > 10
+    main(["info"])
+    assert "resnet50" in capsys.readouterr().out
