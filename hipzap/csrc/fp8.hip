@@ -15,6 +15,7 @@
 namespace {
 
 constexpr float FP8_MAX = 448.f;
+constexpr int QCH = 8;  // 16-B chunks per lane: rows up to 64*8*8 = 4096 elements
 
 __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
@@ -28,10 +29,10 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) 
   if (row >= p.rows) return;
   const bf16_t* x = p.x + (long)row * p.ldx;
   const int nch = p.D >> 3;
-  float v[4][8];
+  float v[QCH][8];
   float amax = 0.f;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < QCH; ++c) {
     const int ch = c * 64 + lane;
     if (ch < nch) {
       unpack8(*reinterpret_cast<const u32x4*>(x + ch * 8), v[c]);
@@ -44,7 +45,7 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) 
   const float inv = 1.f / scale;
   unsigned char* o = p.out + (long)row * p.ldo;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < QCH; ++c) {
     const int ch = c * 64 + lane;
     if (ch < nch) {
       float q[8];
@@ -194,7 +195,7 @@ int launch8(const HzGemmFp8Params& p, hipStream_t st) {
 
 extern "C" int hz_quant_launch(const HzQuantParams* pp, hipStream_t st) {
   const HzQuantParams& p = *pp;
-  if (p.D % 8 || p.D > 2048 || p.ldo % 8) return -1;
+  if (p.D % 8 || p.D > 64 * 8 * QCH || p.ldo % 8) return -1;
   hipLaunchKernelGGL(quant_rows_kernel, dim3((p.rows + 3) / 4), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
