@@ -145,9 +145,34 @@ def decode_input(req) -> tuple[str, torch.Tensor]:
     return model or get_server().settings.default_model, x
 
 
+def _predict_text(s, body):
+    """BERT-style sequence classification: {"model", "input_ids", "token_type_ids"?,
+    "attention_mask"?} -> class probabilities."""
+    model = body.get("model") or "bert-base"
+    ids = torch.tensor(body["input_ids"], dtype=torch.long)
+    if ids.dim() == 1:
+        ids = ids[None]
+    tt = body.get("token_type_ids")
+    am = body.get("attention_mask")
+    tt = torch.tensor(tt, dtype=torch.long).reshape(ids.shape) if tt is not None else None
+    am = torch.tensor(am, dtype=torch.long).reshape(ids.shape) if am is not None else None
+    backend = s.text(model)
+    t0 = time.perf_counter()
+    logits = backend(ids, tt, am)
+    dt = (time.perf_counter() - t0) * 1e3
+    probs = torch.softmax(logits.float(), dim=-1)
+    return _json({"model": model, "backend": backend.backend, "batch": int(ids.shape[0]),
+                  "probs": [[round(float(p), 6) for p in row] for row in probs],
+                  "label": [int(i) for i in probs.argmax(-1)], "timing_ms": round(dt, 3)})
+
+
 @app.route("/predict", methods=["POST"])
 def predict():
     s = get_server()
+    if request.mimetype != "application/octet-stream":
+        body = request.get_json(force=True, silent=True) or {}
+        if "input_ids" in body:
+            return _predict_text(s, body)
     model, x = decode_input(request)
     backend = s.vision(model)
     t0 = time.perf_counter()

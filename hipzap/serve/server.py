@@ -21,6 +21,8 @@ import torch
 from ..models import registry
 from .artifacts import ArtifactStore
 from .settings import ModelSpec, Settings
+from ..utils.tracing import trace_range
+from ..utils.watchdog import maybe_fault
 from .text import generate_text, load_itos, make_stoi
 
 log = logging.getLogger("hipzap.server")
@@ -69,6 +71,80 @@ class VisionBackend:
             return self.model(x.float())
 
 
+class TextBackend:
+    """BERT-style sequence classifier; requests are padded to the captured (batch, seq_len)."""
+
+    def __init__(self, name: str, sd: dict, backend: str, device: str, spec: ModelSpec, capture: bool):
+        self.name, self.backend = name, backend
+        t0 = time.perf_counter()
+        self.adapter = registry.get(name)
+        self.seq_len = int(spec.extra.get("seq_len", 128))
+        if backend == "gpu":
+            from ..engine.engine import Engine
+            self.engine = Engine.from_state_dict(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
+                                                 capture=capture)
+            self.model = None
+        else:
+            from ..models.bert import config_from_sd, make_model
+            cfg = config_from_sd(sd)
+            self.model = make_model(cfg["num_labels"], num_hidden_layers=cfg["layers"], hidden_size=cfg["hidden"],
+                                    num_attention_heads=cfg["heads"], intermediate_size=cfg["ffn"],
+                                    vocab_size=sd["bert.embeddings.word_embeddings.weight"].shape[0],
+                                    max_position_embeddings=cfg["max_pos"])
+            self.model.load_state_dict(sd)
+            self.engine = None
+        self.batch = spec.batch
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+
+    def __call__(self, ids: torch.Tensor, types=None, mask=None) -> torch.Tensor:
+        B, L = ids.shape
+        types = types if types is not None else torch.zeros_like(ids)
+        mask = mask if mask is not None else torch.ones_like(ids)
+        if self.engine is None:
+            with torch.no_grad():
+                return self.model(input_ids=ids, token_type_ids=types, attention_mask=mask).logits
+        from ..models.bert import encode_inputs
+        Lc = self.engine.arch_kw.get("seq_len", self.seq_len)
+        if L > Lc:
+            raise ValueError(f"sequence length {L} exceeds the captured {Lc}")
+        pad = Lc - L
+        ids, types, mask = (torch.nn.functional.pad(t, (0, pad)) for t in (ids, types, mask))
+        outs = []
+        for i in range(0, B, self.batch):
+            sl = slice(i, i + self.batch)
+            ci, ct, cm = ids[sl], types[sl], mask[sl]
+            n = ci.shape[0]
+            if n < self.batch:
+                z = self.batch - n
+                ci, ct, cm = (torch.cat([t, t.new_zeros(z, Lc)]) for t in (ci, ct, cm))
+            outs.append(self.engine.infer(encode_inputs(ci, ct, cm))[:n])
+        return torch.cat(outs)
+
+
+class RoundRobin:
+    """One backend per GPU of the node; requests are dealt round-robin (DP replica serving)."""
+
+    def __init__(self, backends: list, devices: list | None = None, healthy=None):
+        self.backends = backends
+        self.devices = devices or [None] * len(backends)
+        self.healthy = healthy  # callable(device) -> bool (DeviceWatchdog), or None
+        self.backend = backends[0].backend
+        self.cold_ms = sum(b.cold_ms for b in backends)
+        self._i = 0
+        self._lock = threading.Lock()
+
+    def __call__(self, *a, **kw):
+        with self._lock:
+            for _ in range(len(self.backends)):
+                i = self._i
+                self._i = (self._i + 1) % len(self.backends)
+                if self.healthy is None or self.healthy(self.devices[i]):
+                    break
+            else:
+                raise RuntimeError("no healthy device replica")
+        return self.backends[i](*a, **kw)
+
+
 class LMBackend:
     """AWD-LSTM text generation (GET /inference)."""
 
@@ -111,6 +187,7 @@ class ModelServer:
         self.device = f"cuda:{settings.devices[0]}" if backend == "gpu" else "cpu"
         self._models: dict = {}
         self._lock = threading.Lock()
+        self._watchdog = None
         self.stats = {"requests": 0, "errors": 0, "cold_loads": 0}
 
     def spec(self, name: str) -> ModelSpec:
@@ -126,15 +203,41 @@ class ModelServer:
             sd = sd["state_dict"]
         return sd
 
-    def vision(self, name: str) -> VisionBackend:
+    def watchdog(self):
+        """Per-GPU liveness watchdog (started on first GPU model load; HIPZAP_WATCHDOG=0 disables)."""
+        if self.backend != "gpu" or os.environ.get("HIPZAP_WATCHDOG", "1") == "0":
+            return None
+        if self._watchdog is None:
+            from ..utils.watchdog import DeviceWatchdog
+            self._watchdog = DeviceWatchdog(self._devices(), interval_s=float(os.environ.get("HIPZAP_WATCHDOG_S", 5)))
+            self._watchdog.start()
+        return self._watchdog
+
+    def _devices(self) -> list[str]:
+        if self.backend != "gpu":
+            return ["cpu"]
+        return [f"cuda:{d}" for d in self.settings.devices]
+
+    def _load(self, name: str, cls):
         with self._lock:
             if name not in self._models:
                 spec = self.spec(name)
                 sd = self._load_sd(spec)
-                self._models[name] = VisionBackend(spec.name, sd, self.backend, self.device, spec,
-                                                   self.settings.capture_graphs)
+                maybe_fault("load")
+                devs = self._devices()
+                with trace_range(f"cold_start:{name}"):
+                    bes = [cls(spec.name, sd, self.backend, dev, spec, self.settings.capture_graphs) for dev in devs]
+                wd = self.watchdog()
+                healthy = (lambda d: wd.healthy.get(d, True)) if wd is not None else None
+                self._models[name] = bes[0] if len(bes) == 1 else RoundRobin(bes, devs, healthy)
                 self.stats["cold_loads"] += 1
             return self._models[name]
+
+    def vision(self, name: str):
+        return self._load(name, VisionBackend)
+
+    def text(self, name: str):
+        return self._load(name, TextBackend)
 
     def lm(self) -> LMBackend:
         key = "__lm__"

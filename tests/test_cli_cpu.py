@@ -69,3 +69,38 @@ def test_cli_pack_and_info(tmp_path, capsys):
     assert out["entries"] > 10
     main(["info"])
     assert "resnet50" in capsys.readouterr().out
+
+
+def test_watchdog_and_fault_injection(monkeypatch):
+    import pytest as _pt
+
+    from hipzap.serve.server import RoundRobin
+    from hipzap.utils.watchdog import DeviceWatchdog, InjectedFault, maybe_fault
+    state = {"a": True, "b": False}
+    wd = DeviceWatchdog(["a", "b"], timeout_s=0.05, probe=lambda d: (lambda: state[d]))
+    assert wd.check_once() == {"a": True, "b": False} and wd.healthy_devices() == ["a"]
+
+    class B:
+        backend, cold_ms = "gpu", 1.0
+
+        def __init__(self, tag):
+            self.tag = tag
+
+        def __call__(self):
+            return self.tag
+    rr = RoundRobin([B("a"), B("b")], ["a", "b"], lambda d: wd.healthy[d])
+    assert [rr() for _ in range(4)] == ["a"] * 4  # unhealthy replica skipped
+    monkeypatch.setenv("HIPZAP_FAULT", "load,rank3")
+    with _pt.raises(InjectedFault):
+        maybe_fault("rank3")
+    maybe_fault("infer")
+
+
+def test_tracing_ranges():
+    from hipzap.utils.tracing import PhaseTimer, trace_range
+    t = PhaseTimer()
+    with trace_range("a", t):
+        pass
+    with trace_range("b", t):
+        pass
+    assert set(t.phases) == {"a", "b"} and "a=" in t.header()

@@ -124,3 +124,12 @@ def test_environ_multivalue_query():
     env = event_to_environ({"httpMethod": "GET", "path": "/x",
                             "multiValueQueryStringParameters": {"a": ["1", "2"]}, "headers": {}})
     assert env["QUERY_STRING"] == "a=1&a=2"
+
+
+def test_predict_text_bert(client):
+    r = client.post("/predict", json={"model": "bert-base", "input_ids": [[101, 2023, 2003, 102]],
+                                      "attention_mask": [[1, 1, 1, 1]]})
+    assert r.status_code == 200, r.data
+    body = r.json
+    assert body["model"] == "bert-base" and len(body["probs"][0]) == 2
+    assert abs(sum(body["probs"][0]) - 1.0) < 1e-4
