@@ -77,7 +77,8 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const H
       const int ow = hw - oh * p.Q;
       pih[f] = oh * p.stride - p.pad;
       piw[f] = ow * p.stride - p.pad;
-      pb[f] = nbase;
+      // FAST: fold the pixel's own (ih0, iw0) into the base; the per-step offset is uniform
+      pb[f] = FAST ? nbase + pih[f] * p.W + piw[f] : nbase;
     }
   }
   const bf16_t* __restrict__ X = p.x;
@@ -91,6 +92,19 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const H
 #pragma unroll
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Running (r, s, channel-block) position of the next K-step to load. load_step is called with
+  // strictly increasing t (prologue, then t+DEPTH), so the im2col decomposition advances
+  // incrementally instead of two runtime divisions per step (the first PMC profile showed
+  // SALU instructions at 37x the MFMA count, mostly those divisions).
+  const int CB = C >> 5;
+  int cur_cb = 0, cur_r = 0, cur_s = 0;
+  if constexpr (FAST && !XROW) {
+    const int k0 = s_begin * 32;
+    const int rs0 = k0 / C;
+    cur_cb = (k0 - rs0 * C) >> 5;
+    cur_r = rs0 / p.S;
+    cur_s = rs0 - cur_r * p.S;
+  }
   auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP]) {
     const int s_idx = s_begin + t;
     const int k = s_idx * 32;
@@ -105,8 +119,14 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const H
         else b[j] = bf16x8{};
       }
     } else if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
-      const int rs = k / C;
-      const int cb = (k - rs * C) >> 5;
+      const int cb = cur_cb, r = cur_r, s = cur_s;
+      if (++cur_cb == CB) {  // advance the running position (scalar, wave-uniform)
+        cur_cb = 0;
+        if (++cur_s == p.S) {
+          cur_s = 0;
+          ++cur_r;
+        }
+      }
       if constexpr (IS1X1) {
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
@@ -114,13 +134,11 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const H
           else b[j] = bf16x8{};
         }
       } else {
-        const int r = rs / p.S;
-        const int s = rs - r * p.S;
+        const int uoff = cb * HW + r * p.W + s;  // wave-uniform part of the pixel offset
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
-          const int ih = pih[j] + r, iw = piw[j] + s;
-          const bool v = pval[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-          if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + cb * HW + ih * p.W + iw) << 5) + lk);
+          const bool v = pval[j] && (unsigned)(pih[j] + r) < (unsigned)p.H && (unsigned)(piw[j] + s) < (unsigned)p.W;
+          if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + uoff) << 5) + lk);
           else b[j] = bf16x8{};
         }
       }
