@@ -265,6 +265,7 @@ int launch(const HzConvParams& p, hipStream_t st) {
 // cfg = fci*3 + fpi with FC = 1<<fci, FP = 1<<fpi (1, 2, 4); waves per workgroup = p->kw.
 // Mirrored by hipzap/ops/conv.py (TILES).
 extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
+  if (cfg >= 16) return hz_gemm_lds_launch(pp, cfg, st);
   const HzConvParams& p = *pp;
   if (p.Cout % 4 != 0 || p.C % 8 != 0) return -1;
   if (!p.x_rowmajor && p.C % 32 != 0 && p.C > 16) return -1;

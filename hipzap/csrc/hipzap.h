@@ -25,8 +25,10 @@ typedef struct HzConvParams {
   int kw;                    // waves per workgroup splitting K
 } HzConvParams;
 
-// cfg: output tile (FC*16 channels x FP*16 pixels), cfg = log2(FC)*3 + log2(FP)
+// cfg 0..8: register-ring tile (FC*16 channels x FP*16 pixels), cfg = log2(FC)*3 + log2(FP);
+// cfg 16..19: LDS-tiled GEMM (gemm.hip; row-major activations, K % 64 == 0, weight rows % 128 == 0)
 int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t st);
+int hz_gemm_lds_launch(const HzConvParams* p, int cfg, hipStream_t st);
 
 typedef struct HzPoolParams {
   const unsigned short* x;  // NHWC bf16

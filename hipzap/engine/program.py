@@ -67,7 +67,7 @@ class ExecContext:
             if n.attrs.get("cfg") is not None:
                 cfg, kw = n.attrs["cfg"], n.attrs.get("kw", 1)
             else:
-                cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key)
+                cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=pc)
             conv_plans.append((cfg, kw, key))
         # host_io: the request's PCIe transfers are part of the program (and of the graph):
         # pinned host inputs -> device inputs ... device output -> pinned host output.

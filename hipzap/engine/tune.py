@@ -29,9 +29,17 @@ REPS = 16
 
 
 def conv_shapes(graph, params) -> dict:
-    """key -> (PackedConv, (n,h,w), M, has_residual, act, out_f32) per distinct conv shape."""
+    """key -> (PackedConv, (n,h,w), M, has_residual, act, out_f32, rowmajor) per distinct conv /
+    bf16 GEMM shape (GEMM keys carry the ``r`` prefix ExecContext looks up)."""
     out = {}
     for n in graph.nodes:
+        if n.kind == "gemm":
+            pc = params[n.attrs["w"]]
+            M = n.attrs["rows"]
+            out.setdefault("r" + conv_ops.conv_key(M, pc), (pc, (M, 1, 1), M, len(n.inputs) > 1,
+                                                            n.attrs.get("act", "none"), n.attrs.get("out_f32", False),
+                                                            True))
+            continue
         if n.kind != "conv":
             continue
         pc = params[n.attrs["w"]]
@@ -40,7 +48,7 @@ def conv_shapes(graph, params) -> dict:
         q = (w + 2 * pc.pad - pc.s) // pc.stride + 1
         M = nb * p * q
         out.setdefault(conv_ops.conv_key(M, pc), (pc, (nb, h, w), M, len(n.inputs) > 1, n.attrs.get("act", "relu"),
-                                                  n.attrs.get("out_f32", False)))
+                                                  n.attrs.get("out_f32", False), False))
     return out
 
 
@@ -55,14 +63,14 @@ def _capture(lib, prm, cfg, stream):
 def _time_candidate(lib, shape, cand, bufs, streams, concurrent: int) -> float:
     """Median-of-3 us per launch; with ``concurrent`` > 1, that many independent copies run
     on separate streams (throughput under request concurrency)."""
-    pc, (nb, h, w), M, res, act, out_f32 = shape
+    pc, (nb, h, w), M, res, act, out_f32, rowmajor = shape
     cfg, kw = cand
     progs = []
     try:
         for c in range(concurrent):
             x, r, o = bufs[c]
             prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0,
-                                             act, out_f32, cfg, kw)
+                                             act, out_f32, cfg, kw, out_rowmajor=rowmajor, x_rowmajor=rowmajor)
             if lib.hz_conv_launch(C.byref(prm), cfg, streams[c].cuda_stream) != 0:
                 return float("inf")
             progs.append(_capture(lib, prm, cfg, streams[c]))
@@ -89,7 +97,7 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
     with torch.cuda.device(dev):
         streams = [torch.cuda.Stream(dev) for _ in range(concurrent)]
         for key, shape in conv_shapes(graph, params).items():
-            pc, (nb, h, w), M, res, act, out_f32 = shape
+            pc, (nb, h, w), M, res, act, out_f32, rowmajor = shape
             bufs = []
             for _ in range(concurrent):
                 x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
@@ -97,11 +105,11 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
                 o = torch.empty(M * pc.cout, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
                 bufs.append((x, r, o))
             times = []
-            for cand in conv_ops.candidates(M, pc.cout, pc.K):
+            for cand in conv_ops.candidates(M, pc.cout, pc.K, rowmajor, pc):
                 times.append((_time_candidate(lib, shape, cand, bufs, streams, concurrent), cand))
             times.sort()
             best_t, best = times[0]
-            heur = conv_ops.choose_config(M, pc.cout, pc.K)
+            heur = conv_ops.choose_config(M, pc.cout, pc.K, rowmajor=rowmajor, pc=pc)
             heur_t = next((t for t, c in times if tuple(c) == tuple(heur)), None)
             table[key] = list(best)
             report[key] = {"best_us": round(best_t, 2), "best": list(best), "heuristic": list(heur),
@@ -132,6 +140,8 @@ def main():
     # random weights of the real shapes are enough for timing
     params = {}
     for k, v in meta.items():
+        if not isinstance(v, conv_ops.PackedConv):
+            continue
         params[k] = conv_ops.PackedConv((torch.randn(v.wf.shape, device=dev) * 0.02).to(torch.bfloat16),
                                         torch.zeros(v.bias.shape, device=dev), v.cin, v.cout, v.r, v.s, v.stride,
                                         v.pad)

@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from ..engine.graph import Graph
-from ..ops.conv import pack_matrix
+from ..ops.conv import GEMM_ROW_PAD, pack_matrix
 from ..ops.transformer import NormParams
 
 
@@ -18,7 +18,7 @@ def pack_linear_padded(weight: torch.Tensor, bias: torch.Tensor | None, out_mult
     if npad != n:
         w = torch.cat([w, w.new_zeros(npad - n, w.shape[1])])
         b = torch.cat([b, b.new_zeros(npad - n)])
-    return pack_matrix(w, b, w.shape[1])
+    return pack_matrix(w, b, w.shape[1], row_pad=GEMM_ROW_PAD)
 
 
 def pack_qkv(q_w, q_b, k_w, k_b, v_w, v_b):

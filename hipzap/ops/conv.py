@@ -19,7 +19,10 @@ import torch
 from .. import _native as N
 
 TILES = [(fc, fp) for fc in (1, 2, 4) for fp in (1, 2, 4)]  # cfg index -> (FC, FP)
-ROW_PAD = 64
+ROW_PAD = 64        # conv weights: rows padded to the largest register-ring tile (64 channels)
+GEMM_ROW_PAD = 128  # linear weights: rows padded to the largest LDS-tiled GEMM tile (csrc/gemm.hip)
+# cfg >= 16: LDS-tiled GEMM (csrc/gemm.hip), row-major activations, K % 64 == 0 -> (BM, BN)
+LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64)}
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
 
@@ -72,10 +75,10 @@ def fragment_major(w2d: torch.Tensor) -> torch.Tensor:
 
 
 def pack_matrix(w2d: torch.Tensor, bias: torch.Tensor, cin: int, r: int = 1, s: int = 1, stride: int = 1,
-                pad: int = 0) -> PackedConv:
+                pad: int = 0, row_pad: int = ROW_PAD) -> PackedConv:
     cout, K = w2d.shape
     ksteps = int(math.ceil(K / 32))
-    rows = int(math.ceil(cout / ROW_PAD) * ROW_PAD)
+    rows = int(math.ceil(cout / row_pad) * row_pad)
     wp = torch.zeros(rows, ksteps * 32, dtype=torch.bfloat16, device=w2d.device)
     wp[:cout, :K] = w2d.to(torch.bfloat16)
     return PackedConv(fragment_major(wp).contiguous(), bias.float().contiguous(), cin, cout, r, s, stride, pad)
@@ -95,7 +98,7 @@ def pack_linear(weight, bias=None) -> PackedConv:
     b = bias if bias is not None else torch.zeros(weight.shape[0], device=weight.device)
     cin = weight.shape[1]
     assert cin % 8 == 0
-    return pack_matrix(weight.detach().float(), b.detach().float(), cin)
+    return pack_matrix(weight.detach().float(), b.detach().float(), cin, row_pad=GEMM_ROW_PAD)
 
 
 # ----------------------------------------------------------------------------- layouts
@@ -129,19 +132,34 @@ def cfg_of(fc: int, fp: int) -> int:
 
 
 def tile_of(cfg: int) -> tuple[int, int]:
+    """(channels, pixels) of one output tile."""
+    if cfg in LDS_TILES:
+        bm, bn = LDS_TILES[cfg]
+        return bn, bm
     fc, fp = TILES[cfg]
     return fc * 16, fp * 16
 
 
+def lds_ok(M: int, K: int, rowmajor: bool, pc: PackedConv | None = None) -> bool:
+    """Can the LDS-tiled GEMM run this shape? (row-major activations, K % 64, rows padded to 128)."""
+    if not rowmajor or K % 64 or M < 64:
+        return False
+    return pc is None or (pc.wf.shape[0] % (GEMM_ROW_PAD // 16) == 0 and pc.ksteps * 32 == K)
+
+
 def legal(cfg: int, kw: int) -> bool:
+    if cfg in LDS_TILES:
+        return kw == 1
     fc, fp = TILES[cfg]
     return 1 <= kw <= 16 and kw * fc * fp <= 64 and 64 * kw <= max_threads(fc * fp)
 
 
-def candidates(M: int, cout: int, K: int) -> list[tuple[int, int]]:
-    """All legal (cfg, kw) launch choices worth timing for one conv shape."""
+def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv | None = None) -> list[tuple[int, int]]:
+    """All legal (cfg, kw) launch choices worth timing for one conv / GEMM shape."""
     steps = max(1, math.ceil(K / 32))
     out = []
+    if lds_ok(M, K, rowmajor, pc):
+        out += [(cfg, 1) for cfg in LDS_TILES]
     for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue
@@ -152,7 +170,8 @@ def candidates(M: int, cout: int, K: int) -> list[tuple[int, int]]:
     return out
 
 
-def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str | None = None):
+def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str | None = None,
+                  rowmajor: bool = False, pc: PackedConv | None = None):
     """Pick (cfg, kw) for an implicit GEMM of M pixels x cout channels x K.
 
     A measured table (``tuned``, produced on the GPU by ``hipzap.engine.tune``) wins. The
@@ -162,7 +181,15 @@ def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str
     """
     if tuned is not None and key is not None and key in tuned:
         v = tuned[key]
-        return int(v[0]), int(v[1])
+        if int(v[0]) not in LDS_TILES or lds_ok(M, K, rowmajor, pc):
+            return int(v[0]), int(v[1])
+    if lds_ok(M, K, rowmajor, pc) and M >= 512:
+        # large-M GEMM: the biggest LDS tile that still gives every CU a workgroup
+        for cfg in (16, 17, 18, 19):
+            bm, bn = LDS_TILES[cfg]
+            if math.ceil(M / bm) * math.ceil(cout / bn) >= NUM_CUS:
+                return cfg, 1
+        return 19, 1
     steps = max(1, math.ceil(K / 32))
     fc, fp = 1, 1
     full = []
@@ -207,7 +234,9 @@ def linear(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None = None
     """Eager GEMM: y[M,N] = act(x[M,K] @ W^T + b (+ residual)); x row-major (stride ``ldx``)."""
     M = rows if rows is not None else x.shape[0]
     if cfg is None:
-        cfg, kw = choose_config(M, pc.cout, pc.K)
+        cfg, kw = choose_config(M, pc.cout, pc.K, rowmajor=True, pc=pc)
+    if cfg in LDS_TILES:
+        assert lds_ok(M, pc.K, True, pc) and (ldx if ldx is not None else x.stride(0)) % 8 == 0
     kw = kw or 1
     if out is None:
         out = torch.empty(M, pc.cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)

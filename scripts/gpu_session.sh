@@ -23,6 +23,12 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
   step tune 900 python -m hipzap.engine.tune --model ${TUNE_MODEL:-resnet50} --batch ${TUNE_BATCH:-1} --concurrent ${TUNE_CONC:-1 8} --report $OUT/tune_report.json
   mkdir -p $OUT/tuning && cp hipzap/tuning/*.json $OUT/tuning/
 }
+[[ $STEPS == *txtune* ]] && {
+  step txtune_bert 600 python -m hipzap.engine.tune --model bert-base --batch 16 --report $OUT/tune_bert.json
+  step txtune_vit 600 python -m hipzap.engine.tune --model vit-b16 --batch 8 --report $OUT/tune_vit.json
+  mkdir -p $OUT/tuning && cp hipzap/tuning/*.json $OUT/tuning/
+}
+[[ $STEPS == *models* ]] && step bench_models 900 python scripts/bench_models.py
 [[ $STEPS == *bench* || $STEPS == all ]] && {
   for s in ${BENCH_STREAMS:-1 4 8}; do
     step bench_s$s 300 python bench.py --streams $s --steps 300 --warmup 30 --cold-runs 2 ${BENCH_EXTRA:-}

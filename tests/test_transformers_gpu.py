@@ -56,6 +56,24 @@ def test_linear_gemm(M, N, K, act):
     assert _rel(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("cfg", sorted(C.LDS_TILES))
+@pytest.mark.parametrize("M,N,K,act,res", [(2048, 768, 3072, "none", True), (1576, 3072, 768, "gelu", False),
+                                            (200, 1000, 512, "relu", True), (64, 132, 64, "none", False)])
+def test_lds_gemm(cfg, M, N, K, act, res):
+    """LDS-tiled GEMM (csrc/gemm.hip) vs fp32: ragged M and N tails, all tiles."""
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(N, K, generator=g) * 0.03
+    b = torch.randn(N, generator=g)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    r = torch.randn(M, N, generator=g).to(torch.bfloat16) if res else None
+    pc = C.pack_linear(w, b).to(DEV)
+    assert C.lds_ok(M, K, True, pc)
+    y = C.linear(x.to(DEV), pc, residual=None if r is None else r.to(DEV), act=act, cfg=cfg, kw=1)
+    ref = x.float() @ w.to(torch.bfloat16).float().t() + b + (r.float() if res else 0)
+    ref = {"gelu": torch.nn.functional.gelu, "relu": torch.relu}.get(act, lambda t: t)(ref)
+    assert _rel(y, ref) < 2e-2
+
+
 def test_bert_engine_matches_hf():
     torch.manual_seed(0)
     m = bert.make_model(num_labels=2)
