@@ -17,11 +17,6 @@ namespace {
 constexpr float FP8_MAX = 448.f;
 constexpr int QCH = 8;  // 16-B chunks per lane: rows up to 64*8*8 = 4096 elements
 
-__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  return (unsigned)w;
-}
 
 __global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) {
   const int lane = threadIdx.x & 63;

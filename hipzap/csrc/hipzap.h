@@ -115,6 +115,8 @@ typedef struct HzLayerNormParams {
   const float* beta;
   int rows, D, ldx, ldr, ldo;
   float eps;
+  unsigned char* out8;        // optional fused per-row fp8 quantisation of the output [rows][D]
+  float* scale8;              //   and its row scales (amax / 448); out may then be NULL
 } HzLayerNormParams;
 typedef struct HzEmbedParams {
   const int* ids;             // [rows] token ids (rows = B*L)

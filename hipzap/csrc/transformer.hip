@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams 
     }
   }
   const float rstd = rsqrtf(warp_sum(q) / p.D + p.eps);
-  bf16_t* o = p.out + (long)row * p.ldo;
+  float amax = 0.f;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int ch = c * 64 + lane;
@@ -62,15 +62,32 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams 
       const f32x4 g1 = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8 + 4);
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.beta + ch * 8);
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.beta + ch * 8 + 4);
-      float y[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        y[e] = (v[c][e] - mean) * rstd * g0[e] + b0[e];
-        y[e + 4] = (v[c][e + 4] - mean) * rstd * g1[e] + b1[e];
+        v[c][e] = (v[c][e] - mean) * rstd * g0[e] + b0[e];
+        v[c][e + 4] = (v[c][e + 4] - mean) * rstd * g1[e] + b1[e];
       }
-      *reinterpret_cast<u32x4*>(o + ch * 8) = pack8(y);
+      if (p.out) *reinterpret_cast<u32x4*>(p.out + (long)row * p.ldo + ch * 8) = pack8(v[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
     }
   }
+  if (!p.out8) return;
+  // fused fp8 quantisation (same rule as fp8.hip quant_rows: s = amax / 448, e4m3fn)
+  amax = warp_max(amax);
+  const float scale = fmaxf(amax, 1e-12f) / 448.f, inv = 1.f / scale;
+  unsigned char* o8 = p.out8 + (long)row * p.D;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = c * 64 + lane;
+    if (ch < nch) {
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = fminf(fmaxf(v[c][e] * inv, -448.f), 448.f);
+      *reinterpret_cast<u32x2*>(o8 + ch * 8) = u32x2{pack4_fp8(q[0], q[1], q[2], q[3]), pack4_fp8(q[4], q[5], q[6], q[7])};
+    }
+  }
+  if (lane == 0) p.scale8[row] = scale;
 }
 
 // --------------------------------------------------------------------------- BERT embeddings

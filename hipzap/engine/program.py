@@ -157,9 +157,11 @@ class ExecContext:
             npar = self.params[n.attrs["p"]]
             res = n.inputs[1] if len(n.inputs) > 1 else None
             D = g.shape(n.outputs[0])[-1]
-            prm = tx.LayerNormParams(addr(n.inputs[0]), addr(res), addr(n.outputs[0]), npar.gamma.data_ptr(),
-                                     npar.beta.data_ptr(), n.attrs["rows"], D, n.attrs.get("ldx") or D, D, D,
-                                     npar.eps)
+            q8 = g.tensors[n.outputs[0]].dtype == torch.uint8  # fused fp8 quantisation: outputs (x8, scales)
+            prm = tx.LayerNormParams(addr(n.inputs[0]), addr(res), 0 if q8 else addr(n.outputs[0]),
+                                     npar.gamma.data_ptr(), npar.beta.data_ptr(), n.attrs["rows"], D,
+                                     n.attrs.get("ldx") or D, D, D, npar.eps, addr(n.outputs[0]) if q8 else 0,
+                                     addr(n.outputs[1]) if q8 else 0)
             tx.prog_add(self.prog, tx.K_LAYERNORM, prm, n.slot)
         elif n.kind == "attention":
             a = n.attrs

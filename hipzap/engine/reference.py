@@ -101,7 +101,13 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             xm = torch.stack([x[r * ldx: r * ldx + D] for r in range(rows)])
             if len(n.inputs) > 1:
                 xm = xm + vals[n.inputs[1]].float().reshape(rows, D)
-            store(n.outputs[0], F.layer_norm(xm, (D,), npar.gamma.float(), npar.beta.float(), npar.eps))
+            y = F.layer_norm(xm, (D,), npar.gamma.float(), npar.beta.float(), npar.eps)
+            if g.tensors[n.outputs[0]].dtype == torch.uint8:  # fused fp8 quantisation
+                from ..ops.fp8 import quant_rows_ref
+                deq, s = quant_rows_ref(y.to(torch.bfloat16))
+                vals[n.outputs[0]], vals[n.outputs[1]] = deq, s
+            else:
+                store(n.outputs[0], y)
         elif k == "attention":
             a = n.attrs
             mask = vals[n.inputs[1]] if len(n.inputs) > 1 else None

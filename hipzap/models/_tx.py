@@ -51,10 +51,7 @@ class TxBuilder:
         x8 = g.tensor((r, k), torch.uint8, f"{w}.x8")
         sx = g.tensor((r,), torch.float32, f"{w}.sx")
         g.add("quant", [x], [x8, sx])
-        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
-        ins = [x8, sx] if res is None else [x8, sx, res]
-        g.add("gemm_fp8", ins, [out], w=w, act=act, rows=r, out_f32=out_f32, name=name or w)
-        return out
+        return self.gemm8q((x8, sx), w, cols, act=act, res=res, out_f32=out_f32, ext=ext, name=name)
 
     def linear(self, x, w: str, cols: int, fp8: bool = False, **kw):
         return self.gemm8(x, w, cols, **kw) if fp8 else self.gemm(x, w, cols, **kw)
@@ -65,6 +62,26 @@ class TxBuilder:
         out = g.tensor((r, g.shape(x)[1]), torch.bfloat16, name or p)
         ins = [x] if res is None else [x, res]
         g.add("layernorm", ins, [out], p=p, rows=r, ldx=ldx)
+        return out
+
+    def layernorm_q8(self, x, p: str, res=None):
+        """LayerNorm whose output is consumed only by fp8 GEMMs: fused per-row fp8 quantisation."""
+        g = self.g
+        r, d = g.shape(x)
+        x8 = g.tensor((r, d), torch.uint8, f"{p}.x8")
+        sx = g.tensor((r,), torch.float32, f"{p}.sx")
+        ins = [x] if res is None else [x, res]
+        g.add("layernorm", ins, [x8, sx], p=p, rows=r, ldx=None)
+        return x8, sx
+
+    def gemm8q(self, xq, w: str, cols: int, act="none", res=None, out_f32=False, ext=False, name=None):
+        """fp8 GEMM on an already-quantised input ``xq = (x8, scales)``."""
+        g = self.g
+        x8, sx = xq
+        r = g.shape(x8)[0]
+        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
+        ins = [x8, sx] if res is None else [x8, sx, res]
+        g.add("gemm_fp8", ins, [out], w=w, act=act, rows=r, out_f32=out_f32, name=name or w)
         return out
 
     def attention(self, qkv, B, L, heads, mask=None):

@@ -100,12 +100,16 @@ def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12
     f8 = weights == "fp8"
     x = tok
     for i in range(layers):
-        h = tb.layernorm(x, f"l{i}.ln1")
-        qkv = tb.linear(h, f"l{i}.qkv", 3 * D, fp8=f8)
+        if f8:  # pre-LN: the LN outputs feed only fp8 GEMMs -> quantise inside the LayerNorm
+            qkv = tb.gemm8q(tb.layernorm_q8(x, f"l{i}.ln1"), f"l{i}.qkv", 3 * D)
+        else:
+            qkv = tb.gemm(tb.layernorm(x, f"l{i}.ln1"), f"l{i}.qkv", 3 * D)
         ctx = tb.attention(qkv, B, T, heads)
         x2 = tb.linear(ctx, f"l{i}.o", D, fp8=f8, res=x)
-        h2 = tb.layernorm(x2, f"l{i}.ln2")
-        f = tb.linear(h2, f"l{i}.fc1", ffn, fp8=f8, act="gelu")
+        if f8:
+            f = tb.gemm8q(tb.layernorm_q8(x2, f"l{i}.ln2"), f"l{i}.fc1", ffn, act="gelu")
+        else:
+            f = tb.gemm(tb.layernorm(x2, f"l{i}.ln2"), f"l{i}.fc1", ffn, act="gelu")
         x = tb.linear(f, f"l{i}.fc2", D, fp8=f8, res=x2)
     cls = tb.layernorm(x, "final_ln", rows=B, ldx=T * D, name="cls_ln")
     npad = (num_labels + 3) // 4 * 4

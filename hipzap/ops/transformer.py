@@ -16,7 +16,7 @@ K_LAYERNORM, K_EMBED, K_ATTENTION, K_VIT_TOKENS = 2, 3, 4, 5
 class LayerNormParams(C.Structure):
     _fields_ = [("x", C.c_void_p), ("res", C.c_void_p), ("out", C.c_void_p), ("gamma", C.c_void_p),
                 ("beta", C.c_void_p), ("rows", C.c_int), ("D", C.c_int), ("ldx", C.c_int), ("ldr", C.c_int),
-                ("ldo", C.c_int), ("eps", C.c_float)]
+                ("ldo", C.c_int), ("eps", C.c_float), ("out8", C.c_void_p), ("scale8", C.c_void_p)]
 
 
 class EmbedParams(C.Structure):
@@ -74,6 +74,20 @@ def layernorm(x: torch.Tensor, np_: NormParams, residual: torch.Tensor | None = 
                           np_.eps)
     launch(K_LAYERNORM, prm)
     return out
+
+
+def layernorm_q8(x: torch.Tensor, np_: NormParams, residual: torch.Tensor | None = None, keep_bf16: bool = False):
+    """LayerNorm with the per-row fp8 quantisation of its output fused in:
+    returns (x8 uint8 [rows, D], row scales fp32 [rows]) and, with ``keep_bf16``, the bf16 output."""
+    rows, D = x.shape
+    out = torch.empty_like(x) if keep_bf16 else None
+    x8 = torch.empty(rows, D, dtype=torch.uint8, device=x.device)
+    sx = torch.empty(rows, dtype=torch.float32, device=x.device)
+    prm = LayerNormParams(x.data_ptr(), N.ptr(residual), N.ptr(out), np_.gamma.data_ptr(), np_.beta.data_ptr(),
+                          rows, D, x.stride(0), residual.stride(0) if residual is not None else 0, D, np_.eps,
+                          x8.data_ptr(), sx.data_ptr())
+    launch(K_LAYERNORM, prm)
+    return (x8, sx, out) if keep_bf16 else (x8, sx)
 
 
 def attention(qkv: torch.Tensor, B: int, L: int, heads: int, mask: torch.Tensor | None = None,

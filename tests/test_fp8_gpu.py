@@ -51,3 +51,19 @@ def test_vit_fp8_engine_vs_hf():
     assert rel < 0.25, rel
     cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
     assert cos.min() > 0.97, cos
+
+
+def test_layernorm_fused_fp8_quant():
+    """LayerNorm + per-row fp8 quantisation in one kernel == LN then quant_rows."""
+    from hipzap.ops import transformer as T
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(300, 768, generator=g).to(torch.bfloat16)
+    r = torch.randn(300, 768, generator=g).to(torch.bfloat16)
+    npar = T.NormParams(torch.randn(768, generator=g), torch.randn(768, generator=g), 1e-6)
+    x8, sx, y = T.layernorm_q8(x.to(DEV), npar.to(DEV), residual=r.to(DEV), keep_bf16=True)
+    ref = T.layernorm_ref(x, npar, r)
+    assert ((y.float().cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+    deq_ref, s_ref = F8.quant_rows_ref(ref)
+    assert torch.allclose(sx.cpu(), s_ref, rtol=2e-2)
+    deq = x8.cpu().view(torch.float8_e4m3fn).float() * sx.cpu()[:, None]
+    assert ((deq - deq_ref).abs().max() / deq_ref.abs().max()).item() < 5e-2
