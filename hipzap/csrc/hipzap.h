@@ -149,9 +149,20 @@ int hz_embed_ln_launch(const HzEmbedParams* p, hipStream_t st);
 int hz_attention_launch(const HzAttentionParams* p, hipStream_t st);
 int hz_vit_tokens_launch(const HzVitTokensParams* p, hipStream_t st);
 
+// row softmax: out[r][i] = exp(s*x[r][i] + mask[i] - m_r) / sum_i(...), i < D
+typedef struct HzSoftmaxParams {
+  const void* x;       // [rows][ldx] fp32 (x_bf16 = 0) or bf16
+  const float* mask;   // optional additive [D] mask
+  float* out;          // [rows][ldo] fp32
+  int rows, D, ldx, ldo, x_bf16;
+  float scale;
+} HzSoftmaxParams;
+int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t st);
+
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
-       HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11 };
+       HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
+       HZ_K_SOFTMAX = 12 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
 

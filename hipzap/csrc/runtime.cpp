@@ -241,6 +241,7 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_MAXPOOL: return hz_maxpool_launch(static_cast<const HzPoolParams*>(prm), st);
     case HZ_K_QUANT: return hz_quant_launch(static_cast<const HzQuantParams*>(prm), st);
     case HZ_K_GEMM_FP8: return hz_gemm_fp8_launch(static_cast<const HzGemmFp8Params*>(prm), st);
+    case HZ_K_SOFTMAX: return hz_softmax_launch(static_cast<const HzSoftmaxParams*>(prm), st);
     default: return -100;
   }
 }

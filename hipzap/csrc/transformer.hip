@@ -292,6 +292,36 @@ __global__ __launch_bounds__(256) void vit_tokens_kernel(const HzVitTokensParams
 
 }  // namespace
 
+// --------------------------------------------------------------------------- row softmax
+// One wave per row; the row is read twice (max/sum pass, normalise pass) — rows are classifier
+// logits or attention-score rows of <= a few thousand elements, L2-resident after the first pass.
+__global__ __launch_bounds__(256) void softmax_kernel(const HzSoftmaxParams p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  auto val = [&](int i) {
+    float v = p.x_bf16 ? bf2f(reinterpret_cast<const bf16_t*>(p.x)[(long)row * p.ldx + i])
+                       : reinterpret_cast<const float*>(p.x)[(long)row * p.ldx + i];
+    v *= p.scale;
+    return p.mask ? v + p.mask[i] : v;
+  };
+  float m = -INFINITY;
+  for (int i = lane; i < p.D; i += 64) m = fmaxf(m, val(i));
+  m = warp_max(m);
+  float s = 0.f;
+  for (int i = lane; i < p.D; i += 64) s += __expf(val(i) - m);
+  const float inv = 1.f / warp_sum(s);
+  float* o = p.out + (long)row * p.ldo;
+  for (int i = lane; i < p.D; i += 64) o[i] = __expf(val(i) - m) * inv;
+}
+
+extern "C" int hz_softmax_launch(const HzSoftmaxParams* pp, hipStream_t st) {
+  const HzSoftmaxParams& p = *pp;
+  if (p.D < 1 || p.rows < 1) return -1;
+  hipLaunchKernelGGL(softmax_kernel, dim3((p.rows + 3) / 4), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
 extern "C" int hz_layernorm_launch(const HzLayerNormParams* pp, hipStream_t st) {
   const HzLayerNormParams& p = *pp;
   if (p.D % 8 || p.D > 2048) return -1;

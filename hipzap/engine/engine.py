@@ -33,10 +33,22 @@ def load_tuning(model: str, batch: int, contexts: int = 1) -> dict | None:
     return None
 
 
+def add_softmax_head(g) -> None:
+    """Append a row softmax (csrc/transformer.hip softmax_kernel) over the logical classes of
+    the graph's logits so the request returns probabilities (``/predict`` with probs)."""
+    out = g.outputs[0]
+    shape = g.shape(out)
+    rows, cols = shape[0], int(torch.tensor(shape[1:]).prod()) if len(shape) > 1 else 1
+    D = (getattr(g, "meta", None) or {}).get("num_labels", cols)
+    probs = g.tensor((rows, D), torch.float32, "probs", external=True)
+    g.add("softmax", [out], [probs], D=D)
+    g.outputs[0] = probs
+
+
 class Engine:
     def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
                  capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
-                 host_io: bool = True):
+                 host_io: bool = True, probs: bool = False):
         self.model = model
         self.adapter = registry.get(model)
         self.device = torch.device(device)
@@ -50,6 +62,8 @@ class Engine:
         t0 = time.perf_counter()
         with torch.cuda.device(self.device):
             self.graph = self.adapter.build_graph(batch=batch, **self.arch_kw)
+            if probs:
+                add_softmax_head(self.graph)
             self.host_io = host_io
             self.contexts = [ExecContext(self.graph, params, self.device, tuned, host_io=host_io)
                              for _ in range(num_contexts)]

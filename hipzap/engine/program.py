@@ -184,6 +184,14 @@ class ExecContext:
             prm = tx.VitTokensParams(addr(n.inputs[0]), self.params[a["cls"]].data_ptr(),
                                      self.params[a["pos"]].data_ptr(), addr(n.outputs[0]), a["B"], a["np"], D)
             tx.prog_add(self.prog, tx.K_VIT_TOKENS, prm, n.slot)
+        elif n.kind == "softmax":
+            ishape = g.shape(n.inputs[0])
+            rows, ld = ishape[0], int(torch.tensor(ishape[1:]).prod())
+            src = g.tensors[n.inputs[0]]
+            D = n.attrs.get("D") or ld
+            prm = tx.SoftmaxParams(addr(n.inputs[0]), 0, addr(n.outputs[0]), rows, D, ld, g.shape(n.outputs[0])[-1],
+                                   int(src.dtype == torch.bfloat16), float(n.attrs.get("scale", 1.0)))
+            tx.prog_add(self.prog, tx.K_SOFTMAX, prm, n.slot)
         elif n.kind == "fork":
             N.check(lib.hz_prog_add_fork(self.prog, n.slot), "fork")
         elif n.kind == "join":

@@ -11,6 +11,12 @@ import torch.nn.functional as F
 from .. import _native as N
 
 K_LAYERNORM, K_EMBED, K_ATTENTION, K_VIT_TOKENS = 2, 3, 4, 5
+K_SOFTMAX = 12
+
+
+class SoftmaxParams(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("mask", C.c_void_p), ("out", C.c_void_p), ("rows", C.c_int), ("D", C.c_int),
+                ("ldx", C.c_int), ("ldo", C.c_int), ("x_bf16", C.c_int), ("scale", C.c_float)]
 
 
 class LayerNormParams(C.Structure):
@@ -88,6 +94,27 @@ def layernorm_q8(x: torch.Tensor, np_: NormParams, residual: torch.Tensor | None
                           x8.data_ptr(), sx.data_ptr())
     launch(K_LAYERNORM, prm)
     return (x8, sx, out) if keep_bf16 else (x8, sx)
+
+
+def softmax(x: torch.Tensor, cols: int | None = None, scale: float = 1.0, mask: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """Row softmax over the first ``cols`` columns of a 2-D fp32/bf16 tensor -> fp32."""
+    rows, ld = x.shape
+    D = cols or ld
+    assert x.dtype in (torch.float32, torch.bfloat16) and x.stride(1) == 1
+    out = out if out is not None else torch.empty(rows, D, device=x.device, dtype=torch.float32)
+    prm = SoftmaxParams(x.data_ptr(), N.ptr(mask), out.data_ptr(), rows, D, x.stride(0), out.stride(0),
+                        int(x.dtype == torch.bfloat16), scale)
+    launch(K_SOFTMAX, prm)
+    return out
+
+
+def softmax_ref(x: torch.Tensor, cols: int | None = None, scale: float = 1.0, mask=None) -> torch.Tensor:
+    D = cols or x.shape[-1]
+    v = x[..., :D].float() * scale
+    if mask is not None:
+        v = v + mask.float()
+    return torch.softmax(v, dim=-1)
 
 
 def attention(qkv: torch.Tensor, B: int, L: int, heads: int, mask: torch.Tensor | None = None,

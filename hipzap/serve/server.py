@@ -42,10 +42,12 @@ class VisionBackend:
         self.name, self.backend = name, backend
         t0 = time.perf_counter()
         self.adapter = registry.get(name)
+        # "probs": true in the model's settings block -> the softmax runs on device, responses are probabilities
+        self.probs = bool(spec.extra.get("probs", False))
         if backend == "gpu":
             from ..engine.engine import Engine
             self.engine = Engine.from_state_dict(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
-                                                 capture=capture)
+                                                 capture=capture, probs=self.probs)
             self.model = None
         else:
             from ..models.resnet import infer_arch
@@ -68,7 +70,8 @@ class VisionBackend:
                 outs.append(self.engine.infer(chunk)[:n])
             return torch.cat(outs)
         with torch.no_grad():
-            return self.model(x.float())
+            y = self.model(x.float())
+            return torch.softmax(y, 1) if self.probs else y
 
 
 class TextBackend:

@@ -67,3 +67,14 @@ def test_concurrent_contexts(model_sd):
         assert torch.equal(singles[i], singles[i + 4])
     secs = eng.bench(20)
     assert secs > 0
+
+
+def test_probs_head(model_sd):
+    """Engine(probs=True): on-device softmax over the logits (csrc/transformer.hip softmax_kernel)."""
+    name, m, sd = model_sd
+    x = torch.randn(1, 3, 224, 224)
+    logits = Engine.from_state_dict(name, sd, DEV, batch=1).infer(x)
+    probs = Engine.from_state_dict(name, sd, DEV, batch=1, probs=True).infer(x)
+    assert probs.shape == logits.shape
+    assert torch.allclose(probs.sum(1), torch.ones(1), atol=1e-4)
+    assert (probs - torch.softmax(logits.float(), 1)).abs().max().item() < 1e-5

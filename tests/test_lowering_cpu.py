@@ -106,3 +106,21 @@ def test_meta_params_match_real_packing():
     assert set(meta) == set(real)
     for k in meta:
         assert meta[k].wf.shape == real[k].wf.shape and meta[k].bias.shape == real[k].bias.shape
+
+
+def test_softmax_head_oracle():
+    """Engine(probs=True) appends a row-softmax node over the logical classes."""
+    from hipzap.engine.engine import add_softmax_head
+    torch.manual_seed(0)
+    m = randomize_bn(ResNet("resnet18")).eval()
+    P = pack_resnet(m.state_dict())
+    g = build_graph("resnet18", 2)
+    logits_t = g.outputs[0]
+    add_softmax_head(g)
+    assert g.nodes[-1].kind == "softmax" and g.outputs[0] != logits_t
+    x = torch.randn(2, 3, 224, 224)
+    vals = run_graph_reference(g, P, [x], bf16_acts=False)
+    probs = vals[g.outputs[0]].reshape(2, -1)
+    assert probs.shape == (2, 1000)
+    assert torch.allclose(probs.sum(1), torch.ones(2), atol=1e-5)
+    assert torch.allclose(probs, torch.softmax(vals[logits_t].reshape(2, -1).float(), 1), atol=1e-6)

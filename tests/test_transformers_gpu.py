@@ -102,3 +102,13 @@ def test_vit_engine_matches_hf():
     assert out.shape == (2, 1000)
     assert _rel(out, ref) < 5e-2
     assert (out.argmax(1) == ref.argmax(1)).all()
+
+
+@pytest.mark.parametrize("rows,D,ld,dtype", [(8, 1000, 1000, torch.float32), (37, 197, 200, torch.bfloat16),
+                                              (1, 5, 8, torch.float32)])
+def test_softmax_rows(rows, D, ld, dtype):
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(rows, ld, generator=g) * 4).to(dtype)
+    y = T.softmax(x.to(DEV), cols=D, scale=0.5)
+    ref = T.softmax_ref(x, D, 0.5)
+    assert (y.cpu() - ref).abs().max().item() < 1e-5
