@@ -4,17 +4,19 @@
 //
 // The K-across-waves kernel (conv.hip) is right for bs=1 (every operand byte used once), but
 // at M >= ~512 each weight fragment is re-read by every M tile and each activation fragment
-// by every N tile straight from L2: per-CU load bandwidth, not MFMA, was the limit (BERT-base
-// bs=16 at ~205 TFLOP/s). Here a 256-thread workgroup (2x2 waves) owns a BM x BN tile and
-// stages BOTH operands through LDS once per 64-deep K step:
-//   * operands are staged in MFMA fragment order — weights are already packed
-//     fragment-major [N/16][K/32][64][8] (1 KiB per fragment, contiguous), activation fragments
-//     are gathered per lane (16 rows x 64 B) — with global_load_lds (16 B per lane; the LDS image
-//     is lane-linear, cdna_hip_programming.md §5 "Async global->LDS copy"), so every
-//     ds_read_b128 of a fragment is lane-linear and bank-conflict free (no swizzle needed);
-//   * each fragment read from LDS feeds 2-4 MFMAs (waves sharing a row or column of the tile);
-//   * double-buffered stages: the glds of stage t+1 is issued before the MFMAs of stage t
-//     ("Minimum 2-phase" recipe, §5.5 T3+T4), one vmcnt(0) + barrier per stage;
+// by every N tile: the per-CU load path, not the MFMA, was the limit. Here a 256-thread
+// workgroup (2x2 waves, each a (BM/2) x (BN/2) sub-tile of 16x16x32 MFMAs) owns a BM x BN
+// tile and stages BOTH operands through LDS once per 64-deep K step:
+//   * weights are packed fragment-major [N/16][K/32][64][8] (1 KiB per fragment, contiguous):
+//     one global_load_lds (16 B/lane) per fragment, lane-linear LDS image;
+//   * activations are staged in FULL 128-B lines (8 rows x 64 k per wave-instruction), not as
+//     16-row x 64-B fragments (cdna_hip_programming.md §5 "Projection GEMM": fragment-shaped x
+//     loads cost 18-45 %). The LDS image [BM][128 B] is XOR-swizzled per 16-B chunk,
+//     chunk' = chunk ^ ((row >> 1) & 7), so the 16 rows of a ds_read_b128 lane group land in
+//     16 distinct 16-B bank slots (conflict-free); glds writes lane-linearly, so the swizzle is
+//     applied to the per-lane GLOBAL source address;
+//   * 3 LDS stages, two K steps in flight: counted `s_waitcnt vmcnt(G)` + raw s_barrier (never
+//     __syncthreads(), whose fence would drain the in-flight DMA — §5 "Pipelining across barriers");
 //   * same swapped orientation and fused epilogue as conv.hip (4 consecutive output features
 //     per lane: 16-B bias, 8-B residual, 8-B store), XCD-aware tile order.
 // Requirements (checked by the launcher): K % 64 == 0, ldx % 8 == 0, weight rows padded to 128.
@@ -29,13 +31,21 @@ __device__ __forceinline__ void glds16(const void* g, char* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds, 16, 0, 0);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
-  constexpr int FCW = BN / 32, FPW = BM / 32;  // fragments per wave (2x2 waves)
-  constexpr int NWF = BN / 16, NAF = BM / 16;  // fragments per 32-deep k-step in the tile
-  constexpr int KF = NWF + NAF;
-  constexpr int STAGE_FR = 2 * KF;             // BK = 64 = two k-steps per stage
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_FR * 1024];
+  constexpr int FCW = BN / 32, FPW = BM / 32;  // 16x16 fragments per wave (2x2 waves)
+  constexpr int NWG = BN / 16;                 // weight fragments per 32-deep k-step
+  constexpr int XBYTES = BM * 128;             // activation bytes per stage (BK = 64 bf16 = 128 B)
+  constexpr int SBYTES = XBYTES + BN * 128;    // + 2 k-steps x NWG fragments x 1 KiB
+  constexpr int NS = 3;
+  constexpr int XPW = BM / 32, WPW = BN / 32;  // glds pieces per wave per stage (x, w)
+  constexpr int G = XPW + WPW;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave & 1, wm = wave >> 1;
@@ -45,24 +55,34 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   const int n0 = tile_n * BN, m0 = tile_m * BM;
   const int nst = p.ksteps >> 1;
 
-  // per-lane source row of each activation fragment this wave stages (clamped: rows >= M are
-  // computed on duplicated data and never stored)
-  auto stage = [&](int buf, int st) {
-    char* base = smem + buf * STAGE_FR * 1024;
+  // staging sources: x piece q = wave + 4i covers tile rows 8q .. 8q+7, lane -> row 8q + (lane>>3),
+  // swizzled chunk (lane&7) ^ (((q&1)<<2) + (lane>>4)); rows >= M are clamped (never stored)
+  const bf16_t* xsrc[XPW];
 #pragma unroll
-    for (int f = wave; f < STAGE_FR; f += 4) {
-      const int ks = f / KF, q = f - ks * KF;
-      const int kstep = st * 2 + ks;
-      const void* src;
-      if (q < NWF) {
-        src = p.w + (((long)((n0 >> 4) + q) * p.ksteps + kstep) * 64 + lane) * 8;
-      } else {
-        const int row = min(m0 + (q - NWF) * 16 + (lane & 15), p.M - 1);
-        src = p.x + (long)row * p.ldx + kstep * 32 + (lane >> 4) * 8;
-      }
-      glds16(src, base + f * 1024);
+  for (int i = 0; i < XPW; ++i) {
+    const int q = wave + 4 * i;
+    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
+    const int chunk = (lane & 7) ^ (((q & 1) << 2) + (lane >> 4));
+    xsrc[i] = p.x + (long)row * p.ldx + chunk * 8;
+  }
+  const bf16_t* wsrc = p.w + ((long)(n0 >> 4) * p.ksteps * 64 + lane) * 8;
+  auto stage = [&](int buf, int st) {
+    char* base = smem + buf * SBYTES;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) glds16(xsrc[i] + st * 64, base + (wave + 4 * i) * 1024);
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int f = wave + 4 * i;  // f = ks * NWG + g
+      const int ks = f / NWG, g = f - ks * NWG;
+      glds16(wsrc + ((long)g * p.ksteps + st * 2 + ks) * 512, base + XBYTES + f * 1024);
     }
   };
+
+  // reader offsets: B fragment j of k-step ks = rows wm*BM/2 + 16j + (lane&15), chunk 4ks + (lane>>4)
+  const int lr = lane & 15, sw = (lane >> 1) & 7;
+  const int boff0 = (wm * (BM / 2) + lr) * 128 + (((lane >> 4)) ^ sw) * 16;
+  const int boff1 = (wm * (BM / 2) + lr) * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 1024 + lane * 16;
 
   f32x4 acc[FCW][FPW];
 #pragma unroll
@@ -71,27 +91,29 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (nst > 1) stage(1, 1);
+  int cur = 0;
   for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
-    if (st + 1 < nst) stage(cur ^ 1, st + 1);
-    const char* base = smem + cur * STAGE_FR * 1024 + lane * 16;
+    if (st + 1 < nst) wait_vm<G>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < nst) stage(cur == 0 ? 2 : cur - 1, st + 2);
+    const char* base = smem + cur * SBYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 a[FCW], b[FPW];
 #pragma unroll
-      for (int i = 0; i < FCW; ++i) a[i] = *reinterpret_cast<const bf16x8*>(base + (ks * KF + wn * FCW + i) * 1024);
+      for (int i = 0; i < FCW; ++i) a[i] = *reinterpret_cast<const bf16x8*>(base + aoff + (ks * NWG + i) * 1024);
 #pragma unroll
       for (int j = 0; j < FPW; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(base + (ks * KF + NWF + wm * FPW + j) * 1024);
+        b[j] = *reinterpret_cast<const bf16x8*>(base + (ks ? boff1 : boff0) + j * 16 * 128);
 #pragma unroll
       for (int i = 0; i < FCW; ++i)
 #pragma unroll
         for (int j = 0; j < FPW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
   // ---- fused epilogue (row-major out) ----
