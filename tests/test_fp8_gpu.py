@@ -67,3 +67,27 @@ def test_layernorm_fused_fp8_quant():
     assert torch.allclose(sx.cpu(), s_ref, rtol=2e-2)
     deq = x8.cpu().view(torch.float8_e4m3fn).float() * sx.cpu()[:, None]
     assert ((deq - deq_ref).abs().max() / deq_ref.abs().max()).item() < 5e-2
+
+
+def _probe_f8f6f4(layout: int, A: torch.Tensor, Bt: torch.Tensor) -> torch.Tensor:
+    import ctypes
+    from hipzap import _native as N
+    ab = torch.cat([A.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1),
+                    Bt.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1)]).to(DEV)
+    c = torch.zeros(16, 16, device=DEV)
+    N.check(N.lib().hz_diag_launch(2, layout, 64, ctypes.c_void_p(ab.data_ptr()), ctypes.c_void_p(c.data_ptr()), 0,
+                                   N.stream_ptr()), "probe")
+    torch.cuda.synchronize()
+    return c.cpu()
+
+
+def test_mfma_f8f6f4_operand_layout():
+    """Pins the lane->k map of v_mfma_scale_f32_16x16x128_f8f6f4 (layout 0: lane l holds
+    k = 32*(l>>4) + j) that csrc/fp8.hip's MX GEMM relies on, with exact small integers."""
+    g = torch.Generator().manual_seed(7)
+    A = torch.randint(-3, 4, (16, 128), generator=g).float()
+    Bt = torch.randint(-3, 4, (16, 128), generator=g).float()
+    ref = A @ Bt.t()
+    got = {lay: _probe_f8f6f4(lay, A, Bt) for lay in (0, 1)}
+    match = [lay for lay, c in got.items() if torch.equal(c, ref)]
+    assert match == [0], {lay: (c - ref).abs().max().item() for lay, c in got.items()}
