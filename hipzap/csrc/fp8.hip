@@ -195,8 +195,179 @@ extern "C" int hz_quant_launch(const HzQuantParams* pp, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// --------------------------------------------------------------------------- MX fp8 LDS GEMM
+// Large-M fp8 GEMM on v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3): twice the bf16 MFMA
+// rate (MI355X_MICROARCH.md, MFMA table). The block scales are all 1.0 (E8M0 0x7f); the real
+// per-row activation and per-channel weight scales stay fp32 and are applied in the epilogue,
+// so the numerics equal the 16x16x32 fp8 kernel above. Operand map (pinned by
+// tests/test_fp8_gpu.py::test_mfma_f8f6f4_operand_layout): lane l holds row l&15,
+// k = 32*(l>>4) + j, j < 32 (32 bytes = two 16-B halves).
+//   * weights MX-packed [N/16][K/128][half][64 lanes][16 B]: a 2-KiB fragment is two lane-linear
+//     1-KiB glds pieces, and each half is read back with a conflict-free ds_read_b128;
+//   * activations (row-major fp8, 128-B rows per 128-deep k-step) staged in full 128-B lines,
+//     16-B chunks XOR-swizzled with MX_SWZ (chunk' = c ^ f((row>>1)&7), f found by exhaustive
+//     search to make the 16 rows of every ds_read_b128 lane group hit 16 distinct bank slots
+//     for this kernel's chunk pattern 2*(l>>4)+half);
+//   * 3 LDS stages, counted vmcnt + raw s_barrier, as csrc/gemm.hip.
+constexpr unsigned MX_SWZ = 0x32765410u;  // nibble i = f(i)
+__device__ __forceinline__ int mx_swz(int i) { return (MX_SWZ >> (4 * i)) & 7; }
+
+typedef __attribute__((address_space(3))) void lds_void8;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int N>
+__device__ __forceinline__ void wait_vm8() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
+  constexpr int FCW = BN / 32, FPW = BM / 32;
+  constexpr int NWG = BN / 16;                // weight fragments (2 KiB) per stage
+  constexpr int XBYTES = BM * 128;
+  constexpr int SBYTES = XBYTES + NWG * 2048;
+  constexpr int NS = 3;
+  constexpr int XPW = BM / 32, WPW = NWG * 2 / 4;  // glds pieces per wave per stage
+  constexpr int G = XPW + WPW;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 1, wm = wave >> 1;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lid % tiles_n, tile_m = lid / tiles_n;
+  const int n0 = tile_n * BN, m0 = tile_m * BM;
+  const int kb = p.K >> 7;  // 128-deep k-steps = stages
+
+  const unsigned char* xsrc[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int q = wave + 4 * i;
+    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
+    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
+    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
+  }
+  const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
+  auto stage = [&](int buf, int st) {
+    char* base = smem + buf * SBYTES;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i)
+      __builtin_amdgcn_global_load_lds(xsrc[i] + st * 128, (lds_void8*)(base + (wave + 4 * i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int piece = wave + 4 * i;  // = g * 2 + half
+      const int g = piece >> 1, h = piece & 1;
+      __builtin_amdgcn_global_load_lds(wsrc + ((long)g * kb + st) * 2048 + h * 1024,
+                                       (lds_void8*)(base + XBYTES + piece * 1024), 16, 0, 0);
+    }
+  };
+
+  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
+  const int brow = (wm * (BM / 2) + lr) * 128;
+  const int boff0 = brow + ((2 * (lane >> 4)) ^ swz) * 16;
+  const int boff1 = brow + ((2 * (lane >> 4) + 1) ^ swz) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
+
+  f32x4 acc[FCW][FPW];
+#pragma unroll
+  for (int i = 0; i < FCW; ++i)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  if (kb > 1) stage(1, 1);
+  int cur = 0;
+  for (int st = 0; st < kb; ++st) {
+    if (st + 1 < kb) wait_vm8<G>();
+    else wait_vm8<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < kb) stage(cur == 0 ? 2 : cur - 1, st + 2);
+    const char* base = smem + cur * SBYTES;
+    i32x8 a[FCW], b[FPW];
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048 + 1024);
+      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + boff0 + j * 16 * 128);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + j * 16 * 128);
+      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < FCW; ++i)
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                      0x7f7f7f7f);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+  const int lrow = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
+    if (m >= p.M) continue;
+    const float sx = p.sx[m];
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) {
+      const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sx * sw[e];
+      if (p.bias) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bb[e];
+      }
+      const long o = (long)m * p.ldo + n;
+      if (p.res) {
+        const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
+        v[0] += __uint_as_float(rr[0] << 16);
+        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+        v[2] += __uint_as_float(rr[1] << 16);
+        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      }
+      if (p.act == HZ_ACT_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      } else if (p.act == HZ_ACT_GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      } else if (p.act == HZ_ACT_TANH) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+      }
+      if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+      else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+}
+
+template <int BM, int BN>
+int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((gemm_mx_kernel<BM, BN>), dim3(tiles), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
 extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
   const HzGemmFp8Params& p = *pp;
+  if (p.cfg >= 16) {
+    if (!p.wmx || p.K % 128 || p.ldx % 16 || p.N % 4) return -1;
+    switch (p.cfg) {
+      case 16: return launch_mx<128, 128>(p, st);
+      case 17: return launch_mx<64, 128>(p, st);
+      case 18: return launch_mx<128, 64>(p, st);
+      case 19: return launch_mx<64, 64>(p, st);
+      default: return -2;
+    }
+  }
   if (p.N % 4 || p.ldx % 8 || p.ksteps * 32 < p.K) return -1;
   switch (p.cfg) {
     case 0: return launch8<1, 1>(p, st);

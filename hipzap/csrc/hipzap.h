@@ -102,6 +102,7 @@ typedef struct HzGemmFp8Params {
   void* out;                  // [M][ldo] bf16 or fp32
   int M, N, K, ksteps, ldx, ldo;
   int act, out_f32, cfg, kw;
+  const unsigned char* wmx;   // MX-packed weights [N_pad/16][K/128][2][64][16] (cfg 16..19) or NULL
 } HzGemmFp8Params;
 int hz_quant_launch(const HzQuantParams* p, hipStream_t st);
 int hz_gemm_fp8_launch(const HzGemmFp8Params* p, hipStream_t st);

@@ -66,6 +66,8 @@ class ExecContext:
                 key = "r" + conv_ops.conv_key(M, pc)
             if n.attrs.get("cfg") is not None:
                 cfg, kw = n.attrs["cfg"], n.attrs.get("kw", 1)
+            elif n.kind == "gemm_fp8":
+                cfg, kw = fp8.choose_config_fp8(M, pc, tuned, key)
             else:
                 cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=pc)
             conv_plans.append((cfg, kw, key))

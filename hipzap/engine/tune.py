@@ -23,6 +23,7 @@ import torch
 
 from .. import _native as N
 from ..ops import conv as conv_ops
+from ..ops import fp8 as fp8_ops
 
 TUNING_DIR = Path(__file__).resolve().parent.parent / "tuning"
 REPS = 16
@@ -33,6 +34,13 @@ def conv_shapes(graph, params) -> dict:
     bf16 GEMM shape (GEMM keys carry the ``r`` prefix ExecContext looks up)."""
     out = {}
     for n in graph.nodes:
+        if n.kind == "gemm_fp8":
+            pw = params[n.attrs["w"]]
+            M = n.attrs["rows"]
+            out.setdefault(f"f8r{M}x{pw.cout}x{pw.K}", (pw, (M, 1, 1), M, len(n.inputs) > 2,
+                                                        n.attrs.get("act", "none"), n.attrs.get("out_f32", False),
+                                                        "fp8"))
+            continue
         if n.kind == "gemm":
             pc = params[n.attrs["w"]]
             M = n.attrs["rows"]
@@ -55,7 +63,10 @@ def conv_shapes(graph, params) -> dict:
 def _capture(lib, prm, cfg, stream):
     prog = lib.hz_prog_create()
     for _ in range(REPS):
-        N.check(lib.hz_prog_add_conv(prog, C.byref(prm), cfg, 0), "add_conv")
+        if isinstance(prm, fp8_ops.GemmFp8Params):
+            N.check(lib.hz_prog_add_kernel(prog, fp8_ops.K_GEMM_FP8, C.byref(prm), C.sizeof(prm), 0), "add_fp8")
+        else:
+            N.check(lib.hz_prog_add_conv(prog, C.byref(prm), cfg, 0), "add_conv")
     N.check(lib.hz_prog_capture(prog, stream.cuda_stream), "capture")
     return prog
 
@@ -68,10 +79,18 @@ def _time_candidate(lib, shape, cand, bufs, streams, concurrent: int) -> float:
     progs = []
     try:
         for c in range(concurrent):
-            x, r, o = bufs[c]
-            prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0,
-                                             act, out_f32, cfg, kw, out_rowmajor=rowmajor, x_rowmajor=rowmajor)
-            if lib.hz_conv_launch(C.byref(prm), cfg, streams[c].cuda_stream) != 0:
+            x, r, o = bufs[c][:3]
+            if rowmajor == "fp8":
+                sx = torch.full((M,), 1e-2, device=x.device)
+                bufs[c] = (x, r, o, sx)
+                prm = fp8_ops.gemm_params(x.data_ptr(), sx.data_ptr(), pc, M, o.data_ptr(),
+                                          r.data_ptr() if res else 0, act, out_f32, cfg, kw)
+                rc = lib.hz_launch_kernel(fp8_ops.K_GEMM_FP8, C.byref(prm), streams[c].cuda_stream)
+            else:
+                prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0,
+                                                 act, out_f32, cfg, kw, out_rowmajor=rowmajor, x_rowmajor=rowmajor)
+                rc = lib.hz_conv_launch(C.byref(prm), cfg, streams[c].cuda_stream)
+            if rc != 0:
                 return float("inf")
             progs.append(_capture(lib, prm, cfg, streams[c]))
         torch.cuda.synchronize()
@@ -100,16 +119,22 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
             pc, (nb, h, w), M, res, act, out_f32, rowmajor = shape
             bufs = []
             for _ in range(concurrent):
-                x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+                if rowmajor == "fp8":
+                    x = torch.randint(0, 120, (M * pc.K,), device=dev, dtype=torch.uint8, generator=g)
+                else:
+                    x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
                 r = (torch.randn(M * pc.cout, device=dev, generator=g) * 0.5).to(torch.bfloat16)
                 o = torch.empty(M * pc.cout, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
                 bufs.append((x, r, o))
             times = []
-            for cand in conv_ops.candidates(M, pc.cout, pc.K, rowmajor, pc):
+            cands = (fp8_ops.candidates_fp8(M, pc) if rowmajor == "fp8"
+                     else conv_ops.candidates(M, pc.cout, pc.K, rowmajor, pc))
+            for cand in cands:
                 times.append((_time_candidate(lib, shape, cand, bufs, streams, concurrent), cand))
             times.sort()
             best_t, best = times[0]
-            heur = conv_ops.choose_config(M, pc.cout, pc.K, rowmajor=rowmajor, pc=pc)
+            heur = (fp8_ops.choose_config_fp8(M, pc) if rowmajor == "fp8"
+                    else conv_ops.choose_config(M, pc.cout, pc.K, rowmajor=rowmajor, pc=pc))
             heur_t = next((t for t, c in times if tuple(c) == tuple(heur)), None)
             table[key] = list(best)
             report[key] = {"best_us": round(best_t, 2), "best": list(best), "heuristic": list(heur),
@@ -140,6 +165,12 @@ def main():
     # random weights of the real shapes are enough for timing
     params = {}
     for k, v in meta.items():
+        if isinstance(v, fp8_ops.PackedFp8):
+            params[k] = fp8_ops.PackedFp8(
+                torch.randint(0, 120, v.w8.shape, device=dev, dtype=torch.uint8),
+                torch.full(v.sw.shape, 1e-2, device=dev), torch.zeros(v.bias.shape, device=dev), v.cin, v.cout,
+                None if v.w8mx is None else torch.randint(0, 120, v.w8mx.shape, device=dev, dtype=torch.uint8))
+            continue
         if not isinstance(v, conv_ops.PackedConv):
             continue
         params[k] = conv_ops.PackedConv((torch.randn(v.wf.shape, device=dev) * 0.02).to(torch.bfloat16),

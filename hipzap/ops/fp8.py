@@ -28,7 +28,7 @@ class GemmFp8Params(C.Structure):
     _fields_ = [("x", C.c_void_p), ("sx", C.c_void_p), ("w", C.c_void_p), ("sw", C.c_void_p), ("bias", C.c_void_p),
                 ("res", C.c_void_p), ("out", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
                 ("ksteps", C.c_int), ("ldx", C.c_int), ("ldo", C.c_int), ("act", C.c_int), ("out_f32", C.c_int),
-                ("cfg", C.c_int), ("kw", C.c_int)]
+                ("cfg", C.c_int), ("kw", C.c_int), ("wmx", C.c_void_p)]
 
 
 @dataclass
@@ -38,6 +38,7 @@ class PackedFp8:
     bias: torch.Tensor   # fp32 [cout]
     cin: int             # K
     cout: int
+    w8mx: torch.Tensor | None = None  # MX-packed copy [rows_pad/16, K/128, 2, 64, 16] for the LDS GEMM
 
     @property
     def K(self) -> int:
@@ -69,12 +70,53 @@ def quantize_weight(w2d: torch.Tensor, rows_pad: int | None = None):
     return q.view(torch.uint8), sw
 
 
+def mx_pack(q: torch.Tensor) -> torch.Tensor:
+    """[rows, K] e4m3 bytes (rows % 16 == 0, K % 128 == 0) -> [rows/16, K/128, 2, 64, 16]:
+    lane l = 16*(k%128 // 32) + row%16 holds k%32 = 16*half + byte (v_mfma_scale_f32_16x16x128_f8f6f4)."""
+    rows, K = q.shape
+    t = q.reshape(rows // 16, 16, K // 128, 4, 2, 16)          # g, r, kb, lg, half, byte
+    return t.permute(0, 2, 4, 3, 1, 5).reshape(rows // 16, K // 128, 2, 64, 16)
+
+
+def mx_unpack(w: torch.Tensor) -> torch.Tensor:
+    g, kb = w.shape[0], w.shape[1]
+    return w.reshape(g, kb, 2, 4, 16, 16).permute(0, 4, 1, 3, 2, 5).reshape(g * 16, kb * 128)
+
+
 def quantize_linear(pc: PackedConv) -> PackedFp8:
     if pc.r != 1 or pc.s != 1:
         raise ValueError("fp8 path is for Linear layers")
     rows = pc.wf.shape[0] * 16
     q, sw = quantize_weight(pc.dense(), rows)
-    return PackedFp8(fragment_major(q).contiguous(), sw.contiguous(), pc.bias.float().contiguous(), pc.K, pc.cout)
+    mx = mx_pack(q).contiguous() if (pc.K % 128 == 0 and rows % 128 == 0) else None
+    return PackedFp8(fragment_major(q).contiguous(), sw.contiguous(), pc.bias.float().contiguous(), pc.K, pc.cout, mx)
+
+
+MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64)}  # cfg -> (BM, BN), csrc/fp8.hip
+
+
+def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
+    return pw.w8mx is not None and M >= 64 and pw.K % 128 == 0 and (ldx or pw.K) % 16 == 0
+
+
+def candidates_fp8(M: int, pw: PackedFp8) -> list:
+    from .conv import candidates
+    out = [(cfg, 1) for cfg in MX_TILES] if mx_ok(M, pw) else []
+    return out + candidates(M, pw.cout, pw.K)
+
+
+def choose_config_fp8(M: int, pw: PackedFp8, tuned: dict | None = None, key: str | None = None):
+    if tuned is not None and key is not None and key in tuned:
+        cfg, kw = int(tuned[key][0]), int(tuned[key][1])
+        if cfg not in MX_TILES or mx_ok(M, pw):
+            return cfg, kw
+    if mx_ok(M, pw) and M >= 512:
+        for cfg in (16, 17, 18, 19):
+            bm, bn = MX_TILES[cfg]
+            if math.ceil(M / bm) * math.ceil(pw.cout / bn) >= 256:
+                return cfg, 1
+        return 19, 1
+    return choose_config(M, pw.cout, pw.K)
 
 
 def quantize_params(P: dict, names) -> dict:
@@ -106,16 +148,19 @@ def quant_rows(x: torch.Tensor):
 def gemm_params(x8_ptr, sx_ptr, pw: PackedFp8, M, out_ptr, res_ptr=0, act="none", out_f32=False, cfg=0, kw=1,
                 ldx=None, ldo=None) -> GemmFp8Params:
     from .conv import ACT
+    if cfg in MX_TILES and not mx_ok(M, pw, ldx):
+        raise ValueError(f"MX fp8 GEMM config {cfg} not legal for M={M} K={pw.K}")
     return GemmFp8Params(x8_ptr, sx_ptr, pw.w8.data_ptr(), pw.sw.data_ptr(), pw.bias.data_ptr(), res_ptr, out_ptr, M,
                          pw.cout, pw.K, pw.ksteps, ldx if ldx is not None else pw.K,
-                         ldo if ldo is not None else pw.cout, ACT[act], int(out_f32), cfg, kw)
+                         ldo if ldo is not None else pw.cout, ACT[act], int(out_f32), cfg, kw,
+                         pw.w8mx.data_ptr() if pw.w8mx is not None else 0)
 
 
 def gemm_fp8(x8: torch.Tensor, sx: torch.Tensor, pw: PackedFp8, residual=None, act="none", out_f32=False,
              cfg=None, kw=None) -> torch.Tensor:
     M = x8.shape[0]
     if cfg is None:
-        cfg, kw = choose_config(M, pw.cout, pw.K)
+        cfg, kw = choose_config_fp8(M, pw)
     out = torch.empty(M, pw.cout, device=x8.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     prm = gemm_params(x8.data_ptr(), sx.data_ptr(), pw, M, out.data_ptr(), N.ptr(residual), act, out_f32, cfg,
                       kw or 1, x8.stride(0), out.stride(0))

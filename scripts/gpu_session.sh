@@ -26,6 +26,7 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
 [[ $STEPS == *txtune* ]] && {
   step txtune_bert 600 python -m hipzap.engine.tune --model bert-base --batch 16 --report $OUT/tune_bert.json
   step txtune_vit 600 python -m hipzap.engine.tune --model vit-b16 --batch 8 --report $OUT/tune_vit.json
+  step txtune_vit8 600 python -m hipzap.engine.tune --model vit-b16-fp8 --batch 8 --report $OUT/tune_vit8.json
   mkdir -p $OUT/tuning && cp hipzap/tuning/*.json $OUT/tuning/
 }
 [[ $STEPS == *models* ]] && step bench_models 900 python scripts/bench_models.py

@@ -98,3 +98,28 @@ def test_fp8_weight_roundtrip():
     pw = quantize_linear(pack_linear(w, torch.zeros(100)))
     err = (pw.dequant() - w).abs() / w.abs().amax(dim=1, keepdim=True)
     assert err.max() < 0.07 and pw.w8.dtype == torch.uint8 and pw.sw.shape[0] % 64 == 0
+
+
+def test_mx_pack_layout():
+    """MX packing (csrc/fp8.hip gemm_mx_kernel): lane l = 16*((k%128)//32) + row%16 holds
+    k%32 = 16*half + byte; mx_unpack inverts it."""
+    from hipzap.ops import fp8 as F8
+    q = torch.randint(0, 256, (32, 256), dtype=torch.uint8)
+    w = F8.mx_pack(q)
+    assert w.shape == (2, 2, 2, 64, 16)
+    assert torch.equal(F8.mx_unpack(w), q)
+    g, kb, half, lane, byte = 1, 1, 1, 37, 5
+    row, k = g * 16 + lane % 16, kb * 128 + (lane // 16) * 32 + half * 16 + byte
+    assert w[g, kb, half, lane, byte] == q[row, k]
+
+
+def test_quantize_linear_builds_mx_copy():
+    from hipzap.ops import conv as C
+    from hipzap.ops import fp8 as F8
+    pw = F8.quantize_linear(C.pack_linear(torch.randn(200, 256), torch.zeros(200)))
+    assert pw.w8mx is not None and pw.w8mx.shape == (256 // 16, 2, 2, 64, 16)
+    # both packings carry the same bytes
+    dense = pw.w8.reshape(16, 8, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(256, 256)
+    assert torch.equal(F8.mx_unpack(pw.w8mx), dense)
+    assert F8.choose_config_fp8(2048, pw)[0] in F8.MX_TILES
+    assert F8.choose_config_fp8(8, pw)[0] not in F8.MX_TILES
