@@ -48,6 +48,9 @@ def parse():
                     help="replica: independent bs=1 request streams per GPU (headline); scatter: rank 0 scatters "
                          "a global batch over ranks and gathers the logits (configs 3/5)")
     ap.add_argument("--global-batch", type=int, default=32, help="scatter mode: global batch over all ranks")
+    ap.add_argument("--input", choices=["uint8", "fp32"], default=os.environ.get("HIPZAP_BENCH_INPUT", "uint8"),
+                    help="request payload: uint8 HWC images (decoded-JPEG format, ImageNet mean/std applied on "
+                         "device by the preprocess kernel) or pre-normalised fp32 NCHW tensors")
     return ap.parse_args()
 
 
@@ -143,6 +146,13 @@ def torch_reference_throughput(model, device, iters=200):
     return iters / dt
 
 
+def request_input(args, adapter):
+    """One request's payload: a decoded uint8 HWC image (default) or an fp32 NCHW tensor."""
+    if args.input == "uint8" and args.model.startswith("resnet"):
+        return torch.randint(0, 256, (args.batch, 224, 224, 3), dtype=torch.uint8)
+    return adapter.example_input(args.batch)
+
+
 def main():
     args = parse()
     from hipzap.engine.engine import Engine
@@ -185,14 +195,16 @@ def main():
         else:
             params, arch_kw = None, None
         meta, meta_kw = adapter.meta_params()
-        arch_kw = arch_kw or meta_kw
+        arch_kw = dict(arch_kw or meta_kw)
+        if args.input == "uint8" and args.model.startswith("resnet"):
+            arch_kw["input_uint8"] = True
         ta = time.perf_counter()
         params = broadcast_params(params, meta, device)
         torch.cuda.synchronize(device)
         timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         eng = Engine(args.model, params, device, batch=args.batch, num_contexts=args.streams,
                      capture=not args.no_capture, tuned=tuned, arch_kw=arch_kw, timings=timings, host_io=True)
-        x = adapter.example_input(args.batch)
+        x = request_input(args, adapter)
         out = eng.infer(x)
         cold_ms = (time.perf_counter() - t0) * 1e3
         eng.timings["first_infer_total_ms"] = cold_ms
@@ -209,7 +221,7 @@ def main():
     assert torch.isfinite(out).all(), "non-finite logits"
 
     # single-request latency (one context, full round trip incl. host copies), p50
-    x = adapter.example_input(args.batch)
+    x = request_input(args, adapter)
     lat = []
     for i in range(60):
         t = time.perf_counter()
@@ -246,7 +258,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / BASELINE_INF_S, 2), "dtype": "bf16",
-            "data": "synthetic (random-init ResNet-50 weights via torch.save/torch.load, random fp32 images)",
+            "data": "synthetic (random-init ResNet-50 weights via torch.save/torch.load; "
+                    + ("random uint8 224x224x3 images, normalised on device)" if args.input == "uint8"
+                       else "random fp32 NCHW images)"),
             "config": {"model": "ResNet-50", "global_batch": args.batch * world, "seq_len": None,
                        "parallelism": f"dp{world}", "request_batch": args.batch,
                        "streams_per_gpu": args.streams, "hipgraph": not args.no_capture},

@@ -40,6 +40,17 @@ int hz_maxpool_launch(const HzPoolParams* p, hipStream_t st);
 // blocked: x is [N][C/32][HW][32] instead of NHWC
 int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked, hipStream_t st);
 
+// fused global-average-pool + classifier (ResNet head):
+//   out[b][n] = bias[n] + sum_c W[n][c] * mean_hw x[b][c][hw]
+typedef struct HzPoolFcParams {
+  const unsigned short* x;  // channel-blocked bf16 [B][C/32][HW][32]
+  const unsigned short* w;  // fragment-major bf16 [N_pad/16][C/32][64][8] (pack_linear)
+  const float* bias;        // [N]
+  float* out;               // fp32 [B][ldo]
+  int B, C, HW, N, ldo;
+} HzPoolFcParams;
+int hz_pool_fc_launch(const HzPoolFcParams* p, hipStream_t st);
+
 // image pre-processing: src NCHW fp32 (mode 0) or NHWC uint8 (mode 1) -> NHWC bf16 with Cpad channels
 int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
                          int mode, const float* mean, const float* inv_std, hipStream_t st);
@@ -163,7 +174,7 @@ int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t st);
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
-       HZ_K_SOFTMAX = 12 };
+       HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
 

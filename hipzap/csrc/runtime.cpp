@@ -242,6 +242,7 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_QUANT: return hz_quant_launch(static_cast<const HzQuantParams*>(prm), st);
     case HZ_K_GEMM_FP8: return hz_gemm_fp8_launch(static_cast<const HzGemmFp8Params*>(prm), st);
     case HZ_K_SOFTMAX: return hz_softmax_launch(static_cast<const HzSoftmaxParams*>(prm), st);
+    case HZ_K_POOL_FC: return hz_pool_fc_launch(static_cast<const HzPoolFcParams*>(prm), st);
     default: return -100;
   }
 }

@@ -68,6 +68,57 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__
   }
 }
 
+// Fused global-average-pool + FC (one launch instead of avgpool + FC GEMM + a kernel boundary).
+// Block = 4 waves, 4 x 16 output rows, one image (blockIdx.y). Phase 1: every block pools all C
+// channels of its image into LDS (fp32; C*HW*2 bytes, L2-resident after the first block):
+// lane l reads 16 B (8 channels) of channel block 16*wave' + (l>>2) at every pixel — 16 disjoint
+// 64-B runs per instruction, no cross-lane reduction. Phase 2: each wave streams its 16-row
+// weight group (fragment-major: one contiguous 1 KiB per 32-deep k-step) and dots it with the
+// pooled vector; the 4 lanes sharing a row (l, l^16, l^32, l^48) reduce with 2 shuffles.
+__global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
+  extern __shared__ __attribute__((aligned(16))) float pooled[];  // [C]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.y;
+  const int ncb = p.C >> 5;
+  const float inv = 1.f / p.HW;
+  for (int cb0 = wave * 16; cb0 < ncb; cb0 += 64) {
+    const int cb = cb0 + (lane >> 2), sub = lane & 3;
+    if (cb < ncb) {
+      const bf16_t* src = p.x + (((long)b * ncb + cb) * p.HW) * 32 + sub * 8;
+      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 7
+      for (int hw = 0; hw < p.HW; ++hw) {
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(src + hw * 32), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += f[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pooled[cb * 32 + sub * 8 + e] = s[e] * inv;
+    }
+  }
+  __syncthreads();
+  const int g = blockIdx.x * 4 + wave;  // 16-row weight group
+  if (g * 16 >= p.N) return;
+  const int ks = p.C >> 5;
+  const bf16_t* wg = p.w + ((long)g * ks * 64 + lane) * 8;
+  const float* pl = pooled + (lane >> 4) * 8;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < ks; ++k) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(wg + (long)k * 512), f);
+    const f32x4 p0 = *reinterpret_cast<const f32x4*>(pl + k * 32);
+    const f32x4 p1 = *reinterpret_cast<const f32x4*>(pl + k * 32 + 4);
+    acc += f[0] * p0[0] + f[1] * p0[1] + f[2] * p0[2] + f[3] * p0[3] + f[4] * p1[0] + f[5] * p1[1] + f[6] * p1[2] +
+           f[7] * p1[3];
+  }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  const int n = g * 16 + lane;
+  if (lane < 16 && n < p.N) p.out[(long)b * p.ldo + n] = acc + (p.bias ? p.bias[n] : 0.f);
+}
+
 // mode 0: src fp32 NCHW (already normalised unless mean/inv_std given)
 // mode 1: src uint8 NHWC (raw image bytes, normalised with mean/inv_std in 0..1 scale)
 __global__ __launch_bounds__(256) void preprocess_kernel(const void* __restrict__ src, bf16_t* __restrict__ dst,
@@ -119,6 +170,14 @@ extern "C" int hz_avgpool_launch(const unsigned short* x, unsigned short* out, i
                                  hipStream_t st) {
   if (C % 64) return -1;
   hipLaunchKernelGGL(avgpool_kernel, dim3(N * (C / 64)), dim3(256), 0, st, x, out, N, HW, C, blocked);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
+  const HzPoolFcParams& p = *pp;
+  if (p.C % 32 || p.C > 16384 || p.HW < 1 || p.N < 1) return -1;
+  const int groups = (p.N + 15) / 16;
+  hipLaunchKernelGGL(pool_fc_kernel, dim3((groups + 3) / 4, p.B), dim3(256), (size_t)p.C * sizeof(float), st, p);
   return (int)hipGetLastError();
 }
 

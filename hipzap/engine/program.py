@@ -15,6 +15,7 @@ from .. import _native as N
 from ..ops import conv as conv_ops
 from ..ops import fp8
 from ..ops import transformer as tx
+from ..ops import vision
 from .graph import Graph, plan_memory
 
 
@@ -186,6 +187,13 @@ class ExecContext:
             prm = tx.VitTokensParams(addr(n.inputs[0]), self.params[a["cls"]].data_ptr(),
                                      self.params[a["pos"]].data_ptr(), addr(n.outputs[0]), a["B"], a["np"], D)
             tx.prog_add(self.prog, tx.K_VIT_TOKENS, prm, n.slot)
+        elif n.kind == "pool_fc":
+            pc = self.params[n.attrs["w"]]
+            nb, h, w, c = g.shape(n.inputs[0])
+            assert conv_ops.is_blocked(c) and pc.K == c and pc.ksteps * 32 == c
+            prm = vision.PoolFcParams(addr(n.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), addr(n.outputs[0]),
+                                      nb, c, h * w, pc.cout, g.shape(n.outputs[0])[-1])
+            tx.prog_add(self.prog, vision.K_POOL_FC, prm, n.slot)
         elif n.kind == "softmax":
             ishape = g.shape(n.inputs[0])
             rows, ld = ishape[0], int(torch.tensor(ishape[1:]).prod())

@@ -117,6 +117,10 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             from ..ops.transformer import embed_ref
             tab, ln = params[n.attrs["emb"]], params[n.attrs["ln"]]
             store(n.outputs[0], embed_ref(vals[n.inputs[0]], vals[n.inputs[1]], tab, ln, n.attrs["L"]))
+        elif k == "pool_fc":
+            from ..ops.vision import pool_fc_ref
+            x = vals[n.inputs[0]].float().reshape(g.shape(n.inputs[0]))
+            store(n.outputs[0], pool_fc_ref(x, params[n.attrs["w"]]))
         elif k == "softmax":
             from ..ops.transformer import softmax_ref
             x = vals[n.inputs[0]].float().reshape(g.shape(n.inputs[0])[0], -1)

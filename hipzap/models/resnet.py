@@ -183,7 +183,7 @@ def pack_resnet(sd: dict, device="cpu") -> dict[str, PackedConv]:
 
 
 def build_graph(arch: str, batch: int, num_classes: int = 1000, image: int = 224,
-                input_uint8: bool = False, side_stream: bool = False) -> Graph:
+                input_uint8: bool = False, side_stream: bool = False, fuse_head: bool = True) -> Graph:
     """Lower ResNet to a static kernel graph for a fixed batch size.
 
     ``side_stream`` puts the downsample conv on a forked stream. Off by default: measured on
@@ -244,8 +244,12 @@ def build_graph(arch: str, batch: int, num_classes: int = 1000, image: int = 224
                 x = conv(y, f"{pre}.conv2", cout, 3, 1, 1, res=idt)
             cin = cout
     nb, h, w, c = g.shape(x)
-    pooled = g.tensor((nb, 1, 1, c), name="avgpool")
-    g.add("avgpool", [x], [pooled])
-    logits = conv(pooled, "fc", num_classes, 1, 1, 0, act="none", out_f32=True, ext=True)
+    if fuse_head:  # one kernel: global average pool + FC (csrc/vision.hip pool_fc_kernel)
+        logits = g.tensor((nb, 1, 1, num_classes), torch.float32, "fc", external=True)
+        g.add("pool_fc", [x], [logits], w="fc", name="pool_fc")
+    else:
+        pooled = g.tensor((nb, 1, 1, c), name="avgpool")
+        g.add("avgpool", [x], [pooled])
+        logits = conv(pooled, "fc", num_classes, 1, 1, 0, act="none", out_f32=True, ext=True)
     g.outputs.append(logits)
     return g

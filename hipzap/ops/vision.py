@@ -1,9 +1,18 @@
 """Eager wrappers + fp32 oracles for the vision helper kernels (csrc/vision.hip)."""
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from .. import _native as N
+
+K_POOL_FC = 13
+
+
+class PoolFcParams(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("out", C.c_void_p), ("B", C.c_int),
+                ("C", C.c_int), ("HW", C.c_int), ("N", C.c_int), ("ldo", C.c_int)]
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -28,6 +37,25 @@ def avgpool_nhwc(x: torch.Tensor, blocked: bool = False) -> torch.Tensor:
     N.check(N.lib().hz_avgpool_launch(src.data_ptr(), out.data_ptr(), n, h * w, c, int(blocked), N.stream_ptr()),
             "avgpool")
     return out
+
+
+def pool_fc(x: torch.Tensor, pc, blocked_input: bool = False) -> torch.Tensor:
+    """Fused global-average-pool + Linear: x logical [B,H,W,C] bf16 -> fp32 logits [B, cout]."""
+    from .conv import to_blocked
+    b, h, w, c = x.shape
+    assert c == pc.K == pc.ksteps * 32 and c % 32 == 0
+    src = x if blocked_input else to_blocked(x)
+    out = torch.empty(b, pc.cout, device=x.device, dtype=torch.float32)
+    prm = PoolFcParams(src.data_ptr(), pc.wf.data_ptr(), pc.bias.data_ptr(), out.data_ptr(), b, c, h * w, pc.cout,
+                       pc.cout)
+    N.check(N.lib().hz_launch_kernel(K_POOL_FC, C.byref(prm), N.stream_ptr()), "pool_fc")
+    return out
+
+
+def pool_fc_ref(x: torch.Tensor, pc) -> torch.Tensor:
+    """fp32 oracle: x logical [B,H,W,C]."""
+    pooled = x.float().mean(dim=(1, 2))
+    return pooled @ pc.dense().float().t() + pc.bias.float()
 
 
 def preprocess(src: torch.Tensor, cpad: int = 8, mean=None, std=None) -> torch.Tensor:

@@ -78,3 +78,21 @@ def test_probs_head(model_sd):
     assert probs.shape == logits.shape
     assert torch.allclose(probs.sum(1), torch.ones(1), atol=1e-4)
     assert (probs - torch.softmax(logits.float(), 1)).abs().max().item() < 1e-5
+
+
+def test_uint8_image_requests(model_sd):
+    """bench.py's default payload: uint8 HWC images normalised on device (preprocess kernel)."""
+    name, m, sd = model_sd
+    a = registry.get(name)
+    params, kw = a.pack({k: v.to(DEV) for k, v in sd.items()}, torch.device(DEV))
+    eng = Engine(name, params, DEV, batch=1, arch_kw=dict(kw, input_uint8=True))
+    img = torch.randint(0, 256, (1, 224, 224, 3), dtype=torch.uint8)
+    y = eng.infer(img)
+    params_cpu, _ = a.pack(sd, "cpu")
+    ref = run_graph_reference(eng.graph, params_cpu, [img])[eng.graph.outputs[0]].reshape(1, -1)
+    assert (y - ref).abs().max().item() / ref.abs().max().item() < 3e-2
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    with torch.no_grad():
+        eager = m((img.permute(0, 3, 1, 2).float() / 255 - mean) / std)
+    assert y.argmax(1).item() == eager.argmax(1).item()

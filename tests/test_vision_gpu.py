@@ -101,3 +101,17 @@ def test_maxpool_avgpool_preprocess():
     u8 = torch.randint(0, 256, (2, 20, 24, 3), dtype=torch.uint8, generator=g)
     p = V.preprocess(u8.to(DEV), mean=V.IMAGENET_MEAN, std=V.IMAGENET_STD).cpu().float()
     assert (p - V.preprocess_reference(u8, mean=V.IMAGENET_MEAN, std=V.IMAGENET_STD)).abs().max() < 2e-2
+
+
+@pytest.mark.parametrize("B,H,C,N", [(1, 7, 2048, 1000), (3, 7, 512, 10), (2, 4, 64, 33)])
+def test_pool_fc(B, H, C, N):
+    """Fused global-average-pool + FC (ResNet head) vs fp32."""
+    from hipzap.ops import conv as Cv
+    from hipzap.ops import vision as V
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, H, H, C, generator=g).to(torch.bfloat16)
+    pc = Cv.pack_linear(torch.randn(N, C, generator=g) * 0.05, torch.randn(N, generator=g))
+    y = V.pool_fc(x.to(DEV), pc.to(DEV))
+    ref = V.pool_fc_ref(x, pc)
+    assert y.shape == (B, N)
+    assert ((y.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-2
