@@ -65,6 +65,7 @@ def _load():
     lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
     P = c_void_p
     _sig(lib, "hz_conv_launch", c_int, C.POINTER(ConvParams), c_int, P)
+    _sig(lib, "hz_conv2_launch", c_int, C.POINTER(ConvParams), C.POINTER(ConvParams), c_int, P)
     _sig(lib, "hz_maxpool_launch", c_int, C.POINTER(PoolParams), P)
     _sig(lib, "hz_avgpool_launch", c_int, P, P, c_int, c_int, c_int, c_int, P)
     _sig(lib, "hz_preprocess_launch", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P)
@@ -74,6 +75,7 @@ def _load():
     _sig(lib, "hz_prog_destroy", None, P)
     _sig(lib, "hz_prog_num_ops", c_int, P)
     _sig(lib, "hz_prog_add_conv", c_int, P, C.POINTER(ConvParams), c_int, c_int)
+    _sig(lib, "hz_prog_add_conv2", c_int, P, C.POINTER(ConvParams), C.POINTER(ConvParams), c_int, c_int)
     _sig(lib, "hz_prog_add_maxpool", c_int, P, C.POINTER(PoolParams), c_int)
     _sig(lib, "hz_prog_add_avgpool", c_int, P, P, P, c_int, c_int, c_int, c_int, c_int)
     _sig(lib, "hz_prog_add_preprocess", c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int)

@@ -29,6 +29,8 @@ typedef struct HzConvParams {
 // cfg 16..19: LDS-tiled GEMM (gemm.hip; row-major activations, K % 64 == 0, weight rows % 128 == 0)
 int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t st);
 int hz_gemm_lds_launch(const HzConvParams* p, int cfg, hipStream_t st);
+// two independent convs with one shared (cfg, kw) in one launch (grouped; conv.hip conv2_kernel)
+int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int cfg, hipStream_t st);
 
 typedef struct HzPoolParams {
   const unsigned short* x;  // NHWC bf16
@@ -183,6 +185,7 @@ HzProgram hz_prog_create(void);
 void hz_prog_destroy(HzProgram p);
 int hz_prog_num_ops(HzProgram p);
 int hz_prog_add_conv(HzProgram p, const HzConvParams* cp, int cfg, int slot);
+int hz_prog_add_conv2(HzProgram p, const HzConvParams* a, const HzConvParams* b, int cfg, int slot);
 int hz_prog_add_maxpool(HzProgram p, const HzPoolParams* pp, int slot);
 int hz_prog_add_avgpool(HzProgram p, const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked,
                         int slot);

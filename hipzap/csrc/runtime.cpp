@@ -101,6 +101,11 @@ int hz_prog_add_conv(HzProgram h, const HzConvParams* cp, int cfg, int slot) {
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
                 [c, cfg](hipStream_t s) { return hz_conv_launch(&c, cfg, s); });
 }
+int hz_prog_add_conv2(HzProgram h, const HzConvParams* a, const HzConvParams* b, int cfg, int slot) {
+  HzConvParams c0 = *a, c1 = *b;
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
+                [c0, c1, cfg](hipStream_t s) { return hz_conv2_launch(&c0, &c1, cfg, s); });
+}
 int hz_prog_add_maxpool(HzProgram h, const HzPoolParams* pp, int slot) {
   HzPoolParams c = *pp;
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_maxpool_launch(&c, s); });

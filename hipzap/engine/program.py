@@ -9,6 +9,8 @@ hipGraph; ``replay()`` is the warm path.
 from __future__ import annotations
 
 import ctypes as C
+import os
+
 import torch
 
 from .. import _native as N
@@ -19,9 +21,29 @@ from ..ops import vision
 from .graph import Graph, plan_memory
 
 
+def pair_key(ka: str, kb: str) -> str:
+    return f"pair:{ka}|{kb}"
+
+
+def conv_pairs(g: Graph) -> dict:
+    """{i: i+1} for adjacent conv nodes that can share one launch: both single-input, same
+    input tensor, same stream slot, not row-major (e.g. ResNet's downsample + conv1)."""
+    out = {}
+    i = 0
+    while i + 1 < len(g.nodes):
+        a, b = g.nodes[i], g.nodes[i + 1]
+        if (a.kind == b.kind == "conv" and len(a.inputs) == 1 and len(b.inputs) == 1 and a.inputs[0] == b.inputs[0]
+                and a.slot == b.slot and not a.attrs.get("rowmajor") and not b.attrs.get("rowmajor")):
+            out[i] = i + 1
+            i += 2
+            continue
+        i += 1
+    return out
+
+
 class ExecContext:
     def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
-                 host_io: bool = False):
+                 host_io: bool = False, pair_convs: bool | None = None):
         self.graph = g
         self.device = torch.device(device)
         self.params = params
@@ -84,13 +106,50 @@ class ExecContext:
                 d = self.ext[t]
                 N.check(lib.hz_prog_add_memcpy(self.prog, d.data_ptr(), hbuf.data_ptr(), d.numel() * d.element_size(),
                                                0), "h2d")
-        for i, n in enumerate(g.nodes):
+        if pair_convs is None:
+            pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
+        self.pairs = conv_pairs(g) if pair_convs else {}
+        i = 0
+        while i < len(g.nodes):
+            n = g.nodes[i]
+            if i in self.pairs:
+                self._add_conv_pair(lib, n, g.nodes[i + 1], conv_plans[i], conv_plans[i + 1], tuned)
+                i += 2
+                continue
             self._add_node(lib, n, conv_plans[i])
+            i += 1
         if host_io:
             N.check(lib.hz_prog_add_memcpy(self.prog, self.host_output.data_ptr(), self.output.data_ptr(),
                                            self.output.numel() * self.output.element_size(), 0), "d2h")
 
     # ------------------------------------------------------------------
+    def _conv_params(self, n, cfg, kw):
+        g, addr = self.graph, self._addr
+        pc = self.params[n.attrs["w"]]
+        nb, h, w, _ = g.shape(n.inputs[0])
+        res = n.inputs[1] if len(n.inputs) > 1 else None
+        prm, _, _ = conv_ops.make_params(
+            addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
+            n.attrs.get("out_f32", False), cfg, kw, out_rowmajor=n.attrs.get("rowmajor", False))
+        return prm
+
+    def _add_conv_pair(self, lib, a, b, plan_a, plan_b, tuned):
+        """Two independent convs reading the same input -> one grouped launch (conv2_kernel)."""
+        key = pair_key(plan_a[2], plan_b[2])
+        if tuned is not None and key in tuned:
+            cfg, kw = int(tuned[key][0]), int(tuned[key][1])
+        else:  # the larger problem's own choice
+            fa = self._conv_flops(a)
+            cfg, kw = (plan_a if fa >= self._conv_flops(b) else plan_b)[:2]
+        pa, pb = self._conv_params(a, cfg, kw), self._conv_params(b, cfg, kw)
+        self.configs.append((a.attrs.get("name", "") + "+" + b.attrs.get("name", ""), key, cfg, kw))
+        N.check(lib.hz_prog_add_conv2(self.prog, C.byref(pa), C.byref(pb), cfg, a.slot), "add_conv2")
+
+    def _conv_flops(self, n) -> int:
+        pc = self.params[n.attrs["w"]]
+        nb, p, q, _ = self.graph.shape(n.outputs[0])
+        return nb * p * q * pc.cout * pc.K
+
     def _add_node(self, lib, n, plan):
         g, addr = self.graph, self._addr
         if n.kind == "conv":

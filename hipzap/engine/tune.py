@@ -145,6 +145,69 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
     return table, report
 
 
+def _time_pair(lib, sa, sb, cand, bufs, stream) -> float:
+    """us per grouped launch (conv2_kernel) of two convs sharing (cfg, kw)."""
+    cfg, kw = cand
+    prms = []
+    for (pc, (nb, h, w), M, res, act, out_f32, _), (x, r, o) in zip((sa, sb), bufs):
+        prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), 0, act, out_f32, cfg, kw)
+        prms.append(prm)
+    if lib.hz_conv2_launch(C.byref(prms[0]), C.byref(prms[1]), cfg, stream.cuda_stream) != 0:
+        return float("inf")
+    prog = lib.hz_prog_create()
+    try:
+        for _ in range(REPS):
+            N.check(lib.hz_prog_add_conv2(prog, C.byref(prms[0]), C.byref(prms[1]), cfg, 0), "add_conv2")
+        N.check(lib.hz_prog_capture(prog, stream.cuda_stream), "capture")
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
+            lib.hz_prog_replay(prog, stream.cuda_stream)
+            stream.synchronize()
+            best = min(best, (time.perf_counter() - t0) * 1e6 / REPS)
+        return best
+    finally:
+        lib.hz_prog_destroy(prog)
+
+
+def tune_pairs(graph, params, device, verbose=False) -> tuple[dict, dict]:
+    """Shared (cfg, kw) for every grouped conv pair ExecContext will launch (program.conv_pairs)."""
+    from .program import conv_pairs, pair_key
+    lib = N.lib()
+    dev = torch.device(device)
+    shapes = conv_shapes(graph, params)
+    table, report = {}, {}
+    g = torch.Generator(device=dev).manual_seed(1)
+    stream = torch.cuda.Stream(dev)
+    for i, j in conv_pairs(graph).items():
+        keys = []
+        for n in (graph.nodes[i], graph.nodes[j]):
+            pc = params[n.attrs["w"]]
+            nb, h, w, _ = graph.shape(n.inputs[0])
+            _, p, q, _ = graph.shape(n.outputs[0])
+            keys.append(conv_ops.conv_key(nb * p * q, pc))
+        key = pair_key(*keys)
+        if key in table:
+            continue
+        sa, sb = shapes[keys[0]], shapes[keys[1]]
+        bufs = []
+        for (pc, (nb, h, w), M, *_rest) in (sa, sb):
+            x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+            bufs.append((x, None, torch.empty(M * pc.cout, device=dev, dtype=torch.bfloat16)))
+        ca = set(map(tuple, conv_ops.candidates(sa[2], sa[0].cout, sa[0].K)))
+        cands = [c for c in conv_ops.candidates(sb[2], sb[0].cout, sb[0].K) if tuple(c) in ca]
+        times = sorted((_time_pair(lib, sa, sb, c, bufs, stream), list(c)) for c in cands)
+        if not times:
+            continue
+        table[key] = times[0][1]
+        report[key] = {"best_us": round(times[0][0], 2), "best": times[0][1],
+                       "top5": [[round(t, 2), c] for t, c in times[:5]]}
+        if verbose:
+            print(f"{key:60s} best {times[0][0]:7.2f}us {times[0][1]}", flush=True)
+    return table, report
+
+
 def table_path(model: str, batch: int, concurrent: int = 1) -> Path:
     suffix = "" if concurrent <= 1 else f"_c{concurrent}"
     return TUNING_DIR / f"{model}_bs{batch}{suffix}.json"
@@ -182,6 +245,9 @@ def main():
             t0 = time.time()
             graph = a.build_graph(batch=b, **kw)
             table, report = tune_graph(graph, params, dev, verbose=True, concurrent=conc)
+            ptable, preport = tune_pairs(graph, params, dev, verbose=True)
+            table.update(ptable)
+            report.update(preport)
             TUNING_DIR.mkdir(exist_ok=True)
             path = table_path(args.model, b, conc)
             with open(path, "w") as f:

@@ -115,3 +115,30 @@ def test_pool_fc(B, H, C, N):
     ref = V.pool_fc_ref(x, pc)
     assert y.shape == (B, N)
     assert ((y.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+@pytest.mark.parametrize("cfg,kw", [(3, 2), (0, 4), (4, 1)])
+@pytest.mark.parametrize("stride2", [False, True])
+def test_conv_pair_grouped_launch(cfg, kw, stride2):
+    """conv2_kernel (downsample + conv1 in one launch) == the two single launches, bitwise."""
+    import ctypes
+    from hipzap import _native as N
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(1, 14, 14, 256, generator=g).to(torch.bfloat16).to(DEV)
+    pa = C.pack_conv(torch.randn(512, 256, 1, 1, generator=g) * 0.05, None, None, 2 if stride2 else 1, 0).to(DEV)
+    pb = C.pack_conv(torch.randn(128, 256, 3 if stride2 else 1, 3 if stride2 else 1, generator=g) * 0.05, None,
+                     None, 2 if stride2 else 1, 1 if stride2 else 0).to(DEV)
+    ya = C.conv2d_nhwc(x, pa, act="none", cfg=cfg, kw=kw)
+    yb = C.conv2d_nhwc(x, pb, act="relu", cfg=cfg, kw=kw)
+    xb = C.to_blocked(x)
+    outs, prms = [], []
+    for pc, act in ((pa, "none"), (pb, "relu")):
+        p = (14 + 2 * pc.pad - pc.r) // pc.stride + 1
+        o = torch.empty(p * p * pc.cout, device=DEV, dtype=torch.bfloat16)
+        prm, _, _ = C.make_params(xb.data_ptr(), pc, 1, 14, 14, o.data_ptr(), 0, act, False, cfg, kw)
+        outs.append((o, (1, p, p, pc.cout)))
+        prms.append(prm)
+    N.check(N.lib().hz_conv2_launch(ctypes.byref(prms[0]), ctypes.byref(prms[1]), cfg, N.stream_ptr()), "conv2")
+    torch.cuda.synchronize()
+    assert torch.equal(C.from_blocked(outs[0][0], outs[0][1]), ya)
+    assert torch.equal(C.from_blocked(outs[1][0], outs[1][1]), yb)
