@@ -209,11 +209,19 @@ extern "C" int hz_quant_launch(const HzQuantParams* pp, hipStream_t st) {
 //     search to make the 16 rows of every ds_read_b128 lane group hit 16 distinct bank slots
 //     for this kernel's chunk pattern 2*(l>>4)+half);
 //   * 3 LDS stages, counted vmcnt + raw s_barrier, as csrc/gemm.hip.
+namespace {
+
 constexpr unsigned MX_SWZ = 0x32765410u;  // nibble i = f(i)
 __device__ __forceinline__ int mx_swz(int i) { return (MX_SWZ >> (4 * i)) & 7; }
 
 typedef __attribute__((address_space(3))) void lds_void8;
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// (a __device__ wrapper: called directly in the template kernel body, the builtin made hipcc drop
+// the kernel's host stub without a diagnostic — undefined symbol at dlopen)
+__device__ __forceinline__ void glds16_8(const void* g, char* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void8*)lds, 16, 0, 0);
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vm8() {
@@ -252,13 +260,12 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
     char* base = smem + buf * SBYTES;
 #pragma unroll
     for (int i = 0; i < XPW; ++i)
-      __builtin_amdgcn_global_load_lds(xsrc[i] + st * 128, (lds_void8*)(base + (wave + 4 * i) * 1024), 16, 0, 0);
+      glds16_8(xsrc[i] + st * 128, base + (wave + 4 * i) * 1024);
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
       const int piece = wave + 4 * i;  // = g * 2 + half
       const int g = piece >> 1, h = piece & 1;
-      __builtin_amdgcn_global_load_lds(wsrc + ((long)g * kb + st) * 2048 + h * 1024,
-                                       (lds_void8*)(base + XBYTES + piece * 1024), 16, 0, 0);
+      glds16_8(wsrc + ((long)g * kb + st) * 2048 + h * 1024, base + XBYTES + piece * 1024);
     }
   };
 
@@ -355,6 +362,8 @@ int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
   hipLaunchKernelGGL((gemm_mx_kernel<BM, BN>), dim3(tiles), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
+
+}  // namespace
 
 extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
   const HzGemmFp8Params& p = *pp;

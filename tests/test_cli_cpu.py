@@ -104,3 +104,14 @@ def test_tracing_ranges():
     with trace_range("b", t):
         pass
     assert set(t.phases) == {"a", "b"} and "a=" in t.header()
+
+
+def test_native_library_links():
+    """libhipzap.so must dlopen with every symbol resolved (no GPU needed): catches kernels whose
+    host stubs were silently not emitted, before a GPU box sees it."""
+    import ctypes
+    from hipzap import _native as N
+    lib = N.lib()
+    for sym in ("hz_conv_launch", "hz_conv2_launch", "hz_gemm_lds_launch", "hz_launch_kernel", "hz_prog_add_kernel",
+                "hz_gemm_fp8_launch", "hz_softmax_launch", "hz_pool_fc_launch"):
+        assert isinstance(getattr(lib, sym), ctypes._CFuncPtr)
