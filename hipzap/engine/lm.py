@@ -174,3 +174,35 @@ class LMEngine:
                 self.prog = None
         except Exception:
             pass
+
+
+class LMPool:
+    """N independent decode contexts (own stream, recurrent state, token buffer, captured step
+    graph) over ONE packed weight set: concurrent GET /inference requests run in parallel instead
+    of queueing on one model's lock (SURVEY.md §8 P10 "per-request state buffers make it
+    reentrant"). A request takes an idle context, resets its state and returns it when done."""
+
+    def __init__(self, packed: dict, device="cuda:0", contexts: int = 4, **kw):
+        import queue
+        self.engines = [LMEngine(packed, device, **kw) for _ in range(max(1, contexts))]
+        self._idle = queue.Queue()
+        for e in self.engines:
+            self._idle.put(e)
+
+    @classmethod
+    def for_vocab(cls, sd: dict, stoi: dict, device="cuda:0", contexts: int = 4, **kw) -> "LMPool":
+        ex = [stoi[w] for w in EXCLUDE_TOKENS if w in stoi]
+        return cls(pack_awd_lstm(sd, device), device, contexts, exclude_ids=ex, **kw)
+
+    def _run(self, fn):
+        e = self._idle.get()
+        try:
+            return fn(e)
+        finally:
+            self._idle.put(e)
+
+    def generate(self, prompt_words, n_words, itos, stoi, seed=None) -> str:
+        return self._run(lambda e: e.generate(prompt_words, n_words, itos, stoi, seed))
+
+    def run_tokens(self, prompt_ids: list, n_words: int, seed: int = 0) -> list:
+        return self._run(lambda e: e.run_tokens(prompt_ids, n_words, seed))

@@ -157,8 +157,8 @@ class LMBackend:
         self.itos, self.stoi = itos, make_stoi(itos)
         self.backend = backend
         if backend == "gpu":
-            from ..engine.lm import LMEngine
-            self.engine = LMEngine.for_vocab(sd, self.stoi, device)
+            from ..engine.lm import LMPool
+            self.engine = LMPool.for_vocab(sd, self.stoi, device, contexts=int(os.environ.get("HIPZAP_LM_CONTEXTS", 4)))
             self.model = None
         else:
             self.model = reference_lm(len(itos))
@@ -170,9 +170,9 @@ class LMBackend:
 
     def generate(self, prompt_words, n_words, seed=None) -> str:
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
-        with self._lock:  # the recurrent state makes one model non-reentrant
-            if self.engine is not None:
-                return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)
+        if self.engine is not None:  # pool of independent decode contexts: reentrant
+            return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)
+        with self._lock:  # the eager CPU model's recurrent state makes it non-reentrant
             with torch.no_grad():
                 def step(tok):
                     res, *_ = self.model(torch.tensor([[tok]]))

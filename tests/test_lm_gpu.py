@@ -88,3 +88,16 @@ def test_generate_text_reference_config(model):
     a = eng.generate([""], 200, itos, stoi, seed=7)
     b = eng.generate([""], 200, itos, stoi, seed=7)
     assert a == b and len(a.split()) >= 150
+
+
+def test_pool_concurrent_requests_match_serial(model):
+    """LMPool: concurrent requests on independent contexts give the same tokens as serial runs."""
+    from concurrent.futures import ThreadPoolExecutor
+    from hipzap.engine.lm import LMPool
+    from hipzap.engine.lm import pack_awd_lstm
+    pool = LMPool(pack_awd_lstm(model.state_dict(), DEV), DEV, contexts=3)
+    jobs = [([5, 6, 7], 40, s) for s in range(6)]
+    serial = [pool.run_tokens(p, n, s) for p, n, s in jobs]
+    with ThreadPoolExecutor(6) as ex:
+        conc = list(ex.map(lambda j: pool.run_tokens(*j), jobs))
+    assert conc == serial
