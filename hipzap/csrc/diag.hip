@@ -17,7 +17,7 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src
 // Operand-layout probe for v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit E8M0 scales):
 // ab = [A: 16 rows x 128 k][B^T: 16 cols x 128 k] bytes; lane l loads byte j of its operand
 // from k = kmap(layout, l, j); C is written through the standard 16x16 C/D map. The host test
-// (tests/test_fp8_gpu.py) finds the layout whose result equals A @ B (exact small integers).
+// (tests/test_fp8_gpu.py) checks which (A map, B map) combinations give A @ B exactly.
 __device__ __forceinline__ int probe_k(int layout, int l, int j) {
   if (layout == 0) return 32 * (l >> 4) + j;                   // 32 consecutive k per lane
   return 8 * (l >> 4) + 32 * (j >> 3) + (j & 7);               // 4 blocks of the 16x16x32 map
@@ -28,10 +28,9 @@ __global__ void probe_mfma_f8_kernel(const unsigned char* ab, float* c, int layo
   i32x8 a, b;
   unsigned char* pa = reinterpret_cast<unsigned char*>(&a);
   unsigned char* pb = reinterpret_cast<unsigned char*>(&b);
-  for (int j = 0; j < 32; ++j) {
-    const int k = probe_k(layout, l, j);
-    pa[j] = ab[(l & 15) * 128 + k];
-    pb[j] = ab[2048 + (l & 15) * 128 + k];
+  for (int j = 0; j < 32; ++j) {  // layout bit 0: A's lane->k map, bit 1: B's
+    pa[j] = ab[(l & 15) * 128 + probe_k(layout & 1, l, j)];
+    pb[j] = ab[2048 + (l & 15) * 128 + probe_k((layout >> 1) & 1, l, j)];
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);

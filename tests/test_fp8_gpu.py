@@ -82,35 +82,14 @@ def _probe_f8f6f4(layout: int, A: torch.Tensor, Bt: torch.Tensor) -> torch.Tenso
 
 
 def test_mfma_f8f6f4_operand_layout():
-    """Pins the lane->k map of v_mfma_scale_f32_16x16x128_f8f6f4 (layout 0: lane l holds
-    k = 32*(l>>4) + j) that csrc/fp8.hip's MX GEMM relies on, with exact small integers."""
+    """What csrc/fp8.hip's MX GEMM relies on (unit block scales): the hardware applies the SAME
+    lane->k permutation to A and B, so any map used consistently for both operands (weights
+    MX-packed, activations gathered with the same map) yields the exact dot product, and mixing
+    two different maps does not (exact small integers, so equality is exact)."""
     g = torch.Generator().manual_seed(7)
     A = torch.randint(-3, 4, (16, 128), generator=g).float()
     Bt = torch.randint(-3, 4, (16, 128), generator=g).float()
     ref = A @ Bt.t()
-    got = {lay: _probe_f8f6f4(lay, A, Bt) for lay in (0, 1)}
-    match = [lay for lay, c in got.items() if torch.equal(c, ref)]
-    assert match == [0], {lay: (c - ref).abs().max().item() for lay, c in got.items()}
-
-
-@pytest.mark.parametrize("cfg", [16, 17, 18, 19])
-@pytest.mark.parametrize("M,N,K,act,res", [(1576, 2304, 768, "none", False), (200, 768, 3072, "gelu", True),
-                                            (64, 132, 128, "none", True)])
-def test_gemm_mx_fp8(cfg, M, N, K, act, res):
-    """LDS-tiled MX fp8 GEMM (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales) == the
-    fp8 oracle: same quantised operands, fp32 accumulation, per-row x per-channel scales."""
-    g = torch.Generator().manual_seed(8)
-    w = torch.randn(N, K, generator=g) * 0.05
-    b = torch.randn(N, generator=g)
-    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
-    r = torch.randn(M, N, generator=g).to(torch.bfloat16) if res else None
-    pw = F8.quantize_linear(C.pack_linear(w, b))
-    assert pw.w8mx is not None
-    pwd = F8.PackedFp8(pw.w8.to(DEV), pw.sw.to(DEV), pw.bias.to(DEV), pw.cin, pw.cout, pw.w8mx.to(DEV))
-    x8, sx = F8.quant_rows(x.to(DEV))
-    y = F8.gemm_fp8(x8, sx, pwd, residual=None if r is None else r.to(DEV), act=act, cfg=cfg, kw=1)
-    xd, _ = F8.quant_rows_ref(x)
-    ref = xd @ pw.dequant().t() + b + (r.float() if res else 0)
-    ref = torch.nn.functional.gelu(ref) if act == "gelu" else ref
-    rel = ((y.float().cpu() - ref).abs().max() / ref.abs().max()).item()
-    assert rel < 2e-2, rel
+    assert torch.equal(_probe_f8f6f4(0, A, Bt), ref)   # both operands: 32 consecutive k per lane
+    assert torch.equal(_probe_f8f6f4(3, A, Bt), ref)   # both operands: 4 blocks of the 16x16x32 map
+    assert not torch.equal(_probe_f8f6f4(1, A, Bt), ref)  # inconsistent maps are detected
