@@ -185,7 +185,7 @@ def main():
         timings = {}
         if rank == 0:
             ta = time.perf_counter()
-            sd = torch.load(ckpt, map_location="cpu", weights_only=True)
+            sd = torch.load(ckpt, map_location="cpu", weights_only=True, mmap=True)
             timings["load_ms"] = (time.perf_counter() - ta) * 1e3
             ta = time.perf_counter()
             sd = {k: v.to(device, non_blocking=True) for k, v in sd.items()}
@@ -194,8 +194,11 @@ def main():
             timings["pack_ms"] = (time.perf_counter() - ta) * 1e3
         else:
             params, arch_kw = None, None
-        meta, meta_kw = adapter.meta_params()
-        arch_kw = dict(arch_kw or meta_kw)
+        if arch_kw is None:  # receiving rank: shapes from a meta-device construction
+            meta, arch_kw = adapter.meta_params()
+        else:
+            meta = None
+        arch_kw = dict(arch_kw)
         if args.input == "uint8" and args.model.startswith("resnet"):
             arch_kw["input_uint8"] = True
         ta = time.perf_counter()

@@ -97,7 +97,7 @@ class Engine:
     @classmethod
     def from_checkpoint(cls, model: str, path: str, device="cuda:0", **kw) -> "Engine":
         t0 = time.perf_counter()
-        sd = torch.load(path, map_location="cpu", weights_only=True)
+        sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True)
         if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
             sd = sd["state_dict"]
         timings = {"load_ms": (time.perf_counter() - t0) * 1e3}

@@ -87,22 +87,26 @@ def unpack_blob(blob: torch.Tensor, meta_params: dict) -> dict:
     return {k: _rebuild(meta_params[k], fields[k]) for k in meta_params}
 
 
-def broadcast_params(params: dict | None, meta_params: dict, device, src: int = 0, group=None) -> dict:
+def broadcast_params(params: dict | None, meta_params, device, src: int = 0, group=None) -> dict:
     """C1: rank ``src`` sends its packed params; every rank returns params on ``device``.
 
     The blob is broadcast as one message, so it streams over every xGMI link at once
-    instead of paying per-tensor launch latency 100+ times.
+    instead of paying per-tensor launch latency 100+ times. ``meta_params`` (the shapes, as
+    meta tensors) is only needed on the receiving ranks and may be a zero-argument callable so
+    the source rank and single-process runs never build it (it costs a model construction).
     """
-    _, total = flat_layout(meta_params)
     if not is_dist():
         return params
     rank = dist.get_rank()
     if rank == src:
         blob = pack_blob(params, device)
-    else:
-        blob = torch.empty(total, dtype=torch.uint8, device=device)
+        dist.broadcast(blob, src=src, group=group)
+        return params
+    meta = meta_params() if callable(meta_params) else meta_params
+    _, total = flat_layout(meta)
+    blob = torch.empty(total, dtype=torch.uint8, device=device)
     dist.broadcast(blob, src=src, group=group)
-    return unpack_blob(blob, meta_params)
+    return unpack_blob(blob, meta)
 
 
 def health_check(device=None) -> int:
