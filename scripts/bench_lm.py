@@ -59,7 +59,19 @@ def main():
         r = c.get("/inference")
         http.append(time.perf_counter() - t)
         assert r.status_code == 200
+    # concurrent requests: LMPool of independent decode contexts sharing the packed weights
+    from concurrent.futures import ThreadPoolExecutor
+    from hipzap.engine.lm import LMPool
+    conc = int(os.environ.get("HIPZAP_LM_CONTEXTS", 4))
+    pool = LMPool(eng.p, "cuda:0", contexts=conc, exclude_ids=[])
+    n_req = 4 * conc
+    with ThreadPoolExecutor(conc) as ex:
+        list(ex.map(lambda s: pool.run_tokens([1], words, s), range(conc)))  # warm
+        t = time.perf_counter()
+        list(ex.map(lambda s: pool.run_tokens([1], words, s), range(n_req)))
+        pool_rps = n_req / (time.perf_counter() - t)
     res = {"metric": "AWD-LSTM GET /inference latency (200 words)", "vocab": V, "words": words,
+           "concurrent_contexts": conc, "requests_per_s_concurrent": round(pool_rps, 2),
            "cold_start_ms": round(cold_ms, 1), "request_s_p50": round(p50, 5),
            "ms_per_token": round(p50 / (words) * 1e3, 4), "http_request_s_p50": round(statistics.median(http), 5),
            "speedup_vs_reference_cpu": round(REFERENCE_REQUEST_S / statistics.median(http), 1),

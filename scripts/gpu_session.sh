@@ -30,6 +30,7 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
   mkdir -p $OUT/tuning && cp hipzap/tuning/*.json $OUT/tuning/
 }
 [[ $STEPS == *models* ]] && step bench_models 900 python scripts/bench_models.py
+[[ $STEPS == *lm* ]] && step bench_lm 600 python scripts/bench_lm.py
 [[ $STEPS == *bench* || $STEPS == all ]] && {
   for s in ${BENCH_STREAMS:-1 4 8}; do
     step bench_s$s 300 python bench.py --streams $s --steps 300 --warmup 30 --cold-runs 2 ${BENCH_EXTRA:-}
@@ -38,5 +39,6 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
 }
 [[ $STEPS == *prof* || $STEPS == all ]] && {
   step rocprof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --streams 1 --steps 50 --warmup 5 --cold-runs 0
+  python scripts/trace_summary.py $OUT/prof $OUT/prof_summary && rm -rf $OUT/prof
 }
 echo "=== done"

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Summarise a `rocprofv3 --kernel-trace --stats --output-format csv` run of bench.py.
+
+Writes (into the output dir): kernel_stats.csv (copied), one_inference_trace.txt (the
+dispatch timeline of one steady-state inference: from one preprocess kernel to the next, with
+start offset, duration, grid and workgroup sizes, VGPRs) and a short summary on stdout.
+Usage: trace_summary.py <rocprof -d dir> <out dir>
+"""
+import csv
+import glob
+import os
+import shutil
+import sys
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    os.makedirs(out, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)
+    traces = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, "kernel_stats.csv"))
+    if not traces:
+        print("no kernel trace found")
+        return
+    rows = list(csv.DictReader(open(traces[0])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
+    if len(starts) < 4:
+        print("too few inferences in trace")
+        return
+    mid = len(starts) // 2
+    seg = rows[starts[mid]: starts[mid + 1]]
+    t0 = int(seg[0]["Start_Timestamp"])
+    lines = ["# one steady-state inference: start_us dur_us grid wg vgpr kernel"]
+    busy = 0
+    for r in seg:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        busy += e - s
+        name = r["Kernel_Name"][:110]
+        lines.append(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} grid={r.get('Grid_Size', '?'):>7} "
+                     f"wg={r.get('Workgroup_Size', '?'):>5} vgpr={r.get('VGPR_Count', r.get('Arch_VGPR_Count', '?')):>4} "
+                     f"{name}")
+    span = (int(seg[-1]["End_Timestamp"]) - t0) / 1e3
+    lines.append(f"# {len(seg)} dispatches, span {span:.1f} us, kernel-busy {busy / 1e3:.1f} us "
+                 "(profiled; durations inflate under the profiler)")
+    with open(os.path.join(out, "one_inference_trace.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print(lines[-1])
+
+
+if __name__ == "__main__":
+    main()
