@@ -228,13 +228,12 @@ __device__ __forceinline__ void wait_vm8() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;
   constexpr int NWG = BN / 16;                // weight fragments (2 KiB) per stage
   constexpr int XBYTES = BM * 128;
   constexpr int SBYTES = XBYTES + NWG * 2048;
-  constexpr int NS = 3;
   constexpr int XPW = BM / 32, WPW = NWG * 2 / 4;  // glds pieces per wave per stage
   constexpr int G = XPW + WPW;
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
@@ -282,14 +281,15 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage(0, 0);
-  if (kb > 1) stage(1, 1);
+  if (NS > 2 && kb > 1) stage(1, 1);
   int cur = 0;
   for (int st = 0; st < kb; ++st) {
-    if (st + 1 < kb) wait_vm8<G>();
+    // stages issued ahead of st: min(NS-2, kb-1-st) may stay in flight
+    if (NS > 2 && st + 1 < kb) wait_vm8<(NS > 2 ? G : 0)>();
     else wait_vm8<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + 2 < kb) stage(cur == 0 ? 2 : cur - 1, st + 2);
+    if (st + NS - 1 < kb) stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
     const char* base = smem + cur * SBYTES;
     i32x8 a[FCW], b[FPW];
 #pragma unroll
@@ -356,10 +356,10 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NS>
 int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_mx_kernel<BM, BN>), dim3(tiles), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS>), dim3(tiles), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -370,10 +370,14 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
   if (p.cfg >= 16) {
     if (!p.wmx || p.K % 128 || p.ldx % 16 || p.N % 4) return -1;
     switch (p.cfg) {
-      case 16: return launch_mx<128, 128>(p, st);
-      case 17: return launch_mx<64, 128>(p, st);
-      case 18: return launch_mx<128, 64>(p, st);
-      case 19: return launch_mx<64, 64>(p, st);
+      case 16: return launch_mx<128, 128, 3>(p, st);
+      case 20: return launch_mx<128, 128, 2>(p, st);
+      case 17: return launch_mx<64, 128, 3>(p, st);
+      case 21: return launch_mx<64, 128, 2>(p, st);
+      case 18: return launch_mx<128, 64, 3>(p, st);
+      case 22: return launch_mx<128, 64, 2>(p, st);
+      case 19: return launch_mx<64, 64, 3>(p, st);
+      case 23: return launch_mx<64, 64, 2>(p, st);
       default: return -2;
     }
   }

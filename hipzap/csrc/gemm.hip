@@ -36,13 +36,12 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;  // 16x16 fragments per wave (2x2 waves)
   constexpr int NWG = BN / 16;                 // weight fragments per 32-deep k-step
   constexpr int XBYTES = BM * 128;             // activation bytes per stage (BK = 64 bf16 = 128 B)
   constexpr int SBYTES = XBYTES + BN * 128;    // + 2 k-steps x NWG fragments x 1 KiB
-  constexpr int NS = 3;
   constexpr int XPW = BM / 32, WPW = BN / 32;  // glds pieces per wave per stage (x, w)
   constexpr int G = XPW + WPW;
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
@@ -91,14 +90,15 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage(0, 0);
-  if (nst > 1) stage(1, 1);
+  if (NS > 2 && nst > 1) stage(1, 1);
   int cur = 0;
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) wait_vm<G>();
+    // stages issued ahead of st: min(NS-2, nst-1-st) may stay in flight
+    if (NS > 2 && st + 1 < nst) wait_vm<(NS > 2 ? G : 0)>();
     else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + 2 < nst) stage(cur == 0 ? 2 : cur - 1, st + 2);
+    if (st + NS - 1 < nst) stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
     const char* base = smem + cur * SBYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -156,24 +156,29 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NS>
 int launch_lds(const HzConvParams& p, hipStream_t st) {
   const int tiles = ((p.Cout + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_lds_kernel<BM, BN>), dim3(tiles), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS>), dim3(tiles), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// cfg 16: 128x128, 17: 64x128 (BM x BN), 18: 128x64, 19: 64x64; row-major activations only.
+// cfg 16: 128x128, 17: 64x128 (BM x BN), 18: 128x64, 19: 64x64 with 3 LDS stages; cfg 20-23: the same
+// tiles with 2 stages (less LDS: more workgroups per CU). Row-major activations only.
 extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
   if (!p.x_rowmajor || !p.out_rowmajor || p.K % 64 || p.ksteps * 32 != p.K || p.ldx % 8 || p.Cout % 4) return -1;
   switch (cfg) {
-    case 16: return launch_lds<128, 128>(p, st);
-    case 17: return launch_lds<64, 128>(p, st);
-    case 18: return launch_lds<128, 64>(p, st);
-    case 19: return launch_lds<64, 64>(p, st);
+    case 16: return launch_lds<128, 128, 3>(p, st);
+    case 20: return launch_lds<128, 128, 2>(p, st);
+    case 17: return launch_lds<64, 128, 3>(p, st);
+    case 21: return launch_lds<64, 128, 2>(p, st);
+    case 18: return launch_lds<128, 64, 3>(p, st);
+    case 22: return launch_lds<128, 64, 2>(p, st);
+    case 19: return launch_lds<64, 64, 3>(p, st);
+    case 23: return launch_lds<64, 64, 2>(p, st);
     default: return -2;
   }
 }

@@ -92,7 +92,9 @@ def quantize_linear(pc: PackedConv) -> PackedFp8:
     return PackedFp8(fragment_major(q).contiguous(), sw.contiguous(), pc.bias.float().contiguous(), pc.K, pc.cout, mx)
 
 
-MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64)}  # cfg -> (BM, BN), csrc/fp8.hip
+# cfg -> (BM, BN), csrc/fp8.hip gemm_mx_kernel; 16-19: 3 LDS stages, 20-23: 2 stages
+MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
+            20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64)}
 
 
 def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
