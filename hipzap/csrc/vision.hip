@@ -69,24 +69,28 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__
 }
 
 // Fused global-average-pool + FC (one launch instead of avgpool + FC GEMM + a kernel boundary).
-// Block = 4 waves, 4 x 16 output rows, one image (blockIdx.y). Phase 1: every block pools all C
-// channels of its image into LDS (fp32; C*HW*2 bytes, L2-resident after the first block):
-// lane l reads 16 B (8 channels) of channel block 16*wave' + (l>>2) at every pixel — 16 disjoint
-// 64-B runs per instruction, no cross-lane reduction. Phase 2: each wave streams its 16-row
-// weight group (fragment-major: one contiguous 1 KiB per 32-deep k-step) and dots it with the
-// pooled vector; the 4 lanes sharing a row (l, l^16, l^32, l^48) reduce with 2 shuffles.
+// Block = one 16-row weight group x one image (blockIdx.y); its 4 waves split the channels
+// (K) four ways, so each wave pools ONLY its own C/4 channels (fp32, into its LDS slice) and
+// then dots them with its K-quarter of the group's weights; the 4 partial sums meet in LDS.
+// Pooling: lane l reads 16 B (8 channels) of channel block (l>>2) of the wave's slice at every
+// pixel, 16 pixels in flight per lane. Weights are fragment-major (one contiguous 1 KiB per
+// 32-deep k-step); the 4 lanes sharing an output row (l, l^16, l^32, l^48) reduce by shuffles.
+// A first version with 16 blocks x 4 full-K groups took 11.7 us (profiled) — per-wave serial
+// latency; this one has N/16 blocks with 1/4 of the chain each.
 __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
-  extern __shared__ __attribute__((aligned(16))) float pooled[];  // [C]
+  extern __shared__ __attribute__((aligned(16))) float pooled[];  // [C] + [4][16] partials
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int b = blockIdx.y;
+  const int b = blockIdx.y, g = blockIdx.x;
   const int ncb = p.C >> 5;
+  const int cpw = (ncb + 3) >> 2;  // channel blocks per wave
+  const int cb_lo = wave * cpw, cb_hi = min(ncb, cb_lo + cpw);
   const float inv = 1.f / p.HW;
-  for (int cb0 = wave * 16; cb0 < ncb; cb0 += 64) {
+  for (int cb0 = cb_lo; cb0 < cb_hi; cb0 += 16) {
     const int cb = cb0 + (lane >> 2), sub = lane & 3;
-    if (cb < ncb) {
+    if (cb < cb_hi) {
       const bf16_t* src = p.x + (((long)b * ncb + cb) * p.HW) * 32 + sub * 8;
       float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 7
+#pragma unroll 16
       for (int hw = 0; hw < p.HW; ++hw) {
         float f[8];
         unpack8(*reinterpret_cast<const u32x4*>(src + hw * 32), f);
@@ -97,15 +101,16 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
       for (int e = 0; e < 8; ++e) pooled[cb * 32 + sub * 8 + e] = s[e] * inv;
     }
   }
-  __syncthreads();
-  const int g = blockIdx.x * 4 + wave;  // 16-row weight group
-  if (g * 16 >= p.N) return;
+  // the wave reads back only its own slice: a wave-level LDS fence is enough
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int ks = p.C >> 5;
   const bf16_t* wg = p.w + ((long)g * ks * 64 + lane) * 8;
   const float* pl = pooled + (lane >> 4) * 8;
   float acc = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < ks; ++k) {
+#pragma unroll 16
+  for (int k = cb_lo; k < cb_hi; ++k) {
     float f[8];
     unpack8(*reinterpret_cast<const u32x4*>(wg + (long)k * 512), f);
     const f32x4 p0 = *reinterpret_cast<const f32x4*>(pl + k * 32);
@@ -115,8 +120,12 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   }
   acc += __shfl_xor(acc, 16, 64);
   acc += __shfl_xor(acc, 32, 64);
-  const int n = g * 16 + lane;
-  if (lane < 16 && n < p.N) p.out[(long)b * p.ldo + n] = acc + (p.bias ? p.bias[n] : 0.f);
+  float* part = pooled + p.C;  // [4 waves][16 rows]
+  if (lane < 16) part[wave * 16 + lane] = acc;
+  __syncthreads();
+  const int n = g * 16 + t;
+  if (t < 16 && n < p.N)
+    p.out[(long)b * p.ldo + n] = part[t] + part[16 + t] + part[32 + t] + part[48 + t] + (p.bias ? p.bias[n] : 0.f);
 }
 
 // mode 0: src fp32 NCHW (already normalised unless mean/inv_std given)
@@ -177,7 +186,7 @@ extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
   const HzPoolFcParams& p = *pp;
   if (p.C % 32 || p.C > 16384 || p.HW < 1 || p.N < 1) return -1;
   const int groups = (p.N + 15) / 16;
-  hipLaunchKernelGGL(pool_fc_kernel, dim3((groups + 3) / 4, p.B), dim3(256), (size_t)p.C * sizeof(float), st, p);
+  hipLaunchKernelGGL(pool_fc_kernel, dim3(groups, p.B), dim3(256), (size_t)(p.C + 64) * sizeof(float), st, p);
   return (int)hipGetLastError();
 }
 
