@@ -41,4 +41,11 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
   step rocprof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --streams 1 --steps 50 --warmup 5 --cold-runs 0
   python scripts/trace_summary.py $OUT/prof $OUT/prof_summary && rm -rf $OUT/prof
 }
+[[ $STEPS == *txprof* ]] && {
+  for mb in "bert-base 16" "vit-b16 8" "vit-b16-fp8 8"; do
+    set -- $mb
+    step prof_$1 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$1 -o run --output-format csv -- python3 scripts/prof_model.py --model $1 --batch $2 --iters 20
+    python scripts/trace_summary.py $OUT/prof_$1 $OUT/prof_summary_$1; rm -rf $OUT/prof_$1
+  done
+}
 echo "=== done"
