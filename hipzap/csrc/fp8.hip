@@ -52,6 +52,8 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) 
   if (lane == 0) p.scale[row] = scale;
 }
 
+__device__ __attribute__((aligned(64))) unsigned int g_zero8[16] = {0};
+
 template <int FC, int FP>
 struct Depth8 {
   static constexpr int value = (FC + FP <= 2) ? 8 : (FC + FP <= 3) ? 6 : (FC + FP <= 4) ? 4 : 3;
@@ -86,25 +88,28 @@ __global__ __launch_bounds__(fp8_max_threads(FC * FP)) void gemm_fp8_kernel(cons
 #pragma unroll
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // branch-free loads (zero bytes for invalid lanes / steps): see conv.hip load_step
+  const unsigned char* __restrict__ Z = reinterpret_cast<const unsigned char*>(g_zero8);
   auto load_step = [&](int t, long(&a)[FC], long(&b)[FP]) {
+    const bool sv = t < nsteps;
     const int s_idx = s_begin + t;
     const int kk = s_idx * 32 + lk;
 #pragma unroll
-    for (int i = 0; i < FC; ++i) a[i] = *reinterpret_cast<const long*>(Wf + ((long)i * steps + s_idx) * 512);
+    for (int i = 0; i < FC; ++i)
+      a[i] = *reinterpret_cast<const long*>(sv ? Wf + ((long)i * steps + s_idx) * 512 : Z);
 #pragma unroll
     for (int j = 0; j < FP; ++j) {
-      if (pval[j] && kk < p.K) b[j] = *reinterpret_cast<const long*>(p.x + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
-      else b[j] = 0;
+      const bool v = sv && pval[j] && kk < p.K;
+      b[j] = *reinterpret_cast<const long*>(v ? p.x + (long)(m0 + j * 16 + lrow) * p.ldx + kk : Z);
     }
   };
 #pragma unroll
-  for (int u = 0; u < DEPTH; ++u)
-    if (u < nsteps) load_step(u, fa[u], fb[u]);
+  for (int u = 0; u < DEPTH; ++u) load_step(u, fa[u], fb[u]);
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
       const int tt = t + u;
-      if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
+      load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
       if (tt < nsteps) {
 #pragma unroll
         for (int i = 0; i < FC; ++i)
