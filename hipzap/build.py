@@ -62,6 +62,10 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, srcs))
+    live = {o.name for o in objs}
+    for stale in OBJDIR.glob("*.o"):  # objects of older source versions
+        if stale.name not in live:
+            stale.unlink(missing_ok=True)
     key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
     stamp = LIBDIR / ".buildkey"
     if LIB.exists() and stamp.exists() and stamp.read_text() == key:

@@ -48,4 +48,8 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
     python scripts/trace_summary.py $OUT/prof_$1 $OUT/prof_summary_$1; rm -rf $OUT/prof_$1
   done
 }
+[[ $STEPS == *lmprof* ]] && {
+  HIPZAP_LM_WORDS=50 step prof_lm 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_lm -o run --output-format csv -- python3 scripts/bench_lm.py
+  python scripts/trace_summary.py $OUT/prof_lm $OUT/prof_summary_lm; rm -rf $OUT/prof_lm
+}
 echo "=== done"
