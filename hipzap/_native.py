@@ -45,13 +45,14 @@ class LstmParams(C.Structure):
 
 class DecoderParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h_state", c_void_p), ("step", c_void_p),
-                ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int)]
+                ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
+                ("seed", c_void_p)]
 
 
 class SamplerParams(C.Structure):
     _fields_ = [("logits", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
                 ("seed", c_void_p), ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int),
-                ("exclude", c_int * 8)]
+                ("exclude", c_int * 8), ("keyed", c_int)]
 
 
 def _sig(lib, name, res, *args):

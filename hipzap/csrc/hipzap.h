@@ -83,6 +83,8 @@ typedef struct HzDecoderParams {
   const int* step;
   float* logits;              // [V]
   int V, H, ldk;
+  float* keys;                // optional [V]: logits + Gumbel(seed, step, row) for the sampler
+  const unsigned long long* seed;
 } HzDecoderParams;
 typedef struct HzSamplerParams {
   const float* logits;        // [V]
@@ -93,6 +95,7 @@ typedef struct HzSamplerParams {
   const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
   int V, n_exclude;
   int exclude[8];
+  int keyed;                  // 1: `logits` already holds the Gumbel-perturbed keys (decoder epilogue)
 } HzSamplerParams;
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);

@@ -23,41 +23,57 @@ namespace {
 constexpr int CHUNK = 8;  // bf16 per 16-B lane load
 
 // --------------------------------------------------------------------------- LSTM cell
+// NCH = ldk / 512 is a template parameter so every weight load of a wave (4 gate rows x NCH
+// 16-B chunks) is issued before the first use — with a runtime chunk loop hipcc waited
+// vmcnt(0) per chunk (one L2/HBM round trip each). The input staging likewise issues all of a
+// thread's loads first (address selects instead of branches around loads).
+template <int NCH>
 __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   extern __shared__ __attribute__((aligned(16))) float vin[];  // [ldk] = [x ; h_prev ; 0-pad]
+  constexpr int PER = NCH * 512 / 256;  // staged elements per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = *p.step;
   const int par = t & 1;
   const float* h_prev = p.h_state + par * p.H;
-  // ---- stage the input vector in LDS (fp32) ----
-  for (int i = tid; i < p.ldk; i += blockDim.x) {
-    float v = 0.f;
-    if (i < p.In) {
-      if (p.emb) {
-        const int tok = p.tok_seq[t];
-        v = bf2f(p.emb[(long)tok * p.lde + i]);
-      } else {
-        v = p.x_state[(par ^ 1) * p.In + i];  // previous layer's output of THIS step
-      }
-    } else if (i < p.In + p.H) {
-      v = h_prev[i - p.In];
-    }
-    vin[i] = v;
+  const int tok = p.emb ? p.tok_seq[t] : 0;
+  const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
+  const float* xprev = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
+  // ---- stage the input vector in LDS (fp32): all loads first, then the selects ----
+  float fv[PER];
+  unsigned short ev[PER];
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const int i = tid + r * 256;
+    const bool in_x = i < p.In, in_h = !in_x && i < p.In + p.H;
+    const float* fsrc = in_h ? h_prev + (i - p.In) : (in_x && !erow ? xprev + i : h_prev);
+    fv[r] = *fsrc;
+    ev[r] = erow ? erow[in_x ? i : 0] : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const int i = tid + r * 256;
+    const bool in_x = i < p.In, in_h = !in_x && i < p.In + p.H;
+    vin[i] = in_h ? fv[r] : in_x ? (erow ? bf2f(ev[r]) : fv[r]) : 0.f;
   }
   __syncthreads();
   const int j = blockIdx.x * 4 + wave;  // hidden unit of this wave
   if (j >= p.H) return;
-  const bf16_t* w = p.w + (long)(4 * j) * p.ldk;
+  const bf16_t* w = p.w + (long)(4 * j) * p.ldk + lane * 8;
+  u32x4 wv[4][NCH];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) wv[q][c] = *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + c * 512);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nchunk = p.ldk / (64 * CHUNK);
-  for (int c = 0; c < nchunk; ++c) {
-    const int k = (c * 64 + lane) * CHUNK;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(vin + k);
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(vin + k + 4);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float f[8];
-      unpack8(*reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + k), f);
+      unpack8(wv[q][c], f);
       acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
                 f[6] * v1[2] + f[7] * v1[3];
     }
@@ -76,41 +92,6 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
     const float h_new = so * tanhf(c_new);
     p.c_state[(par ^ 1) * p.H + j] = c_new;
     p.h_state[(par ^ 1) * p.H + j] = h_new;
-  }
-}
-
-// --------------------------------------------------------------------------- decoder GEMV
-__global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
-  extern __shared__ __attribute__((aligned(16))) float hv[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int par = (*p.step) & 1;
-  const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
-  for (int i = tid; i < p.ldk; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
-  __syncthreads();
-  const int nchunk = p.ldk / (64 * CHUNK);
-  const int nquads = (p.V + 3) >> 2;
-  for (int qd = blockIdx.x * 4 + wave; qd < nquads; qd += gridDim.x * 4) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nchunk; ++c) {
-      const int k = (c * 64 + lane) * CHUNK;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = min(qd * 4 + q, p.V - 1);
-        float f[8];
-        unpack8(*reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + k), f);
-        acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
-                  f[6] * v1[2] + f[7] * v1[3];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = warp_sum(acc[q]);
-    if (lane < 4) {
-      const int r = qd * 4 + lane;
-      const float a = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
-      if (r < p.V) p.logits[r] = a + (p.bias ? p.bias[r] : 0.f);
-    }
   }
 }
 
@@ -141,27 +122,101 @@ __device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
   return -__logf(-__logf(u));
 }
 
+// --------------------------------------------------------------------------- decoder GEMV
+// logits = E . h + b over the tied embedding (bf16 [V][ldk]). Each wave takes 8 rows per
+// iteration with all 8 x NCH 16-B loads in flight (NCH = ldk/512 is compile-time), then one
+// 64-lane reduction per row. With `keys`, the epilogue also writes logit + Gumbel(seed,t,row)
+// so the sampler only has to select (the Philox work is spread over the whole chip instead of
+// one workgroup).
+constexpr int DROWS = 8;
+template <int NCH>
+__global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
+  extern __shared__ __attribute__((aligned(16))) float hv[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = *p.step;
+  const int par = t & 1;
+  const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
+  for (int i = tid; i < p.ldk; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
+  __syncthreads();
+  const unsigned long long seed = p.keys ? *p.seed : 0ull;
+  const int ngroups = (p.V + DROWS - 1) / DROWS;
+  for (int g = blockIdx.x * 4 + wave; g < ngroups; g += gridDim.x * 4) {
+    u32x4 wv[DROWS][NCH];
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) {
+      const int r = min(g * DROWS + q, p.V - 1);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        wv[q][c] = *reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8);
+    }
+    float acc[DROWS];
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * 512 + lane * 8;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
+#pragma unroll
+      for (int q = 0; q < DROWS; ++q) {
+        float f[8];
+        unpack8(wv[q][c], f);
+        acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
+                  f[6] * v1[2] + f[7] * v1[3];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) acc[q] = warp_sum(acc[q]);
+    if (lane < DROWS) {
+      const int r = g * DROWS + lane;
+      float a = acc[0];
+#pragma unroll
+      for (int q = 1; q < DROWS; ++q) a = lane == q ? acc[q] : a;
+      if (r < p.V) {
+        const float lg = a + (p.bias ? p.bias[r] : 0.f);
+        p.logits[r] = lg;
+        if (p.keys) p.keys[r] = lg + gumbel(seed, t, r);
+      }
+    }
+  }
+}
+
 constexpr int TOPK = 10;
 
+// 64-lane argmax of (value, index) with ties to the lower index; every lane gets the result
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+
+// Hierarchical top-10: per-thread sorted top-10 (insertion) -> per-wave top-10 (10 rounds of
+// shuffle argmax over the lanes' list heads, no barriers) -> 16 x 10 candidates in LDS -> wave 0
+// merges them the same way. Two barriers in total (the previous version: 10 rounds of
+// block-wide argmax, 3 barriers each, plus the whole Philox stream on one workgroup).
 __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) {
-  __shared__ float s_val[32];
-  __shared__ int s_idx[32];
-  __shared__ int s_draw[TOPK];
+  __shared__ float c_val[16 * TOPK];
+  __shared__ int c_idx[16 * TOPK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int t = *p.step;
   const bool forced = (t + 1) < *p.n_forced;
   const unsigned long long seed = *p.seed;
   if (!forced) {
-    // local top-K of perturbed logits (sorted descending, insertion)
     float v[TOPK];
     int id[TOPK];
 #pragma unroll
     for (int q = 0; q < TOPK; ++q) {
       v[q] = -INFINITY;
-      id[q] = -1;
+      id[q] = 0x7fffffff;
     }
     for (int j = tid; j < p.V; j += blockDim.x) {
-      const float key = p.logits[j] + gumbel(seed, t, j);
+      const float key = p.keyed ? p.logits[j] : p.logits[j] + gumbel(seed, t, j);
       if (key > v[TOPK - 1]) {
         float cv = key;
         int ci = j;
@@ -178,11 +233,11 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
         }
       }
     }
-    // K rounds of block-wide argmax over the per-thread heads
+    // wave-level merge: the lane list heads compete; the winner pops its head
     int head = 0;
     for (int r = 0; r < TOPK; ++r) {
       float hv = -INFINITY;
-      int hi = -1;
+      int hi = 0x7fffffff;
 #pragma unroll
       for (int q = 0; q < TOPK; ++q)
         if (q == head) {
@@ -190,53 +245,65 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
           hi = id[q];
         }
       float bv = hv;
-      int bt = tid;
+      int bi = hi;
+      wave_argmax(bv, bi);
+      if (hv == bv && hi == bi) ++head;  // indices are unique: exactly one lane pops
+      if (lane == 0) {
+        c_val[wave * TOPK + r] = bv;
+        c_idx[wave * TOPK + r] = bi;
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      // each lane holds up to 3 candidates (nw * TOPK <= 160), kept sorted descending
+      float cv[3];
+      int ci[3];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int ot = __shfl_xor(bt, o, 64);
-        if (ov > bv || (ov == bv && ot < bt)) {
-          bv = ov;
-          bt = ot;
-        }
+      for (int q = 0; q < 3; ++q) {
+        const int e = lane + q * 64;
+        const bool ok = e < nw * TOPK;
+        cv[q] = ok ? c_val[e] : -INFINITY;
+        ci[q] = ok ? c_idx[e] : 0x7fffffff;
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = a + 1; b < 3; ++b)
+          if (cv[b] > cv[a] || (cv[b] == cv[a] && ci[b] < ci[a])) {
+            const float tv = cv[a];
+            const int ti = ci[a];
+            cv[a] = cv[b];
+            ci[a] = ci[b];
+            cv[b] = tv;
+            ci[b] = ti;
+          }
+      int hd = 0;
+      int draws[TOPK];
+#pragma unroll
+      for (int r = 0; r < TOPK; ++r) {
+        float hv = hd == 0 ? cv[0] : hd == 1 ? cv[1] : hd == 2 ? cv[2] : -INFINITY;
+        int hi = hd == 0 ? ci[0] : hd == 1 ? ci[1] : hd == 2 ? ci[2] : 0x7fffffff;
+        float bv = hv;
+        int bi = hi;
+        wave_argmax(bv, bi);
+        if (hv == bv && hi == bi) ++hd;
+        draws[r] = bi;
       }
       if (lane == 0) {
-        s_val[wave] = bv;
-        s_idx[wave] = bt;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        float best = s_val[0];
-        int bth = s_idx[0];
-        for (int w = 1; w < nw; ++w)
-          if (s_val[w] > best || (s_val[w] == best && s_idx[w] < bth)) {
-            best = s_val[w];
-            bth = s_idx[w];
+        int tok = draws[0];
+        for (int r = 0; r < TOPK && r < p.V; ++r) {
+          const int d = draws[r];
+          bool ex = d <= 0;
+          for (int e = 0; e < p.n_exclude; ++e) ex |= (d == p.exclude[e]);
+          if (!ex) {
+            tok = d;
+            break;
           }
-        s_idx[31] = bth;
-      }
-      __syncthreads();
-      const int winner = s_idx[31];
-      if (tid == winner) {
-        s_draw[r] = hi;
-        ++head;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      int tok = s_draw[0];
-      for (int r = 0; r < TOPK && r < p.V; ++r) {
-        const int d = s_draw[r];
-        bool ex = d <= 0;
-        for (int e = 0; e < p.n_exclude; ++e) ex |= (d == p.exclude[e]);
-        if (!ex) {
-          tok = d;
-          break;
         }
-      }
-      p.tok_seq[t + 1] = tok;
-      if (p.draws) {
-        for (int r = 0; r < TOPK; ++r) p.draws[(long)t * TOPK + r] = s_draw[r];
+        p.tok_seq[t + 1] = tok;
+        if (p.draws) {
+          for (int r = 0; r < TOPK; ++r) p.draws[(long)t * TOPK + r] = draws[r];
+        }
       }
     }
   }
@@ -249,16 +316,33 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
 extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   const HzLstmParams& p = *pp;
   if (p.ldk % 512 || p.ldk < p.In + p.H) return -1;
-  hipLaunchKernelGGL(lstm_cell_kernel, dim3((p.H + 3) / 4), dim3(256), p.ldk * sizeof(float), st, p);
+  const dim3 grid((p.H + 3) / 4), block(256);
+  const size_t lds = p.ldk * sizeof(float);
+  switch (p.ldk / 512) {
+    case 1: hipLaunchKernelGGL(lstm_cell_kernel<1>, grid, block, lds, st, p); break;
+    case 2: hipLaunchKernelGGL(lstm_cell_kernel<2>, grid, block, lds, st, p); break;
+    case 3: hipLaunchKernelGGL(lstm_cell_kernel<3>, grid, block, lds, st, p); break;
+    case 4: hipLaunchKernelGGL(lstm_cell_kernel<4>, grid, block, lds, st, p); break;
+    case 5: hipLaunchKernelGGL(lstm_cell_kernel<5>, grid, block, lds, st, p); break;
+    case 6: hipLaunchKernelGGL(lstm_cell_kernel<6>, grid, block, lds, st, p); break;
+    default: return -1;
+  }
   return (int)hipGetLastError();
 }
 
 extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const HzDecoderParams& p = *pp;
-  if (p.ldk % 512 || p.ldk < p.H) return -1;
-  const int quads = (p.V + 3) / 4;
-  const int blocks = min(2048, (quads + 3) / 4);
-  hipLaunchKernelGGL(decoder_kernel, dim3(blocks), dim3(256), p.ldk * sizeof(float), st, p);
+  if (p.ldk % 512 || p.ldk < p.H || (p.keys && !p.seed)) return -1;
+  const int groups = (p.V + DROWS - 1) / DROWS;
+  const dim3 grid(min(2048, (groups + 3) / 4)), block(256);
+  const size_t lds = p.ldk * sizeof(float);
+  switch (p.ldk / 512) {
+    case 1: hipLaunchKernelGGL(decoder_kernel<1>, grid, block, lds, st, p); break;
+    case 2: hipLaunchKernelGGL(decoder_kernel<2>, grid, block, lds, st, p); break;
+    case 3: hipLaunchKernelGGL(decoder_kernel<3>, grid, block, lds, st, p); break;
+    case 4: hipLaunchKernelGGL(decoder_kernel<4>, grid, block, lds, st, p); break;
+    default: return -1;
+  }
   return (int)hipGetLastError();
 }
 

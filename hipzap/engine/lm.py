@@ -85,6 +85,7 @@ class LMEngine:
             self.n_forced = torch.zeros(1, dtype=torch.int32, device=dev)
             self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
             self.logits = torch.zeros(packed["V"], device=dev)
+            self.keys = torch.zeros(packed["V"], device=dev)  # logits + Gumbel noise (decoder epilogue)
             self.draws = torch.full((max_steps, NUM_DRAWS), -1, dtype=torch.int32, device=dev) if record_draws else None
             self.prog = lib.hz_prog_create()
             for i, ly in enumerate(L):
@@ -105,9 +106,11 @@ class LMEngine:
             d.bias = N.ptr(packed["dec_bias"])
             d.h_state, d.step, d.logits = self.h[-1].data_ptr(), self.step.data_ptr(), self.logits.data_ptr()
             d.V, d.H, d.ldk = packed["V"], L[-1]["H"], packed["lde"]
+            d.keys, d.seed = self.keys.data_ptr(), self.seed.data_ptr()
             N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
             s = N.SamplerParams()
-            s.logits, s.tok_seq, s.step = self.logits.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
+            s.logits, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
+            s.keyed = 1
             s.draws = N.ptr(self.draws)
             s.seed, s.n_forced = self.seed.data_ptr(), self.n_forced.data_ptr()
             s.V = packed["V"]
