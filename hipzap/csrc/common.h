@@ -78,3 +78,12 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
   return (unsigned)w;
 }
+
+// OCP MX E8M0 block scale for e4m3 data: the exponent e of the smallest power of two with
+// amax / 2^e <= 448 (frexp: amax/448 = m * 2^e, m in [0.5, 1) => 2^e > amax/448); byte = e + 127.
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int e;
+  frexpf(amax * (1.f / 448.f), &e);
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}

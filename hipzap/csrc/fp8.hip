@@ -228,19 +228,28 @@ __device__ __forceinline__ void glds16_8(const void* g, char* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void8*)lds, 16, 0, 0);
 }
 
+__device__ __forceinline__ void glds4_8(const void* g, char* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void8*)lds, 4, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm8() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int NS>
+// XS: the activations carry MX block scales (p.xs, one E8M0 byte per 32 k): each wave also
+// stages one 4-byte-per-lane piece (64 rows x the 4 block scales of this 128-deep k-step) and
+// the scale goes to the MFMA's B-scale operand (lane l: token l&15, k-block l>>4 — the same
+// lane that holds those 32 bytes).
+template <int BM, int BN, int NS, bool XS>
 __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;
   constexpr int NWG = BN / 16;                // weight fragments (2 KiB) per stage
   constexpr int XBYTES = BM * 128;
-  constexpr int SBYTES = XBYTES + NWG * 2048;
+  constexpr int WBYTES = NWG * 2048;
+  constexpr int SBYTES = XBYTES + WBYTES + (XS ? 1024 : 0);
   constexpr int XPW = BM / 32, WPW = NWG * 2 / 4;  // glds pieces per wave per stage
-  constexpr int G = XPW + WPW;
+  constexpr int G = XPW + WPW + (XS ? 1 : 0);
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -260,8 +269,11 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
     xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
   }
   const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
+  // scale piece of this wave: rows (wave % (BM/64))*64 + lane (waves beyond BM/64 duplicate)
+  const unsigned char* ssrc = XS ? p.xs + (long)min(m0 + (wave % (BM / 64)) * 64 + lane, p.M - 1) * (p.K >> 5) : nullptr;
   auto stage = [&](int buf, int st) {
     char* base = smem + buf * SBYTES;
+    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
 #pragma unroll
     for (int i = 0; i < XPW; ++i)
       glds16_8(xsrc[i] + st * 128, base + (wave + 4 * i) * 1024);
@@ -309,21 +321,75 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
       const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + j * 16 * 128);
       b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
+    int sb[FPW];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      if constexpr (XS) {
+        const int r = wm * (BM / 2) + j * 16 + (lane & 15);
+        sb[j] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
+                                                        (lane >> 4));
+      } else {
+        sb[j] = 0x7f7f7f7f;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FCW; ++i)
 #pragma unroll
       for (int j = 0; j < FPW; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
-                                                                      0x7f7f7f7f);
+                                                                      sb[j]);
     cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
   const int lrow = lane & 15;
+  if (p.out8) {  // MX8 output: per (row, 32-column block) E8M0 scale; no early exits (shuffles)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
+      const bool mv = m < p.M;
+      const float sx = p.sx ? p.sx[min(m, p.M - 1)] : 1.f;
+#pragma unroll
+      for (int i = 0; i < FCW; i += 2) {
+        float v[2][4];
+        float amax = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = min(n0 + wn * (BN / 2) + (i + h) * 16 + (lane >> 4) * 4, p.N - 4);
+          const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+          const f32x4 bb = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = acc[i + h][j][e] * sx * sw[e] + bb[e];
+            if (p.act == HZ_ACT_RELU) x = fmaxf(x, 0.f);
+            else if (p.act == HZ_ACT_GELU) x = gelu_erf(x);
+            else if (p.act == HZ_ACT_TANH) x = tanhf(x);
+            v[h][e] = x;
+            amax = fmaxf(amax, fabsf(x));
+          }
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int ex = mx_exp(amax);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = n0 + wn * (BN / 2) + (i + h) * 16 + (lane >> 4) * 4;
+          float q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = fminf(fmaxf(ldexpf(v[h][e], -ex), -448.f), 448.f);
+          if (mv && n < p.N)
+            *reinterpret_cast<unsigned*>(p.out8 + (long)m * p.ldo + n) = pack4_fp8(q[0], q[1], q[2], q[3]);
+        }
+        const int nb = n0 + wn * (BN / 2) + i * 16;
+        if (mv && (lane >> 4) == 0 && nb < p.N) p.os8[(long)m * (p.ldo >> 5) + (nb >> 5)] = (unsigned char)(ex + 127);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
     const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
     if (m >= p.M) continue;
-    const float sx = p.sx[m];
+    const float sx = p.sx ? p.sx[m] : 1.f;
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
       const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
@@ -364,7 +430,8 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
 template <int BM, int BN, int NS>
 int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS>), dim3(tiles), dim3(256), 0, st, p);
+  if (p.xs) hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -374,6 +441,8 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
   const HzGemmFp8Params& p = *pp;
   if (p.cfg >= 16) {
     if (!p.wmx || p.K % 128 || p.ldx % 16 || p.N % 4) return -1;
+    if (!p.sx && !p.xs) return -1;
+    if (p.out8 && (!p.os8 || p.ldo % 32 || p.N % 32)) return -1;
     switch (p.cfg) {
       case 16: return launch_mx<128, 128, 3>(p, st);
       case 20: return launch_mx<128, 128, 2>(p, st);
@@ -386,7 +455,7 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       default: return -2;
     }
   }
-  if (p.N % 4 || p.ldx % 8 || p.ksteps * 32 < p.K) return -1;
+  if (p.N % 4 || p.ldx % 8 || p.ksteps * 32 < p.K || !p.sx || p.xs || p.out8) return -1;  // ring: per-row scales only
   switch (p.cfg) {
     case 0: return launch8<1, 1>(p, st);
     case 1: return launch8<1, 2>(p, st);

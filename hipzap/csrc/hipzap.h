@@ -118,7 +118,11 @@ typedef struct HzGemmFp8Params {
   void* out;                  // [M][ldo] bf16 or fp32
   int M, N, K, ksteps, ldx, ldo;
   int act, out_f32, cfg, kw;
-  const unsigned char* wmx;   // MX-packed weights [N_pad/16][K/128][2][64][16] (cfg 16..19) or NULL
+  const unsigned char* wmx;   // MX-packed weights [N_pad/16][K/128][2][64][16] (cfg 16..23) or NULL
+  // MX8 activations (OCP MX: e4m3 + one E8M0 power-of-two scale per 32 consecutive k), cfg >= 16:
+  const unsigned char* xs;    // input block scales [M][K/32] (then sx may be NULL) or NULL
+  unsigned char* out8;        // MX8 output instead of `out`: e4m3 [M][ldo] ...
+  unsigned char* os8;         //   ... and E8M0 scales [M][ldo/32]
 } HzGemmFp8Params;
 int hz_quant_launch(const HzQuantParams* p, hipStream_t st);
 int hz_gemm_fp8_launch(const HzGemmFp8Params* p, hipStream_t st);
@@ -153,6 +157,8 @@ typedef struct HzAttentionParams {
   unsigned short* out;        // [B*L][ldo], head h at col h*64
   int B, L, heads, head_dim, ldqkv, k_off, v_off, ldo;
   float scale;
+  unsigned char* out8;        // optional MX8 output (e4m3 [B*L][ldo] + E8M0 [B*L][ldo/32]) instead of out
+  unsigned char* os8;
 } HzAttentionParams;
 typedef struct HzVitTokensParams {
   const unsigned short* patches;  // [B*np][D]

@@ -260,6 +260,29 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
     }
   }
   // lane holds O[q0 + 4*(lane>>4) + i][dt*16 + lrow]
+  if (p.out8) {  // MX8 output: head columns [0,32) = dt 0,1 and [32,64) = dt 2,3 are two E8M0 blocks
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = q0 + 4 * (lane >> 4) + i;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float amax = fmaxf(fabsf(o[2 * hb][i]), fabsf(o[2 * hb + 1][i]));
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+        const int ex = mx_exp(amax);
+        if (q < p.L) {
+          unsigned char* o8 = p.out8 + (row0 + q) * p.ldo + h * ATT_D + hb * 32;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const float x = fminf(fmaxf(ldexpf(o[2 * hb + d][i], -ex), -448.f), 448.f);
+            o8[d * 16 + lrow] = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xff);
+          }
+          if (lrow == 0) p.os8[(row0 + q) * (p.ldo >> 5) + h * 2 + hb] = (unsigned char)(ex + 127);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = q0 + 4 * (lane >> 4) + i;
@@ -339,6 +362,7 @@ extern "C" int hz_embed_ln_launch(const HzEmbedParams* pp, hipStream_t st) {
 extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) {
   const HzAttentionParams& p = *pp;
   if (p.head_dim != ATT_D || p.L > ATT_LMAX || p.L < 1) return -1;
+  if (p.out8 && (!p.os8 || p.ldo % 32)) return -1;
   const int Lp = (p.L + 31) & ~31;
   const size_t lds = (size_t)(2 * Lp * ATT_D + 4 * 16 * Lp) * sizeof(bf16_t);
   hipLaunchKernelGGL(attention_kernel, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);

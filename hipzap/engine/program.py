@@ -90,7 +90,8 @@ class ExecContext:
             if n.attrs.get("cfg") is not None:
                 cfg, kw = n.attrs["cfg"], n.attrs.get("kw", 1)
             elif n.kind == "gemm_fp8":
-                cfg, kw = fp8.choose_config_fp8(M, pc, tuned, key)
+                mx_io = g.tensors[n.inputs[1]].dtype == torch.uint8 or len(n.outputs) == 2
+                cfg, kw = fp8.choose_config_fp8(M, pc, tuned, key, mx_io=mx_io)
             else:
                 cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=pc)
             conv_plans.append((cfg, kw, key))
@@ -210,9 +211,14 @@ class ExecContext:
             pw = self.params[n.attrs["w"]]
             cfg, kw, key = plan
             res = n.inputs[2] if len(n.inputs) > 2 else None
-            prm = fp8.gemm_params(addr(n.inputs[0]), addr(n.inputs[1]), pw, n.attrs["rows"], addr(n.outputs[0]),
-                                  addr(res), n.attrs.get("act", "none"), n.attrs.get("out_f32", False), cfg, kw,
-                                  ldx=g.shape(n.inputs[0])[-1], ldo=g.shape(n.outputs[0])[-1])
+            xs_mx = g.tensors[n.inputs[1]].dtype == torch.uint8  # MX8 block scales, not per-row fp32
+            o_mx = len(n.outputs) == 2
+            prm = fp8.gemm_params(addr(n.inputs[0]), 0 if xs_mx else addr(n.inputs[1]), pw, n.attrs["rows"],
+                                  0 if o_mx else addr(n.outputs[0]), addr(res), n.attrs.get("act", "none"),
+                                  n.attrs.get("out_f32", False), cfg, kw, ldx=g.shape(n.inputs[0])[-1],
+                                  ldo=g.shape(n.outputs[0])[-1], xs_ptr=addr(n.inputs[1]) if xs_mx else 0,
+                                  out8_ptr=addr(n.outputs[0]) if o_mx else 0,
+                                  os8_ptr=addr(n.outputs[1]) if o_mx else 0)
             self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
             tx.prog_add(self.prog, fp8.K_GEMM_FP8, prm, n.slot)
         elif n.kind == "layernorm":
@@ -230,8 +236,10 @@ class ExecContext:
             qkv = n.inputs[0]
             mask = n.inputs[1] if len(n.inputs) > 1 else None
             D = a["heads"] * 64
-            prm = tx.AttentionParams(addr(qkv), addr(mask), addr(n.outputs[0]), a["B"], a["L"], a["heads"], 64,
-                                     g.shape(qkv)[-1], D, 2 * D, D, 0.125)
+            mx = len(n.outputs) == 2  # MX8 output (e4m3 + E8M0 per 32 columns)
+            prm = tx.AttentionParams(addr(qkv), addr(mask), 0 if mx else addr(n.outputs[0]), a["B"], a["L"],
+                                     a["heads"], 64, g.shape(qkv)[-1], D, 2 * D, D, 0.125,
+                                     addr(n.outputs[0]) if mx else 0, addr(n.outputs[1]) if mx else 0)
             tx.prog_add(self.prog, tx.K_ATTENTION, prm, n.slot)
         elif n.kind == "embed_ln":
             tab, ln = self.params[n.attrs["emb"]], self.params[n.attrs["ln"]]

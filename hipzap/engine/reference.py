@@ -78,7 +78,11 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
                 y = y + vals[n.inputs[1]].float().reshape(rows, -1)
             act = n.attrs.get("act", "none")
             y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
-            store(n.outputs[0], y)
+            if len(n.outputs) == 2:  # MX8 output
+                from ..ops.fp8 import quant_mx_ref
+                vals[n.outputs[0]], vals[n.outputs[1]] = quant_mx_ref(y)
+            else:
+                store(n.outputs[0], y)
         elif k == "quant":
             from ..ops.fp8 import quant_rows_ref
             deq, s = quant_rows_ref(vals[n.inputs[0]])
@@ -91,7 +95,11 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
                 y = y + vals[n.inputs[2]].float()
             act = n.attrs.get("act", "none")
             y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
-            store(n.outputs[0], y)
+            if len(n.outputs) == 2:  # MX8 output
+                from ..ops.fp8 import quant_mx_ref
+                vals[n.outputs[0]], vals[n.outputs[1]] = quant_mx_ref(y)
+            else:
+                store(n.outputs[0], y)
         elif k == "layernorm":
             npar = params[n.attrs["p"]]
             rows = n.attrs["rows"]
@@ -112,7 +120,12 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             a = n.attrs
             mask = vals[n.inputs[1]] if len(n.inputs) > 1 else None
             from ..ops.transformer import attention_ref
-            store(n.outputs[0], attention_ref(vals[n.inputs[0]], a["B"], a["L"], a["heads"], mask))
+            y = attention_ref(vals[n.inputs[0]], a["B"], a["L"], a["heads"], mask)
+            if len(n.outputs) == 2:  # MX8 output: the oracle carries the dequantised values
+                from ..ops.fp8 import quant_mx_ref
+                vals[n.outputs[0]], vals[n.outputs[1]] = quant_mx_ref(y.to(torch.bfloat16))
+            else:
+                store(n.outputs[0], y)
         elif k == "embed_ln":
             from ..ops.transformer import embed_ref
             tab, ln = params[n.attrs["emb"]], params[n.attrs["ln"]]

@@ -37,9 +37,11 @@ def conv_shapes(graph, params) -> dict:
         if n.kind == "gemm_fp8":
             pw = params[n.attrs["w"]]
             M = n.attrs["rows"]
+            mode = "fp8" + (":xs" if graph.tensors[n.inputs[1]].dtype == torch.uint8 else "") + \
+                (":o8" if len(n.outputs) == 2 else "")
             out.setdefault(f"f8r{M}x{pw.cout}x{pw.K}", (pw, (M, 1, 1), M, len(n.inputs) > 2,
                                                         n.attrs.get("act", "none"), n.attrs.get("out_f32", False),
-                                                        "fp8"))
+                                                        mode))
             continue
         if n.kind == "gemm":
             pc = params[n.attrs["w"]]
@@ -80,11 +82,18 @@ def _time_candidate(lib, shape, cand, bufs, streams, concurrent: int) -> float:
     try:
         for c in range(concurrent):
             x, r, o = bufs[c][:3]
-            if rowmajor == "fp8":
+            if str(rowmajor).startswith("fp8"):
                 sx = torch.full((M,), 1e-2, device=x.device)
-                bufs[c] = (x, r, o, sx)
-                prm = fp8_ops.gemm_params(x.data_ptr(), sx.data_ptr(), pc, M, o.data_ptr(),
-                                          r.data_ptr() if res else 0, act, out_f32, cfg, kw)
+                xs = torch.full((M * pc.K // 32,), 120, dtype=torch.uint8, device=x.device)
+                o8 = torch.empty(M * pc.cout, dtype=torch.uint8, device=x.device)
+                os8 = torch.empty(M * pc.cout // 32, dtype=torch.uint8, device=x.device)
+                bufs[c] = (x, r, o, sx, xs, o8, os8)
+                use_xs, use_o8 = ":xs" in rowmajor, ":o8" in rowmajor
+                prm = fp8_ops.gemm_params(x.data_ptr(), 0 if use_xs else sx.data_ptr(), pc, M,
+                                          0 if use_o8 else o.data_ptr(), r.data_ptr() if res else 0, act, out_f32,
+                                          cfg, kw, xs_ptr=xs.data_ptr() if use_xs else 0,
+                                          out8_ptr=o8.data_ptr() if use_o8 else 0,
+                                          os8_ptr=os8.data_ptr() if use_o8 else 0)
                 rc = lib.hz_launch_kernel(fp8_ops.K_GEMM_FP8, C.byref(prm), streams[c].cuda_stream)
             else:
                 prm, _, _ = conv_ops.make_params(x.data_ptr(), pc, nb, h, w, o.data_ptr(), r.data_ptr() if res else 0,
@@ -119,7 +128,7 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
             pc, (nb, h, w), M, res, act, out_f32, rowmajor = shape
             bufs = []
             for _ in range(concurrent):
-                if rowmajor == "fp8":
+                if str(rowmajor).startswith("fp8"):
                     x = torch.randint(0, 120, (M * pc.K,), device=dev, dtype=torch.uint8, generator=g)
                 else:
                     x = (torch.randn(nb * h * w * pc.cin, device=dev, generator=g) * 0.5).to(torch.bfloat16)
@@ -127,13 +136,14 @@ def tune_graph(graph, params, device, verbose=False, concurrent: int = 1) -> tup
                 o = torch.empty(M * pc.cout, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
                 bufs.append((x, r, o))
             times = []
-            cands = (fp8_ops.candidates_fp8(M, pc) if rowmajor == "fp8"
+            fp8_mode = str(rowmajor).startswith("fp8")
+            cands = (fp8_ops.candidates_fp8(M, pc, mx_io=rowmajor != "fp8") if fp8_mode
                      else conv_ops.candidates(M, pc.cout, pc.K, rowmajor, pc))
             for cand in cands:
                 times.append((_time_candidate(lib, shape, cand, bufs, streams, concurrent), cand))
             times.sort()
             best_t, best = times[0]
-            heur = (fp8_ops.choose_config_fp8(M, pc) if rowmajor == "fp8"
+            heur = (fp8_ops.choose_config_fp8(M, pc, mx_io=rowmajor != "fp8") if fp8_mode
                     else conv_ops.choose_config(M, pc.cout, pc.K, rowmajor=rowmajor, pc=pc))
             heur_t = next((t for t, c in times if tuple(c) == tuple(heur)), None)
             table[key] = list(best)

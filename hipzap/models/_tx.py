@@ -74,19 +74,33 @@ class TxBuilder:
         g.add("layernorm", ins, [x8, sx], p=p, rows=r, ldx=None)
         return x8, sx
 
-    def gemm8q(self, xq, w: str, cols: int, act="none", res=None, out_f32=False, ext=False, name=None):
-        """fp8 GEMM on an already-quantised input ``xq = (x8, scales)``."""
+    def gemm8q(self, xq, w: str, cols: int, act="none", res=None, out_f32=False, ext=False, name=None,
+               out_mx=False):
+        """fp8 GEMM on an already-quantised input ``xq = (x8, scales)``: per-row fp32 scales
+        ``[rows]`` or MX8 E8M0 block scales ``[rows, K/32]`` (uint8). ``out_mx``: the output is
+        MX8 too, returned as ``(o8, os8)`` for the next fp8 GEMM."""
         g = self.g
         x8, sx = xq
         r = g.shape(x8)[0]
-        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
         ins = [x8, sx] if res is None else [x8, sx, res]
+        if out_mx:
+            o8 = g.tensor((r, cols), torch.uint8, f"{name or w}.o8")
+            os8 = g.tensor((r, cols // 32), torch.uint8, f"{name or w}.os8")
+            g.add("gemm_fp8", ins, [o8, os8], w=w, act=act, rows=r, name=name or w)
+            return o8, os8
+        out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
         g.add("gemm_fp8", ins, [out], w=w, act=act, rows=r, out_f32=out_f32, name=name or w)
         return out
 
-    def attention(self, qkv, B, L, heads, mask=None):
+    def attention(self, qkv, B, L, heads, mask=None, out_mx=False):
+        """Fused attention; ``out_mx``: MX8 output ``(ctx8, ctxs)`` for an fp8 consumer."""
         g = self.g
-        out = g.tensor((B * L, heads * 64), torch.bfloat16, "ctx")
         ins = [qkv] if mask is None else [qkv, mask]
+        if out_mx:
+            o8 = g.tensor((B * L, heads * 64), torch.uint8, "ctx.o8")
+            os8 = g.tensor((B * L, heads * 2), torch.uint8, "ctx.os8")
+            g.add("attention", ins, [o8, os8], B=B, L=L, heads=heads)
+            return o8, os8
+        out = g.tensor((B * L, heads * 64), torch.bfloat16, "ctx")
         g.add("attention", ins, [out], B=B, L=L, heads=heads)
         return out

@@ -100,17 +100,20 @@ def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12
     f8 = weights == "fp8"
     x = tok
     for i in range(layers):
-        if f8:  # pre-LN: the LN outputs feed only fp8 GEMMs -> quantise inside the LayerNorm
+        if f8:
+            # every fp8 GEMM input is produced already quantised by its producer: the pre-LN
+            # LayerNorms emit e4m3 + per-row scales, attention and FC1 emit MX8 (e4m3 + one E8M0
+            # scale per 32 columns) consumed by the block-scaled MFMA — no quantisation kernels
             qkv = tb.gemm8q(tb.layernorm_q8(x, f"l{i}.ln1"), f"l{i}.qkv", 3 * D)
+            x2 = tb.gemm8q(tb.attention(qkv, B, T, heads, out_mx=True), f"l{i}.o", D, res=x)
+            f = tb.gemm8q(tb.layernorm_q8(x2, f"l{i}.ln2"), f"l{i}.fc1", ffn, act="gelu", out_mx=True)
+            x = tb.gemm8q(f, f"l{i}.fc2", D, res=x2)
         else:
             qkv = tb.gemm(tb.layernorm(x, f"l{i}.ln1"), f"l{i}.qkv", 3 * D)
-        ctx = tb.attention(qkv, B, T, heads)
-        x2 = tb.linear(ctx, f"l{i}.o", D, fp8=f8, res=x)
-        if f8:
-            f = tb.gemm8q(tb.layernorm_q8(x2, f"l{i}.ln2"), f"l{i}.fc1", ffn, act="gelu")
-        else:
+            ctx = tb.attention(qkv, B, T, heads)
+            x2 = tb.gemm(ctx, f"l{i}.o", D, res=x)
             f = tb.gemm(tb.layernorm(x2, f"l{i}.ln2"), f"l{i}.fc1", ffn, act="gelu")
-        x = tb.linear(f, f"l{i}.fc2", D, fp8=f8, res=x2)
+            x = tb.gemm(f, f"l{i}.fc2", D, res=x2)
     cls = tb.layernorm(x, "final_ln", rows=B, ldx=T * D, name="cls_ln")
     npad = (num_labels + 3) // 4 * 4
     logits = tb.linear(cls, "head", npad, fp8=f8, out_f32=True, ext=True)

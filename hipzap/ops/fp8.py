@@ -28,7 +28,8 @@ class GemmFp8Params(C.Structure):
     _fields_ = [("x", C.c_void_p), ("sx", C.c_void_p), ("w", C.c_void_p), ("sw", C.c_void_p), ("bias", C.c_void_p),
                 ("res", C.c_void_p), ("out", C.c_void_p), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
                 ("ksteps", C.c_int), ("ldx", C.c_int), ("ldo", C.c_int), ("act", C.c_int), ("out_f32", C.c_int),
-                ("cfg", C.c_int), ("kw", C.c_int), ("wmx", C.c_void_p)]
+                ("cfg", C.c_int), ("kw", C.c_int), ("wmx", C.c_void_p), ("xs", C.c_void_p), ("out8", C.c_void_p),
+                ("os8", C.c_void_p)]
 
 
 @dataclass
@@ -101,18 +102,19 @@ def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
     return pw.w8mx is not None and M >= 64 and pw.K % 128 == 0 and (ldx or pw.K) % 16 == 0
 
 
-def candidates_fp8(M: int, pw: PackedFp8) -> list:
+def candidates_fp8(M: int, pw: PackedFp8, mx_io: bool = False) -> list:
     from .conv import candidates
     out = [(cfg, 1) for cfg in MX_TILES] if mx_ok(M, pw) else []
-    return out + candidates(M, pw.cout, pw.K)
+    return out if mx_io else out + candidates(M, pw.cout, pw.K)
 
 
-def choose_config_fp8(M: int, pw: PackedFp8, tuned: dict | None = None, key: str | None = None):
+def choose_config_fp8(M: int, pw: PackedFp8, tuned: dict | None = None, key: str | None = None, mx_io=False):
+    """``mx_io``: MX8 input or output -> only the MX LDS kernel can run it."""
     if tuned is not None and key is not None and key in tuned:
         cfg, kw = int(tuned[key][0]), int(tuned[key][1])
-        if cfg not in MX_TILES or mx_ok(M, pw):
+        if (cfg not in MX_TILES and not mx_io) or (cfg in MX_TILES and mx_ok(M, pw)):
             return cfg, kw
-    if mx_ok(M, pw) and M >= 512:
+    if mx_ok(M, pw) and (M >= 512 or mx_io):
         for cfg in (16, 17, 18, 19):
             bm, bn = MX_TILES[cfg]
             if math.ceil(M / bm) * math.ceil(pw.cout / bn) >= 256:
@@ -127,6 +129,21 @@ def quantize_params(P: dict, names) -> dict:
         if isinstance(P[n], PackedConv):
             out[n] = quantize_linear(P[n])
     return out
+
+
+def quant_mx_ref(x: torch.Tensor, block: int = 32):
+    """fp32 oracle of MX8 (OCP MX e4m3, one E8M0 scale per ``block`` columns): returns
+    (dequantised x, exponents [rows, cols/block]) with 2^e the smallest power of two such
+    that amax / 2^e <= 448 (frexp rule, csrc/common.h mx_exp)."""
+    x = x.float()
+    r, c = x.shape
+    xb = x.reshape(r, c // block, block)
+    amax = xb.abs().amax(-1)
+    _, e = torch.frexp(amax / FP8_MAX)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp(-127, 127)
+    sc = torch.ldexp(torch.ones_like(amax), e)
+    q = (xb / sc.unsqueeze(-1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float()
+    return (q * sc.unsqueeze(-1)).reshape(r, c), e
 
 
 def quant_rows_ref(x: torch.Tensor):
@@ -148,14 +165,18 @@ def quant_rows(x: torch.Tensor):
 
 
 def gemm_params(x8_ptr, sx_ptr, pw: PackedFp8, M, out_ptr, res_ptr=0, act="none", out_f32=False, cfg=0, kw=1,
-                ldx=None, ldo=None) -> GemmFp8Params:
+                ldx=None, ldo=None, xs_ptr=0, out8_ptr=0, os8_ptr=0) -> GemmFp8Params:
+    """``sx_ptr``: per-row fp32 activation scales, or ``xs_ptr``: MX8 block scales [M][K/32];
+    ``out8_ptr``/``os8_ptr``: write MX8 (e4m3 + E8M0 per 32 columns) instead of ``out_ptr``."""
     from .conv import ACT
     if cfg in MX_TILES and not mx_ok(M, pw, ldx):
         raise ValueError(f"MX fp8 GEMM config {cfg} not legal for M={M} K={pw.K}")
+    if (xs_ptr or out8_ptr) and cfg not in MX_TILES:
+        raise ValueError("MX8 activations need an MX (LDS) GEMM config")
     return GemmFp8Params(x8_ptr, sx_ptr, pw.w8.data_ptr(), pw.sw.data_ptr(), pw.bias.data_ptr(), res_ptr, out_ptr, M,
                          pw.cout, pw.K, pw.ksteps, ldx if ldx is not None else pw.K,
                          ldo if ldo is not None else pw.cout, ACT[act], int(out_f32), cfg, kw,
-                         pw.w8mx.data_ptr() if pw.w8mx is not None else 0)
+                         pw.w8mx.data_ptr() if pw.w8mx is not None else 0, xs_ptr, out8_ptr, os8_ptr)
 
 
 def gemm_fp8(x8: torch.Tensor, sx: torch.Tensor, pw: PackedFp8, residual=None, act="none", out_f32=False,

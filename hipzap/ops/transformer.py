@@ -34,7 +34,8 @@ class EmbedParams(C.Structure):
 class AttentionParams(C.Structure):
     _fields_ = [("qkv", C.c_void_p), ("mask", C.c_void_p), ("out", C.c_void_p), ("B", C.c_int), ("L", C.c_int),
                 ("heads", C.c_int), ("head_dim", C.c_int), ("ldqkv", C.c_int), ("k_off", C.c_int),
-                ("v_off", C.c_int), ("ldo", C.c_int), ("scale", C.c_float)]
+                ("v_off", C.c_int), ("ldo", C.c_int), ("scale", C.c_float), ("out8", C.c_void_p),
+                ("os8", C.c_void_p)]
 
 
 class VitTokensParams(C.Structure):

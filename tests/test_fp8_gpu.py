@@ -93,3 +93,75 @@ def test_mfma_f8f6f4_operand_layout():
     assert torch.equal(_probe_f8f6f4(0, A, Bt), ref)   # both operands: 32 consecutive k per lane
     assert torch.equal(_probe_f8f6f4(3, A, Bt), ref)   # both operands: 4 blocks of the 16x16x32 map
     assert not torch.equal(_probe_f8f6f4(1, A, Bt), ref)  # inconsistent maps are detected
+
+
+def _mx_encode(x: torch.Tensor):
+    """Host MX8 encoding (quant_mx_ref rule): e4m3 bytes + E8M0 bytes [rows, cols/32]."""
+    deq, e = F8.quant_mx_ref(x)
+    sc = torch.ldexp(torch.ones_like(e, dtype=torch.float32), e).repeat_interleave(32, 1)
+    q8 = (deq / sc).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q8, (e + 127).to(torch.uint8), deq
+
+
+def _mx_decode(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
+    sc = torch.ldexp(torch.ones(s8.shape), s8.long() - 127).repeat_interleave(32, 1)
+    return q8.view(torch.float8_e4m3fn).float() * sc
+
+
+@pytest.mark.parametrize("cfg", [16, 19, 21])
+@pytest.mark.parametrize("mx_in,mx_out", [(True, False), (False, True), (True, True)])
+def test_gemm_mx8_activations(cfg, mx_in, mx_out):
+    """MX8 (e4m3 + E8M0 per 32 k) activations into the block-scaled MFMA, and MX8 output from
+    the epilogue, vs the fp32 oracle of the same quantisation."""
+    import ctypes
+    from hipzap import _native as N
+    g = torch.Generator().manual_seed(9)
+    M, Nn, K = 200, 768, 512
+    w = torch.randn(Nn, K, generator=g) * 0.05
+    b = torch.randn(Nn, generator=g)
+    x = torch.randn(M, K, generator=g) * torch.linspace(0.1, 8, K)  # per-block dynamic ranges differ
+    pw = F8.quantize_linear(C.pack_linear(w, b))
+    pwd = F8.PackedFp8(pw.w8.to(DEV), pw.sw.to(DEV), pw.bias.to(DEV), pw.cin, pw.cout, pw.w8mx.to(DEV))
+    if mx_in:
+        q8, s8, xd = _mx_encode(x)
+        x8, xs, sx = q8.to(DEV), s8.to(DEV), None
+    else:
+        x8, sx = F8.quant_rows(x.to(torch.bfloat16).to(DEV))
+        xd, _ = F8.quant_rows_ref(x.to(torch.bfloat16))
+        xs = None
+    ref = torch.nn.functional.gelu(xd @ pw.dequant().t() + b)
+    out = torch.empty(M, Nn, device=DEV, dtype=torch.bfloat16)
+    o8 = torch.zeros(M, Nn, dtype=torch.uint8, device=DEV)
+    os8 = torch.zeros(M, Nn // 32, dtype=torch.uint8, device=DEV)
+    prm = F8.gemm_params(x8.data_ptr(), N.ptr(sx), pwd, M, 0 if mx_out else out.data_ptr(), 0, "gelu", False, cfg,
+                         1, xs_ptr=N.ptr(xs), out8_ptr=o8.data_ptr() if mx_out else 0,
+                         os8_ptr=os8.data_ptr() if mx_out else 0)
+    N.check(N.lib().hz_launch_kernel(F8.K_GEMM_FP8, ctypes.byref(prm), N.stream_ptr()), "gemm mx8")
+    torch.cuda.synchronize()
+    if mx_out:
+        got = _mx_decode(o8.cpu(), os8.cpu())
+        ref_q, _ = F8.quant_mx_ref(ref)
+        assert ((got - ref_q).abs().max() / ref_q.abs().max()).item() < 0.1  # <= one e4m3 step
+    else:
+        assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+
+
+def test_attention_mx8_output():
+    from hipzap.ops import transformer as T
+    import ctypes
+    from hipzap import _native as N
+    g = torch.Generator().manual_seed(10)
+    B, L, H = 2, 197, 12
+    qkv = torch.randn(B * L, 3 * H * 64, generator=g).to(torch.bfloat16)
+    ref = T.attention_ref(qkv, B, L, H, None)
+    o8 = torch.zeros(B * L, H * 64, dtype=torch.uint8, device=DEV)
+    os8 = torch.zeros(B * L, H * 2, dtype=torch.uint8, device=DEV)
+    q = qkv.to(DEV)
+    D = H * 64
+    prm = T.AttentionParams(q.data_ptr(), 0, 0, B, L, H, 64, q.stride(0), D, 2 * D, D, 0.125, o8.data_ptr(),
+                            os8.data_ptr())
+    N.check(N.lib().hz_launch_kernel(T.K_ATTENTION, ctypes.byref(prm), N.stream_ptr()), "attention mx8")
+    torch.cuda.synchronize()
+    got = _mx_decode(o8.cpu(), os8.cpu())
+    ref_q, _ = F8.quant_mx_ref(ref.float())
+    assert ((got - ref_q).abs().max() / ref_q.abs().max()).item() < 0.1  # <= one e4m3 step
