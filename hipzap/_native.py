@@ -52,7 +52,7 @@ class DecoderParams(C.Structure):
 class SamplerParams(C.Structure):
     _fields_ = [("logits", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
                 ("seed", c_void_p), ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int),
-                ("exclude", c_int * 8), ("keyed", c_int)]
+                ("exclude", c_int * 8), ("keyed", c_int), ("cand_val", c_void_p), ("cand_idx", c_void_p)]
 
 
 def _sig(lib, name, res, *args):

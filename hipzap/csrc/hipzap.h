@@ -96,6 +96,8 @@ typedef struct HzSamplerParams {
   int V, n_exclude;
   int exclude[8];
   int keyed;                  // 1: `logits` already holds the Gumbel-perturbed keys (decoder epilogue)
+  float* cand_val;            // scratch [ceil(V/1024)][10]: per-block top-10 (two-stage selection)
+  int* cand_idx;
 } HzSamplerParams;
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);

@@ -38,6 +38,15 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   const int tok = p.emb ? p.tok_seq[t] : 0;
   const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
   const float* xprev = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
+  // weights do not depend on the input vector: issue them first so their latency overlaps
+  // the staging loads (inactive tail waves read row H-1 and write nothing)
+  const int j = blockIdx.x * 4 + wave;  // hidden unit of this wave
+  const bf16_t* w = p.w + (long)(4 * min(j, p.H - 1)) * p.ldk + lane * 8;
+  u32x4 wv[4][NCH];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) wv[q][c] = *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + c * 512);
   // ---- stage the input vector in LDS (fp32): all loads first, then the selects ----
   float fv[PER];
   unsigned short ev[PER];
@@ -56,14 +65,7 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
     vin[i] = in_h ? fv[r] : in_x ? (erow ? bf2f(ev[r]) : fv[r]) : 0.f;
   }
   __syncthreads();
-  const int j = blockIdx.x * 4 + wave;  // hidden unit of this wave
   if (j >= p.H) return;
-  const bf16_t* w = p.w + (long)(4 * j) * p.ldk + lane * 8;
-  u32x4 wv[4][NCH];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) wv[q][c] = *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + c * 512);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -196,18 +198,112 @@ __device__ __forceinline__ void wave_argmax(float& v, int& i) {
   }
 }
 
-// Hierarchical top-10: per-thread sorted top-10 (insertion) -> per-wave top-10 (10 rounds of
-// shuffle argmax over the lanes' list heads, no barriers) -> 16 x 10 candidates in LDS -> wave 0
-// merges them the same way. Two barriers in total (the previous version: 10 rounds of
-// block-wide argmax, 3 barriers each, plus the whole Philox stream on one workgroup).
-__global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) {
-  __shared__ float c_val[16 * TOPK];
-  __shared__ int c_idx[16 * TOPK];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+// Two-stage Gumbel top-10 (10 draws without replacement ∝ exp(logit)):
+//   sampler_partial: ceil(V/1024) blocks; each thread loads its 4 keys unconditionally (one
+//     round trip), sorts them, the wave merges its lanes' lists by 10 rounds of shuffle argmax,
+//     wave 0 merges the 4 wave lists -> the block's top-10 into the candidate buffer;
+//   sampler_final: one wave merges all candidates (loaded 8 at a time) and applies the
+//     reference's selection rule (main.py:63-68), writes the token and advances the step.
+// The previous single-workgroup version read the V keys through a data-dependent branch per
+// element (a dependent L2 round trip each): 110 us per token, ~60 % of the whole decode step.
+constexpr int SPB = 1024;  // keys per partial block (256 threads x 4)
+
+__device__ __forceinline__ void cswap(float& va, int& ia, float& vb, int& ib) {  // descending
+  if (vb > va || (vb == va && ib < ia)) {
+    const float tv = va;
+    const int ti = ia;
+    va = vb;
+    ia = ib;
+    vb = tv;
+    ib = ti;
+  }
+}
+
+// 10 rounds of wave argmax over per-lane sorted lists of length L (head = next unpopped entry).
+template <int L>
+__device__ __forceinline__ void wave_topk(const float (&v)[L], const int (&id)[L], float (&ov)[TOPK],
+                                          int (&oi)[TOPK]) {
+  int head = 0;
+#pragma unroll
+  for (int r = 0; r < TOPK; ++r) {
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < L; ++q)
+      if (q == head) {
+        hv = v[q];
+        hi = id[q];
+      }
+    float bv = hv;
+    int bi = hi;
+    wave_argmax(bv, bi);
+    if (hv == bv && hi == bi && head < L) ++head;  // indices are unique: one lane pops
+    ov[r] = bv;
+    oi[r] = bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void sampler_partial_kernel(const HzSamplerParams p) {
+  __shared__ float w_val[4 * TOPK];
+  __shared__ int w_idx[4 * TOPK];
   const int t = *p.step;
-  const bool forced = (t + 1) < *p.n_forced;
+  if ((t + 1) < *p.n_forced) return;  // prompt step: the next token is given
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long seed = *p.seed;
-  if (!forced) {
+  float v[4];
+  int id[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = blockIdx.x * SPB + r * 256 + tid;
+    id[r] = j;
+    v[r] = p.logits[min(j, p.V - 1)];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (!p.keyed) v[r] += gumbel(seed, t, id[r]);
+    if (id[r] >= p.V) v[r] = -INFINITY;
+  }
+  cswap(v[0], id[0], v[1], id[1]);
+  cswap(v[2], id[2], v[3], id[3]);
+  cswap(v[0], id[0], v[2], id[2]);
+  cswap(v[1], id[1], v[3], id[3]);
+  cswap(v[1], id[1], v[2], id[2]);
+  float wv[TOPK];
+  int wi[TOPK];
+  wave_topk<4>(v, id, wv, wi);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < TOPK; ++r) {
+      w_val[wave * TOPK + r] = wv[r];
+      w_idx[wave * TOPK + r] = wi[r];
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float cv[1] = {lane < 4 * TOPK ? w_val[lane] : -INFINITY};
+    int ci[1] = {lane < 4 * TOPK ? w_idx[lane] : 0x7fffffff};
+    float bv[TOPK];
+    int bi[TOPK];
+    wave_topk<1>(cv, ci, bv, bi);
+    if (lane < TOPK) {
+      float o = bv[0];
+      int oi = bi[0];
+#pragma unroll
+      for (int r = 1; r < TOPK; ++r) {
+        o = lane == r ? bv[r] : o;
+        oi = lane == r ? bi[r] : oi;
+      }
+      p.cand_val[blockIdx.x * TOPK + lane] = o;
+      p.cand_idx[blockIdx.x * TOPK + lane] = oi;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void sampler_final_kernel(const HzSamplerParams p) {
+  const int lane = threadIdx.x;
+  const int t = *p.step;
+  if ((t + 1) >= *p.n_forced) {
+    const int ncand = ((p.V + SPB - 1) / SPB) * TOPK;
     float v[TOPK];
     int id[TOPK];
 #pragma unroll
@@ -215,100 +311,44 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
       v[q] = -INFINITY;
       id[q] = 0x7fffffff;
     }
-    for (int j = tid; j < p.V; j += blockDim.x) {
-      const float key = p.keyed ? p.logits[j] : p.logits[j] + gumbel(seed, t, j);
-      if (key > v[TOPK - 1]) {
-        float cv = key;
-        int ci = j;
+    for (int c0 = 0; c0 < ncand; c0 += 64 * 8) {
+      float cv[8];
+      int ci[8];
 #pragma unroll
-        for (int q = 0; q < TOPK; ++q) {
-          if (cv > v[q]) {
-            const float tv = v[q];
-            const int ti = id[q];
-            v[q] = cv;
-            id[q] = ci;
-            cv = tv;
-            ci = ti;
-          }
-        }
+      for (int u = 0; u < 8; ++u) {  // 8 candidates in flight per lane
+        const int c = min(c0 + u * 64 + lane, ncand - 1);
+        cv[u] = p.cand_val[c];
+        ci[u] = p.cand_idx[c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float x = c0 + u * 64 + lane < ncand ? cv[u] : -INFINITY;
+        int xi = ci[u];
+#pragma unroll
+        for (int q = 0; q < TOPK; ++q) cswap(v[q], id[q], x, xi);  // insertion into the sorted list
       }
     }
-    // wave-level merge: the lane list heads compete; the winner pops its head
-    int head = 0;
-    for (int r = 0; r < TOPK; ++r) {
-      float hv = -INFINITY;
-      int hi = 0x7fffffff;
-#pragma unroll
-      for (int q = 0; q < TOPK; ++q)
-        if (q == head) {
-          hv = v[q];
-          hi = id[q];
+    float dv[TOPK];
+    int draws[TOPK];
+    wave_topk<TOPK>(v, id, dv, draws);
+    if (lane == 0) {
+      int tok = draws[0];
+      for (int r = 0; r < TOPK && r < p.V; ++r) {
+        const int d = draws[r];
+        bool ex = d <= 0;
+        for (int e = 0; e < p.n_exclude; ++e) ex |= (d == p.exclude[e]);
+        if (!ex) {
+          tok = d;
+          break;
         }
-      float bv = hv;
-      int bi = hi;
-      wave_argmax(bv, bi);
-      if (hv == bv && hi == bi) ++head;  // indices are unique: exactly one lane pops
-      if (lane == 0) {
-        c_val[wave * TOPK + r] = bv;
-        c_idx[wave * TOPK + r] = bi;
       }
-    }
-    __syncthreads();
-    if (wave == 0) {
-      // each lane holds up to 3 candidates (nw * TOPK <= 160), kept sorted descending
-      float cv[3];
-      int ci[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int e = lane + q * 64;
-        const bool ok = e < nw * TOPK;
-        cv[q] = ok ? c_val[e] : -INFINITY;
-        ci[q] = ok ? c_idx[e] : 0x7fffffff;
-      }
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = a + 1; b < 3; ++b)
-          if (cv[b] > cv[a] || (cv[b] == cv[a] && ci[b] < ci[a])) {
-            const float tv = cv[a];
-            const int ti = ci[a];
-            cv[a] = cv[b];
-            ci[a] = ci[b];
-            cv[b] = tv;
-            ci[b] = ti;
-          }
-      int hd = 0;
-      int draws[TOPK];
-#pragma unroll
-      for (int r = 0; r < TOPK; ++r) {
-        float hv = hd == 0 ? cv[0] : hd == 1 ? cv[1] : hd == 2 ? cv[2] : -INFINITY;
-        int hi = hd == 0 ? ci[0] : hd == 1 ? ci[1] : hd == 2 ? ci[2] : 0x7fffffff;
-        float bv = hv;
-        int bi = hi;
-        wave_argmax(bv, bi);
-        if (hv == bv && hi == bi) ++hd;
-        draws[r] = bi;
-      }
-      if (lane == 0) {
-        int tok = draws[0];
-        for (int r = 0; r < TOPK && r < p.V; ++r) {
-          const int d = draws[r];
-          bool ex = d <= 0;
-          for (int e = 0; e < p.n_exclude; ++e) ex |= (d == p.exclude[e]);
-          if (!ex) {
-            tok = d;
-            break;
-          }
-        }
-        p.tok_seq[t + 1] = tok;
-        if (p.draws) {
-          for (int r = 0; r < TOPK; ++r) p.draws[(long)t * TOPK + r] = draws[r];
-        }
+      p.tok_seq[t + 1] = tok;
+      if (p.draws) {
+        for (int r = 0; r < TOPK; ++r) p.draws[(long)t * TOPK + r] = draws[r];
       }
     }
   }
-  __syncthreads();
-  if (tid == 0) *p.step = t + 1;
+  if (lane == 0) *p.step = t + 1;
 }
 
 }  // namespace
@@ -348,7 +388,8 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
 
 extern "C" int hz_sampler_launch(const HzSamplerParams* pp, hipStream_t st) {
   const HzSamplerParams& p = *pp;
-  if (p.n_exclude > 8) return -1;
-  hipLaunchKernelGGL(sampler_kernel, dim3(1), dim3(1024), 0, st, p);
+  if (p.n_exclude > 8 || !p.cand_val || !p.cand_idx || p.V < 1) return -1;
+  hipLaunchKernelGGL(sampler_partial_kernel, dim3((p.V + SPB - 1) / SPB), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(sampler_final_kernel, dim3(1), dim3(64), 0, st, p);
   return (int)hipGetLastError();
 }

@@ -111,6 +111,10 @@ class LMEngine:
             s = N.SamplerParams()
             s.logits, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
             s.keyed = 1
+            nblk = (packed["V"] + 1023) // 1024  # two-stage sampler: per-block top-10 candidates
+            self.cand_val = torch.empty(nblk * NUM_DRAWS, device=dev)
+            self.cand_idx = torch.empty(nblk * NUM_DRAWS, dtype=torch.int32, device=dev)
+            s.cand_val, s.cand_idx = self.cand_val.data_ptr(), self.cand_idx.data_ptr()
             s.draws = N.ptr(self.draws)
             s.seed, s.n_forced = self.seed.data_ptr(), self.n_forced.data_ptr()
             s.V = packed["V"]
