@@ -150,12 +150,17 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const HzEmbedParams p) {
 constexpr int ATT_D = 64;
 constexpr int ATT_LMAX = 256;
 
+constexpr int ATT_KST = ATT_D + 8;  // padded K row stride: the 16 rows of a fragment read hit distinct banks
+__device__ __attribute__((aligned(64))) unsigned int g_zero_att[16] = {0};
+
 __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Lp = (p.L + 31) & ~31;  // keys padded to the 32-wide MFMA K step
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);          // [Lp][64]
-  bf16_t* Vt = Ks + Lp * ATT_D;                         // [64][Lp]
-  bf16_t* Ps = Vt + Lp * ATT_D;                         // [4 waves][16][Lp]
+  const int VST = Lp + 8;           // padded V^T / P row strides (bank-conflict-free fragment reads)
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);          // [Lp][ATT_KST]
+  bf16_t* Vt = Ks + Lp * ATT_KST;                       // [64][VST]
+  bf16_t* Ps = Vt + ATT_D * VST;                        // [4 waves][16][VST]
+  const bf16_t* Z = reinterpret_cast<const bf16_t*>(g_zero_att);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
   const int b = bh / p.heads, h = bh - b * p.heads;
@@ -163,18 +168,28 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
   const bf16_t* Q = p.qkv + row0 * p.ldqkv + h * ATT_D;
   const bf16_t* K = Q + p.k_off;
   const bf16_t* V = Q + p.v_off;
-  // ---- stage K (row-major) and V^T in LDS ----
-  for (int i = tid; i < Lp * 8; i += blockDim.x) {
-    const int key = i >> 3, c = (i & 7) * 8;
-    u32x4 kv = u32x4{0, 0, 0, 0}, vv = u32x4{0, 0, 0, 0};
-    if (key < p.L) {
-      kv = *reinterpret_cast<const u32x4*>(K + (long)key * p.ldqkv + c);
-      vv = *reinterpret_cast<const u32x4*>(V + (long)key * p.ldqkv + c);
-    }
-    *reinterpret_cast<u32x4*>(Ks + key * ATT_D + c) = kv;
-    const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv);
+  // ---- stage K (row-major) and V^T in LDS: every load issued first (padding keys read the
+  // zero buffer: an address select, not a branch around the load — one round trip, not 8) ----
+  constexpr int SIT = ATT_LMAX * 8 / 256;
+  u32x4 kv[SIT], vv[SIT];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) Vt[(c + e) * Lp + key] = ve[e];
+  for (int it = 0; it < SIT; ++it) {
+    const int i = tid + it * 256;
+    const int key = i >> 3, c = (i & 7) * 8;
+    const bool v = key < p.L;
+    kv[it] = *reinterpret_cast<const u32x4*>(v ? K + (long)key * p.ldqkv + c : Z);
+    vv[it] = *reinterpret_cast<const u32x4*>(v ? V + (long)key * p.ldqkv + c : Z);
+  }
+#pragma unroll
+  for (int it = 0; it < SIT; ++it) {
+    const int i = tid + it * 256;
+    const int key = i >> 3, c = (i & 7) * 8;
+    if (key < Lp) {
+      *reinterpret_cast<u32x4*>(Ks + key * ATT_KST + c) = kv[it];
+      const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv[it]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Vt[(c + e) * VST + key] = ve[e];
+    }
   }
   __syncthreads();
   const int q0 = blockIdx.y * 64 + wave * 16;
@@ -185,8 +200,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int q = q0 + lrow;
-    if (q < p.L) qa[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)q * p.ldqkv + ks * 32 + lk);
-    else qa[ks] = bf16x8{};
+    qa[ks] = *reinterpret_cast<const bf16x8*>(q < p.L ? Q + (long)q * p.ldqkv + ks * 32 + lk : Z);
   }
   // ---- S = Q K^T: lane holds S[q0 + 4*(lane>>4) + i][kt*16 + lrow] ----
   const int nkt = Lp / 16;
@@ -197,7 +211,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
     if (kt < nkt) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Ks + (kt * 16 + lrow) * ATT_D + ks * 32 + lk);
+        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Ks + (kt * 16 + lrow) * ATT_KST + ks * 32 + lk);
         s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], kb, s[kt], 0, 0, 0);
       }
     }
@@ -236,12 +250,12 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum[i] += __shfl_xor(sum[i], o, 64);
-  bf16_t* P = Ps + wave * 16 * Lp;
+  bf16_t* P = Ps + wave * 16 * VST;
 #pragma unroll
   for (int kt = 0; kt < ATT_LMAX / 16; ++kt) {
     if (kt < nkt) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) P[(4 * (lane >> 4) + i) * Lp + kt * 16 + lrow] = f2bf(s[kt][i] / sum[i]);
+      for (int i = 0; i < 4; ++i) P[(4 * (lane >> 4) + i) * VST + kt * 16 + lrow] = f2bf(s[kt][i] / sum[i]);
     }
   }
   // P is private to this wave: make the writes visible to the wave's own cross-lane reads
@@ -252,10 +266,10 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int ks = 0; ks < Lp / 32; ++ks) {
-    const bf16x8 pa = *reinterpret_cast<const bf16x8*>(P + lrow * Lp + ks * 32 + lk);
+    const bf16x8 pa = *reinterpret_cast<const bf16x8*>(P + lrow * VST + ks * 32 + lk);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + lrow) * Lp + ks * 32 + lk);
+      const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + lrow) * VST + ks * 32 + lk);
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
     }
   }
@@ -364,7 +378,7 @@ extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) 
   if (p.head_dim != ATT_D || p.L > ATT_LMAX || p.L < 1) return -1;
   if (p.out8 && (!p.os8 || p.ldo % 32)) return -1;
   const int Lp = (p.L + 31) & ~31;
-  const size_t lds = (size_t)(2 * Lp * ATT_D + 4 * 16 * Lp) * sizeof(bf16_t);
+  const size_t lds = (size_t)(Lp * ATT_KST + ATT_D * (Lp + 8) + 4 * 16 * (Lp + 8)) * sizeof(bf16_t);
   hipLaunchKernelGGL(attention_kernel, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
   return (int)hipGetLastError();
 }
