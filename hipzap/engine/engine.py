@@ -48,7 +48,7 @@ def add_softmax_head(g) -> None:
 class Engine:
     def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
                  capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
-                 host_io: bool = True, probs: bool = False):
+                 host_io: bool = True, probs: bool = False, zero_copy: str | None = None):
         self.model = model
         self.adapter = registry.get(model)
         self.device = torch.device(device)
@@ -65,7 +65,7 @@ class Engine:
             if probs:
                 add_softmax_head(self.graph)
             self.host_io = host_io
-            self.contexts = [ExecContext(self.graph, params, self.device, tuned, host_io=host_io)
+            self.contexts = [ExecContext(self.graph, params, self.device, tuned, host_io=host_io, zero_copy=zero_copy)
                              for _ in range(num_contexts)]
             self.streams = [torch.cuda.Stream(device=self.device) for _ in range(num_contexts)]
             torch.cuda.synchronize(self.device)

@@ -43,7 +43,7 @@ def conv_pairs(g: Graph) -> dict:
 
 class ExecContext:
     def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
-                 host_io: bool = False, pair_convs: bool | None = None):
+                 host_io: bool = False, pair_convs: bool | None = None, zero_copy: str | None = None):
         self.graph = g
         self.device = torch.device(device)
         self.params = params
@@ -97,16 +97,26 @@ class ExecContext:
             conv_plans.append((cfg, kw, key))
         # host_io: the request's PCIe transfers are part of the program (and of the graph):
         # pinned host inputs -> device inputs ... device output -> pinned host output.
+        # zero_copy ("in", "out", "all"): the first/last kernels read the request from / write the
+        # result to the pinned host buffers directly (UVA), replacing the copy node(s) and their
+        # kernel boundaries; HIPZAP_ZERO_COPY picks the default.
         self.host_io = host_io
+        zc = zero_copy if zero_copy is not None else os.environ.get("HIPZAP_ZERO_COPY", "")
+        self.zc_in, self.zc_out = host_io and zc in ("in", "all", "1"), host_io and zc in ("out", "all", "1")
         if host_io:
             self.host_inputs = [torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype).pin_memory()
                                 for t in g.inputs]
             self.host_input = self.host_inputs[0]
             self.host_output = torch.zeros(self.output.shape, dtype=self.output.dtype).pin_memory()
             for t, hbuf in zip(g.inputs, self.host_inputs):
+                if self.zc_in:
+                    self.ext[t] = hbuf
+                    continue
                 d = self.ext[t]
                 N.check(lib.hz_prog_add_memcpy(self.prog, d.data_ptr(), hbuf.data_ptr(), d.numel() * d.element_size(),
                                                0), "h2d")
+            if self.zc_out:
+                self.ext[g.outputs[0]] = self.host_output
         if pair_convs is None:
             pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
         self.pairs = conv_pairs(g) if pair_convs else {}
@@ -119,7 +129,7 @@ class ExecContext:
                 continue
             self._add_node(lib, n, conv_plans[i])
             i += 1
-        if host_io:
+        if host_io and not self.zc_out:
             N.check(lib.hz_prog_add_memcpy(self.prog, self.host_output.data_ptr(), self.output.data_ptr(),
                                            self.output.numel() * self.output.element_size(), 0), "d2h")
 

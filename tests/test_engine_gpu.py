@@ -96,3 +96,15 @@ def test_uint8_image_requests(model_sd):
     with torch.no_grad():
         eager = m((img.permute(0, 3, 1, 2).float() / 255 - mean) / std)
     assert y.argmax(1).item() == eager.argmax(1).item()
+
+
+@pytest.mark.parametrize("zc", ["in", "out", "all"])
+def test_zero_copy_host_io(model_sd, zc):
+    """Kernels reading the request from / writing logits to pinned host memory (no copy nodes)
+    give the same result as the copy-node program, across several replays."""
+    name, m, sd = model_sd
+    base = Engine.from_state_dict(name, sd, DEV, batch=1, zero_copy="")
+    eng = Engine.from_state_dict(name, sd, DEV, batch=1, zero_copy=zc)
+    for seed in range(3):
+        x = torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(seed))
+        assert torch.equal(eng.infer(x), base.infer(x))
