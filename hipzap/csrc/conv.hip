@@ -27,8 +27,9 @@
 
 namespace {
 
-// 64 zero bytes: the load target of lanes / K-steps that have nothing to read (see load_step)
-__device__ __attribute__((aligned(64))) unsigned int g_zero[16] = {0};
+// 4 KiB of zeros: the load target of lanes with nothing to read (see load_step). Lanes spread
+// over 256 distinct 16-B slots: a single shared zero line became an L2-channel hotspot.
+__device__ __attribute__((aligned(256))) unsigned int g_zero[1024] = {0};
 
 template <int FC, int FP>
 struct Depth {
@@ -113,7 +114,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   // (`if (valid) b = load; else b = 0`) made hipcc wait vmcnt(0) at every join, i.e. the
   // register ring never had more than one step in flight (cdna_hip_programming.md §5
   // "Projection GEMM" trap (c); seen in the ISA of the v3 kernel).
-  const bf16_t* __restrict__ Z = reinterpret_cast<const bf16_t*>(g_zero);
+  const bf16_t* __restrict__ Z = reinterpret_cast<const bf16_t*>(g_zero) + ((lane + (lid & 3) * 64) & 255) * 8;
   auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP]) {
     const bool sv = t < nsteps;  // wave-uniform: steps past this wave's share read zeros
     const int s_idx = s_begin + t;
@@ -168,12 +169,15 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   };
 
 #pragma unroll
-  for (int u = 0; u < DEPTH; ++u) load_step(u, fa[u], fb[u]);
+  for (int u = 0; u < DEPTH; ++u)
+    if (u < nsteps) load_step(u, fa[u], fb[u]);
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
       const int tt = t + u;
-      load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
+      // whole steps past this wave's share are skipped (wave-uniform branch): loading zeros for
+      // them instead measured 10-18 % slower on ResNet-50 (A/B on one box, profiles/r1_ab)
+      if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
       if (tt < nsteps) {
 #pragma unroll
         for (int i = 0; i < FC; ++i)

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const HzQuantParams p) 
   if (lane == 0) p.scale[row] = scale;
 }
 
-__device__ __attribute__((aligned(64))) unsigned int g_zero8[16] = {0};
+__device__ __attribute__((aligned(256))) unsigned int g_zero8[512] = {0};  // spread zero slots (see conv.hip)
 
 template <int FC, int FP>
 struct Depth8 {
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(fp8_max_threads(FC * FP)) void gemm_fp8_kernel(cons
     for (int j = 0; j < FP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // branch-free loads (zero bytes for invalid lanes / steps): see conv.hip load_step
-  const unsigned char* __restrict__ Z = reinterpret_cast<const unsigned char*>(g_zero8);
+  const unsigned char* __restrict__ Z = reinterpret_cast<const unsigned char*>(g_zero8) + ((lane + (lid & 3) * 64) & 255) * 8;
   auto load_step = [&](int t, long(&a)[FC], long(&b)[FP]) {
     const bool sv = t < nsteps;
     const int s_idx = s_begin + t;
@@ -104,12 +104,13 @@ __global__ __launch_bounds__(fp8_max_threads(FC * FP)) void gemm_fp8_kernel(cons
     }
   };
 #pragma unroll
-  for (int u = 0; u < DEPTH; ++u) load_step(u, fa[u], fb[u]);
+  for (int u = 0; u < DEPTH; ++u)
+    if (u < nsteps) load_step(u, fa[u], fb[u]);
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
       const int tt = t + u;
-      load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
+      if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
       if (tt < nsteps) {
 #pragma unroll
         for (int i = 0; i < FC; ++i)

@@ -151,7 +151,6 @@ constexpr int ATT_D = 64;
 constexpr int ATT_LMAX = 256;
 
 constexpr int ATT_KST = ATT_D + 8;  // padded K row stride: the 16 rows of a fragment read hit distinct banks
-__device__ __attribute__((aligned(64))) unsigned int g_zero_att[16] = {0};
 
 __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -160,7 +159,6 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);          // [Lp][ATT_KST]
   bf16_t* Vt = Ks + Lp * ATT_KST;                       // [64][VST]
   bf16_t* Ps = Vt + ATT_D * VST;                        // [4 waves][16][VST]
-  const bf16_t* Z = reinterpret_cast<const bf16_t*>(g_zero_att);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
   const int b = bh / p.heads, h = bh - b * p.heads;
@@ -168,23 +166,26 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
   const bf16_t* Q = p.qkv + row0 * p.ldqkv + h * ATT_D;
   const bf16_t* K = Q + p.k_off;
   const bf16_t* V = Q + p.v_off;
-  // ---- stage K (row-major) and V^T in LDS: every load issued first (padding keys read the
-  // zero buffer: an address select, not a branch around the load — one round trip, not 8) ----
+  // ---- stage K (row-major) and V^T in LDS: every load issued first — one round trip, not one
+  // per iteration. Padding keys (L <= key < Lp) re-read row L-1: their scores are masked to -inf
+  // and their probabilities are exactly 0, so any finite row is correct (no branch, no zero
+  // buffer hotspot) ----
   constexpr int SIT = ATT_LMAX * 8 / 256;
   u32x4 kv[SIT], vv[SIT];
 #pragma unroll
   for (int it = 0; it < SIT; ++it) {
+    if (it * 32 >= Lp) break;  // block-uniform
     const int i = tid + it * 256;
-    const int key = i >> 3, c = (i & 7) * 8;
-    const bool v = key < p.L;
-    kv[it] = *reinterpret_cast<const u32x4*>(v ? K + (long)key * p.ldqkv + c : Z);
-    vv[it] = *reinterpret_cast<const u32x4*>(v ? V + (long)key * p.ldqkv + c : Z);
+    const int key = min(i >> 3, p.L - 1), c = (i & 7) * 8;
+    kv[it] = *reinterpret_cast<const u32x4*>(K + (long)key * p.ldqkv + c);
+    vv[it] = *reinterpret_cast<const u32x4*>(V + (long)key * p.ldqkv + c);
   }
 #pragma unroll
   for (int it = 0; it < SIT; ++it) {
+    if (it * 32 >= Lp) break;
     const int i = tid + it * 256;
     const int key = i >> 3, c = (i & 7) * 8;
-    if (key < Lp) {
+    {
       *reinterpret_cast<u32x4*>(Ks + key * ATT_KST + c) = kv[it];
       const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv[it]);
 #pragma unroll
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int q = q0 + lrow;
-    qa[ks] = *reinterpret_cast<const bf16x8*>(q < p.L ? Q + (long)q * p.ldqkv + ks * 32 + lk : Z);
+    qa[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)min(q, p.L - 1) * p.ldqkv + ks * 32 + lk);  // rows >= L discarded
   }
   // ---- S = Q K^T: lane holds S[q0 + 4*(lane>>4) + i][kt*16 + lrow] ----
   const int nkt = Lp / 16;
