@@ -27,10 +27,6 @@
 
 namespace {
 
-// 4 KiB of zeros: the load target of lanes with nothing to read (see load_step). Lanes spread
-// over 256 distinct 16-B slots: a single shared zero line became an L2-channel hotspot.
-__device__ __attribute__((aligned(256))) unsigned int g_zero[1024] = {0};
-
 template <int FC, int FP>
 struct Depth {
   static constexpr int value = (FC + FP <= 2) ? 6 : (FC + FP <= 3) ? 4 : (FC + FP <= 4) ? 3 : 2;
@@ -109,52 +105,51 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     cur_r = rs0 / p.S;
     cur_s = rs0 - cur_r * p.S;
   }
-  // Every load is issued unconditionally: a lane or step with nothing to read loads 16 zero
-  // bytes from g_zero instead (address select, no data select). A branch around a load
-  // (`if (valid) b = load; else b = 0`) made hipcc wait vmcnt(0) at every join, i.e. the
-  // register ring never had more than one step in flight (cdna_hip_programming.md §5
-  // "Projection GEMM" trap (c); seen in the ISA of the v3 kernel).
-  const bf16_t* __restrict__ Z = reinterpret_cast<const bf16_t*>(g_zero) + ((lane + (lid & 3) * 64) & 255) * 8;
+  // Per-lane validity is a branch around each activation load. Address-select variants that
+  // keep every load unconditional (hipcc then pipelines the whole ring instead of waiting
+  // vmcnt(0) per step) were A/B-measured on one box: +2.7 % single stream but -2 % at 8
+  // concurrent streams with a spread zero region, -10/-18 % with a shared zero line + zero
+  // loads for out-of-range steps (profiles/r1_ab). Throughput is the objective, so this stays.
   auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP]) {
-    const bool sv = t < nsteps;  // wave-uniform: steps past this wave's share read zeros
     const int s_idx = s_begin + t;
     const int k = s_idx * 32;
 #pragma unroll
     for (int i = 0; i < FC; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(sv ? Wf + ((long)i * steps + s_idx) * 512 : Z);
+      a[i] = *reinterpret_cast<const bf16x8*>(Wf + ((long)i * steps + s_idx) * 512);
     if constexpr (XROW) {  // plain GEMM: row-major activations [M][ldx] (transformers)
 #pragma unroll
       for (int j = 0; j < FP; ++j) {
         const int kk = k + lk;
-        const bool v = sv && pval[j] && kk < p.K;
-        b[j] = *reinterpret_cast<const bf16x8*>(v ? X + (long)(m0 + j * 16 + lrow) * p.ldx + kk : Z);
+        if (pval[j] && kk < p.K) b[j] = *reinterpret_cast<const bf16x8*>(X + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
+        else b[j] = bf16x8{};
       }
     } else if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
       const int cb = cur_cb, r = cur_r, s = cur_s;
-      // advance the running position (scalar, wave-uniform; selects, no branches)
-      const bool wrap_c = cur_cb + 1 == CB;
-      const bool wrap_s = wrap_c && cur_s + 1 == p.S;
-      cur_cb = wrap_c ? 0 : cur_cb + 1;
-      cur_r = wrap_s ? cur_r + 1 : cur_r;
-      cur_s = wrap_c ? (wrap_s ? 0 : cur_s + 1) : cur_s;
+      if (++cur_cb == CB) {  // advance the running position (scalar, wave-uniform)
+        cur_cb = 0;
+        if (++cur_s == p.S) {
+          cur_s = 0;
+          ++cur_r;
+        }
+      }
       if constexpr (IS1X1) {
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
-          const bool v = sv && pval[j];
-          b[j] = *reinterpret_cast<const bf16x8*>(v ? X + ((long)(pb[j] + cb * HW) << 5) + lk : Z);
+          if (pval[j]) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + cb * HW) << 5) + lk);
+          else b[j] = bf16x8{};
         }
       } else {
         const int uoff = cb * HW + r * p.W + s;  // wave-uniform part of the pixel offset
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
-          const bool v = sv && pval[j] && (unsigned)(pih[j] + r) < (unsigned)p.H &&
-                         (unsigned)(piw[j] + s) < (unsigned)p.W;
-          b[j] = *reinterpret_cast<const bf16x8*>(v ? X + ((long)(pb[j] + uoff) << 5) + lk : Z);
+          const bool v = pval[j] && (unsigned)(pih[j] + r) < (unsigned)p.H && (unsigned)(piw[j] + s) < (unsigned)p.W;
+          if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + uoff) << 5) + lk);
+          else b[j] = bf16x8{};
         }
       }
     } else {  // plain NHWC input with C in {8, 16}: per-lane (r, s, c) decomposition
       const int kk = k + lk;
-      const bool kval = sv && kk < p.K;
+      const bool kval = kk < p.K;
       const int rs = kk / C;
       const int c = kk - rs * C;
       const int r = rs / p.S;
@@ -163,7 +158,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
       for (int j = 0; j < FP; ++j) {
         const int ih = pih[j] + r, iw = piw[j] + s;
         const bool v = kval && pval[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        b[j] = *reinterpret_cast<const bf16x8*>(v ? X + ((long)(pb[j] + ih * p.W + iw)) * C + c : Z);
+        if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + ih * p.W + iw)) * C + c);
+        else b[j] = bf16x8{};
       }
     }
   };
@@ -175,8 +171,6 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
       const int tt = t + u;
-      // whole steps past this wave's share are skipped (wave-uniform branch): loading zeros for
-      // them instead measured 10-18 % slower on ResNet-50 (A/B on one box, profiles/r1_ab)
       if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
       if (tt < nsteps) {
 #pragma unroll

@@ -36,9 +36,31 @@ __global__ void probe_mfma_f8_kernel(const unsigned char* ab, float* c, int layo
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
   for (int i = 0; i < 4; ++i) c[(4 * (l >> 4) + i) * 16 + (l & 15)] = acc[i];
 }
+
+// Block-scale probe: ab = [A 16x128][B^T 16x128] e4m3 bytes (layout 0 map) + [64 x int scale_a]
+// + [64 x int scale_b] (E8M0 in the low byte, opsel 0); writes D through the C/D map.
+__global__ void probe_mfma_scale_kernel(const unsigned char* ab, float* c) {
+  const int l = threadIdx.x;
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+  i32x8 a, b;
+  unsigned char* pa = reinterpret_cast<unsigned char*>(&a);
+  unsigned char* pb = reinterpret_cast<unsigned char*>(&b);
+  for (int j = 0; j < 32; ++j) {
+    pa[j] = ab[(l & 15) * 128 + probe_k(0, l, j)];
+    pb[j] = ab[2048 + (l & 15) * 128 + probe_k(0, l, j)];
+  }
+  const int* sc = reinterpret_cast<const int*>(ab + 4096);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sc[l], 0, sc[64 + l]);
+  for (int i = 0; i < 4; ++i) c[(4 * (l >> 4) + i) * 16 + (l & 15)] = acc[i];
+}
 }  // namespace
 
 extern "C" int hz_diag_launch(int kind, int blocks, int threads, void* a, void* b, long bytes, hipStream_t st) {
+  if (kind == 3) {  // MFMA block-scale probe
+    hipLaunchKernelGGL(probe_mfma_scale_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)a, (float*)b);
+    return (int)hipGetLastError();
+  }
   if (kind == 2) {  // MFMA f8f6f4 layout probe: blocks = layout id
     hipLaunchKernelGGL(probe_mfma_f8_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)a, (float*)b, blocks);
     return (int)hipGetLastError();

@@ -165,3 +165,40 @@ def test_attention_mx8_output():
     got = _mx_decode(o8.cpu(), os8.cpu())
     ref_q, _ = F8.quant_mx_ref(ref.float())
     assert ((got - ref_q).abs().max() / ref_q.abs().max()).item() < 0.1  # <= one e4m3 step
+
+
+def _probe_scales(A, Bt, sa, sb):
+    import ctypes
+    from hipzap import _native as N
+    buf = torch.cat([A.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1),
+                     Bt.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1),
+                     torch.tensor(sa, dtype=torch.int32).view(torch.uint8),
+                     torch.tensor(sb, dtype=torch.int32).view(torch.uint8)]).to(DEV)
+    c = torch.zeros(16, 16, device=DEV)
+    N.check(N.lib().hz_diag_launch(3, 1, 64, ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(c.data_ptr()), 0,
+                                   N.stream_ptr()), "probe scale")
+    torch.cuda.synchronize()
+    return c.cpu()
+
+
+def test_mfma_block_scale_lane_map():
+    """Which lane's scale byte scales which (row/column, 32-k block) of the f8f6f4 MFMA:
+    csrc/fp8.hip feeds the activation (B) scale of token l&15, k-block l>>4 from lane l."""
+    ones = torch.ones(16, 128)
+    found = {}
+    for operand in ("a", "b"):
+        for lane in (0, 1, 17, 33, 50):
+            sa, sb = [127] * 64, [127] * 64
+            (sa if operand == "a" else sb)[lane] = 129  # x4 on one lane's block
+            d = _probe_scales(ones, ones, sa, sb)
+            diff = (d != 128).nonzero().tolist()
+            found[(operand, lane)] = diff
+    # expected (H1): lane l scales A row l&15 (resp. B column l&15) for k-block l>>4:
+    # one 32-k block x4 -> that row/column sums 3*32 + 4*32 = 224
+    for (operand, lane), diff in found.items():
+        rows = sorted({r for r, _ in diff})
+        cols = sorted({c for _, c in diff})
+        if operand == "a":
+            assert rows == [lane & 15] and len(cols) == 16, (operand, lane, diff[:4], found)
+        else:
+            assert cols == [lane & 15] and len(rows) == 16, (operand, lane, diff[:4], found)
