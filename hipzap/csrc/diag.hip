@@ -54,9 +54,33 @@ __global__ void probe_mfma_scale_kernel(const unsigned char* ab, float* c) {
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sc[l], 0, sc[64 + l]);
   for (int i = 0; i < 4; ++i) c[(4 * (l >> 4) + i) * 16 + (l & 15)] = acc[i];
 }
+
+// Raw-register block-scale probe: ab = [A regs: 64 lanes x 32 B][B regs: 64 x 32 B]
+// [scale_a: 64 x int][scale_b: 64 x int]; each lane's operand registers are loaded verbatim,
+// so the host decides which register byte carries which value (maps a register byte to the
+// scale lane that governs it: the K order the block scales assume).
+__global__ void probe_mfma_scale_raw_kernel(const unsigned char* ab, float* c) {
+  const int l = threadIdx.x;
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+  i32x8 a, b;
+  unsigned char* pa = reinterpret_cast<unsigned char*>(&a);
+  unsigned char* pb = reinterpret_cast<unsigned char*>(&b);
+  for (int j = 0; j < 32; ++j) {
+    pa[j] = ab[l * 32 + j];
+    pb[j] = ab[2048 + l * 32 + j];
+  }
+  const int* sc = reinterpret_cast<const int*>(ab + 4096);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sc[l], 0, sc[64 + l]);
+  for (int i = 0; i < 4; ++i) c[(4 * (l >> 4) + i) * 16 + (l & 15)] = acc[i];
+}
 }  // namespace
 
 extern "C" int hz_diag_launch(int kind, int blocks, int threads, void* a, void* b, long bytes, hipStream_t st) {
+  if (kind == 4) {  // raw-register block-scale probe
+    hipLaunchKernelGGL(probe_mfma_scale_raw_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)a, (float*)b);
+    return (int)hipGetLastError();
+  }
   if (kind == 3) {  // MFMA block-scale probe
     hipLaunchKernelGGL(probe_mfma_scale_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)a, (float*)b);
     return (int)hipGetLastError();

@@ -205,15 +205,16 @@ extern "C" int hz_quant_launch(const HzQuantParams* pp, hipStream_t st) {
 // Large-M fp8 GEMM on v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3): twice the bf16 MFMA
 // rate (MI355X_MICROARCH.md, MFMA table). The block scales are all 1.0 (E8M0 0x7f); the real
 // per-row activation and per-channel weight scales stay fp32 and are applied in the epilogue,
-// so the numerics equal the 16x16x32 fp8 kernel above. Operand map (pinned by
-// tests/test_fp8_gpu.py::test_mfma_f8f6f4_operand_layout): lane l holds row l&15,
-// k = 32*(l>>4) + j, j < 32 (32 bytes = two 16-B halves).
+// so the numerics equal the 16x16x32 fp8 kernel above. Operand map: lane l holds row l&15 and,
+// in register half h, k = 64h + 16*(l>>4) + j, j < 16 — the hardware K order, which only the
+// block scales can observe (tests/test_fp8_gpu.py::test_mfma_block_scale_kblock_map; MX input
+// scales of lane l apply to row l&15, 32-k block l>>4).
 //   * weights MX-packed [N/16][K/128][half][64 lanes][16 B]: a 2-KiB fragment is two lane-linear
 //     1-KiB glds pieces, and each half is read back with a conflict-free ds_read_b128;
 //   * activations (row-major fp8, 128-B rows per 128-deep k-step) staged in full 128-B lines,
 //     16-B chunks XOR-swizzled with MX_SWZ (chunk' = c ^ f((row>>1)&7), f found by exhaustive
 //     search to make the 16 rows of every ds_read_b128 lane group hit 16 distinct bank slots
-//     for this kernel's chunk pattern 2*(l>>4)+half);
+//     for this kernel's chunk pattern (l>>4)+4*half — conflict-free, as for the earlier pattern);
 //   * 3 LDS stages, counted vmcnt + raw s_barrier, as csrc/gemm.hip.
 namespace {
 
@@ -240,8 +241,9 @@ __device__ __forceinline__ void wait_vm8() {
 
 // XS: the activations carry MX block scales (p.xs, one E8M0 byte per 32 k): each wave also
 // stages one 4-byte-per-lane piece (64 rows x the 4 block scales of this 128-deep k-step) and
-// the scale goes to the MFMA's B-scale operand (lane l: token l&15, k-block l>>4 — the same
-// lane that holds those 32 bytes).
+// the scale goes to the MFMA's B-scale operand: lane l supplies token l&15's scale of 32-k block
+// l>>4 (the hardware K order above: block b lives in the register halves of lane groups
+// 2(b&1)..2(b&1)+1, not in lane group b).
 template <int BM, int BN, int NS, bool XS>
 __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;
@@ -288,8 +290,10 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
 
   const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
   const int brow = (wm * (BM / 2) + lr) * 128;
-  const int boff0 = brow + ((2 * (lane >> 4)) ^ swz) * 16;
-  const int boff1 = brow + ((2 * (lane >> 4) + 1) ^ swz) * 16;
+  // hardware K order of the f8f6f4 MFMA (what the E8M0 block scales index): lane group g holds
+  // k = 16g..16g+15 in its low 16 B and 64+16g.. in its high 16 B
+  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
+  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
   const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
 
   f32x4 acc[FCW][FPW];

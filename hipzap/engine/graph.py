@@ -9,6 +9,8 @@ touch to the whole fork..join window, so concurrent branches never alias.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 
 import torch
@@ -94,9 +96,15 @@ def lifetimes(g: Graph) -> dict[int, list[int]]:
     return life
 
 
-def plan_memory(g: Graph) -> tuple[dict[int, int], int]:
-    """Return ({tensor id: arena byte offset}, arena bytes)."""
+def plan_memory(g: Graph, reuse: bool | None = None) -> tuple[dict[int, int], int]:
+    """Return ({tensor id: arena byte offset}, arena bytes). ``reuse=False`` (or env
+    ``HIPZAP_ARENA_NOREUSE=1``) gives every tensor its own slot, so every intermediate stays
+    readable after a run (per-node debugging, ``scripts/debug_nodes.py``)."""
+    if reuse is None:
+        reuse = os.environ.get("HIPZAP_ARENA_NOREUSE", "0") != "1"
     life = lifetimes(g)
+    if not reuse:
+        life = {t: [0, len(g.nodes)] for t in life}
     order = sorted(life.keys(), key=lambda t: -g.tensors[t].nbytes)
     placed: list[tuple[int, int, int, int]] = []  # (offset, end, first, last)
     offsets: dict[int, int] = {}

@@ -73,15 +73,17 @@ def quantize_weight(w2d: torch.Tensor, rows_pad: int | None = None):
 
 def mx_pack(q: torch.Tensor) -> torch.Tensor:
     """[rows, K] e4m3 bytes (rows % 16 == 0, K % 128 == 0) -> [rows/16, K/128, 2, 64, 16]:
-    lane l = 16*(k%128 // 32) + row%16 holds k%32 = 16*half + byte (v_mfma_scale_f32_16x16x128_f8f6f4)."""
+    lane l = 16*lg + row%16, register half h holds k%128 = 64*h + 16*lg + byte — the hardware K
+    order of v_mfma_scale_f32_16x16x128_f8f6f4, which the E8M0 block scales follow (pinned by
+    tests/test_fp8_gpu.py::test_mfma_block_scale_kblock_map)."""
     rows, K = q.shape
-    t = q.reshape(rows // 16, 16, K // 128, 4, 2, 16)          # g, r, kb, lg, half, byte
-    return t.permute(0, 2, 4, 3, 1, 5).reshape(rows // 16, K // 128, 2, 64, 16)
+    t = q.reshape(rows // 16, 16, K // 128, 2, 4, 16)          # g, r, kb, half, lg, byte
+    return t.permute(0, 2, 3, 4, 1, 5).reshape(rows // 16, K // 128, 2, 64, 16)
 
 
 def mx_unpack(w: torch.Tensor) -> torch.Tensor:
     g, kb = w.shape[0], w.shape[1]
-    return w.reshape(g, kb, 2, 4, 16, 16).permute(0, 4, 1, 3, 2, 5).reshape(g * 16, kb * 128)
+    return w.reshape(g, kb, 2, 4, 16, 16).permute(0, 4, 1, 2, 3, 5).reshape(g * 16, kb * 128)
 
 
 def quantize_linear(pc: PackedConv) -> PackedFp8:

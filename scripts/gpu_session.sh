@@ -17,7 +17,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 STEPS=${STEPS:-all}
 python -c "import torch; print(torch.cuda.get_device_name(0))"
-[[ $STEPS == *tests* || $STEPS == all ]] && step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *tests* || $STEPS == all ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* || $STEPS == all ]] && step smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *tune* || $STEPS == all ]] && {
   step tune 900 python -m hipzap.engine.tune --model ${TUNE_MODEL:-resnet50} --batch ${TUNE_BATCH:-1} --concurrent ${TUNE_CONC:-1 8} --report $OUT/tune_report.json

@@ -202,3 +202,47 @@ def test_mfma_block_scale_lane_map():
             assert rows == [lane & 15] and len(cols) == 16, (operand, lane, diff[:4], found)
         else:
             assert cols == [lane & 15] and len(rows) == 16, (operand, lane, diff[:4], found)
+
+
+def _probe_raw(a_regs, b_regs, sa, sb):
+    """a_regs/b_regs: [64 lanes, 32] fp32 values placed verbatim in the operand registers."""
+    import ctypes
+    from hipzap import _native as N
+    buf = torch.cat([a_regs.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1),
+                     b_regs.to(torch.float8_e4m3fn).view(torch.uint8).reshape(-1),
+                     torch.tensor(sa, dtype=torch.int32).view(torch.uint8),
+                     torch.tensor(sb, dtype=torch.int32).view(torch.uint8)]).to(DEV)
+    c = torch.zeros(16, 16, device=DEV)
+    N.check(N.lib().hz_diag_launch(4, 1, 64, ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(c.data_ptr()), 0,
+                                   N.stream_ptr()), "probe scale raw")
+    torch.cuda.synchronize()
+    return c.cpu()
+
+
+def mfma_scale_kblock_map() -> dict:
+    """{(lane group g, register byte j): lane group whose B-scale applies to that byte}.
+    A = ones; B = one nonzero register byte (g, j) in every lane of group g; B scales 2^h for
+    lane group h -> D = 2^(governing group)."""
+    out = {}
+    sa = [127] * 64
+    sb = [127 + (lane >> 4) for lane in range(64)]
+    a = torch.ones(64, 32)
+    for g in range(4):
+        for j in range(32):
+            b = torch.zeros(64, 32)
+            b[16 * g: 16 * g + 16, j] = 1.0
+            d = _probe_raw(a, b, sa, sb)
+            v = d[0, 0].item()
+            assert torch.all(d == v), d
+            out[(g, j)] = int(round(torch.log2(torch.tensor(v)).item()))
+    return out
+
+
+def test_mfma_block_scale_kblock_map():
+    """The hardware K order the block scales follow: register byte j of lane group g is
+    k = 64*(j//16) + 16*g + j%16, i.e. in 32-k block 2*(j//16) + g//2, and lane group b's scale
+    byte scales block b. csrc/fp8.hip (gemm_mx_kernel) and ops/fp8.py (mx_pack) place the data
+    in this order. (Unscaled MFMA results cannot see this: any K permutation shared by A and B
+    gives the same dot product, which is why the operand-layout probe above passes either way.)"""
+    m = mfma_scale_kblock_map()
+    assert all(m[(g, j)] == 2 * (j // 16) + g // 2 for g in range(4) for j in range(32)), m

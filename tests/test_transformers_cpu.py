@@ -101,15 +101,15 @@ def test_fp8_weight_roundtrip():
 
 
 def test_mx_pack_layout():
-    """MX packing (csrc/fp8.hip gemm_mx_kernel): lane l = 16*((k%128)//32) + row%16 holds
-    k%32 = 16*half + byte; mx_unpack inverts it."""
+    """MX packing (csrc/fp8.hip gemm_mx_kernel): lane l = 16*lg + row%16, register half h holds
+    k%128 = 64*h + 16*lg + byte (the f8f6f4 MFMA's hardware K order); mx_unpack inverts it."""
     from hipzap.ops import fp8 as F8
     q = torch.randint(0, 256, (32, 256), dtype=torch.uint8)
     w = F8.mx_pack(q)
     assert w.shape == (2, 2, 2, 64, 16)
     assert torch.equal(F8.mx_unpack(w), q)
     g, kb, half, lane, byte = 1, 1, 1, 37, 5
-    row, k = g * 16 + lane % 16, kb * 128 + (lane // 16) * 32 + half * 16 + byte
+    row, k = g * 16 + lane % 16, kb * 128 + half * 64 + (lane // 16) * 16 + byte
     assert w[g, kb, half, lane, byte] == q[row, k]
 
 
