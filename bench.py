@@ -205,8 +205,12 @@ def main():
         params = broadcast_params(params, meta, device)
         torch.cuda.synchronize(device)
         timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
+        # zero-copy request IO: the preprocess kernel reads the pinned request bytes and pool_fc writes
+        # the pinned logits directly (no copy nodes): +1.7 % single stream, +0.5-1 % at 8 streams
+        # (profiles/r1_ab/zero_copy.txt, interleaved on one box)
         eng = Engine(args.model, params, device, batch=args.batch, num_contexts=args.streams,
-                     capture=not args.no_capture, tuned=tuned, arch_kw=arch_kw, timings=timings, host_io=True)
+                     capture=not args.no_capture, tuned=tuned, arch_kw=arch_kw, timings=timings, host_io=True,
+                     zero_copy=os.environ.get("HIPZAP_ZERO_COPY", "all"))
         x = request_input(args, adapter)
         out = eng.infer(x)
         cold_ms = (time.perf_counter() - t0) * 1e3
