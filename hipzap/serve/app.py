@@ -19,10 +19,11 @@ import time
 
 import numpy as np
 import torch
-from flask import Flask, Response, request
+from flask import Flask, Response, g, request
 
 from .. import __version__
 from ..utils.metrics import METRICS
+from ..utils.tracing import PhaseTimer, trace_range
 from .server import ModelServer
 from .settings import load_settings
 
@@ -48,9 +49,20 @@ def _json(obj, status=200) -> Response:
     return Response(response=json.dumps(obj), status=status, mimetype="application/json")
 
 
+def phase(name: str):
+    """Time a request phase: roctx range + the request's ``X-Timing`` header entry."""
+    return trace_range(name, getattr(g, "hz_timer", None))
+
+
 @app.after_request
 def _cors(resp: Response) -> Response:
     resp.headers["Access-Control-Allow-Origin"] = "*"
+    timer = getattr(g, "hz_timer", None)
+    t0 = getattr(request, "_hz_t0", None)
+    if timer is not None and t0 is not None:  # per-request phase timers (SURVEY.md §5 tracing)
+        timer.add("total", (time.perf_counter() - t0) * 1e3)
+        resp.headers["X-Timing"] = timer.header()
+        resp.headers["Access-Control-Expose-Headers"] = "X-Timing"
     if request.method == "OPTIONS":
         resp.headers["Access-Control-Allow-Methods"] = "GET, POST, OPTIONS"
         req_h = request.headers.get("Access-Control-Request-Headers")
@@ -62,6 +74,7 @@ def _cors(resp: Response) -> Response:
 @app.before_request
 def _preflight():
     request._hz_t0 = time.perf_counter()
+    g.hz_timer = PhaseTimer()
     if request.method == "OPTIONS":
         return Response(status=200)
     return None
@@ -103,7 +116,10 @@ def inference():
     words = [""] if not prompt else prompt.split()
     n = int(request.args.get("words", s.settings.lm_words))
     seed = request.args.get("seed")
-    text = s.lm().generate(words, n, seed=int(seed) if seed is not None else None)
+    with phase("load"):
+        lm = s.lm()
+    with phase("generate"):
+        text = lm.generate(words, n, seed=int(seed) if seed is not None else None)
     return _json({"response": {"text": text}})
 
 
@@ -156,9 +172,11 @@ def _predict_text(s, body):
     am = body.get("attention_mask")
     tt = torch.tensor(tt, dtype=torch.long).reshape(ids.shape) if tt is not None else None
     am = torch.tensor(am, dtype=torch.long).reshape(ids.shape) if am is not None else None
-    backend = s.text(model)
+    with phase("load"):
+        backend = s.text(model)
     t0 = time.perf_counter()
-    logits = backend(ids, tt, am)
+    with phase("infer"):
+        logits = backend(ids, tt, am)
     dt = (time.perf_counter() - t0) * 1e3
     probs = torch.softmax(logits.float(), dim=-1)
     return _json({"model": model, "backend": backend.backend, "batch": int(ids.shape[0]),
@@ -173,10 +191,13 @@ def predict():
         body = request.get_json(force=True, silent=True) or {}
         if "input_ids" in body:
             return _predict_text(s, body)
-    model, x = decode_input(request)
-    backend = s.vision(model)
+    with phase("decode"):
+        model, x = decode_input(request)
+    with phase("load"):
+        backend = s.vision(model)
     t0 = time.perf_counter()
-    logits = backend(x)
+    with phase("infer"):
+        logits = backend(x)
     dt = (time.perf_counter() - t0) * 1e3
     probs = torch.softmax(logits.float(), dim=-1)
     k = min(5, probs.shape[-1])

@@ -37,7 +37,7 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
     grep '^{' $OUT/bench_s$s.log > $OUT/bench_s$s.json || true
   done
 }
-[[ $STEPS == *prof* || $STEPS == all ]] && {
+[[ $STEPS == *" prof"* || $STEPS == prof* || $STEPS == all ]] && {
   step rocprof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --streams 1 --steps 50 --warmup 5 --cold-runs 0
   python scripts/trace_summary.py $OUT/prof $OUT/prof_summary && rm -rf $OUT/prof
 }
@@ -49,7 +49,8 @@ python -c "import torch; print(torch.cuda.get_device_name(0))"
   done
 }
 [[ $STEPS == *lmprof* ]] && {
-  HIPZAP_LM_WORDS=50 step prof_lm 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_lm -o run --output-format csv -- python3 scripts/bench_lm.py
-  python scripts/trace_summary.py $OUT/prof_lm $OUT/prof_summary_lm; rm -rf $OUT/prof_lm
+  export HIPZAP_LM_WORDS=50 HIPZAP_LM_CONTEXTS=1
+  step prof_lm 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_lm -o run --output-format csv -- python3 scripts/bench_lm.py
+  python scripts/trace_summary.py $OUT/prof_lm $OUT/prof_summary_lm lstm_cell_kernel; rm -rf $OUT/prof_lm
 }
 echo "=== done"

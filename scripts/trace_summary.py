@@ -4,7 +4,10 @@
 Writes (into the output dir): kernel_stats.csv (copied), one_inference_trace.txt (the
 dispatch timeline of one steady-state inference: from one preprocess kernel to the next, with
 start offset, duration, grid and workgroup sizes, VGPRs) and a short summary on stdout.
-Usage: trace_summary.py <rocprof -d dir> <out dir>
+Usage: trace_summary.py <rocprof -d dir> <out dir> [marker]
+``marker`` (default ``preprocess``): a substring of the kernel that starts each period
+(e.g. ``lstm_cell_kernel`` for one AWD-LSTM decode step: pass ``lstm_cell_kernel<4>`` or the
+layer-0 instantiation).
 """
 import csv
 import glob
@@ -15,6 +18,7 @@ import sys
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
+    marker = sys.argv[3] if len(sys.argv) > 3 else "preprocess"
     os.makedirs(out, exist_ok=True)
     stats = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)
     traces = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
@@ -25,7 +29,11 @@ def main():
         return
     rows = list(csv.DictReader(open(traces[0])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    if marker != "preprocess":  # several kernels may match (e.g. every LSTM layer): keep period starts
+        first = rows[starts[0]]["Kernel_Name"] if starts else None
+        starts = [i for i in starts if rows[i]["Kernel_Name"] == first]
+        starts = [i for k, i in enumerate(starts) if k == 0 or i - starts[k - 1] > 1]
     if len(starts) < 4:
         print("too few inferences in trace")
         return

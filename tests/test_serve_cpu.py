@@ -66,6 +66,18 @@ def test_predict_json_tensor(client):
     assert probs == sorted(probs, reverse=True)
 
 
+def test_x_timing_header(client):
+    """Per-request phase timers (SURVEY.md §5 tracing): decode/load/infer/total in X-Timing."""
+    r = client.post("/predict", json={"model": "resnet18", "inputs": torch.randn(1, 3, 32, 32).tolist()})
+    phases = dict(kv.split("=") for kv in r.headers["X-Timing"].split(";"))
+    assert {"decode", "load", "infer", "total"} <= set(phases)
+    assert all(float(v) >= 0 for v in phases.values())
+    assert float(phases["total"]) >= float(phases["infer"])
+    assert "X-Timing" in r.headers["Access-Control-Expose-Headers"]
+    gen = dict(kv.split("=") for kv in client.get("/inference?seed=3").headers["X-Timing"].split(";"))
+    assert {"load", "generate", "total"} <= set(gen)
+
+
 def test_predict_npy_and_image(client):
     buf = io.BytesIO()
     np.save(buf, np.random.randn(2, 3, 32, 32).astype(np.float32))
