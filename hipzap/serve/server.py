@@ -57,18 +57,26 @@ class VisionBackend:
             self.model.eval()
             self.engine = None
         self.batch = spec.batch
+        # "batching": {"max_wait_ms": 2} in the model's settings block -> concurrent small requests
+        # are coalesced into one captured-batch replay (serve/batcher.py)
+        bcfg = spec.extra.get("batching")
+        self.batcher = None
+        if bcfg and self.engine is not None and self.batch > 1:
+            from .batcher import DynamicBatcher
+            self.batcher = DynamicBatcher(self._run_padded, self.batch, float(bcfg.get("max_wait_ms", 2.0)), name)
         self.cold_ms = (time.perf_counter() - t0) * 1e3
+
+    def _run_padded(self, chunk: torch.Tensor) -> torch.Tensor:
+        n = chunk.shape[0]
+        if n < self.batch:  # pad the remainder to the captured batch size
+            chunk = torch.cat([chunk, chunk.new_zeros((self.batch - n,) + tuple(chunk.shape[1:]))])
+        return self.engine.infer(chunk)[:n]
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if self.engine is not None:
-            outs = []
-            for i in range(0, x.shape[0], self.batch):
-                chunk = x[i: i + self.batch]
-                n = chunk.shape[0]
-                if n < self.batch:  # pad the remainder to the captured batch size
-                    chunk = torch.cat([chunk, chunk.new_zeros((self.batch - n,) + tuple(chunk.shape[1:]))])
-                outs.append(self.engine.infer(chunk)[:n])
-            return torch.cat(outs)
+            if self.batcher is not None and x.shape[0] < self.batch:
+                return self.batcher(x)
+            return torch.cat([self._run_padded(x[i: i + self.batch]) for i in range(0, x.shape[0], self.batch)])
         with torch.no_grad():
             y = self.model(x.float())
             return torch.softmax(y, 1) if self.probs else y

@@ -108,3 +108,32 @@ def test_zero_copy_host_io(model_sd, zc):
     for seed in range(3):
         x = torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(seed))
         assert torch.equal(eng.infer(x), base.infer(x))
+
+
+def test_dynamic_batching_backend(model_sd):
+    """serve/batcher.py on the GPU: concurrent bs=1 requests coalesced into one batch-4
+    replay return the same logits as the same engine run on each request alone."""
+    import threading
+    from hipzap.serve.server import VisionBackend
+    from hipzap.serve.settings import ModelSpec
+    name, m, sd = model_sd
+    be = VisionBackend(name, sd, "gpu", DEV, ModelSpec(name, batch=4, contexts=1,
+                                                         extra={"batching": {"max_wait_ms": 50}}), True)
+    assert be.batcher is not None
+    xs = [torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(s)) for s in range(4)]
+    solo = [be._run_padded(x) for x in xs]  # batch-4 replay with three zero rows
+    out = [None] * 4
+    bar = threading.Barrier(4)
+
+    def run(i):
+        bar.wait()
+        out[i] = be(xs[i])
+    th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    for a, b in zip(out, solo):
+        assert torch.equal(a, b)  # rows are independent: same kernels, same result per row
+    assert be.batcher.batches < 4  # at least two requests shared a replay
+    be.batcher.close()
