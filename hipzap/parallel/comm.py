@@ -17,6 +17,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from .loopback import default_comm
+
 
 def env_rank() -> tuple[int, int, int]:
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
@@ -87,32 +89,34 @@ def unpack_blob(blob: torch.Tensor, meta_params: dict) -> dict:
     return {k: _rebuild(meta_params[k], fields[k]) for k in meta_params}
 
 
-def broadcast_params(params: dict | None, meta_params, device, src: int = 0, group=None) -> dict:
+def broadcast_params(params: dict | None, meta_params, device, src: int = 0, group=None, comm=None) -> dict:
     """C1: rank ``src`` sends its packed params; every rank returns params on ``device``.
 
     The blob is broadcast as one message, so it streams over every xGMI link at once
     instead of paying per-tensor launch latency 100+ times. ``meta_params`` (the shapes, as
     meta tensors) is only needed on the receiving ranks and may be a zero-argument callable so
     the source rank and single-process runs never build it (it costs a model construction).
+    ``comm``: a ``loopback.Comm`` (default: torch.distributed when initialised).
     """
-    if not is_dist():
+    comm = comm or default_comm(group)
+    if comm.world <= 1:
         return params
-    rank = dist.get_rank()
-    if rank == src:
+    if comm.rank == src:
         blob = pack_blob(params, device)
-        dist.broadcast(blob, src=src, group=group)
+        comm.broadcast(blob, src=src)
         return params
     meta = meta_params() if callable(meta_params) else meta_params
     _, total = flat_layout(meta)
     blob = torch.empty(total, dtype=torch.uint8, device=device)
-    dist.broadcast(blob, src=src, group=group)
+    comm.broadcast(blob, src=src)
     return unpack_blob(blob, meta)
 
 
-def health_check(device=None) -> int:
+def health_check(device=None, comm=None) -> int:
     """C4: 1-int all-reduce; returns the number of live ranks."""
-    if not is_dist():
+    comm = comm or default_comm()
+    if comm.world <= 1:
         return 1
     t = torch.ones(1, dtype=torch.int32, device=device if device is not None else "cpu")
-    dist.all_reduce(t)
+    comm.all_reduce(t)
     return int(t.item())

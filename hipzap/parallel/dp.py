@@ -16,21 +16,22 @@ from __future__ import annotations
 from typing import Callable
 
 import torch
-import torch.distributed as dist
 
-from .comm import is_dist
+from .loopback import Comm, default_comm
 
 
 class DPExecutor:
     def __init__(self, runner: Callable[[torch.Tensor], torch.Tensor], shard_batch: int, in_shape: tuple,
-                 out_shape: tuple, device, in_dtype=torch.float32, out_dtype=torch.float32, group=None):
-        """``runner(x_shard) -> y_shard`` runs one rank's shard (e.g. ``Engine.infer_device``)."""
+                 out_shape: tuple, device, in_dtype=torch.float32, out_dtype=torch.float32, group=None,
+                 comm: Comm | None = None):
+        """``runner(x_shard) -> y_shard`` runs one rank's shard (e.g. ``Engine.infer_device``);
+        ``comm``: torch.distributed (default) or a loopback communicator (tests)."""
         self.runner = runner
         self.shard = shard_batch
         self.device = torch.device(device)
-        self.group = group
-        self.world = dist.get_world_size(group) if is_dist() else 1
-        self.rank = dist.get_rank(group) if is_dist() else 0
+        self.comm = comm or default_comm(group)
+        self.world = self.comm.world
+        self.rank = self.comm.rank
         self.x_shard = torch.zeros((shard_batch,) + tuple(in_shape), dtype=in_dtype, device=self.device)
         self.y_shard = torch.zeros((shard_batch,) + tuple(out_shape), dtype=out_dtype, device=self.device)
         self.global_batch = shard_batch * self.world
@@ -50,14 +51,15 @@ class DPExecutor:
                 self.x_all[n:].zero_()
         if self.world > 1:
             chunks = list(self.x_all.chunk(self.world)) if self.rank == 0 else None
-            dist.scatter(self.x_shard, chunks, src=0, group=self.group)
+            self.comm.scatter(self.x_shard, chunks, src=0)
         else:
             self.x_shard.copy_(self.x_all)
         y = self.runner(self.x_shard)
         self.y_shard.copy_(y.reshape(self.y_shard.shape))
         if self.world > 1:
             outs = list(self.y_all.chunk(self.world)) if self.rank == 0 else None
-            dist.gather(self.y_shard, outs, dst=0, group=self.group)
+            self.comm.gather(self.y_shard, outs, dst=0)
         else:
             self.y_all.copy_(self.y_shard)
-        return self.y_all[:n] if self.rank == 0 else None
+        # a copy: the gather buffer is reused by the next step
+        return self.y_all[:n].clone() if self.rank == 0 else None

@@ -1,0 +1,78 @@
+"""DP logic on the in-process loopback communicator (SURVEY.md §4.2 T-comm-fake): world sizes
+1-8 in one process — weight-blob broadcast (C1), scatter/gather executor (C2/C3) incl. uneven
+batches, health all-reduce (C4), and the failure path (a failing rank aborts its peers)."""
+import pytest
+import torch
+
+from hipzap.parallel.comm import broadcast_params, health_check
+from hipzap.parallel.dp import DPExecutor
+from hipzap.parallel.loopback import CommError, run_ranks
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_collectives(world):
+    def fn(c):
+        t = torch.full((4,), float(c.rank))
+        c.broadcast(t, src=world - 1)
+        s = torch.tensor([c.rank + 1.0])
+        c.all_reduce(s)
+        m = torch.tensor([float(c.rank)])
+        c.all_reduce(m, op="max")
+        out = torch.zeros(2)
+        chunks = [torch.full((2,), 10.0 * r) for r in range(world)] if c.rank == 0 else None
+        c.scatter(out, chunks, src=0) if world > 1 else out.copy_(torch.zeros(2))
+        return t.tolist(), s.item(), m.item(), out.tolist()
+    res = run_ranks(world, fn)
+    for r, (t, s, m, out) in enumerate(res):
+        assert t == [float(world - 1)] * 4
+        assert s == world * (world + 1) / 2 and m == world - 1
+        assert out == [10.0 * r] * 2
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_dp_executor_uneven_batches(world):
+    shard = 3
+
+    def fn(c):
+        def runner(x):  # per-rank "model": row sums + 1000 * rank (which rank computed a row)
+            return x.sum(dim=(1, 2)) + 1000 * c.rank
+        ex = DPExecutor(runner, shard, (2, 4), (), "cpu", comm=c)
+        outs = []
+        for n in (world * shard, world * shard - 1, 1):
+            x = torch.arange(n * 8, dtype=torch.float32).reshape(n, 2, 4) if c.rank == 0 else None
+            outs.append(ex.step(x))
+        return outs
+    res = run_ranks(world, fn)
+    for r in range(1, world):
+        assert res[r] == [None, None, None]
+    for n, y in zip((world * shard, world * shard - 1, 1), res[0]):
+        x = torch.arange(n * 8, dtype=torch.float32).reshape(n, 2, 4)
+        expect = x.sum(dim=(1, 2)) + 1000 * (torch.arange(n) // shard)
+        assert y.shape == (n,) and torch.equal(y, expect)
+    with pytest.raises(ValueError):
+        DPExecutor(lambda x: x, 2, (1,), (1,), "cpu").step(torch.zeros(3, 1))
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_weight_blob_broadcast_resnet18(world):
+    from hipzap.models import registry
+    a = registry.get("resnet18")
+    torch.manual_seed(0)
+    src = a.pack(a.make_model().state_dict(), "cpu")[0]
+    meta, _ = a.meta_params()
+
+    def fn(c):
+        got = broadcast_params(src if c.rank == 0 else None, meta, "cpu", comm=c)
+        return sum(float(p.wf.float().sum() + p.bias.sum()) for p in got.values()), health_check(comm=c)
+    res = run_ranks(world, fn)
+    assert len({d for d, _ in res}) == 1 and all(h == world for _, h in res)
+
+
+def test_failing_rank_aborts_peers_instead_of_hanging():
+    def fn(c):
+        if c.rank == 2:
+            c.fail_at = "gather"
+        ex = DPExecutor(lambda x: x * 2, 1, (1,), (1,), "cpu", comm=c)
+        return ex.step(torch.ones(4, 1) if c.rank == 0 else None)
+    res = run_ranks(4, fn, timeout_s=10)
+    assert all(isinstance(e, CommError) for e in res), res
