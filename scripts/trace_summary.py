@@ -42,13 +42,20 @@ def main():
     t0 = int(seg[0]["Start_Timestamp"])
     lines = ["# one steady-state inference: start_us dur_us grid wg vgpr kernel"]
     busy = 0
+
+    def col(r, *names):
+        for n in names:
+            if r.get(n) not in (None, ""):
+                return r[n]
+        return "?"
     for r in seg:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         busy += e - s
         name = r["Kernel_Name"][:110]
-        lines.append(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} grid={r.get('Grid_Size', '?'):>7} "
-                     f"wg={r.get('Workgroup_Size', '?'):>5} vgpr={r.get('VGPR_Count', r.get('Arch_VGPR_Count', '?')):>4} "
-                     f"{name}")
+        grid = col(r, "Grid_Size", "Grid_Size_X")
+        wg = col(r, "Workgroup_Size", "Workgroup_Size_X")
+        vgpr = col(r, "VGPR_Count", "Arch_VGPR_Count")
+        lines.append(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} grid={grid:>7} wg={wg:>5} vgpr={vgpr:>4} {name}")
     span = (int(seg[-1]["End_Timestamp"]) - t0) / 1e3
     lines.append(f"# {len(seg)} dispatches, span {span:.1f} us, kernel-busy {busy / 1e3:.1f} us "
                  "(profiled; durations inflate under the profiler)")
