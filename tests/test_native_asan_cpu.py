@@ -1,0 +1,29 @@
+"""Host AddressSanitizer + UBSan run of the native runtime (SURVEY.md §5 'race detection /
+sanitizers'): csrc/runtime.cpp is compiled with ``-Xarch_host -fsanitize=address,undefined``
+(host code only — GPU ASan is not used) together with tests/native/runtime_host_asan.cpp, whose
+stub kernel launchers let the Program container run without a GPU. Leak detection is on."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_runtime_host_asan_ubsan(tmp_path):
+    exe = tmp_path / "rt_asan"
+    san = []
+    for f in ("-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
+        san += ["-Xarch_host", f]
+    cmd = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", os.path.join(ROOT, "hipzap", "csrc"),
+           os.path.join(ROOT, "hipzap", "csrc", "runtime.cpp"),
+           os.path.join(ROOT, "tests", "native", "runtime_host_asan.cpp"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert run.returncode == 0 and "runtime host asan: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
