@@ -47,10 +47,53 @@ def run(name, batch, contexts, iters=100):
             "ms_per_batch_concurrent": round(secs / iters / contexts * 1e3, 4)}
 
 
+def torch_reference(name, batch, iters=100):
+    """Stock PyTorch on the same GPU: the HF / eager model in bf16 (channels_last for CNNs),
+    captured in a CUDA(HIP) graph -> hipBLASLt/MIOpen kernels. Same batch, same inputs."""
+    a = registry.get(name)
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    m = a.make_model().eval().to(device=dev, dtype=torch.bfloat16)
+    if name.startswith("bert"):
+        ids = torch.randint(1000, 30000, (batch, 128), device=dev)
+        fwd = lambda: m(input_ids=ids, attention_mask=torch.ones_like(ids)).logits  # noqa: E731
+    elif name.startswith("vit"):
+        x = torch.randn(batch, 3, 224, 224, device=dev, dtype=torch.bfloat16)
+        fwd = lambda: m(pixel_values=x).logits  # noqa: E731
+    else:
+        m = m.to(memory_format=torch.channels_last)
+        x = torch.randn(batch, 3, 224, 224, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+        fwd = lambda: m(x)  # noqa: E731
+    s = torch.cuda.Stream(dev)
+    with torch.no_grad(), torch.cuda.stream(s):
+        for _ in range(3):
+            fwd()
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        fwd()
+    for _ in range(10):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(iters):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    return batch * iters / (time.perf_counter() - t)
+
+
 def main():
-    names = sys.argv[1:] or list(CONFIGS)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    names = args or list(CONFIGS)
     for name in names:
         c = CONFIGS[name]
+        if "--torch" in sys.argv and not name.endswith("fp8"):
+            try:
+                v = torch_reference(name, c["batch"])
+                print(json.dumps({"model": name, "batch": c["batch"], "impl": "pytorch-bf16-hipgraph",
+                                  "items_per_s": round(v, 1), "unit": c["unit"]}), flush=True)
+            except Exception as e:
+                print(json.dumps({"model": name, "impl": "pytorch", "error": repr(e)[:300]}), flush=True)
         for ctx in (1, 4):
             try:
                 r = run(name, c["batch"], ctx)
