@@ -46,13 +46,14 @@ class LstmParams(C.Structure):
 class DecoderParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h_state", c_void_p), ("step", c_void_p),
                 ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
-                ("seed", c_void_p)]
+                ("seed", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int),
+                ("rpb", c_int)]
 
 
 class SamplerParams(C.Structure):
-    _fields_ = [("logits", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
-                ("seed", c_void_p), ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int),
-                ("exclude", c_int * 8), ("keyed", c_int), ("cand_val", c_void_p), ("cand_idx", c_void_p)]
+    _fields_ = [("keys", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
+                ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int), ("exclude", c_int * 8),
+                ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int), ("rpb", c_int)]
 
 
 def _sig(lib, name, res, *args):
@@ -98,6 +99,7 @@ def _load():
     _sig(lib, "hz_lstm_cell_launch", c_int, C.POINTER(LstmParams), P)
     _sig(lib, "hz_decoder_launch", c_int, C.POINTER(DecoderParams), P)
     _sig(lib, "hz_sampler_launch", c_int, C.POINTER(SamplerParams), P)
+    _sig(lib, "hz_decoder_geometry", None, c_int, C.POINTER(c_int), C.POINTER(c_int))
     _sig(lib, "hz_prog_add_lstm", c_int, P, C.POINTER(LstmParams), c_int)
     _sig(lib, "hz_prog_add_decoder", c_int, P, C.POINTER(DecoderParams), c_int)
     _sig(lib, "hz_prog_add_sampler", c_int, P, C.POINTER(SamplerParams), c_int)

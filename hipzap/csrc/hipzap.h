@@ -85,20 +85,24 @@ typedef struct HzDecoderParams {
   int V, H, ldk;
   float* keys;                // optional [V]: logits + Gumbel(seed, step, row) for the sampler
   const unsigned long long* seed;
+  float* bmax_val;            // with keys: [nblk] per-workgroup max key (value, row) -> sampler
+  int* bmax_idx;
+  int nblk, rpb;              // workgroups and rows per workgroup (hz_decoder_geometry)
 } HzDecoderParams;
 typedef struct HzSamplerParams {
-  const float* logits;        // [V]
+  const float* keys;          // [V] Gumbel-perturbed logits (decoder epilogue)
   int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
   int* step;                  // increments
   int* draws;                 // optional [steps][10] record of the draws
-  const unsigned long long* seed;  // device: per-request RNG seed
   const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
   int V, n_exclude;
   int exclude[8];
-  int keyed;                  // 1: `logits` already holds the Gumbel-perturbed keys (decoder epilogue)
-  float* cand_val;            // scratch [ceil(V/1024)][10]: per-block top-10 (two-stage selection)
-  int* cand_idx;
+  const float* bmax_val;      // [nblk] decoder workgroup maxima (value, row)
+  const int* bmax_idx;
+  int nblk, rpb;              // decoder geometry: workgroup b owns rows [b*rpb, (b+1)*rpb)
 } HzSamplerParams;
+// decoder launch geometry for vocabulary V: workgroups and rows per workgroup (contiguous)
+void hz_decoder_geometry(int V, int* nblk, int* rpb);
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);
 int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);

@@ -125,15 +125,23 @@ __device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
 }
 
 // --------------------------------------------------------------------------- decoder GEMV
-// logits = E . h + b over the tied embedding (bf16 [V][ldk]). Each wave takes 8 rows per
-// iteration with all 8 x NCH 16-B loads in flight (NCH = ldk/512 is compile-time), then one
-// 64-lane reduction per row. With `keys`, the epilogue also writes logit + Gumbel(seed,t,row)
-// so the sampler only has to select (the Philox work is spread over the whole chip instead of
-// one workgroup).
+// logits = E . h + b over the tied embedding (bf16 [V][ldk]). Workgroup b owns the contiguous
+// rows [b*rpb, (b+1)*rpb); each wave takes 8 rows per iteration with all 8 x NCH 16-B loads in
+// flight (NCH = ldk/512 is compile-time), then one 64-lane reduction per row. With `keys`, the
+// epilogue also writes logit + Gumbel(seed,t,row) (the Philox work is spread over the whole chip)
+// and the workgroup's largest key (value, row) for the sampler's pruning.
 constexpr int DROWS = 8;
+
+// total order of sampler keys: larger value first, ties to the lower row
+__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   extern __shared__ __attribute__((aligned(16))) float hv[];
+  __shared__ float w_best[4];
+  __shared__ int w_besti[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = *p.step;
   const int par = t & 1;
@@ -142,7 +150,11 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   __syncthreads();
   const unsigned long long seed = p.keys ? *p.seed : 0ull;
   const int ngroups = (p.V + DROWS - 1) / DROWS;
-  for (int g = blockIdx.x * 4 + wave; g < ngroups; g += gridDim.x * 4) {
+  const int gpb = p.rpb / DROWS;
+  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+  for (int g = blockIdx.x * gpb + wave; g < g_end; g += 4) {
     u32x4 wv[DROWS][NCH];
 #pragma unroll
     for (int q = 0; q < DROWS; ++q) {
@@ -177,178 +189,190 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
       if (r < p.V) {
         const float lg = a + (p.bias ? p.bias[r] : 0.f);
         p.logits[r] = lg;
-        if (p.keys) p.keys[r] = lg + gumbel(seed, t, r);
+        if (p.keys) {
+          const float key = lg + gumbel(seed, t, r);
+          p.keys[r] = key;
+          if (better(key, r, best, besti)) {
+            best = key;
+            besti = r;
+          }
+        }
       }
+    }
+  }
+  if (p.keys) {  // workgroup max key: lanes 0-7 hold the candidates, xor 1/2/4 stays inside them
+#pragma unroll
+    for (int o = 1; o < DROWS; o <<= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (better(ov, oi, best, besti)) {
+        best = ov;
+        besti = oi;
+      }
+    }
+    if (lane == 0) {
+      w_best[wave] = best;
+      w_besti[wave] = besti;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < 4; ++w)
+        if (better(w_best[w], w_besti[w], best, besti)) {
+          best = w_best[w];
+          besti = w_besti[w];
+        }
+      p.bmax_val[blockIdx.x] = best;
+      p.bmax_idx[blockIdx.x] = besti;
     }
   }
 }
 
 constexpr int TOPK = 10;
 
-// 64-lane argmax of (value, index) with ties to the lower index; every lane gets the result
-__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+// Bitonic sort of NC independent (value, row) vectors (one pair per lane each) across the
+// wave into descending `better` order (lane 0 = best): 21 compare-exchange steps of one
+// shuffle pair per vector; the NC chains interleave so the shuffle latency is hidden.
+template <int NC>
+__device__ __forceinline__ void wave_sort64(float (&v)[NC], int (&i)[NC]) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(i, o, 64);
-    if (ov > v || (ov == v && oi < i)) {
-      v = ov;
-      i = oi;
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const bool keep_better = ((lane & k) == 0) == ((lane & j) == 0);
+      float ov[NC];
+      int oi[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        ov[c] = __shfl_xor(v[c], j, 64);
+        oi[c] = __shfl_xor(i[c], j, 64);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (keep_better == better(ov[c], oi[c], v[c], i[c])) {
+          v[c] = ov[c];
+          i[c] = oi[c];
+        }
     }
   }
 }
 
-// Two-stage Gumbel top-10 (10 draws without replacement ∝ exp(logit)):
-//   sampler_partial: ceil(V/1024) blocks; each thread loads its 4 keys unconditionally (one
-//     round trip), sorts them, the wave merges its lanes' lists by 10 rounds of shuffle argmax,
-//     wave 0 merges the 4 wave lists -> the block's top-10 into the candidate buffer;
-//   sampler_final: one wave merges all candidates (loaded 8 at a time) and applies the
-//     reference's selection rule (main.py:63-68), writes the token and advances the step.
-// The previous single-workgroup version read the V keys through a data-dependent branch per
-// element (a dependent L2 round trip each): 110 us per token, ~60 % of the whole decode step.
-constexpr int SPB = 1024;  // keys per partial block (256 threads x 4)
+// Sampler: 10 draws without replacement ∝ exp(logit) = the 10 largest Gumbel keys
+// (Plackett-Luce), selected exactly with pruning instead of a scan of all V keys:
+//   1. the decoder left each workgroup's max key; every global top-10 key lies in one of the
+//      10 workgroups with the largest maxima (a key in any other workgroup has >= 10 larger
+//      keys: those 10 maxima), and within them it is among the rpb rows of the workgroup;
+//   2. top-10 of the nblk maxima, then top-10 of the 10*rpb keys of the selected workgroups.
+// Each top-10 is a tournament over 64-item chunks: the 16 waves bitonic-sort their chunks
+// (CPW chunks per pass, all loads issued before the first sort), the 10 best of each chunk go
+// to LDS, repeat until one chunk remains. One launch, one workgroup, no atomics. Then the
+// reference's selection rule (main.py:63-68) via a ballot.
+constexpr int SAMPLER_LDS = 1024;  // candidate slots per LDS buffer
+constexpr int SAMPLER_WAVES = 16;
+constexpr int CPW = 2;             // chunks per wave per pass
 
-__device__ __forceinline__ void cswap(float& va, int& ia, float& vb, int& ib) {  // descending
-  if (vb > va || (vb == va && ib < ia)) {
-    const float tv = va;
-    const int ti = ia;
-    va = vb;
-    ia = ib;
-    vb = tv;
-    ib = ti;
-  }
-}
-
-// 10 rounds of wave argmax over per-lane sorted lists of length L (head = next unpopped entry).
-template <int L>
-__device__ __forceinline__ void wave_topk(const float (&v)[L], const int (&id)[L], float (&ov)[TOPK],
-                                          int (&oi)[TOPK]) {
-  int head = 0;
+template <class Load>
+__device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi, float* cv, int* ci, float& ov,
+                                            int& oi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bool first = true;
+  float* in_v = cv;
+  int* in_i = ci;
+  float* out_v = bv;
+  int* out_i = bi;
+  while (true) {
+    const int nch = (n + 63) / 64;
+    if (nch == 1) break;
+    for (int c0 = wave; c0 < nch; c0 += SAMPLER_WAVES * CPW) {
+      float v[CPW];
+      int i[CPW];
 #pragma unroll
-  for (int r = 0; r < TOPK; ++r) {
-    float hv = -INFINITY;
-    int hi = 0x7fffffff;
-#pragma unroll
-    for (int q = 0; q < L; ++q)
-      if (q == head) {
-        hv = v[q];
-        hi = id[q];
-      }
-    float bv = hv;
-    int bi = hi;
-    wave_argmax(bv, bi);
-    if (hv == bv && hi == bi && head < L) ++head;  // indices are unique: one lane pops
-    ov[r] = bv;
-    oi[r] = bi;
-  }
-}
-
-__global__ __launch_bounds__(256) void sampler_partial_kernel(const HzSamplerParams p) {
-  __shared__ float w_val[4 * TOPK];
-  __shared__ int w_idx[4 * TOPK];
-  const int t = *p.step;
-  if ((t + 1) < *p.n_forced) return;  // prompt step: the next token is given
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long seed = *p.seed;
-  float v[4];
-  int id[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = blockIdx.x * SPB + r * 256 + tid;
-    id[r] = j;
-    v[r] = p.logits[min(j, p.V - 1)];
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (!p.keyed) v[r] += gumbel(seed, t, id[r]);
-    if (id[r] >= p.V) v[r] = -INFINITY;
-  }
-  cswap(v[0], id[0], v[1], id[1]);
-  cswap(v[2], id[2], v[3], id[3]);
-  cswap(v[0], id[0], v[2], id[2]);
-  cswap(v[1], id[1], v[3], id[3]);
-  cswap(v[1], id[1], v[2], id[2]);
-  float wv[TOPK];
-  int wi[TOPK];
-  wave_topk<4>(v, id, wv, wi);
-  if (lane == 0) {
-#pragma unroll
-    for (int r = 0; r < TOPK; ++r) {
-      w_val[wave * TOPK + r] = wv[r];
-      w_idx[wave * TOPK + r] = wi[r];
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float cv[1] = {lane < 4 * TOPK ? w_val[lane] : -INFINITY};
-    int ci[1] = {lane < 4 * TOPK ? w_idx[lane] : 0x7fffffff};
-    float bv[TOPK];
-    int bi[TOPK];
-    wave_topk<1>(cv, ci, bv, bi);
-    if (lane < TOPK) {
-      float o = bv[0];
-      int oi = bi[0];
-#pragma unroll
-      for (int r = 1; r < TOPK; ++r) {
-        o = lane == r ? bv[r] : o;
-        oi = lane == r ? bi[r] : oi;
-      }
-      p.cand_val[blockIdx.x * TOPK + lane] = o;
-      p.cand_idx[blockIdx.x * TOPK + lane] = oi;
-    }
-  }
-}
-
-__global__ __launch_bounds__(64) void sampler_final_kernel(const HzSamplerParams p) {
-  const int lane = threadIdx.x;
-  const int t = *p.step;
-  if ((t + 1) >= *p.n_forced) {
-    const int ncand = ((p.V + SPB - 1) / SPB) * TOPK;
-    float v[TOPK];
-    int id[TOPK];
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      v[q] = -INFINITY;
-      id[q] = 0x7fffffff;
-    }
-    for (int c0 = 0; c0 < ncand; c0 += 64 * 8) {
-      float cv[8];
-      int ci[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {  // 8 candidates in flight per lane
-        const int c = min(c0 + u * 64 + lane, ncand - 1);
-        cv[u] = p.cand_val[c];
-        ci[u] = p.cand_idx[c];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        float x = c0 + u * 64 + lane < ncand ? cv[u] : -INFINITY;
-        int xi = ci[u];
-#pragma unroll
-        for (int q = 0; q < TOPK; ++q) cswap(v[q], id[q], x, xi);  // insertion into the sorted list
-      }
-    }
-    float dv[TOPK];
-    int draws[TOPK];
-    wave_topk<TOPK>(v, id, dv, draws);
-    if (lane == 0) {
-      int tok = draws[0];
-      for (int r = 0; r < TOPK && r < p.V; ++r) {
-        const int d = draws[r];
-        bool ex = d <= 0;
-        for (int e = 0; e < p.n_exclude; ++e) ex |= (d == p.exclude[e]);
-        if (!ex) {
-          tok = d;
-          break;
+      for (int u = 0; u < CPW; ++u) {  // all of this pass's loads first
+        const int j = (c0 + u * SAMPLER_WAVES) * 64 + lane;
+        v[u] = -INFINITY;
+        i[u] = 0x7fffffff;
+        if (j < n) {
+          if (first) {
+            load(j, v[u], i[u]);
+          } else {
+            v[u] = in_v[j];
+            i[u] = in_i[j];
+          }
         }
       }
-      p.tok_seq[t + 1] = tok;
-      if (p.draws) {
-        for (int r = 0; r < TOPK; ++r) p.draws[(long)t * TOPK + r] = draws[r];
+      wave_sort64<CPW>(v, i);
+#pragma unroll
+      for (int u = 0; u < CPW; ++u) {
+        const int c = c0 + u * SAMPLER_WAVES;
+        if (lane < TOPK && c < nch) {
+          out_v[c * TOPK + lane] = v[u];
+          out_i[c * TOPK + lane] = i[u];
+        }
       }
     }
+    __syncthreads();
+    n = nch * TOPK;
+    first = false;
+    float* tv = in_v;
+    int* ti = in_i;
+    in_v = out_v;
+    in_i = out_i;
+    out_v = tv;
+    out_i = ti;
   }
-  if (lane == 0) *p.step = t + 1;
+  // one chunk left: every wave sorts it (wave 0's result is used; no extra barrier needed)
+  float v[1] = {-INFINITY};
+  int i[1] = {0x7fffffff};
+  if (lane < n) {
+    if (first) {
+      load(lane, v[0], i[0]);
+    } else {
+      v[0] = in_v[lane];
+      i[0] = in_i[lane];
+    }
+  }
+  wave_sort64<1>(v, i);
+  ov = v[0];
+  oi = i[0];
+  __syncthreads();  // the LDS buffers are reused by the caller's next top-10
+}
+
+__global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) {
+  __shared__ float buf_v[2][SAMPLER_LDS];
+  __shared__ int buf_i[2][SAMPLER_LDS];
+  __shared__ int sel[TOPK];
+  const int lane = threadIdx.x & 63;
+  const int t = *p.step;
+  if ((t + 1) >= *p.n_forced) {
+    float v;
+    int i;
+    // 1. the 10 decoder workgroups with the largest maxima
+    block_top10(p.nblk, [&](int j, float& a, int& b) { a = p.bmax_val[j]; b = p.bmax_idx[j]; },
+                buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
+    const int nsel = min(TOPK, p.nblk);
+    if (threadIdx.x < nsel) sel[threadIdx.x] = min(i / p.rpb, p.nblk - 1);  // (NaN keys: stay in range)
+    __syncthreads();
+    // 2. the 10 largest keys among their rows
+    const int rpb = p.rpb;
+    block_top10(nsel * rpb, [&](int j, float& a, int& b) {
+                  const int q = j / rpb;
+                  const int r = sel[q] * rpb + (j - q * rpb);
+                  a = r < p.V ? p.keys[r] : -INFINITY;
+                  b = r;
+                }, buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
+    if (threadIdx.x < 64) {  // wave 0: lanes 0..9 hold the draws in order
+      const int nd = min(TOPK, p.V);
+      bool ok = lane < nd && i > 0;
+      for (int e = 0; e < p.n_exclude; ++e) ok = ok && i != p.exclude[e];
+      const unsigned long long m = __ballot(ok);
+      const int src = m ? __ffsll((long long)m) - 1 : 0;  // first acceptable draw, else the first
+      const int tok = __shfl(i, src, 64);
+      if (lane == 0) p.tok_seq[t + 1] = tok;
+      if (p.draws && lane < TOPK) p.draws[(long)t * TOPK + lane] = i;
+    }
+  }
+  __syncthreads();  // every thread has read *p.step
+  if (threadIdx.x == 0) *p.step = t + 1;
 }
 
 }  // namespace
@@ -370,11 +394,22 @@ extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+extern "C" void hz_decoder_geometry(int V, int* nblk, int* rpb) {
+  const int groups = (V + DROWS - 1) / DROWS;
+  int nb = min(2048, (groups + 3) / 4);
+  int gpb = (groups + nb - 1) / nb;
+  gpb = (gpb + 3) / 4 * 4;  // whole wave rounds per workgroup
+  *nblk = (groups + gpb - 1) / gpb;
+  *rpb = gpb * DROWS;
+}
+
 extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const HzDecoderParams& p = *pp;
-  if (p.ldk % 512 || p.ldk < p.H || (p.keys && !p.seed)) return -1;
-  const int groups = (p.V + DROWS - 1) / DROWS;
-  const dim3 grid(min(2048, (groups + 3) / 4)), block(256);
+  if (p.ldk % 512 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
+  int nblk, rpb;
+  hz_decoder_geometry(p.V, &nblk, &rpb);
+  if (p.nblk != nblk || p.rpb != rpb) return -1;
+  const dim3 grid(nblk), block(256);
   const size_t lds = p.ldk * sizeof(float);
   switch (p.ldk / 512) {
     case 1: hipLaunchKernelGGL(decoder_kernel<1>, grid, block, lds, st, p); break;
@@ -388,8 +423,12 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
 
 extern "C" int hz_sampler_launch(const HzSamplerParams* pp, hipStream_t st) {
   const HzSamplerParams& p = *pp;
-  if (p.n_exclude > 8 || !p.cand_val || !p.cand_idx || p.V < 1) return -1;
-  hipLaunchKernelGGL(sampler_partial_kernel, dim3((p.V + SPB - 1) / SPB), dim3(256), 0, st, p);
-  hipLaunchKernelGGL(sampler_final_kernel, dim3(1), dim3(64), 0, st, p);
+  int nblk, rpb;
+  hz_decoder_geometry(p.V, &nblk, &rpb);
+  if (p.n_exclude > 8 || p.V < 1 || !p.keys || !p.bmax_val || !p.bmax_idx || p.nblk != nblk || p.rpb != rpb)
+    return -1;
+  // LDS tournament capacity: first-round chunks of either top-10 must fit one buffer
+  if ((nblk + 63) / 64 * TOPK > SAMPLER_LDS || (TOPK * rpb + 63) / 64 * TOPK > SAMPLER_LDS) return -1;
+  hipLaunchKernelGGL(sampler_kernel, dim3(1), dim3(64 * SAMPLER_WAVES), 0, st, p);
   return (int)hipGetLastError();
 }

@@ -101,22 +101,24 @@ class LMEngine:
                 if i == 0 and prm.In > packed["lde"]:
                     raise ValueError("embedding width mismatch")
                 N.check(lib.hz_prog_add_lstm(self.prog, C.byref(prm), 0), "add_lstm")
+            nblk, rpb = C.c_int(), C.c_int()
+            lib.hz_decoder_geometry(packed["V"], C.byref(nblk), C.byref(rpb))
+            nblk, rpb = nblk.value, rpb.value
+            self.bmax_val = torch.empty(nblk, device=dev)  # decoder workgroup maxima -> sampler
+            self.bmax_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
             d = N.DecoderParams()
             d.w = packed["dec"].data_ptr()
             d.bias = N.ptr(packed["dec_bias"])
             d.h_state, d.step, d.logits = self.h[-1].data_ptr(), self.step.data_ptr(), self.logits.data_ptr()
             d.V, d.H, d.ldk = packed["V"], L[-1]["H"], packed["lde"]
             d.keys, d.seed = self.keys.data_ptr(), self.seed.data_ptr()
+            d.bmax_val, d.bmax_idx, d.nblk, d.rpb = self.bmax_val.data_ptr(), self.bmax_idx.data_ptr(), nblk, rpb
             N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
             s = N.SamplerParams()
-            s.logits, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
-            s.keyed = 1
-            nblk = (packed["V"] + 1023) // 1024  # two-stage sampler: per-block top-10 candidates
-            self.cand_val = torch.empty(nblk * NUM_DRAWS, device=dev)
-            self.cand_idx = torch.empty(nblk * NUM_DRAWS, dtype=torch.int32, device=dev)
-            s.cand_val, s.cand_idx = self.cand_val.data_ptr(), self.cand_idx.data_ptr()
+            s.keys, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
+            s.bmax_val, s.bmax_idx, s.nblk, s.rpb = d.bmax_val, d.bmax_idx, nblk, rpb
             s.draws = N.ptr(self.draws)
-            s.seed, s.n_forced = self.seed.data_ptr(), self.n_forced.data_ptr()
+            s.n_forced = self.n_forced.data_ptr()
             s.V = packed["V"]
             ex = [int(e) for e in exclude_ids][:8]
             s.n_exclude = len(ex)

@@ -68,6 +68,21 @@ def test_sampler_distribution_first_draw(model):
     assert chi2 < 25.0, (obs, exp)  # 6 dof
 
 
+@pytest.mark.parametrize("V", [3000, 60000, 7])
+def test_sampler_draws_are_exact_top10_of_keys(V):
+    """The pruned tournament (decoder workgroup maxima -> 10 workgroups -> their rows) returns
+    exactly the 10 largest Gumbel keys in order, for vocabularies with 1 .. 1875 workgroups."""
+    torch.manual_seed(V)
+    m = get_language_model(vocab_sz=V, emb_sz=64, n_hid=96, n_layers=2, pad_token=1, tie_weights=True).eval()
+    eng = LMEngine.from_state_dict(m.state_dict(), DEV, record_draws=True)
+    for seed in range(5):
+        eng.run_tokens([3 % V, 5 % V], 1, seed=seed)
+        keys = eng.keys.cpu()
+        k = min(10, V)
+        order = sorted(range(V), key=lambda r: (-keys[r].item(), r))[:k]
+        assert eng.draws[1].tolist()[:k] == order
+
+
 def test_draws_distinct_and_selection_rule(model):
     excl = [int(torch.topk(_eager_logits(model, [11, 12]), 1).indices)]  # exclude the likeliest token
     eng = LMEngine(LMEngine.from_state_dict(model.state_dict(), DEV).p, DEV, exclude_ids=excl, record_draws=True)
