@@ -7,6 +7,8 @@ Metric (BASELINE.json): inferences/sec (whole node) + p50 cold-start ms, ResNet-
               the real ResNet-50 architecture, written untimed beforehand) -> packs/folds BN
               on its GPU -> RCCL-broadcasts the packed blob to the other ranks -> every rank
               plans its arena, binds native programs, captures hipGraphs -> first inference.
+              Also reported: the same from the pre-packed copy (<ckpt>.hzpack, safetensors
+              streamed to the GPU: no fold/pack), `cold_start_packed_ms_p50`.
   warm step   every rank serves ``--streams`` independent bs=1 requests concurrently: each is
               one hipGraph replay that includes the pinned H2D of the fp32 image, preprocess,
               53 fused conv kernels, pools, FC and the D2H of the logits.
@@ -180,10 +182,18 @@ def main():
             dist.destroy_process_group()
         return
 
-    def cold_start():
+    def cold_start(packed: str | None = None):
+        """``packed``: start from the pre-packed copy of the checkpoint (``<ckpt>.hzpack``, the
+        deploy-time artifact of ``hipzap pack``) instead of torch.load + fold/pack."""
         t0 = time.perf_counter()
         timings = {}
-        if rank == 0:
+        if rank == 0 and packed:
+            from hipzap.engine.packfile import load_packed
+            ta = time.perf_counter()
+            params, arch_kw = load_packed(packed, device)
+            torch.cuda.synchronize(device)
+            timings["load_packed_ms"] = (time.perf_counter() - ta) * 1e3
+        elif rank == 0:
             ta = time.perf_counter()
             sd = torch.load(ckpt, map_location="cpu", weights_only=True, mmap=True)
             timings["load_ms"] = (time.perf_counter() - ta) * 1e3
@@ -226,6 +236,23 @@ def main():
         eng, out, c = cold_start()
         colds.append(c)
     assert torch.isfinite(out).all(), "non-finite logits"
+    breakdown_pth = dict(eng.timings)
+    # packed fast path: rank 0 writes <ckpt>.hzpack once (untimed, as `hipzap pack` would at deploy
+    # time), then every rank cold-starts from it
+    colds_packed, breakdown_packed = [], {}
+    if args.cold_runs:
+        from hipzap.engine.packfile import packed_path, save_packed, source_stamp
+        pk = packed_path(ckpt)
+        if rank == 0:
+            params0, kw0 = adapter.pack(torch.load(ckpt, map_location="cpu", weights_only=True), "cpu")
+            save_packed(params0, kw0, pk, model=args.model, stamp=source_stamp(ckpt))
+        for _ in range(args.cold_runs):
+            del eng
+            torch.cuda.synchronize(device)
+            eng, out, c = cold_start(packed=pk)
+            colds_packed.append(c)
+        breakdown_packed = dict(eng.timings)
+        assert torch.isfinite(out).all(), "non-finite logits (packed path)"
 
     # single-request latency (one context, full round trip incl. host copies), p50
     x = request_input(args, adapter)
@@ -274,7 +301,9 @@ def main():
             "cold_start_ms_p50": round(statistics.median(colds), 2),
             "cold_start_ms_first": round(cold_first, 2),
             "cold_start_process_ms": round(cold_process_ms, 2),
-            "cold_start_breakdown_ms": {k: round(v, 2) for k, v in eng.timings.items()},
+            "cold_start_breakdown_ms": {k: round(v, 2) for k, v in breakdown_pth.items()},
+            "cold_start_packed_ms_p50": round(statistics.median(colds_packed), 2) if colds_packed else None,
+            "cold_start_packed_breakdown_ms": {k: round(v, 2) for k, v in breakdown_packed.items()},
             "latency_ms_p50_single": round(lat_p50, 4),
             "baseline_note": "vs_baseline against BASELINE.md sandbox-CPU ResNet-50 bs=1 (27.2 inf/s); "
                              "no published numbers exist",

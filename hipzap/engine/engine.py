@@ -92,16 +92,48 @@ class Engine:
             torch.cuda.synchronize(dev)
         timings = dict(kw.pop("timings", {}) or {})
         timings["pack_ms"] = (time.perf_counter() - t0) * 1e3
+        eng = cls(model, params, device, arch_kw=dict(arch_kw, **(kw.pop("arch_kw", None) or {})), timings=timings,
+                  **kw)
+        eng.pack_cfg = dict(arch_kw)
+        return eng
+
+    @classmethod
+    def from_packed(cls, model: str, path: str, device="cuda:0", **kw) -> "Engine":
+        """Cold-start fast path: a ``hipzap pack`` / ``write_packed`` file (BN folded, weights in
+        the kernels' layouts) streamed straight into device memory — no fold/pack work."""
+        from .packfile import load_packed
+        t0 = time.perf_counter()
+        params, cfg = load_packed(path, device)
+        torch.cuda.synchronize(torch.device(device))
+        timings = dict(kw.pop("timings", {}) or {})
+        timings["load_packed_ms"] = (time.perf_counter() - t0) * 1e3
+        arch_kw = dict(cfg, **(kw.pop("arch_kw", None) or {}))
         return cls(model, params, device, arch_kw=arch_kw, timings=timings, **kw)
 
     @classmethod
-    def from_checkpoint(cls, model: str, path: str, device="cuda:0", **kw) -> "Engine":
+    def from_checkpoint(cls, model: str, path: str, device="cuda:0", use_packed: bool = True,
+                        write_packed: bool = False, **kw) -> "Engine":
+        """``torch.load`` of a standard state_dict (the reference's format, main.py:99), or, when
+        ``use_packed`` and an up-to-date ``<path>.hzpack`` exists next to it, the packed fast
+        path. ``write_packed``: after packing from the .pth, save the packed copy for next time."""
+        from .packfile import find_packed, packed_path, save_packed, source_stamp
+        if use_packed:
+            pk = find_packed(path, model)
+            if pk is not None:
+                return cls.from_packed(model, pk, device, **kw)
         t0 = time.perf_counter()
         sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True)
         if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
             sd = sd["state_dict"]
         timings = {"load_ms": (time.perf_counter() - t0) * 1e3}
-        return cls.from_state_dict(model, sd, device, timings=timings, **kw)
+        eng = cls.from_state_dict(model, sd, device, timings=timings, **kw)
+        if write_packed:
+            try:
+                save_packed(eng.params, eng.pack_cfg, packed_path(path), model=model, stamp=source_stamp(path))
+            except OSError as e:  # read-only artifact dir: the cache is an optimisation only
+                import logging
+                logging.getLogger("hipzap.engine").warning("could not write packed weights: %s", e)
+        return eng
 
     # -------------------------------------------------------------- warm path
     def _pick(self) -> int:

@@ -24,9 +24,47 @@ def _classes():
     return {c.__name__: c for c in (PackedConv, PackedFp8, NormParams, EmbedTables)}
 
 
-def save_packed(params: dict, cfg: dict, path: str, source_sha256: str | None = None) -> None:
+PACK_SUFFIX = ".hzpack"
+
+
+def packed_path(ckpt_path: str) -> str:
+    """Where the pre-packed copy of a checkpoint lives: next to it (``m.pth`` -> ``m.pth.hzpack``)."""
+    return ckpt_path + PACK_SUFFIX
+
+
+def source_stamp(ckpt_path: str) -> dict:
+    """Cheap identity of the source checkpoint (size + mtime): a cold start must not hash a
+    100-MB file to validate its cache (sha256 of ResNet-50's .pth alone costs ~150 ms)."""
+    st = os.stat(ckpt_path)
+    return {"size": st.st_size, "mtime_ns": st.st_mtime_ns}
+
+
+def find_packed(ckpt_path: str, model: str) -> str | None:
+    """The packed file for ``ckpt_path`` if it exists, was packed for ``model`` and the source
+    checkpoint is unchanged since; else None (the caller packs from the .pth)."""
+    path = packed_path(ckpt_path)
+    if not os.path.exists(path):
+        return None
+    try:
+        meta = read_meta(path)
+    except Exception:  # corrupt/partial file: ignore it, the .pth is the source of truth
+        return None
+    if meta.get("model") != model or meta.get("source_stamp") != source_stamp(ckpt_path):
+        return None
+    return path
+
+
+def read_meta(path: str) -> dict:
+    from safetensors import safe_open
+    with safe_open(path, framework="pt", device="cpu") as f:
+        return json.loads(f.metadata()["hipzap"])
+
+
+def save_packed(params: dict, cfg: dict, path: str, source_sha256: str | None = None, model: str | None = None,
+                stamp: dict | None = None) -> None:
     from safetensors.torch import save_file
-    tensors, meta = {}, {"cfg": cfg, "source_sha256": source_sha256, "entries": {}}
+    tensors, meta = {}, {"cfg": cfg, "source_sha256": source_sha256, "model": model, "source_stamp": stamp,
+                         "entries": {}}
     for key, obj in params.items():
         if torch.is_tensor(obj):
             tensors[key] = obj.detach().contiguous().cpu()
@@ -40,12 +78,14 @@ def save_packed(params: dict, cfg: dict, path: str, source_sha256: str | None = 
             else:
                 fields[f.name] = v
         meta["entries"][key] = {"type": type(obj).__name__, "fields": fields}
-    tmp = path + ".tmp"
+    tmp = f"{path}.tmp{os.getpid()}"
     save_file(tensors, tmp, metadata={"hipzap": json.dumps(meta)})
     os.replace(tmp, path)
 
 
 def load_packed(path: str, device="cpu") -> tuple[dict, dict]:
+    """-> (packed params with every tensor on ``device``, arch cfg). safetensors reads straight
+    into device memory; nothing in the file is executed."""
     from safetensors import safe_open
     classes = _classes()
     out = {}

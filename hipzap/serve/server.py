@@ -37,20 +37,39 @@ def _random_state_dict(name: str, seed: int = 0) -> dict:
     return m.eval().state_dict()
 
 
+def _gpu_engine(name: str, src, device: str, **kw):
+    """``src``: a state_dict, or the local path of a .pth checkpoint (then an up-to-date packed
+    copy next to it is used, and written after the first pack: the cold-start fast path)."""
+    from ..engine.engine import Engine
+    if isinstance(src, str):
+        return Engine.from_checkpoint(name, src, device, use_packed=True,
+                                      write_packed=os.environ.get("HIPZAP_WRITE_PACKED", "1") != "0", **kw)
+    return Engine.from_state_dict(name, src, device, **kw)
+
+
+def _state_dict(src) -> dict:
+    if not isinstance(src, str):
+        return src
+    sd = torch.load(src, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and isinstance(sd.get("state_dict"), dict):
+        sd = sd["state_dict"]
+    return sd
+
+
 class VisionBackend:
-    def __init__(self, name: str, sd: dict, backend: str, device: str, spec: ModelSpec, capture: bool):
+    def __init__(self, name: str, sd, backend: str, device: str, spec: ModelSpec, capture: bool):
         self.name, self.backend = name, backend
         t0 = time.perf_counter()
         self.adapter = registry.get(name)
         # "probs": true in the model's settings block -> the softmax runs on device, responses are probabilities
         self.probs = bool(spec.extra.get("probs", False))
         if backend == "gpu":
-            from ..engine.engine import Engine
-            self.engine = Engine.from_state_dict(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
-                                                 capture=capture, probs=self.probs)
+            self.engine = _gpu_engine(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
+                                      capture=capture, probs=self.probs)
             self.model = None
         else:
             from ..models.resnet import infer_arch
+            sd = _state_dict(sd)
             _, ncls = infer_arch(sd)
             self.model = self.adapter.make_model(ncls)
             self.model.load_state_dict(sd)
@@ -85,18 +104,17 @@ class VisionBackend:
 class TextBackend:
     """BERT-style sequence classifier; requests are padded to the captured (batch, seq_len)."""
 
-    def __init__(self, name: str, sd: dict, backend: str, device: str, spec: ModelSpec, capture: bool):
+    def __init__(self, name: str, sd, backend: str, device: str, spec: ModelSpec, capture: bool):
         self.name, self.backend = name, backend
         t0 = time.perf_counter()
         self.adapter = registry.get(name)
         self.seq_len = int(spec.extra.get("seq_len", 128))
         if backend == "gpu":
-            from ..engine.engine import Engine
-            self.engine = Engine.from_state_dict(name, sd, device, batch=spec.batch, num_contexts=spec.contexts,
-                                                 capture=capture)
+            self.engine = _gpu_engine(name, sd, device, batch=spec.batch, num_contexts=spec.contexts, capture=capture)
             self.model = None
         else:
             from ..models.bert import config_from_sd, make_model
+            sd = _state_dict(sd)
             cfg = config_from_sd(sd)
             self.model = make_model(cfg["num_labels"], num_hidden_layers=cfg["layers"], hidden_size=cfg["hidden"],
                                     num_attention_heads=cfg["heads"], intermediate_size=cfg["ffn"],
@@ -204,15 +222,13 @@ class ModelServer:
     def spec(self, name: str) -> ModelSpec:
         return self.settings.models.get(name) or ModelSpec(name=name)
 
-    def _load_sd(self, spec: ModelSpec) -> dict:
+    def _load_sd(self, spec: ModelSpec):
+        """A state_dict (random-init demo weights) or the local path of the fetched checkpoint
+        (backends torch.load it, or use its packed copy on the GPU)."""
         if spec.key in (None, "random") or os.environ.get("HIPZAP_RANDOM_WEIGHTS"):
             log.warning("model %s: no checkpoint key configured, using random-init weights", spec.name)
             return _random_state_dict(spec.name)
-        path = self.store.fetch(spec.key)
-        sd = torch.load(path, map_location="cpu", weights_only=True)
-        if isinstance(sd, dict) and isinstance(sd.get("state_dict"), dict):
-            sd = sd["state_dict"]
-        return sd
+        return self.store.fetch(spec.key)
 
     def watchdog(self):
         """Per-GPU liveness watchdog (started on first GPU model load; HIPZAP_WATCHDOG=0 disables)."""

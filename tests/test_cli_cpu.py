@@ -60,6 +60,39 @@ def test_packfile_roundtrip(tmp_path):
     assert torch.equal(back["fc"].wf, params["fc"].wf) and back["fc"].cout == 1000
 
 
+def test_packed_cache_validity(tmp_path):
+    """<ckpt>.hzpack is used only if it was packed for this model from this exact file."""
+    import os
+    from hipzap.engine.packfile import find_packed, packed_path, source_stamp
+    a = registry.get("resnet18")
+    ck = str(tmp_path / "r.pth")
+    torch.save(a.make_model().state_dict(), ck)
+    assert find_packed(ck, "resnet18") is None
+    params, cfg = a.pack(torch.load(ck, weights_only=True), "cpu")
+    save_packed(params, cfg, packed_path(ck), model="resnet18", stamp=source_stamp(ck))
+    assert find_packed(ck, "resnet18") == packed_path(ck)
+    assert find_packed(ck, "resnet50") is None  # packed for another model
+    st = os.stat(ck)
+    os.utime(ck, ns=(st.st_atime_ns, st.st_mtime_ns + 10**9))  # checkpoint replaced
+    assert find_packed(ck, "resnet18") is None
+    open(packed_path(ck), "wb").write(b"garbage")  # partial/corrupt cache: ignored, not fatal
+    assert find_packed(ck, "resnet18") is None
+
+
+def test_cpu_backend_loads_checkpoint_path(tmp_path):
+    from hipzap.serve.server import VisionBackend
+    from hipzap.serve.settings import ModelSpec
+    a = registry.get("resnet18")
+    torch.manual_seed(0)
+    m = a.make_model().eval()
+    ck = str(tmp_path / "r.pth")
+    torch.save(m.state_dict(), ck)
+    be = VisionBackend("resnet18", ck, "cpu", "cpu", ModelSpec("resnet18"), False)
+    x = torch.randn(1, 3, 32, 32)
+    with torch.no_grad():
+        assert torch.allclose(be(x), m(x))
+
+
 def test_cli_pack_and_info(tmp_path, capsys):
     a = registry.get("resnet18")
     ck = tmp_path / "r.pth"

@@ -137,3 +137,20 @@ def test_dynamic_batching_backend(model_sd):
         assert torch.equal(a, b)  # rows are independent: same kernels, same result per row
     assert be.batcher.batches < 4  # at least two requests shared a replay
     be.batcher.close()
+
+
+def test_checkpoint_packed_fast_path(model_sd, tmp_path):
+    """Engine.from_checkpoint: first cold start packs from the .pth and writes <ckpt>.hzpack; the
+    next one streams the packed file straight to the GPU and gives identical logits."""
+    from hipzap.engine.packfile import packed_path
+    name, m, sd = model_sd
+    ck = str(tmp_path / f"{name}.pth")
+    torch.save(sd, ck)
+    first = Engine.from_checkpoint(name, ck, DEV, batch=1, write_packed=True)
+    assert "pack_ms" in first.timings
+    import os
+    assert os.path.exists(packed_path(ck))
+    fast = Engine.from_checkpoint(name, ck, DEV, batch=1)
+    assert "load_packed_ms" in fast.timings and "pack_ms" not in fast.timings
+    x = torch.randn(1, 3, 224, 224)
+    assert torch.equal(first.infer(x), fast.infer(x))
