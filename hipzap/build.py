@@ -25,8 +25,9 @@ OBJDIR = PKG.parent / "build" / "obj"
 ARCH = os.environ.get("HIPZAP_ARCH", "gfx950")
 
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+# HIPZAP_CFLAGS: extra compile flags for experiments (e.g. -DHZ_RING_SHRINK=1); part of the object hash
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
-          "-munsafe-fp-atomics", "-I", str(CSRC)]
+          "-munsafe-fp-atomics", "-I", str(CSRC), *os.environ.get("HIPZAP_CFLAGS", "").split()]
 
 
 def sources() -> list[Path]:

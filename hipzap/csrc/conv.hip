@@ -27,9 +27,13 @@
 
 namespace {
 
+#ifndef HZ_RING_SHRINK
+#define HZ_RING_SHRINK 0
+#endif
 template <int FC, int FP>
 struct Depth {
-  static constexpr int value = (FC + FP <= 2) ? 6 : (FC + FP <= 3) ? 4 : (FC + FP <= 4) ? 3 : 2;
+  static constexpr int base = (FC + FP <= 2) ? 6 : (FC + FP <= 3) ? 4 : (FC + FP <= 4) ? 3 : 2;
+  static constexpr int value = base - HZ_RING_SHRINK >= 1 ? base - HZ_RING_SHRINK : 1;
 };
 
 // keep the register ring out of scratch: 1024 threads cap a wave at 128 VGPRs

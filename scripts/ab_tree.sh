@@ -1,13 +1,14 @@
 #!/bin/bash
 # Interleaved A/B of bench.py between the repo (B) and a worktree under ab/A (A), on ONE box,
-# without retuning (same tuning tables): isolates a kernel change.
+# without retuning (same tuning tables): isolates a kernel change. TREES="ab/A ab/C ." compares
+# more variants (each a pre-built tree).
 #   REPS=2 STREAMS="1 8" bash scripts/ab_tree.sh
 set -u
 OUT=${OUT:-gpurun_out/ab_tree}
 mkdir -p $OUT
 for rep in $(seq 1 ${REPS:-2}); do
-  for X in A B; do
-    D=$([ $X = A ] && echo ab/A || echo .)
+  for D in ${TREES:-ab/A .}; do
+    X=$(basename $(cd $D && pwd))
     for s in ${STREAMS:-1 8}; do
       log=$OUT/${X}_s${s}_$rep.log
       (cd $D && timeout -k 10 300 python bench.py --streams $s --steps ${STEPS:-300} --warmup 30 --cold-runs 0) > $log 2>&1
