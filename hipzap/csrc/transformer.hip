@@ -147,18 +147,42 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const HzEmbedParams p) {
 }
 
 // --------------------------------------------------------------------------- attention
+// softmax(Q K^T * scale + mask) V per (batch, head, block of 16*NW queries); one wave owns 16
+// queries and all keys (L <= 256). Keys live on the MFMA lane (cdna_hip_programming.md §3 'An
+// accumulator tile as the next MFMA's operand'):
+//   S^T = K Q^T   (A = K rows from LDS, B = Q^T from global): lane (q = l&15, g = l>>4) holds
+//                 the scores of query q for keys kt*16 + 4g + i, i < 4;
+//   softmax       row max / sum over the lane's values + 2 shuffles (xor 16, 32);
+//   O^T = V^T P^T the P accumulators ARE the B operand (converted to bf16 in registers, k order
+//                 permuted: element j of group g = key 32c + 4g + j (j < 4), 32c + 16 + 4g + j-4);
+//                 A = V^T in the same k order, read from the row-major V image with two
+//                 ds_read_b64_tr_b16 per fragment (T10) — no transposed staging, no P image.
+//   O^T accumulators give each lane 4 consecutive head dims of one query: 8-byte stores.
+// K and V are staged once per workgroup with 16-B loads/stores; padding keys (L <= key < Lp)
+// re-read row L-1 (finite) and are masked to -inf, so their probabilities are exactly 0.
+#ifndef HZ_ATT_NW8_MINL
+#define HZ_ATT_NW8_MINL 64
+#endif
 constexpr int ATT_D = 64;
 constexpr int ATT_LMAX = 256;
+constexpr int ATT_KST = ATT_D + 8;  // K row stride (bf16): the 16 rows of a ds_read_b128 fragment hit distinct banks
+constexpr int ATT_VST = ATT_D + 16; // V row stride: 160 B, so the 8 rows of a transposed read's 32-lane half
+                                    // land on 8 distinct 32-B bank slots
 
-constexpr int ATT_KST = ATT_D + 8;  // padded K row stride: the 16 rows of a fragment read hit distinct banks
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-__global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams p) {
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attention_kernel(const HzAttentionParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Lp = (p.L + 31) & ~31;  // keys padded to the 32-wide MFMA K step
-  const int VST = Lp + 8;           // padded V^T / P row strides (bank-conflict-free fragment reads)
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);          // [Lp][ATT_KST]
-  bf16_t* Vt = Ks + Lp * ATT_KST;                       // [64][VST]
-  bf16_t* Ps = Vt + ATT_D * VST;                        // [4 waves][16][VST]
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);  // [Lp][ATT_KST]
+  bf16_t* Vs = Ks + Lp * ATT_KST;                // [Lp][ATT_VST] row-major
+  float* Ms = reinterpret_cast<float*>(Vs + Lp * ATT_VST);  // [Lp] additive mask (-inf for padding keys)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
   const int b = bh / p.heads, h = bh - b * p.heads;
@@ -166,44 +190,37 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
   const bf16_t* Q = p.qkv + row0 * p.ldqkv + h * ATT_D;
   const bf16_t* K = Q + p.k_off;
   const bf16_t* V = Q + p.v_off;
-  // ---- stage K (row-major) and V^T in LDS: every load issued first — one round trip, not one
-  // per iteration. Padding keys (L <= key < Lp) re-read row L-1: their scores are masked to -inf
-  // and their probabilities are exactly 0, so any finite row is correct (no branch, no zero
-  // buffer hotspot) ----
-  constexpr int SIT = ATT_LMAX * 8 / 256;
+  // ---- stage K, V (row-major) and the mask: every load issued first ----
+  constexpr int SIT = ATT_LMAX * 8 / (64 * NW);
   u32x4 kv[SIT], vv[SIT];
 #pragma unroll
   for (int it = 0; it < SIT; ++it) {
-    if (it * 32 >= Lp) break;  // block-uniform
-    const int i = tid + it * 256;
+    const int i = tid + it * 64 * NW;
+    if (i >= Lp * 8) break;  // uniform per iteration count (Lp*8 is a multiple of 64*NW/..): guarded per lane
     const int key = min(i >> 3, p.L - 1), c = (i & 7) * 8;
     kv[it] = *reinterpret_cast<const u32x4*>(K + (long)key * p.ldqkv + c);
     vv[it] = *reinterpret_cast<const u32x4*>(V + (long)key * p.ldqkv + c);
   }
+  for (int k = tid; k < Lp; k += 64 * NW)
+    Ms[k] = k < p.L ? (p.mask ? p.mask[(long)b * p.L + k] : 0.f) : -INFINITY;
 #pragma unroll
   for (int it = 0; it < SIT; ++it) {
-    if (it * 32 >= Lp) break;
-    const int i = tid + it * 256;
+    const int i = tid + it * 64 * NW;
+    if (i >= Lp * 8) break;
     const int key = i >> 3, c = (i & 7) * 8;
-    {
-      *reinterpret_cast<u32x4*>(Ks + key * ATT_KST + c) = kv[it];
-      const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv[it]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(c + e) * VST + key] = ve[e];
-    }
+    *reinterpret_cast<u32x4*>(Ks + key * ATT_KST + c) = kv[it];
+    *reinterpret_cast<u32x4*>(Vs + key * ATT_VST + c) = vv[it];
   }
   __syncthreads();
-  const int q0 = blockIdx.y * 64 + wave * 16;
-  if (q0 >= p.L) return;  // no barrier follows
-  const int lrow = lane & 15, lk = (lane >> 4) * 8;
-  // ---- Q fragments (A operand: rows = queries, k = head dim) ----
-  bf16x8 qa[2];
+  const int q0 = blockIdx.y * 16 * NW + wave * 16;
+  if (q0 >= p.L) return;  // no barrier follows (the transposed reads below need full EXEC: whole waves only)
+  const int lq = lane & 15, g = lane >> 4;
+  // ---- Q^T fragments (B operand: k = head dim, col = query) ----
+  bf16x8 qb[2];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int q = q0 + lrow;
-    qa[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)min(q, p.L - 1) * p.ldqkv + ks * 32 + lk);  // rows >= L discarded
-  }
-  // ---- S = Q K^T: lane holds S[q0 + 4*(lane>>4) + i][kt*16 + lrow] ----
+  for (int ks = 0; ks < 2; ++ks)
+    qb[ks] = *reinterpret_cast<const bf16x8*>(Q + (long)min(q0 + lq, p.L - 1) * p.ldqkv + ks * 32 + g * 8);
+  // ---- S^T = K Q^T: s[kt][i] = score(query q0+lq, key kt*16 + 4g + i) ----
   const int nkt = Lp / 16;
   f32x4 s[ATT_LMAX / 16];
 #pragma unroll
@@ -212,99 +229,98 @@ __global__ __launch_bounds__(256) void attention_kernel(const HzAttentionParams 
     if (kt < nkt) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Ks + (kt * 16 + lrow) * ATT_KST + ks * 32 + lk);
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], kb, s[kt], 0, 0, 0);
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(Ks + (kt * 16 + lq) * ATT_KST + ks * 32 + g * 8);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb[ks], s[kt], 0, 0, 0);
       }
     }
   }
-  // ---- scale + mask + row softmax (row values live in the 16 lanes of one lane>>4 group) ----
-  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  // ---- scale + mask + softmax over the keys of query lq (4 lanes x the lane's values) ----
+  float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < ATT_LMAX / 16; ++kt) {
     if (kt < nkt) {
-      const int key = kt * 16 + lrow;
-      const float madd = key < p.L ? (p.mask ? p.mask[(long)b * p.L + key] : 0.f) : -INFINITY;
+      const f32x4 madd = *reinterpret_cast<const f32x4*>(Ms + kt * 16 + 4 * g);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        s[kt][i] = s[kt][i] * p.scale + madd;
-        mx[i] = fmaxf(mx[i], s[kt][i]);
+        s[kt][i] = s[kt][i] * p.scale + madd[i];
+        mx = fmaxf(mx, s[kt][i]);
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], o, 64));
-  float sum[4] = {0.f, 0.f, 0.f, 0.f};
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
 #pragma unroll
   for (int kt = 0; kt < ATT_LMAX / 16; ++kt) {
     if (kt < nkt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float e = __expf(s[kt][i] - mx[i]);
+        const float e = __expf(s[kt][i] - mx);
         s[kt][i] = e;
-        sum[i] += e;
+        sum += e;
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) sum[i] += __shfl_xor(sum[i], o, 64);
-  bf16_t* P = Ps + wave * 16 * VST;
-#pragma unroll
-  for (int kt = 0; kt < ATT_LMAX / 16; ++kt) {
-    if (kt < nkt) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) P[(4 * (lane >> 4) + i) * VST + kt * 16 + lrow] = f2bf(s[kt][i] / sum[i]);
-    }
-  }
-  // P is private to this wave: make the writes visible to the wave's own cross-lane reads
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-  // ---- O = P V: A = P (rows q, k = keys), B = V (k = keys, cols = d) via V^T rows ----
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  // ---- O^T = V^T P^T over 32-key steps ----
   f32x4 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < Lp / 32; ++ks) {
-    const bf16x8 pa = *reinterpret_cast<const bf16x8*>(P + lrow * VST + ks * 32 + lk);
+  // transposed-read address of this lane: block row (lane&15)>>2 of the group's 4 rows, columns
+  // 4*(lane&3) .. +3 of the 16-dim tile (T10: lane 4r+c supplies row r, columns 4c..4c+3)
+  const int tr_row = (lane & 15) >> 2, tr_col = (lane & 3) * 4;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (dt * 16 + lrow) * VST + ks * 32 + lk);
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+  for (int c = 0; c < ATT_LMAX / 32; ++c) {
+    if (c < Lp / 32) {
+      const f32x4 pa = s[2 * c], pb = s[2 * c + 1];
+      const u32x4 pw = u32x4{pack_bf16x2(pa[0] * inv, pa[1] * inv), pack_bf16x2(pa[2] * inv, pa[3] * inv),
+                             pack_bf16x2(pb[0] * inv, pb[1] * inv), pack_bf16x2(pb[2] * inv, pb[3] * inv)};
+      const bf16x8 pfrag = *reinterpret_cast<const bf16x8*>(&pw);
+      const int r_lo = 32 * c + 4 * g + tr_row, r_hi = r_lo + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(Vs + r_lo * ATT_VST + dt * 16 + tr_col));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(Vs + r_hi * ATT_VST + dt * 16 + tr_col));
+        const short vv8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(vv8);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pfrag, o[dt], 0, 0, 0);
+      }
     }
   }
-  // lane holds O[q0 + 4*(lane>>4) + i][dt*16 + lrow]
-  if (p.out8) {  // MX8 output: head columns [0,32) = dt 0,1 and [32,64) = dt 2,3 are two E8M0 blocks
+  // lane holds O[q0 + lq][dt*16 + 4g + i]
+  const int q = q0 + lq;
+  if (p.out8) {  // MX8 output: head dims [0,32) = dt 0,1 and [32,64) = dt 2,3 are two E8M0 blocks
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = q0 + 4 * (lane >> 4) + i;
+    for (int hb = 0; hb < 2; ++hb) {
+      float amax = 0.f;
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        float amax = fmaxf(fabsf(o[2 * hb][i]), fabsf(o[2 * hb + 1][i]));
+      for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
-        const int ex = mx_exp(amax);
-        if (q < p.L) {
-          unsigned char* o8 = p.out8 + (row0 + q) * p.ldo + h * ATT_D + hb * 32;
+        for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(o[2 * hb + d][i]));
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int ex = mx_exp(amax);
+      if (q < p.L) {
+        unsigned char* o8 = p.out8 + (row0 + q) * p.ldo + h * ATT_D + hb * 32;
 #pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const float x = fminf(fmaxf(ldexpf(o[2 * hb + d][i], -ex), -448.f), 448.f);
-            o8[d * 16 + lrow] = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xff);
-          }
-          if (lrow == 0) p.os8[(row0 + q) * (p.ldo >> 5) + h * 2 + hb] = (unsigned char)(ex + 127);
+        for (int d = 0; d < 2; ++d) {
+          float x[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = fminf(fmaxf(ldexpf(o[2 * hb + d][i], -ex), -448.f), 448.f);
+          *reinterpret_cast<unsigned*>(o8 + d * 16 + 4 * g) = pack4_fp8(x[0], x[1], x[2], x[3]);
         }
+        if (g == 0) p.os8[(row0 + q) * (p.ldo >> 5) + h * 2 + hb] = (unsigned char)(ex + 127);
       }
     }
     return;
   }
+  if (q < p.L) {
+    bf16_t* out = p.out + (row0 + q) * p.ldo + h * ATT_D + 4 * g;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = q0 + 4 * (lane >> 4) + i;
-    if (q >= p.L) continue;
-    bf16_t* out = p.out + (row0 + q) * p.ldo + h * ATT_D;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) out[dt * 16 + lrow] = f2bf(o[dt][i]);
+    for (int dt = 0; dt < 4; ++dt)
+      *reinterpret_cast<u32x2*>(out + dt * 16) = u32x2{pack_bf16x2(o[dt][0], o[dt][1]), pack_bf16x2(o[dt][2], o[dt][3])};
   }
 }
 
@@ -378,9 +394,12 @@ extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) 
   const HzAttentionParams& p = *pp;
   if (p.head_dim != ATT_D || p.L > ATT_LMAX || p.L < 1) return -1;
   if (p.out8 && (!p.os8 || p.ldo % 32)) return -1;
+  if (p.ldqkv % 8 || p.k_off % 8 || p.v_off % 8 || p.ldo % 4) return -1;  // 16-B staging, 8-B stores
   const int Lp = (p.L + 31) & ~31;
-  const size_t lds = (size_t)(Lp * ATT_KST + ATT_D * (Lp + 8) + 4 * 16 * (Lp + 8)) * sizeof(bf16_t);
-  hipLaunchKernelGGL(attention_kernel, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
+  const size_t lds = (size_t)Lp * (ATT_KST + ATT_VST) * sizeof(bf16_t) + (size_t)Lp * sizeof(float);
+  // 8 waves (128 queries) per workgroup for long sequences: K/V staged half as often
+  if (p.L > HZ_ATT_NW8_MINL) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
+  else hipLaunchKernelGGL(attention_kernel<4>, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
   return (int)hipGetLastError();
 }
 
