@@ -332,11 +332,21 @@ class ExecContext:
             pass
 
 
-def bench_contexts(ctxs: list, streams: list, iters: int) -> float:
-    """Replay every context on its own stream ``iters`` times from C++; returns seconds."""
+def bench_contexts(ctxs: list, streams: list, iters: int, threads: bool | None = None) -> float:
+    """Replay every context on its own stream ``iters`` times from C++; returns seconds.
+    ``threads`` (default: env ``HIPZAP_SUBMIT_THREADS=1``): one host submission thread per
+    stream instead of one thread round-robining over all streams."""
     n = len(ctxs)
     progs = (C.c_void_p * n)(*[c.prog for c in ctxs])
     strs = (C.c_void_p * n)(*[s.cuda_stream for s in streams])
+    if threads is None:
+        threads = os.environ.get("HIPZAP_SUBMIT_THREADS", "0") == "1"
+    if threads and n > 1:
+        out = (C.c_double * 2)()
+        rc = N.lib().hz_prog_bench2(progs, strs, n, iters, 1, out)
+        if rc:
+            raise RuntimeError(f"hz_prog_bench2 failed ({rc})")
+        return out[1] * 1e-6
     us = N.lib().hz_prog_bench(progs, strs, n, iters)
     if us < 0:
         raise RuntimeError(f"hz_prog_bench failed ({us})")
