@@ -6,6 +6,12 @@
 
 namespace {
 
+// K x K window. With K known at compile time (the ResNet 3x3/2 stem pool) every tap is loaded
+// before the first max: out-of-range taps are clamped to the nearest border pixel, which lies in
+// the same window (a window overlapping the image contains its clamped taps), so the max is
+// unchanged and no load is predicated — one memory round trip instead of a dependent chain of
+// K*K (the runtime-K loop below compiled to one wait per tap).
+template <int K>
 __global__ __launch_bounds__(256) void maxpool_kernel(const HzPoolParams p) {
   const int C8 = p.C >> 3;
   const long total = (long)p.N * p.P * p.Q * C8;
@@ -21,17 +27,37 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const HzPoolParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
   const int h0 = pp * p.stride - p.pad, w0 = q * p.stride - p.pad;
-  for (int r = 0; r < p.k; ++r) {
-    const int ih = h0 + r;
-    if ((unsigned)ih >= (unsigned)p.H) continue;
-    for (int s = 0; s < p.k; ++s) {
-      const int iw = w0 + s;
-      if ((unsigned)iw >= (unsigned)p.W) continue;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(p.x + (((long)n * p.H + ih) * p.W + iw) * p.C + c8 * 8);
+  if constexpr (K > 0) {
+    u32x4 v[K * K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int ih = min(max(h0 + r, 0), p.H - 1);
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const int iw = min(max(w0 + s, 0), p.W - 1);
+        v[r * K + s] = *reinterpret_cast<const u32x4*>(p.x + (((long)n * p.H + ih) * p.W + iw) * p.C + c8 * 8);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K * K; ++j) {
       float f[8];
-      unpack8(v, f);
+      unpack8(v[j], f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+    }
+  } else {
+    for (int r = 0; r < p.k; ++r) {
+      const int ih = h0 + r;
+      if ((unsigned)ih >= (unsigned)p.H) continue;
+      for (int s = 0; s < p.k; ++s) {
+        const int iw = w0 + s;
+        if ((unsigned)iw >= (unsigned)p.W) continue;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(p.x + (((long)n * p.H + ih) * p.W + iw) * p.C + c8 * 8);
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+      }
     }
   }
   *reinterpret_cast<u32x4*>(p.out + i * 8) = pack8(m);
@@ -73,36 +99,59 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__
 // (K) four ways, so each wave pools ONLY its own C/4 channels (fp32, into its LDS slice) and
 // then dots them with its K-quarter of the group's weights; the 4 partial sums meet in LDS.
 // Pooling: lane l reads 16 B (8 channels) of channel block (l>>2) of the wave's slice at every
-// pixel, 16 pixels in flight per lane. Weights are fragment-major (one contiguous 1 KiB per
-// 32-deep k-step); the 4 lanes sharing an output row (l, l^16, l^32, l^48) reduce by shuffles.
-// A first version with 16 blocks x 4 full-K groups took 11.7 us (profiled) — per-wave serial
-// latency; this one has N/16 blocks with 1/4 of the chain each.
+// pixel. Weights are fragment-major (one contiguous 1 KiB per 32-deep k-step); the 4 lanes
+// sharing an output row (l, l^16, l^32, l^48) reduce by shuffles.
+// Latency: the wave's first WB weight fragments are issued before the pooling (independent of
+// it). NB = ceil(HW/8) > 0 additionally issues ALL pixel loads before the first use (one round
+// trip instead of one per 8 pixels) but needs 384 VGPRs at HW = 49: one workgroup per CU, which
+// measured -1.5 % at 8 concurrent request streams (profiles/r1_ab/vision_latency.txt), so the
+// runtime loop (NB = 0) is the default (HZ_POOLFC_STATIC).
+template <int NB>
 __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   extern __shared__ __attribute__((aligned(16))) float pooled[];  // [C] + [4][16] partials
+  constexpr int WB = 16;  // weight fragments in flight per wave
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int b = blockIdx.y, g = blockIdx.x;
   const int ncb = p.C >> 5;
   const int cpw = (ncb + 3) >> 2;  // channel blocks per wave
   const int cb_lo = wave * cpw, cb_hi = min(ncb, cb_lo + cpw);
   const float inv = 1.f / p.HW;
+  const int ks = p.C >> 5;
+  const bf16_t* wg = p.w + ((long)g * ks * 64 + lane) * 8;
+  // first batch of weight fragments: independent of the pooling, so in flight with it
+  u32x4 wv[WB];
+#pragma unroll
+  for (int j = 0; j < WB; ++j) wv[j] = *reinterpret_cast<const u32x4*>(wg + (long)min(cb_lo + j, cb_hi - 1) * 512);
   for (int cb0 = cb_lo; cb0 < cb_hi; cb0 += 16) {
     const int cb = cb0 + (lane >> 2), sub = lane & 3;
     if (cb < cb_hi) {
       const bf16_t* src = p.x + (((long)b * ncb + cb) * p.HW) * 32 + sub * 8;
       float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      // 8 independent loads in flight per lane (indices clamped, tail weighted 0): a plain loop
-      // compiled to one dependent L2 round trip per pixel (22 us profiled for 49 pixels)
-      for (int hw0 = 0; hw0 < p.HW; hw0 += 8) {
-        u32x4 v[8];
+      if constexpr (NB > 0) {
+        u32x4 v[NB * 8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const u32x4*>(src + min(hw0 + j, p.HW - 1) * 32);
+        for (int j = 0; j < NB * 8; ++j) v[j] = *reinterpret_cast<const u32x4*>(src + min(j, p.HW - 1) * 32);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < NB * 8; ++j) {
           float f[8];
           unpack8(v[j], f);
-          const float wj = hw0 + j < p.HW ? 1.f : 0.f;
+          const float wj = j < p.HW ? 1.f : 0.f;
 #pragma unroll
           for (int e = 0; e < 8; ++e) s[e] += wj * f[e];
+        }
+      } else {
+        for (int hw0 = 0; hw0 < p.HW; hw0 += 8) {  // 8 independent loads in flight per lane
+          u32x4 v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const u32x4*>(src + min(hw0 + j, p.HW - 1) * 32);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float f[8];
+            unpack8(v[j], f);
+            const float wj = hw0 + j < p.HW ? 1.f : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s[e] += wj * f[e];
+          }
         }
       }
 #pragma unroll
@@ -113,16 +162,15 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int ks = p.C >> 5;
-  const bf16_t* wg = p.w + ((long)g * ks * 64 + lane) * 8;
   const float* pl = pooled + (lane >> 4) * 8;
   float acc = 0.f;
-  for (int k0 = cb_lo; k0 < cb_hi; k0 += 8) {  // 8 weight fragments in flight, then the dots
-    u32x4 wv[8];
+  for (int k0 = cb_lo; k0 < cb_hi; k0 += WB) {
+    if (k0 != cb_lo) {  // later batches (C/4 > WB*32 channels per wave)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wv[j] = *reinterpret_cast<const u32x4*>(wg + (long)min(k0 + j, cb_hi - 1) * 512);
+      for (int j = 0; j < WB; ++j) wv[j] = *reinterpret_cast<const u32x4*>(wg + (long)min(k0 + j, cb_hi - 1) * 512);
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < WB; ++j) {
       const int k = min(k0 + j, cb_hi - 1);
       float f[8];
       unpack8(wv[j], f);
@@ -153,13 +201,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const void* __restrict_
   const long HWl = (long)H * W;
   if (i >= N * HWl) return;
   const long n = i / HWl, hw = i - n * HWl;
-  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int c = 0; c < Cin && c < 8; ++c) {
-    float f;
-    if (mode == 0) f = reinterpret_cast<const float*>(src)[(n * Cin + c) * HWl + hw];
-    else f = (float)reinterpret_cast<const unsigned char*>(src)[i * Cin + c] * (1.0f / 255.0f);
-    if (mean) f = (f - mean[c]) * inv_std[c];
+  // every channel's load (and the normalisation constants) issued before the first use: a
+  // runtime channel loop waited once per channel — over PCIe when the request is read zero-copy
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float f = 0.f;
+    if (c < Cin) {
+      if (mode == 0) f = reinterpret_cast<const float*>(src)[(n * Cin + c) * HWl + hw];
+      else f = (float)reinterpret_cast<const unsigned char*>(src)[i * Cin + c] * (1.0f / 255.0f);
+    }
     v[c] = f;
+  }
+  if (mean) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < Cin) v[c] = (v[c] - mean[c]) * inv_std[c];
   }
   bf16_t* o = dst + i * Cpad;
   *reinterpret_cast<u32x4*>(o) = pack8(v);
@@ -186,7 +243,9 @@ extern "C" int hz_maxpool_launch(const HzPoolParams* pp, hipStream_t st) {
   const HzPoolParams& p = *pp;
   if (p.C % 8) return -1;
   const long total = (long)p.N * p.P * p.Q * (p.C / 8);
-  hipLaunchKernelGGL(maxpool_kernel, dim3((total + 255) / 256), dim3(256), 0, st, p);
+  // clamped taps are only inside the window when the padding is smaller than the window
+  if (p.k == 3 && p.pad < 3) hipLaunchKernelGGL(maxpool_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, p);
+  else hipLaunchKernelGGL(maxpool_kernel<0>, dim3((total + 255) / 256), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -201,7 +260,18 @@ extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
   const HzPoolFcParams& p = *pp;
   if (p.C % 32 || p.C > 16384 || p.HW < 1 || p.N < 1) return -1;
   const int groups = (p.N + 15) / 16;
-  hipLaunchKernelGGL(pool_fc_kernel, dim3(groups, p.B), dim3(256), (size_t)(p.C + 64) * sizeof(float), st, p);
+  const size_t lds = (size_t)(p.C + 64) * sizeof(float);
+  const dim3 grid(groups, p.B);
+#ifndef HZ_POOLFC_STATIC
+#define HZ_POOLFC_STATIC 0  // 1: measured -1.5 % at 8 streams (384 VGPRs, one workgroup per CU)
+#endif
+  switch (HZ_POOLFC_STATIC ? (p.HW + 7) / 8 : 0) {  // compile-time pixel batches: every pooling load in flight
+    case 1: hipLaunchKernelGGL(pool_fc_kernel<1>, grid, dim3(256), lds, st, p); break;
+    case 2: hipLaunchKernelGGL(pool_fc_kernel<2>, grid, dim3(256), lds, st, p); break;
+    case 4: hipLaunchKernelGGL(pool_fc_kernel<4>, grid, dim3(256), lds, st, p); break;
+    case 7: hipLaunchKernelGGL(pool_fc_kernel<7>, grid, dim3(256), lds, st, p); break;  // 7x7 (ResNet @224)
+    default: hipLaunchKernelGGL(pool_fc_kernel<0>, grid, dim3(256), lds, st, p); break;
+  }
   return (int)hipGetLastError();
 }
 
