@@ -16,12 +16,12 @@ import sys
 
 
 def cmd_serve(a):
-    from .serve.app import app
+    from .serve.app import app, serve_threaded
     from .serve.settings import load_settings
     st = load_settings(a.settings, a.stage)
     host, port = a.host or st.host, a.port or st.port
     print(f"hipzap serving stage {st.stage} on {host}:{port} (models bucket {st.models_bucket!r})", flush=True)
-    app.run(host=host, port=port, debug=False, threaded=True)
+    app.run(host=host, port=port, debug=False, threaded=serve_threaded())
 
 
 def cmd_pack(a):

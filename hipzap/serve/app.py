@@ -33,6 +33,15 @@ app = Flask("hipzap")
 _server: ModelServer | None = None
 
 
+def serve_threaded() -> bool:
+    """Threaded WSGI serving for the GPU backend (engines take concurrent requests on their own
+    contexts/streams). The CPU backend serves on the main thread: eager PyTorch CPU inference
+    called from a WSGI worker thread ran 3.5x slower than from the main thread here (OpenMP /
+    oneDNN thread handling; 72-77 ms vs 20 ms per ResNet-18 forward), and the eager AWD-LSTM is
+    not reentrant anyway."""
+    return get_server().backend != "cpu"
+
+
 def get_server() -> ModelServer:
     global _server
     if _server is None:
@@ -150,12 +159,16 @@ def decode_input(req) -> tuple[str, torch.Tensor]:
         else:
             raise ValueError("request needs one of: inputs, tensor_b64, image_b64 (or an .npy body)")
     if x.dtype == torch.uint8:  # HWC / NHWC image bytes -> normalised NCHW float
+        # in numpy: torch's multi-threaded elementwise ops on this request thread would start an
+        # OpenMP team per WSGI thread, spinning against the model's own thread pool
         from ..ops.vision import IMAGENET_MEAN, IMAGENET_STD
-        if x.dim() == 3:
-            x = x[None]
-        x = x.float().div(255.0).permute(0, 3, 1, 2)
-        x = (x - torch.tensor(IMAGENET_MEAN).view(1, 3, 1, 1)) / torch.tensor(IMAGENET_STD).view(1, 3, 1, 1)
-    x = x.float()
+        a = x.numpy()
+        if a.ndim == 3:
+            a = a[None]
+        a = (a.astype(np.float32) * np.float32(1 / 255.0) - np.asarray(IMAGENET_MEAN, np.float32)) \
+            / np.asarray(IMAGENET_STD, np.float32)
+        x = torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2)))
+    x = x.float().contiguous()  # NCHW-contiguous: a permuted view sends CPU convs down a slow path
     if x.dim() == 3:
         x = x[None]
     return model or get_server().settings.default_model, x
