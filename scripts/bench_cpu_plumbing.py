@@ -37,18 +37,20 @@ def _post(url, payload: bytes):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--requests", type=int, default=50)
+    ap.add_argument("--backend", default="cpu", help="cpu (config 1) or gpu (the same HTTP path on MI355X)")
+    ap.add_argument("--model", default="resnet18")
     args = ap.parse_args()
     import numpy as np
     rng = np.random.default_rng(0)
     img = rng.integers(0, 256, (224, 224, 3), dtype=np.uint8)
-    body_img = json.dumps({"model": "resnet18", "image_b64": base64.b64encode(img.tobytes()).decode(),
+    body_img = json.dumps({"model": args.model, "image_b64": base64.b64encode(img.tobytes()).decode(),
                            "shape": [224, 224, 3]}).encode()
     x = rng.standard_normal((1, 3, 224, 224), dtype=np.float32)
-    body_t = json.dumps({"model": "resnet18", "tensor_b64": base64.b64encode(x.tobytes()).decode(),
+    body_t = json.dumps({"model": args.model, "tensor_b64": base64.b64encode(x.tobytes()).decode(),
                          "shape": [1, 3, 224, 224]}).encode()
 
     port = _port()
-    env = dict(os.environ, HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_PORT=str(port), HIPZAP_BACKEND="cpu",
+    env = dict(os.environ, HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_PORT=str(port), HIPZAP_BACKEND=args.backend,
                HIPZAP_SETTINGS="/nonexistent", HIPZAP_LM_VOCAB="300")
     t0 = time.perf_counter()
     proc = subprocess.Popen([sys.executable, "main.py"], cwd=ROOT, env=env, stdout=subprocess.DEVNULL,
@@ -74,13 +76,13 @@ def main():
                 ta = time.perf_counter()
                 r = _post(base + "/predict", body)
                 lat[name].append((time.perf_counter() - ta) * 1e3)
-                assert r["backend"] == "cpu" and len(r["top5"][0]) == 5
+                assert r["backend"] == args.backend and len(r["top5"][0]) == 5
     finally:
         proc.terminate()
         proc.wait(timeout=30)
 
     # the same request through the Lambda (API Gateway v1) adapter, in process
-    os.environ.update(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_BACKEND="cpu", HIPZAP_SETTINGS="/nonexistent")
+    os.environ.update(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_BACKEND=args.backend, HIPZAP_SETTINGS="/nonexistent")
     sys.path.insert(0, ROOT)
     from hipzap.serve.lambda_handler import lambda_handler
     ev = {"httpMethod": "POST", "path": "/predict", "headers": {"content-type": "application/json"},
@@ -92,7 +94,8 @@ def main():
         assert lambda_handler(ev)["statusCode"] == 200
         lam.append((time.perf_counter() - ta) * 1e3)
     print(json.dumps({
-        "metric": "config 1: ResNet-18 single-image POST /predict, CPU Flask/WSGI handler (plumbing, no GPU)",
+        "metric": f"single-image POST /predict through the Flask/WSGI handler: {args.model}, {args.backend} backend"
+                  + (" (config 1: plumbing, no GPU)" if args.backend == "cpu" else ""),
         "requests": args.requests, "cpu_threads": os.cpu_count(),
         "server_up_ms": round(up_ms, 1), "first_request_ms": round(first_ms, 1),
         "cold_start_to_first_200_ms": round(cold_ms, 1),
@@ -100,7 +103,7 @@ def main():
         "http_tensor_b64_ms_p50": round(statistics.median(lat["tensor_b64"]), 2),
         "lambda_event_ms_p50": round(statistics.median(lam), 2),
         "reference_cpu_resnet18_ms": 16.6,
-        "data": "random-init ResNet-18 weights, random uint8 image / fp32 tensor",
+        "data": f"random-init {args.model} weights, random uint8 image / fp32 tensor",
         "first_top1": first["top5"][0][0]}), flush=True)
 
 
