@@ -60,7 +60,7 @@ def run_scatter(args, rank, world, device, adapter, ckpt):
     """BASELINE configs 3/5: global batch scattered over ranks (RCCL), per-rank hipGraph, logits
     gathered to rank 0. Step = scatter + per-rank forward + gather."""
     from hipzap.engine.engine import Engine
-    from hipzap.parallel.comm import broadcast_params, is_dist
+    from hipzap.parallel.comm import broadcast_params, is_dist, max_over_ranks
     from hipzap.parallel.dp import DPExecutor
     shard = args.global_batch // world
     assert shard * world == args.global_batch, "global batch must divide over ranks"
@@ -93,9 +93,7 @@ def run_scatter(args, rank, world, device, adapter, ckpt):
     dt = time.perf_counter() - t1
     if is_dist():
         dist.barrier()
-        tt = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(dt, device)
     del x_in
     if rank == 0:
         value = args.global_batch * args.steps / dt
@@ -159,10 +157,11 @@ def main():
     args = parse()
     from hipzap.engine.engine import Engine
     from hipzap.models import registry
-    from hipzap.parallel.comm import broadcast_params, env_rank, init_distributed, is_dist
+    from hipzap.parallel.comm import (broadcast_params, env_rank, init_distributed, is_dist, local_device,
+                                      max_over_ranks)
 
     rank, world, local = env_rank()
-    device = torch.device("cuda", local)
+    device = local_device(local)
     torch.cuda.set_device(device)
     init_distributed(device=device)
     adapter = registry.get(args.model)
@@ -275,9 +274,7 @@ def main():
     dt = time.perf_counter() - t0
     if is_dist():
         dist.barrier()
-        tt = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(dt, device)
     inf = world * args.streams * args.batch * args.steps
     value = inf / dt
     torch_ref = None

@@ -30,14 +30,33 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
     rank, world, local = env_rank()
     if world <= 1 or (dist.is_available() and dist.is_initialized()):
         return rank, world, local
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # HIPZAP_DIST_BACKEND=gloo: multi-rank rehearsal on one GPU (HIPZAP_SHARE_GPU=1)
+        backend = os.environ.get("HIPZAP_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl" and device is not None:
         kw["device_id"] = device
     dist.init_process_group(**kw)
     return rank, world, local
+
+
+def local_device(local: int) -> torch.device:
+    """This rank's GPU: ``cuda:LOCAL_RANK``. ``HIPZAP_SHARE_GPU=1`` folds ranks onto the visible
+    GPUs (``LOCAL_RANK % device_count``) so a multi-rank run can be rehearsed on one GPU with
+    ``HIPZAP_DIST_BACKEND=gloo`` (RCCL refuses two ranks on one device)."""
+    if os.environ.get("HIPZAP_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
+    return torch.device("cuda", local)
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    """Slowest rank's value (bench timing). Host tensor under gloo, device tensor under RCCL."""
+    if not is_dist():
+        return x
+    dev = "cpu" if dist.get_backend() == "gloo" else device
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def is_dist() -> bool:

@@ -63,19 +63,41 @@ class TorchComm(Comm):
         self.dist, self.group = dist, group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        # gloo (CPU tests, or a multi-rank rehearsal sharing one GPU) has no device scatter/gather:
+        # stage device tensors through host memory. RCCL never takes this path.
+        self.host_stage = dist.get_backend(group) == "gloo"
+
+    def _h(self, t):
+        return t.cpu() if (t is not None and self.host_stage and t.is_cuda) else t
+
+    @staticmethod
+    def _back(dst, src):
+        if dst is not None and src is not dst:
+            dst.copy_(src)
 
     def broadcast(self, t, src=0):
-        self.dist.broadcast(t, src=src, group=self.group)
+        h = self._h(t)
+        self.dist.broadcast(h, src=src, group=self.group)
+        self._back(t, h)
 
     def scatter(self, out, chunks, src=0):
-        self.dist.scatter(out, chunks if self.rank == src else None, src=src, group=self.group)
+        h = self._h(out)
+        hc = [self._h(c) for c in chunks] if self.rank == src else None
+        self.dist.scatter(h, hc, src=src, group=self.group)
+        self._back(out, h)
 
     def gather(self, t, outs, dst=0):
-        self.dist.gather(t, outs if self.rank == dst else None, dst=dst, group=self.group)
+        ho = [self._h(o) for o in outs] if self.rank == dst else None
+        self.dist.gather(self._h(t), ho, dst=dst, group=self.group)
+        if ho is not None:
+            for o, h in zip(outs, ho):
+                self._back(o, h)
 
     def all_reduce(self, t, op="sum"):
         rop = {"sum": self.dist.ReduceOp.SUM, "max": self.dist.ReduceOp.MAX}[op]
-        self.dist.all_reduce(t, op=rop, group=self.group)
+        h = self._h(t)
+        self.dist.all_reduce(h, op=rop, group=self.group)
+        self._back(t, h)
 
     def barrier(self):
         self.dist.barrier(group=self.group)
