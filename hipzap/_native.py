@@ -11,7 +11,11 @@ import os
 import threading
 from pathlib import Path
 
-_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libhipzap.so"
+# HIPZAP_DEBUG=1 selects the HZ_DEBUG variant (device-side contract checks, csrc/common.h HZ_DCHECK;
+# build it with `python -m hipzap.build --debug`); failures are read with hipzap.utils.kcheck
+DEBUG = os.environ.get("HIPZAP_DEBUG") == "1"
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / ("libhipzap_debug.so" if DEBUG else "libhipzap.so")
+DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm")
 _lock = threading.Lock()
 _lib = None
 
@@ -103,6 +107,9 @@ def _load():
     _sig(lib, "hz_prog_add_lstm", c_int, P, C.POINTER(LstmParams), c_int)
     _sig(lib, "hz_prog_add_decoder", c_int, P, C.POINTER(DecoderParams), c_int)
     _sig(lib, "hz_prog_add_sampler", c_int, P, C.POINTER(SamplerParams), c_int)
+    if DEBUG:
+        for unit in DEBUG_UNITS:
+            _sig(lib, f"hz_debug_poll_{unit}", c_int, C.POINTER(C.c_uint))
     for extra in _EXTRA_SIGS:
         extra(lib)
     return lib
@@ -127,7 +134,7 @@ def lib():
                 if os.environ.get("HIPZAP_NO_AUTOBUILD"):
                     raise RuntimeError(f"hipzap native library missing: {_LIB_PATH} (run python -m hipzap.build)")
                 from . import build as _b
-                _b.build(verbose=False)
+                _b.build(verbose=False, debug=DEBUG)
             _lib = _load()
     return _lib
 

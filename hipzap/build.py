@@ -21,6 +21,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libhipzap.so"
+LIB_DEBUG = LIBDIR / "libhipzap_debug.so"  # -DHZ_DEBUG: device-side HZ_DCHECK contracts (csrc/common.h)
 OBJDIR = PKG.parent / "build" / "obj"
 ARCH = os.environ.get("HIPZAP_ARCH", "gfx950")
 
@@ -34,21 +35,25 @@ def sources() -> list[Path]:
     return sorted([p for p in CSRC.iterdir() if p.suffix in (".hip", ".cpp")])
 
 
-def _hash(src: Path) -> str:
+def _flags(debug: bool) -> list[str]:
+    return COMMON + (["-DHZ_DEBUG"] if debug else [])
+
+
+def _hash(src: Path, debug: bool = False) -> str:
     h = hashlib.sha1()
-    h.update(" ".join(COMMON).encode())
+    h.update(" ".join(_flags(debug)).encode())
     h.update(src.read_bytes())
     for hdr in sorted(CSRC.glob("*.h")):  # headers are shared: any change invalidates all
         h.update(hdr.read_bytes())
     return h.hexdigest()[:16]
 
 
-def _compile(src: Path) -> Path:
-    obj = OBJDIR / f"{src.stem}-{_hash(src)}.o"
+def _compile(src: Path, debug: bool = False) -> Path:
+    obj = OBJDIR / f"{src.stem}{'-dbg' if debug else ''}-{_hash(src, debug)}.o"
     if obj.exists():
         return obj
     tmp = obj.with_suffix(".o.tmp")
-    cmd = [HIPCC, *COMMON, "-c", str(src), "-o", str(tmp)]
+    cmd = [HIPCC, *_flags(debug), "-c", str(src), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
@@ -56,35 +61,38 @@ def _compile(src: Path) -> Path:
     return obj
 
 
-def build(verbose: bool = True, jobs: int | None = None) -> Path:
+def build(verbose: bool = True, jobs: int | None = None, debug: bool = False) -> Path:
+    """Release library (``libhipzap.so``) or, with ``debug``, the HZ_DEBUG variant
+    (``libhipzap_debug.so``, loaded when ``HIPZAP_DEBUG=1``)."""
     OBJDIR.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     srcs = sources()
+    lib = LIB_DEBUG if debug else LIB
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda s: _compile(s, debug), srcs))
     live = {o.name for o in objs}
-    for stale in OBJDIR.glob("*.o"):  # objects of older source versions
-        if stale.name not in live:
+    for stale in OBJDIR.glob("*.o"):  # objects of older source versions (of this variant)
+        if stale.name not in live and ("-dbg-" in stale.name) == debug:
             stale.unlink(missing_ok=True)
     key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
-    stamp = LIBDIR / ".buildkey"
-    if LIB.exists() and stamp.exists() and stamp.read_text() == key:
+    stamp = LIBDIR / (".buildkey_debug" if debug else ".buildkey")
+    if lib.exists() and stamp.exists() and stamp.read_text() == key:
         if verbose:
-            print(f"hipzap: {LIB} up to date")
-        return LIB
-    tmp = LIB.with_suffix(".so.tmp")
+            print(f"hipzap: {lib} up to date")
+        return lib
+    tmp = lib.with_suffix(".so.tmp")
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     stamp.write_text(key)
     if verbose:
-        print(f"hipzap: built {LIB} from {len(objs)} sources")
-    return LIB
+        print(f"hipzap: built {lib} from {len(objs)} sources")
+    return lib
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    build(verbose=True, debug="--debug" in sys.argv[1:])
     sys.exit(0)

@@ -13,6 +13,39 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 #define HZ_WAVE 64
 
+// ---- DEBUG kernel variant (SURVEY.md §5 "bounds-check asserts in a DEBUG kernel variant") ----
+// `python -m hipzap.build --debug` compiles every source with -DHZ_DEBUG into
+// hipzap/_lib/libhipzap_debug.so; HIPZAP_DEBUG=1 makes hipzap._native load that library.
+// HZ_DCHECK(cond) guards a global access or a launch contract: in the release build it is the
+// constant `true` (compiled away); in the debug build a false condition records (line, block,
+// thread) of the FIRST failure of the translation unit in a device word, counts all failures,
+// and evaluates to false so the caller SKIPS the access — a failed check never faults the GPU
+// (a kernel fault can reset every GPU of the host). The host reads and clears the records with
+// hz_debug_poll_<unit>() after a sync (hipzap/utils/kcheck.py). Each .hip file that uses
+// HZ_DCHECK instantiates its own record with HZ_DEBUG_UNIT(<unit>) at file scope.
+#ifdef HZ_DEBUG
+#define HZ_DEBUG_UNIT(UNIT)                                                             \
+  static __device__ unsigned hz_dbg_rec[4];                                             \
+  static __device__ __noinline__ bool hz_dbg_fail(int line) {                          \
+    if (atomicCAS(&hz_dbg_rec[0], 0u, (unsigned)line) == 0u) {                          \
+      atomicExch(&hz_dbg_rec[1], blockIdx.x + (blockIdx.y << 20));                      \
+      atomicExch(&hz_dbg_rec[2], threadIdx.x);                                          \
+    }                                                                                   \
+    atomicAdd(&hz_dbg_rec[3], 1u);                                                      \
+    return false;                                                                       \
+  }                                                                                     \
+  extern "C" int hz_debug_poll_##UNIT(unsigned* out) {                                  \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hz_dbg_rec), sizeof(hz_dbg_rec)) != hipSuccess) \
+      return -1;                                                                        \
+    const unsigned z[4] = {0, 0, 0, 0};                                                 \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(hz_dbg_rec), z, sizeof(z));                \
+  }
+#define HZ_DCHECK(cond) (__builtin_expect(!!(cond), 1) ? true : hz_dbg_fail(__LINE__))
+#else
+#define HZ_DEBUG_UNIT(UNIT)
+#define HZ_DCHECK(cond) true
+#endif
+
 #define HZ_CHECK(x)                                                              \
   do {                                                                           \
     hipError_t e__ = (x);                                                        \

@@ -25,6 +25,8 @@
 #include "common.h"
 #include "hipzap.h"
 
+HZ_DEBUG_UNIT(conv)
+
 namespace {
 
 #ifndef HZ_RING_SHRINK
@@ -57,6 +59,12 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 
   const int C = p.C, HW = p.H * p.W;
   const int steps = p.ksteps;
+  // debug contracts: activation extent, packed weight rows (ROW_PAD 64 / GEMM_ROW_PAD 128 in
+  // ops/conv.py), output extent, and that M matches the spatial problem
+  const long xlim = XROW ? (long)p.M * p.ldx : (long)p.N * HW * C;
+  const int wgroups = ((p.Cout + 63) >> 6) << 2;
+  const long olim = p.out_rowmajor ? (long)(p.M - 1) * p.ldo + p.Cout : (long)p.N * p.Cout * p.P * p.Q;
+  if (!HZ_DCHECK(XROW || p.M == p.N * p.P * p.Q)) return;
   const int spw = (steps + KW - 1) / KW;
   const int s_begin = wave * spw;
   const int nsteps = max(0, min(steps, s_begin + spw) - s_begin);
@@ -119,12 +127,14 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     const int k = s_idx * 32;
 #pragma unroll
     for (int i = 0; i < FC; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(Wf + ((long)i * steps + s_idx) * 512);
+      if (HZ_DCHECK((n0 >> 4) + i < wgroups && s_idx < steps))
+        a[i] = *reinterpret_cast<const bf16x8*>(Wf + ((long)i * steps + s_idx) * 512);
     if constexpr (XROW) {  // plain GEMM: row-major activations [M][ldx] (transformers)
 #pragma unroll
       for (int j = 0; j < FP; ++j) {
         const int kk = k + lk;
-        if (pval[j] && kk < p.K) b[j] = *reinterpret_cast<const bf16x8*>(X + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
+        if (pval[j] && kk < p.K && HZ_DCHECK((long)(m0 + j * 16 + lrow) * p.ldx + kk + 8 <= xlim))
+          b[j] = *reinterpret_cast<const bf16x8*>(X + (long)(m0 + j * 16 + lrow) * p.ldx + kk);
         else b[j] = bf16x8{};
       }
     } else if constexpr (FAST) {  // C % 32 == 0: one (r, s, 32-channel block) per step, wave-uniform
@@ -139,7 +149,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
       if constexpr (IS1X1) {
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
-          if (pval[j]) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + cb * HW) << 5) + lk);
+          const long off = ((long)(pb[j] + cb * HW) << 5) + lk;
+          if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) b[j] = *reinterpret_cast<const bf16x8*>(X + off);
           else b[j] = bf16x8{};
         }
       } else {
@@ -147,7 +158,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
           const bool v = pval[j] && (unsigned)(pih[j] + r) < (unsigned)p.H && (unsigned)(piw[j] + s) < (unsigned)p.W;
-          if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + uoff) << 5) + lk);
+          const long off = ((long)(pb[j] + uoff) << 5) + lk;
+          if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) b[j] = *reinterpret_cast<const bf16x8*>(X + off);
           else b[j] = bf16x8{};
         }
       }
@@ -162,7 +174,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
       for (int j = 0; j < FP; ++j) {
         const int ih = pih[j] + r, iw = piw[j] + s;
         const bool v = kval && pval[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        if (v) b[j] = *reinterpret_cast<const bf16x8*>(X + ((long)(pb[j] + ih * p.W + iw)) * C + c);
+        const long off = ((long)(pb[j] + ih * p.W + iw)) * C + c;
+        if (v && HZ_DCHECK(off + 8 <= xlim)) b[j] = *reinterpret_cast<const bf16x8*>(X + off);
         else b[j] = bf16x8{};
       }
     }
@@ -204,6 +217,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
       const int hw = m - ni * PQ;
       o = (((long)ni * (p.Cout >> 5) + (n >> 5)) * PQ + hw) * 32 + (n & 31);
     }
+    if (!HZ_DCHECK(o >= 0 && o + 4 <= olim)) return;
     if (p.res) {
       const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
       v[0] += __uint_as_float(rr[0] << 16);

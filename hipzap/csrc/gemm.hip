@@ -23,6 +23,8 @@
 #include "common.h"
 #include "hipzap.h"
 
+HZ_DEBUG_UNIT(gemm)
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -65,6 +67,13 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
     xsrc[i] = p.x + (long)row * p.ldx + chunk * 8;
   }
   const bf16_t* wsrc = p.w + ((long)(n0 >> 4) * p.ksteps * 64 + lane) * 8;
+  // debug contracts: the tile's weight rows exist in the 128-row padded packing, and the last
+  // staged activation line lies inside [M][ldx] (the DMA cannot be skipped, so a violation
+  // re-points the sources at the tensor bases instead)
+  if (!HZ_DCHECK(n0 + BN <= ((p.Cout + 127) / 128) * 128)) wsrc = p.w + lane * 8;
+#pragma unroll
+  for (int i = 0; i < XPW; ++i)
+    if (!HZ_DCHECK(xsrc[i] - p.x + (long)(nst - 1) * 64 + 8 <= (long)p.M * p.ldx)) xsrc[i] = p.x;
   auto stage = [&](int buf, int st) {
     char* base = smem + buf * SBYTES;
 #pragma unroll
@@ -133,6 +142,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
         for (int e = 0; e < 4; ++e) v[e] += bb[e];
       }
       const long o = (long)m * p.ldo + n;
+      if (!HZ_DCHECK(o + 4 <= (long)(p.M - 1) * p.ldo + p.Cout)) continue;
       if (p.res) {
         const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
         v[0] += __uint_as_float(rr[0] << 16);

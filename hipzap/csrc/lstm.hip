@@ -18,6 +18,8 @@
 #include "common.h"
 #include "hipzap.h"
 
+HZ_DEBUG_UNIT(lstm)
+
 namespace {
 
 constexpr int CHUNK = 8;  // bf16 per 16-B lane load
@@ -36,6 +38,7 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   const int par = t & 1;
   const float* h_prev = p.h_state + par * p.H;
   const int tok = p.emb ? p.tok_seq[t] : 0;
+  if (!HZ_DCHECK(tok >= 0 && p.In + p.H <= p.ldk && p.ldk == NCH * 512)) return;
   const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
   const float* xprev = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
   // weights do not depend on the input vector: issue them first so their latency overlaps
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   const int t = *p.step;
   const int par = t & 1;
   const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
+  if (!HZ_DCHECK(p.H <= p.ldk && p.rpb % DROWS == 0)) return;
   for (int i = tid; i < p.ldk; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
   __syncthreads();
   const unsigned long long seed = p.keys ? *p.seed : 0ull;

@@ -11,6 +11,8 @@
 #include "common.h"
 #include "hipzap.h"
 
+HZ_DEBUG_UNIT(transformer)
+
 namespace {
 
 // --------------------------------------------------------------------------- LayerNorm
@@ -19,6 +21,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams 
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.rows) return;
+  if (!HZ_DCHECK(p.D <= 4 * 64 * 8 && p.ldx >= p.D && (!p.res || p.ldr >= p.D))) return;
   const bf16_t* x = p.x + (long)row * p.ldx;
   const bf16_t* r = p.res ? p.res + (long)row * p.ldr : nullptr;
   const int nch = p.D >> 3;
@@ -190,6 +193,11 @@ __global__ __launch_bounds__(64 * NW) void attention_kernel(const HzAttentionPar
   const bf16_t* Q = p.qkv + row0 * p.ldqkv + h * ATT_D;
   const bf16_t* K = Q + p.k_off;
   const bf16_t* V = Q + p.v_off;
+  // debug contracts (uniform per block, before any barrier): the head's Q/K/V columns and its
+  // output columns lie inside their rows, and the sequence fits the LDS staging
+  if (!HZ_DCHECK(b < p.B && p.L <= ATT_LMAX && h * ATT_D + max(0, max(p.k_off, p.v_off)) + ATT_D <= p.ldqkv &&
+                 h * ATT_D + ATT_D <= p.ldo))
+    return;
   // ---- stage K, V (row-major) and the mask: every load issued first ----
   constexpr int SIT = ATT_LMAX * 8 / (64 * NW);
   u32x4 kv[SIT], vv[SIT];

@@ -4,6 +4,8 @@
 #include "common.h"
 #include "hipzap.h"
 
+HZ_DEBUG_UNIT(vision)
+
 namespace {
 
 // K x K window. With K known at compile time (the ResNet 3x3/2 stem pool) every tap is loaded
@@ -27,6 +29,7 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const HzPoolParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
   const int h0 = pp * p.stride - p.pad, w0 = q * p.stride - p.pad;
+  if (!HZ_DCHECK(h0 < p.H && w0 < p.W && h0 + p.k > 0 && w0 + p.k > 0)) return;  // window overlaps the image
   if constexpr (K > 0) {
     u32x4 v[K * K];
 #pragma unroll
@@ -118,6 +121,7 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   const float inv = 1.f / p.HW;
   const int ks = p.C >> 5;
   const bf16_t* wg = p.w + ((long)g * ks * 64 + lane) * 8;
+  if (!HZ_DCHECK(p.ldo >= p.N && p.C % 32 == 0)) return;
   // first batch of weight fragments: independent of the pooling, so in flight with it
   u32x4 wv[WB];
 #pragma unroll

@@ -14,6 +14,7 @@ import time
 
 import torch
 
+from .. import _native
 from ..models import registry
 from .program import ExecContext, bench_contexts
 
@@ -160,6 +161,9 @@ class Engine:
                     d.copy_(xi.reshape(d.shape), non_blocking=True)
                 ctx.replay(s)
                 out = ctx.output.to("cpu", non_blocking=False)
+        if _native.DEBUG:  # debug kernel variant: surface any failed device-side contract check
+            from ..utils import kcheck
+            kcheck.check(f"{self.model} infer")
         return self._post(out)
 
     def _post(self, out):
