@@ -32,7 +32,15 @@ class ConvParams(C.Structure):
         ("act", c_int), ("out_f32", c_int), ("out_rowmajor", c_int), ("ldo", c_int),
         ("x_rowmajor", c_int), ("ldx", c_int),
         ("tiles_n", c_int), ("kw", c_int),
+        ("lnf", c_void_p),  # const HzLnFold* (device memory) or NULL
     ]
+
+
+class LnFold(C.Structure):
+    """Mirror of HzLnFold (csrc/hipzap.h); copied to device memory, pointed to by ConvParams.lnf."""
+    _fields_ = [("stats_in", c_void_p), ("c1", c_void_p), ("res_stats", c_void_p), ("res_gamma", c_void_p),
+                ("res_beta", c_void_p), ("stats_out", c_void_p), ("nslab_in", c_int), ("nslab_res", c_int),
+                ("ld_stats", c_int), ("inv_d", C.c_float), ("eps_in", C.c_float), ("eps_res", C.c_float)]
 
 
 class PoolParams(C.Structure):

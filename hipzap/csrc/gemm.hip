@@ -38,6 +38,19 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// mean / rstd of row m from the producer's (sum, sumsq) slabs (HzLnFold)
+__device__ __forceinline__ void row_stats(const float* st, int nslab, int ld, int m, float inv_d, float eps,
+                                          float& mu, float& rs) {
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < nslab; ++s) {
+    const float2 t = *reinterpret_cast<const float2*>(st + 2 * ((long)s * ld + m));
+    a += t.x;
+    b += t.y;
+  }
+  mu = a * inv_d;
+  rs = rsqrtf(fmaxf(b * inv_d - mu * mu, 0.f) + eps);
+}
+
 template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;  // 16x16 fragments per wave (2x2 waves)
@@ -126,29 +139,47 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   }
 
   // ---- fused epilogue (row-major out) ----
+  // Optional folded LayerNorm (HzLnFold, hipzap.h): input-side correction rstd*(acc - mean*c1),
+  // normalised residual, and per-row (sum, sumsq) partials of the stored bf16 output.
+  const HzLnFold* __restrict__ lf = p.lnf;
+  const bool f_in = lf && lf->stats_in, f_res = lf && lf->res_stats, f_out = lf && lf->stats_out;
   const int lrow = lane & 15;
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
     const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
-    if (m >= p.M) continue;
+    const bool mval = m < p.M;
+    float mu_in = 0.f, rs_in = 1.f, mu_r = 0.f, rs_r = 1.f;
+    if (f_in && mval) row_stats(lf->stats_in, lf->nslab_in, lf->ld_stats, m, lf->inv_d, lf->eps_in, mu_in, rs_in);
+    if (f_res && mval) row_stats(lf->res_stats, lf->nslab_res, lf->ld_stats, m, lf->inv_d, lf->eps_res, mu_r, rs_r);
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
       const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
-      if (n >= p.Cout) continue;
+      const long o = (long)m * p.ldo + n;
+      if (!mval || n >= p.Cout || !HZ_DCHECK(o + 4 <= (long)(p.M - 1) * p.ldo + p.Cout)) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (f_in) {
+        const f32x4 c = *reinterpret_cast<const f32x4*>(lf->c1 + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = rs_in * (v[e] - mu_in * c[e]);
+      }
       if (p.bias) {
         const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += bb[e];
       }
-      const long o = (long)m * p.ldo + n;
-      if (!HZ_DCHECK(o + 4 <= (long)(p.M - 1) * p.ldo + p.Cout)) continue;
       if (p.res) {
         const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
-        v[0] += __uint_as_float(rr[0] << 16);
-        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-        v[2] += __uint_as_float(rr[1] << 16);
-        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+        float r[4] = {__uint_as_float(rr[0] << 16), __uint_as_float(rr[0] & 0xffff0000u),
+                      __uint_as_float(rr[1] << 16), __uint_as_float(rr[1] & 0xffff0000u)};
+        if (f_res) {
+          const f32x4 gg = *reinterpret_cast<const f32x4*>(lf->res_gamma + n);
+          const f32x4 bt = *reinterpret_cast<const f32x4*>(lf->res_beta + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] = (r[e] - mu_r) * rs_r * gg[e] + bt[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += r[e];
       }
       if (p.act == HZ_ACT_RELU) {
 #pragma unroll
@@ -160,8 +191,27 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
       }
-      if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
-      else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      if (p.out_f32) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+        const u32x2 q = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = q;
+        if (f_out) {  // statistics of exactly what the consumers will read (bf16-rounded)
+          const float a0 = __uint_as_float(q[0] << 16), a1 = __uint_as_float(q[0] & 0xffff0000u);
+          const float a2 = __uint_as_float(q[1] << 16), a3 = __uint_as_float(q[1] & 0xffff0000u);
+          s1 += (a0 + a1) + (a2 + a3);
+          s2 += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+        }
+      }
+    }
+    if (f_out) {  // wave-uniform: every lane reaches the shuffles. Lanes l, l^16, l^32, l^48 share row m.
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      const long so = 2 * ((long)(tile_n * 2 + wn) * lf->ld_stats + m);
+      if (lane < 16 && mval && HZ_DCHECK(m < lf->ld_stats))
+        *reinterpret_cast<float2*>(lf->stats_out + so) = make_float2(s1, s2);
     }
   }
 }

@@ -23,7 +23,26 @@ typedef struct HzConvParams {
   int x_rowmajor, ldx;        // GEMM mode: activations row-major [M][ldx] (M = N*H*W, 1x1 only)
   int tiles_n;               // filled by the launcher
   int kw;                    // waves per workgroup splitting K
+  const struct HzLnFold* lnf; // LDS GEMM only: LayerNorm folded into this GEMM (device memory), or NULL
 } HzConvParams;
+
+// Post-LN transformer LayerNorm folded into the neighbouring GEMMs (gemm.hip, BERT). A GEMM
+// whose input is LN(y) runs on the raw y with gamma folded into its weights (W' = W diag(gamma),
+// c1[n] = sum_k W'[n][k], bias' = bias + W beta) and corrects in the epilogue:
+//   out = rstd * (y.W'^T - mean * c1) + bias'
+// A GEMM whose residual is LN(y) normalises the residual elementwise. The producing GEMM writes
+// per-row partial (sum, sumsq) of its bf16-rounded output, one float2 slab per (N tile, wave
+// column): deterministic, no atomics; consumers sum the slabs of a row.
+typedef struct HzLnFold {
+  const float* stats_in;   // [nslab_in][ld_stats] float2 of the GEMM input rows, or NULL
+  const float* c1;         // [Cout] (with stats_in)
+  const float* res_stats;  // [nslab_res][ld_stats] float2 of the residual rows, or NULL
+  const float* res_gamma;  // [Cout] (with res_stats)
+  const float* res_beta;
+  float* stats_out;        // [2 * tiles_n][ld_stats] float2 of this GEMM's output rows, or NULL
+  int nslab_in, nslab_res, ld_stats;
+  float inv_d, eps_in, eps_res;  // inv_d = 1 / LayerNorm width
+} HzLnFold;
 
 // cfg 0..8: register-ring tile (FC*16 channels x FP*16 pixels), cfg = log2(FC)*3 + log2(FP);
 // cfg 16..19: LDS-tiled GEMM (gemm.hip; row-major activations, K % 64 == 0, weight rows % 128 == 0)

@@ -41,6 +41,11 @@ def conv_pairs(g: Graph) -> dict:
     return out
 
 
+def _ln_folded(n) -> bool:
+    a = n.attrs
+    return n.kind == "gemm" and bool(a.get("ln_in") or a.get("res_ln") or a.get("stats_out") is not None)
+
+
 class ExecContext:
     def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
                  host_io: bool = False, pair_convs: bool | None = None, zero_copy: str | None = None):
@@ -48,6 +53,7 @@ class ExecContext:
         self.device = torch.device(device)
         self.params = params
         self._keep: list = []
+        self._nslab: dict[int, int] = {}  # stats tensor -> slabs written by its producer (HzLnFold)
         lib = N.lib()
         offsets, arena_bytes = plan_memory(g)
         self.arena_bytes = arena_bytes
@@ -94,6 +100,10 @@ class ExecContext:
                 cfg, kw = fp8.choose_config_fp8(M, pc, tuned, key, mx_io=mx_io)
             else:
                 cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=pc)
+            if _ln_folded(n) and cfg not in conv_ops.LDS_TILES:  # HzLnFold lives in the LDS GEMM epilogue
+                if not conv_ops.lds_ok(M, pc.K, True, pc):
+                    raise ValueError(f"{n.attrs.get('name')}: folded LayerNorm needs the LDS GEMM (M={M} < 64?)")
+                cfg, kw = 19, 1
             conv_plans.append((cfg, kw, key))
         # host_io: the request's PCIe transfers are part of the program (and of the graph):
         # pinned host inputs -> device inputs ... device output -> pinned host output.
@@ -156,6 +166,33 @@ class ExecContext:
         self.configs.append((a.attrs.get("name", "") + "+" + b.attrs.get("name", ""), key, cfg, kw))
         N.check(lib.hz_prog_add_conv2(self.prog, C.byref(pa), C.byref(pb), cfg, a.slot), "add_conv2")
 
+    def _ln_fold(self, n, pc, cfg: int, M: int) -> int:
+        """Device copy of this GEMM's HzLnFold (csrc/hipzap.h); returns its address. Producers run
+        before their consumers, so each stats tensor's slab count is known when it is read."""
+        g, a = self.graph, n.attrs
+        f = N.LnFold()
+        if a.get("ln_in"):
+            pname, st = a["ln_in"]
+            f.stats_in, f.c1 = self._addr(st), self.params[a["w"] + ".c1"].data_ptr()
+            f.nslab_in, f.eps_in = self._nslab[st], self.params[pname].eps
+            f.ld_stats, f.inv_d = g.shape(st)[1], 1.0 / pc.K
+        if a.get("res_ln"):
+            pname, st = a["res_ln"]
+            npar = self.params[pname]
+            f.res_stats, f.res_gamma, f.res_beta = self._addr(st), npar.gamma.data_ptr(), npar.beta.data_ptr()
+            f.nslab_res, f.eps_res = self._nslab[st], npar.eps
+            f.ld_stats, f.inv_d = g.shape(st)[1], 1.0 / pc.cout
+        if a.get("stats_out") is not None:
+            st = a["stats_out"]
+            bn = conv_ops.LDS_TILES[cfg][1]
+            self._nslab[st] = 2 * ((pc.cout + bn - 1) // bn)
+            assert self._nslab[st] <= g.shape(st)[0] and g.shape(st)[1] == M
+            f.stats_out, f.ld_stats, f.inv_d = self._addr(st), M, 1.0 / pc.cout
+        assert f.ld_stats == M, "stats slabs are indexed by this GEMM's rows"
+        buf = torch.frombuffer(bytearray(bytes(f)), dtype=torch.uint8).to(self.device)
+        self._keep.append(buf)
+        return buf.data_ptr()
+
     def _conv_flops(self, n) -> int:
         pc = self.params[n.attrs["w"]]
         nb, p, q, _ = self.graph.shape(n.outputs[0])
@@ -205,12 +242,14 @@ class ExecContext:
             pc = self.params[n.attrs["w"]]
             cfg, kw, key = plan
             M = n.attrs["rows"]
-            res = n.inputs[1] if len(n.inputs) > 1 else None
+            res = n.inputs[1] if n.attrs.get("has_res", len(n.inputs) > 1) else None
             out_spec = g.tensors[n.outputs[0]]
             ldx = n.attrs.get("ldx") or g.shape(n.inputs[0])[-1]
             prm, _, _ = conv_ops.make_params(addr(n.inputs[0]), pc, M, 1, 1, addr(n.outputs[0]), addr(res),
                                              n.attrs.get("act", "none"), n.attrs.get("out_f32", False), cfg, kw,
                                              out_rowmajor=True, ldo=out_spec.shape[-1], x_rowmajor=True, ldx=ldx)
+            if _ln_folded(n):
+                prm.lnf = self._ln_fold(n, pc, cfg, M)
             self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
             N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_gemm")
         elif n.kind == "quant":

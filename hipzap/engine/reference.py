@@ -73,12 +73,25 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             rows, ldx = n.attrs["rows"], n.attrs.get("ldx") or g.shape(n.inputs[0])[-1]
             xm = torch.stack([x[r * ldx: r * ldx + pc.K] for r in range(rows)])
             w = pc.dense() if not hasattr(pc, "dequant") else pc.dequant()
-            y = xm @ w.t() + pc.bias.float()
-            if len(n.inputs) > 1:
-                y = y + vals[n.inputs[1]].float().reshape(rows, -1)
-            act = n.attrs.get("act", "none")
+            a = n.attrs
+            y = xm @ w.t()
+            if a.get("ln_in"):  # folded LayerNorm of the raw input (stats taken from the input itself)
+                eps = params[a["ln_in"][0]].eps
+                mu, var = xm.mean(1, keepdim=True), xm.var(1, unbiased=False, keepdim=True)
+                y = torch.rsqrt(var + eps) * (y - mu * params[a["w"] + ".c1"].float()[None, :])
+            y = y + pc.bias.float()
+            if a.get("has_res", len(n.inputs) > 1):
+                r = vals[n.inputs[1]].float().reshape(rows, -1)
+                if a.get("res_ln"):
+                    npar = params[a["res_ln"][0]]
+                    r = F.layer_norm(r, (r.shape[-1],), npar.gamma.float(), npar.beta.float(), npar.eps)
+                y = y + r
+            act = a.get("act", "none")
             y = torch.relu(y) if act == "relu" else F.gelu(y) if act == "gelu" else torch.tanh(y) if act == "tanh" else y
-            if len(n.outputs) == 2:  # MX8 output
+            if a.get("stats_out") is not None:  # the oracle's consumers recompute statistics themselves
+                store(n.outputs[0], y)
+                vals[a["stats_out"]] = torch.zeros(g.shape(a["stats_out"]))
+            elif len(n.outputs) == 2:  # MX8 output
                 from ..ops.fp8 import quant_mx_ref
                 vals[n.outputs[0]], vals[n.outputs[1]] = quant_mx_ref(y)
             else:

@@ -25,6 +25,15 @@ def pack_qkv(q_w, q_b, k_w, k_b, v_w, v_b):
     return pack_linear_padded(torch.cat([q_w, k_w, v_w]), torch.cat([q_b, k_b, v_b]))
 
 
+def fold_ln_linear(weight: torch.Tensor, bias: torch.Tensor, ln: NormParams):
+    """Linear whose input is LayerNorm(y), folded to run on the raw y (HzLnFold, csrc/hipzap.h):
+    W' = W diag(gamma), bias' = bias + W beta, c1[n] = sum_k W'[n][k] of the bf16-packed W' (so
+    the epilogue's mean * c1 cancels exactly what the MFMA accumulated). -> (packed W', c1)."""
+    w = weight.detach().float()
+    pc = pack_linear_padded(w * ln.gamma.float()[None, :], bias.detach().float() + w @ ln.beta.float())
+    return pc, pc.dense().sum(1).contiguous()
+
+
 def norm(sd, prefix, eps):
     return NormParams(sd[f"{prefix}.weight"].float().contiguous(), sd[f"{prefix}.bias"].float().contiguous(), eps)
 
@@ -36,13 +45,30 @@ class TxBuilder:
         self.g = g
 
     def gemm(self, x, w: str, cols: int, act="none", res=None, rows=None, ldx=None, out_f32=False, ext=False,
-             name=None):
+             name=None, ln_in=None, res_ln=None, stats_out=False):
+        """``ln_in`` / ``res_ln`` = (LayerNorm param, stats tensor): the input / residual is the raw
+        pre-LN sum and the LayerNorm is folded into this GEMM (``w`` packed by fold_ln_linear, its
+        ``c1`` at ``w + ".c1"``). ``stats_out``: also emit the per-row (sum, sumsq) slabs of the
+        output for folded consumers; returns (out, stats)."""
         g = self.g
         r = rows if rows is not None else g.shape(x)[0]
         out = g.tensor((r, cols), torch.float32 if out_f32 else torch.bfloat16, name or w, external=ext)
         ins = [x] if res is None else [x, res]
-        g.add("gemm", ins, [out], w=w, act=act, rows=r, ldx=ldx, out_f32=out_f32, name=name or w)
-        return out
+        attrs = dict(w=w, act=act, rows=r, ldx=ldx, out_f32=out_f32, name=name or w, has_res=res is not None)
+        outs = [out]
+        if ln_in is not None:
+            attrs["ln_in"] = ln_in
+            ins.append(ln_in[1])
+        if res_ln is not None:
+            assert res is not None
+            attrs["res_ln"] = res_ln
+            ins.append(res_ln[1])
+        if stats_out:  # slabs for the smallest N tile (64 columns, 2 wave columns each): [2*ceil(cols/64), r, 2]
+            st = g.tensor((2 * ((cols + 63) // 64), r, 2), torch.float32, f"{name or w}.stats")
+            attrs["stats_out"] = st
+            outs.append(st)
+        g.add("gemm", ins, outs, **attrs)
+        return (out, outs[1]) if stats_out else out
 
     def gemm8(self, x, w: str, cols: int, act="none", res=None, out_f32=False, ext=False, name=None):
         """fp8 GEMM: per-row dynamic quantisation of ``x`` then the fp8 MFMA GEMM."""

@@ -15,11 +15,18 @@ Linear/LayerNorm/Softmax HIP path. Not in the reference (SURVEY.md §2e N4, N6-N
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..engine.graph import Graph
 from ..ops.transformer import EmbedTables
-from ._tx import TxBuilder, norm, pack_linear_padded, pack_qkv
+from ._tx import TxBuilder, fold_ln_linear, norm, pack_linear_padded, pack_qkv
+
+
+def ln_fold_default() -> bool:
+    """HIPZAP_LN_FOLD=0 keeps the 24 standalone LayerNorm kernels (A/B switch)."""
+    return os.environ.get("HIPZAP_LN_FOLD", "1") != "0"
 
 
 def make_model(num_labels: int = 2, **cfg):
@@ -39,9 +46,12 @@ def config_from_sd(sd: dict) -> dict:
             "max_pos": sd["bert.embeddings.position_embeddings.weight"].shape[0]}
 
 
-def pack_bert(sd: dict, device="cpu", eps: float = 1e-12) -> tuple[dict, dict]:
+def pack_bert(sd: dict, device="cpu", eps: float = 1e-12, ln_fold: bool | None = None) -> tuple[dict, dict]:
+    """``ln_fold``: fold every encoder LayerNorm into its consumer GEMMs (see build_graph); the
+    returned cfg records the choice so the graph is built to match the packed weights."""
     sd = {k: v.to(device) for k, v in sd.items()}
     cfg = config_from_sd(sd)
+    cfg["ln_fold"] = ln_fold_default() if ln_fold is None else bool(ln_fold)
     P = {
         "emb": EmbedTables(sd["bert.embeddings.word_embeddings.weight"].to(torch.bfloat16).contiguous(),
                            sd["bert.embeddings.position_embeddings.weight"].to(torch.bfloat16).contiguous(),
@@ -51,12 +61,22 @@ def pack_bert(sd: dict, device="cpu", eps: float = 1e-12) -> tuple[dict, dict]:
     for i in range(cfg["layers"]):
         pre = f"bert.encoder.layer.{i}"
         a = f"{pre}.attention.self"
-        P[f"l{i}.qkv"] = pack_qkv(sd[f"{a}.query.weight"], sd[f"{a}.query.bias"], sd[f"{a}.key.weight"],
-                                  sd[f"{a}.key.bias"], sd[f"{a}.value.weight"], sd[f"{a}.value.bias"])
+        if cfg["ln_fold"] and i > 0:  # input = raw sum of layer i-1, normalised by its ln2
+            P[f"l{i}.qkv"], P[f"l{i}.qkv.c1"] = fold_ln_linear(
+                torch.cat([sd[f"{a}.query.weight"], sd[f"{a}.key.weight"], sd[f"{a}.value.weight"]]),
+                torch.cat([sd[f"{a}.query.bias"], sd[f"{a}.key.bias"], sd[f"{a}.value.bias"]]), P[f"l{i - 1}.ln2"])
+        else:
+            P[f"l{i}.qkv"] = pack_qkv(sd[f"{a}.query.weight"], sd[f"{a}.query.bias"], sd[f"{a}.key.weight"],
+                                      sd[f"{a}.key.bias"], sd[f"{a}.value.weight"], sd[f"{a}.value.bias"])
         P[f"l{i}.o"] = pack_linear_padded(sd[f"{pre}.attention.output.dense.weight"],
                                           sd[f"{pre}.attention.output.dense.bias"])
         P[f"l{i}.ln1"] = norm(sd, f"{pre}.attention.output.LayerNorm", eps)
-        P[f"l{i}.ffn1"] = pack_linear_padded(sd[f"{pre}.intermediate.dense.weight"], sd[f"{pre}.intermediate.dense.bias"])
+        if cfg["ln_fold"]:
+            P[f"l{i}.ffn1"], P[f"l{i}.ffn1.c1"] = fold_ln_linear(
+                sd[f"{pre}.intermediate.dense.weight"], sd[f"{pre}.intermediate.dense.bias"], P[f"l{i}.ln1"])
+        else:
+            P[f"l{i}.ffn1"] = pack_linear_padded(sd[f"{pre}.intermediate.dense.weight"],
+                                                 sd[f"{pre}.intermediate.dense.bias"])
         P[f"l{i}.ffn2"] = pack_linear_padded(sd[f"{pre}.output.dense.weight"], sd[f"{pre}.output.dense.bias"])
         P[f"l{i}.ln2"] = norm(sd, f"{pre}.output.LayerNorm", eps)
     P["pooler"] = pack_linear_padded(sd["bert.pooler.dense.weight"], sd["bert.pooler.dense.bias"])
@@ -65,7 +85,12 @@ def pack_bert(sd: dict, device="cpu", eps: float = 1e-12) -> tuple[dict, dict]:
 
 
 def build_graph(batch: int, seq_len: int = 128, layers: int = 12, hidden: int = 768, heads: int = 12,
-                ffn: int = 3072, num_labels: int = 2, **_) -> Graph:
+                ffn: int = 3072, num_labels: int = 2, ln_fold: bool = False, **_) -> Graph:
+    """``ln_fold`` (must match pack_bert's cfg): no standalone encoder LayerNorm. The O-proj and
+    FFN2 GEMMs emit per-row (sum, sumsq) slabs of their raw output y; FFN1 and the next layer's
+    QKV run on y with gamma/beta folded into their weights and normalise in the epilogue; the
+    residual reads of y are normalised in the epilogue too (HzLnFold, csrc/hipzap.h). Only the
+    B CLS rows get a real LayerNorm, for the pooler. 5 kernels per layer instead of 7."""
     B, L, D = batch, seq_len, hidden
     T = B * L
     g = Graph(f"bert_bs{B}_L{L}")
@@ -76,15 +101,26 @@ def build_graph(batch: int, seq_len: int = 128, layers: int = 12, hidden: int = 
     tb = TxBuilder(g)
     x = g.tensor((T, D), torch.bfloat16, "emb")
     g.add("embed_ln", [ids, types], [x], emb="emb", ln="emb_ln", L=L)
+    ln_x = None  # (LayerNorm param, stats) while x is a raw pre-LN sum (ln_fold)
     for i in range(layers):
-        qkv = tb.gemm(x, f"l{i}.qkv", 3 * D)
+        qkv = tb.gemm(x, f"l{i}.qkv", 3 * D, ln_in=ln_x)
         ctx = tb.attention(qkv, B, L, heads, mask)
+        if ln_fold:
+            y, s1 = tb.gemm(ctx, f"l{i}.o", D, res=x, res_ln=ln_x, stats_out=True)
+            h = tb.gemm(y, f"l{i}.ffn1", ffn, act="gelu", ln_in=(f"l{i}.ln1", s1))
+            x, s2 = tb.gemm(h, f"l{i}.ffn2", D, res=y, res_ln=(f"l{i}.ln1", s1), stats_out=True)
+            ln_x = (f"l{i}.ln2", s2)
+            continue
         y = tb.gemm(ctx, f"l{i}.o", D, res=x)
         x1 = tb.layernorm(y, f"l{i}.ln1")
         h = tb.gemm(x1, f"l{i}.ffn1", ffn, act="gelu")
         y2 = tb.gemm(h, f"l{i}.ffn2", D, res=x1)
         x = tb.layernorm(y2, f"l{i}.ln2")
-    pooled = tb.gemm(x, "pooler", D, act="tanh", rows=B, ldx=L * D)
+    if ln_x is not None:  # the pooler reads only the CLS rows: normalise just those B rows
+        xc = tb.layernorm(x, ln_x[0], rows=B, ldx=L * D, name="cls_ln")
+        pooled = tb.gemm(xc, "pooler", D, act="tanh", rows=B)
+    else:
+        pooled = tb.gemm(x, "pooler", D, act="tanh", rows=B, ldx=L * D)
     npad = (num_labels + 3) // 4 * 4
     logits = tb.gemm(pooled, "cls", npad, out_f32=True, ext=True)
     g.outputs.append(logits)

@@ -9,15 +9,22 @@ from hipzap.models import bert, registry, vit
 
 def _small_bert():
     torch.manual_seed(0)
-    return bert.make_model(num_labels=3, num_hidden_layers=2, vocab_size=500, max_position_embeddings=64)
+    m = bert.make_model(num_labels=3, num_hidden_layers=2, vocab_size=500, max_position_embeddings=64)
+    with torch.no_grad():  # non-trivial LayerNorm affine params (HF init is gamma=1, beta=0)
+        for name, p in m.named_parameters():
+            if "LayerNorm" in name:
+                p.add_(0.3 * torch.randn_like(p))
+    return m
 
 
-def test_bert_graph_oracle_matches_hf():
+@pytest.mark.parametrize("ln_fold", [True, False])
+def test_bert_graph_oracle_matches_hf(ln_fold):
     m = _small_bert()
-    P, cfg = bert.pack_bert(m.state_dict())
-    assert cfg["layers"] == 2 and cfg["num_labels"] == 3
+    P, cfg = bert.pack_bert(m.state_dict(), ln_fold=ln_fold)
+    assert cfg["layers"] == 2 and cfg["num_labels"] == 3 and cfg["ln_fold"] == ln_fold
     B, L = 2, 16
-    g = bert.build_graph(B, L, layers=2, num_labels=3)
+    g = bert.build_graph(B, L, layers=2, num_labels=3, ln_fold=ln_fold)
+    assert [n.kind for n in g.nodes].count("layernorm") == (1 if ln_fold else 4)
     ids = torch.randint(0, 500, (B, L))
     tt = torch.randint(0, 2, (B, L))
     am = torch.ones(B, L, dtype=torch.long)
@@ -38,7 +45,9 @@ def test_bert_base_shapes_meta():
     assert meta["l0.qkv"].cout == 2304 and meta["cls"].cout == 4  # 2 labels padded to 4
     g = a.build_graph(batch=16, **cfg)
     kinds = [n.kind for n in g.nodes]
-    assert kinds.count("gemm") == 12 * 4 + 2 and kinds.count("attention") == 12 and kinds.count("layernorm") == 24
+    # LayerNorms folded into the GEMMs (cfg["ln_fold"], default): only the CLS-row LN for the pooler
+    nln = 1 if cfg["ln_fold"] else 24
+    assert kinds.count("gemm") == 12 * 4 + 2 and kinds.count("attention") == 12 and kinds.count("layernorm") == nln
 
 
 @pytest.mark.parametrize("legacy_keys", [False, True])

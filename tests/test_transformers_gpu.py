@@ -74,9 +74,17 @@ def test_lds_gemm(cfg, M, N, K, act, res):
     assert _rel(y, ref) < 2e-2
 
 
-def test_bert_engine_matches_hf():
+@pytest.mark.parametrize("ln_fold", ["1", "0"])
+def test_bert_engine_matches_hf(ln_fold, monkeypatch):
+    """ln_fold=1: LayerNorms folded into the LDS GEMM epilogues (HzLnFold); LayerNorm affine
+    params randomised so a wrong fold cannot hide behind gamma=1, beta=0."""
+    monkeypatch.setenv("HIPZAP_LN_FOLD", ln_fold)
     torch.manual_seed(0)
     m = bert.make_model(num_labels=2)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if "LayerNorm" in name:
+                p.add_(0.3 * torch.randn_like(p))
     sd = m.state_dict()
     B, L = 4, 128
     eng = Engine.from_state_dict("bert-base", sd, DEV, batch=B)
