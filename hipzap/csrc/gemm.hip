@@ -38,20 +38,45 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// mean / rstd of row m from the producer's (sum, sumsq) slabs (HzLnFold)
-__device__ __forceinline__ void row_stats(const float* st, int nslab, int ld, int m, float inv_d, float eps,
-                                          float& mu, float& rs) {
-  float a = 0.f, b = 0.f;
-  for (int s = 0; s < nslab; ++s) {
-    const float2 t = *reinterpret_cast<const float2*>(st + 2 * ((long)s * ld + m));
-    a += t.x;
-    b += t.y;
+// mean / rstd of this lane's FPW rows (m = mbase + 16 j) from a producer's (sum, sumsq) slabs
+// (HzLnFold). The 4 lane groups sharing a row split the slabs (group g: slabs g, g+4, ...), every
+// load is unconditional (clamped slab / row, zero weight) so all of them are in flight at once —
+// one memory latency per tile instead of a serial chain — then an xor-shuffle combines the groups.
+// Wave-uniform call (shuffles). nslab <= 4 * HZ_LNF_MAXT (checked by the host).
+#define HZ_LNF_MAXT 6
+template <int FPW>
+__device__ __forceinline__ void rows_stats(const float* __restrict__ st, int nslab, int ld, int mbase, int M,
+                                           float inv_d, float eps, float (&mu)[FPW], float (&rs)[FPW]) {
+  const int g = (threadIdx.x & 63) >> 4;
+  float a[FPW], b[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) a[j] = b[j] = 0.f;
+#pragma unroll
+  for (int t = 0; t < HZ_LNF_MAXT; ++t) {
+    const int s = g + 4 * t;
+    const float w = s < nslab ? 1.f : 0.f;
+    const long sb = (long)min(s, nslab - 1) * ld;
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const float2 v = *reinterpret_cast<const float2*>(st + 2 * (sb + min(mbase + 16 * j, M - 1)));
+      a[j] += w * v.x;
+      b[j] += w * v.y;
+    }
   }
-  mu = a * inv_d;
-  rs = rsqrtf(fmaxf(b * inv_d - mu * mu, 0.f) + eps);
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    a[j] += __shfl_xor(a[j], 16);
+    b[j] += __shfl_xor(b[j], 16);
+    a[j] += __shfl_xor(a[j], 32);
+    b[j] += __shfl_xor(b[j], 32);
+    mu[j] = a[j] * inv_d;
+    rs[j] = rsqrtf(fmaxf(b[j] * inv_d - mu[j] * mu[j], 0.f) + eps);
+  }
 }
 
-template <int BM, int BN, int NS>
+// LNF: folded-LayerNorm variant (p.lnf != NULL); a separate instantiation so the plain GEMM keeps
+// its register budget (the fold's statistics cost ~60 VGPRs, which halves occupancy)
+template <int BM, int BN, int NS, bool LNF>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   constexpr int FCW = BN / 32, FPW = BM / 32;  // 16x16 fragments per wave (2x2 waves)
   constexpr int NWG = BN / 16;                 // weight fragments per 32-deep k-step
@@ -113,6 +138,18 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
 
   stage(0, 0);
   if (NS > 2 && nst > 1) stage(1, 1);
+  // folded LayerNorm: row statistics of the producer are complete at kernel start; their loads
+  // go out behind the first stages' DMA, so the wait overlaps the first K step's
+  const HzLnFold* __restrict__ lf = LNF ? p.lnf : nullptr;
+  const bool f_in = LNF && lf->stats_in, f_res = LNF && lf->res_stats, f_out = LNF && lf->stats_out;
+  const int lrow = lane & 15;
+  float mu_in[FPW], rs_in[FPW], mu_r[FPW], rs_r[FPW];
+  if (f_in)
+    rows_stats<FPW>(lf->stats_in, lf->nslab_in, lf->ld_stats, m0 + wm * (BM / 2) + lrow, p.M, lf->inv_d, lf->eps_in,
+                    mu_in, rs_in);
+  if (f_res)
+    rows_stats<FPW>(lf->res_stats, lf->nslab_res, lf->ld_stats, m0 + wm * (BM / 2) + lrow, p.M, lf->inv_d,
+                    lf->eps_res, mu_r, rs_r);
   int cur = 0;
   for (int st = 0; st < nst; ++st) {
     // stages issued ahead of st: min(NS-2, nst-1-st) may stay in flight
@@ -141,16 +178,10 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   // ---- fused epilogue (row-major out) ----
   // Optional folded LayerNorm (HzLnFold, hipzap.h): input-side correction rstd*(acc - mean*c1),
   // normalised residual, and per-row (sum, sumsq) partials of the stored bf16 output.
-  const HzLnFold* __restrict__ lf = p.lnf;
-  const bool f_in = lf && lf->stats_in, f_res = lf && lf->res_stats, f_out = lf && lf->stats_out;
-  const int lrow = lane & 15;
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
     const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
     const bool mval = m < p.M;
-    float mu_in = 0.f, rs_in = 1.f, mu_r = 0.f, rs_r = 1.f;
-    if (f_in && mval) row_stats(lf->stats_in, lf->nslab_in, lf->ld_stats, m, lf->inv_d, lf->eps_in, mu_in, rs_in);
-    if (f_res && mval) row_stats(lf->res_stats, lf->nslab_res, lf->ld_stats, m, lf->inv_d, lf->eps_res, mu_r, rs_r);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
@@ -161,7 +192,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
       if (f_in) {
         const f32x4 c = *reinterpret_cast<const f32x4*>(lf->c1 + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = rs_in * (v[e] - mu_in * c[e]);
+        for (int e = 0; e < 4; ++e) v[e] = rs_in[j] * (v[e] - mu_in[j] * c[e]);
       }
       if (p.bias) {
         const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
@@ -176,7 +207,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
           const f32x4 gg = *reinterpret_cast<const f32x4*>(lf->res_gamma + n);
           const f32x4 bt = *reinterpret_cast<const f32x4*>(lf->res_beta + n);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] = (r[e] - mu_r) * rs_r * gg[e] + bt[e];
+          for (int e = 0; e < 4; ++e) r[e] = (r[e] - mu_r[j]) * rs_r[j] * gg[e] + bt[e];
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += r[e];
@@ -219,7 +250,8 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
 template <int BM, int BN, int NS>
 int launch_lds(const HzConvParams& p, hipStream_t st) {
   const int tiles = ((p.Cout + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS>), dim3(tiles), dim3(256), 0, st, p);
+  if (p.lnf) hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 

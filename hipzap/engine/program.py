@@ -189,6 +189,7 @@ class ExecContext:
             assert self._nslab[st] <= g.shape(st)[0] and g.shape(st)[1] == M
             f.stats_out, f.ld_stats, f.inv_d = self._addr(st), M, 1.0 / pc.cout
         assert f.ld_stats == M, "stats slabs are indexed by this GEMM's rows"
+        assert max(f.nslab_in, f.nslab_res) <= 24, "rows_stats reads at most 4 * HZ_LNF_MAXT slabs (gemm.hip)"
         buf = torch.frombuffer(bytearray(bytes(f)), dtype=torch.uint8).to(self.device)
         self._keep.append(buf)
         return buf.data_ptr()

@@ -25,8 +25,10 @@ from ._tx import TxBuilder, fold_ln_linear, norm, pack_linear_padded, pack_qkv
 
 
 def ln_fold_default() -> bool:
-    """HIPZAP_LN_FOLD=0 keeps the 24 standalone LayerNorm kernels (A/B switch)."""
-    return os.environ.get("HIPZAP_LN_FOLD", "1") != "0"
+    """HIPZAP_LN_FOLD=1 folds the encoder LayerNorms into the GEMMs. Off by default: measured on
+    one MI355X (profiles/r1_ab/bert_lnfold.txt, interleaved A/B) it removes 23 LayerNorm launches
+    but the GEMM epilogues' statistics work costs more (14.3k vs 14.9k seq/s, 1 context; equal at 4)."""
+    return os.environ.get("HIPZAP_LN_FOLD", "0") == "1"
 
 
 def make_model(num_labels: int = 2, **cfg):
