@@ -109,6 +109,9 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__
 // trip instead of one per 8 pixels) but needs 384 VGPRs at HW = 49: one workgroup per CU, which
 // measured -1.5 % at 8 concurrent request streams (profiles/r1_ab/vision_latency.txt), so the
 // runtime loop (NB = 0) is the default (HZ_POOLFC_STATIC).
+#ifndef HZ_POOLFC_PB
+#define HZ_POOLFC_PB 16  // pixel loads in flight per lane in the runtime loop: 4 round trips at HW = 49 (8: 7)
+#endif
 template <int NB>
 __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   extern __shared__ __attribute__((aligned(16))) float pooled[];  // [C] + [4][16] partials
@@ -144,12 +147,13 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
           for (int e = 0; e < 8; ++e) s[e] += wj * f[e];
         }
       } else {
-        for (int hw0 = 0; hw0 < p.HW; hw0 += 8) {  // 8 independent loads in flight per lane
-          u32x4 v[8];
+        for (int hw0 = 0; hw0 < p.HW; hw0 += HZ_POOLFC_PB) {  // PB independent loads in flight per lane
+          u32x4 v[HZ_POOLFC_PB];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const u32x4*>(src + min(hw0 + j, p.HW - 1) * 32);
+          for (int j = 0; j < HZ_POOLFC_PB; ++j)
+            v[j] = *reinterpret_cast<const u32x4*>(src + min(hw0 + j, p.HW - 1) * 32);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
+          for (int j = 0; j < HZ_POOLFC_PB; ++j) {
             float f[8];
             unpack8(v[j], f);
             const float wj = hw0 + j < p.HW ? 1.f : 0.f;
@@ -227,6 +231,52 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const void* __restrict_
   for (int c = 8; c < Cpad; c += 8) *reinterpret_cast<u32x4*>(o + c) = u32x4{0, 0, 0, 0};
 }
 
+// uint8 HWC, 3 channels (the request payload of the vision models), read zero-copy from pinned host
+// memory: the generic kernel's per-thread byte loads at stride 3 make every wave instruction touch the
+// same three 64 B lines again (uncached over PCIe). Here a workgroup owns 1024 pixels = 3072 bytes:
+// three fully coalesced dword loads per thread (768 distinct dwords, each read once), restaged through
+// LDS so thread t then owns bytes [12t, 12t+12) = 4 whole pixels. Needs npix % 4 == 0 and a 4-byte
+// aligned source (checked by the launcher; the generic kernel covers the rest).
+__global__ __launch_bounds__(256) void preprocess_u8c3_kernel(const unsigned* __restrict__ src,
+                                                              bf16_t* __restrict__ dst, long npix, int Cpad,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ inv_std) {
+  __shared__ unsigned buf[768];
+  const int t = threadIdx.x;
+  const long ndw = npix / 4 * 3;
+  const long d0 = (long)blockIdx.x * 768;
+  unsigned r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const long d = d0 + k * 256 + t;
+    r[k] = d < ndw ? src[d] : 0u;
+  }
+  float mu[3] = {0.f, 0.f, 0.f}, is[3] = {1.f, 1.f, 1.f};
+  if (mean) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) mu[c] = mean[c], is[c] = inv_std[c];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) buf[k * 256 + t] = r[k];
+  __syncthreads();
+  const long px = (long)blockIdx.x * 1024 + 4 * t;
+  if (px >= npix) return;
+  const unsigned w[3] = {buf[3 * t], buf[3 * t + 1], buf[3 * t + 2]};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int b = 3 * q + c;  // byte within the thread's 12
+      const float f = (float)((w[b >> 2] >> (8 * (b & 3))) & 0xffu) * (1.0f / 255.0f);
+      v[c] = mean ? (f - mu[c]) * is[c] : f;
+    }
+    bf16_t* o = dst + (px + q) * Cpad;
+    *reinterpret_cast<u32x4*>(o) = pack8(v);
+    for (int c = 8; c < Cpad; c += 8) *reinterpret_cast<u32x4*>(o + c) = u32x4{0, 0, 0, 0};
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i + 3 < n) {
@@ -279,10 +329,18 @@ extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+#ifndef HZ_PREPROC_GENERIC
+#define HZ_PREPROC_GENERIC 0  // 1: uint8 3-channel payloads through the generic per-pixel kernel (A/B)
+#endif
 extern "C" int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
                                     int mode, const float* mean, const float* inv_std, hipStream_t st) {
   if (Cpad % 8 || Cin > 8) return -1;
   const long total = (long)N * H * W;
+  if (mode == 1 && Cin == 3 && total % 4 == 0 && ((uintptr_t)src & 3) == 0 && !HZ_PREPROC_GENERIC) {
+    hipLaunchKernelGGL(preprocess_u8c3_kernel, dim3((total + 1023) / 1024), dim3(256), 0, st,
+                       static_cast<const unsigned*>(src), dst, total, Cpad, mean, inv_std);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(preprocess_kernel, dim3((total + 255) / 256), dim3(256), 0, st, src, dst, N, Cin, H, W, Cpad,
                      mode, mean, inv_std);
   return (int)hipGetLastError();

@@ -103,6 +103,20 @@ def test_maxpool_avgpool_preprocess():
     assert (p - V.preprocess_reference(u8, mean=V.IMAGENET_MEAN, std=V.IMAGENET_STD)).abs().max() < 2e-2
 
 
+@pytest.mark.parametrize("shape,cpad", [((2, 30, 34), 8), ((1, 224, 224), 8), ((3, 16, 16), 16), ((1, 5, 7), 8)])
+def test_preprocess_uint8_coalesced(shape, cpad):
+    """uint8 3-channel payloads: 1024-pixel workgroups with a partial last one, Cpad > 8, and a pixel
+    count that is not a multiple of 4 (generic per-pixel kernel) -- all bit-exact vs fp32 math."""
+    g = torch.Generator().manual_seed(2)
+    u8 = torch.randint(0, 256, (*shape, 3), dtype=torch.uint8, generator=g)
+    for mean, std in ((None, None), (V.IMAGENET_MEAN, V.IMAGENET_STD)):
+        p = V.preprocess(u8.to(DEV), cpad=cpad, mean=mean, std=std).cpu().float()
+        ref = V.preprocess_reference(u8, cpad=cpad, mean=mean, std=std)
+        assert p.shape == ref.shape
+        assert (p - ref).abs().max() < 2e-2
+        assert torch.equal(p[..., 3:], torch.zeros_like(p[..., 3:]))
+
+
 @pytest.mark.parametrize("B,H,C,N", [(1, 7, 2048, 1000), (3, 7, 512, 10), (2, 4, 64, 33)])
 def test_pool_fc(B, H, C, N):
     """Fused global-average-pool + FC (ResNet head) vs fp32."""
