@@ -22,12 +22,14 @@ from .program import ExecContext, bench_contexts
 def load_tuning(model: str, batch: int, contexts: int = 1) -> dict | None:
     """Measured launch-config table written by ``python -m hipzap.engine.tune`` (if any).
 
-    Prefers the table tuned for the same request concurrency (``_c<contexts>``), falling back
-    to the single-stream (latency) table.
+    Prefers the table tuned for the same request concurrency (``_c<contexts>``), then the one
+    tuned for the highest concurrency below it (a throughput objective is closer to ``contexts``
+    streams than the latency objective is), then the single-stream (latency) table.
     """
     import json
     from .tune import table_path
-    for p in (table_path(model, batch, contexts), table_path(model, batch, 1)):
+    for c in range(contexts, 0, -1):
+        p = table_path(model, batch, c)
         if p.exists():
             with open(p) as f:
                 return json.load(f)
@@ -49,7 +51,12 @@ def add_softmax_head(g) -> None:
 class Engine:
     def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
                  capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
-                 host_io: bool = True, probs: bool = False, zero_copy: str | None = None):
+                 host_io: bool = True, probs: bool = False, zero_copy: str | None = None,
+                 eager_contexts: int | None = None):
+        """``eager_contexts``: plan + capture only this many of the ``num_contexts`` request
+        contexts before the engine is ready (cold start = time to the first served request); the
+        rest are built by :meth:`ensure_contexts` (``bench`` calls it), e.g. after the first
+        request, the way a warm container scales up its concurrency. None: all up front."""
         self.model = model
         self.adapter = registry.get(model)
         self.device = torch.device(device)
@@ -60,26 +67,53 @@ class Engine:
         if tuned is None:
             tuned = load_tuning(model, batch, num_contexts)
         self.tuned = tuned
+        self.num_contexts = num_contexts
+        self._capture, self._zero_copy = capture, zero_copy
+        n0 = num_contexts if eager_contexts is None else max(1, min(eager_contexts, num_contexts))
         t0 = time.perf_counter()
         with torch.cuda.device(self.device):
             self.graph = self.adapter.build_graph(batch=batch, **self.arch_kw)
             if probs:
                 add_softmax_head(self.graph)
             self.host_io = host_io
-            self.contexts = [ExecContext(self.graph, params, self.device, tuned, host_io=host_io, zero_copy=zero_copy)
-                             for _ in range(num_contexts)]
-            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(num_contexts)]
+            self.contexts, self.streams = self._new_contexts(n0)
             torch.cuda.synchronize(self.device)
             self.timings["plan_ms"] = (time.perf_counter() - t0) * 1e3
             t0 = time.perf_counter()
-            if capture:
-                for c, s in zip(self.contexts, self.streams):
-                    c.capture(s)
-                torch.cuda.synchronize(self.device)
+            self._capture_all(self.contexts, self.streams)
+            torch.cuda.synchronize(self.device)
             self.timings["capture_ms"] = (time.perf_counter() - t0) * 1e3
         self._rr = 0
         self._locks = [threading.Lock() for _ in self.contexts]
         self._rr_lock = threading.Lock()
+
+    def _new_contexts(self, n: int):
+        ctxs = [ExecContext(self.graph, self.params, self.device, self.tuned, host_io=self.host_io,
+                            zero_copy=self._zero_copy) for _ in range(n)]
+        return ctxs, [torch.cuda.Stream(device=self.device) for _ in range(n)]
+
+    def _capture_all(self, ctxs, streams) -> None:
+        if self._capture:
+            for c, s in zip(ctxs, streams):
+                c.capture(s)
+
+    def ensure_contexts(self) -> float:
+        """Plan + capture the contexts deferred by ``eager_contexts``; returns the ms spent."""
+        n = self.num_contexts - len(self.contexts)
+        if n <= 0:
+            return 0.0
+        t0 = time.perf_counter()
+        with torch.cuda.device(self.device):
+            ctxs, sts = self._new_contexts(n)
+            self._capture_all(ctxs, sts)
+            torch.cuda.synchronize(self.device)
+        with self._rr_lock:  # lists grow in step; _pick reads len(self.contexts) under this lock
+            self._locks += [threading.Lock() for _ in ctxs]
+            self.streams += sts
+            self.contexts += ctxs
+        ms = (time.perf_counter() - t0) * 1e3
+        self.timings["deferred_contexts_ms"] = ms
+        return ms
 
     # -------------------------------------------------------------- construction
     @classmethod
@@ -183,6 +217,7 @@ class Engine:
 
     def bench(self, iters: int) -> float:
         """Replay all contexts concurrently ``iters`` times (C++ loop); returns seconds."""
+        self.ensure_contexts()
         return bench_contexts(self.contexts, self.streams, iters)
 
     def describe(self) -> dict:

@@ -69,6 +69,21 @@ def test_concurrent_contexts(model_sd):
     assert secs > 0
 
 
+def test_deferred_contexts(model_sd):
+    """eager_contexts=1: one context serves the first request; ensure_contexts (and bench) build
+    the rest, which produce the same logits."""
+    name, m, sd = model_sd
+    eng = Engine.from_state_dict(name, sd, DEV, batch=1, num_contexts=3, eager_contexts=1)
+    assert len(eng.contexts) == 1
+    x = torch.randn(1, 3, 224, 224)
+    y0 = eng.infer(x)
+    assert eng.ensure_contexts() > 0 and len(eng.contexts) == len(eng.streams) == len(eng._locks) == 3
+    assert eng.ensure_contexts() == 0.0
+    for _ in range(3):
+        assert torch.equal(eng.infer(x), y0)
+    assert eng.bench(5) > 0
+
+
 def test_probs_head(model_sd):
     """Engine(probs=True): on-device softmax over the logits (csrc/transformer.hip softmax_kernel)."""
     name, m, sd = model_sd
