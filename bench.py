@@ -2,22 +2,28 @@
 """hipzap headline benchmark: ResNet-50 bs=1 serving throughput (whole node) + cold start.
 
 Metric (BASELINE.json): inferences/sec (whole node) + p50 cold-start ms, ResNet-50 bs=1 at
-1/2/4/8 GPU. One process per GPU (torchrun); every rank is a serving replica:
-  cold start  rank 0 torch.load()s a standard state_dict checkpoint (random-init weights of
-              the real ResNet-50 architecture, written untimed beforehand) -> packs/folds BN
-              on its GPU -> RCCL-broadcasts the packed blob to the other ranks -> every rank
-              plans its arena, binds native programs, captures hipGraphs -> first inference.
-              Also reported: the same from the pre-packed copy (<ckpt>.hzpack, safetensors
-              streamed to the GPU: no fold/pack), `cold_start_packed_ms_p50`.
-              Only the first request context is built before that first inference; the other
-              streams-1 are planned + captured right after it (``deferred_contexts_ms``).
-  warm step   every rank serves ``--streams`` (default 32: the peak of the measured
-              concurrency sweep, profiles/r1_session5/streams_sweep.md) independent bs=1 requests
-              concurrently: each is
-              one hipGraph replay that includes the pinned H2D of the fp32 image, preprocess,
-              53 fused conv kernels, pools, FC and the D2H of the logits.
-Timed region: K steps bracketed by barrier + cuda.synchronize on both sides; the slowest
-rank's time is used. value = world * streams * K / t  (weak scaling: fixed work per GPU).
+1/2/4/8 GPU. One process per GPU (torchrun); every rank is a serving replica.
+
+cold start (headline ``cold_start_ms_p50``): measured FIRST, before this process touches a GPU,
+  as the p50 over ``--cold-trials`` FRESH child processes of spawn -> first logits
+  (hipzap/coldstart.py) from the deploy artifact a serverless replica starts from: the
+  ``.hzplan`` plan image (torch-free: mmap, one DMA of the packed weights, bind, hipGraph
+  capture, one bs=1 request). ``cold_start_pth_ms_p50``: the same from the ``.pth``
+  state_dict (import torch, torch.load, fold/pack on the GPU). Artifacts (random-init weights
+  of the real ResNet-50 architecture, their plan image) are written untimed beforehand, on the
+  CPU, as ``hipzap plan`` does at deploy time. In-process rebuilds inside this warm process are
+  reported separately (``cold_start_inprocess_*``).
+warm path: every rank serves ``--streams`` (default 32, profiles/r1_session5/streams_sweep.md)
+  concurrent bs=1 request streams; each request is one hipGraph replay (zero-copy pinned uint8
+  image -> preprocess -> 53 fused conv kernels -> pool+FC -> logits in pinned memory).
+  ``--serve executor`` (default): one native client thread per stream sends requests back to
+  back through the request executor (csrc/executor.cpp, the serving path of Engine.infer):
+  payload copied into a pinned input, one replay, the client sleeps until ITS result is done,
+  logits copied out — throughput and p50/p99 latency are what concurrent clients see.
+  ``--serve pipelined``: replays queued back to back without host work (device-bound ceiling,
+  always reported too).
+Timed region: K steps (= K requests per stream) bracketed by barrier + cuda.synchronize on both
+sides; the slowest rank's time is used. value = world * streams * K / t (weak scaling).
 """
 import time
 
@@ -46,7 +52,13 @@ def parse():
     ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 32)),
                     help="concurrent bs=1 request contexts per GPU")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
-    ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds for p50")
+    ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 5)),
+                    help="fresh processes per cold-start path (0: skip)")
+    ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds (secondary figure)")
+    ap.add_argument("--serve", choices=["executor", "threads", "pipelined"], default="executor",
+                    help="executor: closed-loop clients through the native request executor (headline); "
+                         "threads: every client thread launches + synchronises its own context; "
+                         "pipelined: replays queued back to back, no host work (device ceiling)")
     ap.add_argument("--compare-torch", action="store_true", help="also time PyTorch/MIOpen bf16 + CUDA graph")
     ap.add_argument("--no-capture", action="store_true")
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
@@ -73,10 +85,8 @@ def run_scatter(args, rank, world, device, adapter, ckpt):
     if rank == 0:
         sd = torch.load(ckpt, map_location="cpu", weights_only=True)
         params, arch_kw = adapter.pack({k: v.to(device) for k, v in sd.items()}, device)
-    meta, meta_kw = adapter.meta_params()
-    params = broadcast_params(params, meta, device)
-    eng = Engine(args.model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw or meta_kw,
-                 host_io=False)
+    params, arch_kw = broadcast_params(params, lambda kw: adapter.meta_params(**kw), device, arch_kw=arch_kw)
+    eng = Engine(args.model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
     x_in = adapter.example_input(shard)
     in_shape = tuple(eng.contexts[0].input.shape[1:])
     out_shape = tuple(eng.contexts[0].output.shape[1:])
@@ -123,6 +133,34 @@ def write_checkpoint(path, model):
     os.replace(tmp, path)
 
 
+def prepare_artifacts(model: str, ckpt_dir: str, plan_contexts: int = 1) -> tuple[str, str]:
+    """Deploy-time artifacts, written untimed on the CPU (no GPU call): the random-init
+    checkpoint, its packed safetensors copy and its plan image; reused while up to date."""
+    from hipzap.engine.packfile import find_packed, packed_path, save_packed, source_stamp
+    from hipzap.engine.plan import export_from_checkpoint, plan_path
+    from hipzap.lite import plan_usable, read_meta
+    from hipzap.models import registry
+    ckpt = os.path.join(ckpt_dir, f"{model}_seed0.pth")
+    if not os.path.exists(ckpt):
+        write_checkpoint(ckpt, model)
+    stamp = source_stamp(ckpt)
+    if find_packed(ckpt, model) is None:
+        params, kw = registry.get(model).pack(torch.load(ckpt, map_location="cpu", weights_only=True), "cpu")
+        save_packed(params, kw, packed_path(ckpt), model=model, stamp=stamp)
+    plan = plan_path(ckpt)
+    if not (plan_usable(plan) and read_meta(plan).get("source") == stamp):
+        export_from_checkpoint(model, ckpt, plan, batch=1, contexts=plan_contexts)
+    return ckpt, plan
+
+
+def fresh_cold_start(args, device_index: int) -> dict:
+    """Cold start over fresh processes (hipzap/coldstart.py), before this process uses a GPU."""
+    from hipzap.coldstart import measure_fresh
+    ckpt, plan = prepare_artifacts(args.model, args.ckpt_dir)
+    return {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index),
+            "pth": measure_fresh("pth", ckpt, args.model, args.cold_trials, device=device_index)}
+
+
 def torch_reference_throughput(model, device, iters=200):
     """Stock PyTorch path on the same GPU: bf16 channels_last + CUDA(HIP) graph, bs=1."""
     from hipzap.models import registry
@@ -159,19 +197,28 @@ def request_input(args, adapter):
 
 def main():
     args = parse()
+    from hipzap.parallel.comm import env_rank
+    rank, world, local = env_rank()
+    # 1. cold start over fresh processes, before this process makes any GPU call (the other
+    #    ranks wait in the process-group rendezvous meanwhile)
+    fresh = None
+    if rank == 0:
+        if args.mode == "replica" and args.cold_trials > 0 and args.model.startswith("resnet"):
+            dev_index = local % max(1, torch.cuda.device_count()) if os.environ.get("HIPZAP_SHARE_GPU") == "1" \
+                else local
+            fresh = fresh_cold_start(args, dev_index)
+        else:
+            prepare_artifacts(args.model, args.ckpt_dir)
+
     from hipzap.engine.engine import Engine
     from hipzap.models import registry
-    from hipzap.parallel.comm import (broadcast_params, env_rank, init_distributed, is_dist, local_device,
-                                      max_over_ranks)
+    from hipzap.parallel.comm import broadcast_params, init_distributed, is_dist, local_device, max_over_ranks
 
-    rank, world, local = env_rank()
     device = local_device(local)
     torch.cuda.set_device(device)
     init_distributed(device=device)
     adapter = registry.get(args.model)
     ckpt = os.path.join(args.ckpt_dir, f"{args.model}_seed0.pth")
-    if rank == 0 and not os.path.exists(ckpt):
-        write_checkpoint(ckpt, args.model)
     tuned = None  # Engine picks hipzap/tuning/<model>_bs<B>[_c<streams>].json
     if args.tuned:
         with open(args.tuned) as f:
@@ -186,8 +233,9 @@ def main():
         return
 
     def cold_start(packed: str | None = None):
-        """``packed``: start from the pre-packed copy of the checkpoint (``<ckpt>.hzpack``, the
-        deploy-time artifact of ``hipzap pack``) instead of torch.load + fold/pack."""
+        """In-process cold start: rank 0 loads (``packed``: the pre-packed copy ``<ckpt>.hzpack``)
+        and RCCL-broadcasts the packed blob + its architecture metadata; every rank plans and
+        captures its first request context and serves one request."""
         t0 = time.perf_counter()
         timings = {}
         if rank == 0 and packed:
@@ -207,17 +255,13 @@ def main():
             timings["pack_ms"] = (time.perf_counter() - ta) * 1e3
         else:
             params, arch_kw = None, None
-        if arch_kw is None:  # receiving rank: shapes from a meta-device construction
-            meta, arch_kw = adapter.meta_params()
-        else:
-            meta = None
+        ta = time.perf_counter()
+        params, arch_kw = broadcast_params(params, lambda kw: adapter.meta_params(**kw), device, arch_kw=arch_kw)
+        torch.cuda.synchronize(device)
+        timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         arch_kw = dict(arch_kw)
         if args.input == "uint8" and args.model.startswith("resnet"):
             arch_kw["input_uint8"] = True
-        ta = time.perf_counter()
-        params = broadcast_params(params, meta, device)
-        torch.cuda.synchronize(device)
-        timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         # zero-copy request IO: the preprocess kernel reads the pinned request bytes and pool_fc writes
         # the pinned logits directly (no copy nodes): +1.7 % single stream, +0.5-1 % at 8 streams
         # (profiles/r1_ab/zero_copy.txt, interleaved on one box)
@@ -230,6 +274,7 @@ def main():
         eng.timings["first_infer_total_ms"] = cold_ms
         return eng, out, cold_ms
 
+    # 2. in-process cold starts (secondary figures: warm torch, warm HIP runtime)
     eng, out, cold_first = cold_start()
     cold_process_ms = (time.time() - T_PROC0) * 1e3
     colds = [cold_first]
@@ -240,19 +285,13 @@ def main():
         colds.append(c)
     assert torch.isfinite(out).all(), "non-finite logits"
     breakdown_pth = dict(eng.timings)
-    # packed fast path: rank 0 writes <ckpt>.hzpack once (untimed, as `hipzap pack` would at deploy
-    # time), then every rank cold-starts from it
     colds_packed, breakdown_packed = [], {}
     if args.cold_runs:
-        from hipzap.engine.packfile import packed_path, save_packed, source_stamp
-        pk = packed_path(ckpt)
-        if rank == 0:
-            params0, kw0 = adapter.pack(torch.load(ckpt, map_location="cpu", weights_only=True), "cpu")
-            save_packed(params0, kw0, pk, model=args.model, stamp=source_stamp(ckpt))
+        from hipzap.engine.packfile import packed_path
         for _ in range(args.cold_runs):
             del eng
             torch.cuda.synchronize(device)
-            eng, out, c = cold_start(packed=pk)
+            eng, out, c = cold_start(packed=packed_path(ckpt))
             colds_packed.append(c)
         breakdown_packed = dict(eng.timings)
         assert torch.isfinite(out).all(), "non-finite logits (packed path)"
@@ -260,7 +299,7 @@ def main():
     # the other streams-1 request contexts are planned + captured after the first request was served
     # (a warm container scaling up its concurrency), outside the cold-start figure; reported below
     deferred_ms = eng.ensure_contexts()
-    # single-request latency (one context, full round trip incl. host copies), p50
+    # single-request latency, one request at a time (round-robin over the contexts), p50/p99
     x = request_input(args, adapter)
     lat = []
     for i in range(210):
@@ -270,21 +309,41 @@ def main():
     lat = sorted(lat[10:])
     lat_p50, lat_p99 = statistics.median(lat), lat[min(len(lat) - 1, int(0.99 * len(lat)))]
 
-    # throughput: warmup then K timed steps, each step = `streams` concurrent bs=1 requests
+    def pct(v, q):
+        v = sorted(v)
+        return v[min(len(v) - 1, int(q * len(v)))]
+
+    # 3. throughput: W warmup steps, then K timed steps; a step = one request on every stream
+    payload = x.reshape(eng.contexts[0].host_input.shape)
+
+    def run(steps, mode):
+        if mode == "pipelined":
+            return eng.bench(steps), None
+        return eng.serve_bench(steps, payload, mode=mode)
+
+    other = "pipelined" if args.serve != "pipelined" else "executor"
     if args.warmup:
-        eng.bench(args.warmup)
+        run(args.warmup, args.serve)
     if is_dist():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    eng.bench(args.steps)
+    _, lat_load = run(args.steps, args.serve)
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     if is_dist():
         dist.barrier()
     dt = max_over_ranks(dt, device)
+    # the other serving mode, untimed for the headline (same K), for reference
+    dt_other, lat_other = run(args.steps, other)
+    dt_other = max_over_ranks(dt_other, device)
+    lat_closed = lat_load if args.serve != "pipelined" else lat_other
     inf = world * args.streams * args.batch * args.steps
     value = inf / dt
+    # strict single-stream throughput (one context, replays back to back)
+    single = eng.contexts[0]
+    from hipzap.engine.program import bench_contexts
+    t_single = bench_contexts([single], [eng.streams[0]], 200)
     torch_ref = None
     if args.compare_torch and rank == 0:
         try:
@@ -302,17 +361,27 @@ def main():
                        else "random fp32 NCHW images)"),
             "config": {"model": "ResNet-50", "global_batch": args.batch * world, "seq_len": None,
                        "parallelism": f"dp{world}", "request_batch": args.batch,
-                       "streams_per_gpu": args.streams, "hipgraph": not args.no_capture},
-            "cold_start_ms_p50": round(statistics.median(colds), 2),
-            "cold_start_ms_first": round(cold_first, 2),
-            "cold_start_process_ms": round(cold_process_ms, 2),
-            "cold_start_breakdown_ms": {k: round(v, 2) for k, v in breakdown_pth.items()},
-            "cold_start_packed_ms_p50": round(statistics.median(colds_packed), 2) if colds_packed else None,
-            "cold_start_packed_breakdown_ms": {k: round(v, 2) for k, v in breakdown_packed.items()},
+                       "streams_per_gpu": args.streams, "hipgraph": not args.no_capture,
+                       "serving": args.serve},
+            "cold_start_ms_p50": fresh["plan"]["p50_ms"] if fresh else None,
+            "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
+                               "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict",
+            "cold_start_pth_ms_p50": fresh["pth"]["p50_ms"] if fresh else None,
+            "cold_start_fresh_process": fresh,
+            "cold_start_inprocess_ms_first": round(cold_first, 2),
+            "cold_start_inprocess_ms_p50": round(statistics.median(colds), 2),
+            "cold_start_inprocess_breakdown_ms": {k: round(v, 2) for k, v in breakdown_pth.items()},
+            "cold_start_inprocess_packed_ms_p50": round(statistics.median(colds_packed), 2) if colds_packed else None,
+            "cold_start_inprocess_packed_breakdown_ms": {k: round(v, 2) for k, v in breakdown_packed.items()},
+            "bench_process_first_request_ms": round(cold_process_ms, 2),
             "deferred_contexts_ms": round(deferred_ms, 2),
+            "served_closed_loop_inf_s": round(inf / (dt if args.serve != "pipelined" else dt_other), 2),
+            "device_pipelined_inf_s": round(inf / (dt if args.serve == "pipelined" else dt_other), 2),
+            "latency_ms_under_load_p50": round(pct(lat_closed, 0.5), 4),
+            "latency_ms_under_load_p99": round(pct(lat_closed, 0.99), 4),
             "latency_ms_p50_single": round(lat_p50, 4),
-            "latency_ms_under_load": round(dt / args.steps * 1e3, 4),
             "latency_ms_p99_single": round(lat_p99, 4),
+            "single_stream_inf_s": round(200 / t_single, 2),
             "baseline_note": "vs_baseline against BASELINE.md sandbox-CPU ResNet-50 bs=1 (27.2 inf/s); "
                              "no published numbers exist",
         }

@@ -2,6 +2,7 @@
 
     python -m hipzap serve --port 8082            # local dev server (reference: main.py:115-127)
     python -m hipzap pack --model resnet50 --ckpt m.pth --out m.hzpack
+    python -m hipzap plan --model resnet50 --ckpt m.pth [--contexts 24]  # torch-free cold-start image
     python -m hipzap tune --model resnet50 --batch 1 --concurrent 1 8
     python -m hipzap upload --models-dir ./models  # scripts/upload_models.py parity
     python -m hipzap info
@@ -37,6 +38,14 @@ def cmd_pack(a):
     h = hashlib.sha256(open(a.ckpt, "rb").read()).hexdigest()
     save_packed(params, cfg, a.out, h)
     print(json.dumps({"out": a.out, "entries": len(params), "source_sha256": h}))
+
+
+def cmd_plan(a):
+    from .engine.plan import export_from_checkpoint
+    from .lite import read_meta
+    out = export_from_checkpoint(a.model, a.ckpt, a.out, batch=a.batch, contexts=a.contexts, probs=a.probs)
+    m = read_meta(out)
+    print(json.dumps({"out": out, "ops": m["n_ops"], "blob_bytes": m["blob_bytes"], "source": m["source"]}))
 
 
 def cmd_tune(a):
@@ -85,6 +94,13 @@ def main(argv=None):
     p.add_argument("--model", required=True)
     p.add_argument("--ckpt", required=True)
     p.add_argument("--out", required=True)
+    pl = sub.add_parser("plan")
+    pl.add_argument("--model", required=True)
+    pl.add_argument("--ckpt", required=True)
+    pl.add_argument("--out", default=None, help="default: <ckpt>.hzplan")
+    pl.add_argument("--batch", type=int, default=1)
+    pl.add_argument("--contexts", type=int, default=1, help="request concurrency the launch configs are tuned for")
+    pl.add_argument("--probs", action="store_true", help="softmax head on device")
     t = sub.add_parser("tune")
     t.add_argument("--model", default="resnet50")
     t.add_argument("--batch", type=int, nargs="+", default=[1])
@@ -99,7 +115,7 @@ def main(argv=None):
     args, rest = ap.parse_known_args(argv)
     if args.cmd == "bench":
         return cmd_bench(args, rest)
-    {"serve": cmd_serve, "pack": cmd_pack, "tune": cmd_tune, "upload": cmd_upload, "info": cmd_info}[args.cmd](args)
+    {"serve": cmd_serve, "pack": cmd_pack, "plan": cmd_plan, "tune": cmd_tune, "upload": cmd_upload, "info": cmd_info}[args.cmd](args)
 
 
 if __name__ == "__main__":

@@ -105,6 +105,9 @@ def _load():
     _sig(lib, "hz_prog_bench", c_double, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int)
     _sig(lib, "hz_prog_bench2", c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int, c_int,
          C.POINTER(c_double))
+    PP = C.POINTER(c_void_p)
+    _sig(lib, "hz_serve_bench", c_int, PP, PP, PP, PP, C.c_uint64, PP, PP, C.c_uint64, c_int, c_int,
+         C.POINTER(c_double), C.POINTER(c_double))
     _sig(lib, "hz_diag_launch", c_int, c_int, c_int, c_int, P, P, c_long, P)
     _sig(lib, "hz_prog_add_diag", c_int, P, c_int, c_int, c_int, P, P, c_long, c_int)
     _sig(lib, "hz_prog_replay_n", c_int, P, P, c_int)
@@ -117,6 +120,30 @@ def _load():
     _sig(lib, "hz_prog_add_lstm", c_int, P, C.POINTER(LstmParams), c_int)
     _sig(lib, "hz_prog_add_decoder", c_int, P, C.POINTER(DecoderParams), c_int)
     _sig(lib, "hz_prog_add_sampler", c_int, P, C.POINTER(SamplerParams), c_int)
+    # plan images (csrc/plan.cpp; hipzap/lite.py is the torch-free client)
+    U64, D = C.c_uint64, c_double
+    _sig(lib, "hz_abi_version", U64)
+    _sig(lib, "hz_plan_last_error", C.c_char_p)
+    _sig(lib, "hz_plan_open", P, C.c_char_p, c_int, c_int, C.POINTER(D))
+    _sig(lib, "hz_plan_add_contexts", c_int, P, c_int, c_int)
+    _sig(lib, "hz_plan_num_contexts", c_int, P)
+    _sig(lib, "hz_plan_timings", None, P, C.POINTER(D))
+    _sig(lib, "hz_plan_blob", P, P, C.POINTER(U64))
+    _sig(lib, "hz_plan_host", P, P, c_int)
+    _sig(lib, "hz_plan_device", P, P, c_int)
+    _sig(lib, "hz_plan_stream", P, P, c_int)
+    _sig(lib, "hz_plan_replay", c_int, P, c_int)
+    _sig(lib, "hz_plan_sync", c_int, P, c_int)
+    _sig(lib, "hz_plan_infer", c_int, P, c_int, P, U64, U64, P, U64, U64)
+    _sig(lib, "hz_plan_bench", D, P, c_int)
+    _sig(lib, "hz_plan_close", None, P)
+    _sig(lib, "hz_plan_prog", P, P, c_int)
+    PP_ = C.POINTER(c_void_p)
+    _sig(lib, "hz_exec_create", P, PP_, PP_, PP_, C.POINTER(U64), c_int, PP_, U64, c_int)
+    _sig(lib, "hz_exec_submit", c_int, P, PP_, P, C.POINTER(D))
+    _sig(lib, "hz_exec_stats", None, P, C.POINTER(U64), C.POINTER(U64))
+    _sig(lib, "hz_exec_destroy", None, P)
+    _sig(lib, "hz_exec_bench", c_int, P, c_int, c_int, PP_, C.POINTER(D), C.POINTER(D))
     if DEBUG:
         for unit in DEBUG_UNITS:
             _sig(lib, f"hz_debug_poll_{unit}", c_int, C.POINTER(C.c_uint))

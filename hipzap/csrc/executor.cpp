@@ -1,0 +1,213 @@
+// hipzap request executor: the serving scheduler between request threads and the GPU.
+//
+// Measured problem (profiles/r2_serving): 32 request threads that each hipGraphLaunch +
+// hipStreamSynchronize their own context contend inside the HIP runtime (spin-waiting
+// synchronisation, submission locks): 5.5k inf/s closed-loop with a 58 ms p99, against 10.4k
+// when one thread queues the same replays back to back. The executor keeps that shape:
+//   request thread  take a free context slot -> copy its payload into the slot's pinned input
+//                   -> queue the slot -> sleep on the slot's condition variable -> copy the
+//                   result out of the pinned output -> release the slot
+//   worker thread   the ONLY thread that touches HIP on the request path: launches queued
+//                   slots (one hipGraphLaunch + one event record each) and polls the in-flight
+//                   slots' completion events, waking each request as its replay finishes
+// Host copies are spread over the request threads; submissions are serialised on one thread
+// (which is how the pipelined device ceiling was measured); request threads never spin.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "hipzap.h"
+
+namespace {
+
+constexpr int kMaxIn = 4;
+
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Slot {
+  HzProgram prog = nullptr;
+  hipStream_t st = nullptr;
+  void* in[kMaxIn] = {};
+  void* out = nullptr;
+  hipEvent_t ev = nullptr;
+  bool done = false;
+  int rc = 0;
+  std::condition_variable cv;
+};
+
+struct Exec {
+  std::vector<Slot> slots;
+  int n_in = 1;
+  uint64_t in_bytes[kMaxIn] = {};
+  uint64_t out_bytes = 0;
+  std::mutex mu;
+  std::condition_variable cv_free, cv_work;
+  std::vector<int> free_slots;
+  std::deque<int> to_launch;
+  std::vector<int> inflight;  // worker-owned
+  bool stop = false;
+  std::thread worker;
+  uint64_t served = 0, polls = 0;
+
+  void complete(int s, int rc) {
+    std::lock_guard<std::mutex> g(mu);
+    slots[s].rc = rc;
+    slots[s].done = true;
+    slots[s].cv.notify_one();
+    ++served;
+  }
+
+  void run() {
+    std::vector<int> launch;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (to_launch.empty() && inflight.empty())
+          cv_work.wait(lk, [&] { return stop || !to_launch.empty(); });
+        if (stop && to_launch.empty() && inflight.empty()) return;
+        launch.assign(to_launch.begin(), to_launch.end());
+        to_launch.clear();
+      }
+      for (int s : launch) {
+        int rc = hz_prog_replay(slots[s].prog, slots[s].st);
+        if (!rc) rc = (int)hipEventRecord(slots[s].ev, slots[s].st);
+        if (rc)
+          complete(s, rc);
+        else
+          inflight.push_back(s);
+      }
+      bool progressed = !launch.empty();
+      for (size_t i = 0; i < inflight.size();) {
+        const int s = inflight[i];
+        const hipError_t q = hipEventQuery(slots[s].ev);
+        ++polls;
+        if (q == hipErrorNotReady) {
+          ++i;
+          continue;
+        }
+        complete(s, q == hipSuccess ? 0 : (int)q);
+        inflight[i] = inflight.back();
+        inflight.pop_back();
+        progressed = true;
+      }
+      if (!progressed) std::this_thread::yield();
+    }
+  }
+
+  int submit_wait(const void* const* in, void* out, double* lat_us) {
+    const double t0 = now_us();
+    int s;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv_free.wait(lk, [&] { return stop || !free_slots.empty(); });
+      if (stop) return -10;
+      s = free_slots.back();
+      free_slots.pop_back();
+    }
+    Slot& sl = slots[s];
+    for (int k = 0; k < n_in; ++k)
+      if (in && in[k] && in_bytes[k]) std::memcpy(sl.in[k], in[k], in_bytes[k]);
+    int rc;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      sl.done = false;
+      to_launch.push_back(s);
+      cv_work.notify_one();
+      sl.cv.wait(lk, [&] { return sl.done; });
+      rc = sl.rc;
+    }
+    if (!rc && out && out_bytes) std::memcpy(out, sl.out, out_bytes);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      free_slots.push_back(s);
+    }
+    cv_free.notify_one();
+    if (lat_us) *lat_us = now_us() - t0;
+    return rc;
+  }
+
+  ~Exec() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv_work.notify_all();
+    cv_free.notify_all();
+    if (worker.joinable()) worker.join();
+    for (auto& s : slots)
+      if (s.ev) (void)hipEventDestroy(s.ev);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+// progs/streams: n bound, captured contexts; host_in[k * n + i] = context i's pinned input k;
+// host_out[i] = its pinned output. The executor does not own any of them.
+void* hz_exec_create(HzProgram* progs, hipStream_t* streams, void** host_in, const uint64_t* in_bytes, int n_in,
+                     void** host_out, uint64_t out_bytes, int n) {
+  if (n <= 0 || n_in < 0 || n_in > kMaxIn) return nullptr;
+  auto* e = new Exec();
+  e->slots = std::vector<Slot>(n);
+  e->n_in = n_in;
+  for (int k = 0; k < n_in; ++k) e->in_bytes[k] = in_bytes[k];
+  e->out_bytes = out_bytes;
+  for (int i = 0; i < n; ++i) {
+    Slot& s = e->slots[i];
+    s.prog = progs[i];
+    s.st = streams[i];
+    for (int k = 0; k < n_in; ++k) s.in[k] = host_in[k * n + i];
+    s.out = host_out[i];
+    if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+      delete e;
+      return nullptr;
+    }
+    e->free_slots.push_back(n - 1 - i);  // slot 0 first
+  }
+  e->worker = std::thread([e] { e->run(); });
+  return e;
+}
+
+int hz_exec_submit(void* h, const void* const* in, void* out, double* lat_us) {
+  return static_cast<Exec*>(h)->submit_wait(in, out, lat_us);
+}
+
+void hz_exec_stats(void* h, uint64_t* served, uint64_t* polls) {
+  Exec* e = static_cast<Exec*>(h);
+  std::lock_guard<std::mutex> g(e->mu);
+  *served = e->served;
+  *polls = e->polls;
+}
+
+void hz_exec_destroy(void* h) { delete static_cast<Exec*>(h); }
+
+// `clients` native threads, each serving `iters` requests back to back through the executor
+// (payload in[] for every request); per-request latency in lat_us[client * iters + i]
+int hz_exec_bench(void* h, int clients, int iters, const void* const* in, double* lat_us, double* wall_us) {
+  Exec* e = static_cast<Exec*>(h);
+  std::vector<std::thread> th;
+  std::vector<int> rcs(clients, 0);
+  std::vector<std::vector<uint8_t>> outs(clients, std::vector<uint8_t>(e->out_bytes + 1));
+  const double t0 = now_us();
+  for (int c = 0; c < clients; ++c)
+    th.emplace_back([&, c] {
+      for (int it = 0; it < iters && !rcs[c]; ++it)
+        rcs[c] = e->submit_wait(in, outs[c].data(), lat_us + (size_t)c * iters + it);
+    });
+  for (auto& t : th) t.join();
+  *wall_us = now_us() - t0;
+  int rc = 0;
+  for (int r : rcs) rc |= r;
+  return rc;
+}
+
+}  // extern "C"

@@ -240,9 +240,69 @@ int hz_prog_replay_n(HzProgram p, hipStream_t st, int n);  // n back-to-back rep
 // returns elapsed microseconds (host wall, includes the final sync) or negative on error.
 double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters);
 int hz_prog_bench2(HzProgram* progs, hipStream_t* streams, int n, int iters, int threads, double* out);
+// closed-loop serving benchmark (one host thread per context; per-request latency in lat_us[n*iters])
+int hz_serve_bench(HzProgram* progs, hipStream_t* streams, void** in_dst, void** in_src, uint64_t in_bytes,
+                   void** out_src, void** out_dst, uint64_t out_bytes, int n, int iters, double* lat_us,
+                   double* wall_us);
 // diagnostics (csrc/diag.hip): kind 0 = no-op kernel, 1 = copy `bytes` from a to b
 int hz_diag_launch(int kind, int blocks, int threads, void* a, void* b, long bytes, hipStream_t st);
 int hz_prog_add_diag(HzProgram p, int kind, int blocks, int threads, void* a, void* b, long bytes, int slot);
+
+// ---- plan images (csrc/plan.cpp, engine/plan.py): serialised bound programs ----
+// bump HZ_ABI_EPOCH when a kernel's parameter SEMANTICS change without a size change
+#define HZ_ABI_EPOCH 1
+enum { HZ_PLAN_OP_CONV = 1, HZ_PLAN_OP_CONV2 = 2, HZ_PLAN_OP_MAXPOOL = 3, HZ_PLAN_OP_AVGPOOL = 4,
+       HZ_PLAN_OP_PREPROCESS = 5, HZ_PLAN_OP_MEMCPY = 6, HZ_PLAN_OP_KERNEL = 7, HZ_PLAN_OP_FORK = 8,
+       HZ_PLAN_OP_JOIN = 9 };
+// argument records of the ops whose hz_prog_add_* takes scalars
+typedef struct HzAvgpoolArgs {
+  const unsigned short* x;
+  unsigned short* out;
+  int N, HW, C, blocked;
+} HzAvgpoolArgs;
+typedef struct HzPreprocessArgs {
+  const void* src;
+  unsigned short* dst;
+  const float* mean;
+  const float* inv_std;
+  int N, Cin, H, W, Cpad, mode;
+} HzPreprocessArgs;
+typedef struct HzMemcpyArgs {
+  void* dst;
+  const void* src;
+  uint64_t bytes;
+} HzMemcpyArgs;
+// load-phase timings (ms) reported by hz_plan_open / hz_plan_timings
+enum { HZ_PLAN_T_PARSE = 0, HZ_PLAN_T_HIP_INIT = 1, HZ_PLAN_T_UPLOAD = 2, HZ_PLAN_T_CTX_ALLOC = 3,
+       HZ_PLAN_T_BIND = 4, HZ_PLAN_T_CAPTURE = 5, HZ_PLAN_NT = 8 };
+uint64_t hz_abi_version(void);
+const char* hz_plan_last_error(void);
+// read_blob = 0: allocate the weight blob but leave it unfilled (an RCCL broadcast fills it)
+void* hz_plan_open(const char* path, int device, int read_blob, double* timings);
+int hz_plan_add_contexts(void* plan, int n, int capture);
+int hz_plan_num_contexts(void* plan);
+void hz_plan_timings(void* plan, double* out);
+void* hz_plan_blob(void* plan, uint64_t* bytes);
+void* hz_plan_host(void* plan, int ctx);
+void* hz_plan_device(void* plan, int ctx);
+void* hz_plan_stream(void* plan, int ctx);
+int hz_plan_replay(void* plan, int ctx);
+int hz_plan_sync(void* plan, int ctx);
+int hz_plan_infer(void* plan, int ctx, const void* in, uint64_t in_off, uint64_t in_bytes, void* out,
+                  uint64_t out_off, uint64_t out_bytes);
+double hz_plan_bench(void* plan, int iters);
+HzProgram hz_plan_prog(void* plan, int ctx);
+
+// ---- request executor (csrc/executor.cpp): one worker thread submits + polls completions ----
+// host_in[k * n + i] = context i's pinned input k (n_in <= 4); host_out[i] = its pinned output
+void* hz_exec_create(HzProgram* progs, hipStream_t* streams, void** host_in, const uint64_t* in_bytes, int n_in,
+                     void** host_out, uint64_t out_bytes, int n);
+// blocking: one request (in[k] = payload of input k), result copied to out; latency in *lat_us
+int hz_exec_submit(void* exec, const void* const* in, void* out, double* lat_us);
+void hz_exec_stats(void* exec, uint64_t* served, uint64_t* polls);
+void hz_exec_destroy(void* exec);
+int hz_exec_bench(void* exec, int clients, int iters, const void* const* in, double* lat_us, double* wall_us);
+void hz_plan_close(void* plan);
 
 #ifdef __cplusplus
 }

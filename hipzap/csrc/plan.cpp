@@ -1,0 +1,422 @@
+// hipzap plan images: a torch-free cold start (VERDICT r1 "next round" #1).
+//
+// A plan (`<ckpt>.hzplan`, written at deploy time by hipzap/engine/plan.py) is a fully bound
+// native Program serialised with relocations instead of pointers:
+//   region 0  shared device blob (packed weights + constants; its bytes are in the file)
+//   region 1  per-context device block (activation arena + static device I/O), zero-filled
+//   region 2  per-context pinned host block (request input / logits, zero-copy I/O)
+// Loading is: mmap -> hipMalloc + H2D of the blob (or an RCCL broadcast into it) -> per context
+// one hipMalloc + one hipHostMalloc + patch every pointer field -> hz_prog_add_* -> hipGraph
+// capture. No Python tensor library, no packing, no planning on the cold path: process start
+// -> first logits is HIP init + one DMA of the weights + a graph instantiation.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hipzap.h"
+
+namespace {
+
+constexpr uint32_t kPlanVersion = 1;
+constexpr char kMagic[8] = {'H', 'Z', 'P', 'L', 'A', 'N', '0', '1'};
+
+// file header: magic + 15 little-endian u64 fields (see plan.py PlanHeader)
+struct FileHeader {
+  char magic[8];
+  uint64_t version, abi, n_ops;
+  uint64_t meta_off, meta_len;
+  uint64_t ops_off, ops_len;
+  uint64_t blob_off, blob_len;
+  uint64_t ctx_dev_bytes, ctx_host_bytes;
+  uint64_t flags, reserved0, reserved1, reserved2;
+};
+static_assert(sizeof(FileHeader) == 128, "plan header is 128 bytes");
+
+struct OpHeader {  // followed by plen param bytes (padded to 8) and nrel relocations
+  uint32_t type;
+  int32_t arg;   // conv cfg or kernel kind
+  int32_t slot;
+  uint32_t plen;
+  uint32_t nrel;
+  uint32_t pad;
+};
+struct Reloc {
+  uint32_t off;     // byte offset of the pointer field inside the params
+  uint32_t region;  // 0 blob, 1 context device block, 2 context host block
+  uint64_t roff;    // offset inside the region
+};
+
+struct PlanOp {
+  OpHeader h;
+  const uint8_t* prm;
+  const Reloc* rel;
+};
+
+struct PlanCtx {
+  void* dev = nullptr;
+  void* host = nullptr;
+  HzProgram prog = nullptr;
+  hipStream_t st = nullptr;
+};
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg, int rc = -1) {
+  g_err = msg;
+  return rc;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Plan {
+  int device = 0;
+  int fd = -1;
+  uint8_t* map = nullptr;
+  size_t map_len = 0;
+  FileHeader h{};
+  std::vector<PlanOp> ops;
+  void* blob = nullptr;
+  std::vector<PlanCtx> ctx;
+  std::mutex mu;
+  double t[HZ_PLAN_NT] = {};
+
+  ~Plan() {
+    (void)hipSetDevice(device);
+    for (auto& c : ctx) free_ctx(c);
+    if (blob) (void)hipFree(blob);
+    if (map) munmap(map, map_len);
+    if (fd >= 0) close(fd);
+  }
+
+  static void free_ctx(PlanCtx& c) {
+    if (c.st) (void)hipStreamSynchronize(c.st);
+    if (c.prog) hz_prog_destroy(c.prog);
+    if (c.st) (void)hipStreamDestroy(c.st);
+    if (c.dev) (void)hipFree(c.dev);
+    if (c.host) (void)hipHostFree(c.host);
+    c = PlanCtx{};
+  }
+
+  int parse() {
+    if (map_len < sizeof(FileHeader)) return fail("plan: file too small");
+    std::memcpy(&h, map, sizeof(h));
+    if (std::memcmp(h.magic, kMagic, 8) != 0) return fail("plan: bad magic");
+    if (h.version != kPlanVersion) return fail("plan: unsupported version " + std::to_string(h.version));
+    if (h.abi != hz_abi_version())
+      return fail("plan: written for a different native ABI (" + std::to_string(h.abi) + " != " +
+                  std::to_string(hz_abi_version()) + "); re-export it");
+    if (h.ops_off + h.ops_len > map_len || h.blob_off + h.blob_len > map_len) return fail("plan: truncated file");
+    const uint8_t* p = map + h.ops_off;
+    const uint8_t* end = p + h.ops_len;
+    ops.reserve(h.n_ops);
+    for (uint64_t i = 0; i < h.n_ops; ++i) {
+      if (p + sizeof(OpHeader) > end) return fail("plan: truncated op table");
+      PlanOp op;
+      std::memcpy(&op.h, p, sizeof(OpHeader));
+      p += sizeof(OpHeader);
+      op.prm = p;
+      p += (op.h.plen + 7u) & ~7u;
+      op.rel = reinterpret_cast<const Reloc*>(p);
+      p += sizeof(Reloc) * op.h.nrel;
+      if (p > end) return fail("plan: truncated op record");
+      for (uint32_t r = 0; r < op.h.nrel; ++r) {
+        const Reloc& rl = op.rel[r];
+        const uint64_t lim = rl.region == 0 ? h.blob_len : rl.region == 1 ? h.ctx_dev_bytes : h.ctx_host_bytes;
+        if (rl.region > 2 || rl.off + 8 > op.h.plen || rl.roff > lim)
+          return fail("plan: relocation out of range in op " + std::to_string(i));
+      }
+      ops.push_back(op);
+    }
+    return 0;
+  }
+
+  // blob upload: the file is mmapped; HIP stages pageable memory through its own pinned
+  // buffers, chunked so the page-cache reads of chunk i+1 overlap the DMA of chunk i
+  int upload_blob(hipStream_t st) {
+    const uint8_t* src = map + h.blob_off;
+    const size_t chunk = size_t(8) << 20;
+    for (size_t off = 0; off < h.blob_len; off += chunk) {
+      const size_t n = h.blob_len - off < chunk ? h.blob_len - off : chunk;
+      hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, src + off, n, hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return fail(std::string("plan: blob H2D failed: ") + hipGetErrorString(e), (int)e);
+    }
+    hipError_t e = hipStreamSynchronize(st);
+    return e == hipSuccess ? 0 : fail("plan: blob H2D sync failed", (int)e);
+  }
+
+  int bind(PlanCtx& c) {
+    c.prog = hz_prog_create();
+    std::vector<uint8_t> buf;
+    for (size_t i = 0; i < ops.size(); ++i) {
+      const PlanOp& op = ops[i];
+      buf.assign(op.prm, op.prm + op.h.plen);
+      buf.resize(op.h.plen + 8);  // slack: no op reads past plen
+      for (uint32_t r = 0; r < op.h.nrel; ++r) {
+        const Reloc& rl = op.rel[r];
+        uint8_t* base = static_cast<uint8_t*>(rl.region == 0 ? blob : rl.region == 1 ? c.dev : c.host);
+        const uint64_t v = reinterpret_cast<uint64_t>(base + rl.roff);
+        std::memcpy(buf.data() + rl.off, &v, 8);
+      }
+      const void* prm = buf.data();
+      int rc = 0;
+      switch (op.h.type) {
+        case HZ_PLAN_OP_CONV:
+          rc = hz_prog_add_conv(c.prog, static_cast<const HzConvParams*>(prm), op.h.arg, op.h.slot);
+          break;
+        case HZ_PLAN_OP_CONV2: {
+          const HzConvParams* a = static_cast<const HzConvParams*>(prm);
+          rc = hz_prog_add_conv2(c.prog, a, a + 1, op.h.arg, op.h.slot);
+          break;
+        }
+        case HZ_PLAN_OP_MAXPOOL:
+          rc = hz_prog_add_maxpool(c.prog, static_cast<const HzPoolParams*>(prm), op.h.slot);
+          break;
+        case HZ_PLAN_OP_AVGPOOL: {
+          const HzAvgpoolArgs* a = static_cast<const HzAvgpoolArgs*>(prm);
+          rc = hz_prog_add_avgpool(c.prog, a->x, a->out, a->N, a->HW, a->C, a->blocked, op.h.slot);
+          break;
+        }
+        case HZ_PLAN_OP_PREPROCESS: {
+          const HzPreprocessArgs* a = static_cast<const HzPreprocessArgs*>(prm);
+          rc = hz_prog_add_preprocess(c.prog, a->src, a->dst, a->N, a->Cin, a->H, a->W, a->Cpad, a->mode, a->mean,
+                                      a->inv_std, op.h.slot);
+          break;
+        }
+        case HZ_PLAN_OP_MEMCPY: {
+          const HzMemcpyArgs* a = static_cast<const HzMemcpyArgs*>(prm);
+          rc = hz_prog_add_memcpy(c.prog, a->dst, a->src, a->bytes, op.h.slot);
+          break;
+        }
+        case HZ_PLAN_OP_KERNEL: rc = hz_prog_add_kernel(c.prog, op.h.arg, prm, op.h.plen, op.h.slot); break;
+        case HZ_PLAN_OP_FORK: rc = hz_prog_add_fork(c.prog, op.h.slot); break;
+        case HZ_PLAN_OP_JOIN: rc = hz_prog_add_join(c.prog, op.h.slot); break;
+        default: return fail("plan: unknown op type " + std::to_string(op.h.type));
+      }
+      if (rc) return fail("plan: binding op " + std::to_string(i) + " failed", rc);
+    }
+    return 0;
+  }
+
+  int add_contexts(int n, int capture) {
+    for (int k = 0; k < n; ++k) {
+      PlanCtx c;
+      double t0 = now_ms();
+      hipError_t e = hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipMalloc(&c.dev, h.ctx_dev_bytes ? h.ctx_dev_bytes : 256);
+      if (e == hipSuccess && h.ctx_dev_bytes) e = hipMemsetAsync(c.dev, 0, h.ctx_dev_bytes, c.st);
+      if (e == hipSuccess) e = hipHostMalloc(&c.host, h.ctx_host_bytes ? h.ctx_host_bytes : 256, hipHostMallocDefault);
+      if (e != hipSuccess) {
+        free_ctx(c);
+        return fail(std::string("plan: context allocation failed: ") + hipGetErrorString(e), (int)e);
+      }
+      std::memset(c.host, 0, h.ctx_host_bytes);
+      double t1 = now_ms();
+      int rc = bind(c);
+      double t2 = now_ms();
+      if (!rc && capture) rc = hz_prog_capture(c.prog, c.st);
+      if (!rc && hipStreamSynchronize(c.st) != hipSuccess) rc = fail("plan: context sync failed");
+      double t3 = now_ms();
+      if (rc) {
+        if (g_err.empty()) g_err = "plan: capture failed rc=" + std::to_string(rc);
+        free_ctx(c);
+        return rc;
+      }
+      t[HZ_PLAN_T_CTX_ALLOC] += t1 - t0;
+      t[HZ_PLAN_T_BIND] += t2 - t1;
+      t[HZ_PLAN_T_CAPTURE] += t3 - t2;
+      std::lock_guard<std::mutex> g(mu);
+      ctx.push_back(c);
+    }
+    return 0;
+  }
+};
+
+Plan* P(void* h) { return static_cast<Plan*>(h); }
+
+}  // namespace
+
+extern "C" {
+
+uint64_t hz_abi_version(void) {
+  // FNV-1a over the plan format version and every struct a plan serialises: a library whose
+  // parameter layouts changed refuses old plans instead of launching garbage
+  const uint64_t parts[] = {kPlanVersion,
+                            sizeof(HzConvParams),
+                            sizeof(HzPoolParams),
+                            sizeof(HzPoolFcParams),
+                            sizeof(HzLayerNormParams),
+                            sizeof(HzEmbedParams),
+                            sizeof(HzAttentionParams),
+                            sizeof(HzVitTokensParams),
+                            sizeof(HzSoftmaxParams),
+                            sizeof(HzQuantParams),
+                            sizeof(HzGemmFp8Params),
+                            sizeof(HzLstmParams),
+                            sizeof(HzDecoderParams),
+                            sizeof(HzSamplerParams),
+                            sizeof(HzAvgpoolArgs),
+                            sizeof(HzPreprocessArgs),
+                            sizeof(HzMemcpyArgs),
+                            HZ_ABI_EPOCH};
+  uint64_t x = 1469598103934665603ull;
+  for (uint64_t v : parts) {
+    x ^= v;
+    x *= 1099511628211ull;
+  }
+  return x & 0x7fffffffffffffffull;
+}
+
+const char* hz_plan_last_error(void) { return g_err.c_str(); }
+
+void* hz_plan_open(const char* path, int device, int read_blob, double* timings) {
+  g_err.clear();
+  double t0 = now_ms();
+  auto* p = new Plan();
+  p->device = device;
+  p->fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (p->fd < 0) {
+    fail(std::string("plan: cannot open ") + path);
+    delete p;
+    return nullptr;
+  }
+  struct stat st {};
+  fstat(p->fd, &st);
+  p->map_len = (size_t)st.st_size;
+  void* m = mmap(nullptr, p->map_len, PROT_READ, MAP_PRIVATE, p->fd, 0);
+  if (m == MAP_FAILED) {
+    fail("plan: mmap failed");
+    delete p;
+    return nullptr;
+  }
+  p->map = static_cast<uint8_t*>(m);
+  if (p->parse()) {
+    delete p;
+    return nullptr;
+  }
+  // the weights are read once, sequentially
+  madvise(p->map + (p->h.blob_off & ~size_t(4095)), p->h.blob_len, MADV_SEQUENTIAL | MADV_WILLNEED);
+  double t1 = now_ms();
+  p->t[HZ_PLAN_T_PARSE] = t1 - t0;
+  // first HIP call of a fresh process: runtime + device initialisation
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipFree(nullptr);
+  double t2 = now_ms();
+  p->t[HZ_PLAN_T_HIP_INIT] = t2 - t1;
+  if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);
+  if (e != hipSuccess) {
+    fail(std::string("plan: device init/alloc failed: ") + hipGetErrorString(e));
+    delete p;
+    return nullptr;
+  }
+  if (read_blob) {
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || p->upload_blob(s)) {
+      if (g_err.empty()) fail("plan: stream creation failed");
+      delete p;
+      return nullptr;
+    }
+    (void)hipStreamDestroy(s);
+  }
+  p->t[HZ_PLAN_T_UPLOAD] = now_ms() - t2;
+  if (timings) std::memcpy(timings, p->t, sizeof(p->t));
+  return p;
+}
+
+int hz_plan_add_contexts(void* h, int n, int capture) {
+  g_err.clear();
+  if (hipSetDevice(P(h)->device) != hipSuccess) return fail("plan: hipSetDevice failed");
+  return P(h)->add_contexts(n, capture);
+}
+
+int hz_plan_num_contexts(void* h) {
+  std::lock_guard<std::mutex> g(P(h)->mu);
+  return (int)P(h)->ctx.size();
+}
+
+void hz_plan_timings(void* h, double* out) { std::memcpy(out, P(h)->t, sizeof(P(h)->t)); }
+
+void* hz_plan_blob(void* h, uint64_t* bytes) {
+  if (bytes) *bytes = P(h)->h.blob_len;
+  return P(h)->blob;
+}
+
+void* hz_plan_host(void* h, int ctx) {
+  std::lock_guard<std::mutex> g(P(h)->mu);
+  return ctx < (int)P(h)->ctx.size() ? P(h)->ctx[ctx].host : nullptr;
+}
+
+void* hz_plan_device(void* h, int ctx) {
+  std::lock_guard<std::mutex> g(P(h)->mu);
+  return ctx < (int)P(h)->ctx.size() ? P(h)->ctx[ctx].dev : nullptr;
+}
+
+void* hz_plan_stream(void* h, int ctx) {
+  std::lock_guard<std::mutex> g(P(h)->mu);
+  return ctx < (int)P(h)->ctx.size() ? (void*)P(h)->ctx[ctx].st : nullptr;
+}
+
+static PlanCtx get_ctx(Plan* p, int i) {
+  std::lock_guard<std::mutex> g(p->mu);
+  return i >= 0 && i < (int)p->ctx.size() ? p->ctx[i] : PlanCtx{};
+}
+
+int hz_plan_replay(void* h, int ctx) {
+  PlanCtx c = get_ctx(P(h), ctx);
+  if (!c.prog) return fail("plan: no such context");
+  return hz_prog_replay(c.prog, c.st);
+}
+
+int hz_plan_sync(void* h, int ctx) {
+  PlanCtx c = get_ctx(P(h), ctx);
+  if (!c.st) return fail("plan: no such context");
+  return (int)hipStreamSynchronize(c.st);
+}
+
+// one request on context `ctx`: copy the payload into the pinned input, replay, wait, copy the
+// result out (called from Python with the GIL released, one thread per in-flight request)
+int hz_plan_infer(void* h, int ctx, const void* in, uint64_t in_off, uint64_t in_bytes, void* out, uint64_t out_off,
+                  uint64_t out_bytes) {
+  Plan* p = P(h);
+  PlanCtx c = get_ctx(p, ctx);
+  if (!c.prog) return fail("plan: no such context");
+  if (in_off + in_bytes > p->h.ctx_host_bytes || out_off + out_bytes > p->h.ctx_host_bytes)
+    return fail("plan: I/O outside the host block");
+  uint8_t* host = static_cast<uint8_t*>(c.host);
+  if (in && in_bytes) std::memcpy(host + in_off, in, in_bytes);
+  int rc = hz_prog_replay(c.prog, c.st);
+  if (rc) return fail("plan: replay failed", rc);
+  hipError_t e = hipStreamSynchronize(c.st);
+  if (e != hipSuccess) return fail(std::string("plan: sync failed: ") + hipGetErrorString(e), (int)e);
+  if (out && out_bytes) std::memcpy(out, host + out_off, out_bytes);
+  return 0;
+}
+
+double hz_plan_bench(void* h, int iters) {
+  Plan* p = P(h);
+  std::vector<HzProgram> progs;
+  std::vector<hipStream_t> sts;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    for (auto& c : p->ctx) {
+      progs.push_back(c.prog);
+      sts.push_back(c.st);
+    }
+  }
+  return hz_prog_bench(progs.data(), sts.data(), (int)progs.size(), iters);
+}
+
+HzProgram hz_plan_prog(void* h, int ctx) { return get_ctx(P(h), ctx).prog; }
+
+void hz_plan_close(void* h) { delete P(h); }
+
+}  // extern "C"

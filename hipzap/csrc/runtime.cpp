@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <thread>
@@ -226,6 +227,38 @@ int hz_prog_bench2(HzProgram* progs, hipStream_t* streams, int n, int iters, int
   auto t2 = std::chrono::steady_clock::now();
   out[0] = std::chrono::duration<double, std::micro>(t1 - t0).count();
   out[1] = std::chrono::duration<double, std::micro>(t2 - t0).count();
+  return rc;
+}
+
+// Closed-loop serving benchmark: one host thread per context, each serving `iters` requests
+// back to back the way a request thread does: copy the payload into the pinned input, replay,
+// wait for THIS request's completion, copy the result out. Per-request latency (submission ->
+// result in host memory) goes to lat_us[ctx * iters + i]; wall_us = total wall time. Unlike
+// hz_prog_bench (replays queued back to back, no host work), every request here pays its own
+// host copies and synchronisation, so throughput and p99 are what concurrent clients see.
+int hz_serve_bench(HzProgram* progs, hipStream_t* streams, void** in_dst, void** in_src, uint64_t in_bytes,
+                   void** out_src, void** out_dst, uint64_t out_bytes, int n, int iters, double* lat_us,
+                   double* wall_us) {
+  std::vector<std::thread> th;
+  std::vector<int> rcs(n, 0);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] {
+      for (int it = 0; it < iters && !rcs[i]; ++it) {
+        auto a = std::chrono::steady_clock::now();
+        if (in_bytes) memcpy(in_dst[i], in_src[i], in_bytes);
+        int rc = hz_prog_replay(progs[i], streams[i]);
+        if (!rc) rc = (int)hipStreamSynchronize(streams[i]);
+        if (!rc && out_bytes) memcpy(out_dst[i], out_src[i], out_bytes);
+        rcs[i] = rc;
+        lat_us[(size_t)i * iters + it] =
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count();
+      }
+    });
+  for (auto& t : th) t.join();
+  *wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  int rc = 0;
+  for (int r : rcs) rc |= r;
   return rc;
 }
 

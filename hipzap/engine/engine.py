@@ -16,7 +16,7 @@ import torch
 
 from .. import _native
 from ..models import registry
-from .program import ExecContext, bench_contexts
+from .program import ExecContext, bench_contexts, serve_bench_contexts
 
 
 def load_tuning(model: str, batch: int, contexts: int = 1) -> dict | None:
@@ -86,6 +86,8 @@ class Engine:
         self._rr = 0
         self._locks = [threading.Lock() for _ in self.contexts]
         self._rr_lock = threading.Lock()
+        self._build_lock = threading.Lock()  # ensure_contexts from concurrent request threads
+        self._exec = None
 
     def _new_contexts(self, n: int):
         ctxs = [ExecContext(self.graph, self.params, self.device, self.tuned, host_io=self.host_io,
@@ -98,22 +100,24 @@ class Engine:
                 c.capture(s)
 
     def ensure_contexts(self) -> float:
-        """Plan + capture the contexts deferred by ``eager_contexts``; returns the ms spent."""
-        n = self.num_contexts - len(self.contexts)
-        if n <= 0:
-            return 0.0
-        t0 = time.perf_counter()
-        with torch.cuda.device(self.device):
-            ctxs, sts = self._new_contexts(n)
-            self._capture_all(ctxs, sts)
-            torch.cuda.synchronize(self.device)
-        with self._rr_lock:  # lists grow in step; _pick reads len(self.contexts) under this lock
-            self._locks += [threading.Lock() for _ in ctxs]
-            self.streams += sts
-            self.contexts += ctxs
-        ms = (time.perf_counter() - t0) * 1e3
-        self.timings["deferred_contexts_ms"] = ms
-        return ms
+        """Plan + capture the contexts deferred by ``eager_contexts``; returns the ms spent.
+        Safe to call from several request threads: one builds, the others find nothing to do."""
+        with self._build_lock:
+            n = self.num_contexts - len(self.contexts)
+            if n <= 0:
+                return 0.0
+            t0 = time.perf_counter()
+            with torch.cuda.device(self.device):
+                ctxs, sts = self._new_contexts(n)
+                self._capture_all(ctxs, sts)
+                torch.cuda.synchronize(self.device)
+            with self._rr_lock:  # lists grow in step; _pick reads len(self.contexts) under this lock
+                self._locks += [threading.Lock() for _ in ctxs]
+                self.streams += sts
+                self.contexts += ctxs
+            ms = (time.perf_counter() - t0) * 1e3
+            self.timings["deferred_contexts_ms"] = ms
+            return ms
 
     # -------------------------------------------------------------- construction
     @classmethod
@@ -177,10 +181,47 @@ class Engine:
             self._rr = (self._rr + 1) % len(self.contexts)
         return i
 
+    # -------------------------------------------------------------- request executor
+    def executor(self):
+        """The native request executor over all contexts (csrc/executor.cpp), built once every
+        context exists (host-I/O, captured engines only); None otherwise."""
+        ex = self._exec
+        if ex is not None or not (self.host_io and self._capture and len(self.contexts) == self.num_contexts):
+            return ex
+        from ..executor import Executor
+        with self._build_lock:
+            if self._exec is None:
+                for lk in self._locks:  # no request may be in flight on the legacy path meanwhile
+                    lk.acquire()
+                try:
+                    cs = self.contexts
+                    self._exec = Executor(
+                        [c.prog for c in cs], [s.cuda_stream for s in self.streams],
+                        [[c.host_inputs[k].data_ptr() for c in cs] for k in range(len(cs[0].host_inputs))],
+                        [h.numel() * h.element_size() for h in cs[0].host_inputs],
+                        [c.host_output.data_ptr() for c in cs],
+                        cs[0].host_output.numel() * cs[0].host_output.element_size())
+                finally:
+                    for lk in self._locks:
+                        lk.release()
+        return self._exec
+
     def infer(self, x) -> torch.Tensor:
         """Run one request; ``x`` is the graph input tensor, or a list of tensors for
-        multi-input graphs (BERT: ids, token types, additive mask). Returns host output."""
+        multi-input graphs (BERT: ids, token types, additive mask). Returns host output.
+        Thread-safe: concurrent callers are served by the native executor (one submission
+        thread, callers sleep until their own replay completes)."""
         xs = list(x) if isinstance(x, (list, tuple)) else [x]
+        ex = self.executor()
+        if ex is not None:
+            c0 = self.contexts[0]
+            ins = [xi.to(hb.dtype).reshape(hb.shape).contiguous() for hb, xi in zip(c0.host_inputs, xs)]
+            out = torch.empty_like(c0.host_output)
+            ex.submit([t.data_ptr() for t in ins], out.data_ptr())
+            if _native.DEBUG:
+                from ..utils import kcheck
+                kcheck.check(f"{self.model} infer")
+            return self._post(out)
         i = self._pick()
         ctx, s = self.contexts[i], self.streams[i]
         with self._locks[i], torch.cuda.device(self.device), torch.cuda.stream(s):
@@ -207,18 +248,47 @@ class Engine:
             return self.adapter.postprocess_output(out)
 
     def infer_device(self, x: torch.Tensor, ctx_index: int = 0) -> torch.Tensor:
-        """Device-resident variant (no host copies); output aliases the static buffer."""
+        """Device-resident variant (no host copies); output aliases the static buffer.
+
+        Stream-ordered with the CALLER's current stream (where ``x`` was produced, e.g. by a DP
+        scatter, and where the returned output will be read): the context stream waits for the
+        caller before reading ``x``, and the caller waits for the replay before it can touch
+        the output. ``x`` is recorded on the context stream so the caching allocator cannot
+        reuse its memory while the copy is still in flight."""
         ctx, s = self.contexts[ctx_index], self.streams[ctx_index]
-        with torch.cuda.device(self.device), torch.cuda.stream(s):
-            if x is not None:
-                ctx.input.copy_(x.reshape(ctx.input.shape), non_blocking=True)
-            ctx.replay(s)
+        with torch.cuda.device(self.device):
+            caller = torch.cuda.current_stream(self.device)
+            s.wait_stream(caller)
+            with torch.cuda.stream(s):
+                if x is not None:
+                    ctx.input.copy_(x.reshape(ctx.input.shape), non_blocking=True)
+                ctx.replay(s)
+            caller.wait_stream(s)
+        if x is not None and x.is_cuda:
+            x.record_stream(s)
         return ctx.output
 
     def bench(self, iters: int) -> float:
         """Replay all contexts concurrently ``iters`` times (C++ loop); returns seconds."""
         self.ensure_contexts()
         return bench_contexts(self.contexts, self.streams, iters)
+
+    def serve_bench(self, iters: int, payload=None, clients: int | None = None,
+                    mode: str = "executor") -> tuple[float, list]:
+        """Closed-loop serving benchmark: ``clients`` (default: one per context) native client
+        threads each send ``iters`` requests back to back, every request = payload copied into
+        a pinned input, one replay, wait, logits copied out. ``mode="executor"``: through the
+        request executor (the serving path); ``"threads"``: every client drives its own context
+        (launch + hipStreamSynchronize per thread; kept for comparison). Returns (seconds,
+        per-request latencies in ms)."""
+        self.ensure_contexts()
+        c0 = self.contexts[0]
+        p = payload if payload is not None else c0.host_input
+        p = p.to(c0.host_input.dtype).reshape(c0.host_input.shape).contiguous()
+        if mode == "threads":
+            return serve_bench_contexts(self.contexts, self.streams, iters, [p.clone() for _ in self.contexts])
+        ex = self.executor()
+        return ex.bench(clients or len(self.contexts), iters, [p.data_ptr()])
 
     def describe(self) -> dict:
         c = self.contexts[0]

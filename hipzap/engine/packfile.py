@@ -3,8 +3,9 @@
 ``torch.load`` of a standard state_dict stays the public format (reference parity:
 main.py:99). ``hipzap pack`` additionally writes the *packed* device layout (BN folded,
 fragment-major bf16/fp8, padded) as a safetensors file + JSON metadata next to the .pth, keyed
-by the checkpoint's sha256, so a cold start can skip folding/packing and stream the blob
-straight into device memory (safetensors: no pickle, nothing executed on load).
+by the checkpoint's size, mtime and a sampled-content sha256, so a cold start can skip
+folding/packing and stream the blob straight into device memory (safetensors: no pickle,
+nothing executed on load). The torch-free plan image (engine/plan.py) uses the same key.
 """
 from __future__ import annotations
 
@@ -13,8 +14,6 @@ import json
 import os
 
 import torch
-
-from ..parallel.comm import _rebuild, _tensor_fields
 
 
 def _classes():
@@ -32,11 +31,31 @@ def packed_path(ckpt_path: str) -> str:
     return ckpt_path + PACK_SUFFIX
 
 
+def sampled_digest(path: str, chunks: int = 16, chunk: int = 65536) -> str:
+    """sha256 over ``chunks`` evenly spaced 64-KiB windows of the file (plus its size): ~1 MiB
+    read instead of the whole file, but a replaced checkpoint with the same size and a restored
+    mtime still changes it (random-init or fine-tuned weights differ in every window)."""
+    import hashlib
+    h = hashlib.sha256()
+    size = os.path.getsize(path)
+    h.update(str(size).encode())
+    with open(path, "rb") as f:
+        if size <= chunks * chunk:
+            h.update(f.read())
+        else:
+            step = (size - chunk) // (chunks - 1)
+            for i in range(chunks):
+                f.seek(i * step)
+                h.update(f.read(chunk))
+    return h.hexdigest()[:32]
+
+
 def source_stamp(ckpt_path: str) -> dict:
-    """Cheap identity of the source checkpoint (size + mtime): a cold start must not hash a
-    100-MB file to validate its cache (sha256 of ResNet-50's .pth alone costs ~150 ms)."""
+    """Cheap identity of the source checkpoint: size + mtime + a sampled-content digest. A cold
+    start must not hash a 100-MB file to validate its cache (sha256 of ResNet-50's .pth alone
+    costs ~150 ms); the sampled digest reads ~1 MiB."""
     st = os.stat(ckpt_path)
-    return {"size": st.st_size, "mtime_ns": st.st_mtime_ns}
+    return {"size": st.st_size, "mtime_ns": st.st_mtime_ns, "sampled_sha256": sampled_digest(ckpt_path)}
 
 
 def find_packed(ckpt_path: str, model: str) -> str | None:

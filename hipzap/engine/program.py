@@ -48,13 +48,19 @@ def _ln_folded(n) -> bool:
 
 class ExecContext:
     def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
-                 host_io: bool = False, pair_convs: bool | None = None, zero_copy: str | None = None):
+                 host_io: bool = False, pair_convs: bool | None = None, zero_copy: str | None = None,
+                 lib=None):
+        """``lib``: the native library (default) or a recorder with the same ``hz_prog_add_*``
+        surface (engine/plan.py ``PlanRecorder``: binds against CPU tensors and serialises the
+        program as a plan image instead of launching it)."""
         self.graph = g
+        self.recording = lib is not None and getattr(lib, "recording", False)
         self.device = torch.device(device)
         self.params = params
         self._keep: list = []
         self._nslab: dict[int, int] = {}  # stats tensor -> slabs written by its producer (HzLnFold)
-        lib = N.lib()
+        lib = lib if lib is not None else N.lib()
+        self._lib = lib
         offsets, arena_bytes = plan_memory(g)
         self.arena_bytes = arena_bytes
         self.arena = torch.empty(max(arena_bytes, 256), dtype=torch.uint8, device=self.device)
@@ -114,10 +120,10 @@ class ExecContext:
         zc = zero_copy if zero_copy is not None else os.environ.get("HIPZAP_ZERO_COPY", "")
         self.zc_in, self.zc_out = host_io and zc in ("in", "all", "1"), host_io and zc in ("out", "all", "1")
         if host_io:
-            self.host_inputs = [torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype).pin_memory()
-                                for t in g.inputs]
+            pin = (lambda t: t) if self.recording else (lambda t: t.pin_memory())
+            self.host_inputs = [pin(torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype)) for t in g.inputs]
             self.host_input = self.host_inputs[0]
-            self.host_output = torch.zeros(self.output.shape, dtype=self.output.dtype).pin_memory()
+            self.host_output = pin(torch.zeros(self.output.shape, dtype=self.output.dtype))
             for t, hbuf in zip(g.inputs, self.host_inputs):
                 if self.zc_in:
                     self.ext[t] = hbuf
@@ -170,6 +176,8 @@ class ExecContext:
         """Device copy of this GEMM's HzLnFold (csrc/hipzap.h); returns its address. Producers run
         before their consumers, so each stats tensor's slab count is known when it is read."""
         g, a = self.graph, n.attrs
+        if self.recording:  # HzLnFold holds arena pointers in device memory: not relocatable
+            raise NotImplementedError("plan images do not support the folded-LayerNorm GEMMs (HIPZAP_LN_FOLD)")
         f = N.LnFold()
         if a.get("ln_in"):
             pname, st = a["ln_in"]
@@ -256,7 +264,7 @@ class ExecContext:
         elif n.kind == "quant":
             rows, D = g.shape(n.inputs[0])
             prm = fp8.QuantParams(addr(n.inputs[0]), addr(n.outputs[0]), addr(n.outputs[1]), rows, D, D, D)
-            tx.prog_add(self.prog, fp8.K_QUANT, prm, n.slot)
+            tx.prog_add(self.prog, fp8.K_QUANT, prm, n.slot, lib=lib)
         elif n.kind == "gemm_fp8":
             pw = self.params[n.attrs["w"]]
             cfg, kw, key = plan
@@ -270,7 +278,7 @@ class ExecContext:
                                   out8_ptr=addr(n.outputs[0]) if o_mx else 0,
                                   os8_ptr=addr(n.outputs[1]) if o_mx else 0)
             self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
-            tx.prog_add(self.prog, fp8.K_GEMM_FP8, prm, n.slot)
+            tx.prog_add(self.prog, fp8.K_GEMM_FP8, prm, n.slot, lib=lib)
         elif n.kind == "layernorm":
             npar = self.params[n.attrs["p"]]
             res = n.inputs[1] if len(n.inputs) > 1 else None
@@ -280,7 +288,7 @@ class ExecContext:
                                      npar.gamma.data_ptr(), npar.beta.data_ptr(), n.attrs["rows"], D,
                                      n.attrs.get("ldx") or D, D, D, npar.eps, addr(n.outputs[0]) if q8 else 0,
                                      addr(n.outputs[1]) if q8 else 0)
-            tx.prog_add(self.prog, tx.K_LAYERNORM, prm, n.slot)
+            tx.prog_add(self.prog, tx.K_LAYERNORM, prm, n.slot, lib=lib)
         elif n.kind == "attention":
             a = n.attrs
             qkv = n.inputs[0]
@@ -290,27 +298,27 @@ class ExecContext:
             prm = tx.AttentionParams(addr(qkv), addr(mask), 0 if mx else addr(n.outputs[0]), a["B"], a["L"],
                                      a["heads"], 64, g.shape(qkv)[-1], D, 2 * D, D, 0.125,
                                      addr(n.outputs[0]) if mx else 0, addr(n.outputs[1]) if mx else 0)
-            tx.prog_add(self.prog, tx.K_ATTENTION, prm, n.slot)
+            tx.prog_add(self.prog, tx.K_ATTENTION, prm, n.slot, lib=lib)
         elif n.kind == "embed_ln":
             tab, ln = self.params[n.attrs["emb"]], self.params[n.attrs["ln"]]
             rows, D = g.shape(n.outputs[0])
             prm = tx.EmbedParams(addr(n.inputs[0]), addr(n.inputs[1]), tab.word.data_ptr(), tab.pos.data_ptr(),
                                  tab.type.data_ptr(), ln.gamma.data_ptr(), ln.beta.data_ptr(), addr(n.outputs[0]),
                                  rows, n.attrs["L"], D, ln.eps)
-            tx.prog_add(self.prog, tx.K_EMBED, prm, n.slot)
+            tx.prog_add(self.prog, tx.K_EMBED, prm, n.slot, lib=lib)
         elif n.kind == "vit_tokens":
             a = n.attrs
             D = g.shape(n.outputs[0])[-1]
             prm = tx.VitTokensParams(addr(n.inputs[0]), self.params[a["cls"]].data_ptr(),
                                      self.params[a["pos"]].data_ptr(), addr(n.outputs[0]), a["B"], a["np"], D)
-            tx.prog_add(self.prog, tx.K_VIT_TOKENS, prm, n.slot)
+            tx.prog_add(self.prog, tx.K_VIT_TOKENS, prm, n.slot, lib=lib)
         elif n.kind == "pool_fc":
             pc = self.params[n.attrs["w"]]
             nb, h, w, c = g.shape(n.inputs[0])
             assert conv_ops.is_blocked(c) and pc.K == c and pc.ksteps * 32 == c
             prm = vision.PoolFcParams(addr(n.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), addr(n.outputs[0]),
                                       nb, c, h * w, pc.cout, g.shape(n.outputs[0])[-1])
-            tx.prog_add(self.prog, vision.K_POOL_FC, prm, n.slot)
+            tx.prog_add(self.prog, vision.K_POOL_FC, prm, n.slot, lib=lib)
         elif n.kind == "softmax":
             ishape = g.shape(n.inputs[0])
             rows, ld = ishape[0], int(torch.tensor(ishape[1:]).prod())
@@ -318,7 +326,7 @@ class ExecContext:
             D = n.attrs.get("D") or ld
             prm = tx.SoftmaxParams(addr(n.inputs[0]), 0, addr(n.outputs[0]), rows, D, ld, g.shape(n.outputs[0])[-1],
                                    int(src.dtype == torch.bfloat16), float(n.attrs.get("scale", 1.0)))
-            tx.prog_add(self.prog, tx.K_SOFTMAX, prm, n.slot)
+            tx.prog_add(self.prog, tx.K_SOFTMAX, prm, n.slot, lib=lib)
         elif n.kind == "fork":
             N.check(lib.hz_prog_add_fork(self.prog, n.slot), "fork")
         elif n.kind == "join":
@@ -366,7 +374,7 @@ class ExecContext:
     def __del__(self):
         try:
             if getattr(self, "prog", None):
-                N.lib().hz_prog_destroy(self.prog)
+                self._lib.hz_prog_destroy(self.prog)
                 self.prog = None
         except Exception:
             pass
@@ -391,3 +399,26 @@ def bench_contexts(ctxs: list, streams: list, iters: int, threads: bool | None =
     if us < 0:
         raise RuntimeError(f"hz_prog_bench failed ({us})")
     return us * 1e-6
+
+
+def serve_bench_contexts(ctxs: list, streams: list, iters: int, payloads: list | None = None) -> tuple[float, list]:
+    """Closed-loop serving benchmark over host-I/O contexts (csrc/runtime.cpp hz_serve_bench):
+    one native thread per context, each request = copy its payload into the pinned input,
+    replay, wait, copy the logits out. Returns (seconds, per-request latencies in ms)."""
+    n = len(ctxs)
+    assert all(c.host_io for c in ctxs), "serve_bench needs host-I/O contexts"
+    in_bytes = ctxs[0].host_input.numel() * ctxs[0].host_input.element_size()
+    out_bytes = ctxs[0].host_output.numel() * ctxs[0].host_output.element_size()
+    if payloads is None:
+        payloads = [c.host_input.clone() for c in ctxs]
+    outs = [c.host_output.clone() for c in ctxs]
+    V = C.c_void_p * n
+    lat = (C.c_double * (n * iters))()
+    wall = C.c_double()
+    rc = N.lib().hz_serve_bench(V(*[c.prog for c in ctxs]), V(*[s.cuda_stream for s in streams]),
+                                V(*[c.host_input.data_ptr() for c in ctxs]), V(*[p.data_ptr() for p in payloads]),
+                                in_bytes, V(*[c.host_output.data_ptr() for c in ctxs]),
+                                V(*[o.data_ptr() for o in outs]), out_bytes, n, iters, lat, C.byref(wall))
+    if rc:
+        raise RuntimeError(f"hz_serve_bench failed ({rc})")
+    return wall.value * 1e-6, [v * 1e-3 for v in lat]

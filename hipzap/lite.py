@@ -1,0 +1,233 @@
+"""Torch-free serving runtime over plan images (``.hzplan``, engine/plan.py + csrc/plan.cpp).
+
+The serverless cold path: process start -> ctypes load of
+``libhipzap.so`` -> mmap the plan -> HIP init -> one DMA of the packed weights -> bind +
+capture -> first request. Nothing here imports torch (``import torch`` alone is ~1.5 s of a
+~2 s cold process); requests are plain byte buffers (a decoded uint8 HWC image for the vision
+models) and results come back as ``array.array`` (or numpy, if the caller asks and has it).
+
+Concurrency mirrors :class:`hipzap.engine.engine.Engine`: N contexts (own arena, pinned I/O,
+stream and captured graph) over one weight blob; ``infer`` releases the GIL inside the native
+call, so request threads overlap.
+"""
+from __future__ import annotations
+
+import array
+import ctypes as C
+import json
+import struct
+import threading
+import time
+
+from . import _native as N
+
+HEADER = struct.Struct("<8s15Q")
+PHASES = ("parse_ms", "hip_init_ms", "upload_ms", "ctx_alloc_ms", "bind_ms", "capture_ms")
+_TYPECODE = {"float32": "f", "uint8": "B", "int32": "i", "int64": "q", "bfloat16": "H", "float16": "H"}
+
+
+class PlanError(RuntimeError):
+    pass
+
+
+def lib():
+    """The native library (plan prototypes are registered by hipzap._native)."""
+    return N.lib()
+
+
+def read_meta(path: str) -> dict:
+    """The plan's JSON metadata (model, I/O offsets and shapes, launch configs, source stamp)."""
+    with open(path, "rb") as f:
+        hdr = f.read(HEADER.size)
+        if len(hdr) < HEADER.size or hdr[:8] != b"HZPLAN01":
+            raise PlanError(f"{path}: not a hipzap plan image")
+        fields = HEADER.unpack(hdr)
+        meta_off, meta_len = fields[4], fields[5]
+        f.seek(meta_off)
+        meta = json.loads(f.read(meta_len))
+    meta["abi"] = fields[2]
+    return meta
+
+
+def plan_usable(path: str) -> bool:
+    """True if ``path`` is a plan image this library build can load (same native ABI)."""
+    try:
+        return read_meta(path)["abi"] == lib().hz_abi_version()
+    except (OSError, PlanError, ValueError, KeyError):
+        return False
+
+
+def _in_buffer(x):
+    """(address, nbytes, keepalive) of a host buffer: bytes, bytearray, memoryview, numpy array
+    or CPU torch tensor (duck-typed: torch is never imported here)."""
+    if hasattr(x, "data_ptr") and hasattr(x, "element_size"):  # torch.Tensor
+        x = x.contiguous()
+        return x.data_ptr(), x.numel() * x.element_size(), x
+    if hasattr(x, "__array_interface__") and hasattr(x, "ctypes"):  # numpy
+        if not x.flags["C_CONTIGUOUS"]:
+            x = x.copy(order="C")
+        return x.ctypes.data, x.nbytes, x
+    if isinstance(x, bytes):
+        return C.cast(C.c_char_p(x), C.c_void_p).value, len(x), x
+    mv = memoryview(x).cast("B")
+    if mv.readonly:
+        b = bytes(mv)
+        return C.cast(C.c_char_p(b), C.c_void_p).value, len(b), b
+    buf = (C.c_char * mv.nbytes).from_buffer(mv)
+    return C.addressof(buf), mv.nbytes, buf
+
+
+class PlanEngine:
+    """One plan image on one GPU. ``read_blob=False`` + ``fill_blob(address, nbytes)`` lets a DP
+    rank receive the weights by RCCL broadcast instead of reading the file."""
+
+    def __init__(self, path: str, device: int = 0, contexts: int = 1, eager_contexts: int | None = None,
+                 capture: bool = True, read_blob: bool = True, fill_blob=None):
+        t0 = time.perf_counter()
+        self.path = path
+        self.meta = read_meta(path)
+        self.device = device
+        L = lib()
+        if self.meta["abi"] != L.hz_abi_version():
+            raise PlanError(f"{path}: plan written for native ABI {self.meta['abi']}, library is "
+                            f"{L.hz_abi_version()} (re-export with `hipzap plan`)")
+        tm = (C.c_double * 8)()
+        h = L.hz_plan_open(path.encode(), device, int(read_blob), tm)
+        if not h:
+            raise PlanError(L.hz_plan_last_error().decode())
+        self._h = h
+        self.timings = {"meta_ms": 0.0}
+        if fill_blob is not None:
+            nb = C.c_uint64()
+            addr = L.hz_plan_blob(h, C.byref(nb))
+            ta = time.perf_counter()
+            fill_blob(addr, nb.value)
+            self.timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
+        self.num_contexts = contexts
+        self._capture = bool(capture)
+        n0 = contexts if eager_contexts is None else max(1, min(eager_contexts, contexts))
+        self._check(L.hz_plan_add_contexts(h, n0, int(capture)), "add_contexts")
+        self._locks = [threading.Lock() for _ in range(n0)]
+        self._rr, self._rr_lock, self._build_lock = 0, threading.Lock(), threading.Lock()
+        self._exec = None
+        L.hz_plan_timings(h, tm)
+        self.timings.update({k: tm[i] for i, k in enumerate(PHASES)})
+        self.timings["total_ms"] = (time.perf_counter() - t0) * 1e3
+        inp, out = self.meta["inputs"], self.meta["output"]
+        self.in_specs = inp
+        self.out_spec = out
+        self._out_n = out["bytes"] // array.array(_TYPECODE[out["dtype"]]).itemsize
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise PlanError(f"{what} failed ({rc}): {lib().hz_plan_last_error().decode()}")
+
+    # ---------------------------------------------------------------- contexts
+    def ensure_contexts(self) -> float:
+        """Build the contexts deferred by ``eager_contexts`` (thread-safe); returns ms spent."""
+        with self._build_lock:
+            have = lib().hz_plan_num_contexts(self._h)
+            n = self.num_contexts - have
+            if n <= 0:
+                return 0.0
+            t0 = time.perf_counter()
+            self._check(lib().hz_plan_add_contexts(self._h, n, int(self._capture)), "add_contexts")
+            with self._rr_lock:
+                self._locks += [threading.Lock() for _ in range(n)]
+            return (time.perf_counter() - t0) * 1e3
+
+    @property
+    def contexts(self) -> int:
+        return len(self._locks)
+
+    def executor(self):
+        """Native request executor over all contexts, once every context exists (else None)."""
+        ex = getattr(self, "_exec", None)
+        if ex is not None or not self._capture or len(self._locks) != self.num_contexts:
+            return ex
+        from .executor import Executor
+        with self._build_lock:
+            if getattr(self, "_exec", None) is None:
+                for lk in self._locks:
+                    lk.acquire()
+                try:
+                    L, n = lib(), len(self._locks)
+                    hosts = [L.hz_plan_host(self._h, i) for i in range(n)]
+                    self._exec = Executor([L.hz_plan_prog(self._h, i) for i in range(n)],
+                                          [L.hz_plan_stream(self._h, i) for i in range(n)],
+                                          [[h + sp["off"] for h in hosts] for sp in self.in_specs],
+                                          [sp["bytes"] for sp in self.in_specs],
+                                          [h + self.out_spec["off"] for h in hosts], self.out_spec["bytes"])
+                finally:
+                    for lk in self._locks:
+                        lk.release()
+        return self._exec
+
+    def _pick(self) -> int:
+        with self._rr_lock:
+            i = self._rr % len(self._locks)
+            self._rr += 1
+        return i
+
+    # ---------------------------------------------------------------- requests
+    def infer_raw(self, x, ctx: int | None = None) -> array.array:
+        """One request: ``x`` = the input's exact bytes (uint8 HWC image for the ResNet plans).
+        Returns the output as a flat ``array.array`` (float32 logits)."""
+        if len(self.in_specs) != 1:
+            raise PlanError("multi-input plan: use infer_many")
+        addr, nb, keep = _in_buffer(x)
+        spec = self.in_specs[0]
+        if nb != spec["bytes"]:
+            raise PlanError(f"request is {nb} bytes, plan input {spec['shape']} {spec['dtype']} is {spec['bytes']}")
+        out = array.array(_TYPECODE[self.out_spec["dtype"]], bytes(self.out_spec["bytes"]))
+        oaddr, _ = out.buffer_info()
+        ex = self.executor() if ctx is None else None
+        if ex is not None:
+            ex.submit([addr], oaddr)
+            del keep
+            return out
+        i = self._pick() if ctx is None else ctx
+        with self._locks[i]:
+            rc = lib().hz_plan_infer(self._h, i, addr, spec["off"], nb, oaddr, self.out_spec["off"],
+                                     self.out_spec["bytes"])
+        del keep
+        self._check(rc, "infer")
+        return out
+
+    def infer(self, x, ctx: int | None = None):
+        """Like :meth:`infer_raw`, shaped ``[batch, classes]`` as a numpy array when numpy is
+        importable (it is not needed on the cold path: import happens on first use)."""
+        out = self.infer_raw(x, ctx)
+        try:
+            import numpy as np
+        except ImportError:
+            return out
+        return np.frombuffer(out, dtype=np.float32 if out.typecode == "f" else None).reshape(
+            self.out_spec["shape"][0], -1)
+
+    def bench(self, iters: int) -> float:
+        """Replay every context ``iters`` times from C++ (no host I/O); seconds."""
+        self.ensure_contexts()
+        us = lib().hz_plan_bench(self._h, iters)
+        if us < 0:
+            raise PlanError(f"bench failed ({us})")
+        return us * 1e-6
+
+    def close(self) -> None:
+        ex = getattr(self, "_exec", None)
+        if ex is not None:
+            ex.close()
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            lib().hz_plan_close(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def describe(self) -> dict:
+        return {"model": self.meta["model"], "batch": self.meta["batch"], "contexts": self.contexts,
+                "ops": self.meta["n_ops"], "blob_MB": round(self.meta["blob_bytes"] / 2**20, 2),
+                "timings_ms": {k: round(v, 2) for k, v in self.timings.items()}}

@@ -23,6 +23,16 @@ def names() -> list[str]:
     return sorted(_REG)
 
 
+_HF_NAMES = {"layers": "num_hidden_layers", "hidden": "hidden_size", "heads": "num_attention_heads",
+             "ffn": "intermediate_size"}
+
+
+def _hf_arch(arch: dict, **extra) -> dict:
+    """hipzap cfg keys (``config_from_sd``) -> transformers config kwargs; unknown keys dropped."""
+    names = dict(_HF_NAMES, **extra)
+    return {names[k]: v for k, v in arch.items() if k in names and v is not None}
+
+
 class VisionAdapter:
     arch = "resnet50"
     num_classes = 1000
@@ -39,9 +49,10 @@ class VisionAdapter:
             raise ValueError(f"checkpoint is {arch}, engine expects {self.arch}")
         return pack_resnet(sd, device), {"num_classes": ncls}
 
-    def meta_params(self, num_classes=None):
+    def meta_params(self, num_classes=None, **_arch):
         """Packed-parameter shapes without weights (meta tensors): what non-root DP ranks
-        allocate before receiving the broadcast blob."""
+        allocate before receiving the broadcast blob. Keyword arguments are the source rank's
+        broadcast architecture metadata (``pack``'s cfg), so a non-default head is honoured."""
         from .resnet import pack_resnet
         with torch.device("meta"):
             m = self.make_model(num_classes)
@@ -82,11 +93,11 @@ class TextClassifierAdapter:
         cfg["seq_len"] = self.seq_len
         return params, cfg
 
-    def meta_params(self, num_labels=2):
-        from .bert import pack_bert
+    def meta_params(self, num_labels=2, ln_fold=None, **arch):
+        from .bert import make_model, pack_bert
         with torch.device("meta"):
-            m = self.make_model(num_labels)
-        params, cfg = pack_bert(m.state_dict(), "meta")
+            m = make_model(num_labels, **_hf_arch(arch, max_pos="max_position_embeddings"))
+        params, cfg = pack_bert(m.state_dict(), "meta", ln_fold=ln_fold)
         cfg["seq_len"] = self.seq_len
         return params, cfg
 
@@ -122,10 +133,11 @@ class ImageTransformerAdapter(VisionAdapter):
         from .vit import pack_vit
         return pack_vit(sd, device, weights=self.weights)
 
-    def meta_params(self, num_classes=None):
-        from .vit import pack_vit
+    def meta_params(self, num_classes=None, num_labels=None, **arch):
+        from .vit import make_model, pack_vit
         with torch.device("meta"):
-            m = self.make_model(num_classes)
+            m = make_model(num_labels or num_classes or self.num_classes,
+                           **_hf_arch(arch, patch="patch_size", image="image_size"))
         return pack_vit(m.state_dict(), "meta", weights=self.weights)
 
     def build_graph(self, batch=1, **kw):

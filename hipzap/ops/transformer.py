@@ -47,8 +47,9 @@ def launch(kind: int, prm, stream=None):
     N.check(N.lib().hz_launch_kernel(kind, C.byref(prm), N.stream_ptr(stream)), f"kernel {kind}")
 
 
-def prog_add(prog, kind: int, prm, slot: int = 0):
-    N.check(N.lib().hz_prog_add_kernel(prog, kind, C.byref(prm), C.sizeof(prm), slot), f"prog_add {kind}")
+def prog_add(prog, kind: int, prm=None, slot: int = 0, lib=None):
+    lib = lib if lib is not None else N.lib()
+    N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(prm), C.sizeof(prm), slot), f"prog_add {kind}")
 
 
 @dataclass

@@ -108,27 +108,69 @@ def unpack_blob(blob: torch.Tensor, meta_params: dict) -> dict:
     return {k: _rebuild(meta_params[k], fields[k]) for k in meta_params}
 
 
-def broadcast_params(params: dict | None, meta_params, device, src: int = 0, group=None, comm=None) -> dict:
+_NOTSET = object()
+
+
+def broadcast_object(obj, device, src: int = 0, comm=None):
+    """Broadcast a small JSON-serialisable object (length, then bytes) from ``src``."""
+    import json
+    comm = comm or default_comm()
+    if comm.world <= 1:
+        return obj
+    dev = device if device is not None else "cpu"
+    n = torch.zeros(1, dtype=torch.int64, device=dev)
+    data = json.dumps(obj).encode() if comm.rank == src else b""
+    if comm.rank == src:
+        n.fill_(len(data))
+    comm.broadcast(n, src=src)
+    buf = torch.zeros(int(n.item()), dtype=torch.uint8, device=dev)
+    if comm.rank == src:
+        buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    comm.broadcast(buf, src=src)
+    return obj if comm.rank == src else json.loads(bytes(buf.cpu().tolist()).decode())
+
+
+def broadcast_params(params: dict | None, meta_params, device, src: int = 0, group=None, comm=None,
+                     arch_kw=_NOTSET):
     """C1: rank ``src`` sends its packed params; every rank returns params on ``device``.
 
     The blob is broadcast as one message, so it streams over every xGMI link at once
     instead of paying per-tensor launch latency 100+ times. ``meta_params`` (the shapes, as
-    meta tensors) is only needed on the receiving ranks and may be a zero-argument callable so
-    the source rank and single-process runs never build it (it costs a model construction).
+    meta tensors) is only needed on the receiving ranks and may be a callable so the source
+    rank and single-process runs never build it (it costs a model construction).
+
+    ``arch_kw`` (the source's ``pack`` cfg): broadcast first, together with the blob size, so
+    receivers build their layout from the SOURCE's architecture (``meta_params(arch_kw)``)
+    instead of guessing defaults, and a layout mismatch fails loudly before any weight moves.
+    Then the call returns ``(params, arch_kw)``; without it, just ``params``.
     ``comm``: a ``loopback.Comm`` (default: torch.distributed when initialised).
     """
     comm = comm or default_comm(group)
+    with_meta = arch_kw is not _NOTSET
     if comm.world <= 1:
-        return params
+        return (params, arch_kw) if with_meta else params
+    total_src = flat_layout(params)[1] if comm.rank == src else None
+    if with_meta:
+        hdr = broadcast_object({"arch_kw": arch_kw, "blob_bytes": total_src}, device, src, comm)
+        arch_kw = hdr["arch_kw"]
     if comm.rank == src:
         blob = pack_blob(params, device)
         comm.broadcast(blob, src=src)
-        return params
-    meta = meta_params() if callable(meta_params) else meta_params
+        return (params, arch_kw) if with_meta else params
+    if callable(meta_params):
+        meta = meta_params(arch_kw or {}) if with_meta else meta_params()
+    else:
+        meta = meta_params
+    if isinstance(meta, tuple):  # adapter.meta_params() returns (params, cfg)
+        meta = meta[0]
     _, total = flat_layout(meta)
+    if with_meta and total != hdr["blob_bytes"]:
+        raise ValueError(f"packed layout mismatch: source blob is {hdr['blob_bytes']} bytes, this rank's "
+                         f"layout for {arch_kw} is {total}")
     blob = torch.empty(total, dtype=torch.uint8, device=device)
     comm.broadcast(blob, src=src)
-    return unpack_blob(blob, meta)
+    out = unpack_blob(blob, meta)
+    return (out, arch_kw) if with_meta else out
 
 
 def health_check(device=None, comm=None) -> int:
