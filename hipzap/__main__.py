@@ -17,10 +17,18 @@ import sys
 
 
 def cmd_serve(a):
-    from .serve.app import app, serve_threaded
     from .serve.settings import load_settings
     st = load_settings(a.settings, a.stage)
     host, port = a.host or st.host, a.port or st.port
+    if a.gpus and a.gpus > 1:  # one worker process per GPU sharing the listening socket (serve/cluster.py)
+        from .serve.cluster import launch
+        sys.exit(launch(a.gpus, host, port, settings=a.settings, stage=a.stage))
+    from werkzeug.serving import WSGIRequestHandler
+
+    from .serve.app import app, serve_threaded, set_server
+    from .serve.server import ModelServer
+    set_server(ModelServer(st))  # the settings named on the command line, not the default file
+    WSGIRequestHandler.protocol_version = "HTTP/1.1"  # keep-alive: no TCP handshake per request
     print(f"hipzap serving stage {st.stage} on {host}:{port} (models bucket {st.models_bucket!r})", flush=True)
     app.run(host=host, port=port, debug=False, threaded=serve_threaded())
 
@@ -43,7 +51,8 @@ def cmd_pack(a):
 def cmd_plan(a):
     from .engine.plan import export_from_checkpoint
     from .lite import read_meta
-    out = export_from_checkpoint(a.model, a.ckpt, a.out, batch=a.batch, contexts=a.contexts, probs=a.probs)
+    out = export_from_checkpoint(a.model, a.ckpt, a.out, batch=a.batch, contexts=a.contexts, probs=a.probs,
+                                 dp_shard=a.dp_shard)
     m = read_meta(out)
     print(json.dumps({"out": out, "ops": m["n_ops"], "blob_bytes": m["blob_bytes"], "source": m["source"]}))
 
@@ -90,6 +99,7 @@ def main(argv=None):
     s.add_argument("--port", type=int, default=None)
     s.add_argument("--stage", default=None)
     s.add_argument("--settings", default=None)
+    s.add_argument("--gpus", type=int, default=0, help="> 1: data-parallel cluster, one worker process per GPU")
     p = sub.add_parser("pack")
     p.add_argument("--model", required=True)
     p.add_argument("--ckpt", required=True)
@@ -101,6 +111,8 @@ def main(argv=None):
     pl.add_argument("--batch", type=int, default=1)
     pl.add_argument("--contexts", type=int, default=1, help="request concurrency the launch configs are tuned for")
     pl.add_argument("--probs", action="store_true", help="softmax head on device")
+    pl.add_argument("--dp-shard", type=int, default=None,
+                    help="also write <ckpt>.dp<S>.hzplan: the per-GPU shard program of batched DP requests")
     t = sub.add_parser("tune")
     t.add_argument("--model", default="resnet50")
     t.add_argument("--batch", type=int, nargs="+", default=[1])

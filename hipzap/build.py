@@ -22,6 +22,10 @@ CSRC = PKG / "csrc"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libhipzap.so"
 LIB_DEBUG = LIBDIR / "libhipzap_debug.so"  # -DHZ_DEBUG: device-side HZ_DCHECK contracts (csrc/common.h)
+# the RCCL communicator is its own library: only multi-GPU processes map the 570 MB librccl
+LIB_COMM = LIBDIR / "libhipzap_comm.so"
+COMM_SRC = CSRC / "comm"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 OBJDIR = PKG.parent / "build" / "obj"
 ARCH = os.environ.get("HIPZAP_ARCH", "gfx950")
 
@@ -72,8 +76,10 @@ def build(verbose: bool = True, jobs: int | None = None, debug: bool = False) ->
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, debug), srcs))
     live = {o.name for o in objs}
+    stems = {s.stem for s in srcs}
     for stale in OBJDIR.glob("*.o"):  # objects of older source versions (of this variant)
-        if stale.name not in live and ("-dbg-" in stale.name) == debug:
+        stem = stale.name.rsplit("-", 2 if "-dbg-" in stale.name else 1)[0]
+        if stale.name not in live and ("-dbg-" in stale.name) == debug and stem in stems:
             stale.unlink(missing_ok=True)
     key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
     stamp = LIBDIR / (".buildkey_debug" if debug else ".buildkey")
@@ -93,6 +99,32 @@ def build(verbose: bool = True, jobs: int | None = None, debug: bool = False) ->
     return lib
 
 
+def build_comm(verbose: bool = True) -> Path:
+    """``libhipzap_comm.so``: csrc/comm/*.cpp (host code over RCCL), linked against librccl."""
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    objs = [_compile(src) for src in sorted(COMM_SRC.glob("*.cpp"))]
+    key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
+    stamp = LIBDIR / ".buildkey_comm"
+    if LIB_COMM.exists() and stamp.exists() and stamp.read_text() == key:
+        if verbose:
+            print(f"hipzap: {LIB_COMM} up to date")
+        return LIB_COMM
+    tmp = LIB_COMM.with_suffix(".so.tmp")
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-L", str(ROCM / "lib"), "-lrccl", "-ldl",
+           f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(tmp)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"comm link failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, LIB_COMM)
+    stamp.write_text(key)
+    if verbose:
+        print(f"hipzap: built {LIB_COMM}")
+    return LIB_COMM
+
+
 if __name__ == "__main__":
     build(verbose=True, debug="--debug" in sys.argv[1:])
+    if "--debug" not in sys.argv[1:]:
+        build_comm(verbose=True)
     sys.exit(0)

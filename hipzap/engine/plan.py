@@ -174,10 +174,12 @@ def _dtype_name(dt: torch.dtype) -> str:
 
 def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int = 1, contexts: int = 1,
                 zero_copy: str = "all", probs: bool = False, tuned: dict | None = None,
-                source: dict | None = None) -> dict:
+                source: dict | None = None, host_io: bool = True) -> dict:
     """Write a plan image for ``model`` with CPU-resident packed ``params`` (``adapter.pack(sd,
     "cpu")``). ``contexts``: the request concurrency the launch configs are tuned for (the conv
     tables differ for 1 vs 24 streams); any number of contexts can be instantiated at load.
+    ``host_io``: request I/O in pinned host memory (serving, zero-copy by default); False: the
+    inputs/outputs live in the context's device block (a DP shard fed by an RCCL scatter).
     Returns the metadata dict stored in the file."""
     adapter = registry.get(model)
     g = adapter.build_graph(batch=batch, **arch_kw)
@@ -186,14 +188,15 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
     if tuned is None:
         tuned = load_tuning(model, batch, contexts)
     rec = PlanRecorder()
-    ctx = ExecContext(g, params, torch.device("cpu"), tuned, host_io=True, zero_copy=zero_copy, lib=rec)
+    ctx = ExecContext(g, params, torch.device("cpu"), tuned, host_io=host_io, zero_copy=zero_copy if host_io else "",
+                      lib=rec)
     regs = _Regions()
     for obj in params.values():
         for t in _tensors(obj):
             regs.add(t, 0, True)
     for t in ctx._keep:
         regs.add(t, 0, True)
-    host = list(ctx.host_inputs) + [ctx.host_output]
+    host = (list(ctx.host_inputs) + [ctx.host_output]) if host_io else []
     host_ptrs = {h.untyped_storage().data_ptr() for h in host}
     regs.add(ctx.arena, 1, False)
     for tid, t in ctx.ext.items():
@@ -246,17 +249,17 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
         for (off, region, r_off) in rels:
             ops_bytes += RELOC.pack(off, region, blob_off(r_off) if region == 0 else r_off)
 
-    def host_off(t):
-        return regs.resolve(t.data_ptr())[1]
+    def io(t):
+        region, off = regs.resolve(t.data_ptr())
+        return {"region": region, "off": off, "shape": list(t.shape), "dtype": _dtype_name(t.dtype),
+                "bytes": t.numel() * t.element_size()}
 
-    out_spec = ctx.host_output
+    out_spec = ctx.host_output if host_io else ctx.output
     meta = {
         "format": "hzplan", "version": VERSION, "model": model, "batch": batch, "arch_kw": arch_kw,
-        "tuned_contexts": contexts, "zero_copy": zero_copy, "probs": probs,
-        "inputs": [{"off": host_off(h), "shape": list(h.shape), "dtype": _dtype_name(h.dtype),
-                    "bytes": h.numel() * h.element_size()} for h in ctx.host_inputs],
-        "output": {"off": host_off(out_spec), "shape": list(out_spec.shape), "dtype": _dtype_name(out_spec.dtype),
-                   "bytes": out_spec.numel() * out_spec.element_size(),
+        "tuned_contexts": contexts, "zero_copy": zero_copy if host_io else "", "probs": probs, "host_io": host_io,
+        "inputs": [io(h) for h in (ctx.host_inputs if host_io else ctx.inputs)],
+        "output": {**io(out_spec),
                    "num_labels": (getattr(g, "meta", None) or {}).get("num_labels",
                                                                        (getattr(g, "meta", None) or {}).get(
                                                                            "num_classes"))},
@@ -264,6 +267,12 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
         "ctx_dev_bytes": regs.size[1], "ctx_host_bytes": regs.size[2], "blob_bytes": blob_len,
         "arena_bytes": ctx.arena_bytes,
     }
+    import hashlib
+    h = hashlib.sha256()
+    for old, data in keep:  # digest of the blob exactly as written (offsets + bytes)
+        h.update(remap[old][0].to_bytes(8, "little"))
+        h.update(data.numpy().tobytes())
+    meta["blob_sha256"] = h.hexdigest()
     meta_b = json.dumps(meta).encode()
     meta_off = HEADER.size
     ops_off = (meta_off + len(meta_b) + 7) // 8 * 8
@@ -293,7 +302,7 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
 
 
 def export_from_checkpoint(model: str, ckpt: str, path: str | None = None, batch: int = 1, contexts: int = 1,
-                           input_uint8: bool | None = None, **kw) -> str:
+                           input_uint8: bool | None = None, dp_shard: int | None = None, **kw) -> str:
     """``torch.load`` the checkpoint, pack it on the CPU and write its plan image (deploy time,
     ``hipzap plan``); the plan is keyed to the checkpoint's identity (size, mtime, sampled hash)."""
     from .packfile import source_stamp
@@ -307,6 +316,10 @@ def export_from_checkpoint(model: str, ckpt: str, path: str | None = None, batch
         input_uint8 = model.startswith("resnet")
     if input_uint8 and model.startswith("resnet"):
         arch_kw["input_uint8"] = True
+    stamp = source_stamp(ckpt)
+    if dp_shard:  # device-I/O shard program of a DP cluster (serve/cluster.py PlanShardRunner)
+        shard_path = plan_path(ckpt, f"dp{dp_shard}")
+        export_plan(model, params, arch_kw, shard_path, batch=dp_shard, contexts=1, source=stamp, host_io=False)
     path = path or plan_path(ckpt)
-    export_plan(model, params, arch_kw, path, batch=batch, contexts=contexts, source=source_stamp(ckpt), **kw)
+    export_plan(model, params, arch_kw, path, batch=batch, contexts=contexts, source=stamp, **kw)
     return path

@@ -140,10 +140,37 @@ class PlanEngine:
     def contexts(self) -> int:
         return len(self._locks)
 
+    @property
+    def host_io(self) -> bool:
+        return self.meta.get("host_io", True)
+
+    # ---------------------------------------------------------------- device-I/O plans (DP shards)
+    def device_io(self, ctx: int = 0) -> tuple[list, int]:
+        """(input device addresses, output device address) of a device-I/O plan's context."""
+        if self.host_io:
+            raise PlanError("host-I/O plan: requests go through infer/infer_raw")
+        base = lib().hz_plan_device(self._h, ctx)
+        return [base + sp["off"] for sp in self.in_specs], base + self.out_spec["off"]
+
+    def stream(self, ctx: int = 0) -> int:
+        return lib().hz_plan_stream(self._h, ctx)
+
+    def replay(self, ctx: int = 0) -> None:
+        """Enqueue one replay of context ``ctx`` on its stream (no wait)."""
+        self._check(lib().hz_plan_replay(self._h, ctx), "replay")
+
+    def sync(self, ctx: int = 0) -> None:
+        self._check(lib().hz_plan_sync(self._h, ctx), "sync")
+
+    def blob(self) -> tuple[int, int]:
+        """(device address, bytes) of the shared weight blob."""
+        nb = C.c_uint64()
+        return lib().hz_plan_blob(self._h, C.byref(nb)), nb.value
+
     def executor(self):
         """Native request executor over all contexts, once every context exists (else None)."""
         ex = getattr(self, "_exec", None)
-        if ex is not None or not self._capture or len(self._locks) != self.num_contexts:
+        if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts:
             return ex
         from .executor import Executor
         with self._build_lock:
@@ -173,8 +200,8 @@ class PlanEngine:
     def infer_raw(self, x, ctx: int | None = None) -> array.array:
         """One request: ``x`` = the input's exact bytes (uint8 HWC image for the ResNet plans).
         Returns the output as a flat ``array.array`` (float32 logits)."""
-        if len(self.in_specs) != 1:
-            raise PlanError("multi-input plan: use infer_many")
+        if len(self.in_specs) != 1 or not self.host_io:
+            raise PlanError("infer_raw needs a single-input host-I/O plan")
         addr, nb, keep = _in_buffer(x)
         spec = self.in_specs[0]
         if nb != spec["bytes"]:

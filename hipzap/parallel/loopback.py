@@ -20,20 +20,7 @@ import threading
 
 import torch
 
-
-class CommError(RuntimeError):
-    pass
-
-
-class Comm:
-    rank: int = 0
-    world: int = 1
-
-    def broadcast(self, t: torch.Tensor, src: int = 0) -> None: ...
-    def scatter(self, out: torch.Tensor, chunks: list | None, src: int = 0) -> None: ...
-    def gather(self, t: torch.Tensor, outs: list | None, dst: int = 0) -> None: ...
-    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None: ...
-    def barrier(self) -> None: ...
+from .base import Comm, CommError  # noqa: F401  (re-exported: callers import them from here)
 
 
 class SingleComm(Comm):

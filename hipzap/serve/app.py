@@ -6,6 +6,8 @@ Routes (reference: /root/reference/main.py:17-18, 105-112):
   POST /predict     image / tensor classification -> {"model", "top5", "timing_ms", ...}
                     (north-star API; ``model`` selects resnet50 (default), resnet18, ...)
   GET  /health      liveness + loaded models;  GET /metrics  Prometheus text;  GET /  info
+torch is imported lazily: a plan-backed vision model (server.PlanVisionBackend) serves uint8
+images end to end without it (decode -> pinned input -> hipGraph -> top-5 in numpy).
 CORS is applied to every route and origin (main.py:18 used flask_cors, which is not
 installed here: implemented in-house — ``Access-Control-Allow-Origin: *`` plus preflight).
 """
@@ -15,10 +17,10 @@ import base64
 import io
 import json
 import logging
+import sys
 import time
 
 import numpy as np
-import torch
 from flask import Flask, Response, g, request
 
 from .. import __version__
@@ -31,6 +33,14 @@ log = logging.getLogger("hipzap.app")
 
 app = Flask("hipzap")
 _server: ModelServer | None = None
+# DP cluster worker state (serve/cluster.py): batched uint8 requests for the DP model are
+# scattered over every GPU of the node through the cluster's control plane
+CLUSTER: dict = {}
+_DP = {"member": None, "model": None, "item_shape": None}
+
+
+def set_dp(member, model: str | None, item_shape) -> None:
+    _DP.update(member=member, model=model, item_shape=tuple(item_shape) if item_shape else None)
 
 
 def serve_threaded() -> bool:
@@ -132,51 +142,67 @@ def inference():
     return _json({"response": {"text": text}})
 
 
-def decode_input(req) -> tuple[str, torch.Tensor]:
-    """Accepted request bodies:
+def decode_input(req):
+    """-> (model, numpy array). Accepted request bodies:
     * ``application/octet-stream``: a ``.npy`` array (``np.save``; no pickles);
     * JSON ``{"inputs": nested list, "model": ...}`` (float tensor, NCHW or CHW);
-    * JSON ``{"image_b64": base64 uint8 HWC bytes, "shape": [H, W, 3]}`` — normalised with
-      ImageNet mean/std on the way in;
+    * JSON ``{"image_b64": base64 uint8 HWC bytes, "shape": [H, W, 3]}`` (or [N, H, W, 3]);
     * JSON ``{"tensor_b64": base64 float32 bytes, "shape": [...]}``.
-    """
+    uint8 arrays are images (HWC / NHWC), served as is by plan-backed models (normalised on
+    device) and normalised to NCHW float for the others (:func:`to_model_input`)."""
     model = req.args.get("model")
     if req.mimetype == "application/octet-stream":
         arr = np.load(io.BytesIO(req.get_data()), allow_pickle=False)
-        x = torch.from_numpy(np.ascontiguousarray(arr))
     else:
         body = req.get_json(force=True, silent=False)
         model = body.get("model", model)
         if "inputs" in body:
-            x = torch.tensor(body["inputs"], dtype=torch.float32)
+            arr = np.asarray(body["inputs"], dtype=np.float32)
         elif "tensor_b64" in body:
-            raw = base64.b64decode(body["tensor_b64"])
-            x = torch.from_numpy(np.frombuffer(raw, dtype=np.float32).copy()).reshape(body["shape"])
+            arr = np.frombuffer(base64.b64decode(body["tensor_b64"]), dtype=np.float32).reshape(body["shape"])
         elif "image_b64" in body:
-            raw = base64.b64decode(body["image_b64"])
-            img = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).reshape(body["shape"])
-            x = img
+            arr = np.frombuffer(base64.b64decode(body["image_b64"]), dtype=np.uint8).reshape(body["shape"])
         else:
             raise ValueError("request needs one of: inputs, tensor_b64, image_b64 (or an .npy body)")
-    if x.dtype == torch.uint8:  # HWC / NHWC image bytes -> normalised NCHW float
+    if arr.dtype == np.uint8 and arr.ndim == 3:
+        arr = arr[None]
+    return model or get_server().settings.default_model, arr
+
+
+def to_model_input(arr):
+    """numpy request array -> float32 NCHW torch tensor for the torch-built backends."""
+    import torch
+    if arr.dtype == np.uint8:  # NHWC image bytes -> normalised NCHW float
         # in numpy: torch's multi-threaded elementwise ops on this request thread would start an
         # OpenMP team per WSGI thread, spinning against the model's own thread pool
         from ..ops.vision import IMAGENET_MEAN, IMAGENET_STD
-        a = x.numpy()
-        if a.ndim == 3:
-            a = a[None]
-        a = (a.astype(np.float32) * np.float32(1 / 255.0) - np.asarray(IMAGENET_MEAN, np.float32)) \
+        a = (arr.astype(np.float32) * np.float32(1 / 255.0) - np.asarray(IMAGENET_MEAN, np.float32)) \
             / np.asarray(IMAGENET_STD, np.float32)
-        x = torch.from_numpy(np.ascontiguousarray(a.transpose(0, 3, 1, 2)))
-    x = x.float().contiguous()  # NCHW-contiguous: a permuted view sends CPU convs down a slow path
+        arr = a.transpose(0, 3, 1, 2)
+    x = torch.from_numpy(np.require(arr, np.float32, ["C", "W"]))  # NCHW-contiguous (CPU convs), writable
     if x.dim() == 3:
         x = x[None]
-    return model or get_server().settings.default_model, x
+    return x
+
+
+def softmax_np(x):
+    x = np.asarray(x, np.float32)
+    e = np.exp(x - x.max(-1, keepdims=True))
+    return e / e.sum(-1, keepdims=True)
+
+
+def topk_np(p, k: int):
+    """[(indices, values)] per row, highest first."""
+    idx = np.argpartition(-p, k - 1, axis=-1)[:, :k]
+    vals = np.take_along_axis(p, idx, -1)
+    order = np.argsort(-vals, axis=-1)
+    return np.take_along_axis(idx, order, -1), np.take_along_axis(vals, order, -1)
 
 
 def _predict_text(s, body):
     """BERT-style sequence classification: {"model", "input_ids", "token_type_ids"?,
     "attention_mask"?} -> class probabilities."""
+    import torch
     model = body.get("model") or "bert-base"
     ids = torch.tensor(body["input_ids"], dtype=torch.long)
     if ids.dim() == 1:
@@ -205,21 +231,35 @@ def predict():
         if "input_ids" in body:
             return _predict_text(s, body)
     with phase("decode"):
-        model, x = decode_input(request)
+        model, arr = decode_input(request)
     with phase("load"):
         backend = s.vision(model)
     t0 = time.perf_counter()
-    with phase("infer"):
-        logits = backend(x)
+    dp = _DP["member"]
+    if (dp is not None and dp.alive and model == _DP["model"] and arr.dtype == np.uint8 and arr.shape[0] > 1
+            and tuple(arr.shape[1:]) == _DP["item_shape"]):
+        with phase("dp_scatter_gather"):  # C2 scatter -> every GPU's shard -> C3 gather
+            out = dp.submit(arr)
+        logits, probs = out, softmax_np(out)
+    elif arr.dtype == np.uint8 and hasattr(backend, "infer_u8") and backend.accepts_u8(arr.shape):
+        with phase("infer"):  # torch-free: pinned input -> captured graph (preprocess on device)
+            out = backend.infer_u8(arr)
+        logits = None if backend.probs else out
+        probs = out if backend.probs else softmax_np(out)
+    else:
+        x = to_model_input(arr)
+        with phase("infer"):
+            lg = backend(x)
+        logits = lg.float().numpy()
+        probs = softmax_np(logits)
     dt = (time.perf_counter() - t0) * 1e3
-    probs = torch.softmax(logits.float(), dim=-1)
     k = min(5, probs.shape[-1])
-    top = torch.topk(probs, k, dim=-1)
-    out = {"model": model, "backend": backend.backend, "batch": int(x.shape[0]),
-           "top5": [[[int(i), round(float(p), 6)] for i, p in zip(ti, tp)] for ti, tp in zip(top.indices, top.values)],
+    ti, tp = topk_np(probs, k)
+    out = {"model": model, "backend": backend.backend, "batch": int(arr.shape[0]),
+           "top5": [[[int(i), round(float(p), 6)] for i, p in zip(r_i, r_p)] for r_i, r_p in zip(ti, tp)],
            "timing_ms": round(dt, 3)}
-    if request.args.get("logits"):
-        out["logits"] = logits.float().tolist()
+    if request.args.get("logits") and logits is not None:
+        out["logits"] = logits.tolist()
     return _json(out)
 
 
@@ -227,8 +267,18 @@ def predict():
 def health():
     s = get_server()
     info = {"status": "ok", "backend": s.backend, "models": s.loaded()}
+    if CLUSTER:
+        m, c = CLUSTER.get("member"), CLUSTER.get("coordinator")
+        info["cluster"] = {"rank": CLUSTER["rank"], "world": CLUSTER["world"], "device": CLUSTER["device"],
+                           "cold_start_ms": CLUSTER["cold_start_ms"],
+                           "members": m.members if m else None, "epoch": m.epoch if m else None,
+                           "health": m.health if m else None, "dp": _DP["member"] is not None,
+                           "reforms": c.reforms if c else (m.reforms if m else None)}
     if s.backend == "gpu":
-        info["devices"] = [torch.cuda.get_device_name(d) for d in s.settings.devices]
+        info["devices"] = list(s.settings.devices)
+        if "torch" in sys.modules:  # names only when torch is loaded anyway (never imported for this)
+            import torch
+            info["device_names"] = [torch.cuda.get_device_name(d) for d in s.settings.devices]
     return _json(info)
 
 

@@ -8,6 +8,10 @@ captured hipGraphs (the warm path). Backends:
     is visible; the native library is REQUIRED there (no silent eager fallback);
   * ``cpu``: eager PyTorch on the host — the BASELINE config-1 "CPU plumbing" path and the
     development path in GPU-less containers.
+Vision models whose checkpoint has an up-to-date plan image next to it (``<ckpt>.hzplan``,
+``hipzap plan``) are served by :class:`PlanVisionBackend`: torch-free (hipzap/lite.py), uint8
+images straight into the captured graph. torch is imported lazily, only by the paths that
+need it, so a plan-backed server process never pays for it.
 """
 from __future__ import annotations
 
@@ -16,19 +20,17 @@ import os
 import threading
 import time
 
-import torch
-
-from ..models import registry
 from .artifacts import ArtifactStore
 from .settings import ModelSpec, Settings
 from ..utils.tracing import trace_range
 from ..utils.watchdog import maybe_fault
-from .text import generate_text, load_itos, make_stoi
 
 log = logging.getLogger("hipzap.server")
 
 
 def _random_state_dict(name: str, seed: int = 0) -> dict:
+    import torch
+    from ..models import registry
     from ..models.resnet import randomize_bn
     torch.manual_seed(seed)
     m = registry.get(name).make_model()
@@ -48,6 +50,7 @@ def _gpu_engine(name: str, src, device: str, **kw):
 
 
 def _state_dict(src) -> dict:
+    import torch
     if not isinstance(src, str):
         return src
     sd = torch.load(src, map_location="cpu", weights_only=True)
@@ -58,6 +61,7 @@ def _state_dict(src) -> dict:
 
 class VisionBackend:
     def __init__(self, name: str, sd, backend: str, device: str, spec: ModelSpec, capture: bool):
+        from ..models import registry
         self.name, self.backend = name, backend
         t0 = time.perf_counter()
         self.adapter = registry.get(name)
@@ -85,13 +89,15 @@ class VisionBackend:
             self.batcher = DynamicBatcher(self._run_padded, self.batch, float(bcfg.get("max_wait_ms", 2.0)), name)
         self.cold_ms = (time.perf_counter() - t0) * 1e3
 
-    def _run_padded(self, chunk: torch.Tensor) -> torch.Tensor:
+    def _run_padded(self, chunk):
+        import torch
         n = chunk.shape[0]
         if n < self.batch:  # pad the remainder to the captured batch size
             chunk = torch.cat([chunk, chunk.new_zeros((self.batch - n,) + tuple(chunk.shape[1:]))])
         return self.engine.infer(chunk)[:n]
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x):
+        import torch
         if self.engine is not None:
             if self.batcher is not None and x.shape[0] < self.batch:
                 return self.batcher(x)
@@ -105,6 +111,7 @@ class TextBackend:
     """BERT-style sequence classifier; requests are padded to the captured (batch, seq_len)."""
 
     def __init__(self, name: str, sd, backend: str, device: str, spec: ModelSpec, capture: bool):
+        from ..models import registry
         self.name, self.backend = name, backend
         t0 = time.perf_counter()
         self.adapter = registry.get(name)
@@ -125,7 +132,8 @@ class TextBackend:
         self.batch = spec.batch
         self.cold_ms = (time.perf_counter() - t0) * 1e3
 
-    def __call__(self, ids: torch.Tensor, types=None, mask=None) -> torch.Tensor:
+    def __call__(self, ids, types=None, mask=None):
+        import torch
         B, L = ids.shape
         types = types if types is not None else torch.zeros_like(ids)
         mask = mask if mask is not None else torch.ones_like(ids)
@@ -179,6 +187,7 @@ class LMBackend:
 
     def __init__(self, sd: dict, itos: list, backend: str, device: str):
         from ..models.awd_lstm import reference_lm
+        from .text import make_stoi
         t0 = time.perf_counter()
         self.itos, self.stoi = itos, make_stoi(itos)
         self.backend = backend
@@ -195,6 +204,8 @@ class LMBackend:
         self._lock = threading.Lock()
 
     def generate(self, prompt_words, n_words, seed=None) -> str:
+        import torch
+        from .text import generate_text
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         if self.engine is not None:  # pool of independent decode contexts: reentrant
             return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)
@@ -211,12 +222,13 @@ class ModelServer:
         self.settings = settings
         self.store = ArtifactStore(settings.models_bucket, settings.artifact_root)
         if backend is None:
-            backend = os.environ.get("HIPZAP_BACKEND") or ("gpu" if torch.cuda.is_available() else "cpu")
+            backend = os.environ.get("HIPZAP_BACKEND") or ("gpu" if gpu_visible() else "cpu")
         self.backend = backend
         self.device = f"cuda:{settings.devices[0]}" if backend == "gpu" else "cpu"
         self._models: dict = {}
         self._lock = threading.Lock()
         self._watchdog = None
+        self.comm = None  # set by a DP cluster worker (serve/cluster.py): plan weights arrive by RCCL broadcast
         self.stats = {"requests": 0, "errors": 0, "cold_loads": 0}
 
     def spec(self, name: str) -> ModelSpec:
@@ -261,12 +273,46 @@ class ModelServer:
             return self._models[name]
 
     def vision(self, name: str):
+        plan = self._plan_for(name)
+        if plan is not None:
+            with self._lock:
+                if name not in self._models:
+                    spec = self.spec(name)
+                    with trace_range(f"cold_start:{name}"):
+                        self._models[name] = PlanVisionBackend(name, plan, self.settings.devices[0], spec,
+                                                               comm=self.comm)
+                    self.stats["cold_loads"] += 1
+                return self._models[name]
         return self._load(name, VisionBackend)
+
+    def _plan_for(self, name: str) -> str | None:
+        """The up-to-date plan image of this model's checkpoint, if the GPU backend can use it
+        (``extra.plan`` names one explicitly; else ``<ckpt>.hzplan``; HIPZAP_PLAN=0 disables)."""
+        if self.backend != "gpu" or os.environ.get("HIPZAP_PLAN", "1") == "0":
+            return None
+        spec = self.spec(name)
+        if spec.extra.get("plan"):
+            return spec.extra["plan"]
+        if spec.key in (None, "random") or os.environ.get("HIPZAP_RANDOM_WEIGHTS"):
+            return None
+        from ..lite import plan_usable, read_meta
+        from ..engine.packfile import source_stamp
+        ckpt = self.store.fetch(spec.key)
+        path = ckpt + ".hzplan"
+        try:
+            if plan_usable(path) and read_meta(path).get("source") == source_stamp(ckpt) \
+                    and read_meta(path).get("model") == name:
+                return path
+        except OSError:
+            pass
+        return None
 
     def text(self, name: str):
         return self._load(name, TextBackend)
 
     def lm(self) -> LMBackend:
+        import torch
+        from .text import load_itos
         key = "__lm__"
         with self._lock:
             if key not in self._models:
@@ -287,6 +333,73 @@ class ModelServer:
         return {k: {"backend": getattr(v, "backend", "?"), "cold_ms": round(getattr(v, "cold_ms", 0), 1)}
                 for k, v in self._models.items()}
 
+
+def gpu_visible() -> bool:
+    """A GPU is visible to this process (HIP runtime query; torch is not imported)."""
+    try:
+        from ..hip import device_count
+        return device_count() > 0
+    except Exception:
+        return False
+
+
+class PlanVisionBackend:
+    """Torch-free vision serving from a plan image (``hipzap plan``; hipzap/lite.py): a request
+    is a uint8 HWC image (the decoded-JPEG format) copied into a pinned input and one hipGraph
+    replay (device preprocess -> convs -> pool+FC [-> softmax]) through the native request
+    executor. ``comm`` (DP cluster worker): rank 0 reads the weights and RCCL-broadcasts them,
+    the other ranks never read the blob from disk. Other input formats (fp32 NCHW tensors) go
+    to a torch-built :class:`VisionBackend`, constructed on first use."""
+    backend = "gpu"
+
+    def __init__(self, name: str, plan: str, device: int, spec: ModelSpec, comm=None):
+        from ..lite import PlanEngine
+        t0 = time.perf_counter()
+        self.name, self.plan, self.spec, self.device = name, plan, spec, device
+        fill = None
+        if comm is not None and comm.world > 1:
+            fill = lambda addr, n: comm.broadcast_ptr(addr, n, 0)  # noqa: E731
+        self.engine = PlanEngine(plan, device=device, contexts=max(1, spec.contexts), eager_contexts=1,
+                                 read_blob=comm is None or comm.rank == 0, fill_blob=fill)
+        self.meta = self.engine.meta
+        self.in_shape = tuple(self.meta["inputs"][0]["shape"])  # [B, H, W, 3] uint8
+        self.batch = self.in_shape[0]
+        self.probs = bool(self.meta.get("probs"))
+        self.num_labels = self.meta["output"].get("num_labels") or self.meta["output"]["shape"][-1]
+        self._torch, self._torch_lock = None, threading.Lock()
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+        # the other request contexts are built right after the engine is ready (warm scale-up)
+        threading.Thread(target=self.engine.ensure_contexts, daemon=True, name=f"{name}-contexts").start()
+
+    def accepts_u8(self, shape) -> bool:
+        return len(shape) == 4 and tuple(shape[1:]) == self.in_shape[1:]
+
+    def infer_u8(self, imgs):
+        """``imgs``: uint8 numpy array [N, H, W, 3] -> numpy [N, classes] (logits or probs)."""
+        import numpy as np
+        n = imgs.shape[0]
+        out = np.empty((n, self.num_labels), np.float32)
+        B = self.batch
+        for i in range(0, n, B):
+            chunk = imgs[i: i + B]
+            m = chunk.shape[0]
+            if m < B:
+                chunk = np.concatenate([chunk, np.zeros((B - m,) + chunk.shape[1:], np.uint8)])
+            y = np.frombuffer(self.engine.infer_raw(np.ascontiguousarray(chunk)), np.float32)
+            out[i: i + m] = y.reshape(B, -1)[:m, : self.num_labels]
+        return out
+
+    def __call__(self, x):
+        """torch-tensor entry (fp32 NCHW etc.): served by a torch-built engine of the same
+        checkpoint (the plan's source), built on first use."""
+        with self._torch_lock:
+            if self._torch is None:
+                ckpt = self.plan[: -len(".hzplan")]
+                if not os.path.exists(ckpt):
+                    raise ValueError(f"{self.name} is served from a plan image: send uint8 HWC images "
+                                     f"{list(self.in_shape[1:])} (image_b64 or a uint8 .npy)")
+                self._torch = VisionBackend(self.name, ckpt, "gpu", f"cuda:{self.device}", self.spec, True)
+        return self._torch(x)
 
 def synthetic_vocab(n: int) -> list[str]:
     """fastai-style vocabulary for random-weight demos: specials first, then pseudo-words."""

@@ -67,8 +67,8 @@ def apply_environment(cfg: dict, stage: str = DEFAULT_STAGE, environ=None) -> di
 
 def load_settings(path: str | None = None, stage: str | None = None, environ=None) -> Settings:
     environ = os.environ if environ is None else environ
-    stage = stage or environ.get("HIPZAP_STAGE", DEFAULT_STAGE)
-    path = path or environ.get("HIPZAP_SETTINGS", "zappa_settings.json")
+    stage = stage or environ.get("HIPZAP_STAGE") or DEFAULT_STAGE
+    path = path or environ.get("HIPZAP_SETTINGS") or "zappa_settings.json"
     raw = {}
     if path and os.path.exists(path):
         raw = read_zappa_settings(path)

@@ -1,0 +1,134 @@
+"""DP serving cluster on the GPU box (serve/cluster.py):
+* the native RCCL communicator (world 1 here: the box has one GPU; RCCL refuses two ranks on one
+  device) — every collective, async-error polling, a bounded wait;
+* a 2-worker cluster REHEARSAL on the one GPU (HIPZAP_SHARE_GPU=1, socket communicator): the
+  launcher's shared listening socket, rank 0 broadcasting the plan weights to rank 1, bs=1
+  requests on either worker, and a batched POST scattered over both workers' shard programs and
+  gathered back, equal to the single-GPU plan engine's logits."""
+import base64
+import ctypes as C
+import http.client
+import io
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from hipzap.engine.plan import export_from_checkpoint, plan_path
+from hipzap.lite import PlanEngine
+from hipzap.models import registry
+from hipzap.models.resnet import randomize_bn
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rccl_world1_collectives(tmp_path):
+    from hipzap import hip
+    from hipzap.parallel.rccl import FileRendezvous, RcclComm
+    comm = RcclComm.from_rendezvous(FileRendezvous(str(tmp_path)), 1, 0, 0, timeout_s=30)
+    assert comm.world == 1 and comm.rank == 0 and comm.poll() == 0
+    buf = hip.DeviceBuffer(1024)
+    host = (C.c_int * 256)(*range(256))
+    hip.memcpy(buf.ptr, C.addressof(host), 1024, hip.H2D)
+    comm.allreduce_ptr(buf.ptr, 256, "int32", "sum")
+    comm.broadcast_ptr(buf.ptr, 1024, 0)
+    out = hip.DeviceBuffer(1024)
+    comm.scatter_ptr(buf.ptr, out.ptr, 1024, 0)
+    comm.gather_ptr(out.ptr, buf.ptr, 1024, 0)
+    back = (C.c_int * 256)()
+    hip.memcpy(C.addressof(back), buf.ptr, 1024, hip.D2H)
+    assert list(back) == list(range(256))
+    comm.barrier()
+    # the torch-tensor interface (DPExecutor / broadcast_params use it)
+    t = torch.arange(8, dtype=torch.int32, device="cuda:0")
+    comm.all_reduce(t)
+    assert t.tolist() == list(range(8))
+    comm.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _post(port, body, ctype, path="/predict"):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+    c.request("POST", path, body=body, headers={"Content-Type": ctype})
+    r = c.getresponse()
+    return r.status, json.loads(r.read())
+
+
+@pytest.fixture(scope="module")
+def rehearsal(tmp_path_factory):
+    torch.manual_seed(0)
+    d = tmp_path_factory.mktemp("cluster")
+    ckpt = str(d / "resnet50.model.pth")
+    torch.save(randomize_bn(registry.get("resnet50").make_model()).eval().state_dict(), ckpt)
+    plan = export_from_checkpoint("resnet50", ckpt, batch=1, contexts=1, dp_shard=4)
+    settings = str(d / "zappa_settings.json")
+    with open(settings, "w") as f:
+        json.dump({"dev": {"hipzap": {"default_model": "resnet50", "models": {"resnet50": {
+            "contexts": 2, "extra": {"plan": plan, "dp_plan": plan_path(ckpt, "dp4")}}}}}}, f)
+    port = _free_port()
+    env = dict(os.environ, HIPZAP_COMM="socket", HIPZAP_SHARE_GPU="1", HIPZAP_HEALTH_S="1", HIPZAP_LOG="INFO")
+    log = open(d / "cluster.log", "w")
+    p = subprocess.Popen([sys.executable, "-m", "hipzap", "serve", "--gpus", "2", "--settings", settings,
+                          "--host", "127.0.0.1", "--port", str(port)], cwd=ROOT, env=env, stdout=log,
+                         stderr=subprocess.STDOUT)
+    t0 = time.time()
+    seen = set()
+    while time.time() - t0 < 180 and len(seen) < 2:
+        assert p.poll() is None, open(d / "cluster.log").read()[-3000:]
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+            c.request("GET", "/health")
+            h = json.loads(c.getresponse().read())
+            seen.add(h["cluster"]["rank"])
+        except (OSError, KeyError, ValueError):
+            time.sleep(0.2)
+    assert len(seen) == 2, open(d / "cluster.log").read()[-3000:]
+    yield port, plan, d
+    p.terminate()
+    try:
+        p.wait(timeout=30)
+    except subprocess.TimeoutExpired:
+        p.kill()
+    log.close()
+
+
+def test_cluster_bs1_and_batched_scatter_gather(rehearsal):
+    port, plan, d = rehearsal
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (10, 224, 224, 3), dtype=np.uint8)
+    pe = PlanEngine(plan, device=0)
+    ref = np.stack([np.frombuffer(pe.infer_raw(imgs[i: i + 1]), np.float32) for i in range(10)])
+    # bs=1 on whichever worker accepts the connection
+    for i in range(4):
+        st, body = _post(port, json.dumps({"image_b64": base64.b64encode(imgs[i].tobytes()).decode(),
+                                           "shape": [224, 224, 3]}), "application/json", "/predict?logits=1")
+        assert st == 200, body
+        np.testing.assert_array_equal(np.asarray(body["logits"][0], np.float32), ref[i])
+    # a batch of 10 = 2 ranks x shard 4 = 8 per step -> 2 scatter/gather steps, the last one padded
+    buf = io.BytesIO()
+    np.save(buf, imgs)
+    st, body = _post(port, buf.getvalue(), "application/octet-stream", "/predict?logits=1")
+    assert st == 200, body
+    got = np.asarray(body["logits"], np.float32)
+    assert got.shape == (10, 1000)
+    # shard program = batch-4 launches (other tiles than bs=1): equal to bf16 rounding
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 2e-2
+    assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.9
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    c.request("GET", "/health")
+    h = json.loads(c.getresponse().read())["cluster"]
+    assert h["world"] == 2 and h["dp"] and h["members"] == [0, 1]
