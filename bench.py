@@ -223,6 +223,21 @@ def main():
     if args.tuned:
         with open(args.tuned) as f:
             tuned = json.load(f)
+    # C1 weight broadcast over the native RCCL communicator (csrc/comm, the serving cluster's
+    # transport); every rank agrees on it or all fall back to torch.distributed
+    native_comm = None
+    if is_dist() and dist.get_backend() == "nccl" and os.environ.get("HIPZAP_NATIVE_COMM", "1") != "0":
+        ok = 1
+        try:
+            from hipzap.parallel.rccl import RcclComm
+            native_comm = RcclComm.from_torch(device.index, timeout_s=120)
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {rank}: native RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            native_comm = None
     if is_dist():
         dist.barrier()
     if args.mode == "scatter":
@@ -256,7 +271,8 @@ def main():
         else:
             params, arch_kw = None, None
         ta = time.perf_counter()
-        params, arch_kw = broadcast_params(params, lambda kw: adapter.meta_params(**kw), device, arch_kw=arch_kw)
+        params, arch_kw = broadcast_params(params, lambda kw: adapter.meta_params(**kw), device, arch_kw=arch_kw,
+                                           comm=native_comm)
         torch.cuda.synchronize(device)
         timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         arch_kw = dict(arch_kw)
@@ -362,7 +378,9 @@ def main():
             "config": {"model": "ResNet-50", "global_batch": args.batch * world, "seq_len": None,
                        "parallelism": f"dp{world}", "request_batch": args.batch,
                        "streams_per_gpu": args.streams, "hipgraph": not args.no_capture,
-                       "serving": args.serve},
+                       "serving": args.serve,
+                       "weight_broadcast": "native-rccl" if native_comm is not None else
+                       ("torch.distributed" if world > 1 else None)},
             "cold_start_ms_p50": fresh["plan"]["p50_ms"] if fresh else None,
             "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
                                "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict",

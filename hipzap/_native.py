@@ -57,17 +57,19 @@ class LstmParams(C.Structure):
                 ("In", c_int), ("H", c_int), ("ldk", c_int)]
 
 
+class SamplerParams(C.Structure):
+    _fields_ = [("keys", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
+                ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int), ("exclude", c_int * 8),
+                ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int), ("rpb", c_int),
+                ("bacc_val", c_void_p), ("bacc_idx", c_void_p)]
+
+
 class DecoderParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h_state", c_void_p), ("step", c_void_p),
                 ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
                 ("seed", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int),
-                ("rpb", c_int)]
-
-
-class SamplerParams(C.Structure):
-    _fields_ = [("keys", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
-                ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int), ("exclude", c_int * 8),
-                ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int), ("rpb", c_int)]
+                ("rpb", c_int), ("bacc_val", c_void_p), ("bacc_idx", c_void_p), ("n_exclude", c_int),
+                ("exclude", c_int * 8)]
 
 
 def _sig(lib, name, res, *args):

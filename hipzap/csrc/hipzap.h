@@ -93,8 +93,24 @@ typedef struct HzLstmParams {
   float* h_state;             // [2][H] fp32, ping-pong by step parity
   float* c_state;             // [2][H] fp32
   const int* step;            // device step counter t
-  int In, H, ldk;             // ldk = padded In + H (multiple of 512)
+  int In, H, ldk;             // ldk = padded In + H (multiple of 64; chunks of 512 are predicated)
 } HzLstmParams;
+typedef struct HzSamplerParams {
+  const float* keys;          // [V] Gumbel-perturbed logits (decoder epilogue)
+  int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
+  int* step;                  // increments
+  int* draws;                 // optional [steps][10] record of the draws
+  const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
+  int V, n_exclude;
+  int exclude[8];
+  const float* bmax_val;      // [nblk] decoder workgroup maxima (value, row)
+  const int* bmax_idx;
+  int nblk, rpb;              // decoder geometry: workgroup b owns rows [b*rpb, (b+1)*rpb)
+  // with draws == NULL: the token is the argmax of the ACCEPTABLE keys (row != 0, not excluded),
+  // from the decoder's per-workgroup acceptable maxima; exact for the reference rule (see lstm.hip)
+  const float* bacc_val;      // [nblk] or NULL (then the top-10 tournament always runs)
+  const int* bacc_idx;
+} HzSamplerParams;
 typedef struct HzDecoderParams {
   const unsigned short* w;    // [V][ldk] bf16 (tied embedding, K padded)
   const float* bias;          // [V] or NULL
@@ -107,19 +123,11 @@ typedef struct HzDecoderParams {
   float* bmax_val;            // with keys: [nblk] per-workgroup max key (value, row) -> sampler
   int* bmax_idx;
   int nblk, rpb;              // workgroups and rows per workgroup (hz_decoder_geometry)
-} HzDecoderParams;
-typedef struct HzSamplerParams {
-  const float* keys;          // [V] Gumbel-perturbed logits (decoder epilogue)
-  int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
-  int* step;                  // increments
-  int* draws;                 // optional [steps][10] record of the draws
-  const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
-  int V, n_exclude;
+  float* bacc_val;            // optional [nblk]: per-workgroup max key over ACCEPTABLE rows
+  int* bacc_idx;              //   (row != 0 and not in exclude[]), -inf/INT_MAX if none
+  int n_exclude;
   int exclude[8];
-  const float* bmax_val;      // [nblk] decoder workgroup maxima (value, row)
-  const int* bmax_idx;
-  int nblk, rpb;              // decoder geometry: workgroup b owns rows [b*rpb, (b+1)*rpb)
-} HzSamplerParams;
+} HzDecoderParams;
 // decoder launch geometry for vocabulary V: workgroups and rows per workgroup (contiguous)
 void hz_decoder_geometry(int V, int* nblk, int* rpb);
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);

@@ -15,6 +15,8 @@
 //   with P ∝ exp(logit) (Plackett-Luce), i.e. torch.multinomial(exp(logits), 10) of
 //   main.py:61 in distribution, without exp() overflow. The main.py:63-68 selection rule
 //   (first draw not 0 and not excluded, else the first draw) runs on device too.
+#include <cstdlib>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -25,31 +27,41 @@ namespace {
 constexpr int CHUNK = 8;  // bf16 per 16-B lane load
 
 // --------------------------------------------------------------------------- LSTM cell
-// NCH = ldk / 512 is a template parameter so every weight load of a wave (4 gate rows x NCH
-// 16-B chunks) is issued before the first use — with a runtime chunk loop hipcc waited
-// vmcnt(0) per chunk (one L2/HBM round trip each). The input staging likewise issues all of a
-// thread's loads first (address selects instead of branches around loads).
-template <int NCH>
+// NCH = ceil(ldk / 512) is a template parameter so every weight load of a wave (4 gate rows x
+// its chunks) is issued before the first use. ldk is In + H padded to 64 only (v1 padded to
+// 512: 2150 -> 2560 streamed 16 % zeros); lanes past ldk in the last chunk are predicated off.
+// KW waves split one unit's K range (v1: one wave per unit, H/4 = 288 workgroups of 4.5 waves per
+// CU) so twice as many independent load streams are in flight; the KW partial gate sums meet in
+// LDS and the first wave of the unit applies the cell update.
+template <int NCH, int KW>
 __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
-  extern __shared__ __attribute__((aligned(16))) float vin[];  // [ldk] = [x ; h_prev ; 0-pad]
-  constexpr int PER = NCH * 512 / 256;  // staged elements per thread
+  extern __shared__ __attribute__((aligned(16))) float vin[];  // [NCH*512] = [x ; h_prev ; 0-pad]
+  __shared__ float part[4][4];                                  // [wave][gate] partial sums
+  constexpr int UPW = 4 / KW;                 // units per workgroup
+  constexpr int NC = (NCH + KW - 1) / KW;     // chunks per wave
+  constexpr int PER = NCH * 512 / 256;        // staged elements per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slot = wave / KW, kw = wave - slot * KW;
   const int t = *p.step;
   const int par = t & 1;
   const float* h_prev = p.h_state + par * p.H;
   const int tok = p.emb ? p.tok_seq[t] : 0;
-  if (!HZ_DCHECK(tok >= 0 && p.In + p.H <= p.ldk && p.ldk == NCH * 512)) return;
+  if (!HZ_DCHECK(tok >= 0 && p.In + p.H <= p.ldk && p.ldk <= NCH * 512 && p.ldk % 8 == 0)) return;
   const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
   const float* xprev = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
   // weights do not depend on the input vector: issue them first so their latency overlaps
-  // the staging loads (inactive tail waves read row H-1 and write nothing)
-  const int j = blockIdx.x * 4 + wave;  // hidden unit of this wave
+  // the staging loads (inactive tail units read row H-1 and write nothing)
+  const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
   const bf16_t* w = p.w + (long)(4 * min(j, p.H - 1)) * p.ldk + lane * 8;
-  u32x4 wv[4][NCH];
+  u32x4 wv[4][NC];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) wv[q][c] = *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + c * 512);
+    for (int c = 0; c < NC; ++c) {
+      const int k = (kw * NC + c) * 512 + lane * 8;
+      wv[q][c] = k < p.ldk ? *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8))
+                           : u32x4{0u, 0u, 0u, 0u};
+    }
   // ---- stage the input vector in LDS (fp32): all loads first, then the selects ----
   float fv[PER];
   unsigned short ev[PER];
@@ -68,11 +80,11 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
     vin[i] = in_h ? fv[r] : in_x ? (erow ? bf2f(ev[r]) : fv[r]) : 0.f;
   }
   __syncthreads();
-  if (j >= p.H) return;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
+  for (int c = 0; c < NC; ++c) {
+    const int k = (kw * NC + c) * 512 + lane * 8;
+    if ((kw * NC + c) >= NCH) break;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(vin + k);
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(vin + k + 4);
 #pragma unroll
@@ -85,7 +97,18 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = warp_sum(acc[q]);
-  if (lane == 0) {
+  if (KW > 1) {
+    if (lane == 0 && kw > 0)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[wave][q] = acc[q];
+    __syncthreads();
+    if (kw == 0)
+#pragma unroll
+      for (int o = 1; o < KW; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += part[wave + o][q];
+  }
+  if (lane == 0 && kw == 0 && j < p.H) {
     const float gi = acc[0] + p.bias[4 * j + 0];
     const float gf = acc[1] + p.bias[4 * j + 1];
     const float gg = acc[2] + p.bias[4 * j + 2];
@@ -140,97 +163,6 @@ __device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
   return av > bv || (av == bv && ai < bi);
 }
 
-template <int NCH>
-__global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
-  extern __shared__ __attribute__((aligned(16))) float hv[];
-  __shared__ float w_best[4];
-  __shared__ int w_besti[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int t = *p.step;
-  const int par = t & 1;
-  const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
-  if (!HZ_DCHECK(p.H <= p.ldk && p.rpb % DROWS == 0)) return;
-  for (int i = tid; i < p.ldk; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
-  __syncthreads();
-  const unsigned long long seed = p.keys ? *p.seed : 0ull;
-  const int ngroups = (p.V + DROWS - 1) / DROWS;
-  const int gpb = p.rpb / DROWS;
-  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
-  float best = -INFINITY;
-  int besti = 0x7fffffff;
-  for (int g = blockIdx.x * gpb + wave; g < g_end; g += 4) {
-    u32x4 wv[DROWS][NCH];
-#pragma unroll
-    for (int q = 0; q < DROWS; ++q) {
-      const int r = min(g * DROWS + q, p.V - 1);
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-        wv[q][c] = *reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8);
-    }
-    float acc[DROWS];
-#pragma unroll
-    for (int q = 0; q < DROWS; ++q) acc[q] = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int k = c * 512 + lane * 8;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
-#pragma unroll
-      for (int q = 0; q < DROWS; ++q) {
-        float f[8];
-        unpack8(wv[q][c], f);
-        acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
-                  f[6] * v1[2] + f[7] * v1[3];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < DROWS; ++q) acc[q] = warp_sum(acc[q]);
-    if (lane < DROWS) {
-      const int r = g * DROWS + lane;
-      float a = acc[0];
-#pragma unroll
-      for (int q = 1; q < DROWS; ++q) a = lane == q ? acc[q] : a;
-      if (r < p.V) {
-        const float lg = a + (p.bias ? p.bias[r] : 0.f);
-        p.logits[r] = lg;
-        if (p.keys) {
-          const float key = lg + gumbel(seed, t, r);
-          p.keys[r] = key;
-          if (better(key, r, best, besti)) {
-            best = key;
-            besti = r;
-          }
-        }
-      }
-    }
-  }
-  if (p.keys) {  // workgroup max key: lanes 0-7 hold the candidates, xor 1/2/4 stays inside them
-#pragma unroll
-    for (int o = 1; o < DROWS; o <<= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(besti, o, 64);
-      if (better(ov, oi, best, besti)) {
-        best = ov;
-        besti = oi;
-      }
-    }
-    if (lane == 0) {
-      w_best[wave] = best;
-      w_besti[wave] = besti;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < 4; ++w)
-        if (better(w_best[w], w_besti[w], best, besti)) {
-          best = w_best[w];
-          besti = w_besti[w];
-        }
-      p.bmax_val[blockIdx.x] = best;
-      p.bmax_idx[blockIdx.x] = besti;
-    }
-  }
-}
-
 constexpr int TOPK = 10;
 
 // Bitonic sort of NC independent (value, row) vectors (one pair per lane each) across the
@@ -272,10 +204,10 @@ __device__ __forceinline__ void wave_sort64(float (&v)[NC], int (&i)[NC]) {
 // to LDS, repeat until one chunk remains. One launch, one workgroup, no atomics. Then the
 // reference's selection rule (main.py:63-68) via a ballot.
 constexpr int SAMPLER_LDS = 1024;  // candidate slots per LDS buffer
-constexpr int SAMPLER_WAVES = 16;
+constexpr int SAMPLER_WAVES = 16;  // standalone sampler_kernel: 1024 threads
 constexpr int CPW = 2;             // chunks per wave per pass
 
-template <class Load>
+template <int WAVES, int CPWT, class Load>
 __device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi, float* cv, int* ci, float& ov,
                                             int& oi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -287,12 +219,12 @@ __device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi
   while (true) {
     const int nch = (n + 63) / 64;
     if (nch == 1) break;
-    for (int c0 = wave; c0 < nch; c0 += SAMPLER_WAVES * CPW) {
-      float v[CPW];
-      int i[CPW];
+    for (int c0 = wave; c0 < nch; c0 += WAVES * CPWT) {
+      float v[CPWT];
+      int i[CPWT];
 #pragma unroll
-      for (int u = 0; u < CPW; ++u) {  // all of this pass's loads first
-        const int j = (c0 + u * SAMPLER_WAVES) * 64 + lane;
+      for (int u = 0; u < CPWT; ++u) {  // all of this pass's loads first
+        const int j = (c0 + u * WAVES) * 64 + lane;
         v[u] = -INFINITY;
         i[u] = 0x7fffffff;
         if (j < n) {
@@ -304,10 +236,10 @@ __device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi
           }
         }
       }
-      wave_sort64<CPW>(v, i);
+      wave_sort64<CPWT>(v, i);
 #pragma unroll
-      for (int u = 0; u < CPW; ++u) {
-        const int c = c0 + u * SAMPLER_WAVES;
+      for (int u = 0; u < CPWT; ++u) {
+        const int c = c0 + u * WAVES;
         if (lane < TOPK && c < nch) {
           out_v[c * TOPK + lane] = v[u];
           out_i[c * TOPK + lane] = i[u];
@@ -341,29 +273,94 @@ __device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi
   __syncthreads();  // the LDS buffers are reused by the caller's next top-10
 }
 
-__global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) {
+// Fast path (no draw record requested): the reference keeps the first of its 10 draws that is
+// acceptable (not id 0, not excluded), else the first draw (main.py:63-68). At most 9 ids are
+// unacceptable, so at most 9 keys can rank above the best ACCEPTABLE key: it is always among
+// the 10 draws, hence always the one kept. The token is therefore exactly the argmax of the
+// acceptable keys (per-workgroup maxima from the decoder epilogue -> one block reduction); only
+// when no acceptable id exists at all (V <= 9) does the reference fall back to the first draw.
+template <int WAVES>
+__device__ __forceinline__ void sample_argmax(const HzSamplerParams& p, int t) {
+  __shared__ float w_v[WAVES];
+  __shared__ int w_i[WAVES], w_h[WAVES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((t + 1) >= *p.n_forced) {
+    float bv = -INFINITY, av = -INFINITY;
+    int bi = 0x7fffffff, ai = 0x7fffffff;
+    for (int j = threadIdx.x; j < p.nblk; j += WAVES * 64) {
+      const float v0 = p.bacc_val[j], v1 = p.bmax_val[j];
+      const int i0 = p.bacc_idx[j], i1 = p.bmax_idx[j];
+      if (better(v0, i0, av, ai)) {
+        av = v0;
+        ai = i0;
+      }
+      if (better(v1, i1, bv, bi)) {
+        bv = v1;
+        bi = i1;
+      }
+    }
+    // acceptable candidates rank above all others; the overall best is the fallback
+    const bool has = ai != 0x7fffffff;
+    float kv = has ? av : bv;
+    int ki = has ? ai : bi;
+    int kh = has;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(kv, o, 64);
+      const int oi = __shfl_xor(ki, o, 64);
+      const int oh = __shfl_xor(kh, o, 64);
+      if (oh > kh || (oh == kh && better(ov, oi, kv, ki))) {
+        kv = ov;
+        ki = oi;
+        kh = oh;
+      }
+    }
+    if (lane == 0) {
+      w_v[wave] = kv;
+      w_i[wave] = ki;
+      w_h[wave] = kh;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float v = w_v[0];
+      int i = w_i[0], h = w_h[0];
+      for (int w = 1; w < WAVES; ++w)
+        if (w_h[w] > h || (w_h[w] == h && better(w_v[w], w_i[w], v, i))) {
+          v = w_v[w];
+          i = w_i[w];
+          h = w_h[w];
+        }
+      p.tok_seq[t + 1] = min(max(i, 0), p.V - 1);
+    }
+  }
+  __syncthreads();  // every thread has read *p.step
+  if (threadIdx.x == 0) *p.step = t + 1;
+}
+
+// one sampling step with the calling workgroup (WAVES waves): top-10 keys -> draws -> token
+template <int WAVES, int CPWT>
+__device__ __forceinline__ void sample_step(const HzSamplerParams& p, int t) {
   __shared__ float buf_v[2][SAMPLER_LDS];
   __shared__ int buf_i[2][SAMPLER_LDS];
   __shared__ int sel[TOPK];
   const int lane = threadIdx.x & 63;
-  const int t = *p.step;
   if ((t + 1) >= *p.n_forced) {
     float v;
     int i;
     // 1. the 10 decoder workgroups with the largest maxima
-    block_top10(p.nblk, [&](int j, float& a, int& b) { a = p.bmax_val[j]; b = p.bmax_idx[j]; },
-                buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
+    block_top10<WAVES, CPWT>(p.nblk, [&](int j, float& a, int& b) { a = p.bmax_val[j]; b = p.bmax_idx[j]; },
+                             buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
     const int nsel = min(TOPK, p.nblk);
     if (threadIdx.x < nsel) sel[threadIdx.x] = min(i / p.rpb, p.nblk - 1);  // (NaN keys: stay in range)
     __syncthreads();
     // 2. the 10 largest keys among their rows
     const int rpb = p.rpb;
-    block_top10(nsel * rpb, [&](int j, float& a, int& b) {
-                  const int q = j / rpb;
-                  const int r = sel[q] * rpb + (j - q * rpb);
-                  a = r < p.V ? p.keys[r] : -INFINITY;
-                  b = r;
-                }, buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
+    block_top10<WAVES, CPWT>(nsel * rpb, [&](int j, float& a, int& b) {
+                               const int q = j / rpb;
+                               const int r = sel[q] * rpb + (j - q * rpb);
+                               a = r < p.V ? p.keys[r] : -INFINITY;
+                               b = r;
+                             }, buf_v[0], buf_i[0], buf_v[1], buf_i[1], v, i);
     if (threadIdx.x < 64) {  // wave 0: lanes 0..9 hold the draws in order
       const int nd = min(TOPK, p.V);
       bool ok = lane < nd && i > 0;
@@ -379,20 +376,151 @@ __global__ __launch_bounds__(1024) void sampler_kernel(const HzSamplerParams p) 
   if (threadIdx.x == 0) *p.step = t + 1;
 }
 
+// 4 waves x 8 chunks per pass: the 1875 decoder maxima of V=60000 fit one pass, and barriers
+// synchronise 4 waves instead of 16
+template <int WAVES, int CPWT>
+__global__ __launch_bounds__(WAVES * 64) void sampler_kernel(const HzSamplerParams p) {
+  sample_step<WAVES, CPWT>(p, *p.step);
+}
+
+__global__ __launch_bounds__(1024) void argmax_sampler_kernel(const HzSamplerParams p) {
+  sample_argmax<16>(p, *p.step);
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
+  extern __shared__ __attribute__((aligned(16))) float hv[];
+  __shared__ float w_best[4];
+  __shared__ int w_besti[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = *p.step;
+  const int par = t & 1;
+  const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
+  if (!HZ_DCHECK(p.H <= p.ldk && p.ldk <= NCH * 512 && p.rpb % DROWS == 0)) return;
+  for (int i = tid; i < NCH * 512; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
+  __syncthreads();
+  const unsigned long long seed = p.keys ? *p.seed : 0ull;
+  const int ngroups = (p.V + DROWS - 1) / DROWS;
+  const int gpb = p.rpb / DROWS;
+  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
+  float best = -INFINITY, abest = -INFINITY;
+  int besti = 0x7fffffff, abesti = 0x7fffffff;
+  for (int g = blockIdx.x * gpb + wave; g < g_end; g += 4) {
+    u32x4 wv[DROWS][NCH];
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) {
+      const int r = min(g * DROWS + q, p.V - 1);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        wv[q][c] = c * 512 + lane * 8 < p.ldk
+                       ? *reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8)
+                       : u32x4{0u, 0u, 0u, 0u};
+    }
+    float acc[DROWS];
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * 512 + lane * 8;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
+#pragma unroll
+      for (int q = 0; q < DROWS; ++q) {
+        float f[8];
+        unpack8(wv[q][c], f);
+        acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
+                  f[6] * v1[2] + f[7] * v1[3];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < DROWS; ++q) acc[q] = warp_sum(acc[q]);
+    if (lane < DROWS) {
+      const int r = g * DROWS + lane;
+      float a = acc[0];
+#pragma unroll
+      for (int q = 1; q < DROWS; ++q) a = lane == q ? acc[q] : a;
+      if (r < p.V) {
+        const float lg = a + (p.bias ? p.bias[r] : 0.f);
+        p.logits[r] = lg;
+        if (p.keys) {
+          const float key = lg + gumbel(seed, t, r);
+          p.keys[r] = key;
+          if (better(key, r, best, besti)) {
+            best = key;
+            besti = r;
+          }
+          bool acc = r != 0;
+          for (int e = 0; e < p.n_exclude; ++e) acc = acc && r != p.exclude[e];
+          if (acc && better(key, r, abest, abesti)) {
+            abest = key;
+            abesti = r;
+          }
+        }
+      }
+    }
+  }
+  if (p.keys) {  // workgroup max keys: lanes 0-7 hold the candidates, xor 1/2/4 stays inside them
+    __shared__ float a_best[4];
+    __shared__ int a_besti[4];
+#pragma unroll
+    for (int o = 1; o < DROWS; o <<= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      const float av = __shfl_xor(abest, o, 64);
+      const int ai = __shfl_xor(abesti, o, 64);
+      if (better(ov, oi, best, besti)) {
+        best = ov;
+        besti = oi;
+      }
+      if (better(av, ai, abest, abesti)) {
+        abest = av;
+        abesti = ai;
+      }
+    }
+    if (lane == 0) {
+      w_best[wave] = best;
+      w_besti[wave] = besti;
+      a_best[wave] = abest;
+      a_besti[wave] = abesti;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < 4; ++w) {
+        if (better(w_best[w], w_besti[w], best, besti)) {
+          best = w_best[w];
+          besti = w_besti[w];
+        }
+        if (better(a_best[w], a_besti[w], abest, abesti)) {
+          abest = a_best[w];
+          abesti = a_besti[w];
+        }
+      }
+      p.bmax_val[blockIdx.x] = best;
+      p.bmax_idx[blockIdx.x] = besti;
+      if (p.bacc_val) {
+        p.bacc_val[blockIdx.x] = abest;
+        p.bacc_idx[blockIdx.x] = abesti;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   const HzLstmParams& p = *pp;
-  if (p.ldk % 512 || p.ldk < p.In + p.H) return -1;
-  const dim3 grid((p.H + 3) / 4), block(256);
-  const size_t lds = p.ldk * sizeof(float);
-  switch (p.ldk / 512) {
-    case 1: hipLaunchKernelGGL(lstm_cell_kernel<1>, grid, block, lds, st, p); break;
-    case 2: hipLaunchKernelGGL(lstm_cell_kernel<2>, grid, block, lds, st, p); break;
-    case 3: hipLaunchKernelGGL(lstm_cell_kernel<3>, grid, block, lds, st, p); break;
-    case 4: hipLaunchKernelGGL(lstm_cell_kernel<4>, grid, block, lds, st, p); break;
-    case 5: hipLaunchKernelGGL(lstm_cell_kernel<5>, grid, block, lds, st, p); break;
-    case 6: hipLaunchKernelGGL(lstm_cell_kernel<6>, grid, block, lds, st, p); break;
+  if (p.ldk % 64 || p.ldk < p.In + p.H || p.In <= 0 || p.H <= 0) return -1;
+  constexpr int KW = 2;  // waves per unit (K split)
+  const int nch = (p.ldk + 511) / 512;
+  const dim3 grid((p.H + 4 / KW - 1) / (4 / KW)), block(256);
+  const size_t lds = (size_t)nch * 512 * sizeof(float);
+  switch (nch) {
+    case 1: hipLaunchKernelGGL((lstm_cell_kernel<1, KW>), grid, block, lds, st, p); break;
+    case 2: hipLaunchKernelGGL((lstm_cell_kernel<2, KW>), grid, block, lds, st, p); break;
+    case 3: hipLaunchKernelGGL((lstm_cell_kernel<3, KW>), grid, block, lds, st, p); break;
+    case 4: hipLaunchKernelGGL((lstm_cell_kernel<4, KW>), grid, block, lds, st, p); break;
+    case 5: hipLaunchKernelGGL((lstm_cell_kernel<5, KW>), grid, block, lds, st, p); break;
+    case 6: hipLaunchKernelGGL((lstm_cell_kernel<6, KW>), grid, block, lds, st, p); break;
     default: return -1;
   }
   return (int)hipGetLastError();
@@ -409,13 +537,14 @@ extern "C" void hz_decoder_geometry(int V, int* nblk, int* rpb) {
 
 extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const HzDecoderParams& p = *pp;
-  if (p.ldk % 512 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
+  if (p.ldk % 64 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
   int nblk, rpb;
   hz_decoder_geometry(p.V, &nblk, &rpb);
   if (p.nblk != nblk || p.rpb != rpb) return -1;
   const dim3 grid(nblk), block(256);
-  const size_t lds = p.ldk * sizeof(float);
-  switch (p.ldk / 512) {
+  const int nch = (p.ldk + 511) / 512;
+  const size_t lds = (size_t)nch * 512 * sizeof(float);
+  switch (nch) {
     case 1: hipLaunchKernelGGL(decoder_kernel<1>, grid, block, lds, st, p); break;
     case 2: hipLaunchKernelGGL(decoder_kernel<2>, grid, block, lds, st, p); break;
     case 3: hipLaunchKernelGGL(decoder_kernel<3>, grid, block, lds, st, p); break;
@@ -433,6 +562,9 @@ extern "C" int hz_sampler_launch(const HzSamplerParams* pp, hipStream_t st) {
     return -1;
   // LDS tournament capacity: first-round chunks of either top-10 must fit one buffer
   if ((nblk + 63) / 64 * TOPK > SAMPLER_LDS || (TOPK * rpb + 63) / 64 * TOPK > SAMPLER_LDS) return -1;
-  hipLaunchKernelGGL(sampler_kernel, dim3(1), dim3(64 * SAMPLER_WAVES), 0, st, p);
+  if (p.bacc_val && p.bacc_idx && !p.draws && !getenv("HIPZAP_SAMPLER_TOURNAMENT"))
+    hipLaunchKernelGGL(argmax_sampler_kernel, dim3(1), dim3(1024), 0, st, p);
+  else  // draws recorded (tests, diagnostics): the exact top-10 tournament
+    hipLaunchKernelGGL((sampler_kernel<SAMPLER_WAVES, CPW>), dim3(1), dim3(64 * SAMPLER_WAVES), 0, st, p);
   return (int)hipGetLastError();
 }

@@ -4,7 +4,8 @@ The reference rebuilds the model and runs 201 CPU forwards per request with auto
 (main.py:84-103; 8.9 s measured). Here:
   * cold start packs the state_dict once: per layer ``[W_ih | W_hh]`` concatenated,
     gate rows interleaved (unit j -> rows 4j..4j+3), ``b_ih + b_hh`` folded, K padded to a
-    multiple of 512, bf16; the tied embedding/decoder matrix is stored once (bf16, padded);
+    multiple of 64 (128-B rows; the kernels predicate the partial last 512-chunk), bf16;
+    the tied embedding/decoder matrix is stored once (bf16, padded);
   * one decode step = ``L`` fused LSTM-cell kernels + decoder GEMV + device sampler
     (csrc/lstm.hip), captured ONCE as a hipGraph; the recurrent state, the step counter, the
     prompt length, the RNG seed and the token sequence all live on the device, so a request
@@ -44,7 +45,7 @@ def pack_awd_lstm(sd: dict, device) -> dict:
         # interleave gates: new row 4j+q = old row q*H + j
         w = w.reshape(4, H, n_in + H).permute(1, 0, 2).reshape(4 * H, n_in + H)
         b = b.reshape(4, H).t().reshape(4 * H)
-        ldk = _pad_to(n_in + H, 512)
+        ldk = _pad_to(n_in + H, 64)
         wp = torch.zeros(4 * H, ldk, dtype=torch.bfloat16, device=dev)
         wp[:, : n_in + H] = w.to(dev, torch.bfloat16)
         layers.append({"w": wp, "bias": b.to(dev).contiguous(), "In": n_in, "H": H, "ldk": ldk})
@@ -53,7 +54,7 @@ def pack_awd_lstm(sd: dict, device) -> dict:
         raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
     emb = sd["0.encoder.weight"].float()
     V, E = emb.shape
-    lde = _pad_to(max(E, layers[-1]["H"]), 512)
+    lde = _pad_to(max(E, layers[-1]["H"]), 64)
     embp = torch.zeros(V, lde, dtype=torch.bfloat16, device=dev)
     embp[:, :E] = emb.to(dev, torch.bfloat16)
     dec_w = sd.get("1.decoder.weight")
@@ -106,6 +107,9 @@ class LMEngine:
             nblk, rpb = nblk.value, rpb.value
             self.bmax_val = torch.empty(nblk, device=dev)  # decoder workgroup maxima -> sampler
             self.bmax_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
+            self.bacc_val = torch.empty(nblk, device=dev)  # maxima over acceptable rows (argmax sampler)
+            self.bacc_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
+            ex = [int(e) for e in exclude_ids][:8]
             d = N.DecoderParams()
             d.w = packed["dec"].data_ptr()
             d.bias = N.ptr(packed["dec_bias"])
@@ -113,17 +117,21 @@ class LMEngine:
             d.V, d.H, d.ldk = packed["V"], L[-1]["H"], packed["lde"]
             d.keys, d.seed = self.keys.data_ptr(), self.seed.data_ptr()
             d.bmax_val, d.bmax_idx, d.nblk, d.rpb = self.bmax_val.data_ptr(), self.bmax_idx.data_ptr(), nblk, rpb
-            N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
+            d.bacc_val, d.bacc_idx = self.bacc_val.data_ptr(), self.bacc_idx.data_ptr()
+            d.n_exclude = len(ex)
+            for i, e in enumerate(ex):
+                d.exclude[i] = e
             s = N.SamplerParams()
             s.keys, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
             s.bmax_val, s.bmax_idx, s.nblk, s.rpb = d.bmax_val, d.bmax_idx, nblk, rpb
             s.draws = N.ptr(self.draws)
             s.n_forced = self.n_forced.data_ptr()
             s.V = packed["V"]
-            ex = [int(e) for e in exclude_ids][:8]
+            s.bacc_val, s.bacc_idx = d.bacc_val, d.bacc_idx  # used when no draw record is requested
             s.n_exclude = len(ex)
             for i, e in enumerate(ex):
                 s.exclude[i] = e
+            N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
             N.check(lib.hz_prog_add_sampler(self.prog, C.byref(s), 0), "add_sampler")
             if capture:
                 N.check(lib.hz_prog_capture(self.prog, self.stream.cuda_stream), "capture")

@@ -116,3 +116,39 @@ def test_pool_concurrent_requests_match_serial(model):
     with ThreadPoolExecutor(6) as ex:
         conc = list(ex.map(lambda j: pool.run_tokens(*j), jobs))
     assert conc == serial
+
+
+def test_reference_dims_v60000_logits_match_eager():
+    """The reference's serving configuration at the survey's vocabulary (emb 1000, hidden 1150,
+    3 layers, tied, V=60000; main.py:96): device logits vs the eager fp32 model."""
+    torch.manual_seed(3)
+    m = reference_lm(60000).eval()
+    eng = LMEngine.from_state_dict(m.state_dict(), DEV)
+    ids = [7, 59999, 123, 40000]
+    got, ref = eng.step_logits(ids), _eager_logits(m, ids)
+    rel = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 3e-2, rel
+    assert int(got.argmax()) == int(ref.argmax())
+    # bf16 weights: the ranking of the likeliest tokens is preserved
+    assert len(set(torch.topk(got, 10).indices.tolist()) & set(torch.topk(ref, 10).indices.tolist())) >= 8
+
+
+@pytest.mark.parametrize("V", [3000, 60000, 7])
+def test_argmax_sampler_equals_top10_rule(V):
+    """The fast sampler (argmax over acceptable keys, no draw record) picks exactly the token the
+    reference rule picks from the 10 draws (tournament + main.py:63-68 selection): identical
+    token sequences over many steps, with the likeliest token excluded and id 0 forbidden."""
+    torch.manual_seed(V + 5)
+    m = get_language_model(vocab_sz=V, emb_sz=96, n_hid=128, n_layers=3, pad_token=1, tie_weights=True).eval()
+    from hipzap.engine.lm import pack_awd_lstm
+    packed = pack_awd_lstm(m.state_dict(), DEV)
+    excl = [int(torch.topk(_eager_logits(m, [4, 1 % V]), 1).indices), 2 % V]
+    fast = LMEngine(packed, DEV, exclude_ids=excl)                       # argmax sampler
+    rule = LMEngine(packed, DEV, exclude_ids=excl, record_draws=True)    # tournament + selection rule
+    for seed in range(4):
+        a = fast.run_tokens([4, 1 % V], 80, seed=seed)
+        b = rule.run_tokens([4, 1 % V], 80, seed=seed)
+        assert a == b
+        for step, tok in enumerate(b):
+            row = rule.draws[1 + step].tolist()[:min(10, V)]
+            assert tok == select_token(row, set(excl))
