@@ -32,6 +32,9 @@ def _pad_to(n: int, m: int) -> int:
 def pack_awd_lstm(sd: dict, device) -> dict:
     """state_dict (reference key layout) -> device-ready packed tensors."""
     dev = torch.device(device)
+    if any(k.endswith("_reverse") for k in sd):
+        raise ValueError("bidirectional AWD-LSTM: a bidirectional layer needs the whole sequence, so it cannot "
+                         "drive token-by-token generation (GET /inference); use the eager model")
     layers = []
     l = 0
     while f"0.rnns.{l}.module.weight_ih_l0" in sd:

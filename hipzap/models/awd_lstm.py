@@ -62,12 +62,16 @@ class DropConnectLSTM(nn.Module):
     """Single-layer LSTM whose hidden-to-hidden matrix is DropConnect-ed in training.
 
     Keeps the raw matrix as ``weight_hh_l0_raw`` (a Parameter) next to ``module`` (the
-    ``nn.LSTM``), giving the checkpoint keys of the reference.
+    ``nn.LSTM``), giving the checkpoint keys of the reference. ``bidir``: a bidirectional
+    layer of ``n_out // 2`` units per direction (reference awd_lstm.py:57,69-70); as in the
+    reference's ``WeightDropout(rnn, weight_p)`` only the forward direction's ``weight_hh_l0``
+    is DropConnect-ed (``_reverse`` weights are plain LSTM parameters).
     """
 
-    def __init__(self, n_in: int, n_out: int, p: float):
+    def __init__(self, n_in: int, n_out: int, p: float, bidir: bool = False):
         super().__init__()
-        self.module = nn.LSTM(n_in, n_out, 1)
+        self.ndir = 2 if bidir else 1
+        self.module = nn.LSTM(n_in, n_out // self.ndir, 1, bidirectional=bidir)
         self.p = p
         self.weight_hh_l0_raw = nn.Parameter(self.module.weight_hh_l0.detach().clone())
 
@@ -78,8 +82,10 @@ class DropConnectLSTM(nn.Module):
     def forward(self, x, hc):
         w_hh = F.dropout(self.weight_hh_l0_raw, self.p, self.training) if self.training else self.module.weight_hh_l0
         m = self.module
-        out, h, c = torch._VF.lstm(x, hc, [m.weight_ih_l0, w_hh, m.bias_ih_l0, m.bias_hh_l0], True, 1, 0.0,
-                                   self.training, False, False)
+        ws = [m.weight_ih_l0, w_hh, m.bias_ih_l0, m.bias_hh_l0]
+        if self.ndir == 2:
+            ws += [m.weight_ih_l0_reverse, m.weight_hh_l0_reverse, m.bias_ih_l0_reverse, m.bias_hh_l0_reverse]
+        out, h, c = torch._VF.lstm(x, hc, ws, True, 1, 0.0, self.training, self.ndir == 2, False)
         return out, (h, c)
 
 
@@ -89,14 +95,13 @@ class RNNCore(nn.Module):
         super().__init__()
         if qrnn:
             raise NotImplementedError("QRNN is dead code in the reference (missing module); not supported")
-        if bidir:
-            raise NotImplementedError("bidirectional AWD-LSTM is not used by the reference")
+        self.ndir = 2 if bidir else 1
         self.bs = 1
         self.emb_sz, self.n_hid, self.n_layers = emb_sz, n_hid, n_layers
         self.encoder = nn.Embedding(vocab_sz, emb_sz, padding_idx=pad_token)
         self.encoder_dp = EmbeddingRowDropout(self.encoder, embed_p)
         dims = [emb_sz] + [n_hid] * (n_layers - 1) + [emb_sz]
-        self.rnns = nn.ModuleList([DropConnectLSTM(dims[i], dims[i + 1], weight_p) for i in range(n_layers)])
+        self.rnns = nn.ModuleList([DropConnectLSTM(dims[i], dims[i + 1], weight_p, bidir) for i in range(n_layers)])
         self.encoder.weight.data.uniform_(-0.1, 0.1)
         self.input_dp = LockedDropout(input_p)
         self.hidden_dps = nn.ModuleList([LockedDropout(hidden_p) for _ in range(n_layers)])
@@ -107,8 +112,8 @@ class RNNCore(nn.Module):
 
     def reset(self):
         p = self.encoder.weight
-        self.hidden = [(p.new_zeros(1, self.bs, r.module.hidden_size), p.new_zeros(1, self.bs, r.module.hidden_size))
-                       for r in self.rnns]
+        self.hidden = [(p.new_zeros(r.ndir, self.bs, r.module.hidden_size),
+                        p.new_zeros(r.ndir, self.bs, r.module.hidden_size)) for r in self.rnns]
 
     def forward(self, inp):
         sl, bs = inp.shape

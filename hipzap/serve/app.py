@@ -284,4 +284,5 @@ def health():
 
 @app.route("/metrics", methods=["GET"])
 def metrics():
-    return Response(METRICS.render(), mimetype="text/plain; version=0.0.4")
+    from ..utils.gpu_metrics import render as gpu_render
+    return Response(METRICS.render() + gpu_render(), mimetype="text/plain; version=0.0.4")

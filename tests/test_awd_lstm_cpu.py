@@ -74,3 +74,28 @@ def test_tied_decoder_and_hidden_reset_on_batch_change():
 def test_qrnn_unsupported():
     with pytest.raises(NotImplementedError):
         get_language_model(**dict(KW, qrnn=True))
+
+
+def test_bidirectional_core_matches_reference():
+    """bidir=True (reference awd_lstm.py:57,69-70,95): same keys and shapes, same eval forward."""
+    kw = dict(KW, bidir=True)
+    ref = _ref_module().get_language_model(**kw)
+    ours = get_language_model(**kw)
+    assert set(ref.state_dict()) == set(ours.state_dict())
+    sd = ref.state_dict()
+    ours.load_state_dict(sd)
+    ref.eval(); ours.eval()
+    ref.reset(); ours.reset()
+    x = torch.randint(0, KW["vocab_sz"], (7, 3))
+    with torch.no_grad():
+        a = ref(x)[0]
+        b = ours(x)[0]
+    assert torch.allclose(a, b, atol=1e-5)
+    assert ours[0].hidden[0][0].shape == (2, 3, KW["n_hid"] // 2)
+
+
+def test_bidirectional_checkpoint_refused_by_gpu_packer():
+    from hipzap.engine.lm import pack_awd_lstm
+    sd = get_language_model(**dict(KW, bidir=True)).state_dict()
+    with pytest.raises(ValueError, match="bidirectional"):
+        pack_awd_lstm(sd, "cpu")

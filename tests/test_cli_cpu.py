@@ -148,3 +148,38 @@ def test_native_library_links():
     for sym in ("hz_conv_launch", "hz_conv2_launch", "hz_gemm_lds_launch", "hz_launch_kernel", "hz_prog_add_kernel",
                 "hz_gemm_fp8_launch", "hz_softmax_launch", "hz_pool_fc_launch"):
         assert isinstance(getattr(lib, sym), ctypes._CFuncPtr)
+
+
+def test_gpu_metrics_from_sysfs(tmp_path):
+    """Per-GPU utilisation scraped from amdgpu sysfs files (a fake tree here)."""
+    from hipzap.utils import gpu_metrics
+    for i, busy in enumerate((37, 0)):
+        dev = tmp_path / f"card{i}" / "device"
+        (dev / "hwmon" / "hwmon3").mkdir(parents=True)
+        (dev / "gpu_busy_percent").write_text(f"{busy}\n")
+        (dev / "mem_info_vram_used").write_text("1073741824\n")
+        (dev / "mem_info_vram_total").write_text("309237645312\n")
+        (dev / "hwmon" / "hwmon3" / "power1_average").write_text("650000000\n")
+    (tmp_path / "card0-DP-1").mkdir()  # a connector: ignored
+    text = gpu_metrics.render(str(tmp_path))
+    assert 'hipzap_gpu_busy_percent{gpu="0"} 37' in text and 'hipzap_gpu_busy_percent{gpu="1"} 0' in text
+    assert 'hipzap_gpu_power_watts{gpu="0"} 650' in text
+    assert gpu_metrics.render(str(tmp_path / "none")) == ""
+
+
+def test_load_tuning_falls_back_to_highest_lower_concurrency(tmp_path, monkeypatch):
+    """the conv table chosen for N streams is the one tuned for the highest
+    concurrency <= N (c24 for 32 streams), else the latency table."""
+    import json
+    from hipzap.engine import engine as eng_mod
+    from hipzap.engine import tune
+    for suffix, tag in (("", "base"), ("_c8", "c8"), ("_c24", "c24")):
+        (tmp_path / f"resnet50_bs1{suffix}.json").write_text(json.dumps({"tag": tag}))
+
+    def table_path(model, batch, c=1):
+        return tmp_path / (f"{model}_bs{batch}" + (f"_c{c}" if c > 1 else "") + ".json")
+    monkeypatch.setattr(tune, "table_path", table_path)
+    pick = lambda n: (eng_mod.load_tuning("resnet50", 1, n) or {}).get("tag")  # noqa: E731
+    assert pick(32) == "c24" and pick(24) == "c24" and pick(16) == "c8" and pick(8) == "c8"
+    assert pick(4) == "base" and pick(1) == "base"
+    assert eng_mod.load_tuning("resnet50", 7, 4) is None

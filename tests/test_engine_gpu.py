@@ -33,8 +33,11 @@ def test_engine_matches_oracle(model_sd, batch):
     rel = (y - ref).abs().max().item() / ref.abs().max().item()
     assert rel < 3e-2, rel
     with torch.no_grad():
-        eager = m(x)
-    assert (y.argmax(1) == eager.argmax(1)).float().mean() >= 0.66
+        eager = m(x)  # the unfolded fp32 torch model (BN in eval mode)
+    rel_e = (y - eager).abs().max().item() / eager.abs().max().item()
+    assert rel_e < 3e-2, rel_e
+    top3 = eager.topk(3, dim=1).indices
+    assert all(int(y[i].argmax()) in top3[i].tolist() for i in range(batch))
 
 
 def test_graph_replay_equals_eager_and_tracks_input(model_sd):

@@ -106,14 +106,15 @@ def test_maxpool_avgpool_preprocess():
 @pytest.mark.parametrize("shape,cpad", [((2, 30, 34), 8), ((1, 224, 224), 8), ((3, 16, 16), 16), ((1, 5, 7), 8)])
 def test_preprocess_uint8_coalesced(shape, cpad):
     """uint8 3-channel payloads: 1024-pixel workgroups with a partial last one, Cpad > 8, and a pixel
-    count that is not a multiple of 4 (generic per-pixel kernel) -- all bit-exact vs fp32 math."""
+    count that is not a multiple of 4 (generic per-pixel kernel) -- every element within one bf16
+    ulp of the fp32 math (the output is bf16; fma ordering may move the rounding by one ulp)."""
     g = torch.Generator().manual_seed(2)
     u8 = torch.randint(0, 256, (*shape, 3), dtype=torch.uint8, generator=g)
     for mean, std in ((None, None), (V.IMAGENET_MEAN, V.IMAGENET_STD)):
         p = V.preprocess(u8.to(DEV), cpad=cpad, mean=mean, std=std).cpu().float()
         ref = V.preprocess_reference(u8, cpad=cpad, mean=mean, std=std)
         assert p.shape == ref.shape
-        assert (p - ref).abs().max() < 2e-2
+        assert bool(((p - ref).abs() <= ref.abs() * 2.0 ** -7 + 1e-6).all()), (p - ref).abs().max()
         assert torch.equal(p[..., 3:], torch.zeros_like(p[..., 3:]))
 
 
