@@ -13,7 +13,7 @@ cold start (headline ``cold_start_ms_p50``): measured FIRST, before this process
   of the real ResNet-50 architecture, their plan image) are written untimed beforehand, on the
   CPU, as ``hipzap plan`` does at deploy time. In-process rebuilds inside this warm process are
   reported separately (``cold_start_inprocess_*``).
-warm path: every rank serves ``--streams`` (default 32, profiles/r1_session5/streams_sweep.md)
+warm path: every rank serves ``--streams`` (default 24: same throughput as 32-48 with the executor at lower latency, profiles/r2_serving/streams_sweep.md)
   concurrent bs=1 request streams; each request is one hipGraph replay (zero-copy pinned uint8
   image -> preprocess -> 53 fused conv kernels -> pool+FC -> logits in pinned memory).
   ``--serve executor`` (default): one native client thread per stream sends requests back to
@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 32)),
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 24)),
                     help="concurrent bs=1 request contexts per GPU")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
     ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 5)),
