@@ -23,11 +23,21 @@ def cmd_serve(a):
     if a.gpus and a.gpus > 1:  # one worker process per GPU sharing the listening socket (serve/cluster.py)
         from .serve.cluster import launch
         sys.exit(launch(a.gpus, host, port, settings=a.settings, stage=a.stage))
-    from werkzeug.serving import WSGIRequestHandler
-
     from .serve.app import app, serve_threaded, set_server
-    from .serve.server import ModelServer
-    set_server(ModelServer(st))  # the settings named on the command line, not the default file
+    from .serve.server import ModelServer, PlanVisionBackend
+    srv = ModelServer(st)  # the settings named on the command line, not the default file
+    set_server(srv)
+    if srv.backend == "gpu" and os.environ.get("HIPZAP_NATIVE_HTTP", "1") != "0":
+        # native HTTP/1.1 front end: POST /predict for the plan-backed default model in C++,
+        # everything else through the Flask app (serve/native_http.py)
+        from .serve.native_http import NativeHTTPServer, listening_socket
+        be = srv.vision(st.default_model)  # cold start before the port opens
+        fast = be if isinstance(be, PlanVisionBackend) else None
+        print(f"hipzap serving stage {st.stage} on {host}:{port} (native http, fast route: "
+              f"{fast.name if fast else None})", flush=True)
+        NativeHTTPServer(app, listening_socket(host, port), fast=fast).serve_forever()
+        return
+    from werkzeug.serving import WSGIRequestHandler
     WSGIRequestHandler.protocol_version = "HTTP/1.1"  # keep-alive: no TCP handshake per request
     print(f"hipzap serving stage {st.stage} on {host}:{port} (models bucket {st.models_bucket!r})", flush=True)
     app.run(host=host, port=port, debug=False, threaded=serve_threaded())

@@ -310,6 +310,16 @@ int hz_exec_submit(void* exec, const void* const* in, void* out, double* lat_us)
 void hz_exec_stats(void* exec, uint64_t* served, uint64_t* polls);
 void hz_exec_destroy(void* exec);
 int hz_exec_bench(void* exec, int clients, int iters, const void* const* in, double* lat_us, double* wall_us);
+
+// ---- native HTTP/1.1 front end (csrc/http.cpp): POST /predict fast path + WSGI callback ----
+typedef void (*HzHttpPyHandler)(void* req, const char* method, const char* target, const char* headers,
+                                uint64_t hlen, const char* body, uint64_t blen);
+void* hz_http_start(int listen_fd, HzHttpPyHandler py);
+int hz_http_set_fast(void* srv, void* exec, int H, int W, int C, int out_floats, int classes, int probs,
+                     const char* model);
+void hz_http_respond(void* req, int status, const char* headers, uint64_t hlen, const char* body, uint64_t blen);
+void hz_http_stats(void* srv, uint64_t* out4);
+void hz_http_stop(void* srv);
 void hz_plan_close(void* plan);
 
 #ifdef __cplusplus

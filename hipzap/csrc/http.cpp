@@ -1,0 +1,543 @@
+// hipzap native HTTP/1.1 front end (serving layer, SURVEY.md §1 L5 / §3.6 "warm request").
+//
+// Measured problem (profiles/r2_http): behind werkzeug's threaded WSGI server a POST /predict
+// costs ~1.2 ms of GIL-held Python per request -> ~800 req/s per process, while the GPU serves
+// ~11k inf/s. This server keeps the Flask app as THE application (every route, every body
+// format, the Zappa contract) and takes only the hot route natively:
+//   POST /predict with one uint8 HWC image of the plan's shape, as JSON {"image_b64", "shape"
+//   [, "model"]} or as an .npy body -> base64/npy decode -> the request executor
+//   (csrc/executor.cpp: pinned input, hipGraph replay, wait) -> softmax + top-5 -> the same
+//   JSON schema as the Flask route (hipzap/serve/app.py predict()).
+// Anything else (other routes, batches, other keys or dtypes, query flags) goes to a Python
+// callback that runs the WSGI app and answers through hz_http_respond(). One thread per
+// keep-alive connection, blocking I/O; the GIL is only taken on the fallback path.
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hipzap.h"
+
+namespace {
+
+using PyHandler = HzHttpPyHandler;
+
+struct Fast {
+  void* exec = nullptr;  // HzExecutor over the plan's contexts
+  int H = 0, W = 0, C = 0;
+  int out_floats = 0, classes = 0, probs = 0;
+  std::string model;
+};
+
+struct Server {
+  int lfd = -1;
+  std::atomic<bool> stop{false};
+  std::atomic<int> live{0};
+  std::thread acceptor;
+  PyHandler py = nullptr;
+  Fast fast;
+  std::atomic<bool> has_fast{false};
+  std::mutex fast_mu;
+  std::atomic<uint64_t> n_fast{0}, n_py{0}, n_bad{0};
+};
+
+struct PyReq {
+  std::string out;
+  bool keep = true;
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+const char* reason(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 411: return "Length Required";
+    case 413: return "Payload Too Large";
+    case 500: return "Internal Server Error";
+    case 501: return "Not Implemented";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+bool send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (k <= 0) {
+      if (k < 0 && errno == EINTR) continue;
+      return false;
+    }
+    p += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool send_str(int fd, const std::string& s) { return send_all(fd, s.data(), s.size()); }
+
+std::string simple(int code, const std::string& body, bool keep) {
+  char h[256];
+  snprintf(h, sizeof(h),
+           "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n"
+           "Access-Control-Allow-Origin: *\r\nConnection: %s\r\n\r\n",
+           code, reason(code), body.size(), keep ? "keep-alive" : "close");
+  return std::string(h) + body;
+}
+
+// ---------------------------------------------------------------- small parsers
+int b64val(unsigned char c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+' || c == '-') return 62;
+  if (c == '/' || c == '_') return 63;
+  return -1;
+}
+
+// decode exactly `want` bytes of standard base64 (padding optional); false on any other length
+bool b64decode(const char* s, size_t n, uint8_t* out, size_t want) {
+  while (n && (s[n - 1] == '=')) --n;
+  if ((n * 3) / 4 != want) return false;
+  size_t o = 0, i = 0;
+  for (; i + 4 <= n; i += 4) {
+    int a = b64val(s[i]), b = b64val(s[i + 1]), c = b64val(s[i + 2]), d = b64val(s[i + 3]);
+    if ((a | b | c | d) < 0) return false;
+    const unsigned v = (unsigned)a << 18 | (unsigned)b << 12 | (unsigned)c << 6 | (unsigned)d;
+    out[o++] = (uint8_t)(v >> 16);
+    out[o++] = (uint8_t)(v >> 8);
+    out[o++] = (uint8_t)v;
+  }
+  const size_t rem = n - i;
+  if (rem == 2 || rem == 3) {
+    int a = b64val(s[i]), b = b64val(s[i + 1]), c = rem == 3 ? b64val(s[i + 2]) : 0;
+    if ((a | b | c) < 0) return false;
+    const unsigned v = (unsigned)a << 18 | (unsigned)b << 12 | (unsigned)c << 6;
+    out[o++] = (uint8_t)(v >> 16);
+    if (rem == 3) out[o++] = (uint8_t)(v >> 8);
+  } else if (rem == 1) {
+    return false;
+  }
+  return o == want;
+}
+
+void skip_ws(const char*& p, const char* e) {
+  while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+}
+
+// a JSON string without escapes (keys, base64, model names); false otherwise
+bool json_str(const char*& p, const char* e, const char** s, size_t* n) {
+  if (p >= e || *p != '"') return false;
+  const char* q = ++p;
+  while (p < e && *p != '"') {
+    if (*p == '\\') return false;
+    ++p;
+  }
+  if (p >= e) return false;
+  *s = q;
+  *n = (size_t)(p - q);
+  ++p;
+  return true;
+}
+
+bool json_int_array(const char*& p, const char* e, std::vector<long>& v) {
+  if (p >= e || *p != '[') return false;
+  ++p;
+  for (;;) {
+    skip_ws(p, e);
+    if (p < e && *p == ']' && v.empty()) {
+      ++p;
+      return true;
+    }
+    char* q;
+    const long x = strtol(p, &q, 10);
+    if (q == p || q > e) return false;
+    v.push_back(x);
+    p = q;
+    skip_ws(p, e);
+    if (p < e && *p == ',') {
+      ++p;
+      continue;
+    }
+    if (p < e && *p == ']') {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+}
+
+// {"image_b64": "...", "shape": [..], "model": "..."} and nothing else -> true
+bool parse_json_image(const char* b, size_t n, const char** img, size_t* img_n, std::vector<long>& shape,
+                      std::string& model) {
+  const char *p = b, *e = b + n;
+  skip_ws(p, e);
+  if (p >= e || *p != '{') return false;
+  ++p;
+  bool have_img = false, have_shape = false;
+  for (;;) {
+    skip_ws(p, e);
+    const char* k;
+    size_t kn;
+    if (!json_str(p, e, &k, &kn)) return false;
+    skip_ws(p, e);
+    if (p >= e || *p != ':') return false;
+    ++p;
+    skip_ws(p, e);
+    if (kn == 9 && !memcmp(k, "image_b64", 9)) {
+      if (!json_str(p, e, img, img_n)) return false;
+      have_img = true;
+    } else if (kn == 5 && !memcmp(k, "shape", 5)) {
+      if (!json_int_array(p, e, shape)) return false;
+      have_shape = true;
+    } else if (kn == 5 && !memcmp(k, "model", 5)) {
+      const char* m;
+      size_t mn;
+      if (!json_str(p, e, &m, &mn)) return false;
+      model.assign(m, mn);
+    } else {
+      return false;  // any other key: the Flask route decides
+    }
+    skip_ws(p, e);
+    if (p < e && *p == ',') {
+      ++p;
+      continue;
+    }
+    if (p < e && *p == '}') break;
+    return false;
+  }
+  return have_img && have_shape;
+}
+
+// .npy (v1/v2/v3) uint8 C-order array -> shape + data pointer
+bool parse_npy_u8(const char* b, size_t n, std::vector<long>& shape, const uint8_t** data, size_t* dn) {
+  if (n < 12 || memcmp(b, "\x93NUMPY", 6) != 0) return false;
+  const int major = (unsigned char)b[6];
+  size_t hl, off;
+  if (major == 1) {
+    hl = (unsigned char)b[8] | (unsigned)(unsigned char)b[9] << 8;
+    off = 10;
+  } else {
+    hl = (unsigned char)b[8] | (unsigned)(unsigned char)b[9] << 8 | (unsigned)(unsigned char)b[10] << 16 |
+         (unsigned)(unsigned char)b[11] << 24;
+    off = 12;
+  }
+  if (off + hl > n) return false;
+  const std::string h(b + off, hl);
+  if (h.find("'descr': '|u1'") == std::string::npos && h.find("'descr': '<u1'") == std::string::npos) return false;
+  if (h.find("'fortran_order': False") == std::string::npos) return false;
+  const size_t s0 = h.find("'shape': (");
+  if (s0 == std::string::npos) return false;
+  const char* p = h.c_str() + s0 + 10;
+  for (;;) {
+    while (*p == ' ') ++p;
+    if (*p == ')') break;
+    char* q;
+    const long x = strtol(p, &q, 10);
+    if (q == p) return false;
+    shape.push_back(x);
+    p = q;
+    while (*p == ' ') ++p;
+    if (*p == ',') ++p;
+  }
+  *data = reinterpret_cast<const uint8_t*>(b + off + hl);
+  *dn = n - off - hl;
+  return true;
+}
+
+// ---------------------------------------------------------------- the fast route
+bool try_fast(Server* S, const std::string& method, const std::string& target, const std::string& ctype,
+              const char* body, size_t blen, bool keep, std::string& out) {
+  if (!S->has_fast.load(std::memory_order_acquire) || method != "POST") return false;
+  std::string path = target, query;
+  const size_t qpos = target.find('?');
+  if (qpos != std::string::npos) {
+    path = target.substr(0, qpos);
+    query = target.substr(qpos + 1);
+  }
+  if (path != "/predict") return false;
+  Fast f;
+  {
+    std::lock_guard<std::mutex> g(S->fast_mu);
+    f = S->fast;
+  }
+  std::string qmodel;
+  if (!query.empty()) {
+    if (query.compare(0, 6, "model=") != 0 || query.find('&') != std::string::npos) return false;
+    qmodel = query.substr(6);
+  }
+  const double t0 = now_ms();
+  std::vector<long> shape;
+  std::string model = qmodel;
+  const size_t want = (size_t)f.H * f.W * f.C;
+  thread_local std::vector<uint8_t> img;
+  const uint8_t* src = nullptr;
+  if (ctype.compare(0, 16, "application/json") == 0) {
+    const char* b64;
+    size_t b64n;
+    std::string bm;
+    if (!parse_json_image(body, blen, &b64, &b64n, shape, bm)) return false;
+    if (!bm.empty()) model = bm;
+    if (shape.size() == 4 && shape[0] == 1) shape.erase(shape.begin());
+    if (shape.size() != 3 || shape[0] != f.H || shape[1] != f.W || shape[2] != f.C) return false;
+    img.resize(want);
+    if (!b64decode(b64, b64n, img.data(), want)) return false;
+    src = img.data();
+  } else if (ctype.compare(0, 24, "application/octet-stream") == 0) {
+    const uint8_t* d;
+    size_t dn;
+    if (!parse_npy_u8(body, blen, shape, &d, &dn)) return false;
+    if (shape.size() == 4 && shape[0] == 1) shape.erase(shape.begin());
+    if (shape.size() != 3 || shape[0] != f.H || shape[1] != f.W || shape[2] != f.C || dn < want) return false;
+    src = d;
+  } else {
+    return false;
+  }
+  if (!model.empty() && model != f.model) return false;
+  const double t1 = now_ms();
+  thread_local std::vector<float> y;
+  y.resize(f.out_floats);
+  double lat = 0;
+  const void* ins[1] = {src};
+  const int rc = hz_exec_submit(f.exec, ins, y.data(), &lat);
+  const double t2 = now_ms();
+  if (rc) {
+    out = simple(503, "{\"error\": \"RuntimeError\", \"message\": \"executor request failed\"}", keep);
+    return true;
+  }
+  // softmax (unless the plan emits probabilities) + top-5, as app.py does with numpy
+  const int n = f.classes;
+  thread_local std::vector<double> pr;
+  pr.resize(n);
+  if (f.probs) {
+    for (int i = 0; i < n; ++i) pr[i] = y[i];
+  } else {
+    float m = -INFINITY;
+    for (int i = 0; i < n; ++i) m = y[i] > m ? y[i] : m;
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += (pr[i] = std::exp((double)y[i] - m));
+    for (int i = 0; i < n; ++i) pr[i] /= s;
+  }
+  const int k = n < 5 ? n : 5;
+  int top[5];
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    for (int i = 0; i < n; ++i) {
+      bool used = false;
+      for (int q = 0; q < j; ++q) used |= top[q] == i;
+      if (!used && (best < 0 || pr[i] > pr[best])) best = i;
+    }
+    top[j] = best;
+  }
+  std::string js = "{\"model\": \"" + f.model + "\", \"backend\": \"gpu\", \"batch\": 1, \"top5\": [[";
+  char tmp[64];
+  for (int j = 0; j < k; ++j) {
+    snprintf(tmp, sizeof(tmp), "%s[%d, %.6g]", j ? ", " : "", top[j], pr[top[j]]);
+    js += tmp;
+  }
+  const double t3 = now_ms();
+  snprintf(tmp, sizeof(tmp), "]], \"timing_ms\": %.3f}", t2 - t1);
+  js += tmp;
+  char h[400];
+  snprintf(h, sizeof(h),
+           "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n"
+           "Access-Control-Allow-Origin: *\r\nAccess-Control-Expose-Headers: X-Timing\r\n"
+           "X-Timing: decode=%.3f;infer=%.3f;total=%.3f\r\nX-Hipzap-Path: native\r\nConnection: %s\r\n\r\n",
+           js.size(), t1 - t0, t2 - t1, t3 - t0, keep ? "keep-alive" : "close");
+  out = std::string(h) + js;
+  return true;
+}
+
+// ---------------------------------------------------------------- connections
+void serve_conn(Server* S, int fd) {
+  S->live++;
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  std::string buf;
+  buf.reserve(1 << 18);
+  char rd[65536];
+  const size_t kMaxBody = size_t(64) << 20;
+  bool open = true;
+  while (open && !S->stop.load()) {
+    // headers
+    size_t hend;
+    while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
+      if (buf.size() > (1 << 16)) {
+        open = false;
+        break;
+      }
+      pollfd pf{fd, POLLIN, 0};
+      const int pr = poll(&pf, 1, 250);
+      if (S->stop.load()) {
+        open = false;
+        break;
+      }
+      if (pr == 0) continue;
+      const ssize_t k = recv(fd, rd, sizeof(rd), 0);
+      if (k <= 0) {
+        open = false;
+        break;
+      }
+      buf.append(rd, (size_t)k);
+    }
+    if (!open) break;
+    const std::string head = buf.substr(0, hend);
+    size_t le = head.find("\r\n");
+    const std::string line = head.substr(0, le);
+    const size_t sp1 = line.find(' '), sp2 = line.rfind(' ');
+    if (sp1 == std::string::npos || sp2 == sp1) {
+      send_str(fd, simple(400, "{\"error\": \"bad request line\"}", false));
+      break;
+    }
+    const std::string method = line.substr(0, sp1), target = line.substr(sp1 + 1, sp2 - sp1 - 1),
+                      version = line.substr(sp2 + 1);
+    std::string headers = le == std::string::npos ? "" : head.substr(le + 2), ctype;
+    long clen = 0;
+    bool keep = version == "HTTP/1.1", chunked = false;
+    {
+      size_t p = 0;
+      while (p < headers.size()) {
+        size_t e = headers.find("\r\n", p);
+        if (e == std::string::npos) e = headers.size();
+        const std::string h = headers.substr(p, e - p);
+        const size_t c = h.find(':');
+        if (c != std::string::npos) {
+          std::string k = h.substr(0, c), v = h.substr(c + 1);
+          for (auto& ch : k) ch = (char)tolower(ch);
+          while (!v.empty() && v[0] == ' ') v.erase(0, 1);
+          if (k == "content-length") clen = atol(v.c_str());
+          else if (k == "content-type") ctype = v;
+          else if (k == "transfer-encoding") chunked = true;
+          else if (k == "connection") {
+            for (auto& ch : v) ch = (char)tolower(ch);
+            if (v.find("close") != std::string::npos) keep = false;
+            if (v.find("keep-alive") != std::string::npos) keep = true;
+          }
+        }
+        p = e + 2;
+      }
+    }
+    std::string resp;
+    if (chunked || clen < 0 || (size_t)clen > kMaxBody) {
+      S->n_bad++;
+      send_str(fd, simple(chunked ? 411 : 413, "{\"error\": \"unsupported body framing\"}", false));
+      break;
+    }
+    // body
+    const size_t need = hend + 4 + (size_t)clen;
+    while (buf.size() < need) {
+      pollfd pf{fd, POLLIN, 0};
+      const int pr = poll(&pf, 1, 250);
+      if (S->stop.load()) {
+        open = false;
+        break;
+      }
+      if (pr == 0) continue;
+      const ssize_t k = recv(fd, rd, sizeof(rd), 0);
+      if (k <= 0) {
+        open = false;
+        break;
+      }
+      buf.append(rd, (size_t)k);
+    }
+    if (!open) break;
+    const char* body = buf.data() + hend + 4;
+    if (try_fast(S, method, target, ctype, body, (size_t)clen, keep, resp)) {
+      S->n_fast++;
+    } else if (S->py) {
+      S->n_py++;
+      PyReq r;
+      r.keep = keep;
+      S->py(&r, method.c_str(), target.c_str(), headers.c_str(), headers.size(), body, (uint64_t)clen);
+      if (r.out.empty()) r.out = simple(500, "{\"error\": \"no response from the application\"}", keep);
+      resp.swap(r.out);
+    } else {
+      resp = simple(404, "{\"error\": \"not found\"}", keep);
+    }
+    if (!send_all(fd, resp.data(), resp.size())) break;
+    buf.erase(0, need);
+    if (!keep) break;
+  }
+  close(fd);
+  S->live--;
+}
+
+void accept_loop(Server* S) {
+  while (!S->stop.load()) {
+    pollfd pf{S->lfd, POLLIN, 0};
+    const int pr = poll(&pf, 1, 250);
+    if (pr <= 0) continue;
+    const int fd = accept(S->lfd, nullptr, nullptr);
+    if (fd < 0) continue;  // another process sharing the socket took it, or EINTR
+    std::thread(serve_conn, S, fd).detach();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// listen_fd: a bound, listening TCP socket (the caller owns it; shared across worker processes)
+void* hz_http_start(int listen_fd, PyHandler py) {
+  auto* S = new Server();
+  S->lfd = listen_fd;
+  S->py = py;
+  S->acceptor = std::thread(accept_loop, S);
+  return S;
+}
+
+// the native POST /predict route over an executor (see hipzap/serve/native_http.py)
+int hz_http_set_fast(void* h, void* exec, int H, int W, int C, int out_floats, int classes, int probs,
+                     const char* model) {
+  Server* S = static_cast<Server*>(h);
+  if (!exec || H <= 0 || W <= 0 || C <= 0 || classes <= 0 || classes > out_floats) return -1;
+  std::lock_guard<std::mutex> g(S->fast_mu);
+  S->fast = Fast{exec, H, W, C, out_floats, classes, probs, model ? model : ""};
+  S->has_fast.store(true, std::memory_order_release);
+  return 0;
+}
+
+void hz_http_respond(void* req, int status, const char* headers, uint64_t hlen, const char* body, uint64_t blen) {
+  PyReq* r = static_cast<PyReq*>(req);
+  char line[64];
+  snprintf(line, sizeof(line), "HTTP/1.1 %d %s\r\n", status, reason(status));
+  r->out.assign(line);
+  r->out.append(headers, hlen);  // "Name: value\r\n" lines incl. Content-Length
+  r->out.append(r->keep ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+  r->out.append(body, blen);
+}
+
+void hz_http_stats(void* h, uint64_t* out4) {
+  Server* S = static_cast<Server*>(h);
+  out4[0] = S->n_fast.load();
+  out4[1] = S->n_py.load();
+  out4[2] = S->n_bad.load();
+  out4[3] = (uint64_t)S->live.load();
+}
+
+// stop accepting, let open connections notice within one poll period, then free
+void hz_http_stop(void* h) {
+  Server* S = static_cast<Server*>(h);
+  S->stop.store(true);
+  if (S->acceptor.joinable()) S->acceptor.join();
+  for (int i = 0; i < 100 && S->live.load() > 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  if (S->live.load() == 0) delete S;  // else leak rather than free state a connection still uses
+}
+
+}  // extern "C"

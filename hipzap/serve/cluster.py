@@ -517,11 +517,19 @@ def worker_main() -> int:
     app_mod.set_server(srv)
     app_mod.CLUSTER.update({"rank": rank, "world": world, "device": device, "cold_start_ms": round(cold_ms, 2),
                             "member": member, "coordinator": coord})
-    WSGIRequestHandler.protocol_version = "HTTP/1.1"
     fd = int(os.environ["HIPZAP_LISTEN_FD"])
-    httpd = make_server(st.host, st.port, app_mod.app, threaded=True, fd=fd)
     log.info("worker %d/%d on GPU %d ready in %.1f ms (%s)", rank, world, device, cold_ms, backend.__class__.__name__)
     del np
+    if os.environ.get("HIPZAP_NATIVE_HTTP", "1") != "0":
+        from .native_http import NativeHTTPServer
+        from .server import PlanVisionBackend
+        fast = backend if isinstance(backend, PlanVisionBackend) else None
+        srv_http = NativeHTTPServer(app_mod.app, socket.socket(fileno=fd), fast=fast)
+        app_mod.CLUSTER["http"] = srv_http
+        srv_http.serve_forever()
+        return 0
+    WSGIRequestHandler.protocol_version = "HTTP/1.1"
+    httpd = make_server(st.host, st.port, app_mod.app, threaded=True, fd=fd)
     try:
         httpd.serve_forever()
     except KeyboardInterrupt:

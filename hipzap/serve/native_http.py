@@ -1,0 +1,123 @@
+"""Serve the WSGI app through the native HTTP/1.1 front end (csrc/http.cpp).
+
+The hot route -- ``POST /predict`` with one uint8 image of a plan-backed model's shape (JSON
+``image_b64``/``shape`` or an ``.npy`` body) -- is answered in C++ straight through the request
+executor, without the GIL. Every other request is handed to the Flask app through a ctypes
+callback that builds a WSGI environ (the same adapter the Lambda handler uses), so behaviour
+and the Zappa contract are unchanged; only the throughput of the hot route is.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import io
+import logging
+import socket
+import sys
+import threading
+from urllib.parse import unquote
+
+from .. import _native as N
+
+log = logging.getLogger("hipzap.http")
+
+_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64)
+
+
+def listening_socket(host: str, port: int, backlog: int = 1024) -> socket.socket:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.bind((host, port))
+    s.listen(backlog)
+    return s
+
+
+def _environ(method: str, target: str, headers: str, body: bytes, server_port: str) -> dict:
+    path, _, query = target.partition("?")
+    env = {
+        "REQUEST_METHOD": method, "SCRIPT_NAME": "", "PATH_INFO": unquote(path), "QUERY_STRING": query,
+        "SERVER_NAME": "hipzap", "SERVER_PORT": server_port, "SERVER_PROTOCOL": "HTTP/1.1",
+        "REMOTE_ADDR": "127.0.0.1", "CONTENT_LENGTH": str(len(body)), "CONTENT_TYPE": "",
+        "wsgi.version": (1, 0), "wsgi.url_scheme": "http", "wsgi.input": io.BytesIO(body),
+        "wsgi.errors": sys.stderr, "wsgi.multithread": True, "wsgi.multiprocess": False, "wsgi.run_once": False,
+    }
+    for line in headers.split("\r\n"):
+        k, sep, v = line.partition(":")
+        if not sep:
+            continue
+        k, v = k.strip().lower(), v.strip()
+        if k == "content-type":
+            env["CONTENT_TYPE"] = v
+        elif k != "content-length":
+            env["HTTP_" + k.upper().replace("-", "_")] = v
+    return env
+
+
+class NativeHTTPServer:
+    """``app``: any WSGI app (the Flask app). ``sock``: a listening socket (shared by cluster
+    workers). ``fast``: a :class:`~hipzap.serve.server.PlanVisionBackend` whose model gets the
+    native ``POST /predict`` route (its contexts are built first so the executor covers them)."""
+
+    def __init__(self, app, sock: socket.socket, fast=None):
+        from .lambda_handler import call_wsgi
+        self.app, self.sock = app, sock
+        self._call_wsgi = call_wsgi
+        self._port = str(sock.getsockname()[1])
+        self._cb = _CB(self._handle)  # keep a reference: the C side calls it from its threads
+        self._h = N.lib().hz_http_start(sock.fileno(), self._cb)
+        if not self._h:
+            raise RuntimeError("hz_http_start failed")
+        self.fast_model = None
+        if fast is not None:
+            self.set_fast(fast)
+        self._stopped = threading.Event()
+
+    def set_fast(self, backend) -> None:
+        eng = backend.engine
+        eng.ensure_contexts()
+        ex = eng.executor()
+        if ex is None:
+            raise RuntimeError("plan engine has no executor (capture disabled?)")
+        self._exec = ex  # keep alive
+        b, h, w, c = backend.in_shape
+        out = eng.out_spec
+        rc = N.lib().hz_http_set_fast(self._h, ex._h, h, w, c, out["bytes"] // 4, int(backend.num_labels),
+                                      int(backend.probs), backend.name.encode())
+        if rc or b != 1:
+            raise RuntimeError(f"native /predict route rejected (rc={rc}, plan batch {b})")
+        self.fast_model = backend.name
+
+    def _handle(self, req, method, target, headers, hlen, body_ptr, blen):
+        try:
+            body = C.string_at(body_ptr, blen) if blen else b""
+            env = _environ(method.decode(), target.decode(), C.string_at(headers, hlen).decode("latin-1"), body,
+                           self._port)
+            code, hdrs, out = self._call_wsgi(self.app, env)
+            lines = "".join(f"{k}: {v}\r\n" for k, v in hdrs if k.lower() not in ("content-length", "connection"))
+            lines += f"Content-Length: {len(out)}\r\n"
+            raw = lines.encode("latin-1")
+            N.lib().hz_http_respond(req, code, raw, len(raw), out, len(out))
+        except Exception as e:  # noqa: BLE001 - must answer; the C side waits for the response
+            log.exception("native http callback failed")
+            msg = ('{"error": "%s"}' % type(e).__name__).encode()
+            hdr = f"Content-Type: application/json\r\nContent-Length: {len(msg)}\r\n".encode()
+            N.lib().hz_http_respond(req, 500, hdr, len(hdr), msg, len(msg))
+
+    def stats(self) -> dict:
+        a = (C.c_uint64 * 4)()
+        N.lib().hz_http_stats(self._h, a)
+        return {"native": a[0], "wsgi": a[1], "rejected": a[2], "open_connections": a[3]}
+
+    def serve_forever(self) -> None:
+        try:
+            while not self._stopped.wait(0.5):
+                pass
+        except KeyboardInterrupt:
+            pass
+        finally:
+            self.stop()
+
+    def stop(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        self._stopped.set()
+        if h:
+            N.lib().hz_http_stop(h)

@@ -108,3 +108,39 @@ def test_health_reports_plan_model(plan_server):
     r = c.get("/health")
     assert r.status_code == 200 and "resnet50" in r.get_json()["models"]
     assert os.path.exists(plan)
+
+
+def test_native_http_fast_route_matches_flask_route(plan_server):
+    """The C++ POST /predict route (csrc/http.cpp) answers the plan-backed model natively with the
+    same top-5 as the Flask route; other requests still reach the Flask app."""
+    import http.client
+    from hipzap.serve.native_http import NativeHTTPServer, listening_socket
+    c, srv, plan, ckpt = plan_server
+    be = srv.vision("resnet50")
+    sock = listening_socket("127.0.0.1", 0)
+    hs = NativeHTTPServer(app_mod.app, sock, fast=be)
+    try:
+        port = sock.getsockname()[1]
+        conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+        for i in range(3):
+            img = _img(10 + i)
+            body = json.dumps({"image_b64": base64.b64encode(img.tobytes()).decode(), "shape": [224, 224, 3]})
+            conn.request("POST", "/predict", body=body, headers={"Content-Type": "application/json"})
+            r = conn.getresponse()
+            native = json.loads(r.read())
+            assert r.status == 200 and r.getheader("X-Hipzap-Path") == "native"
+            flask = c.post("/predict", data=body, content_type="application/json").get_json()
+            # random-init logits are large: most probabilities underflow to exactly 0, and the
+            # order among those ties is arbitrary -> compare the entries with mass
+            nz = [t for t in flask["top5"][0] if t[1] > 1e-6]
+            assert [t[0] for t in native["top5"][0][: len(nz)]] == [t[0] for t in nz]
+            np.testing.assert_allclose([t[1] for t in native["top5"][0]], [t[1] for t in flask["top5"][0]],
+                                       rtol=1e-4, atol=1e-6)
+        conn.request("GET", "/health")
+        r = conn.getresponse()
+        assert r.status == 200 and "resnet50" in json.loads(r.read())["models"]
+        st = hs.stats()
+        assert st["native"] == 3 and st["wsgi"] == 1
+    finally:
+        hs.stop()
+        sock.close()
