@@ -140,6 +140,7 @@ def _load():
     _sig(lib, "hz_plan_bench", D, P, c_int)
     _sig(lib, "hz_plan_close", None, P)
     _sig(lib, "hz_plan_prog", P, P, c_int)
+    _sig(lib, "hz_plan_capture_ctx", c_int, P, c_int)
     PP_ = C.POINTER(c_void_p)
     _sig(lib, "hz_exec_create", P, PP_, PP_, PP_, C.POINTER(U64), c_int, PP_, U64, c_int)
     _sig(lib, "hz_exec_submit", c_int, P, PP_, P, C.POINTER(D))

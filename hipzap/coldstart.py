@@ -26,7 +26,8 @@ def run_plan(path: str, device: int) -> dict:
     t_imp = time.time()
     from hipzap.lite import PlanEngine
     t_lib = time.time()
-    eng = PlanEngine(path, device=device, contexts=1)
+    eng = PlanEngine(path, device=device, contexts=1,
+                     capture="lazy" if os.environ.get("HIPZAP_PLAN_LAZY_CAPTURE", "1") == "1" else True)
     t_ready = time.time()
     spec = eng.in_specs[0]
     out = eng.infer_raw(os.urandom(spec["bytes"]))

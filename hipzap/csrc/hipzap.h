@@ -300,6 +300,7 @@ int hz_plan_infer(void* plan, int ctx, const void* in, uint64_t in_off, uint64_t
                   uint64_t out_off, uint64_t out_bytes);
 double hz_plan_bench(void* plan, int iters);
 HzProgram hz_plan_prog(void* plan, int ctx);
+int hz_plan_capture_ctx(void* plan, int ctx);
 
 // ---- request executor (csrc/executor.cpp): one worker thread submits + polls completions ----
 // host_in[k * n + i] = context i's pinned input k (n_in <= 4); host_out[i] = its pinned output

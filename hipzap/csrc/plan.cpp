@@ -16,6 +16,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -140,17 +141,62 @@ struct Plan {
     return 0;
   }
 
-  // blob upload: the file is mmapped; HIP stages pageable memory through its own pinned
-  // buffers, chunked so the page-cache reads of chunk i+1 overlap the DMA of chunk i
+  // blob upload, HIPZAP_PLAN_UPLOAD selects (measured: profiles/r2_coldstart):
+  //   register  pin the mmapped file pages in place (hipHostRegister) -> one DMA -> unpin
+  //   staged    read() chunks into two pinned staging buffers, DMA chunk i while reading i+1
+  //   pageable  hipMemcpyAsync from the mapping (HIP stages pageable memory internally)
   int upload_blob(hipStream_t st) {
+    const char* mode = getenv("HIPZAP_PLAN_UPLOAD");
+    const std::string m = mode ? mode : "staged";
+    hipError_t e = hipSuccess;
+    if (m == "register") {
+      const size_t pg = 4096, off = h.blob_off & ~(pg - 1), len = h.blob_off + h.blob_len - off;
+      void* base = map + off;
+      if (hipHostRegister(base, len, hipHostRegisterDefault) == hipSuccess) {
+        void* dptr = nullptr;
+        e = hipHostGetDevicePointer(&dptr, base, 0);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(blob, map + h.blob_off, h.blob_len, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipHostUnregister(base);
+        if (e == hipSuccess) return 0;
+      }
+      (void)hipGetLastError();  // fall through to the staged copy
+    }
+    if (m != "pageable") {
+      const size_t chunk = size_t(4) << 20;
+      void* stage[2] = {nullptr, nullptr};
+      hipEvent_t done[2] = {nullptr, nullptr};
+      bool ok = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
+                hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
+                hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
+      int k = 0;
+      for (size_t off = 0; ok && off < h.blob_len; off += chunk, k ^= 1) {
+        const size_t n = h.blob_len - off < chunk ? h.blob_len - off : chunk;
+        if (off >= 2 * chunk) ok = hipEventSynchronize(done[k]) == hipSuccess;  // buffer k free again
+        if (!ok) break;
+        ssize_t got = pread(fd, stage[k], n, (off_t)(h.blob_off + off));
+        ok = got == (ssize_t)n &&
+             hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, stage[k], n, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipEventRecord(done[k], st) == hipSuccess;
+      }
+      if (ok) ok = hipStreamSynchronize(st) == hipSuccess;
+      for (int i = 0; i < 2; ++i) {
+        if (done[i]) (void)hipEventDestroy(done[i]);
+        if (stage[i]) (void)hipHostFree(stage[i]);
+      }
+      if (ok) return 0;
+      (void)hipGetLastError();
+    }
     const uint8_t* src = map + h.blob_off;
     const size_t chunk = size_t(8) << 20;
     for (size_t off = 0; off < h.blob_len; off += chunk) {
       const size_t n = h.blob_len - off < chunk ? h.blob_len - off : chunk;
-      hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, src + off, n, hipMemcpyHostToDevice, st);
+      e = hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, src + off, n, hipMemcpyHostToDevice, st);
       if (e != hipSuccess) return fail(std::string("plan: blob H2D failed: ") + hipGetErrorString(e), (int)e);
     }
-    hipError_t e = hipStreamSynchronize(st);
+    e = hipStreamSynchronize(st);
     return e == hipSuccess ? 0 : fail("plan: blob H2D sync failed", (int)e);
   }
 
@@ -416,6 +462,20 @@ double hz_plan_bench(void* h, int iters) {
 }
 
 HzProgram hz_plan_prog(void* h, int ctx) { return get_ctx(P(h), ctx).prog; }
+
+// capture a context that was added with capture = 0 (lazy capture: its first requests ran the
+// program eagerly); no request may be in flight on it
+int hz_plan_capture_ctx(void* h, int ctx) {
+  Plan* p = P(h);
+  PlanCtx c = get_ctx(p, ctx);
+  if (!c.prog) return fail("plan: no such context");
+  if (hipSetDevice(p->device) != hipSuccess) return fail("plan: hipSetDevice failed");
+  const double t0 = now_ms();
+  int rc = hz_prog_capture(c.prog, c.st);
+  if (!rc) rc = (int)hipStreamSynchronize(c.st);
+  p->t[HZ_PLAN_T_CAPTURE] += now_ms() - t0;
+  return rc;
+}
 
 void hz_plan_close(void* h) { delete P(h); }
 

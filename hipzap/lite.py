@@ -82,7 +82,10 @@ class PlanEngine:
     rank receive the weights by RCCL broadcast instead of reading the file."""
 
     def __init__(self, path: str, device: int = 0, contexts: int = 1, eager_contexts: int | None = None,
-                 capture: bool = True, read_blob: bool = True, fill_blob=None):
+                 capture: bool | str = True, read_blob: bool = True, fill_blob=None):
+        """``capture="lazy"``: the eager contexts are NOT captured at load; their first requests
+        run the bound program launch by launch and :meth:`ensure_contexts` captures them (cold
+        start -> first response without the graph instantiation on the critical path)."""
         t0 = time.perf_counter()
         self.path = path
         self.meta = read_meta(path)
@@ -105,8 +108,10 @@ class PlanEngine:
             self.timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         self.num_contexts = contexts
         self._capture = bool(capture)
+        self._lazy = capture == "lazy"
         n0 = contexts if eager_contexts is None else max(1, min(eager_contexts, contexts))
-        self._check(L.hz_plan_add_contexts(h, n0, int(capture)), "add_contexts")
+        self._check(L.hz_plan_add_contexts(h, n0, 0 if self._lazy else int(bool(capture))), "add_contexts")
+        self._uncaptured = list(range(n0)) if self._lazy else []
         self._locks = [threading.Lock() for _ in range(n0)]
         self._rr, self._rr_lock, self._build_lock = 0, threading.Lock(), threading.Lock()
         self._exec = None
@@ -126,11 +131,15 @@ class PlanEngine:
     def ensure_contexts(self) -> float:
         """Build the contexts deferred by ``eager_contexts`` (thread-safe); returns ms spent."""
         with self._build_lock:
+            t0 = time.perf_counter()
+            for i in self._uncaptured:  # lazy capture of the eager contexts (no request in flight)
+                with self._locks[i]:
+                    self._check(lib().hz_plan_capture_ctx(self._h, i), "capture_ctx")
+            self._uncaptured = []
             have = lib().hz_plan_num_contexts(self._h)
             n = self.num_contexts - have
             if n <= 0:
-                return 0.0
-            t0 = time.perf_counter()
+                return (time.perf_counter() - t0) * 1e3
             self._check(lib().hz_plan_add_contexts(self._h, n, int(self._capture)), "add_contexts")
             with self._rr_lock:
                 self._locks += [threading.Lock() for _ in range(n)]
@@ -170,7 +179,8 @@ class PlanEngine:
     def executor(self):
         """Native request executor over all contexts, once every context exists (else None)."""
         ex = getattr(self, "_exec", None)
-        if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts:
+        if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts \
+                or self._uncaptured:
             return ex
         from .executor import Executor
         with self._build_lock:

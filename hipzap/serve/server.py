@@ -359,8 +359,9 @@ class PlanVisionBackend:
         fill = None
         if comm is not None and comm.world > 1:
             fill = lambda addr, n: comm.broadcast_ptr(addr, n, 0)  # noqa: E731
+        # first request runs the bound program eagerly; the background scale-up below captures it
         self.engine = PlanEngine(plan, device=device, contexts=max(1, spec.contexts), eager_contexts=1,
-                                 read_blob=comm is None or comm.rank == 0, fill_blob=fill)
+                                 read_blob=comm is None or comm.rank == 0, fill_blob=fill, capture="lazy")
         self.meta = self.engine.meta
         self.in_shape = tuple(self.meta["inputs"][0]["shape"])  # [B, H, W, 3] uint8
         self.batch = self.in_shape[0]
