@@ -15,7 +15,8 @@
 //     chunk' = chunk ^ ((row >> 1) & 7), so the 16 rows of a ds_read_b128 lane group land in
 //     16 distinct 16-B bank slots (conflict-free); glds writes lane-linearly, so the swizzle is
 //     applied to the per-lane GLOBAL source address;
-//   * 3 LDS stages, two K steps in flight: counted `s_waitcnt vmcnt(G)` + raw s_barrier (never
+//   * 2, 3 or 4 LDS stages (up to NS-1 K steps in flight; the N=768 projections are latency-bound
+//     with 12 K steps per tile): counted `s_waitcnt vmcnt(k*G)` + raw s_barrier (never
 //     __syncthreads(), whose fence would drain the in-flight DMA — §5 "Pipelining across barriers");
 //   * same swapped orientation and fused epilogue as conv.hip (4 consecutive output features
 //     per lane: 16-B bias, 8-B residual, 8-B store), XCD-aware tile order.
@@ -136,8 +137,9 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
 #pragma unroll
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
-  if (NS > 2 && nst > 1) stage(1, 1);
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < nst) stage(s0, s0);
   // folded LayerNorm: row statistics of the producer are complete at kernel start; their loads
   // go out behind the first stages' DMA, so the wait overlaps the first K step's
   const HzLnFold* __restrict__ lf = LNF ? p.lnf : nullptr;
@@ -153,7 +155,9 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   int cur = 0;
   for (int st = 0; st < nst; ++st) {
     // stages issued ahead of st: min(NS-2, nst-1-st) may stay in flight
-    if (NS > 2 && st + 1 < nst) wait_vm<(NS > 2 ? G : 0)>();
+    const int ahead = min(NS - 2, nst - 1 - st);
+    if (NS > 3 && ahead >= 2) wait_vm<(NS > 3 ? 2 * G : 0)>();
+    else if (NS > 2 && ahead >= 1) wait_vm<(NS > 2 ? G : 0)>();
     else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -258,7 +262,8 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
 }  // namespace
 
 // cfg 16: 128x128, 17: 64x128 (BM x BN), 18: 128x64, 19: 64x64 with 3 LDS stages; cfg 20-23: the same
-// tiles with 2 stages (less LDS: more workgroups per CU). Row-major activations only.
+// tiles with 2 stages (less LDS: more workgroups per CU); cfg 24-27: 4 stages (deeper prefetch for
+// short-K / latency-bound shapes). Row-major activations only.
 extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
   if (!p.x_rowmajor || !p.out_rowmajor || p.K % 64 || p.ksteps * 32 != p.K || p.ldx % 8 || p.Cout % 4) return -1;
@@ -271,6 +276,10 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
     case 22: return launch_lds<128, 64, 2>(p, st);
     case 19: return launch_lds<64, 64, 3>(p, st);
     case 23: return launch_lds<64, 64, 2>(p, st);
+    case 24: return launch_lds<128, 128, 4>(p, st);
+    case 25: return launch_lds<64, 128, 4>(p, st);
+    case 26: return launch_lds<128, 64, 4>(p, st);
+    case 27: return launch_lds<64, 64, 4>(p, st);
     default: return -2;
   }
 }

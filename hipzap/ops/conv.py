@@ -24,7 +24,8 @@ GEMM_ROW_PAD = 128  # linear weights: rows padded to the largest LDS-tiled GEMM 
 # cfg >= 16: LDS-tiled GEMM (csrc/gemm.hip), row-major activations, K % 64 == 0 -> (BM, BN);
 # 16-19 use 3 LDS stages, 20-23 the same tiles with 2 (half the LDS: more workgroups per CU)
 LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
-             20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64)}
+             20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64),
+             24: (128, 128), 25: (64, 128), 26: (128, 64), 27: (64, 64)}  # 3 / 2 / 4 LDS stages
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
 
