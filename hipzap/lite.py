@@ -22,7 +22,8 @@ import time
 from . import _native as N
 
 HEADER = struct.Struct("<8s15Q")
-PHASES = ("parse_ms", "hip_init_ms", "upload_ms", "ctx_alloc_ms", "bind_ms", "capture_ms")
+PHASES = ("parse_ms", "hip_init_ms", "upload_ms", "ctx_alloc_ms", "bind_ms", "capture_ms", "blob_alloc_ms",
+          "first_copy_ms")
 _TYPECODE = {"float32": "f", "uint8": "B", "int32": "i", "int64": "q", "bfloat16": "H", "float16": "H"}
 
 
