@@ -54,11 +54,13 @@ class PoolParams(C.Structure):
 class LstmParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("emb", c_void_p), ("lde", c_int), ("tok_seq", c_void_p),
                 ("x_state", c_void_p), ("h_state", c_void_p), ("c_state", c_void_p), ("step", c_void_p),
-                ("In", c_int), ("H", c_int), ("ldk", c_int)]
+                ("In", c_int), ("H", c_int), ("ldk", c_int), ("step_off", c_int), ("n_forced", c_void_p),
+                ("bacc_val", c_void_p), ("bacc_idx", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p),
+                ("nblk", c_int), ("V", c_int)]
 
 
 class SamplerParams(C.Structure):
-    _fields_ = [("keys", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("draws", c_void_p),
+    _fields_ = [("keys", c_void_p), ("tok_seq", c_void_p), ("step", c_void_p), ("step_off", c_int), ("draws", c_void_p),
                 ("n_forced", c_void_p), ("V", c_int), ("n_exclude", c_int), ("exclude", c_int * 8),
                 ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int), ("rpb", c_int),
                 ("bacc_val", c_void_p), ("bacc_idx", c_void_p)]
@@ -66,7 +68,7 @@ class SamplerParams(C.Structure):
 
 class DecoderParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h_state", c_void_p), ("step", c_void_p),
-                ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
+                ("step_off", c_int), ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
                 ("seed", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int),
                 ("rpb", c_int), ("bacc_val", c_void_p), ("bacc_idx", c_void_p), ("n_exclude", c_int),
                 ("exclude", c_int * 8)]
@@ -122,6 +124,8 @@ def _load():
     _sig(lib, "hz_prog_add_lstm", c_int, P, C.POINTER(LstmParams), c_int)
     _sig(lib, "hz_prog_add_decoder", c_int, P, C.POINTER(DecoderParams), c_int)
     _sig(lib, "hz_prog_add_sampler", c_int, P, C.POINTER(SamplerParams), c_int)
+    _sig(lib, "hz_prog_add_step_bump", c_int, P, P, c_int, c_int)
+    _sig(lib, "hz_step_bump_launch", c_int, P, c_int, P)
     # plan images (csrc/plan.cpp; hipzap/lite.py is the torch-free client)
     U64, D = C.c_uint64, c_double
     _sig(lib, "hz_abi_version", U64)

@@ -88,17 +88,28 @@ typedef struct HzLstmParams {
   const float* bias;          // [4H] fp32 (b_ih + b_hh, same interleave)
   const unsigned short* emb;  // layer 0: embedding [V][lde] bf16 (input gathered by token); else NULL
   int lde;
-  const int* tok_seq;         // token sequence; step t consumes tok_seq[t]
+  int* tok_seq;               // token sequence; step t consumes tok_seq[t]
   const float* x_state;       // layers > 0: previous layer's h_state [2][In]
   float* h_state;             // [2][H] fp32, ping-pong by step parity
   float* c_state;             // [2][H] fp32
-  const int* step;            // device step counter t
+  const int* step;            // device step counter: this op runs step t = *step + step_off
   int In, H, ldk;             // ldk = padded In + H (multiple of 64; chunks of 512 are predicated)
+  int step_off;
+  // layer 0 only, optional (fused sampler): for t >= *n_forced the token of step t is the argmax
+  // of the previous step's decoder maxima (the argmax sampler's rule, computed redundantly by
+  // every workgroup); workgroup 0 records it in tok_seq[t]. NULL bacc_val: tok_seq[t] is read.
+  const int* n_forced;
+  const float* bacc_val;      // [nblk] decoder per-workgroup maxima over acceptable rows
+  const int* bacc_idx;
+  const float* bmax_val;      // [nblk] overall maxima (fallback when no row is acceptable)
+  const int* bmax_idx;
+  int nblk, V;
 } HzLstmParams;
 typedef struct HzSamplerParams {
   const float* keys;          // [V] Gumbel-perturbed logits (decoder epilogue)
   int* tok_seq;               // writes tok_seq[t+1] when t+1 >= n_forced
-  int* step;                  // increments
+  const int* step;            // this op samples after step t = *step + step_off (no increment:
+  int step_off;               //   hz_step_bump_launch advances the counter once per graph)
   int* draws;                 // optional [steps][10] record of the draws
   const int* n_forced;        // device: prompt length (tokens 0..n_forced-1 are given)
   int V, n_exclude;
@@ -115,7 +126,8 @@ typedef struct HzDecoderParams {
   const unsigned short* w;    // [V][ldk] bf16 (tied embedding, K padded)
   const float* bias;          // [V] or NULL
   const float* h_state;       // last layer [2][H]
-  const int* step;
+  const int* step;            // step t = *step + step_off
+  int step_off;
   float* logits;              // [V]
   int V, H, ldk;
   float* keys;                // optional [V]: logits + Gumbel(seed, step, row) for the sampler
@@ -133,6 +145,8 @@ void hz_decoder_geometry(int V, int* nblk, int* rpb);
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);
 int hz_decoder_launch(const HzDecoderParams* p, hipStream_t st);
 int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);
+// *step += n (one thread): closes a captured run of decode steps
+int hz_step_bump_launch(int* step, int n, hipStream_t st);
 
 // ---- FP8 (OCP e4m3fn) path (csrc/fp8.hip) ----
 typedef struct HzQuantParams {
@@ -237,6 +251,7 @@ int hz_prog_add_memcpy(HzProgram p, void* dst, const void* src, size_t bytes, in
 int hz_prog_add_lstm(HzProgram p, const HzLstmParams* lp, int slot);
 int hz_prog_add_decoder(HzProgram p, const HzDecoderParams* dp, int slot);
 int hz_prog_add_sampler(HzProgram p, const HzSamplerParams* sp, int slot);
+int hz_prog_add_step_bump(HzProgram p, int* step, int n, int slot);
 int hz_prog_add_fork(HzProgram p, int slot);   // side stream `slot` waits for main
 int hz_prog_add_join(HzProgram p, int slot);   // main waits for side stream `slot`
 int hz_prog_run(HzProgram p, hipStream_t st);  // eager launch of every op

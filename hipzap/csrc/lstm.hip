@@ -26,6 +26,79 @@ namespace {
 
 constexpr int CHUNK = 8;  // bf16 per 16-B lane load
 
+// total order of sampler keys: larger value first, ties to the lower row
+__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
+// LDS-only workgroup barrier: unlike __syncthreads() it does not wait for the caller's
+// outstanding global loads (the LSTM weight stream stays in flight across it)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int WAVES>
+__device__ __forceinline__ void block_reduce_best(float* sv, int* si, float& v, int& i);
+
+// best (value, row) of n entries, reduced by the calling workgroup (WAVES waves); every thread
+// gets the result. Slots: 2*WAVES floats / ints of LDS.
+template <int WAVES>
+__device__ __forceinline__ void block_best(const float* val, const int* idx, int n, float* sv, int* si, float& v,
+                                           int& i) {
+  v = -INFINITY;
+  i = 0x7fffffff;
+  for (int j = threadIdx.x; j < n; j += WAVES * 64) {
+    const float a = val[j];
+    const int b = idx[j];
+    if (better(a, b, v, i)) {
+      v = a;
+      i = b;
+    }
+  }
+  block_reduce_best<WAVES>(sv, si, v, i);
+}
+
+// workgroup-wide best of every thread's (v, i); every thread gets it
+template <int WAVES>
+__device__ __forceinline__ void block_reduce_best(float* sv, int* si, float& v, int& i) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  if (lane == 0) {
+    sv[wave] = v;
+    si[wave] = i;
+  }
+  lds_barrier();
+  v = sv[0];
+  i = si[0];
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w)
+    if (better(sv[w], si[w], v, i)) {
+      v = sv[w];
+      i = si[w];
+    }
+}
+
+// The argmax sampler's token (exactness argument at sample_argmax): the best key over the
+// ACCEPTABLE rows from the decoder's per-workgroup maxima, or, when no row is acceptable at all
+// (V <= 9), the best key overall. Uniform control flow; every thread gets the token.
+template <int WAVES>
+__device__ __forceinline__ int block_token(const float* bacc_val, const int* bacc_idx, const float* bmax_val,
+                                           const int* bmax_idx, int nblk, int V) {
+  __shared__ float sv[2][WAVES];
+  __shared__ int si[2][WAVES];
+  float v;
+  int i;
+  block_best<WAVES>(bacc_val, bacc_idx, nblk, sv[0], si[0], v, i);
+  if (i == 0x7fffffff) block_best<WAVES>(bmax_val, bmax_idx, nblk, sv[1], si[1], v, i);
+  return min(max(i, 0), V - 1);
+}
+
 // --------------------------------------------------------------------------- LSTM cell
 // NCH = ceil(ldk / 512) is a template parameter so every weight load of a wave (4 gate rows x
 // its chunks) is issued before the first use. ldk is In + H padded to 64 only (v1 padded to
@@ -42,15 +115,27 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   constexpr int PER = NCH * 512 / 256;        // staged elements per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int slot = wave / KW, kw = wave - slot * KW;
-  const int t = *p.step;
+  const int t = *p.step + p.step_off;
   const int par = t & 1;
   const float* h_prev = p.h_state + par * p.H;
-  const int tok = p.emb ? p.tok_seq[t] : 0;
-  if (!HZ_DCHECK(tok >= 0 && p.In + p.H <= p.ldk && p.ldk <= NCH * 512 && p.ldk % 8 == 0)) return;
-  const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
+  if (!HZ_DCHECK(p.In + p.H <= p.ldk && p.ldk <= NCH * 512 && p.ldk % 8 == 0)) return;
   const float* xprev = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
   // weights do not depend on the input vector: issue them first so their latency overlaps
-  // the staging loads (inactive tail units read row H-1 and write nothing)
+  // the token selection and the staging loads (inactive tail units read row H-1, write nothing)
+  // fused sampler: load the previous decoder's acceptable maxima FIRST (vmcnt retires in issue
+  // order: a wait for loads issued after the weight stream would wait for the weights too)
+  const bool fused = p.emb && p.bacc_val && t >= *p.n_forced;
+  constexpr int TPT = 8;  // maxima per thread: nblk <= 2048 (hz_decoder_geometry)
+  float tv[TPT];
+  int ti[TPT];
+  if (fused) {
+#pragma unroll
+    for (int r = 0; r < TPT; ++r) {
+      const int e = tid + r * 256;
+      tv[r] = e < p.nblk ? p.bacc_val[e] : -INFINITY;
+      ti[r] = e < p.nblk ? p.bacc_idx[e] : 0x7fffffff;
+    }
+  }
   const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
   const bf16_t* w = p.w + (long)(4 * min(j, p.H - 1)) * p.ldk + lane * 8;
   u32x4 wv[4][NC];
@@ -59,9 +144,34 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int k = (kw * NC + c) * 512 + lane * 8;
-      wv[q][c] = k < p.ldk ? *reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8))
-                           : u32x4{0u, 0u, 0u, 0u};
+      const u32x4* src = reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8));
+      wv[q][c] = k < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
     }
+  int tok = 0;
+  if (fused) {  // this step's token from the last decoder (the argmax sampler's rule)
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    float v = tv[0];
+    int i = ti[0];
+#pragma unroll
+    for (int r = 1; r < TPT; ++r)
+      if (better(tv[r], ti[r], v, i)) {
+        v = tv[r];
+        i = ti[r];
+      }
+    block_reduce_best<4>(sv, si, v, i);
+    if (i == 0x7fffffff) {  // no acceptable row anywhere (V <= 9): the best key overall
+      __shared__ float sv2[4];
+      __shared__ int si2[4];
+      block_best<4>(p.bmax_val, p.bmax_idx, p.nblk, sv2, si2, v, i);
+    }
+    tok = min(max(i, 0), p.V - 1);
+    if (blockIdx.x == 0 && tid == 0) p.tok_seq[t] = tok;
+  } else if (p.emb) {
+    tok = p.tok_seq[t];
+  }
+  if (!HZ_DCHECK(tok >= 0)) return;
+  const bf16_t* erow = p.emb ? p.emb + (long)tok * p.lde : nullptr;
   // ---- stage the input vector in LDS (fp32): all loads first, then the selects ----
   float fv[PER];
   unsigned short ev[PER];
@@ -157,11 +267,6 @@ __device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
 // epilogue also writes logit + Gumbel(seed,t,row) (the Philox work is spread over the whole chip)
 // and the workgroup's largest key (value, row) for the sampler's pruning.
 constexpr int DROWS = 8;
-
-// total order of sampler keys: larger value first, ties to the lower row
-__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
-  return av > bv || (av == bv && ai < bi);
-}
 
 constexpr int TOPK = 10;
 
@@ -281,60 +386,10 @@ __device__ __forceinline__ void block_top10(int n, Load load, float* bv, int* bi
 // when no acceptable id exists at all (V <= 9) does the reference fall back to the first draw.
 template <int WAVES>
 __device__ __forceinline__ void sample_argmax(const HzSamplerParams& p, int t) {
-  __shared__ float w_v[WAVES];
-  __shared__ int w_i[WAVES], w_h[WAVES];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if ((t + 1) >= *p.n_forced) {
-    float bv = -INFINITY, av = -INFINITY;
-    int bi = 0x7fffffff, ai = 0x7fffffff;
-    for (int j = threadIdx.x; j < p.nblk; j += WAVES * 64) {
-      const float v0 = p.bacc_val[j], v1 = p.bmax_val[j];
-      const int i0 = p.bacc_idx[j], i1 = p.bmax_idx[j];
-      if (better(v0, i0, av, ai)) {
-        av = v0;
-        ai = i0;
-      }
-      if (better(v1, i1, bv, bi)) {
-        bv = v1;
-        bi = i1;
-      }
-    }
-    // acceptable candidates rank above all others; the overall best is the fallback
-    const bool has = ai != 0x7fffffff;
-    float kv = has ? av : bv;
-    int ki = has ? ai : bi;
-    int kh = has;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(kv, o, 64);
-      const int oi = __shfl_xor(ki, o, 64);
-      const int oh = __shfl_xor(kh, o, 64);
-      if (oh > kh || (oh == kh && better(ov, oi, kv, ki))) {
-        kv = ov;
-        ki = oi;
-        kh = oh;
-      }
-    }
-    if (lane == 0) {
-      w_v[wave] = kv;
-      w_i[wave] = ki;
-      w_h[wave] = kh;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float v = w_v[0];
-      int i = w_i[0], h = w_h[0];
-      for (int w = 1; w < WAVES; ++w)
-        if (w_h[w] > h || (w_h[w] == h && better(w_v[w], w_i[w], v, i))) {
-          v = w_v[w];
-          i = w_i[w];
-          h = w_h[w];
-        }
-      p.tok_seq[t + 1] = min(max(i, 0), p.V - 1);
-    }
+    const int tok = block_token<WAVES>(p.bacc_val, p.bacc_idx, p.bmax_val, p.bmax_idx, p.nblk, p.V);
+    if (threadIdx.x == 0) p.tok_seq[t + 1] = tok;
   }
-  __syncthreads();  // every thread has read *p.step
-  if (threadIdx.x == 0) *p.step = t + 1;
 }
 
 // one sampling step with the calling workgroup (WAVES waves): top-10 keys -> draws -> token
@@ -372,60 +427,61 @@ __device__ __forceinline__ void sample_step(const HzSamplerParams& p, int t) {
       if (p.draws && lane < TOPK) p.draws[(long)t * TOPK + lane] = i;
     }
   }
-  __syncthreads();  // every thread has read *p.step
-  if (threadIdx.x == 0) *p.step = t + 1;
 }
 
 // 4 waves x 8 chunks per pass: the 1875 decoder maxima of V=60000 fit one pass, and barriers
 // synchronise 4 waves instead of 16
 template <int WAVES, int CPWT>
 __global__ __launch_bounds__(WAVES * 64) void sampler_kernel(const HzSamplerParams p) {
-  sample_step<WAVES, CPWT>(p, *p.step);
+  sample_step<WAVES, CPWT>(p, *p.step + p.step_off);
 }
 
 __global__ __launch_bounds__(1024) void argmax_sampler_kernel(const HzSamplerParams p) {
-  sample_argmax<16>(p, *p.step);
+  sample_argmax<16>(p, *p.step + p.step_off);
 }
 
-template <int NCH>
+template <int NCH, int R>
 __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   extern __shared__ __attribute__((aligned(16))) float hv[];
   __shared__ float w_best[4];
   __shared__ int w_besti[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int t = *p.step;
+  const int t = *p.step + p.step_off;
   const int par = t & 1;
   const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
+  // R rows per wave round (R <= DROWS): fewer registers -> more resident waves
   if (!HZ_DCHECK(p.H <= p.ldk && p.ldk <= NCH * 512 && p.rpb % DROWS == 0)) return;
+  const int ngroups = (p.V + R - 1) / R;
+  const int gpb = p.rpb / R;
+  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
+  // (measured: issuing the first round of weight rows BEFORE staging h made the kernel 14 %
+  // slower, 26.4 vs 23.1 us at V = 60000, so h is staged first)
   for (int i = tid; i < NCH * 512; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
   __syncthreads();
   const unsigned long long seed = p.keys ? *p.seed : 0ull;
-  const int ngroups = (p.V + DROWS - 1) / DROWS;
-  const int gpb = p.rpb / DROWS;
-  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
   float best = -INFINITY, abest = -INFINITY;
   int besti = 0x7fffffff, abesti = 0x7fffffff;
   for (int g = blockIdx.x * gpb + wave; g < g_end; g += 4) {
-    u32x4 wv[DROWS][NCH];
+    u32x4 wv[R][NCH];
 #pragma unroll
-    for (int q = 0; q < DROWS; ++q) {
-      const int r = min(g * DROWS + q, p.V - 1);
+    for (int q = 0; q < R; ++q) {
+      const int r = min(g * R + q, p.V - 1);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
-        wv[q][c] = c * 512 + lane * 8 < p.ldk
-                       ? *reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8)
-                       : u32x4{0u, 0u, 0u, 0u};
+      for (int c = 0; c < NCH; ++c) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8);
+        wv[q][c] = c * 512 + lane * 8 < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
+      }
     }
-    float acc[DROWS];
+    float acc[R];
 #pragma unroll
-    for (int q = 0; q < DROWS; ++q) acc[q] = 0.f;
+    for (int q = 0; q < R; ++q) acc[q] = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int k = c * 512 + lane * 8;
       const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
 #pragma unroll
-      for (int q = 0; q < DROWS; ++q) {
+      for (int q = 0; q < R; ++q) {
         float f[8];
         unpack8(wv[q][c], f);
         acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
@@ -433,12 +489,12 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
       }
     }
 #pragma unroll
-    for (int q = 0; q < DROWS; ++q) acc[q] = warp_sum(acc[q]);
-    if (lane < DROWS) {
-      const int r = g * DROWS + lane;
+    for (int q = 0; q < R; ++q) acc[q] = warp_sum(acc[q]);
+    if (lane < R) {
+      const int r = g * R + lane;
       float a = acc[0];
 #pragma unroll
-      for (int q = 1; q < DROWS; ++q) a = lane == q ? acc[q] : a;
+      for (int q = 1; q < R; ++q) a = lane == q ? acc[q] : a;
       if (r < p.V) {
         const float lg = a + (p.bias ? p.bias[r] : 0.f);
         p.logits[r] = lg;
@@ -459,11 +515,11 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
       }
     }
   }
-  if (p.keys) {  // workgroup max keys: lanes 0-7 hold the candidates, xor 1/2/4 stays inside them
+  if (p.keys) {  // workgroup max keys: lanes 0..R-1 hold the candidates, xor 1..R/2 stays inside them
     __shared__ float a_best[4];
     __shared__ int a_besti[4];
 #pragma unroll
-    for (int o = 1; o < DROWS; o <<= 1) {
+    for (int o = 1; o < R; o <<= 1) {
       const float ov = __shfl_xor(best, o, 64);
       const int oi = __shfl_xor(besti, o, 64);
       const float av = __shfl_xor(abest, o, 64);
@@ -510,6 +566,8 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
 extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   const HzLstmParams& p = *pp;
   if (p.ldk % 64 || p.ldk < p.In + p.H || p.In <= 0 || p.H <= 0) return -1;
+  if (p.bacc_val && (!p.emb || !p.n_forced || !p.bacc_idx || !p.bmax_val || !p.bmax_idx || p.nblk < 1 || p.nblk > 2048 || p.V < 1))
+    return -1;
   constexpr int KW = 2;  // waves per unit (K split)
   const int nch = (p.ldk + 511) / 512;
   const dim3 grid((p.H + 4 / KW - 1) / (4 / KW)), block(256);
@@ -523,6 +581,18 @@ extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
     case 6: hipLaunchKernelGGL((lstm_cell_kernel<6, KW>), grid, block, lds, st, p); break;
     default: return -1;
   }
+  return (int)hipGetLastError();
+}
+
+namespace {
+__global__ void step_bump_kernel(int* step, int n) {
+  if (threadIdx.x == 0) *step += n;
+}
+}  // namespace
+
+extern "C" int hz_step_bump_launch(int* step, int n, hipStream_t st) {
+  if (!step) return -1;
+  hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(64), 0, st, step, n);
   return (int)hipGetLastError();
 }
 
@@ -544,11 +614,14 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const dim3 grid(nblk), block(256);
   const int nch = (p.ldk + 511) / 512;
   const size_t lds = (size_t)nch * 512 * sizeof(float);
+  // 4 rows per wave round: 72 VGPRs, 7 waves/SIMD (8 rows: 104 VGPRs, 4 waves/SIMD; 22.7 vs 23.3 us
+  // at V = 60000). Non-temporal weight loads measured slower for the decoder and the LSTM cells.
+  constexpr int R = 4;
   switch (nch) {
-    case 1: hipLaunchKernelGGL(decoder_kernel<1>, grid, block, lds, st, p); break;
-    case 2: hipLaunchKernelGGL(decoder_kernel<2>, grid, block, lds, st, p); break;
-    case 3: hipLaunchKernelGGL(decoder_kernel<3>, grid, block, lds, st, p); break;
-    case 4: hipLaunchKernelGGL(decoder_kernel<4>, grid, block, lds, st, p); break;
+    case 1: hipLaunchKernelGGL((decoder_kernel<1, R>), grid, block, lds, st, p); break;
+    case 2: hipLaunchKernelGGL((decoder_kernel<2, R>), grid, block, lds, st, p); break;
+    case 3: hipLaunchKernelGGL((decoder_kernel<3, R>), grid, block, lds, st, p); break;
+    case 4: hipLaunchKernelGGL((decoder_kernel<4, R>), grid, block, lds, st, p); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -143,6 +143,9 @@ int hz_prog_add_sampler(HzProgram h, const HzSamplerParams* sp, int slot) {
   HzSamplerParams c = *sp;
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [c](hipStream_t s) { return hz_sampler_launch(&c, s); });
 }
+int hz_prog_add_step_bump(HzProgram h, int* step, int n, int slot) {
+  return add_op(static_cast<Program*>(h), slot, Op::LAUNCH, [=](hipStream_t s) { return hz_step_bump_launch(step, n, s); });
+}
 int hz_prog_add_fork(HzProgram h, int slot) {
   if (slot < 1) return -4;
   return add_op(static_cast<Program*>(h), slot, Op::FORK, nullptr);

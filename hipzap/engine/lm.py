@@ -6,10 +6,15 @@ The reference rebuilds the model and runs 201 CPU forwards per request with auto
     gate rows interleaved (unit j -> rows 4j..4j+3), ``b_ih + b_hh`` folded, K padded to a
     multiple of 64 (128-B rows; the kernels predicate the partial last 512-chunk), bf16;
     the tied embedding/decoder matrix is stored once (bf16, padded);
-  * one decode step = ``L`` fused LSTM-cell kernels + decoder GEMV + device sampler
-    (csrc/lstm.hip), captured ONCE as a hipGraph; the recurrent state, the step counter, the
-    prompt length, the RNG seed and the token sequence all live on the device, so a request
-    is ``P + n - 1`` back-to-back graph replays and a single device->host copy at the end.
+  * one decode step = ``L`` fused LSTM-cell kernels + decoder GEMV (csrc/lstm.hip); the
+    argmax sampler is fused into the NEXT step's layer-0 kernel (every workgroup reduces the
+    decoder's per-workgroup maxima itself), so a step is L + 1 kernels. ``unroll`` steps are
+    captured into ONE hipGraph (kernel k of step u reads step ``*step + u``; a 1-thread kernel
+    advances the counter once per graph). The recurrent state, the step counter, the prompt
+    length, the RNG seed and the token sequence all live on the device, so a request is
+    ``ceil((P + n - 1) / unroll)`` graph replays, one final sampler launch and a single
+    device->host copy. With ``record_draws`` the standalone top-10 tournament sampler runs in
+    every step instead (exactness / distribution tests).
   * the SURVEY §5.4 checkpoint rule applies: effective W_hh = ``module.weight_hh_l0`` when
     present, else ``weight_hh_l0_raw``.
 """
@@ -17,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 import threading
 
 import torch
@@ -73,7 +79,7 @@ def pack_awd_lstm(sd: dict, device) -> dict:
 
 class LMEngine:
     def __init__(self, packed: dict, device="cuda:0", max_steps: int = 1024, exclude_ids=(), record_draws=False,
-                 capture: bool = True):
+                 capture: bool = True, unroll: int = 8):
         self.p = packed
         self.device = torch.device(device)
         self.max_steps = max_steps
@@ -91,7 +97,16 @@ class LMEngine:
             self.logits = torch.zeros(packed["V"], device=dev)
             self.keys = torch.zeros(packed["V"], device=dev)  # logits + Gumbel noise (decoder epilogue)
             self.draws = torch.full((max_steps, NUM_DRAWS), -1, dtype=torch.int32, device=dev) if record_draws else None
-            self.prog = lib.hz_prog_create()
+            nblk, rpb = C.c_int(), C.c_int()
+            lib.hz_decoder_geometry(packed["V"], C.byref(nblk), C.byref(rpb))
+            nblk, rpb = nblk.value, rpb.value
+            self.bmax_val = torch.empty(nblk, device=dev)  # decoder workgroup maxima -> sampler
+            self.bmax_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
+            self.bacc_val = torch.empty(nblk, device=dev)  # maxima over acceptable rows (argmax sampler)
+            self.bacc_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
+            # fused argmax sampler unless draws are recorded (tournament) or forced off
+            self.fused_sampler = not record_draws and not os.environ.get("HIPZAP_SAMPLER_TOURNAMENT")
+            lstm_prms = []
             for i, ly in enumerate(L):
                 prm = N.LstmParams()
                 prm.w, prm.bias = ly["w"].data_ptr(), ly["bias"].data_ptr()
@@ -104,14 +119,12 @@ class LMEngine:
                 prm.In, prm.H, prm.ldk = ly["In"], ly["H"], ly["ldk"]
                 if i == 0 and prm.In > packed["lde"]:
                     raise ValueError("embedding width mismatch")
-                N.check(lib.hz_prog_add_lstm(self.prog, C.byref(prm), 0), "add_lstm")
-            nblk, rpb = C.c_int(), C.c_int()
-            lib.hz_decoder_geometry(packed["V"], C.byref(nblk), C.byref(rpb))
-            nblk, rpb = nblk.value, rpb.value
-            self.bmax_val = torch.empty(nblk, device=dev)  # decoder workgroup maxima -> sampler
-            self.bmax_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
-            self.bacc_val = torch.empty(nblk, device=dev)  # maxima over acceptable rows (argmax sampler)
-            self.bacc_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
+                if i == 0 and self.fused_sampler:
+                    prm.n_forced = self.n_forced.data_ptr()
+                    prm.bacc_val, prm.bacc_idx = self.bacc_val.data_ptr(), self.bacc_idx.data_ptr()
+                    prm.bmax_val, prm.bmax_idx = self.bmax_val.data_ptr(), self.bmax_idx.data_ptr()
+                    prm.nblk, prm.V = nblk, packed["V"]
+                lstm_prms.append(prm)
             ex = [int(e) for e in exclude_ids][:8]
             d = N.DecoderParams()
             d.w = packed["dec"].data_ptr()
@@ -134,10 +147,34 @@ class LMEngine:
             s.n_exclude = len(ex)
             for i, e in enumerate(ex):
                 s.exclude[i] = e
-            N.check(lib.hz_prog_add_decoder(self.prog, C.byref(d), 0), "add_decoder")
-            N.check(lib.hz_prog_add_sampler(self.prog, C.byref(s), 0), "add_sampler")
-            if capture:
-                N.check(lib.hz_prog_capture(self.prog, self.stream.cuda_stream), "capture")
+            self._final = None
+            if self.fused_sampler:  # the last step's token: nothing runs after its decoder
+                self._final = N.SamplerParams.from_buffer_copy(s)
+                self._final.step_off = -1
+            # one step's ops in order (diagnostics: scripts/diag_lm.py)
+            self._ops = [("lstm", prm) for prm in lstm_prms] + [("decoder", d)]
+            if not self.fused_sampler:
+                self._ops.append(("sampler", s))
+
+            def build(reps):
+                prog = lib.hz_prog_create()
+                for u in range(reps):  # kernels of the u-th step of the graph run step *step + u
+                    for kind, prm in self._ops:
+                        q = type(prm).from_buffer_copy(prm)
+                        q.step_off = u
+                        add = {"lstm": lib.hz_prog_add_lstm, "decoder": lib.hz_prog_add_decoder,
+                               "sampler": lib.hz_prog_add_sampler}[kind]
+                        N.check(add(prog, C.byref(q), 0), "add_" + kind)
+                N.check(lib.hz_prog_add_step_bump(prog, self.step.data_ptr(), reps, 0), "add_step_bump")
+                if capture:
+                    N.check(lib.hz_prog_capture(prog, self.stream.cuda_stream), "capture")
+                return prog
+
+            # one step per graph for remainders, `unroll` steps per graph for the bulk of a request:
+            # a graph replay costs ~10 us of host/CP time, more than a step's kernel boundaries
+            self.prog = build(1)
+            self.unroll = max(1, int(unroll)) if capture else 1
+            self.prog_multi = build(self.unroll) if self.unroll > 1 else None
             torch.cuda.synchronize(dev)
         self._lock = threading.Lock()
 
@@ -165,8 +202,13 @@ class LMEngine:
             self.n_forced.fill_(P)
             self.seed.fill_(int(seed) & ((1 << 62) - 1))
             self.tok_seq[:P].copy_(torch.tensor(prompt_ids, dtype=torch.int32), non_blocking=False)
-            if total > 0:
-                N.check(N.lib().hz_prog_replay_n(self.prog, self.stream.cuda_stream, total), "replay_n")
+            bulk, rem = divmod(total, self.unroll) if self.prog_multi else (0, total)
+            if bulk:
+                N.check(N.lib().hz_prog_replay_n(self.prog_multi, self.stream.cuda_stream, bulk), "replay_n")
+            if rem:
+                N.check(N.lib().hz_prog_replay_n(self.prog, self.stream.cuda_stream, rem), "replay_n")
+            if self._final is not None and n_words > 0:
+                N.check(N.lib().hz_sampler_launch(C.byref(self._final), self.stream.cuda_stream), "final sampler")
             out = self.tok_seq[P: P + n_words].to("cpu")
         return out.tolist()
 
@@ -189,9 +231,10 @@ class LMEngine:
 
     def __del__(self):
         try:
-            if getattr(self, "prog", None):
-                N.lib().hz_prog_destroy(self.prog)
-                self.prog = None
+            for name in ("prog", "prog_multi"):
+                if getattr(self, name, None):
+                    N.lib().hz_prog_destroy(getattr(self, name))
+                    setattr(self, name, None)
         except Exception:
             pass
 

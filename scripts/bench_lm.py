@@ -26,12 +26,13 @@ REFERENCE_REQUEST_S = 8.86
 def main():
     V = int(os.environ.get("HIPZAP_LM_VOCAB", 60000))
     words = int(os.environ.get("HIPZAP_LM_WORDS", 200))
+    unroll = int(os.environ.get("HIPZAP_LM_UNROLL", 8))  # decode steps per captured graph
     torch.manual_seed(0)
     itos = synthetic_vocab(V)
     stoi = {w: i for i, w in enumerate(itos)}
     sd = reference_lm(V).state_dict()
     t0 = time.perf_counter()
-    eng = LMEngine.for_vocab(sd, stoi, "cuda:0")
+    eng = LMEngine.for_vocab(sd, stoi, "cuda:0", unroll=unroll)
     cold_ms = (time.perf_counter() - t0) * 1e3
     eng.generate([""], words, itos, stoi, seed=0)  # warm
     lat = []
@@ -63,14 +64,14 @@ def main():
     from concurrent.futures import ThreadPoolExecutor
     from hipzap.engine.lm import LMPool
     conc = int(os.environ.get("HIPZAP_LM_CONTEXTS", 4))
-    pool = LMPool(eng.p, "cuda:0", contexts=conc, exclude_ids=[])
+    pool = LMPool(eng.p, "cuda:0", contexts=conc, exclude_ids=[], unroll=unroll)
     n_req = 4 * conc
     with ThreadPoolExecutor(conc) as ex:
         list(ex.map(lambda s: pool.run_tokens([1], words, s), range(conc)))  # warm
         t = time.perf_counter()
         list(ex.map(lambda s: pool.run_tokens([1], words, s), range(n_req)))
         pool_rps = n_req / (time.perf_counter() - t)
-    res = {"metric": "AWD-LSTM GET /inference latency (200 words)", "vocab": V, "words": words,
+    res = {"metric": "AWD-LSTM GET /inference latency (200 words)", "vocab": V, "words": words, "steps_per_graph": unroll,
            "concurrent_contexts": conc, "requests_per_s_concurrent": round(pool_rps, 2),
            "cold_start_ms": round(cold_ms, 1), "request_s_p50": round(p50, 5),
            "ms_per_token": round(p50 / (words) * 1e3, 4), "http_request_s_p50": round(statistics.median(http), 5),

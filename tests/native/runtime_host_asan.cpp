@@ -30,6 +30,11 @@ STUB(hz_embed_ln_launch, HzEmbedParams, 10, L)
 STUB(hz_attention_launch, HzAttentionParams, 11, L)
 STUB(hz_vit_tokens_launch, HzVitTokensParams, 12, B)
 STUB(hz_softmax_launch, HzSoftmaxParams, 13, rows)
+extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
+  g_calls.push_back(18);
+  g_vals.push_back(n);
+  return 0;
+}
 extern "C" int hz_conv_launch(const HzConvParams* p, int cfg, hipStream_t) {
   g_calls.push_back(1);
   g_vals.push_back(p->K * 100 + cfg);

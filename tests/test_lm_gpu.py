@@ -152,3 +152,18 @@ def test_argmax_sampler_equals_top10_rule(V):
         for step, tok in enumerate(b):
             row = rule.draws[1 + step].tolist()[:min(10, V)]
             assert tok == select_token(row, set(excl))
+
+
+def test_multi_step_graph_matches_single_step_replays(model):
+    """`unroll` decode steps captured in one graph (bulk of a request) + single-step graphs (the
+    remainder) give the same tokens and the same final logits as one graph replay per step."""
+    from hipzap.engine.lm import pack_awd_lstm
+    packed = pack_awd_lstm(model.state_dict(), DEV)
+    one = LMEngine(packed, DEV, unroll=1)
+    multi = LMEngine(packed, DEV, unroll=8)
+    assert multi.prog_multi and one.prog_multi is None
+    for prompt, n in (([5, 17, 200], 21), ([9], 8), ([1, 2, 3, 4], 3)):
+        a = one.run_tokens(prompt, n, seed=7)
+        b = multi.run_tokens(prompt, n, seed=7)
+        assert a == b
+        assert torch.equal(one.logits, multi.logits)
