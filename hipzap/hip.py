@@ -26,7 +26,8 @@ def hip():
                     ("hipHostMalloc", I, [C.POINTER(P), S, C.c_uint]), ("hipHostFree", I, [P]),
                     ("hipMemcpy", I, [P, P, S, I]), ("hipMemcpyAsync", I, [P, P, S, I, P]),
                     ("hipMemsetAsync", I, [P, I, S, P]), ("hipStreamSynchronize", I, [P]),
-                    ("hipDeviceSynchronize", I, []), ("hipGetErrorString", C.c_char_p, [I])):
+                    ("hipDeviceSynchronize", I, []), ("hipGetErrorString", C.c_char_p, [I]),
+                    ("hipStreamCreateWithFlags", I, [C.POINTER(P), C.c_uint]), ("hipGetDevice", I, [C.POINTER(I)])):
                 f = getattr(h, name)
                 f.restype, f.argtypes = res, args
             _hip = h
@@ -92,9 +93,33 @@ class PinnedBuffer:
             pass
 
 
+_tls = threading.local()
+
+
+def _private_stream() -> int:
+    """This thread's non-blocking stream on the current device. Synchronous copies go through it
+    instead of the legacy NULL stream: a NULL-stream copy while another thread captures a hipGraph
+    fails with 'operation would make the legacy stream depend on a capturing blocking stream' (the
+    lazy capture of PlanEngine contexts runs in a background thread of the serving workers)."""
+    d = C.c_int(0)
+    check(hip().hipGetDevice(C.byref(d)), "hipGetDevice")
+    streams = getattr(_tls, "streams", None)
+    if streams is None:
+        streams = _tls.streams = {}
+    s = streams.get(d.value)
+    if s is None:
+        p = C.c_void_p()
+        check(hip().hipStreamCreateWithFlags(C.byref(p), 1), "hipStreamCreateWithFlags")  # hipStreamNonBlocking
+        s = streams[d.value] = p.value
+    return s
+
+
 def memcpy(dst: int, src: int, nbytes: int, kind: int = DEFAULT, stream=None) -> None:
+    """Copy; with ``stream=None`` synchronous (on this thread's private non-blocking stream)."""
     if stream is None:
-        check(hip().hipMemcpy(dst, src, nbytes, kind), "hipMemcpy")
+        s = _private_stream()
+        check(hip().hipMemcpyAsync(dst, src, nbytes, kind, s), "hipMemcpyAsync")
+        check(hip().hipStreamSynchronize(s), "hipStreamSynchronize")
     else:
         check(hip().hipMemcpyAsync(dst, src, nbytes, kind, stream), "hipMemcpyAsync")
 
