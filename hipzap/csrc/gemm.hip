@@ -21,6 +21,8 @@
 //   * same swapped orientation and fused epilogue as conv.hip (4 consecutive output features
 //     per lane: 16-B bias, 8-B residual, 8-B store), XCD-aware tile order.
 // Requirements (checked by the launcher): K % 64 == 0, ldx % 8 == 0, weight rows padded to 128.
+#include <cstdlib>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -77,21 +79,31 @@ __device__ __forceinline__ void rows_stats(const float* __restrict__ st, int nsl
 
 // LNF: folded-LayerNorm variant (p.lnf != NULL); a separate instantiation so the plain GEMM keeps
 // its register budget (the fold's statistics cost ~60 VGPRs, which halves occupancy)
-template <int BM, int BN, int NS, bool LNF>
-__global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
-  constexpr int FCW = BN / 32, FPW = BM / 32;  // 16x16 fragments per wave (2x2 waves)
+// WM x WN waves (4 or 8): wave (wm, wn) owns rows wm*BM/WM.. and features wn*BN/WN..
+template <int BM, int BN, int NS, bool LNF, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvParams p, int group_m) {
+  constexpr int NW = WM * WN;
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 16x16 fragments per wave
   constexpr int NWG = BN / 16;                 // weight fragments per 32-deep k-step
   constexpr int XBYTES = BM * 128;             // activation bytes per stage (BK = 64 bf16 = 128 B)
   constexpr int SBYTES = XBYTES + BN * 128;    // + 2 k-steps x NWG fragments x 1 KiB
-  constexpr int XPW = BM / 32, WPW = BN / 32;  // glds pieces per wave per stage (x, w)
+  constexpr int XPW = BM / 8 / NW, WPW = 2 * NWG / NW;  // glds pieces per wave per stage (x, w)
+  static_assert(XPW * 8 * NW == BM && WPW * NW == 2 * NWG && FCW >= 1 && FPW >= 1, "tile / wave split");
   constexpr int G = XPW + WPW;
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave & 1, wm = wave >> 1;
-  const int tiles_n = (p.Cout + BN - 1) / BN;
+  const int wn = wave % WN, wm = wave / WN;
+  const int tiles_n = (p.Cout + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile_n = lid % tiles_n, tile_m = lid / tiles_n;
+  // grouped raster: consecutive logical tiles (= one XCD's share after xcd_remap) walk group_m
+  // tile rows before the next feature tile, so an XCD's L2 holds a group_m x (share / group_m)
+  // block of X rows and W columns instead of two X row-panels x ALL of W (5.1 MB > 4 MB L2 at
+  // BERT FFN1); group_m = 1 is the plain row-major raster
+  const int per_group = group_m * tiles_n, gid = lid / per_group, first_m = gid * group_m;
+  const int gsz = min(tiles_m - first_m, group_m);
+  const int tile_m = first_m + (lid - gid * per_group) % gsz;
+  const int tile_n = (lid - gid * per_group) / gsz;
   const int n0 = tile_n * BN, m0 = tile_m * BM;
   const int nst = p.ksteps >> 1;
 
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   const bf16_t* xsrc[XPW];
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
-    const int q = wave + 4 * i;
+    const int q = wave + NW * i;
     const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
     const int chunk = (lane & 7) ^ (((q & 1) << 2) + (lane >> 4));
     xsrc[i] = p.x + (long)row * p.ldx + chunk * 8;
@@ -116,10 +128,10 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   auto stage = [&](int buf, int st) {
     char* base = smem + buf * SBYTES;
 #pragma unroll
-    for (int i = 0; i < XPW; ++i) glds16(xsrc[i] + st * 64, base + (wave + 4 * i) * 1024);
+    for (int i = 0; i < XPW; ++i) glds16(xsrc[i] + st * 64, base + (wave + NW * i) * 1024);
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
-      const int f = wave + 4 * i;  // f = ks * NWG + g
+      const int f = wave + NW * i;  // f = ks * NWG + g
       const int ks = f / NWG, g = f - ks * NWG;
       glds16(wsrc + ((long)g * p.ksteps + st * 2 + ks) * 512, base + XBYTES + f * 1024);
     }
@@ -127,8 +139,8 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
 
   // reader offsets: B fragment j of k-step ks = rows wm*BM/2 + 16j + (lane&15), chunk 4ks + (lane>>4)
   const int lr = lane & 15, sw = (lane >> 1) & 7;
-  const int boff0 = (wm * (BM / 2) + lr) * 128 + (((lane >> 4)) ^ sw) * 16;
-  const int boff1 = (wm * (BM / 2) + lr) * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
+  const int boff0 = (wm * (BM / WM) + lr) * 128 + (((lane >> 4)) ^ sw) * 16;
+  const int boff1 = (wm * (BM / WM) + lr) * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
   const int aoff = XBYTES + (wn * FCW) * 1024 + lane * 16;
 
   f32x4 acc[FCW][FPW];
@@ -147,10 +159,10 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   const int lrow = lane & 15;
   float mu_in[FPW], rs_in[FPW], mu_r[FPW], rs_r[FPW];
   if (f_in)
-    rows_stats<FPW>(lf->stats_in, lf->nslab_in, lf->ld_stats, m0 + wm * (BM / 2) + lrow, p.M, lf->inv_d, lf->eps_in,
+    rows_stats<FPW>(lf->stats_in, lf->nslab_in, lf->ld_stats, m0 + wm * (BM / WM) + lrow, p.M, lf->inv_d, lf->eps_in,
                     mu_in, rs_in);
   if (f_res)
-    rows_stats<FPW>(lf->res_stats, lf->nslab_res, lf->ld_stats, m0 + wm * (BM / 2) + lrow, p.M, lf->inv_d,
+    rows_stats<FPW>(lf->res_stats, lf->nslab_res, lf->ld_stats, m0 + wm * (BM / WM) + lrow, p.M, lf->inv_d,
                     lf->eps_res, mu_r, rs_r);
   int cur = 0;
   for (int st = 0; st < nst; ++st) {
@@ -184,12 +196,12 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
   // normalised residual, and per-row (sum, sumsq) partials of the stored bf16 output.
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
-    const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
+    const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
     const bool mval = m < p.M;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
-      const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      const int n = n0 + wn * (BN / WN) + i * 16 + (lane >> 4) * 4;
       const long o = (long)m * p.ldo + n;
       if (!mval || n >= p.Cout || !HZ_DCHECK(o + 4 <= (long)(p.M - 1) * p.ldo + p.Cout)) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
@@ -244,18 +256,28 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const HzConvParams p) {
       s2 += __shfl_xor(s2, 16);
       s1 += __shfl_xor(s1, 32);
       s2 += __shfl_xor(s2, 32);
-      const long so = 2 * ((long)(tile_n * 2 + wn) * lf->ld_stats + m);
+      const long so = 2 * ((long)(tile_n * WN + wn) * lf->ld_stats + m);
       if (lane < 16 && mval && HZ_DCHECK(m < lf->ld_stats))
         *reinterpret_cast<float2*>(lf->stats_out + so) = make_float2(s1, s2);
     }
   }
 }
 
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, int WM = 2, int WN = 2>
 int launch_lds(const HzConvParams& p, hipStream_t st) {
+  // the last feature tile must stay inside the 128-row padded weight packing (BN = 96 / 192 / 288
+  // tiles fit only some widths: every BERT / ViT projection, not arbitrary N)
+  if (((p.Cout + BN - 1) / BN) * BN > ((p.Cout + 127) / 128) * 128) return -4;
   const int tiles = ((p.Cout + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  if (p.lnf) hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p);
+  const dim3 block(64 * WM * WN);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  if (p.lnf) {  // the folded-LayerNorm statistics slabs assume 2 feature halves per tile
+    if (WN != 2) return -3;
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
+  } else {
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN>), dim3(tiles), block, 0, st, p, group_m);
+  }
   return (int)hipGetLastError();
 }
 
@@ -263,7 +285,9 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
 
 // cfg 16: 128x128, 17: 64x128 (BM x BN), 18: 128x64, 19: 64x64 with 3 LDS stages; cfg 20-23: the same
 // tiles with 2 stages (less LDS: more workgroups per CU); cfg 24-27: 4 stages (deeper prefetch for
-// short-K / latency-bound shapes). Row-major activations only.
+// short-K / latency-bound shapes); cfg 28-33: 8-wave workgroups (128x128 3/2 stages, 256x128,
+// 128x64, 64x128, 256x64); cfg 34-40: one-tile-per-CU shapes for M = 2048 (64x96, 128x192,
+// 64x288, 256x96). Row-major activations only.
 extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
   if (!p.x_rowmajor || !p.out_rowmajor || p.K % 64 || p.ksteps * 32 != p.K || p.ldx % 8 || p.Cout % 4) return -1;
@@ -280,6 +304,22 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
     case 25: return launch_lds<64, 128, 4>(p, st);
     case 26: return launch_lds<128, 64, 4>(p, st);
     case 27: return launch_lds<64, 64, 4>(p, st);
+    // 8 waves per workgroup (two per SIMD at one workgroup per CU)
+    case 28: return launch_lds<128, 128, 3, 2, 4>(p, st);
+    case 29: return launch_lds<128, 128, 2, 2, 4>(p, st);
+    case 30: return launch_lds<256, 128, 2, 4, 2>(p, st);
+    case 31: return launch_lds<128, 64, 3, 4, 2>(p, st);
+    case 32: return launch_lds<64, 128, 3, 2, 4>(p, st);
+    case 33: return launch_lds<256, 64, 2, 4, 2>(p, st);
+    // tiles sized so that an M = 2048 projection makes exactly 256 tiles (one per CU): N = 768 ->
+    // 64 x 96, N = 3072 -> 128 x 192, N = 2304 -> 64 x 288, N = 3072 -> 256 x 96
+    case 34: return launch_lds<64, 96, 3, 2, 2>(p, st);
+    case 35: return launch_lds<128, 192, 3, 2, 4>(p, st);
+    case 36: return launch_lds<128, 192, 2, 2, 4>(p, st);
+    case 37: return launch_lds<64, 288, 2, 2, 2>(p, st);
+    case 38: return launch_lds<64, 288, 3, 2, 2>(p, st);
+    case 39: return launch_lds<256, 96, 2, 2, 2>(p, st);
+    case 40: return launch_lds<64, 96, 4, 2, 2>(p, st);
     default: return -2;
   }
 }

@@ -25,7 +25,11 @@ GEMM_ROW_PAD = 128  # linear weights: rows padded to the largest LDS-tiled GEMM 
 # 16-19 use 3 LDS stages, 20-23 the same tiles with 2 (half the LDS: more workgroups per CU)
 LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
              20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64),
-             24: (128, 128), 25: (64, 128), 26: (128, 64), 27: (64, 64)}  # 3 / 2 / 4 LDS stages
+             24: (128, 128), 25: (64, 128), 26: (128, 64), 27: (64, 64),  # 3 / 2 / 4 LDS stages
+             28: (128, 128), 29: (128, 128), 30: (256, 128), 31: (128, 64), 32: (64, 128),
+             33: (256, 64),  # 28-33: 8-wave workgroups
+             34: (64, 96), 35: (128, 192), 36: (128, 192), 37: (64, 288), 38: (64, 288), 39: (256, 96),
+             40: (64, 96)}  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
 
@@ -150,6 +154,12 @@ def lds_ok(M: int, K: int, rowmajor: bool, pc: PackedConv | None = None) -> bool
     return pc is None or (pc.wf.shape[0] % (GEMM_ROW_PAD // 16) == 0 and pc.ksteps * 32 == K)
 
 
+def lds_fits(cfg: int, cout: int) -> bool:
+    """The last BN-wide feature tile stays inside the GEMM_ROW_PAD-padded weight rows."""
+    bn = LDS_TILES[cfg][1]
+    return math.ceil(cout / bn) * bn <= math.ceil(cout / GEMM_ROW_PAD) * GEMM_ROW_PAD
+
+
 def legal(cfg: int, kw: int) -> bool:
     if cfg in LDS_TILES:
         return kw == 1
@@ -162,7 +172,7 @@ def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv
     steps = max(1, math.ceil(K / 32))
     out = []
     if lds_ok(M, K, rowmajor, pc):
-        out += [(cfg, 1) for cfg in LDS_TILES]
+        out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout)]
     for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue
@@ -184,7 +194,7 @@ def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str
     """
     if tuned is not None and key is not None and key in tuned:
         v = tuned[key]
-        if int(v[0]) not in LDS_TILES or lds_ok(M, K, rowmajor, pc):
+        if int(v[0]) not in LDS_TILES or (lds_ok(M, K, rowmajor, pc) and lds_fits(int(v[0]), cout)):
             return int(v[0]), int(v[1])
     if lds_ok(M, K, rowmajor, pc) and M >= 512:
         # large-M GEMM: the biggest LDS tile that still gives every CU a workgroup
