@@ -91,9 +91,12 @@ struct Plan {
   std::mutex mu;
   double t[HZ_PLAN_NT] = {};
 
+  hipStream_t spare = nullptr;  // the upload stream, handed to the first context (stream creation is
+                                // ~10-25 ms of lazy runtime work in a fresh process)
   ~Plan() {
     (void)hipSetDevice(device);
     for (auto& c : ctx) free_ctx(c);
+    if (spare) (void)hipStreamDestroy(spare);
     if (blob) (void)hipFree(blob);
     if (map) munmap(map, map_len);
     if (fd >= 0) close(fd);
@@ -195,25 +198,39 @@ struct Plan {
       const size_t chunk = size_t(4) << 20;
       void* stage[2] = {nullptr, nullptr};
       hipEvent_t done[2] = {nullptr, nullptr};
+      double ph[5] = {0, 0, 0, 0, 0};  // diagnostics: host alloc, pread, buffer waits, final sync, free
+      double tp = now_ms();
       bool ok = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
                 hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
                 hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
+      ph[0] = now_ms() - tp;
       int k = 0;
       for (size_t off = 0; ok && off < h.blob_len; off += chunk, k ^= 1) {
         const size_t n = h.blob_len - off < chunk ? h.blob_len - off : chunk;
+        tp = now_ms();
         if (off >= 2 * chunk) ok = hipEventSynchronize(done[k]) == hipSuccess;  // buffer k free again
+        ph[2] += now_ms() - tp;
         if (!ok) break;
+        tp = now_ms();
         ssize_t got = pread(fd, stage[k], n, (off_t)(h.blob_off + off));
+        ph[1] += now_ms() - tp;
         ok = got == (ssize_t)n &&
              hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, stage[k], n, hipMemcpyHostToDevice, st) == hipSuccess &&
              hipEventRecord(done[k], st) == hipSuccess;
       }
+      tp = now_ms();
       if (ok) ok = hipStreamSynchronize(st) == hipSuccess;
+      ph[3] = now_ms() - tp;
+      tp = now_ms();
       for (int i = 0; i < 2; ++i) {
         if (done[i]) (void)hipEventDestroy(done[i]);
         if (stage[i]) (void)hipHostFree(stage[i]);
       }
+      ph[4] = now_ms() - tp;
+      if (probe && probe[0] == '2')
+        std::fprintf(stderr, "hipzap plan upload: host_alloc %.2f pread %.2f waits %.2f sync %.2f free %.2f ms\n", ph[0],
+                     ph[1], ph[2], ph[3], ph[4]);
       if (ok) return 0;
       (void)hipGetLastError();
     }
@@ -285,7 +302,13 @@ struct Plan {
     for (int k = 0; k < n; ++k) {
       PlanCtx c;
       double t0 = now_ms();
-      hipError_t e = hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking);
+      hipError_t e = hipSuccess;
+      if (spare) {
+        c.st = spare;
+        spare = nullptr;
+      } else {
+        e = hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking);
+      }
       if (e == hipSuccess) e = hipMalloc(&c.dev, h.ctx_dev_bytes ? h.ctx_dev_bytes : 256);
       if (e == hipSuccess && h.ctx_dev_bytes) e = hipMemsetAsync(c.dev, 0, h.ctx_dev_bytes, c.st);
       if (e == hipSuccess) e = hipHostMalloc(&c.host, h.ctx_host_bytes ? h.ctx_host_bytes : 256, hipHostMallocDefault);
@@ -394,13 +417,17 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
     return nullptr;
   }
   if (read_blob) {
-    hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || p->upload_blob(s)) {
-      if (g_err.empty()) fail("plan: stream creation failed");
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      fail("plan: stream creation failed");
       delete p;
       return nullptr;
     }
-    (void)hipStreamDestroy(s);
+    p->spare = s;  // kept: becomes the first context's stream
+    if (p->upload_blob(s)) {
+      delete p;
+      return nullptr;
+    }
   }
   p->t[HZ_PLAN_T_UPLOAD] = now_ms() - t2 - p->t[HZ_PLAN_T_BLOB_ALLOC];
   if (timings) std::memcpy(timings, p->t, sizeof(p->t));
