@@ -66,9 +66,12 @@ struct PlanCtx {
   void* host = nullptr;
   HzProgram prog = nullptr;
   hipStream_t st = nullptr;
+  bool own_stream = true;  // false: borrowed from an earlier context (HIPZAP_CTX_STREAMS)
 };
 
 thread_local std::string g_err;
+
+int capture_ctx_prog(const PlanCtx& c);
 
 int fail(const std::string& msg, int rc = -1) {
   g_err = msg;
@@ -95,6 +98,9 @@ struct Plan {
                                 // ~10-25 ms of lazy runtime work in a fresh process)
   ~Plan() {
     (void)hipSetDevice(device);
+    // borrowed streams first: their owners' free_ctx destroys the stream
+    for (auto& c : ctx)
+      if (!c.own_stream) free_ctx(c);
     for (auto& c : ctx) free_ctx(c);
     if (spare) (void)hipStreamDestroy(spare);
     if (blob) (void)hipFree(blob);
@@ -105,7 +111,7 @@ struct Plan {
   static void free_ctx(PlanCtx& c) {
     if (c.st) (void)hipStreamSynchronize(c.st);
     if (c.prog) hz_prog_destroy(c.prog);
-    if (c.st) (void)hipStreamDestroy(c.st);
+    if (c.st && c.own_stream) (void)hipStreamDestroy(c.st);
     if (c.dev) (void)hipFree(c.dev);
     if (c.host) (void)hipHostFree(c.host);
     c = PlanCtx{};
@@ -303,7 +309,19 @@ struct Plan {
       PlanCtx c;
       double t0 = now_ms();
       hipError_t e = hipSuccess;
-      if (spare) {
+      // HIPZAP_CTX_STREAMS=k: contexts share k streams round-robin (k ~ the hardware queues)
+      const char* ks = getenv("HIPZAP_CTX_STREAMS");
+      const int kshare = ks ? atoi(ks) : 0;
+      size_t nctx;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        nctx = ctx.size();
+      }
+      if (kshare > 0 && nctx >= (size_t)kshare) {
+        std::lock_guard<std::mutex> g(mu);
+        c.st = ctx[nctx % kshare].st;
+        c.own_stream = false;
+      } else if (spare) {
         c.st = spare;
         spare = nullptr;
       } else {
@@ -320,7 +338,7 @@ struct Plan {
       double t1 = now_ms();
       int rc = bind(c);
       double t2 = now_ms();
-      if (!rc && capture) rc = hz_prog_capture(c.prog, c.st);
+      if (!rc && capture) rc = capture_ctx_prog(c);
       if (!rc && hipStreamSynchronize(c.st) != hipSuccess) rc = fail("plan: context sync failed");
       double t3 = now_ms();
       if (rc) {
@@ -339,6 +357,22 @@ struct Plan {
 };
 
 Plan* P(void* h) { return static_cast<Plan*>(h); }
+
+// Capture a context's program. A borrowed (shared) stream may carry other contexts' replays
+// issued by other threads meanwhile, which a capture on it would swallow: capture those on a
+// private stream instead (a graph replays on any stream).
+int capture_ctx_prog(const PlanCtx& c) {
+  if (c.own_stream) {
+    int rc = hz_prog_capture(c.prog, c.st);
+    return rc ? rc : (int)hipStreamSynchronize(c.st);
+  }
+  hipStream_t tmp = nullptr;
+  if (hipStreamCreateWithFlags(&tmp, hipStreamNonBlocking) != hipSuccess) return fail("plan: stream creation failed");
+  int rc = hz_prog_capture(c.prog, tmp);
+  if (!rc) rc = (int)hipStreamSynchronize(tmp);
+  (void)hipStreamDestroy(tmp);
+  return rc;
+}
 
 }  // namespace
 
@@ -527,8 +561,7 @@ int hz_plan_capture_ctx(void* h, int ctx) {
   if (!c.prog) return fail("plan: no such context");
   if (hipSetDevice(p->device) != hipSuccess) return fail("plan: hipSetDevice failed");
   const double t0 = now_ms();
-  int rc = hz_prog_capture(c.prog, c.st);
-  if (!rc) rc = (int)hipStreamSynchronize(c.st);
+  int rc = capture_ctx_prog(c);
   p->t[HZ_PLAN_T_CAPTURE] += now_ms() - t0;
   return rc;
 }
