@@ -71,7 +71,8 @@ struct PlanCtx {
 
 thread_local std::string g_err;
 
-int capture_ctx_prog(const PlanCtx& c);
+struct Plan;
+int capture_ctx_prog(Plan* p, const PlanCtx& c);
 
 int fail(const std::string& msg, int rc = -1) {
   g_err = msg;
@@ -96,6 +97,8 @@ struct Plan {
 
   hipStream_t spare = nullptr;  // the upload stream, handed to the first context (stream creation is
                                 // ~10-25 ms of lazy runtime work in a fresh process)
+  hipStream_t cap_st = nullptr;  // private capture stream for contexts on borrowed streams
+  std::mutex cap_mu;
   ~Plan() {
     (void)hipSetDevice(device);
     // borrowed streams first: their owners' free_ctx destroys the stream
@@ -103,6 +106,7 @@ struct Plan {
       if (!c.own_stream) free_ctx(c);
     for (auto& c : ctx) free_ctx(c);
     if (spare) (void)hipStreamDestroy(spare);
+    if (cap_st) (void)hipStreamDestroy(cap_st);
     if (blob) (void)hipFree(blob);
     if (map) munmap(map, map_len);
     if (fd >= 0) close(fd);
@@ -310,6 +314,7 @@ struct Plan {
       double t0 = now_ms();
       hipError_t e = hipSuccess;
       // HIPZAP_CTX_STREAMS=k: contexts share k streams round-robin (k ~ the hardware queues)
+      // (default 0 = one stream each; see engine.py _new_contexts for the measurements)
       const char* ks = getenv("HIPZAP_CTX_STREAMS");
       const int kshare = ks ? atoi(ks) : 0;
       size_t nctx;
@@ -338,7 +343,7 @@ struct Plan {
       double t1 = now_ms();
       int rc = bind(c);
       double t2 = now_ms();
-      if (!rc && capture) rc = capture_ctx_prog(c);
+      if (!rc && capture) rc = capture_ctx_prog(this, c);
       if (!rc && hipStreamSynchronize(c.st) != hipSuccess) rc = fail("plan: context sync failed");
       double t3 = now_ms();
       if (rc) {
@@ -361,17 +366,18 @@ Plan* P(void* h) { return static_cast<Plan*>(h); }
 // Capture a context's program. A borrowed (shared) stream may carry other contexts' replays
 // issued by other threads meanwhile, which a capture on it would swallow: capture those on a
 // private stream instead (a graph replays on any stream).
-int capture_ctx_prog(const PlanCtx& c) {
+int capture_ctx_prog(Plan* p, const PlanCtx& c) {
   if (c.own_stream) {
     int rc = hz_prog_capture(c.prog, c.st);
     return rc ? rc : (int)hipStreamSynchronize(c.st);
   }
-  hipStream_t tmp = nullptr;
-  if (hipStreamCreateWithFlags(&tmp, hipStreamNonBlocking) != hipSuccess) return fail("plan: stream creation failed");
-  int rc = hz_prog_capture(c.prog, tmp);
-  if (!rc) rc = (int)hipStreamSynchronize(tmp);
-  (void)hipStreamDestroy(tmp);
-  return rc;
+  std::lock_guard<std::mutex> g(p->cap_mu);  // one private capture stream per plan
+  if (!p->cap_st && hipStreamCreateWithFlags(&p->cap_st, hipStreamNonBlocking) != hipSuccess) {
+    p->cap_st = nullptr;
+    return fail("plan: stream creation failed");
+  }
+  int rc = hz_prog_capture(c.prog, p->cap_st);
+  return rc ? rc : (int)hipStreamSynchronize(p->cap_st);
 }
 
 }  // namespace
@@ -561,7 +567,7 @@ int hz_plan_capture_ctx(void* h, int ctx) {
   if (!c.prog) return fail("plan: no such context");
   if (hipSetDevice(p->device) != hipSuccess) return fail("plan: hipSetDevice failed");
   const double t0 = now_ms();
-  int rc = capture_ctx_prog(c);
+  int rc = capture_ctx_prog(p, c);
   p->t[HZ_PLAN_T_CAPTURE] += now_ms() - t0;
   return rc;
 }

@@ -93,8 +93,10 @@ class Engine:
     def _new_contexts(self, n: int):
         ctxs = [ExecContext(self.graph, self.params, self.device, self.tuned, host_io=self.host_io,
                             zero_copy=self._zero_copy) for _ in range(n)]
-        # HIPZAP_CTX_STREAMS=k: contexts share k streams round-robin (k ~ the hardware queues) instead
-        # of one stream each (scripts/diag_cumask.py: 4 shared streams replay 15 % faster than 16 own)
+        # HIPZAP_CTX_STREAMS=k: contexts share k streams round-robin instead of one stream each (0,
+        # default). k = 4 replays 11 % faster when the 4 streams land on the 4 hardware queues, but
+        # which queue a stream gets is the runtime's choice: after engine rebuilds the same k = 4
+        # ran at 6.5k (two queues' worth) vs 11.3k with own streams (profiles/r2_dispatch/)
         k = int(os.environ.get("HIPZAP_CTX_STREAMS", "0"))
         pool = getattr(self, "_stream_pool", [])
         self._stream_pool = pool
@@ -113,10 +115,13 @@ class Engine:
     def _capture_all(self, ctxs, streams) -> None:
         if self._capture:
             shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0
+            cap = torch.cuda.Stream(device=self.device) if shared else None
             for c, s in zip(ctxs, streams):
                 # a shared stream may carry other contexts' replays (other threads) that a capture
                 # on it would swallow: capture on a private stream, replay on the shared one
-                c.capture(torch.cuda.Stream(device=self.device) if shared else s)
+                c.capture(cap if shared else s)
+            if cap is not None:
+                cap.synchronize()
 
     def ensure_contexts(self) -> float:
         """Plan + capture the contexts deferred by ``eager_contexts``; returns the ms spent.
