@@ -1,19 +1,13 @@
 #!/bin/bash
-# Interleaved A/B of bench.py under different environment settings on ONE box:
-#   VARIANTS="base:  zc:HIPZAP_ZERO_COPY=all" STREAMS="1 8" REPS=2 bash scripts/ab_env.sh
-# (box-to-box variance is larger than most effects; only same-box interleaved runs compare)
+# Same-box A/B of an environment variable on the serving bench (interleaved runs).
+#   bash scripts/ab_env.sh OUTDIR VAR "v1 v2 ..." [bench args...]   (value "unset" = not set)
 set -u
-OUT=${OUT:-gpurun_out/ab_env}
-mkdir -p $OUT
-for rep in $(seq 1 ${REPS:-2}); do
-  for v in ${VARIANTS}; do
-    tag=${v%%:*}; envs=${v#*:}
-    for s in ${STREAMS:-1 8}; do
-      log=$OUT/${tag}_s${s}_$rep.log
-      env $(echo $envs | tr ',' ' ') timeout -k 10 300 python bench.py --streams $s --steps ${STEPS:-300} --warmup 30 --cold-runs 0 ${EXTRA:-} > $log 2>&1
-      rc=$?
-      echo "$tag s$s rep$rep rc=$rc $(grep -h '^{' $log | python3 -c 'import sys,json; [print(json.loads(l).get("value"), json.loads(l).get("latency_ms_p50_single")) for l in sys.stdin]' 2>/dev/null)"
-      if [ $rc -ne 0 ]; then echo "STOP $tag rc=$rc"; tail -5 $log; exit $rc; fi
-    done
-  done
+out=$1; var=$2; vals=$3; shift 3
+mkdir -p "$out"
+for v in $vals $vals; do
+  if [ "$v" = unset ]; then
+    timeout -k 10 200 python bench.py "$@" >> "$out/$v.jsonl" 2>> "$out/err.log" || exit 1
+  else
+    env "$var=$v" timeout -k 10 200 python bench.py "$@" >> "$out/$v.jsonl" 2>> "$out/err.log" || exit 1
+  fi
 done

@@ -48,9 +48,12 @@ def test_vit_fp8_engine_vs_hf():
     with torch.no_grad():
         ref = m(pixel_values=x).logits
     rel = ((out - ref).abs().max() / ref.abs().max()).item()
-    assert rel < 0.25, rel
+    # measured on MI355X (scripts/check_vit_fp8_err.py, same seed): rel 0.099, cos 0.993, top-1
+    # equal; bf16 engine 0.010 / 0.99993. e4m3 weights + per-row e4m3 activations through 12 layers
+    assert rel < 0.15, rel
     cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
-    assert cos.min() > 0.97, cos
+    assert cos.min() > 0.985, cos
+    assert torch.equal(out.argmax(1), ref.argmax(1))
 
 
 def test_layernorm_fused_fp8_quant():
