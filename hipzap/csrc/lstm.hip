@@ -615,7 +615,10 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const int nch = (p.ldk + 511) / 512;
   const size_t lds = (size_t)nch * 512 * sizeof(float);
   // 4 rows per wave round: 72 VGPRs, 7 waves/SIMD (8 rows: 104 VGPRs, 4 waves/SIMD; 22.7 vs 23.3 us
-  // at V = 60000). Non-temporal weight loads measured slower for the decoder and the LSTM cells.
+  // at V = 60000). Non-temporal weight loads measured slower for the decoder and the LSTM cells; so
+  // was a streaming variant (a wave walks 1/2/4 whole blocks with the next 4 rows in flight, h
+  // staged once per workgroup): 23.8 / 29.9 / 53.1 vs 22.3 us -- one short round per workgroup
+  // with every load of the chip in flight at once is what reaches ~5.5 TB/s.
   constexpr int R = 4;
   switch (nch) {
     case 1: hipLaunchKernelGGL((decoder_kernel<1, R>), grid, block, lds, st, p); break;
