@@ -1,12 +1,45 @@
 #!/usr/bin/env python3
 """Per-kernel summary of a rocprofv3 SQLite output (``*_results.db``, ROCm 7 default format):
-calls, total/avg/min/max duration, sorted by total. ``python scripts/rocpd_stats.py x.db [N]``"""
+calls, total/avg/min/max duration, sorted by total. ``python scripts/rocpd_stats.py x.db [N]``
+
+``--timeline FIRST LAST``: instead, the dispatch timeline of one request -- on the stream with
+the most dispatches, the last complete run from a kernel whose name contains FIRST through the
+next one containing LAST (start offset, duration, grid, workgroup, VGPRs, name)."""
 import sqlite3
 import sys
 
 
+def timeline(c, name, first, last):
+    rows = c.execute(f"select stream_id, start, end, grid_x, workgroup_x, vgpr_count, {name} from kernels "
+                     "order by start").fetchall()
+    counts = {}
+    for r in rows:
+        counts[r[0]] = counts.get(r[0], 0) + 1
+    sid = max(counts, key=counts.get)
+    rs = [r for r in rows if r[0] == sid]
+    ends = [i for i, r in enumerate(rs) if last in r[6]]
+    for e in reversed(ends):
+        starts = [i for i in range(e, -1, -1) if first in rs[i][6]]
+        if starts:
+            seg = rs[starts[0]:e + 1]
+            t0 = seg[0][1]
+            print("# one request: start_us dur_us grid wg vgpr kernel")
+            for _, st, en, gx, wx, vg, n in seg:
+                print(f"{(st - t0) / 1e3:8.1f} {(en - st) / 1e3:7.1f} grid={gx:7d} wg={wx:5d} vgpr={vg:4d} {n[:100]}")
+            busy = sum(en - st for _, st, en, *_ in seg)
+            print(f"# {len(seg)} dispatches, span {(seg[-1][2] - t0) / 1e3:.1f} us, kernel-busy {busy / 1e3:.1f} us "
+                  "(profiled; durations inflate under the profiler)")
+            return
+    print("# no complete request found")
+
+
 def main():
     db = sys.argv[1]
+    if len(sys.argv) > 4 and sys.argv[2] == "--timeline":
+        c = sqlite3.connect(db)
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+        timeline(c, "kernel_name" if "kernel_name" in cols else "name", sys.argv[3], sys.argv[4])
+        return
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     c = sqlite3.connect(db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]

@@ -172,3 +172,20 @@ def test_checkpoint_packed_fast_path(model_sd, tmp_path):
     assert "load_packed_ms" in fast.timings and "pack_ms" not in fast.timings
     x = torch.randn(1, 3, 224, 224)
     assert torch.equal(first.infer(x), fast.infer(x))
+
+
+def test_shared_context_streams_bitwise(monkeypatch):
+    """HIPZAP_CTX_STREAMS=2: 6 request contexts share 2 streams (captured on a private stream,
+    replayed on the shared one) and return the same logits as one stream per context."""
+    from hipzap.models.resnet import randomize_bn
+    torch.manual_seed(0)
+    sd = randomize_bn(registry.get("resnet18").make_model()).eval().state_dict()
+    x = torch.randn(1, 3, 224, 224)
+    monkeypatch.setenv("HIPZAP_CTX_STREAMS", "0")
+    ref = Engine.from_state_dict("resnet18", sd, "cuda:0", batch=1, num_contexts=2).infer(x)
+    monkeypatch.setenv("HIPZAP_CTX_STREAMS", "2")
+    eng = Engine.from_state_dict("resnet18", sd, "cuda:0", batch=1, num_contexts=6)
+    eng.ensure_contexts()
+    assert len({s.cuda_stream for s in eng.streams}) == 2
+    outs = [eng.infer(x) for _ in range(12)]
+    assert all(torch.equal(o, ref) for o in outs)

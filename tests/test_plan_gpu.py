@@ -140,3 +140,29 @@ def test_engine_executor_concurrent_requests(r50):
         assert torch.equal(g, r)
     wall, lat = eng.serve_bench(5)
     assert wall > 0 and len(lat) == 4 * 5 and min(lat) > 0
+
+
+def test_plan_shared_context_streams(r50, monkeypatch):
+    """HIPZAP_CTX_STREAMS=2 in the native loader: contexts 3.. borrow the first two streams (and
+    are captured on the plan's private capture stream); concurrent requests still return the
+    single-context logits."""
+    _, _, path, _ = r50
+    ref_pe = PlanEngine(path, device=0, contexts=1)
+    xs = [os.urandom(224 * 224 * 3) for _ in range(8)]
+    ref = [ref_pe.infer_raw(x) for x in xs]
+    ref_pe.close()
+    monkeypatch.setenv("HIPZAP_CTX_STREAMS", "2")
+    pe = PlanEngine(path, device=0, contexts=5, eager_contexts=2)
+    assert pe.ensure_contexts() > 0 and pe.contexts == 5
+    got = [None] * len(xs)
+
+    def work(i):
+        got[i] = pe.infer_raw(xs[i])
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(xs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == ref
+    pe.close()
