@@ -101,6 +101,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Grouped tile raster: consecutive logical tiles (= one XCD's share after xcd_remap) walk
+// group_m tile rows before the next column tile, so the XCD's L2 holds a group_m-row block of the
+// row operand and a few column tiles of the other instead of whole row panels x ALL columns.
+// group_m = 1 is the plain row-major raster.
+__device__ __forceinline__ void grouped_tile(int lid, int tiles_m, int tiles_n, int group_m, int& tile_m, int& tile_n) {
+  const int per_group = group_m * tiles_n, gid = lid / per_group, first_m = gid * group_m;
+  const int gsz = min(tiles_m - first_m, group_m);
+  tile_m = first_m + (lid - gid * per_group) % gsz;
+  tile_n = (lid - gid * per_group) / gsz;
+}
+
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }

@@ -9,6 +9,8 @@
 //     what fp8 buys. Weights: per-output-channel scales s_n, packed [N/16][K/32][64][8] bytes.
 // gfx950 converts with v_cvt_pk_fp8_f32, which on CDNA4 is the OCP e4m3fn encoding (NOT the
 // MI300 FNUZ variant) — checked against torch.float8_e4m3fn in tests/test_fp8_gpu.py.
+#include <cstdlib>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -245,7 +247,7 @@ __device__ __forceinline__ void wait_vm8() {
 // l>>4 (the hardware K order above: block b lives in the register halves of lane groups
 // 2(b&1)..2(b&1)+1, not in lane group b).
 template <int BM, int BN, int NS, bool XS>
-__global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
+__global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, int group_m) {
   constexpr int FCW = BN / 32, FPW = BM / 32;
   constexpr int NWG = BN / 16;                // weight fragments (2 KiB) per stage
   constexpr int XBYTES = BM * 128;
@@ -257,9 +259,10 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave & 1, wm = wave >> 1;
-  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile_n = lid % tiles_n, tile_m = lid / tiles_n;
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
   const int n0 = tile_n * BN, m0 = tile_m * BM;
   const int kb = p.K >> 7;  // 128-deep k-steps = stages
 
@@ -435,8 +438,10 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p) {
 template <int BM, int BN, int NS>
 int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  if (p.xs) hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  if (p.xs) hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p, group_m);
+  else hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p, group_m);
   return (int)hipGetLastError();
 }
 

@@ -96,14 +96,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   const int wn = wave % WN, wm = wave / WN;
   const int tiles_n = (p.Cout + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  // grouped raster: consecutive logical tiles (= one XCD's share after xcd_remap) walk group_m
-  // tile rows before the next feature tile, so an XCD's L2 holds a group_m x (share / group_m)
-  // block of X rows and W columns instead of two X row-panels x ALL of W (5.1 MB > 4 MB L2 at
-  // BERT FFN1); group_m = 1 is the plain row-major raster
-  const int per_group = group_m * tiles_n, gid = lid / per_group, first_m = gid * group_m;
-  const int gsz = min(tiles_m - first_m, group_m);
-  const int tile_m = first_m + (lid - gid * per_group) % gsz;
-  const int tile_n = (lid - gid * per_group) / gsz;
+  // grouped raster (common.h): an XCD's L2 holds a group_m-row block of X and a few W column
+  // tiles instead of two X row-panels x ALL of W (5.1 MB > 4 MB L2 at BERT FFN1)
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
   const int n0 = tile_n * BN, m0 = tile_m * BM;
   const int nst = p.ksteps >> 1;
 
