@@ -8,6 +8,8 @@
 //                  16-lane shuffles, P written once to LDS as bf16 and re-read as the A
 //                  operand of P.V. L <= 256, head dim 64 (BERT L=128, ViT L=197).
 //   * patch_tokens — ViT: CLS token + position embedding add around the patch-embed GEMM.
+#include <cstdlib>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -406,7 +408,8 @@ extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) 
   const int Lp = (p.L + 31) & ~31;
   const size_t lds = (size_t)Lp * (ATT_KST + ATT_VST) * sizeof(bf16_t) + (size_t)Lp * sizeof(float);
   // 8 waves (128 queries) per workgroup for long sequences: K/V staged half as often
-  if (p.L > HZ_ATT_NW8_MINL) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
+  static const int nw8_minl = getenv("HIPZAP_ATT_NW8_MINL") ? atoi(getenv("HIPZAP_ATT_NW8_MINL")) : HZ_ATT_NW8_MINL;
+  if (p.L > nw8_minl) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
   else hipLaunchKernelGGL(attention_kernel<4>, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
   return (int)hipGetLastError();
 }

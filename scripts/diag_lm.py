@@ -39,7 +39,8 @@ def main():
     eng.run_tokens([1, 2], 4, 0)
     lib = N.lib()
     ops = eng._ops  # (kind, params) in step order; the sampler is fused into layer 0
-    res_final = timed(lambda p: N.check(lib.hz_prog_add_sampler(p, C.byref(eng._final), 0), "final"))
+    res_final = None if eng._final is None else \
+        timed(lambda p: N.check(lib.hz_prog_add_sampler(p, C.byref(eng._final), 0), "final"))
     res = {"V": V, "standalone_argmax_sampler_us": res_final}
     for k, (kind, prm) in enumerate(ops):
         add = {"lstm": lib.hz_prog_add_lstm, "decoder": lib.hz_prog_add_decoder,
