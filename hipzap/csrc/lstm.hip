@@ -568,7 +568,9 @@ extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   if (p.ldk % 64 || p.ldk < p.In + p.H || p.In <= 0 || p.H <= 0) return -1;
   if (p.bacc_val && (!p.emb || !p.n_forced || !p.bacc_idx || !p.bmax_val || !p.bmax_idx || p.nblk < 1 || p.nblk > 2048 || p.V < 1))
     return -1;
-  constexpr int KW = 2;  // waves per unit (K split)
+  // waves per unit (K split): 2 (per-layer us at the reference dims, KW = 1 / 2 / 4: layer 0
+  // 7.73 / 7.71 / 8.30, layer 1 5.64 / 5.48 / 5.58; profiles/r2_awd_lstm/v2/lstm_kw_ab)
+  constexpr int KW = 2;
   const int nch = (p.ldk + 511) / 512;
   const dim3 grid((p.H + 4 / KW - 1) / (4 / KW)), block(256);
   const size_t lds = (size_t)nch * 512 * sizeof(float);
