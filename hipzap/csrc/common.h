@@ -101,6 +101,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// a / b for 0 <= a < 2^24, 1 <= b < 2^24 with a / b < 2^20 (index math: tiles, pixels, K
+// positions): a float-reciprocal estimate (within 1 of the quotient there) fixed up exactly --
+// about 8 VALU instead of the ~20-instruction integer division sequence, which dominated the
+// prologue of the bs=1 conv kernels (scripts/native/conv_stamps.hip). HZ_INT_DIV: plain division.
+__device__ __forceinline__ int fdiv(int a, int b) {
+#ifdef HZ_INT_DIV
+  return a / b;
+#else
+  int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+  const int r = a - q * b;
+  q -= r < 0;
+  q += r >= b;
+  return q;
+#endif
+}
+
 // Grouped tile raster: consecutive logical tiles (= one XCD's share after xcd_remap) walk
 // group_m tile rows before the next column tile, so the XCD's L2 holds a group_m-row block of the
 // row operand and a few column tiles of the other instead of whole row panels x ALL columns.

@@ -27,6 +27,14 @@
 
 HZ_DEBUG_UNIT(conv)
 
+// phase timestamps for scripts/native/conv_stamps.hip (which defines them before including this
+// file); empty in the library
+#ifndef HZ_STAMP
+#define HZ_STAMP_DECL
+#define HZ_STAMP(i)
+#define HZ_STAMP_FLUSH
+#endif
+
 namespace {
 
 #ifndef HZ_RING_SHRINK
@@ -46,14 +54,16 @@ template <int FC, int FP, bool FAST, bool IS1X1, bool XROW>
 __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) {
   constexpr int DEPTH = Depth<FC, FP>::value;
   constexpr int NF = FC * FP;
+  HZ_STAMP_DECL
+  HZ_STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int KW = blockDim.x >> 6;
   const int lrow = lane & 15, lk = (lane >> 4) * 8;
 
-  const int tile_n = lid % p.tiles_n;
-  const int tile_m = lid / p.tiles_n;
+  const int tile_m = fdiv(lid, p.tiles_n);
+  const int tile_n = lid - tile_m * p.tiles_n;
   const int n0 = tile_n * FC * 16;
   const int m0 = tile_m * FP * 16;
 
@@ -65,7 +75,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   const int wgroups = ((p.Cout + 63) >> 6) << 2;
   const long olim = p.out_rowmajor ? (long)(p.M - 1) * p.ldo + p.Cout : (long)p.N * p.Cout * p.P * p.Q;
   if (!HZ_DCHECK(XROW || p.M == p.N * p.P * p.Q)) return;
-  const int spw = (steps + KW - 1) / KW;
+  const int spw = (steps + KW - 1) >> (31 - __builtin_clz(KW));  // KW is a power of two
   const int s_begin = wave * spw;
   const int nsteps = max(0, min(steps, s_begin + spw) - s_begin);
 
@@ -78,14 +88,14 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     const int m = m0 + f * 16 + lrow;
     pval[f] = m < p.M;
     const int mm = pval[f] ? m : 0;
-    const int ni = mm / PQ;
+    const int ni = fdiv(mm, PQ);
     const int hw = mm - ni * PQ;
     const int nbase = FAST ? ni * (C >> 5) * HW : ni * HW;
     if constexpr (IS1X1) {
       pb[f] = nbase + hw;
       pih[f] = piw[f] = 0;
     } else {
-      const int oh = hw / p.Q;
+      const int oh = fdiv(hw, p.Q);
       const int ow = hw - oh * p.Q;
       pih[f] = oh * p.stride - p.pad;
       piw[f] = ow * p.stride - p.pad;
@@ -112,9 +122,9 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   int cur_cb = 0, cur_r = 0, cur_s = 0;
   if constexpr (FAST && !XROW) {
     const int k0 = s_begin * 32;
-    const int rs0 = k0 / C;
+    const int rs0 = fdiv(k0, C);
     cur_cb = (k0 - rs0 * C) >> 5;
-    cur_r = rs0 / p.S;
+    cur_r = fdiv(rs0, p.S);
     cur_s = rs0 - cur_r * p.S;
   }
   // Per-lane validity is a branch around each activation load. Address-select variants that
@@ -166,9 +176,9 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     } else {  // plain NHWC input with C in {8, 16}: per-lane (r, s, c) decomposition
       const int kk = k + lk;
       const bool kval = kk < p.K;
-      const int rs = kk / C;
+      const int rs = fdiv(kk, C);
       const int c = kk - rs * C;
-      const int r = rs / p.S;
+      const int r = fdiv(rs, p.S);
       const int s = rs - r * p.S;
 #pragma unroll
       for (int j = 0; j < FP; ++j) {
@@ -184,6 +194,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
   for (int u = 0; u < DEPTH; ++u)
     if (u < nsteps) load_step(u, fa[u], fb[u]);
+  HZ_STAMP(1);
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
@@ -213,7 +224,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     if (p.out_rowmajor) {
       o = (long)m * p.ldo + n;
     } else {  // channel-blocked [N][Cout/32][P*Q][32]
-      const int ni = m / PQ;
+      const int ni = fdiv(m, PQ);
       const int hw = m - ni * PQ;
       o = (((long)ni * (p.Cout >> 5) + (n >> 5)) * PQ + hw) * 32 + (n & 31);
     }
@@ -239,11 +250,15 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
   };
 
+  HZ_STAMP(2);
   if (KW == 1) {
+    HZ_STAMP(3);
 #pragma unroll
     for (int i = 0; i < FC; ++i)
 #pragma unroll
       for (int j = 0; j < FP; ++j) epilogue(i, j, acc[i][j]);
+    HZ_STAMP(4);
+    HZ_STAMP_FLUSH;
     return;
   }
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -253,16 +268,19 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
     for (int j = 0; j < FP; ++j) red[(wave * NF + i * FP + j) * 64 + lane] = acc[i][j];
   __syncthreads();
+  HZ_STAMP(3);
 #pragma unroll
   for (int i = 0; i < FC; ++i)
 #pragma unroll
     for (int j = 0; j < FP; ++j) {
       const int ij = i * FP + j;
-      if ((ij % KW) != wave) continue;
+      if ((ij & (KW - 1)) != wave) continue;  // KW is a power of two
       f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int w = 0; w < KW; ++w) s += red[(w * NF + ij) * 64 + lane];
       epilogue(i, j, s);
     }
+  HZ_STAMP(4);
+  HZ_STAMP_FLUSH;
 }
 
 template <int FC, int FP, bool FAST, bool IS1X1, bool XROW>
@@ -294,7 +312,8 @@ template <int FC, int FP>
 int launch2(const HzConvParams& a, const HzConvParams& b, hipStream_t st) {
   HzConvParams q0 = a, q1 = b;
   const int kw = a.kw < 1 ? 1 : a.kw;
-  if (b.kw != a.kw || kw > 16 || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP)) return -5;
+  if (b.kw != a.kw || kw > 16 || (kw & (kw - 1)) || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP))
+    return -5;
   if (a.x_rowmajor || b.x_rowmajor) return -1;
   q0.tiles_n = (a.Cout + FC * 16 - 1) / (FC * 16);
   q1.tiles_n = (b.Cout + FC * 16 - 1) / (FC * 16);
@@ -314,7 +333,7 @@ template <int FC, int FP>
 int launch(const HzConvParams& p, hipStream_t st) {
   HzConvParams q = p;
   const int kw = p.kw < 1 ? 1 : p.kw;
-  if (kw > 16 || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP)) return -5;
+  if (kw > 16 || (kw & (kw - 1)) || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP)) return -5;
   q.tiles_n = (p.Cout + FC * 16 - 1) / (FC * 16);
   const int tiles_m = (p.M + FP * 16 - 1) / (FP * 16);
   const bool is1x1 = p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0;

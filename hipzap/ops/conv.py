@@ -164,7 +164,7 @@ def legal(cfg: int, kw: int) -> bool:
     if cfg in LDS_TILES:
         return kw == 1
     fc, fp = TILES[cfg]
-    return 1 <= kw <= 16 and kw * fc * fp <= 64 and 64 * kw <= max_threads(fc * fp)
+    return 1 <= kw <= 16 and kw & (kw - 1) == 0 and kw * fc * fp <= 64 and 64 * kw <= max_threads(fc * fp)
 
 
 def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv | None = None) -> list[tuple[int, int]]:
