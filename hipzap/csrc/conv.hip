@@ -59,7 +59,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int KW = blockDim.x >> 6;
+  const int KW = p.kw;  // = blockDim.x / 64 (set by the launcher; a kernarg, unlike blockDim, which
+                       // costs a dispatch-packet load on the prologue's critical path)
   const int lrow = lane & 15, lk = (lane >> 4) * 8;
 
   const int tile_m = fdiv(lid, p.tiles_n);
@@ -312,6 +313,7 @@ template <int FC, int FP>
 int launch2(const HzConvParams& a, const HzConvParams& b, hipStream_t st) {
   HzConvParams q0 = a, q1 = b;
   const int kw = a.kw < 1 ? 1 : a.kw;
+  q0.kw = q1.kw = kw;
   if (b.kw != a.kw || kw > 16 || (kw & (kw - 1)) || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP))
     return -5;
   if (a.x_rowmajor || b.x_rowmajor) return -1;
@@ -333,6 +335,7 @@ template <int FC, int FP>
 int launch(const HzConvParams& p, hipStream_t st) {
   HzConvParams q = p;
   const int kw = p.kw < 1 ? 1 : p.kw;
+  q.kw = kw;
   if (kw > 16 || (kw & (kw - 1)) || kw * FC * FP > 64 || 64 * kw > conv_max_threads(FC * FP)) return -5;
   q.tiles_n = (p.Cout + FC * 16 - 1) / (FC * 16);
   const int tiles_m = (p.M + FP * 16 - 1) / (FP * 16);

@@ -9,7 +9,6 @@
 #include <vector>
 
 __device__ unsigned long long* g_stamps;
-#define HZ_STAMP 1
 #define HZ_STAMP_DECL unsigned long long hz_st[5] = {0, 0, 0, 0, 0};
 #define HZ_STAMP(i) hz_st[i] = __builtin_amdgcn_s_memtime()
 #define HZ_STAMP_FLUSH                                                                          \
