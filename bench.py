@@ -157,8 +157,13 @@ def fresh_cold_start(args, device_index: int) -> dict:
     """Cold start over fresh processes (hipzap/coldstart.py), before this process uses a GPU."""
     from hipzap.coldstart import measure_fresh
     ckpt, plan = prepare_artifacts(args.model, args.ckpt_dir)
-    return {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index),
-            "pth": measure_fresh("pth", ckpt, args.model, args.cold_trials, device=device_index)}
+    res = {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index),
+           "pth": measure_fresh("pth", ckpt, args.model, args.cold_trials, device=device_index)}
+    try:  # the Python-free server binary (csrc/tools/serve_plan.cpp) on the same plan image
+        res["native"] = measure_fresh("native", plan, args.model, args.cold_trials, device=device_index)
+    except Exception as e:  # noqa: BLE001 - not built: the Python plan path stays the headline
+        print(f"native cold start skipped: {e}", file=sys.stderr)
+    return res
 
 
 def torch_reference_throughput(model, device, iters=200):
@@ -385,6 +390,8 @@ def main():
             "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
                                "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict",
             "cold_start_pth_ms_p50": fresh["pth"]["p50_ms"] if fresh else None,
+            # the Python-free server binary (hipzap-serve-plan --once) on the same plan image
+            "cold_start_native_ms_p50": (fresh.get("native") or {}).get("p50_ms") if fresh else None,
             "cold_start_fresh_process": fresh,
             "cold_start_inprocess_ms_first": round(cold_first, 2),
             "cold_start_inprocess_ms_p50": round(statistics.median(colds), 2),

@@ -123,8 +123,41 @@ def build_comm(verbose: bool = True) -> Path:
     return LIB_COMM
 
 
+TOOLS_SRC = CSRC / "tools"
+SERVE_PLAN = LIBDIR / "hipzap-serve-plan"
+
+
+def build_tools(verbose: bool = True) -> list[Path]:
+    """Native executables (csrc/tools/*.cpp) linked against libhipzap.so (rpath $ORIGIN):
+    ``hipzap-serve-plan``, the Python-free plan server / cold-start probe."""
+    build(verbose=False)
+    out = []
+    for src in sorted(TOOLS_SRC.glob("*.cpp")):
+        exe = LIBDIR / ("hipzap-" + src.stem.replace("_", "-"))
+        h = hashlib.sha1(src.read_bytes() + (CSRC / "hipzap.h").read_bytes() + " ".join(COMMON).encode())
+        key = h.hexdigest()[:16]
+        stamp = LIBDIR / f".buildkey_tool_{src.stem}"
+        if exe.exists() and stamp.exists() and stamp.read_text() == key:
+            if verbose:
+                print(f"hipzap: {exe} up to date")
+            out.append(exe)
+            continue
+        tmp = exe.with_suffix(".tmp")
+        cmd = [HIPCC, *COMMON, str(src), "-L", str(LIBDIR), "-lhipzap", "-Wl,-rpath,$ORIGIN", "-o", str(tmp)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"tool build failed for {src.name}:\n{r.stderr[-6000:]}")
+        os.replace(tmp, exe)
+        stamp.write_text(key)
+        if verbose:
+            print(f"hipzap: built {exe}")
+        out.append(exe)
+    return out
+
+
 if __name__ == "__main__":
     build(verbose=True, debug="--debug" in sys.argv[1:])
     if "--debug" not in sys.argv[1:]:
         build_comm(verbose=True)
+        build_tools(verbose=True)
     sys.exit(0)

@@ -4,6 +4,9 @@
     python -m hipzap.coldstart pth <ckpt.pth> --model resnet50           torch.load + pack path
     python -m hipzap.coldstart hzpack <ckpt.pth> --model resnet50        packed safetensors path
 
+``measure_fresh("native", plan)`` spawns the Python-free ``hipzap-serve-plan PLAN --once IMAGE``
+(csrc/tools/serve_plan.cpp) instead: exec -> HIP init -> plan upload -> one eager request.
+
 The parent (``bench.py``, ``scripts/cold_start.py``) records ``time.time()`` just before it
 spawns this process; ``t_first`` below is on the same clock, so ``t_first - t_spawn`` is the
 whole serverless cold start: interpreter start, imports, HIP init, weights to the GPU, graph
@@ -69,11 +72,22 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     walls, res = [], []
+    if mode == "native":
+        import tempfile
+        from hipzap.lite import read_meta
+        exe = os.path.join(root, "hipzap", "_lib", "hipzap-serve-plan")
+        if not os.path.exists(exe):
+            raise RuntimeError(f"{exe} not built (python -m hipzap.build)")
+        nbytes = read_meta(path)["inputs"][0]["bytes"]
+        img = os.path.join(tempfile.mkdtemp(prefix="hzcold"), "image.raw")
+        with open(img, "wb") as f:
+            f.write(os.urandom(nbytes))
+        cmd = [exe, path, "--once", img, "--device", str(device)]
+    else:
+        cmd = [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device)]
     for _ in range(trials):
         t = time.time()
-        r = subprocess.run([sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device",
-                            str(device)], cwd=root, capture_output=True, text=True, timeout=timeout,
-                           env=env)
+        r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout, env=env)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         if r.returncode != 0 or not lines:
             raise RuntimeError(f"cold-start child ({mode}) failed rc={r.returncode}: {r.stderr[-3000:]}")
@@ -86,7 +100,7 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
             "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2),
             "all_ms": [round(w, 1) for w in walls],
             "median_trial_phases_ms": {k: round(v, 2) for k, v in med["phases_ms"].items()},
-            "torch_imported": med.get("torch_imported", True)}
+            "torch_imported": med.get("torch_imported", mode not in ("plan", "native"))}
 
 
 def main(argv=None) -> int:

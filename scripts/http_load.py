@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--format", choices=["json", "npy"], default="json")
     ap.add_argument("--port", type=int, default=18082)
     ap.add_argument("--server-log", default=None, help="copy the server log here")
+    ap.add_argument("--native", action="store_true",
+                    help="serve with the Python-free hipzap-serve-plan binary instead of python -m hipzap serve")
     a = ap.parse_args()
     from bench import prepare_artifacts
     ckpt, plan = prepare_artifacts("resnet50", "/tmp/hipzap_bench")
@@ -115,6 +117,9 @@ def main():
     cmd = [sys.executable, "-m", "hipzap", "serve", "--settings", settings, "--port", str(a.port)]
     if a.gpus > 1:
         cmd += ["--gpus", str(a.gpus)]
+    if a.native:
+        cmd = [os.path.join(ROOT, "hipzap", "_lib", "hipzap-serve-plan"), plan, "--port", str(a.port),
+               "--contexts", str(a.contexts)]
     env = dict(os.environ, HIPZAP_WATCHDOG="0")
     log_path = os.path.join(d, "server.log")
     log_f = open(log_path, "w")  # never a pipe: the access log would fill it and block the server
@@ -159,6 +164,7 @@ def main():
     lat = sorted(x for r in res for x in r[0])
     errors = sum(r[1] for r in res)
     print(json.dumps({
+        "server": "hipzap-serve-plan" if a.native else "python -m hipzap serve",
         "gpus": a.gpus, "clients": a.clients, "requests": len(lat), "format": a.format, "errors": errors,
         "req_per_s": round(len(lat) / wall, 1), "p50_ms": round(statistics.median(lat), 3),
         "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3), "max_ms": round(lat[-1], 3),
