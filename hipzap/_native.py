@@ -56,7 +56,8 @@ class LstmParams(C.Structure):
                 ("x_state", c_void_p), ("h_state", c_void_p), ("c_state", c_void_p), ("step", c_void_p),
                 ("In", c_int), ("H", c_int), ("ldk", c_int), ("step_off", c_int), ("n_forced", c_void_p),
                 ("bacc_val", c_void_p), ("bacc_idx", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p),
-                ("nblk", c_int), ("V", c_int)]
+                ("nblk", c_int), ("V", c_int), ("pre", c_void_p), ("xtab", c_void_p), ("pre0", c_void_p),
+                ("h0_state", c_void_p), ("c0_state", c_void_p), ("H0", c_int), ("pad0", c_int)]
 
 
 class SamplerParams(C.Structure):
@@ -71,7 +72,11 @@ class DecoderParams(C.Structure):
                 ("step_off", c_int), ("logits", c_void_p), ("V", c_int), ("H", c_int), ("ldk", c_int), ("keys", c_void_p),
                 ("seed", c_void_p), ("bmax_val", c_void_p), ("bmax_idx", c_void_p), ("nblk", c_int),
                 ("rpb", c_int), ("bacc_val", c_void_p), ("bacc_idx", c_void_p), ("n_exclude", c_int),
-                ("exclude", c_int * 8)]
+                ("exclude", c_int * 8), ("n_hh", c_int), ("hh_blocks", c_int), ("hh_w", c_void_p * 4),
+                ("hh_b", c_void_p * 4), ("hh_h", c_void_p * 4), ("hh_out", c_void_p * 4), ("hh_H", c_int * 4),
+                ("hh_ld", c_int * 4), ("hh_blk", c_int * 5)]
+
+HH_ROWS = 16  # HZ_HH_ROWS (hipzap.h): rows per recurrent-partial workgroup of the decoder kernel
 
 
 def _sig(lib, name, res, *args):

@@ -104,6 +104,18 @@ typedef struct HzLstmParams {
   const float* bmax_val;      // [nblk] overall maxima (fallback when no row is acceptable)
   const int* bmax_idx;
   int nblk, V;
+  // split mode (pre != NULL; csrc/lstm.hip lstm_x_kernel): w holds W_ih only ([4H][ldk], ldk =
+  // In padded to 64) and the recurrent half arrives precomputed by the previous step's decoder
+  // kernel: pre[4H] = W_hh . h_{t-1} + b (bias is then unused)
+  const float* pre;
+  // split mode, layer 0 folded into the layer-1 kernel (xtab != NULL; In = H0): h0_t is rebuilt
+  // in every workgroup from xtab[tok] (= W_ih^0 . emb[tok], fp32 [V][4*H0]), pre0 and c0_{t-1};
+  // token selection as above (emb unused); workgroup 0 publishes h0_t / c0_t
+  const float* xtab;
+  const float* pre0;          // [4*H0]
+  float* h0_state;            // [2][H0]
+  float* c0_state;            // [2][H0]
+  int H0, pad0;
 } HzLstmParams;
 typedef struct HzSamplerParams {
   const float* keys;          // [V] Gumbel-perturbed logits (decoder epilogue)
@@ -139,7 +151,18 @@ typedef struct HzDecoderParams {
   int* bacc_idx;              //   (row != 0 and not in exclude[]), -inf/INT_MAX if none
   int n_exclude;
   int exclude[8];
+  // split LSTM mode: hh_blocks extra workgroups (blockIdx < hh_blocks, before the decoder's)
+  // compute the NEXT step's recurrent gate partials hh_out[l] = W_hh^l . h^l_t + b^l, layer l
+  // owning workgroups [hh_blk[l], hh_blk[l+1]) of HZ_HH_ROWS rows each
+  int n_hh, hh_blocks;
+  const unsigned short* hh_w[4];  // [4H][ld] bf16, gate-interleaved like HzLstmParams.w
+  const float* hh_b[4];           // [4H]
+  const float* hh_h[4];           // the layer's h_state [2][H]
+  float* hh_out[4];               // [4H] -> HzLstmParams.pre / pre0
+  int hh_H[4], hh_ld[4];
+  int hh_blk[5];
 } HzDecoderParams;
+#define HZ_HH_ROWS 16
 // decoder launch geometry for vocabulary V: workgroups and rows per workgroup (contiguous)
 void hz_decoder_geometry(int V, int* nblk, int* rpb);
 int hz_lstm_cell_launch(const HzLstmParams* p, hipStream_t st);

@@ -233,6 +233,155 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
   }
 }
 
+// --------------------------------------------------------------------------- split-mode LSTM
+// W_ih . x only: the recurrent half W_hh . h_{t-1} + b was computed by the previous step's
+// decoder kernel (hh_rows below), where it streams at the decoder's full HBM rate instead of
+// inside these short latency-bound kernels -> each layer kernel streams half the bytes.
+// FUSE0: this is the layer-1 kernel and layer 0 is folded into it. Layer 0's input projection is
+// a table lookup, xtab[tok] = W_ih^0 . emb[tok] (fp32 [V][4 H0], built once at pack time from the
+// fp32 weights: 1.1 GB at the reference dims, cheap in 288 GB), so h0_t needs no GEMV at all:
+// every workgroup rebuilds all H0 units from xtab[tok] + pre0 and c0_{t-1} straight into LDS
+// (workgroup 0 publishes h0_t / c0_t), and the token selection of the fused sampler runs first.
+// 8 waves: 4 units x 2 K-halves per workgroup.
+template <int NCH, bool FUSE0>
+__global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
+  extern __shared__ __attribute__((aligned(16))) float vin[];  // [NCH*512] input vector, fp32
+  __shared__ float part[8][4];
+  constexpr int WAVES = 8, KW = 2, UPW = WAVES / KW;
+  constexpr int NC = (NCH + KW - 1) / KW;  // 512-chunks per wave
+  constexpr int TPT = 4;                    // decoder maxima per thread (nblk <= 2048)
+  constexpr int U0 = 3;                     // layer-0 units per thread (H0 <= 1536)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slot = wave / KW, kw = wave - slot * KW;
+  const int t = *p.step + p.step_off;
+  const int par = t & 1;
+  if (!HZ_DCHECK(p.In <= p.ldk && p.ldk <= NCH * 512 && (!FUSE0 || (p.H0 == p.In && p.H0 <= U0 * 512)))) return;
+  // ---- token-independent loads, issued in the order their values are needed (vmcnt retires in
+  // issue order): decoder maxima, layer-0 recurrent partials and cell state, this unit's W_ih rows
+  const bool fused = FUSE0 && p.bacc_val && t >= *p.n_forced;
+  float tv[TPT];
+  int ti[TPT];
+  if (fused) {
+#pragma unroll
+    for (int r = 0; r < TPT; ++r) {
+      const int e = tid + r * 512;
+      tv[r] = e < p.nblk ? p.bacc_val[e] : -INFINITY;
+      ti[r] = e < p.nblk ? p.bacc_idx[e] : 0x7fffffff;
+    }
+  }
+  f32x4 g0[U0];
+  float c0[U0];
+  if (FUSE0) {
+#pragma unroll
+    for (int r = 0; r < U0; ++r) {
+      const int u = min(tid + r * 512, p.H0 - 1);
+      g0[r] = *reinterpret_cast<const f32x4*>(p.pre0 + 4 * u);
+      c0[r] = p.c0_state[par * p.H0 + u];
+    }
+  }
+  const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
+  const int jc = min(j, p.H - 1);
+  const bf16_t* w = p.w + (long)(4 * jc) * p.ldk + lane * 8;
+  u32x4 wv[4][NC];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int k = (kw * NC + c) * 512 + lane * 8;
+      const u32x4* src = reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8));
+      wv[q][c] = k < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
+    }
+  const f32x4 pj = *reinterpret_cast<const f32x4*>(p.pre + 4 * jc);
+  const float cj = p.c_state[par * p.H + jc];
+  // ---- the input vector in LDS ----
+  if (FUSE0) {
+    int tok;
+    if (fused) {
+      __shared__ float sv[WAVES];
+      __shared__ int si[WAVES];
+      float v = tv[0];
+      int i = ti[0];
+#pragma unroll
+      for (int r = 1; r < TPT; ++r)
+        if (better(tv[r], ti[r], v, i)) {
+          v = tv[r];
+          i = ti[r];
+        }
+      block_reduce_best<WAVES>(sv, si, v, i);
+      if (i == 0x7fffffff) {  // no acceptable row anywhere (V <= 9): the best key overall
+        __shared__ float sv2[WAVES];
+        __shared__ int si2[WAVES];
+        block_best<WAVES>(p.bmax_val, p.bmax_idx, p.nblk, sv2, si2, v, i);
+      }
+      tok = min(max(i, 0), p.V - 1);
+      if (blockIdx.x == 0 && tid == 0) p.tok_seq[t] = tok;
+    } else {
+      tok = p.tok_seq[t];
+    }
+    const float* xr = p.xtab + (long)tok * 4 * p.H0;
+    f32x4 xg[U0];
+#pragma unroll
+    for (int r = 0; r < U0; ++r) xg[r] = *reinterpret_cast<const f32x4*>(xr + 4 * min(tid + r * 512, p.H0 - 1));
+#pragma unroll
+    for (int r = 0; r < U0; ++r) {
+      const int u = tid + r * 512;
+      if (u < p.H0) {
+        const f32x4 g = xg[r] + g0[r];
+        const float si = 1.f / (1.f + __expf(-g[0]));
+        const float sf = 1.f / (1.f + __expf(-g[1]));
+        const float so = 1.f / (1.f + __expf(-g[3]));
+        const float c_new = sf * c0[r] + si * tanhf(g[2]);
+        const float h_new = so * tanhf(c_new);
+        vin[u] = h_new;
+        if (blockIdx.x == 0) {
+          p.c0_state[(par ^ 1) * p.H0 + u] = c_new;
+          p.h0_state[(par ^ 1) * p.H0 + u] = h_new;
+        }
+      } else if (u < NCH * 512) {
+        vin[u] = 0.f;
+      }
+    }
+  } else {
+    const float* x = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
+    for (int i = tid; i < NCH * 512; i += 512) vin[i] = i < p.In ? x[i] : 0.f;
+  }
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = (kw * NC + c) * 512 + lane * 8;
+    if ((kw * NC + c) >= NCH) break;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(vin + k);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(vin + k + 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float f[8];
+      unpack8(wv[q][c], f);
+      acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
+                f[6] * v1[2] + f[7] * v1[3];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = warp_sum(acc[q]);
+  if (lane == 0 && kw > 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[wave][q] = acc[q];
+  __syncthreads();
+  if (lane == 0 && kw == 0 && j < p.H) {
+#pragma unroll
+    for (int o = 1; o < KW; ++o)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += part[wave + o][q];
+    const float si = 1.f / (1.f + __expf(-(acc[0] + pj[0])));
+    const float sf = 1.f / (1.f + __expf(-(acc[1] + pj[1])));
+    const float so = 1.f / (1.f + __expf(-(acc[3] + pj[3])));
+    const float c_new = sf * cj + si * tanhf(acc[2] + pj[2]);
+    const float h_new = so * tanhf(c_new);
+    p.c_state[(par ^ 1) * p.H + j] = c_new;
+    p.h_state[(par ^ 1) * p.H + j] = h_new;
+  }
+}
+
 // --------------------------------------------------------------------------- Philox4x32-10
 __device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0, unsigned k1,
                                        unsigned& o0) {
@@ -440,7 +589,73 @@ __global__ __launch_bounds__(1024) void argmax_sampler_kernel(const HzSamplerPar
   sample_argmax<16>(p, *p.step + p.step_off);
 }
 
-template <int NCH, int R>
+template <class T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int l) {  // uniform select, no dynamic kernarg index
+  return l == 0 ? a[0] : l == 1 ? a[1] : l == 2 ? a[2] : a[3];
+}
+
+#ifndef HZ_HH_RR
+#define HZ_HH_RR 4
+#endif
+// Split LSTM mode: rows [r0, r0 + HZ_HH_ROWS) of layer l's next-step recurrent gate partials
+// W_hh^l . h^l_t + b^l. 4 waves x RR rows per round, every 16-B load of a round in flight.
+template <int NCHH>
+__device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par, float* hv) {
+  constexpr int RR = HZ_HH_RR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int l = 0;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) l += (k < p.n_hh && b >= p.hh_blk[k]);
+  const int H = pick4(p.hh_H, l), ld = pick4(p.hh_ld, l), rows = 4 * H;
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(pick4(p.hh_w, l));
+  const float* bias = pick4(p.hh_b, l);
+  const float* h = pick4(p.hh_h, l) + (par ^ 1) * H;  // h^l of this step
+  float* out = pick4(p.hh_out, l);
+  const int r0 = (b - (l == 0 ? p.hh_blk[0] : l == 1 ? p.hh_blk[1] : l == 2 ? p.hh_blk[2] : p.hh_blk[3])) * HZ_HH_ROWS;
+  if (!HZ_DCHECK(H <= ld && ld <= NCHH * 512)) return;
+  for (int i = tid; i < NCHH * 512; i += blockDim.x) hv[i] = i < H ? h[i] : 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int rr = 0; rr < HZ_HH_ROWS; rr += 4 * RR) {
+    u32x4 wv[RR][NCHH];
+#pragma unroll
+    for (int q = 0; q < RR; ++q) {
+      const int r = min(r0 + rr + wave * RR + q, rows - 1);
+#pragma unroll
+      for (int c = 0; c < NCHH; ++c) {
+        const int k = c * 512 + lane * 8;
+        wv[q][c] = k < ld ? *reinterpret_cast<const u32x4*>(W + (long)r * ld + k) : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    float acc[RR];
+#pragma unroll
+    for (int q = 0; q < RR; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCHH; ++c) {
+      const int k = c * 512 + lane * 8;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
+#pragma unroll
+      for (int q = 0; q < RR; ++q) {
+        float f[8];
+        unpack8(wv[q][c], f);
+        acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
+                  f[6] * v1[2] + f[7] * v1[3];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RR; ++q) acc[q] = warp_sum(acc[q]);
+    if (lane < RR) {
+      const int r = r0 + rr + wave * RR + lane;
+      float a = acc[0];
+#pragma unroll
+      for (int q = 1; q < RR; ++q) a = lane == q ? acc[q] : a;
+      if (r < rows) out[r] = a + bias[r];
+    }
+  }
+}
+
+template <int NCH, int R, int NCHH>
 __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   extern __shared__ __attribute__((aligned(16))) float hv[];
   __shared__ float w_best[4];
@@ -448,12 +663,17 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = *p.step + p.step_off;
   const int par = t & 1;
+  if (NCHH > 0 && (int)blockIdx.x < p.hh_blocks) {  // split LSTM mode: next step's W_hh partials
+    hh_rows<NCHH>(p, blockIdx.x, par, hv);
+    return;
+  }
+  const int blk = blockIdx.x - (NCHH > 0 ? p.hh_blocks : 0);
   const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
   // R rows per wave round (R <= DROWS): fewer registers -> more resident waves
   if (!HZ_DCHECK(p.H <= p.ldk && p.ldk <= NCH * 512 && p.rpb % DROWS == 0)) return;
   const int ngroups = (p.V + R - 1) / R;
   const int gpb = p.rpb / R;
-  const int g_end = min(ngroups, (blockIdx.x + 1) * gpb);
+  const int g_end = min(ngroups, (blk + 1) * gpb);
   // (measured: issuing the first round of weight rows BEFORE staging h made the kernel 14 %
   // slower, 26.4 vs 23.1 us at V = 60000, so h is staged first)
   for (int i = tid; i < NCH * 512; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
@@ -461,7 +681,7 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   const unsigned long long seed = p.keys ? *p.seed : 0ull;
   float best = -INFINITY, abest = -INFINITY;
   int besti = 0x7fffffff, abesti = 0x7fffffff;
-  for (int g = blockIdx.x * gpb + wave; g < g_end; g += 4) {
+  for (int g = blk * gpb + wave; g < g_end; g += 4) {
     u32x4 wv[R][NCH];
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -551,11 +771,11 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
           abesti = a_besti[w];
         }
       }
-      p.bmax_val[blockIdx.x] = best;
-      p.bmax_idx[blockIdx.x] = besti;
+      p.bmax_val[blk] = best;
+      p.bmax_idx[blk] = besti;
       if (p.bacc_val) {
-        p.bacc_val[blockIdx.x] = abest;
-        p.bacc_idx[blockIdx.x] = abesti;
+        p.bacc_val[blk] = abest;
+        p.bacc_idx[blk] = abesti;
       }
     }
   }
@@ -563,8 +783,33 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
 
 }  // namespace
 
+static int lstm_x_launch(const HzLstmParams& p, hipStream_t st) {
+  if (p.ldk % 64 || p.ldk < p.In || p.In <= 0 || p.H <= 0 || p.ldk > 6 * 512) return -1;
+  const bool fuse0 = p.xtab != nullptr;
+  if (fuse0 && (p.H0 != p.In || p.H0 > 3 * 512 || !p.pre0 || !p.h0_state || !p.c0_state || !p.tok_seq)) return -1;
+  if (!fuse0 && !p.x_state) return -1;
+  if (p.bacc_val && (!fuse0 || !p.n_forced || !p.bacc_idx || !p.bmax_val || !p.bmax_idx || p.nblk < 1 || p.nblk > 2048 ||
+                     p.V < 1))
+    return -1;
+  const int nch = (p.ldk + 511) / 512;
+  const dim3 grid((p.H + 3) / 4), block(512);
+  const size_t lds = (size_t)nch * 512 * sizeof(float);
+#define HZ_LX(N)                                                                          \
+  case N:                                                                                 \
+    if (fuse0) hipLaunchKernelGGL((lstm_x_kernel<N, true>), grid, block, lds, st, p);     \
+    else hipLaunchKernelGGL((lstm_x_kernel<N, false>), grid, block, lds, st, p);          \
+    break;
+  switch (nch) {
+    HZ_LX(1) HZ_LX(2) HZ_LX(3) HZ_LX(4) HZ_LX(5) HZ_LX(6)
+    default: return -1;
+  }
+#undef HZ_LX
+  return (int)hipGetLastError();
+}
+
 extern "C" int hz_lstm_cell_launch(const HzLstmParams* pp, hipStream_t st) {
   const HzLstmParams& p = *pp;
+  if (p.pre) return lstm_x_launch(p, st);
   if (p.ldk % 64 || p.ldk < p.In + p.H || p.In <= 0 || p.H <= 0) return -1;
   if (p.bacc_val && (!p.emb || !p.n_forced || !p.bacc_idx || !p.bmax_val || !p.bmax_idx || p.nblk < 1 || p.nblk > 2048 || p.V < 1))
     return -1;
@@ -609,26 +854,41 @@ extern "C" void hz_decoder_geometry(int V, int* nblk, int* rpb) {
 
 extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const HzDecoderParams& p = *pp;
-  if (p.ldk % 64 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
+  if (p.ldk % 8 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
   int nblk, rpb;
   hz_decoder_geometry(p.V, &nblk, &rpb);
   if (p.nblk != nblk || p.rpb != rpb) return -1;
-  const dim3 grid(nblk), block(256);
+  // split LSTM mode: recurrent-partial workgroups ahead of the decoder's (hh_rows)
+  constexpr int NCHH = 3;
+  if (p.n_hh < 0 || p.n_hh > 4) return -1;
+  if (p.n_hh > 0) {
+    if (p.hh_blk[0] != 0 || p.hh_blk[p.n_hh] != p.hh_blocks) return -1;
+    for (int l = 0; l < p.n_hh; ++l)
+      if (!p.hh_w[l] || !p.hh_b[l] || !p.hh_h[l] || !p.hh_out[l] || p.hh_H[l] < 1 || p.hh_ld[l] % 64 ||
+          p.hh_ld[l] < p.hh_H[l] || p.hh_ld[l] > NCHH * 512 ||
+          p.hh_blk[l + 1] - p.hh_blk[l] != (4 * p.hh_H[l] + HZ_HH_ROWS - 1) / HZ_HH_ROWS)
+        return -1;
+  }
+  const int hh = p.n_hh > 0 ? p.hh_blocks : 0;
+  const dim3 grid(nblk + hh), block(256);
   const int nch = (p.ldk + 511) / 512;
-  const size_t lds = (size_t)nch * 512 * sizeof(float);
+  const size_t lds = (size_t)(hh ? max(nch, NCHH) : nch) * 512 * sizeof(float);
   // 4 rows per wave round: 72 VGPRs, 7 waves/SIMD (8 rows: 104 VGPRs, 4 waves/SIMD; 22.7 vs 23.3 us
   // at V = 60000). Non-temporal weight loads measured slower for the decoder and the LSTM cells; so
   // was a streaming variant (a wave walks 1/2/4 whole blocks with the next 4 rows in flight, h
   // staged once per workgroup): 23.8 / 29.9 / 53.1 vs 22.3 us -- one short round per workgroup
   // with every load of the chip in flight at once is what reaches ~5.5 TB/s.
   constexpr int R = 4;
+#define HZ_DEC(N)                                                                       \
+  case N:                                                                               \
+    if (hh) hipLaunchKernelGGL((decoder_kernel<N, R, NCHH>), grid, block, lds, st, p);  \
+    else hipLaunchKernelGGL((decoder_kernel<N, R, 0>), grid, block, lds, st, p);        \
+    break;
   switch (nch) {
-    case 1: hipLaunchKernelGGL((decoder_kernel<1, R>), grid, block, lds, st, p); break;
-    case 2: hipLaunchKernelGGL((decoder_kernel<2, R>), grid, block, lds, st, p); break;
-    case 3: hipLaunchKernelGGL((decoder_kernel<3, R>), grid, block, lds, st, p); break;
-    case 4: hipLaunchKernelGGL((decoder_kernel<4, R>), grid, block, lds, st, p); break;
+    HZ_DEC(1) HZ_DEC(2) HZ_DEC(3) HZ_DEC(4)
     default: return -1;
   }
+#undef HZ_DEC
   return (int)hipGetLastError();
 }
 

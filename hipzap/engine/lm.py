@@ -6,9 +6,14 @@ The reference rebuilds the model and runs 201 CPU forwards per request with auto
     gate rows interleaved (unit j -> rows 4j..4j+3), ``b_ih + b_hh`` folded, K padded to a
     multiple of 64 (128-B rows; the kernels predicate the partial last 512-chunk), bf16;
     the tied embedding/decoder matrix is stored once (bf16, padded);
-  * one decode step = ``L`` fused LSTM-cell kernels + decoder GEMV (csrc/lstm.hip); the
-    argmax sampler is fused into the NEXT step's layer-0 kernel (every workgroup reduces the
-    decoder's per-workgroup maxima itself), so a step is L + 1 kernels. ``unroll`` steps are
+  * split layout (default, profiles/r2_awd_lstm/v3): the recurrent halves W_hh^l h^l_{t-1} + b^l
+    of every layer are computed one step AHEAD inside the decoder kernel (bandwidth-bound, so
+    they stream at its rate), layer kernels stream W_ih only, and layer 0 is a lookup in
+    ``xtab = W_ih^0 . emb^T`` (fp32 [V, 4 H0]) folded into the layer-1 kernel: a step is
+    ``L`` kernels (layer 1 with layer 0 and the token, layers 2.., decoder + W_hh rows).
+    Classic layout (``HIPZAP_LM_SPLIT=0``): ``L`` fused [W_ih | W_hh] cell kernels + decoder.
+  * the argmax sampler is fused into the NEXT step's first kernel (every workgroup reduces the
+    decoder's per-workgroup maxima itself). ``unroll`` steps are
     captured into ONE hipGraph (kernel k of step u reads step ``*step + u``; a 1-thread kernel
     advances the counter once per graph). The recurrent state, the step counter, the prompt
     length, the RNG seed and the token sequence all live on the device, so a request is
@@ -35,13 +40,38 @@ def _pad_to(n: int, m: int) -> int:
     return int(math.ceil(n / m) * m)
 
 
-def pack_awd_lstm(sd: dict, device) -> dict:
-    """state_dict (reference key layout) -> device-ready packed tensors."""
+def _interleave(w: torch.Tensor, H: int) -> torch.Tensor:
+    """gate-major [4H, K] (i, f, g, o blocks) -> unit-major rows: new row 4j+q = old row q*H + j"""
+    return w.reshape(4, H, -1).permute(1, 0, 2).reshape(4 * H, -1)
+
+
+def _bf16_rows(w: torch.Tensor, ld: int, dev) -> torch.Tensor:
+    wp = torch.zeros(w.shape[0], ld, dtype=torch.bfloat16, device=dev)
+    wp[:, : w.shape[1]] = w.to(dev, torch.bfloat16)
+    return wp
+
+
+def split_default(layers: list) -> bool:
+    """Split mode (csrc/lstm.hip lstm_x_kernel + the decoder's hh_rows): >= 2 layers, <= 4, every
+    hidden size <= 1536 (one 3-chunk recurrent row), unless HIPZAP_LM_SPLIT=0."""
+    if os.environ.get("HIPZAP_LM_SPLIT", "1") == "0":
+        return False
+    return 2 <= len(layers) <= 4 and all(ly["H"] <= 1536 for ly in layers)
+
+
+def pack_awd_lstm(sd: dict, device, split: bool | None = None) -> dict:
+    """state_dict (reference key layout) -> device-ready packed tensors.
+
+    classic: per layer ``[W_ih | W_hh]`` in one bf16 matrix (one GEMV per layer kernel).
+    split (default when it applies): ``W_ih`` and ``W_hh`` packed apart -- the recurrent GEMVs
+    run a step ahead inside the decoder kernel -- and layer 0's input projection becomes the
+    fp32 table ``xtab[v] = W_ih^0 . emb[v]`` ([V, 4 H0], exact fp32 from the checkpoint
+    weights), so layer 0 needs no weight stream at all."""
     dev = torch.device(device)
     if any(k.endswith("_reverse") for k in sd):
         raise ValueError("bidirectional AWD-LSTM: a bidirectional layer needs the whole sequence, so it cannot "
                          "drive token-by-token generation (GET /inference); use the eager model")
-    layers = []
+    raw = []
     l = 0
     while f"0.rnns.{l}.module.weight_ih_l0" in sd:
         pre = f"0.rnns.{l}"
@@ -49,21 +79,36 @@ def pack_awd_lstm(sd: dict, device) -> dict:
         w_hh = sd.get(f"{pre}.module.weight_hh_l0", sd.get(f"{pre}.weight_hh_l0_raw")).float()
         b = sd[f"{pre}.module.bias_ih_l0"].float() + sd[f"{pre}.module.bias_hh_l0"].float()
         four_h, n_in = w_ih.shape
-        H = four_h // 4
-        w = torch.cat([w_ih, w_hh], dim=1)  # [4H, In+H]
-        # interleave gates: new row 4j+q = old row q*H + j
-        w = w.reshape(4, H, n_in + H).permute(1, 0, 2).reshape(4 * H, n_in + H)
-        b = b.reshape(4, H).t().reshape(4 * H)
-        ldk = _pad_to(n_in + H, 64)
-        wp = torch.zeros(4 * H, ldk, dtype=torch.bfloat16, device=dev)
-        wp[:, : n_in + H] = w.to(dev, torch.bfloat16)
-        layers.append({"w": wp, "bias": b.to(dev).contiguous(), "In": n_in, "H": H, "ldk": ldk})
+        raw.append((w_ih, w_hh, b, n_in, four_h // 4))
         l += 1
-    if not layers:
+    if not raw:
         raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
+    if split is None:
+        split = split_default([{"H": H} for *_, H in raw])
+    layers = []
+    for i, (w_ih, w_hh, b, n_in, H) in enumerate(raw):
+        b = b.reshape(4, H).t().reshape(4 * H).to(dev).contiguous()
+        if split:
+            ldk, ldh = _pad_to(n_in, 64), _pad_to(H, 64)
+            layers.append({"w": None if i == 0 else _bf16_rows(_interleave(w_ih, H), ldk, dev),
+                           "w_hh": _bf16_rows(_interleave(w_hh, H), ldh, dev), "bias": b, "In": n_in, "H": H,
+                           "ldk": ldk, "ldh": ldh})
+        else:
+            ldk = _pad_to(n_in + H, 64)
+            w = _interleave(torch.cat([w_ih, w_hh], dim=1), H)  # [4H, In+H]
+            layers.append({"w": _bf16_rows(w, ldk, dev), "bias": b, "In": n_in, "H": H, "ldk": ldk})
     emb = sd["0.encoder.weight"].float()
     V, E = emb.shape
-    lde = _pad_to(max(E, layers[-1]["H"]), 64)
+    xtab = None
+    if split:
+        w_ih0, H0 = raw[0][0], raw[0][4]
+        if w_ih0.shape[1] != E:
+            raise ValueError("embedding width mismatch")
+        with torch.no_grad():
+            xtab = (emb.to(dev) @ _interleave(w_ih0, H0).to(dev).t()).contiguous()  # [V, 4 H0] fp32
+    # split: the embedding only feeds the (tied) decoder, whose 16-B row loads need K % 8 only --
+    # 1000 instead of 1024 columns streams 2.4 % fewer decoder bytes per token
+    lde = _pad_to(max(E, layers[-1]["H"]), 8 if split else 64)
     embp = torch.zeros(V, lde, dtype=torch.bfloat16, device=dev)
     embp[:, :E] = emb.to(dev, torch.bfloat16)
     dec_w = sd.get("1.decoder.weight")
@@ -74,7 +119,8 @@ def pack_awd_lstm(sd: dict, device) -> dict:
         decp = embp  # tied (awd_lstm.py:40)
     dec_b = sd.get("1.decoder.bias")
     dec_b = dec_b.float().to(dev) if dec_b is not None else None
-    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": dec_b, "V": V, "E": E, "lde": lde}
+    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": dec_b, "V": V, "E": E, "lde": lde,
+            "split": bool(split), "xtab": xtab}
 
 
 class LMEngine:
@@ -106,8 +152,16 @@ class LMEngine:
             self.bacc_idx = torch.empty(nblk, dtype=torch.int32, device=dev)
             # fused argmax sampler unless draws are recorded (tournament) or forced off
             self.fused_sampler = not record_draws and not os.environ.get("HIPZAP_SAMPLER_TOURNAMENT")
+            self.split = bool(packed.get("split"))
+            # split mode: pre[l] = W_hh^l . h^l_{t-1} + b^l, written a step ahead by the decoder kernel
+            # (measured: hosting layer l's rows in layer l+1's kernel instead, whose input IS h^l_t,
+            # made those latency-bound kernels slower by more than the decoder kernel saved --
+            # 44.6 vs 42.7 us/token, profiles/r2_awd_lstm/v3)
+            self.pre = [torch.empty(4 * ly["H"], device=dev) for ly in L] if self.split else []
             lstm_prms = []
             for i, ly in enumerate(L):
+                if self.split and i == 0:
+                    continue  # folded into layer 1's kernel (xtab lookup)
                 prm = N.LstmParams()
                 prm.w, prm.bias = ly["w"].data_ptr(), ly["bias"].data_ptr()
                 prm.emb = packed["emb"].data_ptr() if i == 0 else 0
@@ -119,7 +173,17 @@ class LMEngine:
                 prm.In, prm.H, prm.ldk = ly["In"], ly["H"], ly["ldk"]
                 if i == 0 and prm.In > packed["lde"]:
                     raise ValueError("embedding width mismatch")
-                if i == 0 and self.fused_sampler:
+                first = i == (1 if self.split else 0)  # the kernel that consumes the token
+                if self.split:
+                    prm.emb = 0
+                    prm.pre = self.pre[i].data_ptr()
+                    if i == 1:
+                        prm.x_state = 0
+                        prm.xtab = packed["xtab"].data_ptr()
+                        prm.pre0 = self.pre[0].data_ptr()
+                        prm.h0_state, prm.c0_state = self.h[0].data_ptr(), self.c[0].data_ptr()
+                        prm.H0 = L[0]["H"]
+                if first and self.fused_sampler:
                     prm.n_forced = self.n_forced.data_ptr()
                     prm.bacc_val, prm.bacc_idx = self.bacc_val.data_ptr(), self.bacc_idx.data_ptr()
                     prm.bmax_val, prm.bmax_idx = self.bmax_val.data_ptr(), self.bmax_idx.data_ptr()
@@ -137,6 +201,17 @@ class LMEngine:
             d.n_exclude = len(ex)
             for i, e in enumerate(ex):
                 d.exclude[i] = e
+            if self.split:  # the next step's recurrent partials ride in the decoder launch
+                d.n_hh = len(L)
+                blk = 0
+                for i, ly in enumerate(L):
+                    d.hh_w[i], d.hh_b[i] = ly["w_hh"].data_ptr(), ly["bias"].data_ptr()
+                    d.hh_h[i], d.hh_out[i] = self.h[i].data_ptr(), self.pre[i].data_ptr()
+                    d.hh_H[i], d.hh_ld[i] = ly["H"], ly["ldh"]
+                    d.hh_blk[i] = blk
+                    blk += -(-4 * ly["H"] // N.HH_ROWS)
+                d.hh_blk[len(L)] = blk
+                d.hh_blocks = blk
             s = N.SamplerParams()
             s.keys, s.tok_seq, s.step = self.keys.data_ptr(), self.tok_seq.data_ptr(), self.step.data_ptr()
             s.bmax_val, s.bmax_idx, s.nblk, s.rpb = d.bmax_val, d.bmax_idx, nblk, rpb
@@ -198,6 +273,8 @@ class LMEngine:
         with self._lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             for t in self.h + self.c:
                 t.zero_()
+            for pre, ly in zip(self.pre, self.p["layers"]):  # W_hh . 0 + b
+                pre.copy_(ly["bias"])
             self.step.zero_()
             self.n_forced.fill_(P)
             self.seed.fill_(int(seed) & ((1 << 62) - 1))
