@@ -31,6 +31,16 @@ __device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
   return av > bv || (av == bv && ai < bi);
 }
 
+// 16-B weight load at column k of a row of ld bf16, clamped into the row instead of predicated:
+// `k < ld ? load : 0` compiles to an exec-masked branch whose zero write in the other lanes is a
+// write-after-write hazard on the destination VGPRs of a load in flight, so the compiler put an
+// s_waitcnt vmcnt(0) after the first loads -- the weight stream of every LSTM kernel was issued
+// in two serialised halves. Columns past ld re-read the row's last 16 B; every caller multiplies
+// them with a vector operand that is zero there.
+__device__ __forceinline__ u32x4 ld_row(const bf16_t* row, int k, int ld) {
+  return *reinterpret_cast<const u32x4*>(row + min(k, ld - 8));
+}
+
 // LDS-only workgroup barrier: unlike __syncthreads() it does not wait for the caller's
 // outstanding global loads (the LSTM weight stream stays in flight across it)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -132,21 +142,19 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const HzLstmParams p) {
 #pragma unroll
     for (int r = 0; r < TPT; ++r) {
       const int e = tid + r * 256;
-      tv[r] = e < p.nblk ? p.bacc_val[e] : -INFINITY;
-      ti[r] = e < p.nblk ? p.bacc_idx[e] : 0x7fffffff;
+      const int ec = min(e, p.nblk - 1);  // unconditional load (see ld_row); duplicates do not change the max
+      tv[r] = p.bacc_val[ec];
+      ti[r] = p.bacc_idx[ec];
     }
   }
   const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
-  const bf16_t* w = p.w + (long)(4 * min(j, p.H - 1)) * p.ldk + lane * 8;
+  const bf16_t* w = p.w + (long)(4 * min(j, p.H - 1)) * p.ldk;
   u32x4 wv[4][NC];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int k = (kw * NC + c) * 512 + lane * 8;
-      const u32x4* src = reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8));
-      wv[q][c] = k < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
-    }
+    for (int c = 0; c < NC; ++c) wv[q][c] = ld_row(w + (long)q * p.ldk, (kw * NC + c) * 512 + lane * 8, p.ldk);
+  __builtin_amdgcn_sched_barrier(0);  // the whole weight stream issued before anything waits
   int tok = 0;
   if (fused) {  // this step's token from the last decoder (the argmax sampler's rule)
     __shared__ float sv[4];
@@ -253,50 +261,61 @@ __global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
   constexpr int U0 = 3;                     // layer-0 units per thread (H0 <= 1536)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int slot = wave / KW, kw = wave - slot * KW;
-  const int t = *p.step + p.step_off;
-  const int par = t & 1;
-  if (!HZ_DCHECK(p.In <= p.ldk && p.ldk <= NCH * 512 && (!FUSE0 || (p.H0 == p.In && p.H0 <= U0 * 512)))) return;
-  // ---- token-independent loads, issued in the order their values are needed (vmcnt retires in
-  // issue order): decoder maxima, layer-0 recurrent partials and cell state, this unit's W_ih rows
-  const bool fused = FUSE0 && p.bacc_val && t >= *p.n_forced;
+  const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
+  const int jc = min(j, p.H - 1);
+  // ---- every load that does not need the step counter, before anything waits: the step is a
+  // global counter (an L2 miss across XCDs), so step-dependent (parity) operands are loaded for
+  // BOTH parities and selected later; the weight stream goes last (vmcnt retires in issue order)
   float tv[TPT];
   int ti[TPT];
-  if (fused) {
+  if (FUSE0) {  // decoder maxima (clamped: duplicates do not change the argmax). Unconditional
+    // loads: a branch on bacc_val made the compiler zero these registers on the other path,
+    // a write-after-write hazard that cost a vmcnt(0) before the weight stream.
+    const float* bv = p.bacc_val ? p.bacc_val : p.pre0;
+    const int* bi = p.bacc_val ? p.bacc_idx : reinterpret_cast<const int*>(p.pre0);
+    const int nb = p.bacc_val ? p.nblk : 1;
 #pragma unroll
     for (int r = 0; r < TPT; ++r) {
-      const int e = tid + r * 512;
-      tv[r] = e < p.nblk ? p.bacc_val[e] : -INFINITY;
-      ti[r] = e < p.nblk ? p.bacc_idx[e] : 0x7fffffff;
+      const int ec = min(tid + r * 512, nb - 1);
+      tv[r] = bv[ec];
+      ti[r] = bi[ec];
     }
   }
   f32x4 g0[U0];
-  float c0[U0];
+  float c0[2][U0];
+  float xs[2][NCH];
   if (FUSE0) {
 #pragma unroll
     for (int r = 0; r < U0; ++r) {
       const int u = min(tid + r * 512, p.H0 - 1);
       g0[r] = *reinterpret_cast<const f32x4*>(p.pre0 + 4 * u);
-      c0[r] = p.c0_state[par * p.H0 + u];
+      c0[0][r] = p.c0_state[u];
+      c0[1][r] = p.c0_state[p.H0 + u];
+    }
+  } else {  // the previous layer's h of this step, both parity halves
+#pragma unroll
+    for (int r = 0; r < NCH; ++r) {
+      const int i = min(tid + r * 512, p.In - 1);
+      xs[0][r] = p.x_state[i];
+      xs[1][r] = p.x_state[p.In + i];
     }
   }
-  const int j = blockIdx.x * UPW + slot;  // hidden unit of this wave
-  const int jc = min(j, p.H - 1);
-  const bf16_t* w = p.w + (long)(4 * jc) * p.ldk + lane * 8;
+  const f32x4 pj = *reinterpret_cast<const f32x4*>(p.pre + 4 * jc);
+  const float cj0 = p.c_state[jc], cj1 = p.c_state[p.H + jc];
+  const bf16_t* w = p.w + (long)(4 * jc) * p.ldk;
   u32x4 wv[4][NC];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int k = (kw * NC + c) * 512 + lane * 8;
-      const u32x4* src = reinterpret_cast<const u32x4*>(w + (long)q * p.ldk + (k - lane * 8));
-      wv[q][c] = k < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
-    }
-  const f32x4 pj = *reinterpret_cast<const f32x4*>(p.pre + 4 * jc);
-  const float cj = p.c_state[par * p.H + jc];
+    for (int c = 0; c < NC; ++c) wv[q][c] = ld_row(w + (long)q * p.ldk, (kw * NC + c) * 512 + lane * 8, p.ldk);
+  __builtin_amdgcn_sched_barrier(0);  // the whole weight stream issued before anything waits
+  const int t = *p.step + p.step_off;
+  const int par = t & 1;
+  if (!HZ_DCHECK(p.In <= p.ldk && p.ldk <= NCH * 512 && (!FUSE0 || (p.H0 == p.In && p.H0 <= U0 * 512)))) return;
   // ---- the input vector in LDS ----
   if (FUSE0) {
     int tok;
-    if (fused) {
+    if (p.bacc_val && t >= *p.n_forced) {  // this step's token from the last decoder's maxima
       __shared__ float sv[WAVES];
       __shared__ int si[WAVES];
       float v = tv[0];
@@ -330,7 +349,7 @@ __global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
         const float si = 1.f / (1.f + __expf(-g[0]));
         const float sf = 1.f / (1.f + __expf(-g[1]));
         const float so = 1.f / (1.f + __expf(-g[3]));
-        const float c_new = sf * c0[r] + si * tanhf(g[2]);
+        const float c_new = sf * (par ? c0[1][r] : c0[0][r]) + si * tanhf(g[2]);
         const float h_new = so * tanhf(c_new);
         vin[u] = h_new;
         if (blockIdx.x == 0) {
@@ -341,11 +360,14 @@ __global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
         vin[u] = 0.f;
       }
     }
-  } else {
-    const float* x = p.x_state + (par ^ 1) * p.In;  // previous layer's output of THIS step
-    for (int i = tid; i < NCH * 512; i += 512) vin[i] = i < p.In ? x[i] : 0.f;
+  } else {  // the previous layer's output of THIS step: parity half par ^ 1
+#pragma unroll
+    for (int r = 0; r < NCH; ++r) {
+      const int i = tid + r * 512;
+      vin[i] = i < p.In ? (par ? xs[0][r] : xs[1][r]) : 0.f;
+    }
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: the weight loads stay in flight
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -366,7 +388,7 @@ __global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
   if (lane == 0 && kw > 0)
 #pragma unroll
     for (int q = 0; q < 4; ++q) part[wave][q] = acc[q];
-  __syncthreads();
+  lds_barrier();
   if (lane == 0 && kw == 0 && j < p.H) {
 #pragma unroll
     for (int o = 1; o < KW; ++o)
@@ -375,7 +397,7 @@ __global__ __launch_bounds__(512) void lstm_x_kernel(const HzLstmParams p) {
     const float si = 1.f / (1.f + __expf(-(acc[0] + pj[0])));
     const float sf = 1.f / (1.f + __expf(-(acc[1] + pj[1])));
     const float so = 1.f / (1.f + __expf(-(acc[3] + pj[3])));
-    const float c_new = sf * cj + si * tanhf(acc[2] + pj[2]);
+    const float c_new = sf * (par ? cj1 : cj0) + si * tanhf(acc[2] + pj[2]);
     const float h_new = so * tanhf(c_new);
     p.c_state[(par ^ 1) * p.H + j] = c_new;
     p.h_state[(par ^ 1) * p.H + j] = h_new;
@@ -589,18 +611,43 @@ __global__ __launch_bounds__(1024) void argmax_sampler_kernel(const HzSamplerPar
   sample_argmax<16>(p, *p.step + p.step_off);
 }
 
+// x[k .. k+8) for k = c*512 + lane*8 of every 512-chunk c (zero past n; n even, x 8-B aligned):
+// the vector operand of a GEMV row loaded straight into registers. Issued BEFORE the weight
+// loads, so waiting for it does not wait for the weight stream (vmcnt retires in issue order),
+// and no LDS staging / workgroup barrier stands between the kernel start and the weight stream.
+// Loads are clamped into [0, n) like ld_row (positions past n hold duplicates: callers zero the
+// matching weights with wmask).
+template <int NC>
+__device__ __forceinline__ void load_vec(const float* x, int n, int lane, f32x4 (&v)[NC][2]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int k = c * 512 + lane * 8 + hf * 4 + pr * 2;
+        const float2 e = *reinterpret_cast<const float2*>(x + min(k, n - 2));
+        v[c][hf][2 * pr] = e.x;
+        v[c][hf][2 * pr + 1] = e.y;
+      }
+}
+
+// The clamped columns past ld are zeroed on the WEIGHT side, at use (a mask on the register
+// vector operand is loop-invariant: the compiler hoisted it, and its wait, above the weight loads).
+__device__ __forceinline__ u32x4 wmask(const u32x4 w, int k, int ld) { return k < ld ? w : u32x4{0u, 0u, 0u, 0u}; }
+
 template <class T>
 __device__ __forceinline__ T pick4(const T (&a)[4], int l) {  // uniform select, no dynamic kernarg index
   return l == 0 ? a[0] : l == 1 ? a[1] : l == 2 ? a[2] : a[3];
 }
 
 #ifndef HZ_HH_RR
-#define HZ_HH_RR 4
+#define HZ_HH_RR 2  // 70 VGPRs with the register vector operand (4 rows: 98, 4 waves/SIMD)
 #endif
 // Split LSTM mode: rows [r0, r0 + HZ_HH_ROWS) of layer l's next-step recurrent gate partials
 // W_hh^l . h^l_t + b^l. 4 waves x RR rows per round, every 16-B load of a round in flight.
 template <int NCHH>
-__device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par, float* hv) {
+__device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par) {
   constexpr int RR = HZ_HH_RR;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int l = 0;
@@ -613,8 +660,6 @@ __device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par
   float* out = pick4(p.hh_out, l);
   const int r0 = (b - (l == 0 ? p.hh_blk[0] : l == 1 ? p.hh_blk[1] : l == 2 ? p.hh_blk[2] : p.hh_blk[3])) * HZ_HH_ROWS;
   if (!HZ_DCHECK(H <= ld && ld <= NCHH * 512)) return;
-  for (int i = tid; i < NCHH * 512; i += blockDim.x) hv[i] = i < H ? h[i] : 0.f;
-  __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < HZ_HH_ROWS; rr += 4 * RR) {
     u32x4 wv[RR][NCHH];
@@ -624,21 +669,23 @@ __device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par
 #pragma unroll
       for (int c = 0; c < NCHH; ++c) {
         const int k = c * 512 + lane * 8;
-        wv[q][c] = k < ld ? *reinterpret_cast<const u32x4*>(W + (long)r * ld + k) : u32x4{0u, 0u, 0u, 0u};
+        wv[q][c] = ld_row(W + (long)r * ld, k, ld);
       }
     }
+    f32x4 hr[NCHH][2];  // h after the weights: its address needs the step counter, theirs does not
+    load_vec<NCHH>(h, H, lane, hr);
+    __builtin_amdgcn_sched_barrier(0);
     float acc[RR];
 #pragma unroll
     for (int q = 0; q < RR; ++q) acc[q] = 0.f;
 #pragma unroll
     for (int c = 0; c < NCHH; ++c) {
       const int k = c * 512 + lane * 8;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
+      const f32x4 v0 = hr[c][0], v1 = hr[c][1];
 #pragma unroll
       for (int q = 0; q < RR; ++q) {
         float f[8];
-        unpack8(wv[q][c], f);
+        unpack8(wmask(wv[q][c], k, ld), f);
         acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
                   f[6] * v1[2] + f[7] * v1[3];
       }
@@ -657,15 +704,16 @@ __device__ __forceinline__ void hh_rows(const HzDecoderParams& p, int b, int par
 
 template <int NCH, int R, int NCHH>
 __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
-  extern __shared__ __attribute__((aligned(16))) float hv[];
   __shared__ float w_best[4];
   __shared__ int w_besti[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = *p.step + p.step_off;
   const int par = t & 1;
-  if (NCHH > 0 && (int)blockIdx.x < p.hh_blocks) {  // split LSTM mode: next step's W_hh partials
-    hh_rows<NCHH>(p, blockIdx.x, par, hv);
-    return;
+  if constexpr (NCHH > 0) {
+    if ((int)blockIdx.x < p.hh_blocks) {  // split LSTM mode: next step's W_hh partials
+      hh_rows<NCHH>(p, blockIdx.x, par);
+      return;
+    }
   }
   const int blk = blockIdx.x - (NCHH > 0 ? p.hh_blocks : 0);
   const float* h = p.h_state + (par ^ 1) * p.H;  // last layer's output of this step
@@ -674,10 +722,8 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
   const int ngroups = (p.V + R - 1) / R;
   const int gpb = p.rpb / R;
   const int g_end = min(ngroups, (blk + 1) * gpb);
-  // (measured: issuing the first round of weight rows BEFORE staging h made the kernel 14 %
-  // slower, 26.4 vs 23.1 us at V = 60000, so h is staged first)
-  for (int i = tid; i < NCH * 512; i += blockDim.x) hv[i] = i < p.H ? h[i] : 0.f;
-  __syncthreads();
+  // h is not staged through LDS (v2 staged it first, then issued the weights: a load latency and
+  // a barrier ahead of every workgroup's weight stream); each lane loads its own K positions
   const unsigned long long seed = p.keys ? *p.seed : 0ull;
   float best = -INFINITY, abest = -INFINITY;
   int besti = 0x7fffffff, abesti = 0x7fffffff;
@@ -687,23 +733,22 @@ __global__ __launch_bounds__(256) void decoder_kernel(const HzDecoderParams p) {
     for (int q = 0; q < R; ++q) {
       const int r = min(g * R + q, p.V - 1);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(p.w + (long)r * p.ldk + c * 512 + lane * 8);
-        wv[q][c] = c * 512 + lane * 8 < p.ldk ? *src : u32x4{0u, 0u, 0u, 0u};
-      }
+      for (int c = 0; c < NCH; ++c) wv[q][c] = ld_row(p.w + (long)r * p.ldk, c * 512 + lane * 8, p.ldk);
     }
+    f32x4 hr[NCH][2];  // after the weights: h's address needs the step counter, theirs does not
+    load_vec<NCH>(h, p.H, lane, hr);
+    __builtin_amdgcn_sched_barrier(0);  // every load of the round issued before the first use
     float acc[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) acc[q] = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int k = c * 512 + lane * 8;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(hv + k);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(hv + k + 4);
+      const f32x4 v0 = hr[c][0], v1 = hr[c][1];
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         float f[8];
-        unpack8(wv[q][c], f);
+        unpack8(wmask(wv[q][c], k, p.ldk), f);
         acc[q] += f[0] * v0[0] + f[1] * v0[1] + f[2] * v0[2] + f[3] * v0[3] + f[4] * v1[0] + f[5] * v1[1] +
                   f[6] * v1[2] + f[7] * v1[3];
       }
@@ -854,7 +899,7 @@ extern "C" void hz_decoder_geometry(int V, int* nblk, int* rpb) {
 
 extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const HzDecoderParams& p = *pp;
-  if (p.ldk % 8 || p.ldk < p.H || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
+  if (p.ldk % 8 || p.ldk < p.H || p.H % 2 || (p.keys && (!p.seed || !p.bmax_val || !p.bmax_idx))) return -1;
   int nblk, rpb;
   hz_decoder_geometry(p.V, &nblk, &rpb);
   if (p.nblk != nblk || p.rpb != rpb) return -1;
@@ -864,7 +909,7 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   if (p.n_hh > 0) {
     if (p.hh_blk[0] != 0 || p.hh_blk[p.n_hh] != p.hh_blocks) return -1;
     for (int l = 0; l < p.n_hh; ++l)
-      if (!p.hh_w[l] || !p.hh_b[l] || !p.hh_h[l] || !p.hh_out[l] || p.hh_H[l] < 1 || p.hh_ld[l] % 64 ||
+      if (!p.hh_w[l] || !p.hh_b[l] || !p.hh_h[l] || !p.hh_out[l] || p.hh_H[l] < 1 || p.hh_H[l] % 2 || p.hh_ld[l] % 64 ||
           p.hh_ld[l] < p.hh_H[l] || p.hh_ld[l] > NCHH * 512 ||
           p.hh_blk[l + 1] - p.hh_blk[l] != (4 * p.hh_H[l] + HZ_HH_ROWS - 1) / HZ_HH_ROWS)
         return -1;
@@ -872,7 +917,7 @@ extern "C" int hz_decoder_launch(const HzDecoderParams* pp, hipStream_t st) {
   const int hh = p.n_hh > 0 ? p.hh_blocks : 0;
   const dim3 grid(nblk + hh), block(256);
   const int nch = (p.ldk + 511) / 512;
-  const size_t lds = (size_t)(hh ? max(nch, NCHH) : nch) * 512 * sizeof(float);
+  const size_t lds = 0;  // the vector operand lives in registers (load_vec)
   // 4 rows per wave round: 72 VGPRs, 7 waves/SIMD (8 rows: 104 VGPRs, 4 waves/SIMD; 22.7 vs 23.3 us
   // at V = 60000). Non-temporal weight loads measured slower for the decoder and the LSTM cells; so
   // was a streaming variant (a wave walks 1/2/4 whole blocks with the next 4 rows in flight, h
