@@ -72,7 +72,7 @@ def parse():
     return ap.parse_args()
 
 
-def run_scatter(args, rank, world, device, adapter, ckpt):
+def run_scatter(args, rank, world, device, adapter, ckpt, tuned=None):
     """BASELINE configs 3/5: global batch scattered over ranks (RCCL), per-rank hipGraph, logits
     gathered to rank 0. Step = scatter + per-rank forward + gather."""
     from hipzap.engine.engine import Engine
@@ -86,7 +86,8 @@ def run_scatter(args, rank, world, device, adapter, ckpt):
         sd = torch.load(ckpt, map_location="cpu", weights_only=True)
         params, arch_kw = adapter.pack({k: v.to(device) for k, v in sd.items()}, device)
     params, arch_kw = broadcast_params(params, lambda kw: adapter.meta_params(**kw), device, arch_kw=arch_kw)
-    eng = Engine(args.model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
+    eng = Engine(args.model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False,
+                 tuned=tuned)
     x_in = adapter.example_input(shard)
     in_shape = tuple(eng.contexts[0].input.shape[1:])
     out_shape = tuple(eng.contexts[0].output.shape[1:])
@@ -246,7 +247,7 @@ def main():
     if is_dist():
         dist.barrier()
     if args.mode == "scatter":
-        run_scatter(args, rank, world, device, adapter, ckpt)
+        run_scatter(args, rank, world, device, adapter, ckpt, tuned)
         if is_dist():
             dist.barrier()
             dist.destroy_process_group()

@@ -21,6 +21,15 @@
 //   * same swapped orientation and fused epilogue as conv.hip (4 consecutive output features
 //     per lane: 16-B bias, 8-B residual, 8-B store), XCD-aware tile order.
 // Requirements (checked by the launcher): K % 64 == 0, ldx % 8 == 0, weight rows padded to 128.
+//
+// CV (implicit-GEMM convolution at large M, e.g. ResNet-50 at batch >= 4): the same tile, the same
+// LDS image, only the activation SOURCE changes. Rows are output pixels of a channel-blocked
+// [N][C/32][H][W][32] input (C % 64 == 0, so a 64-deep K step is two 32-channel blocks of ONE
+// filter tap (r, s)); each lane's 16-B chunk is fetched with buffer_load ... lds through a buffer
+// descriptor over the whole input, and a tap that falls into the zero padding gets an offset past
+// the descriptor's range, which the hardware range check turns into zeros in LDS (no zero buffer,
+// no predicated DMA). The running (r, s, channel block) of the next staged K step is scalar and
+// advances incrementally; the epilogue stores channel-blocked output (+ residual in that layout).
 #include <cstdlib>
 
 #include "common.h"
@@ -80,7 +89,7 @@ __device__ __forceinline__ void rows_stats(const float* __restrict__ st, int nsl
 // LNF: folded-LayerNorm variant (p.lnf != NULL); a separate instantiation so the plain GEMM keeps
 // its register budget (the fold's statistics cost ~60 VGPRs, which halves occupancy)
 // WM x WN waves (4 or 8): wave (wm, wn) owns rows wm*BM/WM.. and features wn*BN/WN..
-template <int BM, int BN, int NS, bool LNF, int WM, int WN>
+template <int BM, int BN, int NS, bool LNF, int WM, int WN, bool CV = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvParams p, int group_m) {
   constexpr int NW = WM * WN;
   constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 16x16 fragments per wave
@@ -106,25 +115,62 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   // staging sources: x piece q = wave + 4i covers tile rows 8q .. 8q+7, lane -> row 8q + (lane>>3),
   // swizzled chunk (lane&7) ^ (((q&1)<<2) + (lane>>4)); rows >= M are clamped (never stored)
   const bf16_t* xsrc[XPW];
+  // CV: per piece, the element offset of the lane's chunk at tap (0, 0) of channel block 0 and the
+  // input-window origin (ih0, iw0) of its output pixel
+  int xb[XPW], xih[XPW], xiw[XPW];
+  const int PQ = p.P * p.Q, HW = p.H * p.W;
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
     const int q = wave + NW * i;
     const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
     const int chunk = (lane & 7) ^ (((q & 1) << 2) + (lane >> 4));
-    xsrc[i] = p.x + (long)row * p.ldx + chunk * 8;
+    if constexpr (CV) {
+      const int ni = fdiv(row, PQ), hw = row - ni * PQ;
+      const int oh = fdiv(hw, p.Q), ow = hw - oh * p.Q;
+      xih[i] = oh * p.stride - p.pad;
+      xiw[i] = ow * p.stride - p.pad;
+      xb[i] = ((ni * (p.C >> 5) + (chunk >> 2)) * HW + xih[i] * p.W + xiw[i]) * 32 + (chunk & 3) * 8;
+      xsrc[i] = p.x;
+    } else {
+      xsrc[i] = p.x + (long)row * p.ldx + chunk * 8;
+    }
   }
+  // CV: descriptor over the whole input (launcher: < 2^31 bytes); scalar running tap position
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, (short)0, CV ? p.N * p.C * HW * 2 : 0, 0x00020000);
+  int cv_cb = 0, cv_r = 0, cv_s = 0;
   const bf16_t* wsrc = p.w + ((long)(n0 >> 4) * p.ksteps * 64 + lane) * 8;
   // debug contracts: the tile's weight rows exist in the 128-row padded packing, and the last
   // staged activation line lies inside [M][ldx] (the DMA cannot be skipped, so a violation
   // re-points the sources at the tensor bases instead)
   if (!HZ_DCHECK(n0 + BN <= ((p.Cout + 127) / 128) * 128)) wsrc = p.w + lane * 8;
+  if constexpr (!CV) {
 #pragma unroll
-  for (int i = 0; i < XPW; ++i)
-    if (!HZ_DCHECK(xsrc[i] - p.x + (long)(nst - 1) * 64 + 8 <= (long)p.M * p.ldx)) xsrc[i] = p.x;
+    for (int i = 0; i < XPW; ++i)
+      if (!HZ_DCHECK(xsrc[i] - p.x + (long)(nst - 1) * 64 + 8 <= (long)p.M * p.ldx)) xsrc[i] = p.x;
+  }
   auto stage = [&](int buf, int st) {
     char* base = smem + buf * SBYTES;
+    if constexpr (CV) {  // stage() runs for st = 0, 1, 2, ... in order: the tap position is running
+      const int u = ((cv_cb * p.H + cv_r) * p.W + cv_s) * 32;
 #pragma unroll
-    for (int i = 0; i < XPW; ++i) glds16(xsrc[i] + st * 64, base + (wave + NW * i) * 1024);
+      for (int i = 0; i < XPW; ++i) {
+        const bool v = (unsigned)(xih[i] + cv_r) < (unsigned)p.H && (unsigned)(xiw[i] + cv_s) < (unsigned)p.W;
+        const unsigned voff = v ? (unsigned)(xb[i] + u) * 2u : 0x80000000u;  // past the range -> zeros
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_void*)(base + (wave + NW * i) * 1024), 16, voff, 0, 0, 0);
+      }
+      cv_cb += 2;  // C % 64 == 0: a 64-deep step never straddles a tap
+      if (cv_cb == (p.C >> 5)) {
+        cv_cb = 0;
+        if (++cv_s == p.S) {
+          cv_s = 0;
+          ++cv_r;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XPW; ++i) glds16(xsrc[i] + st * 64, base + (wave + NW * i) * 1024);
+    }
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
       const int f = wave + NW * i;  // f = ks * NWG + g
@@ -195,11 +241,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
     const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
     const bool mval = m < p.M;
     float s1 = 0.f, s2 = 0.f;
+    int ni_m = 0, hw_m = 0;  // CV: channel-blocked [N][Cout/32][P*Q][32] output
+    if constexpr (CV) {
+      ni_m = fdiv(mval ? m : 0, PQ);
+      hw_m = m - ni_m * PQ;
+    }
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
       const int n = n0 + wn * (BN / WN) + i * 16 + (lane >> 4) * 4;
-      const long o = (long)m * p.ldo + n;
-      if (!mval || n >= p.Cout || !HZ_DCHECK(o + 4 <= (long)(p.M - 1) * p.ldo + p.Cout)) continue;
+      const long o = CV ? (((long)ni_m * (p.Cout >> 5) + (n >> 5)) * PQ + hw_m) * 32 + (n & 31) : (long)m * p.ldo + n;
+      const long olim = CV ? (long)p.N * p.Cout * PQ : (long)(p.M - 1) * p.ldo + p.Cout;
+      if (!mval || n >= p.Cout || !HZ_DCHECK(o + 4 <= olim)) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (f_in) {
         const f32x4 c = *reinterpret_cast<const f32x4*>(lf->c1 + n);
@@ -259,7 +311,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   }
 }
 
-template <int BM, int BN, int NS, int WM = 2, int WN = 2>
+template <int BM, int BN, int NS, int WM = 2, int WN = 2, bool CVOK = false>
 int launch_lds(const HzConvParams& p, hipStream_t st) {
   // the last feature tile must stay inside the 128-row padded weight packing (BN = 96 / 192 / 288
   // tiles fit only some widths: every BERT / ViT projection, not arbitrary N)
@@ -268,6 +320,13 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
   const dim3 block(64 * WM * WN);
   static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
   const int group_m = group_env < 1 ? 1 : group_env;
+  if (!p.x_rowmajor) {  // implicit-GEMM conv (CV): every feature tile lies inside Cout (rows padded to 64)
+    if (!CVOK || p.out_rowmajor || p.lnf || p.C % 64 || p.Cout % BN || p.Cout % 32 || p.K != p.R * p.S * p.C ||
+        (long)p.N * p.C * p.H * p.W * 2 >= (1L << 31))
+      return -1;
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, true>), dim3(tiles), block, 0, st, p, group_m);
+    return (int)hipGetLastError();
+  }
   if (p.lnf) {  // the folded-LayerNorm statistics slabs assume 2 feature halves per tile
     if (WN != 2) return -3;
     hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
@@ -286,7 +345,27 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
 // 64x288, 256x96). Row-major activations only.
 extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
   const HzConvParams& p = *pp;
-  if (!p.x_rowmajor || !p.out_rowmajor || p.K % 64 || p.ksteps * 32 != p.K || p.ldx % 8 || p.Cout % 4) return -1;
+  if (!p.x_rowmajor) {  // implicit-GEMM conv on channel-blocked activations: the 4- and 8-wave tiles
+    if (p.K % 64 || p.ksteps * 32 != p.K || p.Cout % 4) return -1;
+    switch (cfg) {
+      case 16: return launch_lds<128, 128, 3, 2, 2, true>(p, st);
+      case 20: return launch_lds<128, 128, 2, 2, 2, true>(p, st);
+      case 17: return launch_lds<64, 128, 3, 2, 2, true>(p, st);
+      case 21: return launch_lds<64, 128, 2, 2, 2, true>(p, st);
+      case 18: return launch_lds<128, 64, 3, 2, 2, true>(p, st);
+      case 22: return launch_lds<128, 64, 2, 2, 2, true>(p, st);
+      case 19: return launch_lds<64, 64, 3, 2, 2, true>(p, st);
+      case 23: return launch_lds<64, 64, 2, 2, 2, true>(p, st);
+      case 28: return launch_lds<128, 128, 3, 2, 4, true>(p, st);
+      case 29: return launch_lds<128, 128, 2, 2, 4, true>(p, st);
+      case 30: return launch_lds<256, 128, 2, 4, 2, true>(p, st);
+      case 31: return launch_lds<128, 64, 3, 4, 2, true>(p, st);
+      case 32: return launch_lds<64, 128, 3, 2, 4, true>(p, st);
+      case 33: return launch_lds<256, 64, 2, 4, 2, true>(p, st);
+      default: return -2;
+    }
+  }
+  if (!p.out_rowmajor || p.K % 64 || p.ksteps * 32 != p.K || p.ldx % 8 || p.Cout % 4) return -1;
   switch (cfg) {
     case 16: return launch_lds<128, 128, 3>(p, st);
     case 20: return launch_lds<128, 128, 2>(p, st);

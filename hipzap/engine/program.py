@@ -161,7 +161,12 @@ class ExecContext:
         return prm
 
     def _add_conv_pair(self, lib, a, b, plan_a, plan_b, tuned):
-        """Two independent convs reading the same input -> one grouped launch (conv2_kernel)."""
+        """Two independent convs reading the same input -> one grouped launch (conv2_kernel).
+        Convs planned on the LDS tile (large-M implicit GEMM, gemm.hip CV mode) launch alone."""
+        if plan_a[0] in conv_ops.LDS_TILES or plan_b[0] in conv_ops.LDS_TILES:
+            self._add_node(lib, a, plan_a)
+            self._add_node(lib, b, plan_b)
+            return
         key = pair_key(plan_a[2], plan_b[2])
         if tuned is not None and key in tuned:
             cfg, kw = int(tuned[key][0]), int(tuned[key][1])

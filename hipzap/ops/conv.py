@@ -30,6 +30,10 @@ LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
              33: (256, 64),  # 28-33: 8-wave workgroups
              34: (64, 96), 35: (128, 192), 36: (128, 192), 37: (64, 288), 38: (64, 288), 39: (256, 96),
              40: (64, 96)}  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
+# LDS tiles that also run as an implicit-GEMM conv on channel-blocked activations (csrc/gemm.hip CV
+# mode; ResNet at batch >= 4): C % 64 == 0, Cout % BN == 0
+LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33)
+LDS_CONV_MIN_M = 4096  # heuristic: below this the register-ring conv kernel (bs=1 shapes) stays
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
 
@@ -154,6 +158,17 @@ def lds_ok(M: int, K: int, rowmajor: bool, pc: PackedConv | None = None) -> bool
     return pc is None or (pc.wf.shape[0] % (GEMM_ROW_PAD // 16) == 0 and pc.ksteps * 32 == K)
 
 
+def lds_conv_ok(M: int, pc: PackedConv | None, n_in_bytes: int | None = None) -> bool:
+    """Can the LDS tile run this conv as an implicit GEMM (csrc/gemm.hip CV mode)?"""
+    if pc is None or M < 64 or pc.cin % 64 or pc.cout % 32 or pc.ksteps * 32 != pc.K:
+        return False
+    return n_in_bytes is None or n_in_bytes < 2 ** 31
+
+
+def lds_conv_fits(cfg: int, cout: int) -> bool:
+    return cfg in LDS_CONV_CFGS and cout % LDS_TILES[cfg][1] == 0
+
+
 def lds_fits(cfg: int, cout: int) -> bool:
     """The last BN-wide feature tile stays inside the GEMM_ROW_PAD-padded weight rows."""
     bn = LDS_TILES[cfg][1]
@@ -173,6 +188,8 @@ def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv
     out = []
     if lds_ok(M, K, rowmajor, pc):
         out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout)]
+    elif not rowmajor and lds_conv_ok(M, pc):
+        out += [(cfg, 1) for cfg in LDS_CONV_CFGS if lds_conv_fits(cfg, cout)]
     for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue
@@ -194,8 +211,19 @@ def choose_config(M: int, cout: int, K: int, tuned: dict | None = None, key: str
     """
     if tuned is not None and key is not None and key in tuned:
         v = tuned[key]
-        if int(v[0]) not in LDS_TILES or (lds_ok(M, K, rowmajor, pc) and lds_fits(int(v[0]), cout)):
-            return int(v[0]), int(v[1])
+        c = int(v[0])
+        if (c not in LDS_TILES or (lds_ok(M, K, rowmajor, pc) and lds_fits(c, cout))
+                or (not rowmajor and lds_conv_ok(M, pc) and lds_conv_fits(c, cout))):
+            return c, int(v[1])
+    if not rowmajor and M >= LDS_CONV_MIN_M and K >= 256 and lds_conv_ok(M, pc):
+        # large-M conv (batched ResNet): the biggest LDS tile that still gives every CU a workgroup,
+        # 8-wave tiles first (the bs=32 tuner's winners, profiles/r2_conv_lds); K = 64 1x1 convs are
+        # store-bound and stay on the register-ring kernel
+        for cfg in (29, 32, 33, 31, 19):
+            bm, bn = LDS_TILES[cfg]
+            if lds_conv_fits(cfg, cout) and math.ceil(M / bm) * (cout // bn) >= NUM_CUS:
+                return cfg, 1
+        return 19, 1
     if lds_ok(M, K, rowmajor, pc) and M >= 512:
         # large-M GEMM: the biggest LDS tile that still gives every CU a workgroup
         for cfg in (16, 17, 18, 19):
@@ -269,7 +297,7 @@ def conv2d_nhwc(x: torch.Tensor, pc: PackedConv, residual: torch.Tensor | None =
     q_out = (w + 2 * pc.pad - pc.s) // pc.stride + 1
     M = n * p_out * q_out
     if cfg is None:
-        cfg, kw = choose_config(M, pc.cout, pc.K)
+        cfg, kw = choose_config(M, pc.cout, pc.K, pc=pc if is_blocked(pc.cin) else None)
     kw = kw or 1
     xb = to_blocked(x)
     oshape = (n, p_out, q_out, pc.cout)
