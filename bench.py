@@ -61,6 +61,12 @@ def parse():
                          "pipelined: replays queued back to back, no host work (device ceiling)")
     ap.add_argument("--compare-torch", action="store_true", help="also time PyTorch/MIOpen bf16 + CUDA graph")
     ap.add_argument("--no-capture", action="store_true")
+    ap.add_argument("--dyn-batch", type=int, default=8,
+                    help="secondary figure: the same bs=1 requests served with dynamic batching into replays "
+                         "of this batch (0: skip)")
+    ap.add_argument("--dyn-contexts", type=int, default=4)
+    ap.add_argument("--dyn-clients", type=int, default=32)
+    ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
                     help="replica: independent bs=1 request streams per GPU (headline); scatter: rank 0 scatters "
@@ -192,6 +198,39 @@ def torch_reference_throughput(model, device, iters=200):
     dt = time.perf_counter() - t
     del y
     return iters / dt
+
+
+def dynamic_batching(args, eng, device, world):
+    """Secondary serving figure (not the headline): the SAME bs=1 requests -- one uint8 image
+    each, ``--dyn-clients`` closed-loop native client threads -- served by the dynamic-batching
+    executor (csrc/executor.cpp) over ``--dyn-contexts`` contexts captured at ``--dyn-batch``
+    (batched convs on the LDS implicit GEMM). Whole-job inf/s = max wall over ranks."""
+    from hipzap.engine.engine import Engine
+    from hipzap.parallel.comm import is_dist, max_over_ranks
+    deng = Engine(args.model, eng.params, device, batch=args.dyn_batch, num_contexts=args.dyn_contexts,
+                  capture=not args.no_capture, arch_kw=eng.arch_kw, host_io=True,
+                  zero_copy=os.environ.get("HIPZAP_ZERO_COPY", "all"))
+    ex = deng.batched_executor(max_wait_us=args.dyn_wait_us)
+    h = eng.contexts[0].host_input
+    row = h.reshape(-1)[: ex.in_bytes[0] // h.element_size()].clone()
+    row.copy_((torch.rand(row.shape) * 255).to(row.dtype))
+    ex.bench(args.dyn_clients, max(1, args.warmup), [row.data_ptr()])
+    s0 = ex.stats()
+    if is_dist():
+        dist.barrier()
+    wall, lat = ex.bench(args.dyn_clients, args.steps, [row.data_ptr()])
+    wall = max_over_ranks(wall, device)
+    s1 = ex.stats()
+    lat = sorted(lat)
+    n = args.dyn_clients * args.steps
+    batches = s1["batches"] - s0["batches"]
+    out = {"inf_s": round(world * n / wall, 2), "request_batch": 1, "replay_batch": args.dyn_batch,
+           "contexts": args.dyn_contexts, "clients": args.dyn_clients, "max_wait_us": args.dyn_wait_us,
+           "mean_rows_per_replay": round((s1["served"] - s0["served"]) / max(1, batches), 2),
+           "latency_ms_p50": round(lat[len(lat) // 2], 4), "latency_ms_p99": round(lat[int(0.99 * (len(lat) - 1))], 4)}
+    ex.close()
+    del deng
+    return out
 
 
 def request_input(args, adapter):
@@ -366,6 +405,7 @@ def main():
     single = eng.contexts[0]
     from hipzap.engine.program import bench_contexts
     t_single = bench_contexts([single], [eng.streams[0]], 200)
+    dyn = dynamic_batching(args, eng, device, world) if args.dyn_batch > 1 and args.batch == 1 else None
     torch_ref = None
     if args.compare_torch and rank == 0:
         try:
@@ -411,6 +451,8 @@ def main():
             "baseline_note": "vs_baseline against BASELINE.md sandbox-CPU ResNet-50 bs=1 (27.2 inf/s); "
                              "no published numbers exist",
         }
+        if dyn is not None:
+            res["dynamic_batching"] = dyn
         if torch_ref is not None:
             res["torch_miopen_graph_inf_s_1gpu_1stream"] = round(torch_ref, 2)
         print(json.dumps(res), flush=True)

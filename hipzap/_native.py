@@ -152,6 +152,8 @@ def _load():
     _sig(lib, "hz_plan_capture_ctx", c_int, P, c_int)
     PP_ = C.POINTER(c_void_p)
     _sig(lib, "hz_exec_create", P, PP_, PP_, PP_, C.POINTER(U64), c_int, PP_, U64, c_int)
+    _sig(lib, "hz_exec_create_batched", P, PP_, PP_, PP_, C.POINTER(U64), c_int, PP_, U64, c_int, c_int, D, c_int)
+    _sig(lib, "hz_exec_batches", None, P, C.POINTER(U64))
     _sig(lib, "hz_exec_submit", c_int, P, PP_, P, C.POINTER(D))
     _sig(lib, "hz_exec_stats", None, P, C.POINTER(U64), C.POINTER(U64))
     _sig(lib, "hz_exec_destroy", None, P)

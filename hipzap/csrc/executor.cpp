@@ -12,6 +12,16 @@
 //                   slots' completion events, waking each request as its replay finishes
 // Host copies are spread over the request threads; submissions are serialised on one thread
 // (which is how the pipelined device ceiling was measured); request threads never spin.
+//
+// Dynamic batching (hz_exec_create_batched): the contexts are captured at batch B and every
+// request is still ONE image. Request threads claim a row of the single OPEN slot (opening a free
+// slot if none is open), copy their payload into that row of its pinned input and wait; the slot
+// is sealed when its B rows are claimed, or by the worker as soon as fewer than `min_inflight`
+// batches are on the GPU or the slot has been open `max_wait_us`. A sealed slot is launched once
+// its last claimed row has been copied; each request copies its own output row out and the
+// slot is freed when every claimed row has been read. Unclaimed rows of a partial batch hold stale
+// inputs whose outputs nobody reads. At batch 8-16 the conv layers run on the LDS-tiled implicit
+// GEMM (gemm.hip CV mode), so one batched replay costs far less than B single-image replays.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -41,6 +51,10 @@ struct Slot {
   bool done = false;
   int rc = 0;
   std::condition_variable cv;
+  // dynamic batching: rows claimed / payloads copied / outputs read; sealed = no more rows
+  int claimed = 0, copied = 0, read = 0;
+  bool sealed = false;
+  double t_open = 0;
 };
 
 struct Exec {
@@ -55,14 +69,37 @@ struct Exec {
   std::vector<int> inflight;  // worker-owned
   bool stop = false;
   std::thread worker;
-  uint64_t served = 0, polls = 0;
+  uint64_t served = 0, polls = 0, batches = 0;
+  // dynamic batching (rows > 1)
+  int rows = 1, open = -1, min_inflight = 1;
+  double max_wait_us = 0;
+  uint64_t row_in[kMaxIn] = {};
+  uint64_t row_out = 0;
 
   void complete(int s, int rc) {
     std::lock_guard<std::mutex> g(mu);
     slots[s].rc = rc;
     slots[s].done = true;
-    slots[s].cv.notify_one();
-    ++served;
+    slots[s].cv.notify_all();
+    served += rows == 1 ? 1 : slots[s].claimed;
+    ++batches;
+  }
+
+  // mu held: a sealed slot whose claimed rows are all copied goes to the launch queue
+  void queue_if_ready(int s) {
+    Slot& sl = slots[s];
+    if (sl.sealed && sl.copied == sl.claimed) {
+      to_launch.push_back(s);
+      cv_work.notify_one();
+    }
+  }
+
+  // mu held
+  void seal_open() {
+    const int s = open;
+    open = -1;
+    slots[s].sealed = true;
+    queue_if_ready(s);
   }
 
   void run() {
@@ -71,8 +108,11 @@ struct Exec {
       {
         std::unique_lock<std::mutex> lk(mu);
         if (to_launch.empty() && inflight.empty())
-          cv_work.wait(lk, [&] { return stop || !to_launch.empty(); });
-        if (stop && to_launch.empty() && inflight.empty()) return;
+          cv_work.wait(lk, [&] { return stop || !to_launch.empty() || open >= 0; });
+        if (stop && to_launch.empty() && inflight.empty() && open < 0) return;
+        // dynamic batching: close the filling batch when the GPU is short of work or it is old
+        if (open >= 0 && ((int)inflight.size() < min_inflight || stop || now_us() - slots[open].t_open >= max_wait_us))
+          seal_open();
         launch.assign(to_launch.begin(), to_launch.end());
         to_launch.clear();
       }
@@ -102,7 +142,56 @@ struct Exec {
     }
   }
 
+  int submit_batched(const void* const* in, void* out, double* lat_us) {
+    const double t0 = now_us();
+    int s, r;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      while (open < 0) {
+        if (stop) return -10;
+        if (!free_slots.empty()) {
+          s = free_slots.back();
+          free_slots.pop_back();
+          Slot& o = slots[s];
+          o.claimed = o.copied = o.read = 0;
+          o.sealed = o.done = false;
+          o.t_open = now_us();
+          open = s;
+          cv_work.notify_one();  // the worker decides when to seal
+          cv_free.notify_all();  // waiting requests may join this batch
+          break;
+        }
+        cv_free.wait(lk);
+      }
+      s = open;
+      r = slots[s].claimed++;
+      if (slots[s].claimed == rows) seal_open();
+    }
+    Slot& sl = slots[s];
+    for (int k = 0; k < n_in; ++k)
+      if (in && in[k] && row_in[k]) std::memcpy(static_cast<char*>(sl.in[k]) + r * row_in[k], in[k], row_in[k]);
+    int rc;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      ++sl.copied;
+      queue_if_ready(s);
+      sl.cv.wait(lk, [&] { return sl.done; });
+      rc = sl.rc;
+    }
+    if (!rc && out && row_out) std::memcpy(out, static_cast<const char*>(sl.out) + r * row_out, row_out);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (++sl.read == sl.claimed) {
+        free_slots.push_back(s);
+        cv_free.notify_all();
+      }
+    }
+    if (lat_us) *lat_us = now_us() - t0;
+    return rc;
+  }
+
   int submit_wait(const void* const* in, void* out, double* lat_us) {
+    if (rows > 1) return submit_batched(in, out, lat_us);
     const double t0 = now_us();
     int s;
     {
@@ -175,6 +264,33 @@ void* hz_exec_create(HzProgram* progs, hipStream_t* streams, void** host_in, con
   }
   e->worker = std::thread([e] { e->run(); });
   return e;
+}
+
+// Dynamic batching over contexts captured at batch `rows`: in_bytes / out_bytes are the whole
+// batch's; every request submits ONE row (in_bytes[k] / rows, out_bytes / rows).
+void* hz_exec_create_batched(HzProgram* progs, hipStream_t* streams, void** host_in, const uint64_t* in_bytes,
+                             int n_in, void** host_out, uint64_t out_bytes, int n, int rows, double max_wait_us,
+                             int min_inflight) {
+  if (rows < 1 || out_bytes % rows) return nullptr;
+  for (int k = 0; k < n_in; ++k)
+    if (in_bytes[k] % rows) return nullptr;
+  auto* e = static_cast<Exec*>(hz_exec_create(progs, streams, host_in, in_bytes, n_in, host_out, out_bytes, n));
+  if (!e) return nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->mu);
+    e->rows = rows;
+    e->max_wait_us = max_wait_us;
+    e->min_inflight = min_inflight;
+    for (int k = 0; k < n_in; ++k) e->row_in[k] = in_bytes[k] / rows;
+    e->row_out = out_bytes / rows;
+  }
+  return e;
+}
+
+void hz_exec_batches(void* h, uint64_t* batches) {
+  Exec* e = static_cast<Exec*>(h);
+  std::lock_guard<std::mutex> g(e->mu);
+  *batches = e->batches;
 }
 
 int hz_exec_submit(void* h, const void* const* in, void* out, double* lat_us) {

@@ -346,6 +346,10 @@ int hz_plan_capture_ctx(void* plan, int ctx);
 void* hz_exec_create(HzProgram* progs, hipStream_t* streams, void** host_in, const uint64_t* in_bytes, int n_in,
                      void** host_out, uint64_t out_bytes, int n);
 // blocking: one request (in[k] = payload of input k), result copied to out; latency in *lat_us
+void* hz_exec_create_batched(HzProgram* progs, hipStream_t* streams, void** host_in, const uint64_t* in_bytes,
+                             int n_in, void** host_out, uint64_t out_bytes, int n, int rows, double max_wait_us,
+                             int min_inflight);
+void hz_exec_batches(void* exec, uint64_t* batches);
 int hz_exec_submit(void* exec, const void* const* in, void* out, double* lat_us);
 void hz_exec_stats(void* exec, uint64_t* served, uint64_t* polls);
 void hz_exec_destroy(void* exec);

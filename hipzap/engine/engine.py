@@ -297,6 +297,23 @@ class Engine:
         self.ensure_contexts()
         return bench_contexts(self.contexts, self.streams, iters)
 
+    def batched_executor(self, max_wait_us: float = 200.0, min_inflight: int = 1):
+        """Dynamic-batching request executor over this engine's contexts (captured at
+        ``self.batch``): each request is ONE image; concurrent requests share a replay."""
+        from ..executor import Executor
+        self.ensure_contexts()
+        with self._build_lock:
+            if getattr(self, "_bexec", None) is None:
+                cs = self.contexts
+                self._bexec = Executor(
+                    [c.prog for c in cs], [s.cuda_stream for s in self.streams],
+                    [[c.host_inputs[k].data_ptr() for c in cs] for k in range(len(cs[0].host_inputs))],
+                    [h.numel() * h.element_size() for h in cs[0].host_inputs],
+                    [c.host_output.data_ptr() for c in cs],
+                    cs[0].host_output.numel() * cs[0].host_output.element_size(),
+                    rows=self.batch, max_wait_us=max_wait_us, min_inflight=min_inflight)
+        return self._bexec
+
     def serve_bench(self, iters: int, payload=None, clients: int | None = None,
                     mode: str = "executor") -> tuple[float, list]:
         """Closed-loop serving benchmark: ``clients`` (default: one per context) native client

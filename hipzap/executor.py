@@ -14,17 +14,28 @@ from . import _native as N
 
 
 class Executor:
-    def __init__(self, progs: list, streams: list, host_in: list, in_bytes: list, host_out: list, out_bytes: int):
-        """``host_in[k][i]``: address of context i's pinned input k; ``host_out[i]``: its output."""
+    def __init__(self, progs: list, streams: list, host_in: list, in_bytes: list, host_out: list, out_bytes: int,
+                 rows: int = 1, max_wait_us: float = 200.0, min_inflight: int = 1):
+        """``host_in[k][i]``: address of context i's pinned input k; ``host_out[i]``: its output.
+
+        ``rows > 1``: dynamic batching -- the contexts are captured at batch ``rows`` and every
+        request is ONE row (``in_bytes[k] / rows`` in, ``out_bytes / rows`` out); a filling batch
+        is launched when full, when fewer than ``min_inflight`` batches are on the GPU, or after
+        ``max_wait_us`` (csrc/executor.cpp)."""
         n, n_in = len(progs), len(in_bytes)
         assert n > 0 and all(len(h) == n for h in host_in) and len(host_out) == n and 0 < n_in <= 4
         V = C.c_void_p
         flat_in = [a for k in range(n_in) for a in host_in[k]]
         self._keep = ((V * n)(*progs), (V * n)(*streams), (V * (n * n_in))(*flat_in),
                       (C.c_uint64 * n_in)(*in_bytes), (V * n)(*host_out))
-        self.n, self.n_in, self.out_bytes, self.in_bytes = n, n_in, out_bytes, list(in_bytes)
-        h = N.lib().hz_exec_create(self._keep[0], self._keep[1], self._keep[2], self._keep[3], n_in, self._keep[4],
-                                   out_bytes, n)
+        self.n, self.n_in, self.rows = n, n_in, rows
+        self.out_bytes, self.in_bytes = out_bytes // rows, [b // rows for b in in_bytes]  # per request
+        if rows > 1:
+            h = N.lib().hz_exec_create_batched(self._keep[0], self._keep[1], self._keep[2], self._keep[3], n_in,
+                                               self._keep[4], out_bytes, n, rows, float(max_wait_us), min_inflight)
+        else:
+            h = N.lib().hz_exec_create(self._keep[0], self._keep[1], self._keep[2], self._keep[3], n_in,
+                                       self._keep[4], out_bytes, n)
         if not h:
             raise RuntimeError("hz_exec_create failed")
         self._h = h
@@ -53,7 +64,10 @@ class Executor:
     def stats(self) -> dict:
         s, p = C.c_uint64(), C.c_uint64()
         N.lib().hz_exec_stats(self._h, C.byref(s), C.byref(p))
-        return {"served": s.value, "polls": p.value}
+        b = C.c_uint64()
+        N.lib().hz_exec_batches(self._h, C.byref(b))
+        return {"served": s.value, "polls": p.value, "batches": b.value,
+                "mean_batch": round(s.value / b.value, 3) if b.value else None}
 
     def close(self) -> None:
         h, self._h = getattr(self, "_h", None), None

@@ -33,7 +33,7 @@ def test_lds_conv_every_tile(cfg):
 def test_lds_conv_heuristic_large_m():
     """Batched ResNet layer1 shapes: the heuristic routes M >= LDS_CONV_MIN_M to the LDS tile."""
     for n, cin, h, cout, k, stride, pad in [(4, 64, 56, 64, 3, 1, 1), (2, 256, 56, 128, 1, 1, 0),
-                                            (2, 512, 28, 256, 1, 1, 0)]:
+                                            (8, 512, 28, 256, 1, 1, 0)]:
         pc = C.pack_conv(torch.randn(cout, cin, k, k), None, None, stride, pad)
         M = n * h * h
         assert C.choose_config(M, cout, pc.K, pc=pc)[0] in C.LDS_CONV_CFGS
