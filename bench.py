@@ -64,8 +64,8 @@ def parse():
     ap.add_argument("--dyn-batch", type=int, default=8,
                     help="secondary figure: the same bs=1 requests served with dynamic batching into replays "
                          "of this batch (0: skip)")
-    ap.add_argument("--dyn-contexts", type=int, default=4)
-    ap.add_argument("--dyn-clients", type=int, default=32)
+    ap.add_argument("--dyn-contexts", type=int, default=8)
+    ap.add_argument("--dyn-clients", type=int, default=64)
     ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
