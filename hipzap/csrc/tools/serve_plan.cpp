@@ -1,6 +1,7 @@
 // hipzap-serve-plan: a Python-free serving process for a vision plan image (.hzplan).
 //
-//   hipzap-serve-plan PLAN [--port 8080] [--host 127.0.0.1] [--contexts 24] [--device 0]
+//   hipzap-serve-plan PLAN [--port 8080] [--host 127.0.0.1] [--contexts 24] [--device 0] [--max-wait-us 200]
+//   (a plan exported with --batch B > 1 is served with dynamic batching: each POST is one image)
 //   hipzap-serve-plan PLAN --once IMAGE.raw      (cold-start probe: one request, JSON to stdout)
 //
 // The same native pieces the Python server composes (csrc/plan.cpp loader, csrc/executor.cpp
@@ -48,6 +49,7 @@ bool num_after(const std::string& js, size_t from, const char* key, long long& o
 
 struct Spec {
   long long in_off = 0, in_bytes = 0, out_off = 0, out_bytes = 0, classes = 0, H = 0, W = 0, C = 0;
+  long long rows = 1;  // plan batch: > 1 -> dynamic batching of one-image requests
   int probs = 0;
   std::string model;
   bool host_io = false;
@@ -75,10 +77,10 @@ bool read_spec(const char* path, Spec& s) {
   if (sh == std::string::npos || sh > oi) return false;
   long long d[4] = {0, 0, 0, 0};
   if (std::sscanf(js.c_str() + sh + 10, "%lld, %lld, %lld, %lld", &d[0], &d[1], &d[2], &d[3]) != 4) return false;
-  s.H = d[1], s.W = d[2], s.C = d[3];  // uint8 request [1][H][W][C]
+  s.rows = d[0], s.H = d[1], s.W = d[2], s.C = d[3];  // uint8 input [B][H][W][C], one image per request
   if (!num_after(js, oi, "off", s.out_off) || !num_after(js, oi, "bytes", s.out_bytes)) return false;
-  if (!num_after(js, oi, "num_labels", s.classes) || s.classes <= 0) s.classes = s.out_bytes / 4;  // null
-  return d[0] == 1 && s.in_bytes == d[1] * d[2] * d[3];
+  if (!num_after(js, oi, "num_labels", s.classes) || s.classes <= 0) s.classes = s.out_bytes / 4 / (d[0] > 0 ? d[0] : 1);
+  return d[0] >= 1 && s.in_bytes == d[0] * d[1] * d[2] * d[3] && s.out_bytes % d[0] == 0;
 }
 
 void fallback(void* req, const char* method, const char* target, const char*, uint64_t, const char*, uint64_t);
@@ -107,11 +109,12 @@ int die(const char* what) {
 int main(int argc, char** argv) {
   const double t0 = now_ms();
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s PLAN [--port P] [--host H] [--contexts N] [--device D] [--once IMAGE]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s PLAN [--port P] [--host H] [--contexts N] [--device D] [--max-wait-us U] [--once IMAGE]\n", argv[0]);
     return 2;
   }
   const char* plan_path = argv[1];
   int port = 8080, contexts = 24, device = 0;
+  double max_wait_us = 200.0;
   std::string host = "127.0.0.1";
   const char* once = nullptr;
   for (int i = 2; i + 1 < argc; i += 2) {
@@ -120,6 +123,7 @@ int main(int argc, char** argv) {
     else if (a == "--host") host = argv[i + 1];
     else if (a == "--contexts") contexts = std::atoi(argv[i + 1]);
     else if (a == "--device") device = std::atoi(argv[i + 1]);
+    else if (a == "--max-wait-us") max_wait_us = std::atof(argv[i + 1]);
     else if (a == "--once") once = argv[i + 1];
   }
   Spec sp;
@@ -171,8 +175,11 @@ int main(int argc, char** argv) {
     outs[i] = static_cast<char*>(hz_plan_host(plan, i)) + sp.out_off;
   }
   const uint64_t in_bytes = (uint64_t)sp.in_bytes;
-  void* ex = hz_exec_create(progs.data(), streams.data(), ins.data(), &in_bytes, 1, outs.data(),
-                            (uint64_t)sp.out_bytes, contexts);
+  // a batch-B plan serves one-image requests with dynamic batching (csrc/executor.cpp)
+  void* ex = sp.rows > 1 ? hz_exec_create_batched(progs.data(), streams.data(), ins.data(), &in_bytes, 1, outs.data(),
+                                                  (uint64_t)sp.out_bytes, contexts, (int)sp.rows, max_wait_us, 1)
+                         : hz_exec_create(progs.data(), streams.data(), ins.data(), &in_bytes, 1, outs.data(),
+                                          (uint64_t)sp.out_bytes, contexts);
   if (!ex) return die("executor");
 
   const int fd = socket(AF_INET, SOCK_STREAM, 0);
@@ -195,7 +202,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "hipzap-serve-plan: HTTP server start failed\n");
     return 1;
   }
-  if (hz_http_set_fast(srv, ex, (int)sp.H, (int)sp.W, (int)sp.C, (int)(sp.out_bytes / 4), (int)sp.classes, sp.probs,
+  if (hz_http_set_fast(srv, ex, (int)sp.H, (int)sp.W, (int)sp.C, (int)(sp.out_bytes / sp.rows / 4), (int)sp.classes, sp.probs,
                        sp.model.c_str())) {
     std::fprintf(stderr, "hipzap-serve-plan: fast route rejected (image %lldx%lldx%lld, %lld classes, %lld output bytes)\n",
                  sp.H, sp.W, sp.C, sp.classes, sp.out_bytes);

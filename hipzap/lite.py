@@ -201,6 +201,28 @@ class PlanEngine:
                         lk.release()
         return self._exec
 
+    def batched_executor(self, max_wait_us: float = 200.0, min_inflight: int = 1):
+        """Dynamic-batching executor (csrc/executor.cpp) over every context of a batch-B plan: each
+        request is ONE row (one image); concurrent requests share a replay. Built once the
+        contexts exist and are captured (else None)."""
+        ex = getattr(self, "_bexec", None)
+        if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts \
+                or self._uncaptured:
+            return ex
+        from .executor import Executor
+        with self._build_lock:
+            if getattr(self, "_bexec", None) is None:
+                L, n = lib(), len(self._locks)
+                hosts = [L.hz_plan_host(self._h, i) for i in range(n)]
+                self._bexec = Executor([L.hz_plan_prog(self._h, i) for i in range(n)],
+                                       [L.hz_plan_stream(self._h, i) for i in range(n)],
+                                       [[h + sp["off"] for h in hosts] for sp in self.in_specs],
+                                       [sp["bytes"] for sp in self.in_specs],
+                                       [h + self.out_spec["off"] for h in hosts], self.out_spec["bytes"],
+                                       rows=int(self.in_specs[0]["shape"][0]), max_wait_us=max_wait_us,
+                                       min_inflight=min_inflight)
+        return self._bexec
+
     def _pick(self) -> int:
         with self._rr_lock:
             i = self._rr % len(self._locks)

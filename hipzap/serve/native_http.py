@@ -74,15 +74,16 @@ class NativeHTTPServer:
     def set_fast(self, backend) -> None:
         eng = backend.engine
         eng.ensure_contexts()
-        ex = eng.executor()
+        b, h, w, c = backend.in_shape
+        # a batch-B plan is served with dynamic batching: each POST is one row of a shared replay
+        ex = eng.executor() if b == 1 else eng.batched_executor(getattr(backend, "max_wait_us", 200.0))
         if ex is None:
             raise RuntimeError("plan engine has no executor (capture disabled?)")
         self._exec = ex  # keep alive
-        b, h, w, c = backend.in_shape
         out = eng.out_spec
-        rc = N.lib().hz_http_set_fast(self._h, ex._h, h, w, c, out["bytes"] // 4, int(backend.num_labels),
+        rc = N.lib().hz_http_set_fast(self._h, ex._h, h, w, c, out["bytes"] // b // 4, int(backend.num_labels),
                                       int(backend.probs), backend.name.encode())
-        if rc or b != 1:
+        if rc:
             raise RuntimeError(f"native /predict route rejected (rc={rc}, plan batch {b})")
         self.fast_model = backend.name
 

@@ -367,6 +367,8 @@ class PlanVisionBackend:
         self.batch = self.in_shape[0]
         self.probs = bool(self.meta.get("probs"))
         self.num_labels = self.meta["output"].get("num_labels") or self.meta["output"]["shape"][-1]
+        # batch-B plan behind the native /predict route: dynamic batching, "batching": {"max_wait_ms"}
+        self.max_wait_us = float((spec.extra.get("batching") or {}).get("max_wait_ms", 0.2)) * 1e3
         self._torch, self._torch_lock = None, threading.Lock()
         self.cold_ms = (time.perf_counter() - t0) * 1e3
         # the other request contexts are built right after the engine is ready (warm scale-up)

@@ -144,3 +144,45 @@ def test_native_http_fast_route_matches_flask_route(plan_server):
     finally:
         hs.stop()
         sock.close()
+
+
+def test_native_http_dynamic_batching_batch_plan(plan_server):
+    """A batch-4 plan behind the native POST /predict: concurrent one-image requests share
+    replays (dynamic batching executor) and every client gets its own image's answer."""
+    import http.client
+    from hipzap.serve.native_http import NativeHTTPServer, listening_socket
+    c, srv, plan1, ckpt = plan_server
+    plan4 = export_from_checkpoint("resnet50", ckpt, path=ckpt + ".b4.hzplan", batch=4, contexts=2)
+    be = PlanVisionBackend("resnet50", plan4, 0, ModelSpec(name="resnet50", contexts=2,
+                                                            extra={"plan": plan4, "batching": {"max_wait_ms": 0.5}}))
+    ref_eng = PlanEngine(plan1, device=0)
+    imgs = [_img(100 + i) for i in range(16)]
+    refs = [np.frombuffer(ref_eng.infer_raw(im[None]), np.float32) for im in imgs]
+    sock = listening_socket("127.0.0.1", 0)
+    hs = NativeHTTPServer(app_mod.app, sock, fast=be)
+    bad = []
+    try:
+        port = sock.getsockname()[1]
+
+        def client(k):
+            conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+            for i in range(k, len(imgs), 8):
+                body = json.dumps({"image_b64": base64.b64encode(imgs[i].tobytes()).decode(), "shape": [224, 224, 3]})
+                conn.request("POST", "/predict", body=body, headers={"Content-Type": "application/json"})
+                r = conn.getresponse()
+                out = json.loads(r.read())
+                if r.status != 200 or r.getheader("X-Hipzap-Path") != "native" or \
+                        out["top5"][0][0][0] != int(refs[i].argmax()):
+                    bad.append((i, r.status, out.get("top5", [[None]])[0][:1], int(refs[i].argmax())))
+
+        th = [threading.Thread(target=client, args=(k,)) for k in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not bad, bad
+        st = be.engine.batched_executor().stats()
+        assert st["served"] == 16 and st["batches"] <= 16, st
+    finally:
+        hs.stop()
+        sock.close()
