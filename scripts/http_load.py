@@ -106,20 +106,28 @@ def main():
     ap.add_argument("--server-log", default=None, help="copy the server log here")
     ap.add_argument("--native", action="store_true",
                     help="serve with the Python-free hipzap-serve-plan binary instead of python -m hipzap serve")
+    ap.add_argument("--plan-batch", type=int, default=1,
+                    help="serve a batch-B plan: one-image requests dynamically batched into B-row replays")
+    ap.add_argument("--max-wait-ms", type=float, default=0.2)
     a = ap.parse_args()
     from bench import prepare_artifacts
     ckpt, plan = prepare_artifacts("resnet50", "/tmp/hipzap_bench")
+    if a.plan_batch > 1:
+        from hipzap.engine.plan import export_from_checkpoint
+        plan = export_from_checkpoint("resnet50", ckpt, path=f"{ckpt}.b{a.plan_batch}.hzplan", batch=a.plan_batch,
+                                      contexts=a.contexts)
     d = tempfile.mkdtemp(prefix="hz_http_")
     settings = os.path.join(d, "zappa_settings.json")
     with open(settings, "w") as f:
         json.dump({"dev": {"hipzap": {"default_model": "resnet50", "models": {
-            "resnet50": {"contexts": a.contexts, "extra": {"plan": plan}}}}}}, f)
+            "resnet50": {"contexts": a.contexts, "extra": {"plan": plan, "batching": {"max_wait_ms": a.max_wait_ms}}}}}}},
+                  f)
     cmd = [sys.executable, "-m", "hipzap", "serve", "--settings", settings, "--port", str(a.port)]
     if a.gpus > 1:
         cmd += ["--gpus", str(a.gpus)]
     if a.native:
         cmd = [os.path.join(ROOT, "hipzap", "_lib", "hipzap-serve-plan"), plan, "--port", str(a.port),
-               "--contexts", str(a.contexts)]
+               "--contexts", str(a.contexts), "--max-wait-us", str(a.max_wait_ms * 1e3)]
     env = dict(os.environ, HIPZAP_WATCHDOG="0")
     log_path = os.path.join(d, "server.log")
     log_f = open(log_path, "w")  # never a pipe: the access log would fill it and block the server
@@ -164,7 +172,7 @@ def main():
     lat = sorted(x for r in res for x in r[0])
     errors = sum(r[1] for r in res)
     print(json.dumps({
-        "server": "hipzap-serve-plan" if a.native else "python -m hipzap serve",
+        "server": "hipzap-serve-plan" if a.native else "python -m hipzap serve", "plan_batch": a.plan_batch,
         "gpus": a.gpus, "clients": a.clients, "requests": len(lat), "format": a.format, "errors": errors,
         "req_per_s": round(len(lat) / wall, 1), "p50_ms": round(statistics.median(lat), 3),
         "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3), "max_ms": round(lat[-1], 3),
