@@ -246,19 +246,24 @@ __device__ __forceinline__ void wait_vm8() {
 // the scale goes to the MFMA's B-scale operand: lane l supplies token l&15's scale of 32-k block
 // l>>4 (the hardware K order above: block b lives in the register halves of lane groups
 // 2(b&1)..2(b&1)+1, not in lane group b).
-template <int BM, int BN, int NS, bool XS>
-__global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, int group_m) {
-  constexpr int FCW = BN / 32, FPW = BM / 32;
+// WM x WN waves (4 or 8; 8 = two waves per SIMD at one workgroup per CU, whose ds_reads and
+// MFMAs interleave): wave (wm, wn) owns rows wm*BM/WM.. and features wn*BN/WN..
+template <int BM, int BN, int NS, bool XS, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Params p, int group_m) {
+  constexpr int NW = WM * WN;
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;
   constexpr int NWG = BN / 16;                // weight fragments (2 KiB) per stage
   constexpr int XBYTES = BM * 128;
   constexpr int WBYTES = NWG * 2048;
-  constexpr int SBYTES = XBYTES + WBYTES + (XS ? 1024 : 0);
-  constexpr int XPW = BM / 32, WPW = NWG * 2 / 4;  // glds pieces per wave per stage
+  constexpr int SBYTES = XBYTES + WBYTES + (XS ? NW * 256 : 0);
+  constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;  // glds pieces per wave per stage
+  static_assert(XPW * 8 * NW == BM && WPW * NW == NWG * 2 && FCW % 2 == 0 && FPW >= 1 && BM / 64 <= NW,
+                "tile / wave split");
   constexpr int G = XPW + WPW + (XS ? 1 : 0);
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave & 1, wm = wave >> 1;
+  const int wn = wave % WN, wm = wave / WN;
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   int tile_m, tile_n;
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
   const unsigned char* xsrc[XPW];
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
-    const int q = wave + 4 * i;
+    const int q = wave + NW * i;
     const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
     const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
     xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
@@ -282,17 +287,17 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
     if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
 #pragma unroll
     for (int i = 0; i < XPW; ++i)
-      glds16_8(xsrc[i] + st * 128, base + (wave + 4 * i) * 1024);
+      glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
-      const int piece = wave + 4 * i;  // = g * 2 + half
+      const int piece = wave + NW * i;  // = g * 2 + half
       const int g = piece >> 1, h = piece & 1;
       glds16_8(wsrc + ((long)g * kb + st) * 2048 + h * 1024, base + XBYTES + piece * 1024);
     }
   };
 
   const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
-  const int brow = (wm * (BM / 2) + lr) * 128;
+  const int brow = (wm * (BM / WM) + lr) * 128;
   // hardware K order of the f8f6f4 MFMA (what the E8M0 block scales index): lane group g holds
   // k = 16g..16g+15 in its low 16 B and 64+16g.. in its high 16 B
   const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
 #pragma unroll
     for (int j = 0; j < FPW; ++j) {
       if constexpr (XS) {
-        const int r = wm * (BM / 2) + j * 16 + (lane & 15);
+        const int r = wm * (BM / WM) + j * 16 + (lane & 15);
         sb[j] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
                                                         (lane >> 4));
       } else {
@@ -353,7 +358,7 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
   if (p.out8) {  // MX8 output: per (row, 32-column block) E8M0 scale; no early exits (shuffles)
 #pragma unroll
     for (int j = 0; j < FPW; ++j) {
-      const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
+      const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
       const bool mv = m < p.M;
       const float sx = p.sx ? p.sx[min(m, p.M - 1)] : 1.f;
 #pragma unroll
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
         float amax = 0.f;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int n = min(n0 + wn * (BN / 2) + (i + h) * 16 + (lane >> 4) * 4, p.N - 4);
+          const int n = min(n0 + wn * (BN / WN) + (i + h) * 16 + (lane >> 4) * 4, p.N - 4);
           const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
           const f32x4 bb = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -380,14 +385,14 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
         const int ex = mx_exp(amax);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int n = n0 + wn * (BN / 2) + (i + h) * 16 + (lane >> 4) * 4;
+          const int n = n0 + wn * (BN / WN) + (i + h) * 16 + (lane >> 4) * 4;
           float q[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) q[e] = fminf(fmaxf(ldexpf(v[h][e], -ex), -448.f), 448.f);
           if (mv && n < p.N)
             *reinterpret_cast<unsigned*>(p.out8 + (long)m * p.ldo + n) = pack4_fp8(q[0], q[1], q[2], q[3]);
         }
-        const int nb = n0 + wn * (BN / 2) + i * 16;
+        const int nb = n0 + wn * (BN / WN) + i * 16;
         if (mv && (lane >> 4) == 0 && nb < p.N) p.os8[(long)m * (p.ldo >> 5) + (nb >> 5)] = (unsigned char)(ex + 127);
       }
     }
@@ -395,12 +400,12 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
   }
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
-    const int m = m0 + wm * (BM / 2) + j * 16 + lrow;
+    const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
     if (m >= p.M) continue;
     const float sx = p.sx ? p.sx[m] : 1.f;
 #pragma unroll
     for (int i = 0; i < FCW; ++i) {
-      const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      const int n = n0 + wn * (BN / WN) + i * 16 + (lane >> 4) * 4;
       if (n >= p.N) continue;
       const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
       float v[4];
@@ -435,13 +440,16 @@ __global__ __launch_bounds__(256) void gemm_mx_kernel(const HzGemmFp8Params p, i
   }
 }
 
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, int WM = 2, int WN = 2>
 int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
+  // the 8-wave tiles read BN weight rows per tile: N must fill them (the 4-wave tiles predate this)
+  if (WM * WN > 4 && p.N % BN) return -4;
   const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
   const int group_m = group_env < 1 ? 1 : group_env;
-  if (p.xs) hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, true>), dim3(tiles), dim3(256), 0, st, p, group_m);
-  else hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, false>), dim3(tiles), dim3(256), 0, st, p, group_m);
+  const dim3 block(64 * WM * WN);
+  if (p.xs) hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, true, WM, WN>), dim3(tiles), block, 0, st, p, group_m);
+  else hipLaunchKernelGGL((gemm_mx_kernel<BM, BN, NS, false, WM, WN>), dim3(tiles), block, 0, st, p, group_m);
   return (int)hipGetLastError();
 }
 
@@ -462,6 +470,13 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 22: return launch_mx<128, 64, 2>(p, st);
       case 19: return launch_mx<64, 64, 3>(p, st);
       case 23: return launch_mx<64, 64, 2>(p, st);
+      // 8-wave workgroups (two waves per SIMD): 128x128, 256x128, 128x256 at 2 / 3 LDS stages
+      case 24: return launch_mx<128, 128, 2, 2, 4>(p, st);
+      case 25: return launch_mx<256, 128, 2, 4, 2>(p, st);
+      case 26: return launch_mx<128, 256, 2, 2, 4>(p, st);
+      case 27: return launch_mx<128, 128, 3, 2, 4>(p, st);
+      case 28: return launch_mx<256, 128, 3, 4, 2>(p, st);
+      case 29: return launch_mx<128, 256, 3, 2, 4>(p, st);
       default: return -2;
     }
   }

@@ -97,7 +97,14 @@ def quantize_linear(pc: PackedConv) -> PackedFp8:
 
 # cfg -> (BM, BN), csrc/fp8.hip gemm_mx_kernel; 16-19: 3 LDS stages, 20-23: 2 stages
 MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
-            20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64)}
+            20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64),
+            # 24-29: 8-wave workgroups (2 / 3 stages); N must be a multiple of BN
+            24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256)}
+MX_WIDE = (24, 25, 26, 27, 28, 29)
+
+
+def mx_fits(cfg: int, n: int) -> bool:
+    return cfg not in MX_WIDE or n % MX_TILES[cfg][1] == 0
 
 
 def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
@@ -106,7 +113,7 @@ def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
 
 def candidates_fp8(M: int, pw: PackedFp8, mx_io: bool = False) -> list:
     from .conv import candidates
-    out = [(cfg, 1) for cfg in MX_TILES] if mx_ok(M, pw) else []
+    out = [(cfg, 1) for cfg in MX_TILES if mx_fits(cfg, pw.cout)] if mx_ok(M, pw) else []
     return out if mx_io else out + candidates(M, pw.cout, pw.K)
 
 
@@ -114,7 +121,7 @@ def choose_config_fp8(M: int, pw: PackedFp8, tuned: dict | None = None, key: str
     """``mx_io``: MX8 input or output -> only the MX LDS kernel can run it."""
     if tuned is not None and key is not None and key in tuned:
         cfg, kw = int(tuned[key][0]), int(tuned[key][1])
-        if (cfg not in MX_TILES and not mx_io) or (cfg in MX_TILES and mx_ok(M, pw)):
+        if (cfg not in MX_TILES and not mx_io) or (cfg in MX_TILES and mx_ok(M, pw) and mx_fits(cfg, pw.cout)):
             return cfg, kw
     if mx_ok(M, pw) and (M >= 512 or mx_io):
         for cfg in (16, 17, 18, 19):
