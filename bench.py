@@ -429,7 +429,12 @@ def main():
                        ("torch.distributed" if world > 1 else None)},
             "cold_start_ms_p50": fresh["plan"]["p50_ms"] if fresh else None,
             "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
-                               "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict",
+                               "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict; "
+                               "each child sees only its own GPU (ROCR_VISIBLE_DEVICES, a one-GPU worker) unless "
+                               "the launcher already restricts visibility",
+            "cold_start_isolated": not any(os.environ.get(k) for k in
+                                           ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                            "GPU_DEVICE_ORDINAL")) and os.environ.get("HIPZAP_COLD_ISOLATE", "1") != "0",
             "cold_start_pth_ms_p50": fresh["pth"]["p50_ms"] if fresh else None,
             # the Python-free server binary (hipzap-serve-plan --once) on the same plan image
             "cold_start_native_ms_p50": (fresh.get("native") or {}).get("p50_ms") if fresh else None,

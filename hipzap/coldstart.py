@@ -64,6 +64,21 @@ def run_torch(ckpt: str, model: str, device: int, packed: bool) -> dict:
                           "engine_total": (t_ready - t_lib) * 1e3, "first_request": (t_first - t_ready) * 1e3}}
 
 
+_VIS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+
+def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:
+    """A serverless worker owns ONE GPU (a one-GPU container): the cold-start child sees only
+    ``device`` (``ROCR_VISIBLE_DEVICES``), so HIP init enumerates one agent, not every GPU of the
+    node, and uses it as device 0. Left alone when the parent already restricts visibility (its
+    indices would not be physical ones) or ``HIPZAP_COLD_ISOLATE=0``."""
+    base = dict(os.environ if env is None else env)
+    if base.get("HIPZAP_COLD_ISOLATE", "1") == "0" or any(base.get(k) for k in _VIS):
+        return env, device
+    base["ROCR_VISIBLE_DEVICES"] = str(device)
+    return base, 0
+
+
 def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5, device: int = 0,
                   timeout: float = 300.0, env: dict | None = None) -> dict:
     """Spawn ``trials`` fresh processes of this module; p50/min/max of spawn -> first logits and
@@ -72,6 +87,7 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     walls, res = [], []
+    env, device = isolated_env(env, device)
     if mode == "native":
         import tempfile
         from hipzap.lite import read_meta
