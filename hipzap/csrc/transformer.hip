@@ -411,7 +411,12 @@ extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) 
   const size_t lds = (size_t)Lp * (ATT_KST + ATT_VST) * sizeof(bf16_t) + (size_t)Lp * sizeof(float);
   // 8 waves (128 queries) per workgroup for long sequences: K/V staged half as often
   static const int nw8_minl = getenv("HIPZAP_ATT_NW8_MINL") ? atoi(getenv("HIPZAP_ATT_NW8_MINL")) : HZ_ATT_NW8_MINL;
-  if (p.L > nw8_minl) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
+  // HIPZAP_ATT_NW16=1: 16 waves (256 queries) for L > 128, one workgroup per (batch, head) staging
+  // K/V once instead of once per 128-query block. Same-box A/B on ViT (L = 197): bs64 fp8 +0.4 %,
+  // bs8 -2 % (profiles/r2_att16) -> off by default
+  static const bool nw16 = getenv("HIPZAP_ATT_NW16") && atoi(getenv("HIPZAP_ATT_NW16")) != 0;
+  if (nw16 && p.L > 128) hipLaunchKernelGGL(attention_kernel<16>, dim3(p.B * p.heads, 1), dim3(1024), lds, st, p);
+  else if (p.L > nw8_minl) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
   else hipLaunchKernelGGL(attention_kernel<4>, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
   return (int)hipGetLastError();
 }
