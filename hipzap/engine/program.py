@@ -288,11 +288,14 @@ class ExecContext:
             npar = self.params[n.attrs["p"]]
             res = n.inputs[1] if len(n.inputs) > 1 else None
             D = g.shape(n.outputs[0])[-1]
-            q8 = g.tensors[n.outputs[0]].dtype == torch.uint8  # fused fp8 quantisation: outputs (x8, scales)
-            prm = tx.LayerNormParams(addr(n.inputs[0]), addr(res), 0 if q8 else addr(n.outputs[0]),
+            # fused fp8 quantisation: outputs (x8, scales), or (bf16, x8, scales) when both are kept
+            outs = list(n.outputs)
+            bf = outs.pop(0) if g.tensors[outs[0]].dtype != torch.uint8 else None
+            q8 = len(outs) == 2
+            prm = tx.LayerNormParams(addr(n.inputs[0]), addr(res), addr(bf) if bf is not None else 0,
                                      npar.gamma.data_ptr(), npar.beta.data_ptr(), n.attrs["rows"], D,
-                                     n.attrs.get("ldx") or D, D, D, npar.eps, addr(n.outputs[0]) if q8 else 0,
-                                     addr(n.outputs[1]) if q8 else 0)
+                                     n.attrs.get("ldx") or D, D, D, npar.eps, addr(outs[0]) if q8 else 0,
+                                     addr(outs[1]) if q8 else 0)
             tx.prog_add(self.prog, tx.K_LAYERNORM, prm, n.slot, lib=lib)
         elif n.kind == "attention":
             a = n.attrs

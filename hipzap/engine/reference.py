@@ -123,12 +123,13 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             if len(n.inputs) > 1:
                 xm = xm + vals[n.inputs[1]].float().reshape(rows, D)
             y = F.layer_norm(xm, (D,), npar.gamma.float(), npar.beta.float(), npar.eps)
-            if g.tensors[n.outputs[0]].dtype == torch.uint8:  # fused fp8 quantisation
+            outs = list(n.outputs)
+            if g.tensors[outs[0]].dtype != torch.uint8:
+                store(outs.pop(0), y)
+            if outs:  # fused fp8 quantisation
                 from ..ops.fp8 import quant_rows_ref
                 deq, s = quant_rows_ref(y.to(torch.bfloat16))
-                vals[n.outputs[0]], vals[n.outputs[1]] = deq, s
-            else:
-                store(n.outputs[0], y)
+                vals[outs[0]], vals[outs[1]] = deq, s
         elif k == "attention":
             a = n.attrs
             mask = vals[n.inputs[1]] if len(n.inputs) > 1 else None

@@ -90,13 +90,18 @@ class TxBuilder:
         g.add("layernorm", ins, [out], p=p, rows=r, ldx=ldx)
         return out
 
-    def layernorm_q8(self, x, p: str, res=None):
-        """LayerNorm whose output is consumed only by fp8 GEMMs: fused per-row fp8 quantisation."""
+    def layernorm_q8(self, x, p: str, res=None, keep_bf16=False):
+        """LayerNorm whose output feeds fp8 GEMMs: fused per-row fp8 quantisation. ``keep_bf16``
+        (post-LN residual stream): also the bf16 output, returned as ``(out, (x8, scales))``."""
         g = self.g
         r, d = g.shape(x)
         x8 = g.tensor((r, d), torch.uint8, f"{p}.x8")
         sx = g.tensor((r,), torch.float32, f"{p}.sx")
         ins = [x] if res is None else [x, res]
+        if keep_bf16:
+            out = g.tensor((r, d), torch.bfloat16, p)
+            g.add("layernorm", ins, [out, x8, sx], p=p, rows=r, ldx=None)
+            return out, (x8, sx)
         g.add("layernorm", ins, [x8, sx], p=p, rows=r, ldx=None)
         return x8, sx
 

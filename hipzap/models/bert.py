@@ -48,12 +48,16 @@ def config_from_sd(sd: dict) -> dict:
             "max_pos": sd["bert.embeddings.position_embeddings.weight"].shape[0]}
 
 
-def pack_bert(sd: dict, device="cpu", eps: float = 1e-12, ln_fold: bool | None = None) -> tuple[dict, dict]:
+def pack_bert(sd: dict, device="cpu", eps: float = 1e-12, ln_fold: bool | None = None,
+              weights: str = "bf16") -> tuple[dict, dict]:
     """``ln_fold``: fold every encoder LayerNorm into its consumer GEMMs (see build_graph); the
-    returned cfg records the choice so the graph is built to match the packed weights."""
+    returned cfg records the choice so the graph is built to match the packed weights.
+    ``weights="fp8"``: encoder projections as e4m3 + per-channel scales on the MX fp8 MFMA path
+    (pooler and classifier stay bf16; no LayerNorm fold)."""
     sd = {k: v.to(device) for k, v in sd.items()}
     cfg = config_from_sd(sd)
-    cfg["ln_fold"] = ln_fold_default() if ln_fold is None else bool(ln_fold)
+    cfg["ln_fold"] = False if weights == "fp8" else (ln_fold_default() if ln_fold is None else bool(ln_fold))
+    cfg["weights"] = weights
     P = {
         "emb": EmbedTables(sd["bert.embeddings.word_embeddings.weight"].to(torch.bfloat16).contiguous(),
                            sd["bert.embeddings.position_embeddings.weight"].to(torch.bfloat16).contiguous(),
@@ -83,11 +87,14 @@ def pack_bert(sd: dict, device="cpu", eps: float = 1e-12, ln_fold: bool | None =
         P[f"l{i}.ln2"] = norm(sd, f"{pre}.output.LayerNorm", eps)
     P["pooler"] = pack_linear_padded(sd["bert.pooler.dense.weight"], sd["bert.pooler.dense.bias"])
     P["cls"] = pack_linear_padded(sd["classifier.weight"], sd["classifier.bias"])
+    if weights == "fp8":
+        from ..ops.fp8 import quantize_params
+        P = quantize_params(P, [n for n in P if n.startswith("l") and n.rsplit(".", 1)[-1] in ("qkv", "o", "ffn1", "ffn2")])
     return P, cfg
 
 
 def build_graph(batch: int, seq_len: int = 128, layers: int = 12, hidden: int = 768, heads: int = 12,
-                ffn: int = 3072, num_labels: int = 2, ln_fold: bool = False, **_) -> Graph:
+                ffn: int = 3072, num_labels: int = 2, ln_fold: bool = False, weights: str = "bf16", **_) -> Graph:
     """``ln_fold`` (must match pack_bert's cfg): no standalone encoder LayerNorm. The O-proj and
     FFN2 GEMMs emit per-row (sum, sumsq) slabs of their raw output y; FFN1 and the next layer's
     QKV run on y with gamma/beta folded into their weights and normalise in the epilogue; the
@@ -104,7 +111,21 @@ def build_graph(batch: int, seq_len: int = 128, layers: int = 12, hidden: int = 
     x = g.tensor((T, D), torch.bfloat16, "emb")
     g.add("embed_ln", [ids, types], [x], emb="emb", ln="emb_ln", L=L)
     ln_x = None  # (LayerNorm param, stats) while x is a raw pre-LN sum (ln_fold)
+    xq = None  # fp8: (e4m3, per-row scales) of x, emitted by the LayerNorm that produced x
     for i in range(layers):
+        if weights == "fp8":
+            # post-LN: each LayerNorm emits bf16 (the next residual) AND e4m3 + row scales (the next
+            # GEMM's input) in one pass; attention and FFN1 emit MX8 for O-proj / FFN2
+            qkv = tb.gemm8q(xq, f"l{i}.qkv", 3 * D) if xq is not None else tb.gemm8(x, f"l{i}.qkv", 3 * D)
+            y = tb.gemm8q(tb.attention(qkv, B, L, heads, mask, out_mx=True), f"l{i}.o", D, res=x)
+            x1, x1q = tb.layernorm_q8(y, f"l{i}.ln1", keep_bf16=True)
+            h = tb.gemm8q(x1q, f"l{i}.ffn1", ffn, act="gelu", out_mx=True)
+            y2 = tb.gemm8q(h, f"l{i}.ffn2", D, res=x1)
+            if i + 1 < layers:
+                x, xq = tb.layernorm_q8(y2, f"l{i}.ln2", keep_bf16=True)
+            else:
+                x = tb.layernorm(y2, f"l{i}.ln2")
+            continue
         qkv = tb.gemm(x, f"l{i}.qkv", 3 * D, ln_in=ln_x)
         ctx = tb.attention(qkv, B, L, heads, mask)
         if ln_fold:

@@ -80,8 +80,9 @@ class ResNet18(VisionAdapter):
 
 
 class TextClassifierAdapter:
-    """BERT-base sequence classification (north-star config 4)."""
+    """BERT-base sequence classification (north-star config 4); ``weights`` = bf16 or fp8."""
     seq_len = 128
+    weights = "bf16"
 
     def make_model(self, num_labels=2):
         from .bert import make_model
@@ -89,7 +90,7 @@ class TextClassifierAdapter:
 
     def pack(self, sd: dict, device):
         from .bert import pack_bert
-        params, cfg = pack_bert(sd, device)
+        params, cfg = pack_bert(sd, device, weights=self.weights)
         cfg["seq_len"] = self.seq_len
         return params, cfg
 
@@ -97,7 +98,7 @@ class TextClassifierAdapter:
         from .bert import make_model, pack_bert
         with torch.device("meta"):
             m = make_model(num_labels, **_hf_arch(arch, max_pos="max_position_embeddings"))
-        params, cfg = pack_bert(m.state_dict(), "meta", ln_fold=ln_fold)
+        params, cfg = pack_bert(m.state_dict(), "meta", ln_fold=ln_fold, weights=self.weights)
         cfg["seq_len"] = self.seq_len
         return params, cfg
 
@@ -119,6 +120,11 @@ class TextClassifierAdapter:
 @register("bert-base")
 class BertBase(TextClassifierAdapter):
     pass
+
+
+@register("bert-base-fp8")
+class BertBaseFp8(TextClassifierAdapter):
+    weights = "fp8"
 
 
 class ImageTransformerAdapter(VisionAdapter):

@@ -15,6 +15,7 @@ from hipzap.models import registry  # noqa: E402
 
 CONFIGS = {
     "bert-base": dict(batch=16, unit="seq/s", ref_cpu=24.3),
+    "bert-base-fp8": dict(batch=16, unit="seq/s", ref_cpu=24.3),
     "vit-b16": dict(batch=8, unit="img/s", ref_cpu=21.9),
     "vit-b16-fp8": dict(batch=8, unit="img/s", ref_cpu=21.9),
     "resnet50": dict(batch=4, unit="img/s", ref_cpu=27.2),
