@@ -132,3 +132,26 @@ def test_quantize_linear_builds_mx_copy():
     assert torch.equal(F8.mx_unpack(pw.w8mx), dense)
     assert F8.choose_config_fp8(2048, pw)[0] in F8.MX_TILES
     assert F8.choose_config_fp8(8, pw)[0] not in F8.MX_TILES
+
+
+def test_bert_fp8_graph_oracle_vs_hf():
+    """bert-base-fp8 lowering on the CPU oracle: one quantisation kernel (after the embedding
+    LayerNorm), every encoder LayerNorm but the last emits bf16 + e4m3 together, and the fp8
+    logits stay near HF fp32."""
+    import torch
+    from hipzap.engine.reference import run_graph_reference
+    from hipzap.models import bert, registry
+    torch.manual_seed(0)
+    a = registry.get("bert-base-fp8")
+    m = a.make_model().eval()
+    P, cfg = a.pack(m.state_dict(), "cpu")
+    assert cfg["weights"] == "fp8" and not cfg["ln_fold"]
+    g = a.build_graph(batch=2, **cfg)
+    kinds = [n.kind for n in g.nodes]
+    assert kinds.count("quant") == 1 and kinds.count("gemm_fp8") == 4 * cfg["layers"]
+    assert sum(1 for n in g.nodes if n.kind == "layernorm" and len(n.outputs) == 3) == 2 * cfg["layers"] - 1
+    ids = torch.randint(1000, 30000, (2, 128))
+    out = run_graph_reference(g, P, bert.encode_inputs(ids))[g.outputs[0]].reshape(2, -1)[:, :2]
+    with torch.no_grad():
+        ref = m(input_ids=ids).logits
+    assert ((out - ref).abs().max() / ref.abs().max()).item() < 0.25
