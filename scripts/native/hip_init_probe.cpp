@@ -25,8 +25,16 @@ int main(int argc, char** argv) {
   void* p = nullptr;
   if (e == hipSuccess) e = hipMalloc(&p, 64 << 20);
   const double t3 = now_ms();
-  std::printf("{\"lib\": %s, \"dlopen_ms\": %.2f, \"hip_init_ms\": %.2f, \"malloc64MB_ms\": %.2f, \"rc\": %d}\n",
-              argc > 1 ? "true" : "false", t1 - t0, t2 - t1, t3 - t2, (int)e);
+  hipStream_t st = nullptr;
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  const double t4 = now_ms();
+  if (e == hipSuccess) e = hipMemsetAsync(p, 0, 4096, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  const double t5 = now_ms();
+  std::printf("{\"lib\": %s, \"dlopen_ms\": %.2f, \"hip_init_ms\": %.2f, \"malloc64MB_ms\": %.2f, "
+              "\"first_stream_ms\": %.2f, \"first_op_ms\": %.2f, \"rc\": %d}\n",
+              argc > 1 ? "true" : "false", t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, (int)e);
+  if (st) (void)hipStreamDestroy(st);
   if (p) (void)hipFree(p);
   return e == hipSuccess ? 0 : 1;
 }
