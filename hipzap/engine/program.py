@@ -105,7 +105,9 @@ class ExecContext:
                 mx_io = g.tensors[n.inputs[1]].dtype == torch.uint8 or len(n.outputs) == 2
                 cfg, kw = fp8.choose_config_fp8(M, pc, tuned, key, mx_io=mx_io)
             else:
-                cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=pc)
+                # a conv with row-major output (ViT patch embedding) never runs as the LDS implicit GEMM
+                lds_pc = None if n.kind == "conv" and n.attrs.get("rowmajor") else pc
+                cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=lds_pc)
             if _ln_folded(n) and cfg not in conv_ops.LDS_TILES:  # HzLnFold lives in the LDS GEMM epilogue
                 if not conv_ops.lds_ok(M, pc.K, True, pc):
                     raise ValueError(f"{n.attrs.get('name')}: folded LayerNorm needs the LDS GEMM (M={M} < 64?)")
