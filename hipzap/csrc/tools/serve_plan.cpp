@@ -108,6 +108,10 @@ int die(const char* what) {
 
 int main(int argc, char** argv) {
   const double t0 = now_ms();
+  // blit-kernel copies instead of SDMA unless the deployment chose (hipzap/lite.py no_sdma_default:
+  // faster weight upload and first queue; the request path has no copies)
+  const char* keep = std::getenv("HIPZAP_KEEP_SDMA");
+  if (!keep || std::strcmp(keep, "1") != 0) setenv("HSA_ENABLE_SDMA", "0", 0);
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s PLAN [--port P] [--host H] [--contexts N] [--device D] [--max-wait-us U] [--once IMAGE]\n", argv[0]);
     return 2;

@@ -15,6 +15,7 @@ from __future__ import annotations
 import array
 import ctypes as C
 import json
+import os
 import struct
 import threading
 import time
@@ -78,6 +79,16 @@ def _in_buffer(x):
     return C.addressof(buf), mv.nbytes, buf
 
 
+def no_sdma_default() -> None:
+    """Copies through blit kernels instead of the SDMA engines (``HSA_ENABLE_SDMA=0``), unless the
+    deployment chose (or ``HIPZAP_KEEP_SDMA=1``): the plan's 51-MB weight upload is faster that way
+    and the process's first queue is cheaper -- fresh-process cold start 262 -> 237 ms p50,
+    interleaved on one box (``profiles/r2_coldstart/sdma_ab``). The serving path has no copies
+    (zero-copy request I/O). Takes effect only before the process's first HIP call."""
+    if os.environ.get("HIPZAP_KEEP_SDMA", "0") != "1":
+        os.environ.setdefault("HSA_ENABLE_SDMA", "0")
+
+
 class PlanEngine:
     """One plan image on one GPU. ``read_blob=False`` + ``fill_blob(address, nbytes)`` lets a DP
     rank receive the weights by RCCL broadcast instead of reading the file."""
@@ -95,6 +106,7 @@ class PlanEngine:
         if self.meta["abi"] != L.hz_abi_version():
             raise PlanError(f"{path}: plan written for native ABI {self.meta['abi']}, library is "
                             f"{L.hz_abi_version()} (re-export with `hipzap plan`)")
+        no_sdma_default()
         tm = (C.c_double * 8)()
         h = L.hz_plan_open(path.encode(), device, int(read_blob), tm)
         if not h:
