@@ -214,6 +214,8 @@ class Engine:
             return ex
         from ..executor import Executor
         with self._build_lock:
+            if getattr(self, "_bexec", None) is not None:
+                raise RuntimeError("this engine serves through the dynamic-batching executor")
             if self._exec is None:
                 for lk in self._locks:  # no request may be in flight on the legacy path meanwhile
                     lk.acquire()
@@ -303,6 +305,8 @@ class Engine:
         from ..executor import Executor
         self.ensure_contexts()
         with self._build_lock:
+            if self._exec is not None:  # both would drive the same pinned buffers and streams
+                raise RuntimeError("this engine already serves through the per-request executor")
             if getattr(self, "_bexec", None) is None:
                 cs = self.contexts
                 self._bexec = Executor(

@@ -192,6 +192,8 @@ class PlanEngine:
     def executor(self):
         """Native request executor over all contexts, once every context exists (else None)."""
         ex = getattr(self, "_exec", None)
+        if getattr(self, "_bexec", None) is not None:
+            raise PlanError("this plan engine serves through the dynamic-batching executor")
         if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts \
                 or self._uncaptured:
             return ex
@@ -223,6 +225,8 @@ class PlanEngine:
             return ex
         from .executor import Executor
         with self._build_lock:
+            if getattr(self, "_exec", None) is not None:  # same pinned buffers and streams
+                raise PlanError("this plan engine already serves through the per-request executor")
             if getattr(self, "_bexec", None) is None:
                 L, n = lib(), len(self._locks)
                 hosts = [L.hz_plan_host(self._h, i) for i in range(n)]
@@ -253,6 +257,29 @@ class PlanEngine:
             raise PlanError(f"request is {nb} bytes, plan input {spec['shape']} {spec['dtype']} is {spec['bytes']}")
         out = array.array(_TYPECODE[self.out_spec["dtype"]], bytes(self.out_spec["bytes"]))
         oaddr, _ = out.buffer_info()
+        bex = getattr(self, "_bexec", None)
+        if bex is not None:
+            # the contexts belong to the dynamic-batching executor (native /predict): the B rows go
+            # through it as B one-image requests, submitted together so they share a replay
+            rows, ib, ob = bex.rows, bex.in_bytes[0], bex.out_bytes
+            errs = []
+
+            def one(r):
+                try:
+                    bex.submit([addr + r * ib], oaddr + r * ob)
+                except Exception as e:  # noqa: BLE001 - re-raised below
+                    errs.append(e)
+
+            th = [threading.Thread(target=one, args=(r,)) for r in range(1, rows)]
+            for t in th:
+                t.start()
+            one(0)
+            for t in th:
+                t.join()
+            del keep
+            if errs:
+                raise errs[0]
+            return out
         ex = self.executor() if ctx is None else None
         if ex is not None:
             ex.submit([addr], oaddr)
