@@ -310,12 +310,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
 #pragma unroll
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
-  if (NS > 2 && kb > 1) stage(1, 1);
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < kb) stage(s0, s0);
   int cur = 0;
   for (int st = 0; st < kb; ++st) {
-    // stages issued ahead of st: min(NS-2, kb-1-st) may stay in flight
-    if (NS > 2 && st + 1 < kb) wait_vm8<(NS > 2 ? G : 0)>();
+    // stages issued ahead of st: min(NS-2, kb-1-st) may stay in flight (NS = 4: two, the K = 768
+    // projections have only 6 stages, so the prologue's loads are most of a tile's latency)
+    const int ahead = min(NS - 2, kb - 1 - st);
+    if (NS > 3 && ahead >= 2) wait_vm8<(NS > 3 ? 2 * G : 0)>();
+    else if (NS > 2 && ahead >= 1) wait_vm8<(NS > 2 ? G : 0)>();
     else wait_vm8<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -477,6 +481,10 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 27: return launch_mx<128, 128, 3, 2, 4>(p, st);
       case 28: return launch_mx<256, 128, 3, 4, 2>(p, st);
       case 29: return launch_mx<128, 256, 3, 2, 4>(p, st);
+      // 4 LDS stages (two K steps in flight): 8-wave 128x128, 4-wave 64x128 / 128x64
+      case 30: return launch_mx<128, 128, 4, 2, 4>(p, st);
+      case 31: return launch_mx<64, 128, 4>(p, st);
+      case 32: return launch_mx<128, 64, 4>(p, st);
       default: return -2;
     }
   }

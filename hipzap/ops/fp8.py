@@ -99,8 +99,10 @@ def quantize_linear(pc: PackedConv) -> PackedFp8:
 MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             20: (128, 128), 21: (64, 128), 22: (128, 64), 23: (64, 64),
             # 24-29: 8-wave workgroups (2 / 3 stages); N must be a multiple of BN
-            24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256)}
-MX_WIDE = (24, 25, 26, 27, 28, 29)
+            24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256),
+            # 30-32: 4 LDS stages (8-wave 128x128; 4-wave 64x128, 128x64)
+            30: (128, 128), 31: (64, 128), 32: (128, 64)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30)
 
 
 def mx_fits(cfg: int, n: int) -> bool:
