@@ -61,11 +61,11 @@ def parse():
                          "pipelined: replays queued back to back, no host work (device ceiling)")
     ap.add_argument("--compare-torch", action="store_true", help="also time PyTorch/MIOpen bf16 + CUDA graph")
     ap.add_argument("--no-capture", action="store_true")
-    ap.add_argument("--dyn-batch", type=int, default=8,
+    ap.add_argument("--dyn-batch", type=int, default=16,
                     help="secondary figure: the same bs=1 requests served with dynamic batching into replays "
                          "of this batch (0: skip)")
-    ap.add_argument("--dyn-contexts", type=int, default=8)
-    ap.add_argument("--dyn-clients", type=int, default=64)
+    ap.add_argument("--dyn-contexts", type=int, default=6)
+    ap.add_argument("--dyn-clients", type=int, default=96)
     ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
