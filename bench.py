@@ -72,6 +72,9 @@ def parse():
                     help="replica: independent bs=1 request streams per GPU (headline); scatter: rank 0 scatters "
                          "a global batch over ranks and gathers the logits (configs 3/5)")
     ap.add_argument("--global-batch", type=int, default=32, help="scatter mode: global batch over all ranks")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rehearse the N-rank launch only (rendezvous + one all-reduce, no GPU work); rank 0 "
+                         "prints {n_gpus, ranks_seen}")
     ap.add_argument("--input", choices=["uint8", "fp32"], default=os.environ.get("HIPZAP_BENCH_INPUT", "uint8"),
                     help="request payload: uint8 HWC images (decoded-JPEG format, ImageNet mean/std applied on "
                          "device by the preprocess kernel) or pre-normalised fp32 NCHW tensors")
@@ -248,10 +251,101 @@ def request_input(args, adapter):
     return adapter.example_input(args.batch)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def check_gpus(n: int, share: bool) -> None:
+    """Fail loudly unless this node has ``n`` GPUs for ``n`` ranks. ``device_count`` does not
+    initialise HIP on this image, so the launcher may call it before spawning ranks."""
+    have = torch.cuda.device_count()
+    if share:  # multi-rank rehearsal folded onto the visible GPU(s): HIPZAP_SHARE_GPU=1
+        if have < 1:
+            raise SystemExit(f"bench: --gpus {n} with HIPZAP_SHARE_GPU=1 needs at least one GPU, found none")
+        return
+    if have < n:
+        raise SystemExit(f"bench: --gpus {n} needs {n} GPUs on this node, found {have} "
+                         "(HIPZAP_SHARE_GPU=1 rehearses several ranks on one GPU)")
+
+
+def self_launch(args) -> int:
+    """``python bench.py --gpus N`` without torchrun: spawn N rank processes of this script
+    (one per GPU, fresh interpreters started before this process makes any GPU call) with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, exactly as torchrun would. Rank 0 prints the
+    JSON line (stdout is inherited); the launcher exits with the worst rank's code. When one
+    rank fails, the others are stopped after a grace period instead of waiting on its
+    collectives until the process-group timeout."""
+    import signal
+    import subprocess
+    if not args.launch_check:
+        check_gpus(args.gpus, os.environ.get("HIPZAP_SHARE_GPU") == "1")
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HIPZAP_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    codes: dict[int, int] = {}
+    fail_at = None
+    while len(codes) < len(procs):
+        for r, p in enumerate(procs):
+            if r not in codes and p.poll() is not None:
+                codes[r] = p.returncode
+                if p.returncode != 0 and fail_at is None:
+                    print(f"bench: rank {r} exited with {p.returncode}", file=sys.stderr, flush=True)
+                    fail_at = time.time()
+        if fail_at is not None and time.time() - fail_at > 30:
+            for r, p in enumerate(procs):
+                if r not in codes:
+                    try:
+                        os.killpg(p.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+            for r, p in enumerate(procs):
+                if r not in codes:
+                    try:
+                        codes[r] = p.wait(timeout=15)
+                    except subprocess.TimeoutExpired:
+                        os.killpg(p.pid, signal.SIGKILL)
+                        codes[r] = p.wait()
+        time.sleep(0.05)
+    # a rank killed by signal s reports -s: map it to the shell's 128 + s
+    bad = [c if c > 0 else 128 - c for c in codes.values() if c != 0]
+    return max(bad) if bad else 0
+
+
+def launch_check(rank: int, world: int) -> None:
+    """--launch-check: every rank joins the process group (gloo: no GPU call) and all-reduces 1."""
+    from hipzap.parallel.comm import init_distributed, is_dist
+    init_distributed(backend="gloo", timeout_s=60)
+    t = torch.ones(1)
+    if is_dist():
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
+                          "self_launched": os.environ.get("HIPZAP_SELF_LAUNCHED") == "1"}), flush=True)
+    if is_dist():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     from hipzap.parallel.comm import env_rank
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
     rank, world, local = env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
+    if args.launch_check:
+        return launch_check(rank, world)
+    if rank == 0 and world > 1 and os.environ.get("HIPZAP_SELF_LAUNCHED") != "1":
+        check_gpus(world, os.environ.get("HIPZAP_SHARE_GPU") == "1")
     # 1. cold start over fresh processes, before this process makes any GPU call (the other
     #    ranks wait in the process-group rendezvous meanwhile)
     fresh = None

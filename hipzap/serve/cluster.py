@@ -25,7 +25,8 @@ Shape (reference scale-out = Lambda's per-request container fan-out,
   communicator and joins a new one over the survivors (fresh unique id per epoch). Weights are
   already resident, so bs=1 serving never stops; a restarted worker cold-starts from the plan
   on disk and rejoins through the same path. Rank 0 hosts the sequencer: if it dies, batched
-  requests fall back to the receiving worker's GPU alone until it is restarted.
+  requests fall back to the receiving worker's GPU alone until it is restarted; the other
+  members then reconnect to the restarted sequencer and rejoin (one reform).
 """
 from __future__ import annotations
 
@@ -41,6 +42,7 @@ import tempfile
 import threading
 import time
 from concurrent.futures import Future
+from concurrent.futures import TimeoutError as FutureTimeout
 
 from ..parallel.base import CommError
 
@@ -70,7 +72,15 @@ class Coordinator:
         self.lock = threading.Lock()
         self.members: dict[int, tuple] = {}  # original rank -> (conn, wfile, send lock)
         self.seq = 0
-        self.epoch = 0
+        # epochs name the rendezvous keys of every communicator generation (uid<epoch>): a
+        # RESTARTED sequencer continues after the last epoch it published instead of reusing
+        # keys whose stale files are still in the rendezvous directory
+        self._epoch_file = path + ".epoch"
+        try:
+            with open(self._epoch_file) as f:
+                self.epoch = int(f.read().strip() or 0)
+        except (FileNotFoundError, ValueError):
+            self.epoch = 0
         self.reforms: list = []
         self._stop = threading.Event()
         try:
@@ -148,6 +158,10 @@ class Coordinator:
     def reform(self, reason: str) -> None:
         with self.lock:
             self.epoch += 1
+            tmp = f"{self._epoch_file}.{os.getpid()}"
+            with open(tmp, "w") as f:
+                f.write(str(self.epoch))
+            os.replace(tmp, self._epoch_file)
             members = sorted(self.members)
             self.reforms.append({"epoch": self.epoch, "members": members, "reason": reason})
             log.warning("cluster reform epoch %d: members %s (%s)", self.epoch, members, reason)
@@ -187,25 +201,17 @@ class Member:
         self.members = list(range(world)) if comm is not None else [rank]
         self.epoch = 0
         self.timeout_s = timeout_s
-        self.pending: dict[str, tuple] = {}
+        self.pending: dict[str, list] = {}  # token -> [array or None (abandoned), future]
+        self.abandoned = 0
+        self.ctl_path = ctl_path
+        self.reconnect_s = float(os.environ.get("HIPZAP_CTL_RECONNECT_S", 120.0))
+        self._closed = False
         self.health = {"ok": 0, "failed": 0, "last_world": None}
         self.reforms: list = []
         self._ids = itertools.count()
         self._lock = threading.Lock()
-        t0 = time.time()
-        while True:
-            try:
-                self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-                self.sock.connect(ctl_path)
-                break
-            except (FileNotFoundError, ConnectionRefusedError):
-                self.sock.close()
-                if time.time() - t0 > timeout_s:
-                    raise CommError(f"coordinator {ctl_path} not reachable")
-                time.sleep(0.01)
-        self.f = self.sock.makefile("rwb")
         self._wlock = threading.Lock()
-        _send(self.f, self._wlock, {"op": "hello", "rank": rank, "join": join})
+        self._connect(join=join, timeout_s=timeout_s)
         self.alive = True
         self.thread = threading.Thread(target=self._loop, daemon=True, name=f"hz-member-{rank}")
         self.thread.start()
@@ -213,41 +219,95 @@ class Member:
     # ---------------------------------------------------------------- requests
     def submit(self, arr, timeout: float | None = None):
         """Run a batch over the whole cluster (blocking); ``arr``: numpy [n, ...] of the
-        runner's item shape. Returns numpy [n, classes]."""
+        runner's item shape. Returns numpy [n, classes].
+
+        The job stays registered until its sequenced ``run`` reaches this rank, even when the
+        caller gives up first: the ``run`` is already on its way to every other rank, which will
+        enter the scatter/gather, so this (root) rank must join them (``_run`` stages zeros for
+        an abandoned job and drops the output) instead of leaving them blocked until the
+        communicator times out and the whole cluster reforms."""
         if not self.alive:
             raise CommError("control plane is down")
         token = f"{self.rank}-{next(self._ids)}"
         fut: Future = Future()
         with self._lock:
-            self.pending[token] = (arr, fut)
-        _send(self.f, self._wlock, {"op": "submit", "token": token, "n": int(arr.shape[0])})
+            self.pending[token] = [arr, fut]
         try:
-            return fut.result(timeout or self.timeout_s)
-        finally:
+            _send(self.f, self._wlock, {"op": "submit", "token": token, "n": int(arr.shape[0])})
+        except OSError as e:
             with self._lock:
                 self.pending.pop(token, None)
+            raise CommError(f"control plane send failed: {e}") from e
+        try:
+            return fut.result(timeout or self.timeout_s)
+        except FutureTimeout:
+            with self._lock:
+                job = self.pending.get(token)
+                if job is not None:
+                    job[0] = None  # abandoned: the sequenced run still joins the collectives with zeros
+            self.abandoned += 1
+            raise
 
     # ---------------------------------------------------------------- sequenced work
+    def _connect(self, join: bool, timeout_s: float) -> None:
+        t0 = time.time()
+        while True:
+            sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            try:
+                sock.connect(self.ctl_path)
+                break
+            except (FileNotFoundError, ConnectionRefusedError):
+                sock.close()
+                if time.time() - t0 > timeout_s or self._closed:
+                    raise CommError(f"coordinator {self.ctl_path} not reachable")
+                time.sleep(0.01 if not join else 0.2)
+        self.sock = sock
+        self.f = sock.makefile("rwb")
+        _send(self.f, self._wlock, {"op": "hello", "rank": self.rank, "join": join})
+
     def _loop(self):
-        try:
-            while True:
-                msg = _recv(self.f)
-                if msg is None:
-                    break
-                op = msg["op"]
-                if op == "run":
-                    self._run(msg)
-                elif op == "health":
-                    self._health()
-                elif op == "reform":
-                    self._reform(msg)
-        except (OSError, ValueError) as e:
-            log.warning("rank %d: control connection lost: %s", self.rank, e)
-        self.alive = False
-        with self._lock:
-            for arr, fut in self.pending.values():
-                if not fut.done():
-                    fut.set_exception(CommError("control plane lost"))
+        """Sequenced work from the coordinator. When the control connection drops (rank 0, the
+        sequencer's host, died), fail the pending jobs, drop the communicator and keep trying to
+        reach the RESTARTED coordinator at the same path for ``HIPZAP_CTL_RECONNECT_S``: the
+        rejoin (hello with ``join``) makes it reform a communicator over everyone who is back,
+        so batched DP resumes after a rank-0 restart instead of staying off."""
+        while True:
+            try:
+                while True:
+                    msg = _recv(self.f)
+                    if msg is None:
+                        break
+                    op = msg["op"]
+                    if op == "run":
+                        self._run(msg)
+                    elif op == "health":
+                        self._health()
+                    elif op == "reform":
+                        self._reform(msg)
+            except (OSError, ValueError) as e:
+                log.warning("rank %d: control connection lost: %s", self.rank, e)
+            self.alive = False
+            with self._lock:
+                for arr, fut in self.pending.values():
+                    if not fut.done():
+                        fut.set_exception(CommError("control plane lost"))
+                self.pending.clear()
+            old, self.comm = self.comm, None
+            if old is not None:
+                try:
+                    old.abort()
+                    old.close()
+                except Exception:  # noqa: BLE001
+                    pass
+            if self._closed or self.reconnect_s <= 0:
+                return
+            try:
+                self._connect(join=True, timeout_s=self.reconnect_s)
+            except (CommError, OSError) as e:
+                log.error("rank %d: coordinator did not come back: %s", self.rank, e)
+                return
+            log.warning("rank %d: reconnected to the coordinator; waiting for the reform", self.rank)
+            self.alive = True
 
     def _fail(self, reason: str) -> None:
         try:
@@ -259,12 +319,13 @@ class Member:
         root_orig = msg["root"]
         mine = root_orig == self.rank
         with self._lock:
-            job = self.pending.get(msg["token"]) if mine else None
+            job = self.pending.pop(msg["token"], None) if mine else None
         try:
             if self.comm is None or root_orig not in self.members:
                 raise CommError("no communicator for this job")
+            # mine but abandoned (caller timed out) or unknown: still the root of this collective
             out = self.dp_step(self.members.index(root_orig), msg["n"], job[0] if job else None)
-            if job:
+            if job and not job[1].done():
                 job[1].set_result(out)
         except Exception as e:  # noqa: BLE001 - a failed collective must not kill the loop
             if job and not job[1].done():
@@ -283,14 +344,16 @@ class Member:
         for off in range(0, n, G):
             m = min(G, n - off)
             if comm.rank == root:
-                rn.stage(arr[off: off + m], G)
+                rn.stage(arr[off: off + m] if arr is not None else np.zeros((m, rn.in_item), np.uint8), G)
             comm.scatter_ptr(rn.staging if comm.rank == root else 0, rn.shard_in, S * rn.in_item, root,
                              stream=rn.stream, wait=False)
             rn.run()
             comm.gather_ptr(rn.shard_out, rn.gather if comm.rank == root else 0, S * rn.out_item, root,
                             stream=rn.stream, wait=True)
             if comm.rank == root:
-                out[off: off + m] = rn.read_gather(m)
+                y = rn.read_gather(m)
+                if arr is not None:
+                    out[off: off + m] = y
         return out
 
     def _health(self):
@@ -332,6 +395,7 @@ class Member:
 
     def close(self):
         self.alive = False
+        self._closed = True
         try:
             self.sock.shutdown(socket.SHUT_RDWR)
             self.sock.close()
