@@ -162,7 +162,7 @@ def _load():
     _sig(lib, "hz_http_set_fast", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, C.c_char_p)
     _sig(lib, "hz_http_respond", None, P, c_int, C.c_char_p, U64, C.c_char_p, U64)
     _sig(lib, "hz_http_stats", None, P, C.POINTER(U64))
-    _sig(lib, "hz_http_stop", None, P)
+    _sig(lib, "hz_http_stop", C.c_int, P)
     if DEBUG:
         for unit in DEBUG_UNITS:
             _sig(lib, f"hz_debug_poll_{unit}", c_int, C.POINTER(C.c_uint))

@@ -68,6 +68,7 @@ struct Exec {
   std::deque<int> to_launch;
   std::vector<int> inflight;  // worker-owned
   bool stop = false;
+  int active = 0;  // request threads inside submit_wait: the worker outlives every one of them
   std::thread worker;
   uint64_t served = 0, polls = 0, batches = 0;
   // dynamic batching (rows > 1)
@@ -107,9 +108,11 @@ struct Exec {
     for (;;) {
       {
         std::unique_lock<std::mutex> lk(mu);
+        // at shutdown a request may still be copying into a sealed slot (not yet queued): keep
+        // serving until every request thread has left, so none waits on a slot nobody launches
         if (to_launch.empty() && inflight.empty())
-          cv_work.wait(lk, [&] { return stop || !to_launch.empty() || open >= 0; });
-        if (stop && to_launch.empty() && inflight.empty() && open < 0) return;
+          cv_work.wait(lk, [&] { return (stop && active == 0) || !to_launch.empty() || open >= 0; });
+        if (stop && active == 0 && to_launch.empty() && inflight.empty() && open < 0) return;
         // dynamic batching: close the filling batch when the GPU is short of work or it is old
         if (open >= 0 && ((int)inflight.size() < min_inflight || stop || now_us() - slots[open].t_open >= max_wait_us))
           seal_open();
@@ -191,7 +194,20 @@ struct Exec {
   }
 
   int submit_wait(const void* const* in, void* out, double* lat_us) {
-    if (rows > 1) return submit_batched(in, out, lat_us);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (stop) return -10;
+      ++active;
+    }
+    const int rc = rows > 1 ? submit_batched(in, out, lat_us) : submit_one(in, out, lat_us);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (--active == 0 && stop) cv_work.notify_all();
+    }
+    return rc;
+  }
+
+  int submit_one(const void* const* in, void* out, double* lat_us) {
     const double t0 = now_us();
     int s;
     {
@@ -230,7 +246,7 @@ struct Exec {
     }
     cv_work.notify_all();
     cv_free.notify_all();
-    if (worker.joinable()) worker.join();
+    if (worker.joinable()) worker.join();  // returns once no request thread is inside submit_wait
     for (auto& s : slots)
       if (s.ev) (void)hipEventDestroy(s.ev);
   }

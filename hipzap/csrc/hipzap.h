@@ -363,7 +363,7 @@ int hz_http_set_fast(void* srv, void* exec, int H, int W, int C, int out_floats,
                      const char* model);
 void hz_http_respond(void* req, int status, const char* headers, uint64_t hlen, const char* body, uint64_t blen);
 void hz_http_stats(void* srv, uint64_t* out4);
-void hz_http_stop(void* srv);
+int hz_http_stop(void* srv);  // 1: all connections ended; 0: some still live (state leaked)
 void hz_plan_close(void* plan);
 
 #ifdef __cplusplus

@@ -531,13 +531,18 @@ void hz_http_stats(void* h, uint64_t* out4) {
   out4[3] = (uint64_t)S->live.load();
 }
 
-// stop accepting, let open connections notice within one poll period, then free
-void hz_http_stop(void* h) {
+// stop accepting, let open connections notice within one poll period, then free. Returns 1 when
+// every connection thread has ended (the caller may then destroy the executor the fast route
+// submits to), 0 when some are still live after 1 s: the server state is leaked and the caller
+// must leak the executor too rather than free it under a connection inside hz_exec_submit.
+int hz_http_stop(void* h) {
   Server* S = static_cast<Server*>(h);
   S->stop.store(true);
   if (S->acceptor.joinable()) S->acceptor.join();
   for (int i = 0; i < 100 && S->live.load() > 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-  if (S->live.load() == 0) delete S;  // else leak rather than free state a connection still uses
+  if (S->live.load() != 0) return 0;
+  delete S;
+  return 1;
 }
 
 }  // extern "C"

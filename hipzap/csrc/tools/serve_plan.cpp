@@ -218,9 +218,11 @@ int main(int argc, char** argv) {
   signal(SIGINT, on_signal);
   signal(SIGTERM, on_signal);
   while (!g_stop.load()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
-  hz_http_stop(srv);
+  const int drained = hz_http_stop(srv);
   close(fd);
-  hz_exec_destroy(ex);
-  hz_plan_close(plan);
+  if (drained) {  // else a connection may still be inside hz_exec_submit: the process exits instead
+    hz_exec_destroy(ex);
+    hz_plan_close(plan);
+  }
   return 0;
 }

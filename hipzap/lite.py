@@ -197,6 +197,8 @@ class PlanEngine:
         if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts \
                 or self._uncaptured:
             return ex
+        if int(self.in_specs[0]["shape"][0]) > 1:
+            raise PlanError("a batch-B plan serves one-image requests through batched_executor()")
         from .executor import Executor
         with self._build_lock:
             if getattr(self, "_exec", None) is None:
@@ -228,15 +230,23 @@ class PlanEngine:
             if getattr(self, "_exec", None) is not None:  # same pinned buffers and streams
                 raise PlanError("this plan engine already serves through the per-request executor")
             if getattr(self, "_bexec", None) is None:
-                L, n = lib(), len(self._locks)
-                hosts = [L.hz_plan_host(self._h, i) for i in range(n)]
-                self._bexec = Executor([L.hz_plan_prog(self._h, i) for i in range(n)],
-                                       [L.hz_plan_stream(self._h, i) for i in range(n)],
-                                       [[h + sp["off"] for h in hosts] for sp in self.in_specs],
-                                       [sp["bytes"] for sp in self.in_specs],
-                                       [h + self.out_spec["off"] for h in hosts], self.out_spec["bytes"],
-                                       rows=int(self.in_specs[0]["shape"][0]), max_wait_us=max_wait_us,
-                                       min_inflight=min_inflight)
+                # every context lock: a direct hz_plan_infer still in flight owns its context's
+                # pinned buffers and stream until it returns
+                for lk in self._locks:
+                    lk.acquire()
+                try:
+                    L, n = lib(), len(self._locks)
+                    hosts = [L.hz_plan_host(self._h, i) for i in range(n)]
+                    self._bexec = Executor([L.hz_plan_prog(self._h, i) for i in range(n)],
+                                           [L.hz_plan_stream(self._h, i) for i in range(n)],
+                                           [[h + sp["off"] for h in hosts] for sp in self.in_specs],
+                                           [sp["bytes"] for sp in self.in_specs],
+                                           [h + self.out_spec["off"] for h in hosts], self.out_spec["bytes"],
+                                           rows=int(self.in_specs[0]["shape"][0]), max_wait_us=max_wait_us,
+                                           min_inflight=min_inflight)
+                finally:
+                    for lk in self._locks:
+                        lk.release()
         return self._bexec
 
     def _pick(self) -> int:
@@ -246,9 +256,11 @@ class PlanEngine:
         return i
 
     # ---------------------------------------------------------------- requests
-    def infer_raw(self, x, ctx: int | None = None) -> array.array:
+    def infer_raw(self, x, ctx: int | None = None, rows: int | None = None) -> array.array:
         """One request: ``x`` = the input's exact bytes (uint8 HWC image for the ResNet plans).
-        Returns the output as a flat ``array.array`` (float32 logits)."""
+        Returns the output as a flat ``array.array`` (float32 logits). ``rows``: how many leading
+        rows of a batch-B request are real (the rest is padding): on the dynamic-batching
+        executor only those are submitted, and the padding rows' outputs stay zero."""
         if len(self.in_specs) != 1 or not self.host_io:
             raise PlanError("infer_raw needs a single-input host-I/O plan")
         addr, nb, keep = _in_buffer(x)
@@ -258,10 +270,14 @@ class PlanEngine:
         out = array.array(_TYPECODE[self.out_spec["dtype"]], bytes(self.out_spec["bytes"]))
         oaddr, _ = out.buffer_info()
         bex = getattr(self, "_bexec", None)
+        if bex is None and ctx is None and int(spec["shape"][0]) > 1:
+            self.ensure_contexts()
+            bex = self.batched_executor()
         if bex is not None:
-            # the contexts belong to the dynamic-batching executor (native /predict): the B rows go
-            # through it as B one-image requests, submitted together so they share a replay
-            rows, ib, ob = bex.rows, bex.in_bytes[0], bex.out_bytes
+            # the contexts belong to the dynamic-batching executor (native /predict): the real
+            # rows go through it as one-image requests, submitted together so they share a replay
+            ib, ob = bex.in_bytes[0], bex.out_bytes
+            m = bex.rows if rows is None else max(1, min(int(rows), bex.rows))
             errs = []
 
             def one(r):
@@ -270,7 +286,7 @@ class PlanEngine:
                 except Exception as e:  # noqa: BLE001 - re-raised below
                     errs.append(e)
 
-            th = [threading.Thread(target=one, args=(r,)) for r in range(1, rows)]
+            th = [threading.Thread(target=one, args=(r,)) for r in range(1, m)]
             for t in th:
                 t.start()
             one(0)
@@ -313,9 +329,11 @@ class PlanEngine:
         return us * 1e-6
 
     def close(self) -> None:
-        ex = getattr(self, "_exec", None)
-        if ex is not None:
-            ex.close()
+        for name in ("_exec", "_bexec"):
+            ex = getattr(self, name, None)
+            if ex is not None:
+                ex.close()
+                setattr(self, name, None)
         h, self._h = getattr(self, "_h", None), None
         if h:
             lib().hz_plan_close(h)

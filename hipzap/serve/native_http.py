@@ -20,6 +20,7 @@ from .. import _native as N
 
 log = logging.getLogger("hipzap.http")
 
+_LEAKED: list = []  # executors a stopped server may still reference (never freed)
 _CB = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64)
 
 
@@ -63,22 +64,35 @@ class NativeHTTPServer:
         self._call_wsgi = call_wsgi
         self._port = str(sock.getsockname()[1])
         self._cb = _CB(self._handle)  # keep a reference: the C side calls it from its threads
+        self.fast_model = None
+        self._stopped = threading.Event()
+        # the fast route's executor is built BEFORE the port accepts anything: a /predict that
+        # reached the WSGI fallback first could otherwise build the other executor kind over the
+        # same contexts
+        ex = self._prepare_fast(fast) if fast is not None else None
         self._h = N.lib().hz_http_start(sock.fileno(), self._cb)
         if not self._h:
             raise RuntimeError("hz_http_start failed")
-        self.fast_model = None
         if fast is not None:
-            self.set_fast(fast)
-        self._stopped = threading.Event()
+            self._route_fast(fast, ex)
 
-    def set_fast(self, backend) -> None:
+    @staticmethod
+    def _prepare_fast(backend):
         eng = backend.engine
         eng.ensure_contexts()
-        b, h, w, c = backend.in_shape
+        b = backend.in_shape[0]
         # a batch-B plan is served with dynamic batching: each POST is one row of a shared replay
         ex = eng.executor() if b == 1 else eng.batched_executor(getattr(backend, "max_wait_us", 200.0))
         if ex is None:
             raise RuntimeError("plan engine has no executor (capture disabled?)")
+        return ex
+
+    def set_fast(self, backend) -> None:
+        self._route_fast(backend, self._prepare_fast(backend))
+
+    def _route_fast(self, backend, ex) -> None:
+        eng = backend.engine
+        b, h, w, c = backend.in_shape
         self._exec = ex  # keep alive
         out = eng.out_spec
         rc = N.lib().hz_http_set_fast(self._h, ex._h, h, w, c, out["bytes"] // b // 4, int(backend.num_labels),
@@ -120,5 +134,7 @@ class NativeHTTPServer:
     def stop(self) -> None:
         h, self._h = getattr(self, "_h", None), None
         self._stopped.set()
-        if h:
-            N.lib().hz_http_stop(h)
+        if h and not N.lib().hz_http_stop(h):
+            # a connection thread is still live and may be inside the executor: never free it
+            _LEAKED.append(getattr(self, "_exec", None))
+            log.warning("native http: connections still open at stop; executor kept alive")

@@ -388,7 +388,7 @@ class PlanVisionBackend:
             m = chunk.shape[0]
             if m < B:
                 chunk = np.concatenate([chunk, np.zeros((B - m,) + chunk.shape[1:], np.uint8)])
-            y = np.frombuffer(self.engine.infer_raw(np.ascontiguousarray(chunk)), np.float32)
+            y = np.frombuffer(self.engine.infer_raw(np.ascontiguousarray(chunk), rows=m), np.float32)
             out[i: i + m] = y.reshape(B, -1)[:m, : self.num_labels]
         return out
 
