@@ -17,7 +17,7 @@ DEBUG = os.environ.get("HIPZAP_DEBUG") == "1"
 _LIB_PATH = Path(__file__).resolve().parent / "_lib" / ("libhipzap_debug.so" if DEBUG else "libhipzap.so")
 if os.environ.get("HIPZAP_LIB"):  # same-box A/B of two builds (scripts/ab_lib.sh)
     _LIB_PATH = Path(os.environ["HIPZAP_LIB"]).resolve()
-DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm")
+DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch")
 _lock = threading.Lock()
 _lib = None
 
@@ -75,6 +75,33 @@ class DecoderParams(C.Structure):
                 ("exclude", c_int * 8), ("n_hh", c_int), ("hh_blocks", c_int), ("hh_w", c_void_p * 4),
                 ("hh_b", c_void_p * 4), ("hh_h", c_void_p * 4), ("hh_out", c_void_p * 4), ("hh_H", c_int * 4),
                 ("hh_ld", c_int * 4), ("hh_blk", c_int * 5)]
+
+# batched AWD-LSTM decode (csrc/lmbatch.hip, csrc/lmserve.cpp)
+class LmbCtl(C.Structure):
+    _fields_ = [("tok", c_int), ("out", c_int), ("dec_t", c_int), ("rec", c_int)]
+
+
+class LmbLayerParams(C.Structure):
+    _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("x", c_void_p), ("c", c_void_p),
+                ("gpar", c_void_p), ("ctl", c_void_p), ("H", c_int), ("Kh", c_int), ("Kx", c_int), ("R", c_int),
+                ("Bp", c_int), ("step_off", c_int), ("emb", c_void_p), ("dacc", c_void_p), ("nblk", c_int),
+                ("V", c_int), ("outp", c_void_p), ("tok", c_void_p)]
+
+
+class LmbDecParams(C.Structure):
+    _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("gpar", c_void_p), ("ctl", c_void_p),
+                ("seed", c_void_p), ("dacc", c_void_p), ("logits", c_void_p), ("V", c_int), ("Vp", c_int),
+                ("K", c_int), ("Bp", c_int), ("nblk", c_int), ("step_off", c_int), ("n_exclude", c_int),
+                ("pad_", c_int), ("exclude", c_int * 8)]
+
+
+class LmbAdmitParams(C.Structure):
+    _fields_ = [("block", c_void_p), ("ctl", c_void_p), ("seed", c_void_p), ("outp", c_void_p), ("gpar", c_void_p),
+                ("Bp", c_int), ("U", c_int), ("n_layers", c_int), ("pad_", c_int), ("h", c_void_p * 4),
+                ("c", c_void_p * 4), ("Kh", c_int * 4), ("H", c_int * 4)]
+
+
+HZ_K_LMB_LAYER, HZ_K_LMB_DEC, HZ_K_LMB_ADMIT = 14, 15, 16
 
 HH_ROWS = 16  # HZ_HH_ROWS (hipzap.h): rows per recurrent-partial workgroup of the decoder kernel
 
@@ -163,6 +190,14 @@ def _load():
     _sig(lib, "hz_http_respond", None, P, c_int, C.c_char_p, U64, C.c_char_p, U64)
     _sig(lib, "hz_http_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_http_stop", C.c_int, P)
+    _sig(lib, "hz_lmb_layer_launch", c_int, C.POINTER(LmbLayerParams), P)
+    _sig(lib, "hz_lmb_dec_launch", c_int, C.POINTER(LmbDecParams), P)
+    _sig(lib, "hz_lmb_admit_launch", c_int, C.POINTER(LmbAdmitParams), P)
+    _sig(lib, "hz_lmb_dec_blocks", c_int, c_int)
+    _sig(lib, "hz_lmb_create", P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int)
+    _sig(lib, "hz_lmb_submit", c_int, P, P, c_int, c_int, C.c_uint64, P, P, C.POINTER(D))
+    _sig(lib, "hz_lmb_stats", None, P, C.POINTER(U64))
+    _sig(lib, "hz_lmb_destroy", None, P)
     if DEBUG:
         for unit in DEBUG_UNITS:
             _sig(lib, f"hz_debug_poll_{unit}", c_int, C.POINTER(C.c_uint))

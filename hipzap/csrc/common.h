@@ -147,3 +147,34 @@ __device__ __forceinline__ int mx_exp(float amax) {
   frexpf(amax * (1.f / 448.f), &e);
   return e < -127 ? -127 : (e > 127 ? 127 : e);
 }
+
+// ---- Philox4x32-10 Gumbel noise of the AWD-LSTM samplers (csrc/lstm.hip, csrc/lmbatch.hip):
+// the key of vocabulary row j at step t of a request seeded `seed` is logit + gumbel(seed, t, j),
+// the same function in both engines so a request samples the same tokens in either
+__device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0, unsigned k1,
+                                       unsigned& o0) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+    const unsigned h0 = (unsigned)(p0 >> 32), l0 = (unsigned)p0;
+    const unsigned h1 = (unsigned)(p1 >> 32), l1 = (unsigned)p1;
+    const unsigned n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = l1;
+    c2 = n2;
+    c3 = l0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  o0 = c0;
+}
+
+__device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
+  unsigned r;
+  philox((unsigned)j, (unsigned)t, 0x5eedu, 0u, (unsigned)seed, (unsigned)(seed >> 32), r);
+  const float u = ((r >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+  return -__logf(-__logf(u));
+}
+
+

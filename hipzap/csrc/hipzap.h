@@ -171,6 +171,75 @@ int hz_sampler_launch(const HzSamplerParams* p, hipStream_t st);
 // *step += n (one thread): closes a captured run of decode steps
 int hz_step_bump_launch(int* step, int n, hipStream_t st);
 
+// ---- batched AWD-LSTM decode (csrc/lmbatch.hip + csrc/lmserve.cpp) ----
+// Continuous batching for concurrent GET /inference: Bp (16 or 32) request rows share every
+// decode step, so each weight byte is read once per step for all of them. Weights and the
+// recurrent state are fragment-major for mfma_f32_16x16x32_bf16: W as the A operand
+// ([R/16][K/32][64 lanes][8], lane l = row l&15, k 8(l>>4)..+7) and h as the B operand
+// ([K/32][Bp/16][64][8], lane l = request row l&15). h is kept as a bf16 hi/lo pair (hi = bf16(h),
+// lo = bf16(h - hi)): two MFMAs per fragment give ~16 mantissa bits of the fp32 state.
+// Per-step control comes from the host scheduler (row step, forced prompt token or sample, where
+// the token goes): the admit kernel copies it from a pinned host block at each replay start.
+#define HZ_LMB_MAXU 32
+typedef struct HzLmbCtl {     // one (sub-step u, row r) entry, computed by the host
+  int tok;                    // >= 0: forced (prompt) token; -1: sample from the last decoder; -2: idle row
+  int out;                    // sampled token's index in the request's output (-1: none)
+  int dec_t;                  // decoder: step t whose next token is sampled (noise counter), -1: no keys
+  int rec;                    // decoder: 1 = record this row's logits (tests)
+} HzLmbCtl;
+typedef struct HzLmbLayerParams {
+  const unsigned short* w;    // [R/16][(Kh+Kx)/32][64][8] bf16, K order [h_prev | x], rows 4j+q (gate q of unit j)
+  const float* bias;          // [R] fp32 (b_ih + b_hh, same interleave)
+  unsigned short* h;          // this layer's state [2 parity][2 hi/lo][Kh/32][Bp/16][64][8] bf16
+  const unsigned short* x;    // layers > 0: the previous layer's h buffers (its Kh = this Kx)
+  float* c;                   // [Bp][H] fp32 cell state
+  const int* gpar;            // device: h parity of the graph's first sub-step
+  const HzLmbCtl* ctl;        // [U][Bp] (first layer)
+  int H, Kh, Kx, R, Bp, step_off;
+  // first layer: the token of each row (forced, or the argmax of the previous decoder's maxima)
+  // and its embedding as the x operand
+  const unsigned short* emb;  // [Vp/16][Kx/32][64][8] fragment-major embedding (NULL: not first)
+  const unsigned long long* dacc;  // [nblk][Bp] packed (key, row) maxima over acceptable rows
+  int nblk, V;
+  int* const* outp;           // [Bp] request output arrays (pinned host, written by workgroup 0)
+  int* tok;                   // [Bp] this step's tokens (device, diagnostics)
+} HzLmbLayerParams;
+typedef struct HzLmbDecParams {
+  const unsigned short* w;    // [Vp/16][K/32][64][8] bf16 (tied embedding when untied weights are absent)
+  const float* bias;          // [Vp] or NULL
+  const unsigned short* h;    // last layer's h buffers (Kh = K)
+  const int* gpar;
+  const HzLmbCtl* ctl;        // [U][Bp]
+  const unsigned long long* seed;  // [Bp]
+  unsigned long long* dacc;   // [nblk][Bp] -> the next first-layer kernel
+  float* logits;              // [Bp][V] (recorded rows only) or NULL
+  int V, Vp, K, Bp, nblk, step_off, n_exclude, pad_;
+  int exclude[8];
+} HzLmbDecParams;
+typedef struct HzLmbAdmitParams {
+  const int* block;           // pinned host block (csrc/lmserve.cpp layout)
+  HzLmbCtl* ctl;              // [U][Bp] device
+  unsigned long long* seed;   // [Bp]
+  int** outp;                 // [Bp]
+  int* gpar;
+  int Bp, U, n_layers, pad_;
+  unsigned short* h[4];       // per layer: h buffers (zeroed for an admitted row)
+  float* c[4];                // [Bp][H]
+  int Kh[4], H[4];
+} HzLmbAdmitParams;
+int hz_lmb_layer_launch(const HzLmbLayerParams* p, hipStream_t st);
+int hz_lmb_dec_launch(const HzLmbDecParams* p, hipStream_t st);
+int hz_lmb_admit_launch(const HzLmbAdmitParams* p, hipStream_t st);
+int hz_lmb_dec_blocks(int V);  // decoder workgroups (256 vocabulary rows each)
+// scheduler: one worker thread replays the captured U-step program; requests join free rows
+// at replay boundaries and leave when their last token is out (csrc/lmserve.cpp)
+void* hz_lmb_create(HzProgram prog, hipStream_t st, int* host_block, int Bp, int U, int maxp, int maxn,
+                    int* out_pool, float* logits, int V);
+int hz_lmb_submit(void* s, const int* prompt, int P, int n, unsigned long long seed, int* out, float* logits_out,
+                  double* lat_us);
+void hz_lmb_stats(void* s, unsigned long long* out4);  // replays, served, row-steps used, row-steps total
+void hz_lmb_destroy(void* s);
+
 // ---- FP8 (OCP e4m3fn) path (csrc/fp8.hip) ----
 typedef struct HzQuantParams {
   const unsigned short* x;    // [rows][ldx] bf16
@@ -255,7 +324,8 @@ int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t st);
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
-       HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13 };
+       HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
+       HZ_K_LMB_ADMIT = 16 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
 

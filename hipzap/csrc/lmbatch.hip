@@ -1,0 +1,382 @@
+// Batched AWD-LSTM decode: continuous batching of concurrent GET /inference requests
+// (/root/reference/main.py:40-81,84-112 decode loop; VERDICT r2 "next round" #3).
+//
+// The single-request engine (csrc/lstm.hip) streams all ~150 MB of weights for every token of
+// every request. Here Bp request rows (16 or 32) share each decode step, so one pass over the
+// weights serves all of them: every layer and the decoder are skinny GEMMs on the matrix cores
+// (mfma_f32_16x16x32_bf16, A = weight fragment, B = request rows), memory-bound on the weight
+// stream like the GEMV they replace. A step is 1 + L launches:
+//   layer 0   token of every row (forced prompt token, or the argmax of the previous decoder's
+//             per-workgroup maxima -- the exact main.py:63-68 rule, csrc/lstm.hip sample_argmax)
+//             and its embedding as the x operand; gates = W0 [h0_prev ; emb(tok)] + b; cell update
+//   layer l   gates = Wl [hl_prev ; h(l-1)_t] + b; cell update
+//   decoder   logits = E h(L-1)_t + b -> key = logit + Gumbel(seed_r, t_r, v) (common.h, the same
+//             noise as the single-request engine) -> per (workgroup, row) max over acceptable ids
+// Numerics: weights bf16 (as in the single-request engine); the recurrent state is fp32 and
+// enters the MFMAs as a bf16 hi/lo pair (two MFMAs, ~16 mantissa bits), accumulation fp32. Each
+// output element depends only on its own row's operands, so a request's tokens do not depend on
+// which other requests share the batch (tests/test_lmbatch_gpu.py checks bitwise).
+#include "common.h"
+#include "hipzap.h"
+
+HZ_DEBUG_UNIT(lmbatch)
+
+namespace {
+
+constexpr int LW = 8;      // waves per layer workgroup (K split over them)
+constexpr int SPW = 9;     // k-steps (of 32) per wave: K <= 8 * 9 * 32 = 2304
+constexpr int DW = 8;      // decoder waves; 2 vocabulary tiles (32 rows) each
+constexpr int DROWS = DW * 32;  // vocabulary rows per decoder workgroup
+constexpr int DKMAX = 32;  // decoder k-steps (K <= 1024, a multiple of 256)
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// order-preserving (key, row) -> u64; larger is better, ties to the lower row; 0 = nothing
+__device__ __forceinline__ unsigned long long pack_key(float v, int row) {
+  unsigned u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)(0xffffffffu - (unsigned)row);
+}
+__device__ __forceinline__ int key_row(unsigned long long k) { return (int)(0xffffffffu - (unsigned)k); }
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+__device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, int o) {
+  const unsigned lo = __shfl_xor((unsigned)v, o, 64), hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ bf16x8 as_frag(const u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// element offset of (unit/k = j, request row = r) in one [K/32][Bp/16][64][8] state image
+__device__ __forceinline__ int st_off(int j, int r, int NB) {
+  return ((j >> 5) * NB + (r >> 4)) * 512 + ((((j & 31) >> 3) << 4) + (r & 15)) * 8 + (j & 7);
+}
+
+// ------------------------------------------------------------------------ layer kernel
+// One workgroup per 16-row tile (4 hidden units x 4 gates) x all Bp rows; the 8 waves split K.
+// Every load of a wave (its weight fragments, its state fragments) is issued before the first
+// MFMA; partial tiles meet in LDS and 4 x Bp threads apply the cell update.
+template <int NB, bool FIRST>
+__global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p) {
+  __shared__ f32x4 part[LW][NB][64];
+  __shared__ unsigned long long s_best[LW][32];
+  __shared__ int s_tok[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;
+  const int spw = (KS + LW - 1) / LW;
+  const int k0 = wave * spw;
+  const int cnt = max(0, min(spw, KS - k0));
+  const int Bp = NB * 16;
+  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile * 16 < p.R)) return;
+  // ---- loads that need nothing: this sub-step's control + the decoder maxima (FIRST), then the
+  // weight stream; vmcnt retires in issue order, so what the token selection waits for goes first
+  HzLmbCtl cl = {};
+  unsigned long long best = 0;
+  if constexpr (FIRST) {
+    if (tid < Bp) cl = p.ctl[p.step_off * Bp + tid];
+    constexpr int TPT = 16;  // nblk * Bp <= 8192 (checked by the launcher)
+    const int c = tid & (Bp - 1);
+    const int last = (p.nblk - 1) * Bp + c;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) best = umax64(best, p.dacc[min(tid + i * 512, last)]);
+  }
+  u32x4 wf[SPW];
+  const bf16_t* wt = p.w + (size_t)tile * KS * 512 + lane * 8;
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) wf[s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KS - 1) * 512);
+  __builtin_amdgcn_sched_barrier(0);
+  const int par = (*p.gpar + p.step_off) & 1;
+  // state operands: h_prev (own, parity par) for k < Kh; x for k >= Kh (previous layer's output
+  // of this step, parity par ^ 1; FIRST: the embedding rows of the tokens, after selection)
+  u32x4 ah[SPW][NB], al[SPW][NB];
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    const int ks = min(k0 + s, KS - 1);
+    // FIRST: k-steps past Kh are the embedding, loaded after the token selection (a harmless
+    // in-range h fragment here keeps the loop branch-free)
+    const bool hk = FIRST || ks < KSH;
+    const int kh = min(ks, KSH - 1);
+    const bf16_t* src = hk ? p.h + ((size_t)(par * 2) * KSH + kh) * NB * 512
+                           : p.x + ((size_t)((par ^ 1) * 2) * KSX + (ks - KSH)) * NB * 512;
+    const size_t lo_off = (size_t)(hk ? KSH : KSX) * NB * 512;
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+      ah[s][cb] = *reinterpret_cast<const u32x4*>(src + cb * 512 + lane * 8);
+      al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + cb * 512 + lane * 8);
+    }
+  }
+  if constexpr (FIRST) {
+    // ---- token of every row: argmax of the acceptable keys of the last decoder (its maxima per
+    // workgroup), reduced by every workgroup; lanes c, c + Bp, ... of a wave hold the same row
+#pragma unroll
+    for (int o = Bp; o < 64; o <<= 1) best = umax64(best, shfl_xor64(best, o));
+    if (lane < Bp) s_best[wave][lane] = best;
+    lds_barrier();  // LDS only: the weight and state loads stay in flight
+    if (tid < Bp) {
+      unsigned long long b = s_best[0][tid];
+#pragma unroll
+      for (int w = 1; w < LW; ++w) b = umax64(b, s_best[w][tid]);
+      int tok = cl.tok >= 0 ? cl.tok : (cl.tok == -1 && b ? key_row(b) : 0);
+      tok = min(max(tok, 0), p.V - 1);
+      s_tok[tid] = tok;
+      if (tile == 0) {
+        if (p.tok) p.tok[tid] = tok;
+        if (cl.tok == -1 && cl.out >= 0 && p.outp[tid]) p.outp[tid][cl.out] = tok;
+      }
+    }
+    lds_barrier();
+    // embedding fragments of the chosen tokens: lane l holds emb[tok(row l&15)][k 8(l>>4)..+7]
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+      const int ks = min(k0 + s, KS - 1);
+      if (ks >= KSH) {  // wave-uniform
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+          const int tk = s_tok[cb * 16 + (lane & 15)];
+          ah[s][cb] = *reinterpret_cast<const u32x4*>(
+              p.emb + ((size_t)(tk >> 4) * KSX + (ks - KSH)) * 512 + ((lane >> 4) * 16 + (tk & 15)) * 8);
+        }
+      }
+    }
+  }
+  // ---- MFMAs over this wave's k-steps
+  f32x4 acc[NB];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < SPW; ++s) {
+    if (s < cnt) {  // wave-uniform
+      const bool lo = !FIRST || (k0 + s) < KSH;  // the embedding is exact bf16: no lo half
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) {
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[s]), as_frag(ah[s][cb]), acc[cb], 0, 0, 0);
+        if (lo) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[s]), as_frag(al[s][cb]), acc[cb], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) part[wave][cb][lane] = acc[cb];
+  __syncthreads();
+  // ---- cell update: thread (cb, l) owns unit 4*tile + (l >> 4) of request row cb*16 + (l & 15);
+  // its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows 4(l>>4) .. +3)
+  if (tid < NB * 64) {
+    const int cb = tid >> 6, l = tid & 63;
+    f32x4 g = part[0][cb][l];
+#pragma unroll
+    for (int w = 1; w < LW; ++w) g += part[w][cb][l];  // fixed order: deterministic
+    const int j = tile * 4 + (l >> 4), r = cb * 16 + (l & 15);
+    if (j < p.H) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + 4 * j);
+      g += b;
+      const float si = 1.f / (1.f + __expf(-g[0]));
+      const float sf = 1.f / (1.f + __expf(-g[1]));
+      const float so = 1.f / (1.f + __expf(-g[3]));
+      float* cp = p.c + (size_t)r * p.H + j;
+      const float c_new = sf * *cp + si * tanhf(g[2]);
+      const float h_new = so * tanhf(c_new);
+      *cp = c_new;
+      const __bf16 hi = (__bf16)h_new;
+      const __bf16 lo = (__bf16)(h_new - (float)hi);
+      bf16_t* dst = p.h + (size_t)((par ^ 1) * 2) * KSH * NB * 512 + st_off(j, r, NB);
+      dst[0] = __builtin_bit_cast(bf16_t, hi);
+      dst[(size_t)KSH * NB * 512] = __builtin_bit_cast(bf16_t, lo);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ decoder kernel
+// Workgroup = 256 vocabulary rows x all Bp request rows. The whole last-layer state (hi/lo, K <=
+// 1024) is staged once into LDS (fragment-major, lane-linear: 16-B global_load_lds per lane) while
+// the first weight chunk streams in; each wave owns 2 vocabulary tiles and walks K in chunks of 8
+// k-steps with the next chunk's 16 weight fragments in flight.
+template <int NB, int NCH>
+__global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
+  constexpr int CH = 8;         // k-steps per chunk
+  constexpr int KS = NCH * CH;  // K = 256 * NCH
+  constexpr int Bp = NB * 16;
+  __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
+  __shared__ unsigned long long s_best[DW][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int blk = blockIdx.x;
+  if (!HZ_DCHECK(p.K == KS * 32 && p.Bp == Bp)) return;
+  const int tile0 = blk * (DROWS / 16) + wave * 2;
+  const int ntile = p.Vp >> 4;
+  const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
+  const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
+  u32x4 wa[2][CH], wb[2][CH];
+#pragma unroll
+  for (int s = 0; s < CH; ++s) {
+    wa[0][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)s * 512);
+    wb[0][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)s * 512);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int par = (*p.gpar + p.step_off) & 1;
+  // stage the state: KS * 2 * NB fragments of 1 KiB, wave w takes fragments w, w + 8, ...
+  {
+    const bf16_t* src = p.h + (size_t)((par ^ 1) * 2) * KS * NB * 512;  // this step's output of the last layer
+    constexpr int NFRAG = KS * 2 * NB;
+#pragma unroll
+    for (int f0 = 0; f0 < NFRAG; f0 += DW) {
+      const int f = f0 + wave;
+      const int ks = f / (2 * NB), rem = f - ks * 2 * NB, hl = rem / NB, cb = rem - hl * NB;
+      const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 acc[2][NB];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int cur = c & 1;  // compile-time after unrolling: register arrays stay registers
+    if (c + 1 < NCH) {      // next chunk in flight while this one is multiplied
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        wa[cur ^ 1][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)((c + 1) * CH + s) * 512);
+        wb[cur ^ 1][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)((c + 1) * CH + s) * 512);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const int ks = c * CH + s;
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) {
+        const bf16x8 hi = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 0) * NB + cb) * 512 + lane * 8));
+        const bf16x8 lo = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 1) * NB + cb) * 512 + lane * 8));
+        acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wa[cur][s]), hi, acc[0][cb], 0, 0, 0);
+        acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wa[cur][s]), lo, acc[0][cb], 0, 0, 0);
+        acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wb[cur][s]), hi, acc[1][cb], 0, 0, 0);
+        acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wb[cur][s]), lo, acc[1][cb], 0, 0, 0);
+      }
+    }
+  }
+  // ---- epilogue: lane l holds vocabulary rows 16*tile + 4(l>>4) + i of request row cb*16 + (l&15)
+  unsigned long long bst[NB];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) {
+    const int r = cb * 16 + (lane & 15);
+    const HzLmbCtl cl = p.ctl[p.step_off * Bp + r];
+    const unsigned long long seed = p.seed[r];
+    unsigned long long b = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int v = (tile0 + t) * 16 + (lane >> 4) * 4 + i;
+        if (v < p.V) {
+          const float lg = acc[t][cb][i] + (p.bias ? p.bias[v] : 0.f);
+          if (p.logits && cl.rec) p.logits[(size_t)r * p.V + v] = lg;
+          if (cl.dec_t >= 0) {
+            bool ok = v != 0;
+            for (int e = 0; e < p.n_exclude; ++e) ok = ok && v != p.exclude[e];
+            if (ok) b = umax64(b, pack_key(lg + gumbel(seed, cl.dec_t, v), v));
+          }
+        }
+      }
+    b = umax64(b, shfl_xor64(b, 16));
+    b = umax64(b, shfl_xor64(b, 32));
+    bst[cb] = b;
+  }
+  if (lane < 16)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) s_best[wave][cb * 16 + lane] = bst[cb];
+  __syncthreads();
+  if (tid < Bp) {
+    unsigned long long b = s_best[0][tid];
+#pragma unroll
+    for (int w = 1; w < DW; ++w) b = umax64(b, s_best[w][tid]);
+    p.dacc[(size_t)blk * Bp + tid] = b;
+  }
+}
+
+// ------------------------------------------------------------------------ admit kernel
+// First node of every replay: workgroup r copies row r's control for the U sub-steps from the
+// pinned host block and, for a newly admitted request, zeroes the row's recurrent state.
+// Host block (ints): [0] parity of sub-step 0; row r at 8 + r * (8 + 4U): admit flag, seed lo/hi,
+// out pointer lo/hi, 3 spare, then U HzLmbCtl.
+__global__ __launch_bounds__(256) void lmb_admit_kernel(const HzLmbAdmitParams p) {
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int RS = 8 + 4 * p.U;
+  const int* row = p.block + 8 + (size_t)r * RS;
+  __shared__ int s_hdr[8];
+  if (tid < 8) s_hdr[tid] = row[tid];
+  if (tid < 4 * p.U) reinterpret_cast<int*>(p.ctl)[(size_t)(tid >> 2) * p.Bp * 4 + r * 4 + (tid & 3)] = row[8 + tid];
+  if (r == 0 && tid == 0) *p.gpar = p.block[0] & 1;
+  __syncthreads();
+  if (tid == 0) {
+    p.seed[r] = (unsigned long long)(unsigned)s_hdr[1] | ((unsigned long long)(unsigned)s_hdr[2] << 32);
+    p.outp[r] = reinterpret_cast<int*>((unsigned long long)(unsigned)s_hdr[3] | ((unsigned long long)(unsigned)s_hdr[4] << 32));
+  }
+  if (!s_hdr[0]) return;
+  const int NB = p.Bp >> 4;
+  for (int l = 0; l < p.n_layers; ++l) {
+    const int H = p.H[l], Kh = p.Kh[l];
+    for (int j = tid; j < H; j += 256) p.c[l][(size_t)r * H + j] = 0.f;
+    const size_t img = (size_t)Kh * p.Bp;  // elements of one [Kh/32][NB][64][8] image
+    for (int e = tid; e < 4 * Kh; e += 256) {
+      const int im = e / Kh, j = e - im * Kh;  // 4 images: parity x hi/lo
+      p.h[l][im * img + st_off(j, r, NB)] = 0;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int hz_lmb_dec_blocks(int V) { return (V + DROWS - 1) / DROWS; }
+
+extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
+  const HzLmbLayerParams& p = *pp;
+  const bool first = p.emb != nullptr;
+  if (p.Bp != 16 && p.Bp != 32) return -1;
+  if (p.Kh % 32 || p.Kx % 32 || p.Kh < p.H || p.R % 16 || p.R < 4 * p.H || !p.w || !p.bias || !p.h || !p.c || !p.gpar)
+    return -1;
+  const int KS = (p.Kh + p.Kx) / 32;
+  if ((KS + LW - 1) / LW > SPW) return -1;
+  if (first && (!p.ctl || !p.dacc || !p.outp || p.nblk < 1 || p.nblk * p.Bp > 16 * 512 || p.V < 16)) return -1;
+  if (!first && !p.x) return -1;
+  const dim3 grid(p.R / 16), block(512);
+#define HZ_LMBL(NB)                                                                         \
+  if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true>), grid, block, 0, st, p);      \
+  else hipLaunchKernelGGL((lmb_layer_kernel<NB, false>), grid, block, 0, st, p);
+  if (p.Bp == 16) {
+    HZ_LMBL(1)
+  } else {
+    HZ_LMBL(2)
+  }
+#undef HZ_LMBL
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
+  const HzLmbDecParams& p = *pp;
+  if (p.Bp != 16 && p.Bp != 32) return -1;
+  if (p.K % 256 || p.K < 256 || p.K > DKMAX * 32 || p.Vp % 16 || p.Vp < p.V || p.n_exclude < 0 || p.n_exclude > 8)
+    return -1;
+  if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dacc || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
+  const dim3 grid(p.nblk), block(512);
+#define HZ_LMBD(NB, NCH) \
+  case NCH: hipLaunchKernelGGL((lmb_dec_kernel<NB, NCH>), grid, block, 0, st, p); break;
+  if (p.Bp == 16) {
+    switch (p.K / 256) { HZ_LMBD(1, 1) HZ_LMBD(1, 2) HZ_LMBD(1, 3) HZ_LMBD(1, 4) default: return -1; }
+  } else {
+    switch (p.K / 256) { HZ_LMBD(2, 1) HZ_LMBD(2, 2) HZ_LMBD(2, 3) HZ_LMBD(2, 4) default: return -1; }
+  }
+#undef HZ_LMBD
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_lmb_admit_launch(const HzLmbAdmitParams* pp, hipStream_t st) {
+  const HzLmbAdmitParams& p = *pp;
+  if ((p.Bp != 16 && p.Bp != 32) || p.U < 1 || p.U > HZ_LMB_MAXU || p.n_layers < 1 || p.n_layers > 4) return -1;
+  if (!p.block || !p.ctl || !p.seed || !p.outp || !p.gpar) return -1;
+  for (int l = 0; l < p.n_layers; ++l)
+    if (!p.h[l] || !p.c[l] || p.Kh[l] % 32 || p.H[l] > p.Kh[l]) return -1;
+  hipLaunchKernelGGL(lmb_admit_kernel, dim3(p.Bp), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}

@@ -289,6 +289,9 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_GEMM_FP8: return hz_gemm_fp8_launch(static_cast<const HzGemmFp8Params*>(prm), st);
     case HZ_K_SOFTMAX: return hz_softmax_launch(static_cast<const HzSoftmaxParams*>(prm), st);
     case HZ_K_POOL_FC: return hz_pool_fc_launch(static_cast<const HzPoolFcParams*>(prm), st);
+    case HZ_K_LMB_LAYER: return hz_lmb_layer_launch(static_cast<const HzLmbLayerParams*>(prm), st);
+    case HZ_K_LMB_DEC: return hz_lmb_dec_launch(static_cast<const HzLmbDecParams*>(prm), st);
+    case HZ_K_LMB_ADMIT: return hz_lmb_admit_launch(static_cast<const HzLmbAdmitParams*>(prm), st);
     default: return -100;
   }
 }
