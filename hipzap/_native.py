@@ -84,13 +84,13 @@ class LmbCtl(C.Structure):
 class LmbLayerParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("x", c_void_p), ("c", c_void_p),
                 ("gpar", c_void_p), ("ctl", c_void_p), ("H", c_int), ("Kh", c_int), ("Kx", c_int), ("R", c_int),
-                ("Bp", c_int), ("step_off", c_int), ("emb", c_void_p), ("dacc", c_void_p), ("nblk", c_int),
-                ("V", c_int), ("outp", c_void_p), ("tok", c_void_p)]
+                ("Bp", c_int), ("step_off", c_int), ("emb", c_void_p), ("dbest", c_void_p), ("V", c_int),
+                ("pad_", c_int), ("outp", c_void_p), ("tok", c_void_p)]
 
 
 class LmbDecParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("gpar", c_void_p), ("ctl", c_void_p),
-                ("seed", c_void_p), ("dacc", c_void_p), ("logits", c_void_p), ("V", c_int), ("Vp", c_int),
+                ("seed", c_void_p), ("dbest", c_void_p), ("logits", c_void_p), ("V", c_int), ("Vp", c_int),
                 ("K", c_int), ("Bp", c_int), ("nblk", c_int), ("step_off", c_int), ("n_exclude", c_int),
                 ("pad_", c_int), ("exclude", c_int * 8)]
 

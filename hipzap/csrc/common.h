@@ -150,9 +150,10 @@ __device__ __forceinline__ int mx_exp(float amax) {
 
 // ---- Philox4x32-10 Gumbel noise of the AWD-LSTM samplers (csrc/lstm.hip, csrc/lmbatch.hip):
 // the key of vocabulary row j at step t of a request seeded `seed` is logit + gumbel(seed, t, j),
-// the same function in both engines so a request samples the same tokens in either
-__device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0, unsigned k1,
-                                       unsigned& o0) {
+// the same function in both engines so a request samples the same tokens in either. One Philox
+// block (counter (j >> 2, t, 0x5eed, 0), key = seed) yields the noise of the 4 rows 4(j>>2)..+3.
+__device__ __forceinline__ u32x4 philox4(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0,
+                                         unsigned k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
@@ -167,14 +168,22 @@ __device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, un
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  o0 = c0;
+  return u32x4{c0, c1, c2, c3};
 }
 
-__device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
-  unsigned r;
-  philox((unsigned)j, (unsigned)t, 0x5eedu, 0u, (unsigned)seed, (unsigned)(seed >> 32), r);
+__device__ __forceinline__ float gumbel_of(unsigned r) {
   const float u = ((r >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
   return -__logf(-__logf(u));
 }
 
+// noise of rows j0 .. j0+3 (j0 % 4 == 0): one Philox block
+__device__ __forceinline__ f32x4 gumbel4(unsigned long long seed, int t, int j0) {
+  const u32x4 r = philox4((unsigned)j0 >> 2, (unsigned)t, 0x5eedu, 0u, (unsigned)seed, (unsigned)(seed >> 32));
+  return f32x4{gumbel_of(r[0]), gumbel_of(r[1]), gumbel_of(r[2]), gumbel_of(r[3])};
+}
 
+__device__ __forceinline__ float gumbel(unsigned long long seed, int t, int j) {
+  const u32x4 r = philox4((unsigned)j >> 2, (unsigned)t, 0x5eedu, 0u, (unsigned)seed, (unsigned)(seed >> 32));
+  const int q = j & 3;
+  return gumbel_of(q == 0 ? r[0] : q == 1 ? r[1] : q == 2 ? r[2] : r[3]);
+}

@@ -199,8 +199,8 @@ typedef struct HzLmbLayerParams {
   // first layer: the token of each row (forced, or the argmax of the previous decoder's maxima)
   // and its embedding as the x operand
   const unsigned short* emb;  // [Vp/16][Kx/32][64][8] fragment-major embedding (NULL: not first)
-  const unsigned long long* dacc;  // [nblk][Bp] packed (key, row) maxima over acceptable rows
-  int nblk, V;
+  unsigned long long* dbest;  // [2 parity][Bp] running maxima (packed key, row) of the decoder; the
+  int V, pad_;                //   first layer reads the other parity and clears its own
   int* const* outp;           // [Bp] request output arrays (pinned host, written by workgroup 0)
   int* tok;                   // [Bp] this step's tokens (device, diagnostics)
 } HzLmbLayerParams;
@@ -211,7 +211,7 @@ typedef struct HzLmbDecParams {
   const int* gpar;
   const HzLmbCtl* ctl;        // [U][Bp]
   const unsigned long long* seed;  // [Bp]
-  unsigned long long* dacc;   // [nblk][Bp] -> the next first-layer kernel
+  unsigned long long* dbest;  // [2 parity][Bp]: atomic max over acceptable ids -> the next first layer
   float* logits;              // [Bp][V] (recorded rows only) or NULL
   int V, Vp, K, Bp, nblk, step_off, n_exclude, pad_;
   int exclude[8];

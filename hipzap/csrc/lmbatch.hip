@@ -16,6 +16,8 @@
 // enters the MFMAs as a bf16 hi/lo pair (two MFMAs, ~16 mantissa bits), accumulation fp32. Each
 // output element depends only on its own row's operands, so a request's tokens do not depend on
 // which other requests share the batch (tests/test_lmbatch_gpu.py checks bitwise).
+#include <cstdlib>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -57,35 +59,37 @@ __device__ __forceinline__ int st_off(int j, int r, int NB) {
 // One workgroup per 16-row tile (4 hidden units x 4 gates) x all Bp rows; the 8 waves split K.
 // Every load of a wave (its weight fragments, its state fragments) is issued before the first
 // MFMA; partial tiles meet in LDS and 4 x Bp threads apply the cell update.
-template <int NB, bool FIRST>
+template <int NB, bool FIRST, int TPW>
 __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p) {
-  __shared__ f32x4 part[LW][NB][64];
-  __shared__ unsigned long long s_best[LW][32];
+  __shared__ f32x4 part[LW][TPW][NB][64];
   __shared__ int s_tok[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = blockIdx.x;
+  const int tile0 = blockIdx.x * TPW;  // this workgroup's row tiles tile0 .. tile0 + TPW - 1
+  const int ntile = p.R >> 4;
   const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;
   const int spw = (KS + LW - 1) / LW;
   const int k0 = wave * spw;
   const int cnt = max(0, min(spw, KS - k0));
   const int Bp = NB * 16;
-  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile * 16 < p.R)) return;
+  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile0 < ntile)) return;
   // ---- loads that need nothing: this sub-step's control + the decoder maxima (FIRST), then the
   // weight stream; vmcnt retires in issue order, so what the token selection waits for goes first
   HzLmbCtl cl = {};
-  unsigned long long best = 0;
+  unsigned long long best0 = 0, best1 = 0;  // both parities: no wait on the step parity before the weight stream
   if constexpr (FIRST) {
-    if (tid < Bp) cl = p.ctl[p.step_off * Bp + tid];
-    constexpr int TPT = 16;  // nblk * Bp <= 8192 (checked by the launcher)
-    const int c = tid & (Bp - 1);
-    const int last = (p.nblk - 1) * Bp + c;
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) best = umax64(best, p.dacc[min(tid + i * 512, last)]);
+    if (tid < Bp) {
+      cl = p.ctl[p.step_off * Bp + tid];
+      best0 = p.dbest[tid];
+      best1 = p.dbest[Bp + tid];
+    }
   }
-  u32x4 wf[SPW];
-  const bf16_t* wt = p.w + (size_t)tile * KS * 512 + lane * 8;
+  u32x4 wf[TPW][SPW];
 #pragma unroll
-  for (int s = 0; s < SPW; ++s) wf[s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KS - 1) * 512);
+  for (int tt = 0; tt < TPW; ++tt) {
+    const bf16_t* wt = p.w + (size_t)min(tile0 + tt, ntile - 1) * KS * 512 + lane * 8;
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) wf[tt][s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KS - 1) * 512);
+  }
   __builtin_amdgcn_sched_barrier(0);
   const int par = (*p.gpar + p.step_off) & 1;
   // state operands: h_prev (own, parity par) for k < Kh; x for k >= Kh (previous layer's output
@@ -108,25 +112,21 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     }
   }
   if constexpr (FIRST) {
-    // ---- token of every row: argmax of the acceptable keys of the last decoder (its maxima per
-    // workgroup), reduced by every workgroup; lanes c, c + Bp, ... of a wave hold the same row
-#pragma unroll
-    for (int o = Bp; o < 64; o <<= 1) best = umax64(best, shfl_xor64(best, o));
-    if (lane < Bp) s_best[wave][lane] = best;
-    lds_barrier();  // LDS only: the weight and state loads stay in flight
+    // ---- token of every row: the argmax of the acceptable keys of the last decoder (its
+    // workgroups' atomic maxima, buffer of the other parity); workgroup 0 clears this parity's
+    // buffer for this step's decoder
     if (tid < Bp) {
-      unsigned long long b = s_best[0][tid];
-#pragma unroll
-      for (int w = 1; w < LW; ++w) b = umax64(b, s_best[w][tid]);
-      int tok = cl.tok >= 0 ? cl.tok : (cl.tok == -1 && b ? key_row(b) : 0);
+      const unsigned long long best = par ? best0 : best1;
+      int tok = cl.tok >= 0 ? cl.tok : (cl.tok == -1 && best ? key_row(best) : 0);
       tok = min(max(tok, 0), p.V - 1);
       s_tok[tid] = tok;
-      if (tile == 0) {
+      if (tile0 == 0) {
+        p.dbest[(size_t)par * Bp + tid] = 0ull;
         if (p.tok) p.tok[tid] = tok;
         if (cl.tok == -1 && cl.out >= 0 && p.outp[tid]) p.outp[tid][cl.out] = tok;
       }
     }
-    lds_barrier();
+    lds_barrier();  // LDS only: the weight and state loads stay in flight
     // embedding fragments of the chosen tokens: lane l holds emb[tok(row l&15)][k 8(l>>4)..+7]
 #pragma unroll
     for (int s = 0; s < SPW; ++s) {
@@ -142,31 +142,38 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     }
   }
   // ---- MFMAs over this wave's k-steps
-  f32x4 acc[NB];
+  f32x4 acc[TPW][NB];
 #pragma unroll
-  for (int cb = 0; cb < NB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) acc[tt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < SPW; ++s) {
     if (s < cnt) {  // wave-uniform
       const bool lo = !FIRST || (k0 + s) < KSH;  // the embedding is exact bf16: no lo half
 #pragma unroll
-      for (int cb = 0; cb < NB; ++cb) {
-        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[s]), as_frag(ah[s][cb]), acc[cb], 0, 0, 0);
-        if (lo) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[s]), as_frag(al[s][cb]), acc[cb], 0, 0, 0);
-      }
+      for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+          acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(ah[s][cb]), acc[tt][cb], 0, 0, 0);
+          if (lo)
+            acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(al[s][cb]), acc[tt][cb], 0, 0, 0);
+        }
     }
   }
 #pragma unroll
-  for (int cb = 0; cb < NB; ++cb) part[wave][cb][lane] = acc[cb];
-  __syncthreads();
-  // ---- cell update: thread (cb, l) owns unit 4*tile + (l >> 4) of request row cb*16 + (l & 15);
-  // its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows 4(l>>4) .. +3)
-  if (tid < NB * 64) {
-    const int cb = tid >> 6, l = tid & 63;
-    f32x4 g = part[0][cb][l];
+  for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
-    for (int w = 1; w < LW; ++w) g += part[w][cb][l];  // fixed order: deterministic
-    const int j = tile * 4 + (l >> 4), r = cb * 16 + (l & 15);
+    for (int cb = 0; cb < NB; ++cb) part[wave][tt][cb][lane] = acc[tt][cb];
+  __syncthreads();
+  // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row cb*16 + (l & 15);
+  // its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows 4(l>>4) .. +3)
+  if (tid < TPW * NB * 64) {
+    const int tt = tid / (NB * 64), cb = (tid >> 6) % NB, l = tid & 63;
+    f32x4 g = part[0][tt][cb][l];
+#pragma unroll
+    for (int w = 1; w < LW; ++w) g += part[w][tt][cb][l];  // fixed order: deterministic
+    const int j = (tile0 + tt) * 4 + (l >> 4), r = cb * 16 + (l & 15);
     if (j < p.H) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + 4 * j);
       g += b;
@@ -201,8 +208,10 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int blk = blockIdx.x;
   if (!HZ_DCHECK(p.K == KS * 32 && p.Bp == Bp)) return;
-  const int tile0 = blk * (DROWS / 16) + wave * 2;
+  // this workgroup's vocabulary tiles [t_lo, t_hi) (<= 16: 2 per wave)
   const int ntile = p.Vp >> 4;
+  const int t_lo = (int)((long)blk * ntile / p.nblk), t_hi = (int)((long)(blk + 1) * ntile / p.nblk);
+  const int tile0 = t_lo + wave * 2;
   const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
   const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
   u32x4 wa[2][CH], wb[2][CH];
@@ -257,6 +266,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     }
   }
   // ---- epilogue: lane l holds vocabulary rows 16*tile + 4(l>>4) + i of request row cb*16 + (l&15)
+  // (4 consecutive ids: one Philox block gives their noise)
   unsigned long long bst[NB];
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb) {
@@ -265,20 +275,26 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     const unsigned long long seed = p.seed[r];
     unsigned long long b = 0;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+      const int v0 = (tile0 + t) * 16 + (lane >> 4) * 4;
+      if (tile0 + t >= t_hi || v0 >= p.V) continue;
+      f32x4 lg = acc[t][cb];
+      if (p.bias) lg += *reinterpret_cast<const f32x4*>(p.bias + v0);
+      if (p.logits && cl.rec)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int v = (tile0 + t) * 16 + (lane >> 4) * 4 + i;
-        if (v < p.V) {
-          const float lg = acc[t][cb][i] + (p.bias ? p.bias[v] : 0.f);
-          if (p.logits && cl.rec) p.logits[(size_t)r * p.V + v] = lg;
-          if (cl.dec_t >= 0) {
-            bool ok = v != 0;
-            for (int e = 0; e < p.n_exclude; ++e) ok = ok && v != p.exclude[e];
-            if (ok) b = umax64(b, pack_key(lg + gumbel(seed, cl.dec_t, v), v));
-          }
+        for (int i = 0; i < 4; ++i)
+          if (v0 + i < p.V) p.logits[(size_t)r * p.V + v0 + i] = lg[i];
+      if (cl.dec_t >= 0) {
+        const f32x4 gn = gumbel4(seed, cl.dec_t, v0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int v = v0 + i;
+          bool ok = v != 0 && v < p.V;
+          for (int e = 0; e < p.n_exclude; ++e) ok = ok && v != p.exclude[e];
+          if (ok) b = umax64(b, pack_key(lg[i] + gn[i], v));
         }
       }
+    }
     b = umax64(b, shfl_xor64(b, 16));
     b = umax64(b, shfl_xor64(b, 32));
     bst[cb] = b;
@@ -287,11 +303,11 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) s_best[wave][cb * 16 + lane] = bst[cb];
   __syncthreads();
-  if (tid < Bp) {
+  if (tid < Bp) {  // this workgroup's best per request row -> the row's running maximum
     unsigned long long b = s_best[0][tid];
 #pragma unroll
     for (int w = 1; w < DW; ++w) b = umax64(b, s_best[w][tid]);
-    p.dacc[(size_t)blk * Bp + tid] = b;
+    if (b) atomicMax(p.dbest + (size_t)par * Bp + tid, b);
   }
 }
 
@@ -328,7 +344,11 @@ __global__ __launch_bounds__(256) void lmb_admit_kernel(const HzLmbAdmitParams p
 
 }  // namespace
 
-extern "C" int hz_lmb_dec_blocks(int V) { return (V + DROWS - 1) / DROWS; }
+// decoder grid: every CU streams a share (<= 256 workgroups), at most 16 tiles per workgroup
+extern "C" int hz_lmb_dec_blocks(int V) {
+  const int ntile = (V + 15) / 16;
+  return max((ntile + DROWS / 16 - 1) / (DROWS / 16), min(256, (ntile + 1) / 2));
+}
 
 extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
   const HzLmbLayerParams& p = *pp;
@@ -338,16 +358,28 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
     return -1;
   const int KS = (p.Kh + p.Kx) / 32;
   if ((KS + LW - 1) / LW > SPW) return -1;
-  if (first && (!p.ctl || !p.dacc || !p.outp || p.nblk < 1 || p.nblk * p.Bp > 16 * 512 || p.V < 16)) return -1;
+  if (first && (!p.ctl || !p.dbest || !p.outp || p.V < 16)) return -1;
   if (!first && !p.x) return -1;
-  const dim3 grid(p.R / 16), block(512);
-#define HZ_LMBL(NB)                                                                         \
-  if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true>), grid, block, 0, st, p);      \
-  else hipLaunchKernelGGL((lmb_layer_kernel<NB, false>), grid, block, 0, st, p);
+  // tiles per workgroup: 2 halves the state operand each weight byte is paired with (every
+  // workgroup reads all Bp rows' state over its K) and fits the grid in one pass of the CUs
+  const char* tpw_env = getenv("HIPZAP_LMB_TPW");
+  const int tpw = tpw_env && tpw_env[0] == '1' ? 1 : 2;
+  const dim3 grid((p.R / 16 + tpw - 1) / tpw), block(512);
+#define HZ_LMBL(NB, T)                                                                        \
+  if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T>), grid, block, 0, st, p);     \
+  else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T>), grid, block, 0, st, p);
   if (p.Bp == 16) {
-    HZ_LMBL(1)
+    if (tpw == 1) {
+      HZ_LMBL(1, 1)
+    } else {
+      HZ_LMBL(1, 2)
+    }
   } else {
-    HZ_LMBL(2)
+    if (tpw == 1) {
+      HZ_LMBL(2, 1)
+    } else {
+      HZ_LMBL(2, 2)
+    }
   }
 #undef HZ_LMBL
   return (int)hipGetLastError();
@@ -358,7 +390,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if (p.Bp != 16 && p.Bp != 32) return -1;
   if (p.K % 256 || p.K < 256 || p.K > DKMAX * 32 || p.Vp % 16 || p.Vp < p.V || p.n_exclude < 0 || p.n_exclude > 8)
     return -1;
-  if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dacc || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
+  if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
   const dim3 grid(p.nblk), block(512);
 #define HZ_LMBD(NB, NCH) \
   case NCH: hipLaunchKernelGGL((lmb_dec_kernel<NB, NCH>), grid, block, 0, st, p); break;

@@ -138,7 +138,7 @@ class LMBatchEngine:
             self.seed = torch.zeros(Bp, dtype=torch.int64, device=dev)
             self.outp = torch.zeros(Bp, dtype=torch.int64, device=dev)
             self.nblk = lib.hz_lmb_dec_blocks(self.V)
-            self.dacc = torch.zeros(self.nblk * Bp, dtype=torch.int64, device=dev)
+            self.dbest = torch.zeros(2 * Bp, dtype=torch.int64, device=dev)
             self.tok = torch.zeros(Bp, dtype=torch.int32, device=dev)
             self.block = torch.zeros(8 + Bp * (8 + 4 * U), dtype=torch.int32, pin_memory=True)
             self.out_pool = torch.zeros(Bp * max_words, dtype=torch.int32, pin_memory=True)
@@ -159,12 +159,12 @@ class LMBatchEngine:
                 q.gpar, q.ctl = self.gpar.data_ptr(), self.ctl.data_ptr()
                 q.H, q.Kh, q.Kx, q.R, q.Bp = ly["H"], ly["Kh"], ly["Kx"], ly["R"], Bp
                 if i == 0:
-                    q.emb, q.dacc, q.nblk, q.V = packed["emb"].data_ptr(), self.dacc.data_ptr(), self.nblk, self.V
+                    q.emb, q.dbest, q.V = packed["emb"].data_ptr(), self.dbest.data_ptr(), self.V
                     q.outp, q.tok = self.outp.data_ptr(), self.tok.data_ptr()
                 layer_prms.append(q)
             d = N.LmbDecParams()
             d.w, d.bias, d.h = packed["dec"].data_ptr(), packed["dec_bias"].data_ptr(), self.h[-1].data_ptr()
-            d.gpar, d.ctl, d.seed, d.dacc = self.gpar.data_ptr(), self.ctl.data_ptr(), self.seed.data_ptr(), self.dacc.data_ptr()
+            d.gpar, d.ctl, d.seed, d.dbest = self.gpar.data_ptr(), self.ctl.data_ptr(), self.seed.data_ptr(), self.dbest.data_ptr()
             d.logits = self.logits.data_ptr() if self.logits is not None else 0
             d.V, d.Vp, d.K, d.Bp, d.nblk = self.V, packed["Vp"], L[-1]["Kh"], Bp, self.nblk
             d.n_exclude = len(ex)

@@ -39,9 +39,10 @@ def _eager_logits(m, ids):
 
 
 def gumbel_np(seed: int, t: int, V: int) -> np.ndarray:
-    """Host copy of common.h gumbel(seed, t, j) for j = 0..V-1 (Philox4x32-10)."""
+    """Host copy of common.h gumbel(seed, t, j) for j = 0..V-1 (Philox4x32-10, one block per 4 ids)."""
     M = np.uint64(0xFFFFFFFF)
-    c0 = np.arange(V, dtype=np.uint64)
+    j = np.arange(V, dtype=np.uint64)
+    c0 = j >> np.uint64(2)
     c1 = np.full(V, t & 0xFFFFFFFF, np.uint64)
     c2 = np.full(V, 0x5EED, np.uint64)
     c3 = np.zeros(V, np.uint64)
@@ -54,7 +55,8 @@ def gumbel_np(seed: int, t: int, V: int) -> np.ndarray:
         c0, c1, c2, c3 = h1 ^ c1 ^ k0, l1, h0 ^ c3 ^ k1, l0
         k0 = (k0 + np.uint64(0x9E3779B9)) & M
         k1 = (k1 + np.uint64(0xBB67AE85)) & M
-    u = ((c0 >> np.uint64(8)).astype(np.float64) + 0.5) / 16777216.0
+    r = np.choose((j & np.uint64(3)).astype(np.int64), [c0, c1, c2, c3])
+    u = ((r >> np.uint64(8)).astype(np.float64) + 0.5) / 16777216.0
     return -np.log(-np.log(u))
 
 
