@@ -17,7 +17,7 @@ DEBUG = os.environ.get("HIPZAP_DEBUG") == "1"
 _LIB_PATH = Path(__file__).resolve().parent / "_lib" / ("libhipzap_debug.so" if DEBUG else "libhipzap.so")
 if os.environ.get("HIPZAP_LIB"):  # same-box A/B of two builds (scripts/ab_lib.sh)
     _LIB_PATH = Path(os.environ["HIPZAP_LIB"]).resolve()
-DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch")
+DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch", "pack")
 _lock = threading.Lock()
 _lib = None
 
@@ -102,6 +102,13 @@ class LmbAdmitParams(C.Structure):
 
 
 HZ_K_LMB_LAYER, HZ_K_LMB_DEC, HZ_K_LMB_ADMIT = 14, 15, 16
+
+
+class PackConvParams(C.Structure):  # csrc/pack.hip (torch-free checkpoint cold start)
+    _fields_ = [("w", c_void_p), ("gamma", c_void_p), ("beta", c_void_p), ("mean", c_void_p), ("var", c_void_p),
+                ("bias_in", c_void_p), ("wf", c_void_p), ("bias_out", c_void_p), ("cout", c_int), ("cin", c_int),
+                ("r", c_int), ("s", c_int), ("cin_p", c_int), ("rows", c_int), ("ksteps", c_int), ("pad_", c_int),
+                ("eps", c_double)]
 
 HH_ROWS = 16  # HZ_HH_ROWS (hipzap.h): rows per recurrent-partial workgroup of the decoder kernel
 
@@ -190,6 +197,8 @@ def _load():
     _sig(lib, "hz_http_respond", None, P, c_int, C.c_char_p, U64, C.c_char_p, U64)
     _sig(lib, "hz_http_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_http_stop", C.c_int, P)
+    _sig(lib, "hz_pack_conv_launch", c_int, C.POINTER(PackConvParams), P)
+    _sig(lib, "hz_upload_file", c_int, C.c_char_p, c_int, C.POINTER(U64), C.POINTER(U64), C.POINTER(c_void_p), P)
     _sig(lib, "hz_lmb_layer_launch", c_int, C.POINTER(LmbLayerParams), P)
     _sig(lib, "hz_lmb_dec_launch", c_int, C.POINTER(LmbDecParams), P)
     _sig(lib, "hz_lmb_admit_launch", c_int, C.POINTER(LmbAdmitParams), P)

@@ -155,9 +155,41 @@ def build_tools(verbose: bool = True) -> list[Path]:
     return out
 
 
+# weightless plan templates (engine/plan.py export_template): the torch-free .pth cold start of
+# these architectures (hipzap/lite.py PlanEngine.from_checkpoint). (model, classes, batch, contexts)
+TEMPLATES = [("resnet50", 1000, 1, 1), ("resnet18", 1000, 1, 1)]
+
+
+def build_templates(verbose: bool = True) -> list[Path]:
+    """Write the plan templates that are missing or stale (native ABI or lowering code changed).
+    Needs torch on the build host (CPU only), never at serving time."""
+    build(verbose=False)
+    from .lite import code_stamp, lib, plan_usable, read_meta, template_path
+    stamp = code_stamp()
+    out = []
+    for model, ncls, batch, ctx in TEMPLATES:
+        p = Path(template_path(model, batch, ctx, ncls, True))
+        if p.exists() and plan_usable(str(p)) and read_meta(str(p)).get("code_stamp") == stamp:
+            if verbose:
+                print(f"hipzap: {p} up to date")
+            out.append(p)
+            continue
+        p.parent.mkdir(parents=True, exist_ok=True)
+        from .engine.plan import export_template
+        export_template(model, ncls, batch, ctx, True, str(p))
+        if verbose:
+            print(f"hipzap: built template {p} (abi {lib().hz_abi_version():x}, code {stamp})")
+        out.append(p)
+    return out
+
+
 if __name__ == "__main__":
+    if "--templates" in sys.argv[1:]:
+        build_templates(verbose=True)
+        sys.exit(0)
     build(verbose=True, debug="--debug" in sys.argv[1:])
     if "--debug" not in sys.argv[1:]:
         build_comm(verbose=True)
         build_tools(verbose=True)
+        build_templates(verbose=True)
     sys.exit(0)

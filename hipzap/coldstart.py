@@ -3,6 +3,8 @@
     python -m hipzap.coldstart plan <file.hzplan> [--device D]          torch-free plan image
     python -m hipzap.coldstart pth <ckpt.pth> --model resnet50           torch.load + pack path
     python -m hipzap.coldstart hzpack <ckpt.pth> --model resnet50        packed safetensors path
+    python -m hipzap.coldstart pth-lite <ckpt.pth>                       the .pth without torch:
+        weights-only zip reader + plan template + device-side packing (PlanEngine.from_checkpoint)
 
 ``measure_fresh("native", plan)`` spawns the Python-free ``hipzap-serve-plan PLAN --once IMAGE``
 (csrc/tools/serve_plan.cpp) instead: exec -> HIP init -> plan upload -> one eager request.
@@ -41,6 +43,24 @@ def run_plan(path: str, device: int) -> dict:
             "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3, "import_lite": (t_lib - t_imp) * 1e3,
                           **{k: round(v, 3) for k, v in eng.timings.items()},
                           "first_request": (t_first - t_ready) * 1e3}}
+
+
+def run_pth_lite(ckpt: str, device: int) -> dict:
+    t_imp = time.time()
+    from hipzap.lite import PlanEngine
+    t_lib = time.time()
+    eng = PlanEngine.from_checkpoint(ckpt, device=device, contexts=1,
+                                     capture="lazy" if os.environ.get("HIPZAP_PLAN_LAZY_CAPTURE", "1") == "1" else True)
+    t_ready = time.time()
+    out = eng.infer_raw(os.urandom(eng.in_specs[0]["bytes"]))
+    t_first = time.time()
+    import math
+    ok = all(math.isfinite(v) for v in out)
+    return {"mode": "pth-lite", "t_first": t_first, "ok": ok, "torch_imported": "torch" in sys.modules,
+            "numpy_imported": "numpy" in sys.modules,
+            "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3, "import_lite": (t_lib - t_imp) * 1e3,
+                          **{k: round(v, 3) for k, v in eng.timings.items() if isinstance(v, (int, float))},
+                          "engine_total": (t_ready - t_lib) * 1e3, "first_request": (t_first - t_ready) * 1e3}}
 
 
 def run_torch(ckpt: str, model: str, device: int, packed: bool) -> dict:
@@ -116,19 +136,21 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
             "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2),
             "all_ms": [round(w, 1) for w in walls],
             "median_trial_phases_ms": {k: round(v, 2) for k, v in med["phases_ms"].items()},
-            "torch_imported": med.get("torch_imported", mode not in ("plan", "native"))}
+            "torch_imported": med.get("torch_imported", mode not in ("plan", "native", "pth-lite"))}
 
 
 def main(argv=None) -> int:
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["plan", "pth", "hzpack"])
+    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite"])
     ap.add_argument("path")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--device", type=int, default=0)
     a = ap.parse_args(argv)
     if a.mode == "plan":
         res = run_plan(a.path, a.device)
+    elif a.mode == "pth-lite":
+        res = run_pth_lite(a.path, a.device)
     else:
         res = run_torch(a.path, a.model, a.device, packed=a.mode == "hzpack")
     res["t_interp"] = T0

@@ -240,6 +240,25 @@ int hz_lmb_submit(void* s, const int* prompt, int P, int n, unsigned long long s
 void hz_lmb_stats(void* s, unsigned long long* out4);  // replays, served, row-steps used, row-steps total
 void hz_lmb_destroy(void* s);
 
+// ---- device-side packing of raw checkpoint tensors (csrc/pack.hip; torch-free .pth cold start) ----
+typedef struct HzPackConvParams {
+  const float* w;             // OIHW fp32, contiguous (a Linear weight is [cout][cin] with r = s = 1)
+  const float* gamma;         // eval BatchNorm (fp32 [cout]) to fold, or NULL
+  const float* beta;
+  const float* mean;
+  const float* var;
+  const float* bias_in;       // [cout] or NULL
+  unsigned short* wf;         // packed bf16 [rows/16][ksteps][64][8]
+  float* bias_out;            // [cout] fp32
+  int cout, cin, r, s, cin_p, rows, ksteps, pad_;
+  double eps;
+} HzPackConvParams;
+int hz_pack_conv_launch(const HzPackConvParams* p, hipStream_t st);
+// file byte ranges -> device memory (csrc/plan.cpp): pread into two pinned staging buffers, DMA
+// chunk i while reading chunk i+1; synchronous on `st`
+int hz_upload_file(const char* path, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,
+                   void* st);
+
 // ---- FP8 (OCP e4m3fn) path (csrc/fp8.hip) ----
 typedef struct HzQuantParams {
   const unsigned short* x;    // [rows][ldx] bf16

@@ -31,6 +31,7 @@ constexpr int DW = 8;      // decoder waves; 2 vocabulary tiles (32 rows) each
 constexpr int DROWS = DW * 32;  // vocabulary rows per decoder workgroup
 constexpr int DKMAX = 32;  // decoder k-steps (K <= 1024, a multiple of 256)
 
+
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -116,12 +117,14 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     // workgroups' atomic maxima, buffer of the other parity); workgroup 0 clears this parity's
     // buffer for this step's decoder
     if (tid < Bp) {
+      // (measured: sharding these maxima over 8 atomic slots made this kernel 1.3 us slower and
+      // the decoder no faster, profiles/r3_lmbatch)
       const unsigned long long best = par ? best0 : best1;
       int tok = cl.tok >= 0 ? cl.tok : (cl.tok == -1 && best ? key_row(best) : 0);
       tok = min(max(tok, 0), p.V - 1);
       s_tok[tid] = tok;
       if (tile0 == 0) {
-        p.dbest[(size_t)par * Bp + tid] = 0ull;
+        p.dbest[(size_t)par * Bp + tid] = 0ull;  // for this step's decoder
         if (p.tok) p.tok[tid] = tok;
         if (cl.tok == -1 && cl.out >= 0 && p.outp[tid]) p.outp[tid][cl.out] = tok;
       }
@@ -205,6 +208,8 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int Bp = NB * 16;
   __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
   __shared__ unsigned long long s_best[DW][32];
+  __shared__ __attribute__((aligned(16))) HzLmbCtl s_ctl[32];
+  __shared__ __attribute__((aligned(16))) unsigned long long s_seed[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int blk = blockIdx.x;
   if (!HZ_DCHECK(p.K == KS * 32 && p.Bp == Bp)) return;
@@ -214,13 +219,15 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   const int tile0 = t_lo + wave * 2;
   const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
   const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
+  // weight chunks of 8 k-steps (16 fragments per wave), two in flight: chunk c + 2 is issued
+  // into chunk c's registers as soon as chunk c is multiplied, so every wait leaves the next
+  // chunk streaming (the compiler's vmcnt counts retire in issue order)
   u32x4 wa[2][CH], wb[2][CH];
 #pragma unroll
   for (int s = 0; s < CH; ++s) {
     wa[0][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)s * 512);
     wb[0][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)s * 512);
   }
-  __builtin_amdgcn_sched_barrier(0);
   const int par = (*p.gpar + p.step_off) & 1;
   // stage the state: KS * 2 * NB fragments of 1 KiB, wave w takes fragments w, w + 8, ...
   {
@@ -234,8 +241,46 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // the rows' control and seeds go to LDS the same way (an ordinary load here would make hipcc
+  // wait for vmcnt(0) at its first use while the global_load_lds are in flight)
+  if (wave == DW - 1) {
+    if (lane < Bp)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p.ctl + p.step_off * Bp + lane), (lds_void*)s_ctl,
+                                       16, 0, 0);
+    if (lane < Bp / 2)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p.seed + 2 * lane), (lds_void*)s_seed, 16, 0, 0);
+  }
+  if constexpr (NCH > 1) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      wa[1][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)(CH + s) * 512);
+      wb[1][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)(CH + s) * 512);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // the staged state is complete once everything issued before chunk 1 has landed (every wave),
+  // chunk 1 keeps streaming across the barrier
+  if constexpr (NCH > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  // the Gumbel noise of this wave's rows does not depend on the logits: compute it (VALU) while
+  // chunk 1 streams (after the barrier: with a global_load_lds in flight hipcc would wait for
+  // vmcnt(0) at the first use of the control loads)
+  int dt[NB];
+  bool rec[NB];
+  f32x4 gn[2][NB];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb) {
+    const int r = cb * 16 + (lane & 15);
+    const HzLmbCtl cl = s_ctl[r];
+    dt[cb] = cl.dec_t;
+    rec[cb] = cl.rec != 0;
+    const unsigned long long sd = s_seed[r];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      gn[t][cb] = dt[cb] >= 0 ? gumbel4(sd, dt[cb], (tile0 + t) * 16 + (lane >> 4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   f32x4 acc[2][NB];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -244,13 +289,6 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int cur = c & 1;  // compile-time after unrolling: register arrays stay registers
-    if (c + 1 < NCH) {      // next chunk in flight while this one is multiplied
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        wa[cur ^ 1][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)((c + 1) * CH + s) * 512);
-        wb[cur ^ 1][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)((c + 1) * CH + s) * 512);
-      }
-    }
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       const int ks = c * CH + s;
@@ -264,6 +302,15 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
         acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wb[cur][s]), lo, acc[1][cb], 0, 0, 0);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // chunk c's MFMAs are done with its registers
+    if (c + 2 < NCH) {  // refill this chunk's registers with chunk c + 2
+#pragma unroll
+      for (int s = 0; s < CH; ++s) {
+        wa[cur][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)((c + 2) * CH + s) * 512);
+        wb[cur][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)((c + 2) * CH + s) * 512);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
   // ---- epilogue: lane l holds vocabulary rows 16*tile + 4(l>>4) + i of request row cb*16 + (l&15)
   // (4 consecutive ids: one Philox block gives their noise)
@@ -271,8 +318,6 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb) {
     const int r = cb * 16 + (lane & 15);
-    const HzLmbCtl cl = p.ctl[p.step_off * Bp + r];
-    const unsigned long long seed = p.seed[r];
     unsigned long long b = 0;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -280,18 +325,17 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       if (tile0 + t >= t_hi || v0 >= p.V) continue;
       f32x4 lg = acc[t][cb];
       if (p.bias) lg += *reinterpret_cast<const f32x4*>(p.bias + v0);
-      if (p.logits && cl.rec)
+      if (p.logits && rec[cb])
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (v0 + i < p.V) p.logits[(size_t)r * p.V + v0 + i] = lg[i];
-      if (cl.dec_t >= 0) {
-        const f32x4 gn = gumbel4(seed, cl.dec_t, v0);
+      if (dt[cb] >= 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int v = v0 + i;
           bool ok = v != 0 && v < p.V;
           for (int e = 0; e < p.n_exclude; ++e) ok = ok && v != p.exclude[e];
-          if (ok) b = umax64(b, pack_key(lg[i] + gn[i], v));
+          if (ok) b = umax64(b, pack_key(lg[i] + gn[t][cb][i], v));
         }
       }
     }

@@ -1,0 +1,82 @@
+// Device-side weight packing for the torch-free checkpoint cold start (hipzap/lite.py
+// PlanEngine.from_checkpoint; VERDICT r2 "next round" #4): the raw fp32 tensors of a torch.save
+// checkpoint are copied to the GPU as they are stored, and this kernel produces the packed
+// layout the conv/GEMM kernels read -- the same bytes as hipzap/ops/conv.py pack_conv /
+// pack_linear on the host:
+//   * eval BatchNorm folded: scale = float(double(gamma) / sqrt(double(var) + eps)) (rounded once,
+//     as ops/conv.py fold_bn), w' = w * scale, b' = (0 - mean) * scale + beta in IEEE fp32
+//     (no FMA contraction: __fmul_rn / __fadd_rn);
+//   * OIHW -> row-major [cout][R*S*Cin_pad] (K order R, S, C; channels zero-padded), K padded to 32,
+//     rows to `rows`; bf16 round-to-nearest-even (NaN -> 0x7FC0, torch's conversion);
+//   * fragment-major [rows/16][K/32][64 lanes][8] (lane l = row l&15, k 8(l>>4)..+7 of the step).
+// One thread writes one lane's 16 bytes; a second grid-stride pass writes the fp32 bias.
+#include <algorithm>
+
+#include "common.h"
+#include "hipzap.h"
+
+HZ_DEBUG_UNIT(pack)
+
+namespace {
+
+__device__ __forceinline__ unsigned short bf16_rne(float f) {
+  const unsigned u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0x7FC0;  // NaN
+  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float bn_scale(const HzPackConvParams& p, int row) {
+  if (!p.gamma) return 1.f;
+  return (float)((double)p.gamma[row] / sqrt((double)p.var[row] + p.eps));
+}
+
+__global__ __launch_bounds__(256) void pack_conv_kernel(const HzPackConvParams p) {
+  const long nchunk = (long)(p.rows / 16) * p.ksteps * 64;
+  const int K = p.r * p.s * p.cin_p, SC = p.s * p.cin_p;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < nchunk; idx += (long)gridDim.x * blockDim.x) {
+    const int lane = (int)(idx & 63);
+    const long tk = idx >> 6;
+    const int ks = (int)(tk % p.ksteps), tile = (int)(tk / p.ksteps);
+    const int row = tile * 16 + (lane & 15);
+    const int k0 = ks * 32 + 8 * (lane >> 4);
+    unsigned short v[8];
+    const bool live = row < p.cout;
+    const float sc = live ? bn_scale(p, row) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float x = 0.f;
+      if (live && k < K) {
+        const int rr = k / SC, rem = k - rr * SC, ss = rem / p.cin_p, c = rem - ss * p.cin_p;
+        if (c < p.cin) {
+          x = p.w[(((long)row * p.cin + c) * p.r + rr) * p.s + ss];
+          if (p.gamma) x = __fmul_rn(x, sc);
+        }
+      }
+      v[j] = bf16_rne(x);
+    }
+    u32x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (unsigned)v[2 * i] | ((unsigned)v[2 * i + 1] << 16);
+    *reinterpret_cast<u32x4*>(p.wf + idx * 8) = o;
+  }
+  for (long row = (long)blockIdx.x * blockDim.x + threadIdx.x; row < p.cout; row += (long)gridDim.x * blockDim.x) {
+    float b = p.bias_in ? p.bias_in[row] : 0.f;
+    if (p.gamma) b = __fadd_rn(__fmul_rn(__fsub_rn(b, p.mean[row]), bn_scale(p, (int)row)), p.beta[row]);
+    p.bias_out[row] = b;
+  }
+}
+
+}  // namespace
+
+extern "C" int hz_pack_conv_launch(const HzPackConvParams* pp, hipStream_t st) {
+  const HzPackConvParams& p = *pp;
+  if (!p.w || !p.wf || !p.bias_out || p.cout < 1 || p.cin < 1 || p.r < 1 || p.s < 1 || p.cin_p < p.cin ||
+      p.rows % 16 || p.rows < p.cout || p.ksteps * 32 < p.r * p.s * p.cin_p)
+    return -1;
+  if (p.gamma && (!p.beta || !p.mean || !p.var)) return -1;
+  const long nchunk = (long)(p.rows / 16) * p.ksteps * 64;
+  const int blocks = (int)std::min<long>(2048, std::max<long>((nchunk + 255) / 256, (p.cout + 255) / 256));
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(blocks), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}

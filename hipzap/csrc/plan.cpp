@@ -27,6 +27,9 @@
 namespace {
 
 constexpr uint32_t kPlanVersion = 1;
+// flags: the file carries no weight bytes (a template: engine/plan.py export_template); the blob
+// is filled by the caller, e.g. by packing a .pth checkpoint on the device (csrc/pack.hip)
+constexpr uint64_t kFlagWeightless = 1;
 constexpr char kMagic[8] = {'H', 'Z', 'P', 'L', 'A', 'N', '0', '1'};
 
 // file header: magic + 15 little-endian u64 fields (see plan.py PlanHeader)
@@ -129,7 +132,8 @@ struct Plan {
     if (h.abi != hz_abi_version())
       return fail("plan: written for a different native ABI (" + std::to_string(h.abi) + " != " +
                   std::to_string(hz_abi_version()) + "); re-export it");
-    if (h.ops_off + h.ops_len > map_len || h.blob_off + h.blob_len > map_len) return fail("plan: truncated file");
+    if (h.ops_off + h.ops_len > map_len || (!(h.flags & kFlagWeightless) && h.blob_off + h.blob_len > map_len))
+      return fail("plan: truncated file");
     const uint8_t* p = map + h.ops_off;
     const uint8_t* end = p + h.ops_len;
     ops.reserve(h.n_ops);
@@ -415,6 +419,48 @@ uint64_t hz_abi_version(void) {
 
 const char* hz_plan_last_error(void) { return g_err.c_str(); }
 
+// file byte ranges -> device pointers: pread into two pinned 4-MiB staging buffers, the DMA of
+// chunk i overlapping the read of chunk i+1 (the plan blob upload's scheme); synchronous
+int hz_upload_file(const char* path, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,
+                   void* stream) {
+  g_err.clear();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return fail(std::string("upload: cannot open ") + path);
+  const size_t chunk = size_t(4) << 20;
+  void* stage[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  bool ok = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
+            hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
+  int k = 0;
+  size_t issued = 0;
+  for (int i = 0; ok && i < n; ++i) {
+    for (uint64_t off = 0; ok && off < nbytes[i]; off += chunk, k ^= 1, ++issued) {
+      const size_t m = nbytes[i] - off < chunk ? nbytes[i] - off : chunk;
+      if (issued >= 2) ok = hipEventSynchronize(done[k]) == hipSuccess;  // staging buffer k free again
+      if (!ok) break;
+      size_t got = 0;
+      while (got < m) {
+        const ssize_t r = pread(fd, static_cast<uint8_t*>(stage[k]) + got, m - got, (off_t)(file_off[i] + off + got));
+        if (r <= 0) break;
+        got += (size_t)r;
+      }
+      ok = got == m &&
+           hipMemcpyAsync(static_cast<uint8_t*>(dst[i]) + off, stage[k], m, hipMemcpyHostToDevice, st) == hipSuccess &&
+           hipEventRecord(done[k], st) == hipSuccess;
+    }
+  }
+  if (ok) ok = hipStreamSynchronize(st) == hipSuccess;
+  for (int i = 0; i < 2; ++i) {
+    if (done[i]) (void)hipEventDestroy(done[i]);
+    if (stage[i]) (void)hipHostFree(stage[i]);
+  }
+  close(fd);
+  return ok ? 0 : fail("upload: read or copy failed");
+}
+
 void* hz_plan_open(const char* path, int device, int read_blob, double* timings) {
   g_err.clear();
   double t0 = now_ms();
@@ -440,8 +486,14 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
     delete p;
     return nullptr;
   }
+  if ((p->h.flags & kFlagWeightless) && read_blob) {
+    fail("plan: weightless template (its blob comes from a checkpoint: open with read_blob = 0)");
+    delete p;
+    return nullptr;
+  }
   // the weights are read once, sequentially
-  madvise(p->map + (p->h.blob_off & ~size_t(4095)), p->h.blob_len, MADV_SEQUENTIAL | MADV_WILLNEED);
+  if (!(p->h.flags & kFlagWeightless))
+    madvise(p->map + (p->h.blob_off & ~size_t(4095)), p->h.blob_len, MADV_SEQUENTIAL | MADV_WILLNEED);
   double t1 = now_ms();
   p->t[HZ_PLAN_T_PARSE] = t1 - t0;
   // first HIP call of a fresh process: runtime + device initialisation

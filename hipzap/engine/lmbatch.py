@@ -138,7 +138,7 @@ class LMBatchEngine:
             self.seed = torch.zeros(Bp, dtype=torch.int64, device=dev)
             self.outp = torch.zeros(Bp, dtype=torch.int64, device=dev)
             self.nblk = lib.hz_lmb_dec_blocks(self.V)
-            self.dbest = torch.zeros(2 * Bp, dtype=torch.int64, device=dev)
+            self.dbest = torch.zeros(2 * Bp, dtype=torch.int64, device=dev)  # [parity][row]
             self.tok = torch.zeros(Bp, dtype=torch.int32, device=dev)
             self.block = torch.zeros(8 + Bp * (8 + 4 * U), dtype=torch.int32, pin_memory=True)
             self.out_pool = torch.zeros(Bp * max_words, dtype=torch.int32, pin_memory=True)

@@ -41,6 +41,7 @@ OPHDR = struct.Struct("<IiiIII")   # OpHeader
 RELOC = struct.Struct("<IIQ")      # Reloc
 OP_CONV, OP_CONV2, OP_MAXPOOL, OP_AVGPOOL, OP_PREPROCESS, OP_MEMCPY, OP_KERNEL, OP_FORK, OP_JOIN = range(1, 10)
 BLOB_ALIGN = 4096
+FLAG_WEIGHTLESS = 1  # csrc/plan.cpp kFlagWeightless
 
 
 class AvgpoolArgs(C.Structure):
@@ -131,13 +132,14 @@ def _pointer_fields(st) -> list[tuple[int, int]]:
 
 
 def _tensors(obj):
+    """(field name, tensor) of a packed parameter (None for a bare tensor)."""
     if torch.is_tensor(obj):
-        yield obj
+        yield None, obj
     elif dataclasses.is_dataclass(obj):
         for f in dataclasses.fields(obj):
             v = getattr(obj, f.name)
             if torch.is_tensor(v):
-                yield v
+                yield f.name, v
 
 
 class _Regions:
@@ -149,7 +151,9 @@ class _Regions:
         self.blob_items: list = []  # (offset, storage bytes as uint8 tensor)
         self._seen: set = set()
 
-    def add(self, t: torch.Tensor, region: int, keep_bytes: bool):
+    def add(self, t: torch.Tensor, region: int, keep_bytes: bool, label=None):
+        """``label``: (parameter name, field) of a packed-parameter storage (weightless templates
+        place it by name), None for a constant (its bytes travel in the template)."""
         st = t.untyped_storage()
         ptr, nb = st.data_ptr(), st.nbytes()
         if nb == 0 or (ptr, region) in self._seen:
@@ -159,7 +163,9 @@ class _Regions:
         self.size[region] = off + nb
         self.spans.append((ptr, ptr + nb, region, off))
         if keep_bytes:
-            self.blob_items.append((off, torch.empty(0, dtype=torch.uint8).set_(st, 0, (nb,), (1,))))
+            if label is not None and nb != t.numel() * t.element_size():
+                label = None  # a view into a larger storage: ship its bytes instead
+            self.blob_items.append((off, torch.empty(0, dtype=torch.uint8).set_(st, 0, (nb,), (1,)), label))
 
     def resolve(self, v: int) -> tuple[int, int] | None:
         for start, end, region, off in self.spans:
@@ -174,12 +180,17 @@ def _dtype_name(dt: torch.dtype) -> str:
 
 def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int = 1, contexts: int = 1,
                 zero_copy: str = "all", probs: bool = False, tuned: dict | None = None,
-                source: dict | None = None, host_io: bool = True) -> dict:
+                source: dict | None = None, host_io: bool = True, weightless: bool = False,
+                extra_meta: dict | None = None) -> dict:
     """Write a plan image for ``model`` with CPU-resident packed ``params`` (``adapter.pack(sd,
     "cpu")``). ``contexts``: the request concurrency the launch configs are tuned for (the conv
     tables differ for 1 vs 24 streams); any number of contexts can be instantiated at load.
     ``host_io``: request I/O in pinned host memory (serving, zero-copy by default); False: the
     inputs/outputs live in the context's device block (a DP shard fed by an RCCL scatter).
+    ``weightless``: a TEMPLATE -- no weight bytes in the file; ``meta["blob_map"]`` says where each
+    packed parameter's storage goes in the blob (its name and field), ``meta["blob_consts"]`` carries
+    the few constant storages (preprocess mean/std) inline; the loader fills the blob itself
+    (hipzap/lite.py ``PlanEngine.from_checkpoint``: device-side packing of a .pth).
     Returns the metadata dict stored in the file."""
     adapter = registry.get(model)
     g = adapter.build_graph(batch=batch, **arch_kw)
@@ -191,9 +202,9 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
     ctx = ExecContext(g, params, torch.device("cpu"), tuned, host_io=host_io, zero_copy=zero_copy if host_io else "",
                       lib=rec)
     regs = _Regions()
-    for obj in params.values():
-        for t in _tensors(obj):
-            regs.add(t, 0, True)
+    for key, obj in params.items():
+        for field, t in _tensors(obj):
+            regs.add(t, 0, True, label=(key, field))
     for t in ctx._keep:
         regs.add(t, 0, True)
     host = (list(ctx.host_inputs) + [ctx.host_output]) if host_io else []
@@ -227,11 +238,11 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
 
     # compact the blob to the referenced storages
     keep = []
-    for off, data in regs.blob_items:
+    for off, data, label in regs.blob_items:
         if any(off <= r_off < off + max(1, data.numel()) for (_, r_off) in used_blob):
-            keep.append((off, data))
+            keep.append((off, data, label))
     remap, blob_len = {}, 0
-    for off, data in keep:
+    for off, data, _ in keep:
         new = (blob_len + 255) // 256 * 256
         remap[off] = (new, data.numel())
         blob_len = new + data.numel()
@@ -269,17 +280,27 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
     }
     import hashlib
     h = hashlib.sha256()
-    for old, data in keep:  # digest of the blob exactly as written (offsets + bytes)
+    for old, data, _ in keep:  # digest of the blob exactly as written (offsets + bytes)
         h.update(remap[old][0].to_bytes(8, "little"))
         h.update(data.numpy().tobytes())
     meta["blob_sha256"] = h.hexdigest()
+    if weightless:
+        import base64
+        meta["weightless"] = True
+        meta["blob_map"] = {f"{label[0]}/{label[1]}": [remap[old][0], remap[old][1]]
+                            for old, data, label in keep if label is not None}
+        meta["blob_consts"] = [[remap[old][0], base64.b64encode(data.numpy().tobytes()).decode()]
+                               for old, data, label in keep if label is None]
+        del meta["blob_sha256"]  # no weights: nothing to digest
+    if extra_meta:
+        meta.update(extra_meta)
     meta_b = json.dumps(meta).encode()
     meta_off = HEADER.size
     ops_off = (meta_off + len(meta_b) + 7) // 8 * 8
     b_off = (ops_off + len(ops_bytes) + BLOB_ALIGN - 1) // BLOB_ALIGN * BLOB_ALIGN
     abi = N.lib().hz_abi_version()
     hdr = HEADER.pack(MAGIC, VERSION, abi, len(recs), meta_off, len(meta_b), ops_off, len(ops_bytes), b_off, blob_len,
-                      regs.size[1], regs.size[2], 0, 0, 0, 0)
+                      regs.size[1], regs.size[2], FLAG_WEIGHTLESS if weightless else 0, 0, 0, 0)
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "wb") as f:
@@ -289,7 +310,7 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
         f.write(ops_bytes)
         f.write(b"\0" * (b_off - ops_off - len(ops_bytes)))
         pos = 0
-        for old, data in keep:
+        for old, data, _ in ([] if weightless else keep):
             new, nb = remap[old]
             f.write(b"\0" * (new - pos))
             f.write(data.numpy().tobytes())
@@ -322,4 +343,36 @@ def export_from_checkpoint(model: str, ckpt: str, path: str | None = None, batch
         export_plan(model, params, arch_kw, shard_path, batch=dp_shard, contexts=1, source=stamp, host_io=False)
     path = path or plan_path(ckpt)
     export_plan(model, params, arch_kw, path, batch=batch, contexts=contexts, source=stamp, **kw)
+    return path
+
+
+def export_template(model: str, num_classes: int = 1000, batch: int = 1, contexts: int = 1,
+                    input_uint8: bool = True, path: str | None = None) -> str:
+    """Write the weightless plan TEMPLATE of an architecture (no checkpoint involved): the bound
+    program, launch configs and arena layout of ``model`` at ``batch`` / ``contexts``, plus the
+    packing recipe -- which checkpoint tensors (by state_dict key) produce each packed parameter,
+    its geometry and where it goes in the blob. ``hipzap.lite.PlanEngine.from_checkpoint`` then
+    cold-starts ANY checkpoint of that architecture straight from its ``.pth`` without torch: the
+    raw tensors are copied to the device and packed there (csrc/pack.hip). Templates are built
+    with the native library (``hipzap.build``), keyed to the lowering code (``lite.code_stamp``)."""
+    from ..lite import code_stamp, template_path
+    from .nppack import conv_geometry, pack_sources
+    if not model.startswith("resnet"):
+        raise ValueError("plan templates cover the ResNet family (device packer: conv + linear)")
+    adapter = registry.get(model)
+    torch.manual_seed(0)
+    m = adapter.make_model(num_classes).eval()
+    sd = m.state_dict()
+    params, arch_kw = adapter.pack(sd, "cpu")
+    arch_kw = dict(arch_kw, input_uint8=bool(input_uint8))
+    recipe = {}
+    for name, kind, w, bn, b in pack_sources(sd):
+        recipe[name] = {"kind": kind, "w": w, "bn": bn, "b": b, **conv_geometry(name, kind, tuple(sd[w].shape))}
+    path = path or template_path(model, batch, contexts, num_classes, input_uint8)
+    meta = export_plan(model, params, arch_kw, path, batch=batch, contexts=contexts, weightless=True,
+                       extra_meta={"code_stamp": code_stamp(), "pack": recipe})
+    missing = [n for n in recipe if f"{n}/wf" not in meta["blob_map"] or f"{n}/bias" not in meta["blob_map"]]
+    if missing:
+        os.unlink(path)
+        raise ValueError(f"template: packed parameters without a blob slot: {missing}")
     return path

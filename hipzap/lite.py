@@ -79,6 +79,37 @@ def _in_buffer(x):
     return C.addressof(buf), mv.nbytes, buf
 
 
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_STAMP_DIRS = ("engine", "models", "ops", "tuning")
+
+
+def code_stamp() -> str:
+    """Identity of the code that lowers a model to a plan (graph building, arena planning, launch
+    configs, tuning tables): a plan TEMPLATE (weightless) is valid only for the code that wrote
+    it, beyond the native ABI the loader already checks. Hashes file bytes; no imports."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in _STAMP_DIRS:
+        root = os.path.join(_PKG, d)
+        for name in sorted(os.listdir(root)):
+            if name.endswith((".py", ".json")):
+                h.update(name.encode())
+                with open(os.path.join(root, name), "rb") as f:
+                    h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def template_dir() -> str:
+    return os.environ.get("HIPZAP_TEMPLATE_DIR") or os.path.join(_PKG, "_lib", "templates")
+
+
+def template_path(model: str, batch: int = 1, contexts: int = 1, num_classes: int = 1000,
+                  input_uint8: bool = True) -> str:
+    """Where the weightless plan template of an architecture lives (built by ``hipzap.build``)."""
+    return os.path.join(template_dir(), f"{model}-b{batch}-c{contexts}-n{num_classes}{'-u8' if input_uint8 else ''}"
+                                        ".hztmpl")
+
+
 def no_sdma_default() -> None:
     """Copies through blit kernels instead of the SDMA engines (``HSA_ENABLE_SDMA=0``), unless the
     deployment chose (or ``HIPZAP_KEEP_SDMA=1``): the plan's 51-MB weight upload is faster that way
@@ -139,6 +170,102 @@ class PlanEngine:
     def _check(self, rc: int, what: str) -> None:
         if rc != 0:
             raise PlanError(f"{what} failed ({rc}): {lib().hz_plan_last_error().decode()}")
+
+    @classmethod
+    def from_checkpoint(cls, ckpt: str, device: int = 0, contexts: int = 1, batch: int = 1, template: str | None = None,
+                        template_contexts: int = 1, **kw) -> "PlanEngine":
+        """Cold start from the reference's checkpoint format (a ``torch.save`` state_dict,
+        /root/reference/main.py:99) WITHOUT torch: the archive is scanned by the weights-only
+        reader (hipzap/pthreader.py), the architecture's weightless plan template supplies the
+        program, and the raw fp32 tensors are copied to the GPU and packed there (BN folding, bf16,
+        fragment-major: csrc/pack.hip) straight into the plan's weight blob -- byte for byte what
+        ``hipzap plan`` would have written (tests/test_pth_lite_gpu.py)."""
+        import base64
+        from . import hip
+        from .engine.nppack import infer_resnet
+        from .pthreader import scan
+        t0 = time.perf_counter()
+        refs = scan(ckpt)
+        model, ncls = infer_resnet(refs)
+        tmpl = template or template_path(model, batch, template_contexts, ncls, True)
+        if not os.path.exists(tmpl):
+            raise PlanError(f"no plan template {tmpl} for {model} ({ncls} classes): build it with "
+                            f"python -m hipzap.build --templates")
+        meta = read_meta(tmpl)
+        if not meta.get("weightless") or meta.get("code_stamp") != code_stamp():
+            raise PlanError(f"{tmpl}: stale or not a template (rebuild with python -m hipzap.build --templates)")
+        recipe = meta["pack"]
+        t_scan = (time.perf_counter() - t0) * 1e3
+        # every source tensor: fp32, contiguous, the geometry the template was built for
+        jobs = []
+        for name, e in recipe.items():
+            keys = {"w": e["w"], "b": e["b"]}
+            if e["bn"]:
+                keys.update({f: f"{e['bn']}.{f2}" for f, f2 in (("gamma", "weight"), ("beta", "bias"),
+                                                                 ("mean", "running_mean"), ("var", "running_var"))})
+            src = {}
+            for f, k in keys.items():
+                if k is None:
+                    continue
+                r = refs.get(k)
+                if r is None or r.dtype != "float32" or not r.is_contiguous():
+                    raise PlanError(f"{ckpt}: {k} missing, not fp32 or not contiguous")
+                src[f] = r
+            want = (e["cout"], e["cin"]) if e["kind"] == "linear" else (e["cout"], e["cin"], e["r"], e["s"])
+            if tuple(src["w"].shape) != want:
+                raise PlanError(f"{ckpt}: {e['w']} is {src['w'].shape}, template expects {want}")
+            jobs.append((name, e, src))
+        stores = {}
+        for _, _, src in jobs:
+            for r in src.values():
+                stores[r.storage.key] = r.storage
+        timing = {"scan_ms": t_scan}
+
+        def fill(addr: int, nbytes: int) -> None:
+            ta = time.perf_counter()
+            offs, total = {}, 0
+            for k, st in stores.items():
+                offs[k] = total
+                total += (st.nbytes + 255) // 256 * 256
+            staging = hip.DeviceBuffer(total)
+            n = len(stores)
+            U64 = C.c_uint64 * n
+            keys = list(stores)
+            stream = hip._private_stream()
+            rc = lib().hz_upload_file(ckpt.encode(), n, U64(*[stores[k].file_off for k in keys]),
+                                      U64(*[stores[k].nbytes for k in keys]),
+                                      (C.c_void_p * n)(*[staging.ptr + offs[k] for k in keys]), stream)
+            if rc:
+                raise PlanError(f"checkpoint upload failed: {lib().hz_plan_last_error().decode()}")
+            tb = time.perf_counter()
+            from . import _native as NN
+            for name, e, src in jobs:
+                dev = {f: staging.ptr + offs[r.storage.key] + r.offset * 4 for f, r in src.items()}
+                p = NN.PackConvParams()
+                p.w, p.gamma, p.beta, p.mean, p.var = (dev.get(f, 0) for f in ("w", "gamma", "beta", "mean", "var"))
+                p.bias_in = dev.get("b", 0)
+                wf_off, wf_nb = meta["blob_map"][f"{name}/wf"]
+                b_off, b_nb = meta["blob_map"][f"{name}/bias"]
+                if wf_nb != e["rows"] * e["ksteps"] * 64 or b_nb != 4 * e["cout"]:
+                    raise PlanError(f"template slot of {name} does not match its recipe")
+                p.wf, p.bias_out = addr + wf_off, addr + b_off
+                p.cout, p.cin, p.r, p.s, p.cin_p = e["cout"], e["cin"], e["r"], e["s"], e["cin_p"]
+                p.rows, p.ksteps, p.eps = e["rows"], e["ksteps"], 1e-5
+                if lib().hz_pack_conv_launch(C.byref(p), stream):
+                    raise PlanError(f"pack kernel rejected {name}")
+            for off, b64 in meta.get("blob_consts", []):
+                data = base64.b64decode(b64)
+                buf = C.create_string_buffer(data, len(data))
+                hip.memcpy(addr + off, C.addressof(buf), len(data), hip.H2D, stream)
+            hip.sync(stream)
+            staging.free()
+            timing.update({"upload_raw_ms": (tb - ta) * 1e3, "pack_ms": (time.perf_counter() - tb) * 1e3,
+                           "raw_MB": round(total / 2**20, 1)})
+
+        eng = cls(tmpl, device=device, contexts=contexts, read_blob=False, fill_blob=fill, **kw)
+        eng.timings.update(timing)
+        eng.source = ckpt
+        return eng
 
     # ---------------------------------------------------------------- contexts
     def ensure_contexts(self) -> float:

@@ -159,27 +159,34 @@ def _bn(sd, prefix):
 
 
 def pack_resnet(sd: dict, device="cpu") -> dict[str, PackedConv]:
-    """state_dict -> {name: PackedConv} with BN folded (runs once at cold start)."""
+    """state_dict -> {name: PackedConv} with BN folded (runs once at cold start). Which state_dict
+    tensors feed which packed parameter: engine/nppack.py pack_sources (shared with the
+    torch-free packers)."""
+    from ..engine.nppack import pack_sources
     sd = {k: v.to(device) for k, v in sd.items()}
-    arch, _ = infer_arch(sd)
-    block, layers = ARCHS[arch]
-    P = {"conv1": pack_conv(sd["conv1.weight"], None, _bn(sd, "bn1"), stride=2, pad=3, cin_pad=8)}
-    for li, nb in enumerate(layers, start=1):
-        for b in range(nb):
-            pre = f"layer{li}.{b}"
-            stride = 2 if (b == 0 and li > 1) else 1
-            if block is Bottleneck:
-                P[f"{pre}.conv1"] = pack_conv(sd[f"{pre}.conv1.weight"], None, _bn(sd, f"{pre}.bn1"))
-                P[f"{pre}.conv2"] = pack_conv(sd[f"{pre}.conv2.weight"], None, _bn(sd, f"{pre}.bn2"), stride, 1)
-                P[f"{pre}.conv3"] = pack_conv(sd[f"{pre}.conv3.weight"], None, _bn(sd, f"{pre}.bn3"))
-            else:
-                P[f"{pre}.conv1"] = pack_conv(sd[f"{pre}.conv1.weight"], None, _bn(sd, f"{pre}.bn1"), stride, 1)
-                P[f"{pre}.conv2"] = pack_conv(sd[f"{pre}.conv2.weight"], None, _bn(sd, f"{pre}.bn2"), 1, 1)
-            if f"{pre}.downsample.0.weight" in sd:
-                P[f"{pre}.downsample"] = pack_conv(sd[f"{pre}.downsample.0.weight"], None,
-                                                   _bn(sd, f"{pre}.downsample.1"), stride, 0)
-    P["fc"] = pack_linear(sd["fc.weight"], sd["fc.bias"])
+    bottleneck = any(k.endswith("conv3.weight") for k in sd)
+    P = {}
+    for name, kind, w, bn, b in pack_sources(sd):
+        if kind == "linear":
+            P[name] = pack_linear(sd[w], sd[b] if b else None)
+        else:
+            stride, pad = _conv_stride_pad(name, sd[w].shape, bottleneck)
+            P[name] = pack_conv(sd[w], None, _bn(sd, bn), stride, pad, cin_pad=8 if name == "conv1" else None)
     return P
+
+
+def _conv_stride_pad(name: str, wshape, bottleneck: bool) -> tuple[int, int]:
+    """torchvision ResNet geometry: the stem is 7x7/2 pad 3; a stage's first block strides 2 in its
+    3x3 conv (bottleneck conv2, basic conv1) and its downsample (stages 2-4); 3x3 pads 1."""
+    if name == "conv1":
+        return 2, 3
+    li, b, conv = name.split(".")
+    first = b == "0" and li != "layer1"
+    k = wshape[-1]
+    if conv == "downsample":
+        return (2 if first else 1), 0
+    strided = first and ((bottleneck and conv == "conv2") or (not bottleneck and conv == "conv1"))
+    return (2 if strided else 1), (1 if k == 3 else 0)
 
 
 def build_graph(arch: str, batch: int, num_classes: int = 1000, image: int = 224,

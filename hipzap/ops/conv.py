@@ -69,11 +69,16 @@ class PackedConv:
 
 
 def fold_bn(weight: torch.Tensor, bias: torch.Tensor | None, bn: dict | None, eps: float = 1e-5):
-    """Fold eval-mode BatchNorm into conv weight/bias (fp32)."""
+    """Fold eval-mode BatchNorm into conv weight/bias (fp32).
+
+    The per-channel scale gamma / sqrt(var + eps) is computed in float64 and rounded once: torch's
+    CPU sqrt is not correctly rounded (SLEEF), so a float32 scale would differ by an ulp from the
+    torch-free packers (engine/nppack.py, the device pack kernel in csrc/pack.hip) in ~1 % of
+    channels; the rest (w * scale, (b - mean) * scale + beta) is plain IEEE float32 everywhere."""
     w = weight.detach().float()
     b = bias.detach().float() if bias is not None else torch.zeros(w.shape[0], device=w.device)
     if bn is not None:
-        scale = bn["weight"].float() / torch.sqrt(bn["running_var"].float() + eps)
+        scale = (bn["weight"].double() / torch.sqrt(bn["running_var"].double() + eps)).float()
         w = w * scale.view(-1, *([1] * (w.dim() - 1)))
         b = (b - bn["running_mean"].float()) * scale + bn["bias"].float()
     return w, b

@@ -1,0 +1,118 @@
+"""The torch-free checkpoint path on the CPU: the weights-only ``torch.save`` reader
+(hipzap/pthreader.py) against torch.load, its refusal of anything outside the allowlist, the numpy
+packer (engine/nppack.py) bitwise against the torch packer, and a weightless plan template
+(engine/plan.py export_template) placing every packed parameter exactly where the full plan image
+exported from the same checkpoint has it (the device packer writes those slots on the GPU:
+tests/test_pth_lite_gpu.py)."""
+import base64
+import io
+import os
+import pickle
+import sys
+import zipfile
+
+import numpy as np
+import pytest
+import torch
+
+from hipzap import pthreader
+from hipzap.engine import nppack
+from hipzap.models.resnet import pack_resnet, randomize_bn, resnet18, resnet50
+
+
+def _ckpt(tmp_path, mk, name="m.pth"):
+    torch.manual_seed(0)
+    m = randomize_bn(mk()).eval()
+    p = str(tmp_path / name)
+    torch.save(m.state_dict(), p)
+    return p, m.state_dict()
+
+
+def test_reader_matches_torch_load(tmp_path):
+    p, _ = _ckpt(tmp_path, resnet18)
+    ref = torch.load(p, weights_only=True)
+    sd = pthreader.load_state_dict(p)
+    assert list(sd) == list(ref)
+    for k, v in ref.items():
+        assert sd[k].shape == tuple(v.shape) and np.array_equal(sd[k], v.numpy()), k
+    x = {"bf": torch.randn(5, 3).bfloat16(), "h": torch.randn(4).half(), "sc": torch.tensor(3.5), "t": torch.randn(6, 4),
+         "i": torch.arange(7), "p": torch.nn.Parameter(torch.randn(3))}
+    x["view"], x["tr"], x["tied"] = x["t"][2:, 1:3], x["t"].t(), x["t"]
+    torch.save(x, tmp_path / "x.pth")
+    y = pthreader.load_state_dict(str(tmp_path / "x.pth"))
+    assert np.array_equal(y["bf"].to_float32(), x["bf"].float().numpy())
+    for k in ("h", "sc", "t", "i", "p", "view", "tr", "tied"):
+        assert np.array_equal(y[k], x[k].detach().numpy()), k
+    refs = pthreader.scan(str(tmp_path / "x.pth"))
+    assert refs["tied"].storage is refs["t"].storage and refs["view"].offset == 2 * 4 + 1
+    assert refs["t"].is_contiguous() and not refs["tr"].is_contiguous() and not refs["view"].is_contiguous()
+
+
+def test_reader_refuses_non_allowlisted_globals(tmp_path):
+    """A data.pkl that names any other global (here os.system) is refused before anything runs."""
+    marker = tmp_path / "pwned"
+
+    class Evil:
+        def __reduce__(self):
+            return os.system, (f"touch {marker}",)
+
+    buf = io.BytesIO()
+    pickle.dump({"w": Evil()}, buf, protocol=2)
+    p = tmp_path / "evil.pth"
+    with zipfile.ZipFile(p, "w", zipfile.ZIP_STORED) as z:
+        z.writestr("evil/data.pkl", buf.getvalue())
+        z.writestr("evil/byteorder", "little")
+    with pytest.raises(pickle.UnpicklingError, match="not allowed"):
+        pthreader.load_state_dict(str(p))
+    with pytest.raises(pickle.UnpicklingError):
+        pthreader.scan(str(p))
+    assert not marker.exists()
+
+
+def test_scan_needs_no_numpy_or_torch(tmp_path):
+    p, _ = _ckpt(tmp_path, resnet18)
+    code = (f"import sys; from hipzap import pthreader, lite; from hipzap.engine import nppack; "
+            f"r = pthreader.scan({p!r}); print(nppack.infer_resnet(r), 'numpy' in sys.modules, 'torch' in sys.modules)")
+    import subprocess
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["('resnet18',", "1000)", "False", "False"]
+
+
+@pytest.mark.parametrize("mk", [resnet18, resnet50])
+def test_numpy_pack_is_bitwise_the_torch_pack(tmp_path, mk):
+    p, sd = _ckpt(tmp_path, mk)
+    P = pack_resnet(torch.load(p, weights_only=True))
+    Q = nppack.pack_resnet(pthreader.load_state_dict(p))
+    assert set(P) == set(Q)
+    for k, pc in P.items():
+        assert np.array_equal(pc.wf.view(torch.int16).numpy().view(np.uint16), Q[k]["wf"]), k
+        assert np.array_equal(pc.bias.numpy(), Q[k]["bias"]), k
+
+
+def test_template_places_every_parameter_like_the_plan_image(tmp_path):
+    from hipzap.engine.plan import HEADER, export_from_checkpoint, export_template
+    from hipzap.lite import read_meta
+    p, _ = _ckpt(tmp_path, resnet18)
+    plan = export_from_checkpoint("resnet18", p, str(tmp_path / "m.hzplan"))
+    tmpl = export_template("resnet18", 1000, 1, 1, True, str(tmp_path / "r18.hztmpl"))
+    pm, tm = read_meta(plan), read_meta(tmpl)
+    assert tm["weightless"] and os.path.getsize(tmpl) < 1 << 20 and tm["blob_bytes"] == pm["blob_bytes"]
+    with open(plan, "rb") as f:
+        hdr = HEADER.unpack(f.read(HEADER.size))
+        f.seek(hdr[8])
+        blob = f.read(hdr[9])
+    Q = nppack.pack_resnet(pthreader.load_state_dict(p))
+    mine = bytearray(tm["blob_bytes"])
+    for slot, (off, nb) in tm["blob_map"].items():
+        name, field = slot.split("/")
+        data = Q[name][field].tobytes()
+        assert len(data) == nb, slot
+        mine[off: off + nb] = data
+    for off, b64 in tm["blob_consts"]:
+        data = base64.b64decode(b64)
+        mine[off: off + len(data)] = data
+    assert bytes(mine) == blob
+    # the recipe covers every packed parameter with its checkpoint sources
+    assert set(tm["pack"]) == set(Q) and tm["pack"]["fc"]["kind"] == "linear" and tm["pack"]["conv1"]["cin_p"] == 8
