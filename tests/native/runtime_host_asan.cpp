@@ -30,6 +30,9 @@ STUB(hz_embed_ln_launch, HzEmbedParams, 10, L)
 STUB(hz_attention_launch, HzAttentionParams, 11, L)
 STUB(hz_vit_tokens_launch, HzVitTokensParams, 12, B)
 STUB(hz_softmax_launch, HzSoftmaxParams, 13, rows)
+STUB(hz_lmb_layer_launch, HzLmbLayerParams, 14, H)
+STUB(hz_lmb_dec_launch, HzLmbDecParams, 15, V)
+STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
 extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
   g_calls.push_back(18);
   g_vals.push_back(n);

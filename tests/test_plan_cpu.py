@@ -67,7 +67,7 @@ def test_plan_relocations_cover_every_pointer(tmp_path, r18, zero_copy):
     assert len(rec.ops) == len(ops)
     sizes = {0: hdr["blob_len"], 1: hdr["ctx_dev"], 2: hdr["ctx_host"]}
     spans = [(t.untyped_storage().data_ptr(), t.untyped_storage().nbytes())
-             for obj in list(params.values()) + list(ctx._keep) for t in P._tensors(obj)]
+             for obj in list(params.values()) + list(ctx._keep) for _, t in P._tensors(obj)]
 
     def left(ptr):  # bytes from ptr to the end of its storage
         return next(b + n - ptr for b, n in spans if b <= ptr < b + n)
@@ -104,7 +104,7 @@ def test_plan_blob_is_compact(tmp_path, r18):
     path = str(tmp_path / "r18.hzplan")
     meta = P.export_plan("resnet18", params, kw, path)
     sts = {t.untyped_storage().data_ptr(): t.untyped_storage().nbytes()
-           for obj in params.values() for t in P._tensors(obj)}
+           for obj in params.values() for _, t in P._tensors(obj)}
     assert meta["blob_bytes"] <= sum(sts.values()) + 256 * (len(sts) + 4)  # + alignment + preprocess consts
     w_bytes = sum(pc.wf.numel() * 2 for pc in params.values() if hasattr(pc, "wf"))
     assert meta["blob_bytes"] >= w_bytes
