@@ -5,7 +5,7 @@
 // pack_linear on the host:
 //   * eval BatchNorm folded: scale = float(double(gamma) / sqrt(double(var) + eps)) (rounded once,
 //     as ops/conv.py fold_bn), w' = w * scale, b' = (0 - mean) * scale + beta in IEEE fp32
-//     (no FMA contraction: __fmul_rn / __fadd_rn);
+//     (fp contraction off: no fused multiply-add);
 //   * OIHW -> row-major [cout][R*S*Cin_pad] (K order R, S, C; channels zero-padded), K padded to 32,
 //     rows to `rows`; bf16 round-to-nearest-even (NaN -> 0x7FC0, torch's conversion);
 //   * fragment-major [rows/16][K/32][64 lanes][8] (lane l = row l&15, k 8(l>>4)..+7 of the step).
@@ -31,6 +31,9 @@ __device__ __forceinline__ float bn_scale(const HzPackConvParams& p, int row) {
 }
 
 __global__ __launch_bounds__(256) void pack_conv_kernel(const HzPackConvParams p) {
+  // IEEE fp32 ops one by one, as torch computes them: a contracted multiply-add (v_fmac) would
+  // round once instead of twice and differ from the host pack in the last bit
+#pragma clang fp contract(off)
   const long nchunk = (long)(p.rows / 16) * p.ksteps * 64;
   const int K = p.r * p.s * p.cin_p, SC = p.s * p.cin_p;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < nchunk; idx += (long)gridDim.x * blockDim.x) {
@@ -50,7 +53,7 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const HzPackConvParams p
         const int rr = k / SC, rem = k - rr * SC, ss = rem / p.cin_p, c = rem - ss * p.cin_p;
         if (c < p.cin) {
           x = p.w[(((long)row * p.cin + c) * p.r + rr) * p.s + ss];
-          if (p.gamma) x = __fmul_rn(x, sc);
+          if (p.gamma) x = x * sc;
         }
       }
       v[j] = bf16_rne(x);
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const HzPackConvParams p
   }
   for (long row = (long)blockIdx.x * blockDim.x + threadIdx.x; row < p.cout; row += (long)gridDim.x * blockDim.x) {
     float b = p.bias_in ? p.bias_in[row] : 0.f;
-    if (p.gamma) b = __fadd_rn(__fmul_rn(__fsub_rn(b, p.mean[row]), bn_scale(p, (int)row)), p.beta[row]);
+    if (p.gamma) b = (b - p.mean[row]) * bn_scale(p, (int)row) + p.beta[row];
     p.bias_out[row] = b;
   }
 }
