@@ -40,6 +40,14 @@ namespace {
 #ifndef HZ_RING_SHRINK
 #define HZ_RING_SHRINK 0
 #endif
+// HZ_EPI_PREFETCH=1: epilogue operands (folded-BN bias, residual) loaded right after the ring
+// prologue instead of after the K loop (the last dependent memory round trip of a bs=1 conv).
+// Measured same-box interleaved (profiles/r3_ab_conv): single stream +2 % (3,851 vs 3,775
+// inf/s) but 24-stream serving -4 % (10.69k vs 11.11k) -- the extra VGPRs and early loads cost
+// more under concurrency than the latency they hide. Off by default; throughput is the objective.
+#ifndef HZ_EPI_PREFETCH
+#define HZ_EPI_PREFETCH 0
+#endif
 template <int FC, int FP>
 struct Depth {
   static constexpr int base = (FC + FP <= 2) ? 6 : (FC + FP <= 3) ? 4 : (FC + FP <= 4) ? 3 : 2;
@@ -195,6 +203,37 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
   for (int u = 0; u < DEPTH; ++u)
     if (u < nsteps) load_step(u, fa[u], fb[u]);
+  // output element offset of accumulator (i, j) of this lane, -1 when out of range
+  auto out_off = [&](int i, int j) -> long {
+    const int m = m0 + j * 16 + lrow;
+    const int n = n0 + i * 16 + (lane >> 4) * 4;
+    if (m >= p.M || n >= p.Cout) return -1;
+    if (p.out_rowmajor) return (long)m * p.ldo + n;
+    const int ni = fdiv(m, PQ);  // channel-blocked [N][Cout/32][P*Q][32]
+    const int hw = m - ni * PQ;
+    return (((long)ni * (p.Cout >> 5) + (n >> 5)) * PQ + hw) * 32 + (n & 31);
+  };
+  auto owns = [&](int i, int j) { return KW == 1 || ((i * FP + j) & (KW - 1)) == wave; };
+  constexpr bool PF = HZ_EPI_PREFETCH && NF <= 8;
+  f32x4 pf_bias[FC];
+  u32x2 pf_res[FC][FP];
+  if constexpr (PF) {
+#pragma unroll
+    for (int i = 0; i < FC; ++i) {
+      const int n = n0 + i * 16 + (lane >> 4) * 4;
+      pf_bias[i] = p.bias && n < p.Cout ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < FC; ++i)
+#pragma unroll
+      for (int j = 0; j < FP; ++j) {
+        pf_res[i][j] = u32x2{0u, 0u};
+        if (p.res && owns(i, j)) {
+          const long o = out_off(i, j);
+          if (o >= 0 && HZ_DCHECK(o + 4 <= olim)) pf_res[i][j] = *reinterpret_cast<const u32x2*>(p.res + o);
+        }
+      }
+  }
   HZ_STAMP(1);
   for (int t = 0; t < nsteps; t += DEPTH + 1) {
 #pragma unroll
@@ -212,26 +251,18 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   }
 
   auto epilogue = [&](int i, int j, f32x4 a) {
-    const int m = m0 + j * 16 + lrow;
+    const long o = out_off(i, j);
+    if (o < 0) return;
     const int n = n0 + i * 16 + (lane >> 4) * 4;
-    if (m >= p.M || n >= p.Cout) return;
     float v[4] = {a[0], a[1], a[2], a[3]};
     if (p.bias) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
+      const f32x4 bb = PF ? pf_bias[i] : *reinterpret_cast<const f32x4*>(p.bias + n);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += bb[e];
     }
-    long o;
-    if (p.out_rowmajor) {
-      o = (long)m * p.ldo + n;
-    } else {  // channel-blocked [N][Cout/32][P*Q][32]
-      const int ni = fdiv(m, PQ);
-      const int hw = m - ni * PQ;
-      o = (((long)ni * (p.Cout >> 5) + (n >> 5)) * PQ + hw) * 32 + (n & 31);
-    }
     if (!HZ_DCHECK(o >= 0 && o + 4 <= olim)) return;
     if (p.res) {
-      const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
+      const u32x2 rr = PF ? pf_res[i][j] : *reinterpret_cast<const u32x2*>(p.res + o);
       v[0] += __uint_as_float(rr[0] << 16);
       v[1] += __uint_as_float(rr[0] & 0xffff0000u);
       v[2] += __uint_as_float(rr[1] << 16);

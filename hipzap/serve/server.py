@@ -192,14 +192,26 @@ class LMBackend:
         self.itos, self.stoi = itos, make_stoi(itos)
         self.backend = backend
         if backend == "gpu":
-            from ..engine.lm import LMPool
-            self.engine = LMPool.for_vocab(sd, self.stoi, device, contexts=int(os.environ.get("HIPZAP_LM_CONTEXTS", 4)))
+            # default: continuous batching -- concurrent requests share every decode step
+            # (engine/lmbatch.py); HIPZAP_LM_ENGINE=pool: independent per-request contexts
+            kind = os.environ.get("HIPZAP_LM_ENGINE", "batch")
+            if kind == "batch":
+                from ..engine.lmbatch import LMBatchEngine
+                self.engine = LMBatchEngine.for_vocab(sd, self.stoi, device,
+                                                      rows=int(os.environ.get("HIPZAP_LM_ROWS", 32)),
+                                                      unroll=int(os.environ.get("HIPZAP_LM_UNROLL", 8)))
+            else:
+                from ..engine.lm import LMPool
+                self.engine = LMPool.for_vocab(sd, self.stoi, device,
+                                               contexts=int(os.environ.get("HIPZAP_LM_CONTEXTS", 4)))
+            self.engine_kind = kind
             self.model = None
         else:
             self.model = reference_lm(len(itos))
             self.model.load_state_dict(sd)
             self.model.eval()
             self.engine = None
+            self.engine_kind = "eager-cpu"
         self.cold_ms = (time.perf_counter() - t0) * 1e3
         self._lock = threading.Lock()
 
@@ -207,7 +219,7 @@ class LMBackend:
         import torch
         from .text import generate_text
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
-        if self.engine is not None:  # pool of independent decode contexts: reentrant
+        if self.engine is not None:  # batched decode / pool of contexts: reentrant
             return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)
         with self._lock:  # the eager CPU model's recurrent state makes it non-reentrant
             with torch.no_grad():
@@ -324,7 +336,7 @@ class ModelServer:
                     sd = reference_lm(len(itos)).state_dict()
                 else:
                     itos = load_itos(self.store.fetch(st.lm_vocab_key))
-                    sd = torch.load(self.store.fetch(st.lm_model_key), map_location="cpu", weights_only=True)
+                    sd = load_checkpoint(self.store.fetch(st.lm_model_key))
                 self._models[key] = LMBackend(sd, itos, self.backend, self.device)
                 self.stats["cold_loads"] += 1
             return self._models[key]
@@ -332,6 +344,28 @@ class ModelServer:
     def loaded(self) -> dict:
         return {k: {"backend": getattr(v, "backend", "?"), "cold_ms": round(getattr(v, "cold_ms", 0), 1)}
                 for k, v in self._models.items()}
+
+
+def load_checkpoint(path: str) -> dict:
+    """A ``torch.save`` state_dict as torch tensors (main.py:99 ``torch.load(map_location='cpu')``):
+    the weights-only zip reader (hipzap/pthreader.py: mmap, zero copy, shared storages stay
+    shared), falling back to ``torch.load(weights_only=True)`` for legacy (pre-zip) files."""
+    import torch
+    from ..pthreader import NotAZipCheckpoint, load_state_dict
+    try:
+        raw = load_state_dict(path)
+    except NotAZipCheckpoint:
+        return torch.load(path, map_location="cpu", weights_only=True)
+    import warnings
+    out = {}
+    with warnings.catch_warnings():  # read-only mmap views: the packers only read them
+        warnings.simplefilter("ignore", UserWarning)
+        for k, a in raw.items():
+            if hasattr(a, "to_float32"):
+                out[k] = torch.from_numpy(a.view("int16")).view(torch.bfloat16)
+            else:
+                out[k] = torch.from_numpy(a)
+    return out
 
 
 def gpu_visible() -> bool:

@@ -40,19 +40,23 @@ def test_gemm_fp8(M, N, K):
 
 
 def test_vit_fp8_engine_vs_hf():
+    """fp8 against the bf16 engine on the same weights (per-row cosine, top-1) and HF fp32."""
     torch.manual_seed(0)
     m = vit.make_model(num_labels=1000)
-    eng = Engine.from_state_dict("vit-b16-fp8", m.state_dict(), DEV, batch=4)
+    sd = m.state_dict()
+    eng = Engine.from_state_dict("vit-b16-fp8", sd, DEV, batch=4)
+    bf = Engine.from_state_dict("vit-b16", sd, DEV, batch=4)
     x = torch.randn(4, 3, 224, 224)
-    out = eng.infer(x)
+    out, ref16 = eng.infer(x), bf.infer(x)
     with torch.no_grad():
         ref = m(pixel_values=x).logits
-    rel = ((out - ref).abs().max() / ref.abs().max()).item()
-    # measured on MI355X (scripts/check_vit_fp8_err.py, same seed): rel 0.099, cos 0.993, top-1
-    # equal; bf16 engine 0.010 / 0.99993. e4m3 weights + per-row e4m3 activations through 12 layers
-    assert rel < 0.15, rel
+    cos16 = torch.nn.functional.cosine_similarity(out, ref16, dim=1)
+    assert cos16.min() > 0.99, cos16
+    assert torch.equal(out.argmax(1), ref16.argmax(1))
+    # measured on MI355X (scripts/check_vit_fp8_err.py, same seed) vs HF fp32: cos 0.993, top-1
+    # equal (bf16 engine 0.99993); e4m3 weights + per-row e4m3 activations through 12 layers
     cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
-    assert cos.min() > 0.985, cos
+    assert cos.min() > 0.99, cos
     assert torch.equal(out.argmax(1), ref.argmax(1))
 
 
