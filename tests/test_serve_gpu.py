@@ -183,11 +183,11 @@ def test_native_http_dynamic_batching_batch_plan(plan_server):
         assert not bad, bad
         st = be.engine.batched_executor().stats()
         assert st["served"] == 16 and st["batches"] <= 16, st
-        # the WSGI path on the same backend (npy batch of 3 -> one padded 4-row request) goes
-        # through the batched executor too, never around it
+        # the WSGI path on the same backend (npy batch of 3) goes through the batched executor
+        # too, never around it, and submits only its 3 real rows (no padding rows)
         y = be.infer_u8(np.stack(imgs[:3]))
         assert [int(r.argmax()) for r in y] == [int(refs[i].argmax()) for i in range(3)]
-        assert be.engine.batched_executor().stats()["served"] == 20
+        assert be.engine.batched_executor().stats()["served"] == 19
     finally:
         hs.stop()
         sock.close()
