@@ -292,6 +292,7 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_LMB_LAYER: return hz_lmb_layer_launch(static_cast<const HzLmbLayerParams*>(prm), st);
     case HZ_K_LMB_DEC: return hz_lmb_dec_launch(static_cast<const HzLmbDecParams*>(prm), st);
     case HZ_K_LMB_ADMIT: return hz_lmb_admit_launch(static_cast<const HzLmbAdmitParams*>(prm), st);
+    case HZ_K_CONV_CHAIN: return hz_conv_chain_launch(static_cast<const HzConvChainParams*>(prm), st);
     default: return -100;
   }
 }

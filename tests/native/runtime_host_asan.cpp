@@ -33,6 +33,7 @@ STUB(hz_softmax_launch, HzSoftmaxParams, 13, rows)
 STUB(hz_lmb_layer_launch, HzLmbLayerParams, 14, H)
 STUB(hz_lmb_dec_launch, HzLmbDecParams, 15, V)
 STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
+STUB(hz_conv_chain_launch, HzConvChainParams, 17, n_layers)
 extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
   g_calls.push_back(18);
   g_vals.push_back(n);
