@@ -34,12 +34,15 @@ def run_plan(path: str, device: int) -> dict:
     eng = PlanEngine(path, device=device, contexts=1,
                      capture="lazy" if os.environ.get("HIPZAP_PLAN_LAZY_CAPTURE", "1") == "1" else True)
     t_ready = time.time()
-    spec = eng.in_specs[0]
-    out = eng.infer_raw(os.urandom(spec["bytes"]))
+    if eng.kind == "text":  # token ids must index the tables: zeros (id 0, type 0, mask 0)
+        out = eng.infer_raw([bytes(sp["bytes"]) for sp in eng.in_specs])
+    else:
+        out = eng.infer_raw(os.urandom(eng.in_specs[0]["bytes"]))
     t_first = time.time()
     import math
     ok = all(math.isfinite(v) for v in out)
-    return {"mode": "plan", "t_first": t_first, "ok": ok, "torch_imported": "torch" in sys.modules,
+    return {"mode": "plan", "kind": eng.kind, "t_first": t_first, "ok": ok, "torch_imported": "torch" in sys.modules,
+            "numpy_imported": "numpy" in sys.modules,
             "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3, "import_lite": (t_lib - t_imp) * 1e3,
                           **{k: round(v, 3) for k, v in eng.timings.items()},
                           "first_request": (t_first - t_ready) * 1e3}}

@@ -241,6 +241,99 @@ __device__ __forceinline__ void wait_vm8() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Fused epilogue of the MX GEMMs: per-row (sx) x per-channel (sw) scales, bias, residual,
+// activation; bf16 / fp32 output, or MX8 (e4m3 + one E8M0 scale per (row, 32 columns)). The
+// wave owns FPW token fragments from row mw and FCW feature fragments from column nw; lane l
+// holds token mw + 16j + (l&15), features nw + 16i + 4(l>>4) .. +3. Wave-uniform (shuffles).
+template <int FCW, int FPW>
+__device__ __forceinline__ void mx_epilogue(const HzGemmFp8Params& p, const f32x4 (&acc)[FCW][FPW], int mw, int nw,
+                                            int lane) {
+  const int lrow = lane & 15;
+  if (p.out8) {  // MX8 output: per (row, 32-column block) E8M0 scale; no early exits (shuffles)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const int m = mw + j * 16 + lrow;
+      const bool mv = m < p.M;
+      const float sx = p.sx ? p.sx[min(m, p.M - 1)] : 1.f;
+#pragma unroll
+      for (int i = 0; i < FCW; i += 2) {
+        float v[2][4];
+        float amax = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = min(nw + (i + h) * 16 + (lane >> 4) * 4, p.N - 4);
+          const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+          const f32x4 bb = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = acc[i + h][j][e] * sx * sw[e] + bb[e];
+            if (p.act == HZ_ACT_RELU) x = fmaxf(x, 0.f);
+            else if (p.act == HZ_ACT_GELU) x = gelu_erf(x);
+            else if (p.act == HZ_ACT_TANH) x = tanhf(x);
+            v[h][e] = x;
+            amax = fmaxf(amax, fabsf(x));
+          }
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int ex = mx_exp(amax);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = nw + (i + h) * 16 + (lane >> 4) * 4;
+          float q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = fminf(fmaxf(ldexpf(v[h][e], -ex), -448.f), 448.f);
+          if (mv && n < p.N)
+            *reinterpret_cast<unsigned*>(p.out8 + (long)m * p.ldo + n) = pack4_fp8(q[0], q[1], q[2], q[3]);
+        }
+        const int nb = nw + i * 16;
+        if (mv && (lane >> 4) == 0 && nb < p.N) p.os8[(long)m * (p.ldo >> 5) + (nb >> 5)] = (unsigned char)(ex + 127);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int m = mw + j * 16 + lrow;
+    if (m >= p.M) continue;
+    const float sx = p.sx ? p.sx[m] : 1.f;
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) {
+      const int n = nw + i * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sx * sw[e];
+      if (p.bias) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bb[e];
+      }
+      const long o = (long)m * p.ldo + n;
+      if (p.res) {
+        const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
+        v[0] += __uint_as_float(rr[0] << 16);
+        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+        v[2] += __uint_as_float(rr[1] << 16);
+        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      }
+      if (p.act == HZ_ACT_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      } else if (p.act == HZ_ACT_GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      } else if (p.act == HZ_ACT_TANH) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+      }
+      if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
+      else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+}
+
 // XS: the activations carry MX block scales (p.xs, one E8M0 byte per 32 k): each wave also
 // stages one 4-byte-per-lane piece (64 rows x the 4 block scales of this 128-deep k-step) and
 // the scale goes to the MFMA's B-scale operand: lane l supplies token l&15's scale of 32-k block
@@ -358,90 +451,155 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
     cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
-  const int lrow = lane & 15;
-  if (p.out8) {  // MX8 output: per (row, 32-column block) E8M0 scale; no early exits (shuffles)
+  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
+}
+
+// ---- pipelined 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608) ----
+// The 128x128 tiles above move 32 KB per 128-deep k-step for 4 MFLOP: at M = 12,608 the
+// projections run at ~0.8 PF/s, bound by the L2 -> CU staging traffic (~7 TB/s chip-wide,
+// profiles/r3_tx_base), not by the MFMA. This kernel doubles the work per staged byte: a
+// 256 x BN tile (BN = 256: 64 KB per k-step for 16.8 MFLOP), ONE 8-wave workgroup per CU
+// (2 waves per SIMD), wave (wm, wn) owning 128 tokens x BN/4 features. Inside a k-step the wave
+// keeps its BN/64 weight fragments in registers and walks its 8 token fragments in 4 sub-blocks
+// of 2; the next sub-block's fragments are read from LDS while the current one's MFMAs issue
+// (register double buffer), and the NEXT stage's glds pieces are issued between the first two
+// sub-blocks rather than in one burst. Same LDS images, swizzle, hardware K order, block scales
+// and epilogue as gemm_mx_kernel; NS = 2 (BN 256, 132 KB) or 3 (BN 128, 150 KB) stages with
+// counted vmcnt + raw s_barrier.
+template <int BN, int NS, bool XS>
+__global__ __launch_bounds__(512) void gemm_mxp_kernel(const HzGemmFp8Params p, int group_m) {
+  constexpr int BM = 256, WM = 2, WN = 4, NW = 8;
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 4|2 weight, 8 token fragments per wave
+  constexpr int SB = 4, TPS = FPW / SB;                  // sub-blocks of 2 token fragments
+  constexpr int NWG = BN / 16;
+  constexpr int XBYTES = BM * 128;
+  constexpr int WBYTES = NWG * 2048;
+  constexpr int SBYTES = XBYTES + WBYTES + (XS ? NW * 256 : 0);
+  constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;
+  static_assert(XPW * 8 * NW == BM && WPW * NW == NWG * 2 && FCW >= 1 && TPS * SB == FPW, "tile / wave split");
+  constexpr int G = XPW + WPW + (XS ? 1 : 0);
+  static_assert(NS * SBYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int tiles_n = p.N / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
+  const int n0 = tile_n * BN, m0 = tile_m * BM;
+  const int kb = p.K >> 7;
+
+  const unsigned char* xsrc[XPW];
 #pragma unroll
-    for (int j = 0; j < FPW; ++j) {
-      const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
-      const bool mv = m < p.M;
-      const float sx = p.sx ? p.sx[min(m, p.M - 1)] : 1.f;
+  for (int i = 0; i < XPW; ++i) {
+    const int q = wave + NW * i;
+    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
+    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
+    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
+  }
+  const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
+  const unsigned char* ssrc = XS ? p.xs + (long)min(m0 + (wave & 3) * 64 + lane, p.M - 1) * (p.K >> 5) : nullptr;
+  auto stage_x = [&](int buf, int st) {  // activations (+ block scales): XPW (+1) pieces
+    char* base = smem + buf * SBYTES;
+    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
 #pragma unroll
-      for (int i = 0; i < FCW; i += 2) {
-        float v[2][4];
-        float amax = 0.f;
+    for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
+  };
+  auto stage_w = [&](int buf, int st) {  // weights: WPW pieces
+    char* base = smem + buf * SBYTES;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int n = min(n0 + wn * (BN / WN) + (i + h) * 16 + (lane >> 4) * 4, p.N - 4);
-          const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
-          const f32x4 bb = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < WPW; ++i) {
+      const int piece = wave + NW * i;
+      glds16_8(wsrc + ((long)(piece >> 1) * kb + st) * 2048 + (piece & 1) * 1024, base + XBYTES + piece * 1024);
+    }
+  };
+
+  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
+  const int brow = (wm * (BM / WM) + lr) * 128;
+  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
+  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
+  auto rd = [](const char* b0, const char* b1) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(b0);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(b1);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+
+  f32x4 acc[FCW][FPW];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x = acc[i + h][j][e] * sx * sw[e] + bb[e];
-            if (p.act == HZ_ACT_RELU) x = fmaxf(x, 0.f);
-            else if (p.act == HZ_ACT_GELU) x = gelu_erf(x);
-            else if (p.act == HZ_ACT_TANH) x = tanhf(x);
-            v[h][e] = x;
-            amax = fmaxf(amax, fabsf(x));
-          }
+  for (int i = 0; i < FCW; ++i)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < kb) {
+      stage_x(s0, s0);
+      stage_w(s0, s0);
+    }
+  int cur = 0;
+  for (int st = 0; st < kb; ++st) {
+    const int ahead = min(NS - 2, kb - 1 - st);  // stages issued beyond st that may stay in flight
+    if (NS > 2 && ahead >= 1) wait_vm8<(NS > 2 ? G : 0)>();
+    else wait_vm8<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool pre = st + NS - 1 < kb;
+    const int nbuf = cur == 0 ? NS - 1 : cur - 1;
+    const char* base = smem + cur * SBYTES;
+    i32x8 w[FCW], xa[TPS], xb[TPS];
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) w[i] = rd(base + aoff + i * 2048, base + aoff + i * 2048 + 1024);
+#pragma unroll
+    for (int j = 0; j < TPS; ++j) xa[j] = rd(base + boff0 + j * 2048, base + boff1 + j * 2048);
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      if (sb + 1 < SB) {
+#pragma unroll
+        for (int j = 0; j < TPS; ++j)
+          xb[j] = rd(base + boff0 + ((sb + 1) * TPS + j) * 2048, base + boff1 + ((sb + 1) * TPS + j) * 2048);
+      }
+      if (pre && sb == 0) stage_x(nbuf, st + NS - 1);
+      if (pre && sb == 1) stage_w(nbuf, st + NS - 1);
+      int sc[TPS];
+#pragma unroll
+      for (int j = 0; j < TPS; ++j) {
+        if constexpr (XS) {
+          const int r = wm * (BM / WM) + (sb * TPS + j) * 16 + lr;
+          sc[j] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
+                                                           (lane >> 4));
+        } else {
+          sc[j] = 0x7f7f7f7f;
         }
-        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
-        const int ex = mx_exp(amax);
+      }
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int n = n0 + wn * (BN / WN) + (i + h) * 16 + (lane >> 4) * 4;
-          float q[4];
+      for (int i = 0; i < FCW; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) q[e] = fminf(fmaxf(ldexpf(v[h][e], -ex), -448.f), 448.f);
-          if (mv && n < p.N)
-            *reinterpret_cast<unsigned*>(p.out8 + (long)m * p.ldo + n) = pack4_fp8(q[0], q[1], q[2], q[3]);
-        }
-        const int nb = n0 + wn * (BN / WN) + i * 16;
-        if (mv && (lane >> 4) == 0 && nb < p.N) p.os8[(long)m * (p.ldo >> 5) + (nb >> 5)] = (unsigned char)(ex + 127);
+        for (int j = 0; j < TPS; ++j)
+          acc[i][sb * TPS + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w[i], xa[j], acc[i][sb * TPS + j], 0,
+                                                                                  0, 0, 0x7f7f7f7f, 0, sc[j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (sb + 1 < SB) {
+#pragma unroll
+        for (int j = 0; j < TPS; ++j) xa[j] = xb[j];
       }
     }
-    return;
+    cur = cur == NS - 1 ? 0 : cur + 1;
   }
-#pragma unroll
-  for (int j = 0; j < FPW; ++j) {
-    const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
-    if (m >= p.M) continue;
-    const float sx = p.sx ? p.sx[m] : 1.f;
-#pragma unroll
-    for (int i = 0; i < FCW; ++i) {
-      const int n = n0 + wn * (BN / WN) + i * 16 + (lane >> 4) * 4;
-      if (n >= p.N) continue;
-      const f32x4 sw = *reinterpret_cast<const f32x4*>(p.sw + n);
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sx * sw[e];
-      if (p.bias) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bb[e];
-      }
-      const long o = (long)m * p.ldo + n;
-      if (p.res) {
-        const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
-        v[0] += __uint_as_float(rr[0] << 16);
-        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-        v[2] += __uint_as_float(rr[1] << 16);
-        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
-      }
-      if (p.act == HZ_ACT_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      } else if (p.act == HZ_ACT_GELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-      } else if (p.act == HZ_ACT_TANH) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-      }
-      if (p.out_f32) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
-      else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
-  }
+  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
+}
+
+template <int BN, int NS>
+int launch_mxp(const HzGemmFp8Params& p, hipStream_t st) {
+  if (p.N % BN) return -4;
+  const int tiles = (p.N / BN) * ((p.M + 255) / 256);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  if (p.xs) hipLaunchKernelGGL((gemm_mxp_kernel<BN, NS, true>), dim3(tiles), dim3(512), 0, st, p, group_m);
+  else hipLaunchKernelGGL((gemm_mxp_kernel<BN, NS, false>), dim3(tiles), dim3(512), 0, st, p, group_m);
+  return (int)hipGetLastError();
 }
 
 template <int BM, int BN, int NS, int WM = 2, int WN = 2>
@@ -485,6 +643,12 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 30: return launch_mx<128, 128, 4, 2, 4>(p, st);
       case 31: return launch_mx<64, 128, 4>(p, st);
       case 32: return launch_mx<128, 64, 4>(p, st);
+      // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
+      case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
+      // pipelined 256-row kernel: 256x256 / 2 stages, 256x128 / 2 and 3 stages
+      case 40: return launch_mxp<256, 2>(p, st);
+      case 41: return launch_mxp<128, 2>(p, st);
+      case 42: return launch_mxp<128, 3>(p, st);
       default: return -2;
     }
   }

@@ -342,6 +342,8 @@ typedef struct HzEmbedParams {
   unsigned short* out;        // [rows][D]
   int rows, L, D;
   float eps;
+  int vocab, ntypes;          // table rows: ids / types are clamped into range (a bad request id
+                              // cannot read outside the tables; the servers also reject it)
 } HzEmbedParams;
 typedef struct HzAttentionParams {
   const unsigned short* qkv;  // [B*L][ldqkv]: Q at col h*64, K at +k_off, V at +v_off

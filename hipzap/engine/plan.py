@@ -278,6 +278,10 @@ def export_plan(model: str, params: dict, arch_kw: dict, path: str, batch: int =
         "ctx_dev_bytes": regs.size[1], "ctx_host_bytes": regs.size[2], "blob_bytes": blob_len,
         "arena_bytes": ctx.arena_bytes,
     }
+    emb = params.get("emb")
+    if emb is not None and hasattr(emb, "word"):  # BERT-style text plan: inputs ids / types / additive mask
+        meta.update({"kind": "text", "seq_len": int(g.shape(g.inputs[0])[0]) // batch,
+                     "vocab": int(emb.word.shape[0]), "type_vocab": int(emb.type.shape[0])})
     import hashlib
     h = hashlib.sha256()
     for old, data, _ in keep:  # digest of the blob exactly as written (offsets + bytes)

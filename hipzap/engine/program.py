@@ -395,7 +395,7 @@ class ExecContext:
             rows, D = g.shape(n.outputs[0])
             prm = tx.EmbedParams(addr(n.inputs[0]), addr(n.inputs[1]), tab.word.data_ptr(), tab.pos.data_ptr(),
                                  tab.type.data_ptr(), ln.gamma.data_ptr(), ln.beta.data_ptr(), addr(n.outputs[0]),
-                                 rows, n.attrs["L"], D, ln.eps)
+                                 rows, n.attrs["L"], D, ln.eps, tab.word.shape[0], tab.type.shape[0])
             tx.prog_add(self.prog, tx.K_EMBED, prm, n.slot, lib=lib)
         elif n.kind == "vit_tokens":
             a = n.attrs

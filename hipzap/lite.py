@@ -165,6 +165,9 @@ class PlanEngine:
         inp, out = self.meta["inputs"], self.meta["output"]
         self.in_specs = inp
         self.out_spec = out
+        # "vision": a request is one image (batch-B plans batch requests dynamically);
+        # "text": a request is a whole padded batch of sequences (ids, types, additive mask)
+        self.kind = self.meta.get("kind", "vision")
         self._out_n = out["bytes"] // array.array(_TYPECODE[out["dtype"]]).itemsize
 
     def _check(self, rc: int, what: str) -> None:
@@ -324,7 +327,7 @@ class PlanEngine:
         if ex is not None or not self._capture or not self.host_io or len(self._locks) != self.num_contexts \
                 or self._uncaptured:
             return ex
-        if int(self.in_specs[0]["shape"][0]) > 1:
+        if self.kind != "text" and int(self.in_specs[0]["shape"][0]) > 1:
             raise PlanError("a batch-B plan serves one-image requests through batched_executor()")
         from .executor import Executor
         with self._build_lock:
@@ -384,12 +387,15 @@ class PlanEngine:
 
     # ---------------------------------------------------------------- requests
     def infer_raw(self, x, ctx: int | None = None, rows: int | None = None) -> array.array:
-        """One request: ``x`` = the input's exact bytes (uint8 HWC image for the ResNet plans).
-        Returns the output as a flat ``array.array`` (float32 logits). ``rows``: how many leading
-        rows of a batch-B request are real (the rest is padding): on the dynamic-batching
-        executor only those are submitted, and the padding rows' outputs stay zero."""
-        if len(self.in_specs) != 1 or not self.host_io:
-            raise PlanError("infer_raw needs a single-input host-I/O plan")
+        """One request: ``x`` = the input's exact bytes (uint8 HWC image for the ResNet plans), or
+        for a multi-input plan (BERT: ids, token types, additive mask) a sequence with one buffer
+        per input. Returns the output as a flat ``array.array`` (float32 logits). ``rows``: how
+        many leading rows of a batch-B request are real (the rest is padding): on the dynamic-
+        batching executor only those are submitted, and the padding rows' outputs stay zero."""
+        if not self.host_io:
+            raise PlanError("infer_raw needs a host-I/O plan")
+        if len(self.in_specs) > 1:
+            return self._infer_multi(x, ctx)
         addr, nb, keep = _in_buffer(x)
         spec = self.in_specs[0]
         if nb != spec["bytes"]:
@@ -433,6 +439,40 @@ class PlanEngine:
             rc = lib().hz_plan_infer(self._h, i, addr, spec["off"], nb, oaddr, self.out_spec["off"],
                                      self.out_spec["bytes"])
         del keep
+        self._check(rc, "infer")
+        return out
+
+    def _infer_multi(self, xs, ctx: int | None) -> array.array:
+        """A multi-input request: every input through the per-request executor, or (before it
+        exists / with ``ctx``) packed into one copy when the inputs are adjacent in the pinned
+        block (they are: the exporter lays them out in order)."""
+        if not isinstance(xs, (list, tuple)) or len(xs) != len(self.in_specs):
+            raise PlanError(f"this plan takes {len(self.in_specs)} inputs; pass one buffer per input")
+        bufs = [_in_buffer(x) for x in xs]
+        for (addr, nb, _), sp in zip(bufs, self.in_specs):
+            if nb != sp["bytes"]:
+                raise PlanError(f"input {sp['shape']} {sp['dtype']} is {sp['bytes']} bytes, got {nb}")
+        out = array.array(_TYPECODE[self.out_spec["dtype"]], bytes(self.out_spec["bytes"]))
+        oaddr, _ = out.buffer_info()
+        ex = self.executor() if ctx is None else None
+        if ex is not None:
+            ex.submit([b[0] for b in bufs], oaddr)
+            del bufs
+            return out
+        offs = [sp["off"] for sp in self.in_specs]
+        if any(offs[i] + self.in_specs[i]["bytes"] != offs[i + 1] for i in range(len(offs) - 1)):
+            raise PlanError("plan inputs are not adjacent in the host block")
+        packed = bytearray(sum(b[1] for b in bufs))
+        pos = 0
+        for addr, nb, _ in bufs:
+            C.memmove((C.c_char * nb).from_buffer(packed, pos), addr, nb)
+            pos += nb
+        paddr, pnb, keep = _in_buffer(packed)
+        i = self._pick() if ctx is None else ctx
+        with self._locks[i]:
+            rc = lib().hz_plan_infer(self._h, i, paddr, offs[0], pnb, oaddr, self.out_spec["off"],
+                                     self.out_spec["bytes"])
+        del keep, bufs
         self._check(rc, "infer")
         return out
 

@@ -101,8 +101,10 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             # 24-29: 8-wave workgroups (2 / 3 stages); N must be a multiple of BN
             24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256),
             # 30-32: 4 LDS stages (8-wave 128x128; 4-wave 64x128, 128x64)
-            30: (128, 128), 31: (64, 128), 32: (128, 64)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30)
+            30: (128, 128), 31: (64, 128), 32: (128, 64),
+            # 33: 8-wave 256x256 (plain); 40-42: pipelined 256-row kernel (256x256 2 stages, 256x128 2 / 3)
+            33: (256, 256), 40: (256, 256), 41: (256, 128), 42: (256, 128)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 40, 41, 42)
 
 
 def mx_fits(cfg: int, n: int) -> bool:

@@ -28,7 +28,8 @@ class LayerNormParams(C.Structure):
 class EmbedParams(C.Structure):
     _fields_ = [("ids", C.c_void_p), ("types", C.c_void_p), ("word", C.c_void_p), ("pos", C.c_void_p),
                 ("type", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("out", C.c_void_p),
-                ("rows", C.c_int), ("L", C.c_int), ("D", C.c_int), ("eps", C.c_float)]
+                ("rows", C.c_int), ("L", C.c_int), ("D", C.c_int), ("eps", C.c_float),
+                ("vocab", C.c_int), ("ntypes", C.c_int)]
 
 
 class AttentionParams(C.Structure):

@@ -46,6 +46,7 @@ class SocketComm(Comm):
         self.peers: dict[int, socket.socket] = {}
         self._hub = None
         self._closed = False
+        self._rdzv, self._key = rdzv_dir, key
         path = os.path.join(rdzv_dir, f"{key}.sock")
         if world <= 1:
             return
@@ -208,6 +209,22 @@ class SocketComm(Comm):
 
     def abort(self) -> None:
         self.close()
+
+    def shrink(self, exclude: list[int], abort_parent: bool = True) -> "SocketComm":
+        """The survivors' communicator (same contract as ``RcclComm.shrink``: every survivor
+        calls it with the same excluded ranks; ranks are renumbered densely). The new star is
+        keyed by the parent's key and the excluded set, so no new rendezvous id is needed."""
+        if self._closed:
+            raise CommError("parent communicator already closed; re-initialise instead")
+        excl = sorted(set(int(r) for r in exclude))
+        if self.rank in excl:
+            raise CommError(f"rank {self.rank} cannot shrink itself out")
+        new_rank = self.rank - sum(1 for r in excl if r < self.rank)
+        key = f"{self._key}.x{'_'.join(map(str, excl))}"
+        if abort_parent:
+            self.close()
+        return SocketComm(self._rdzv, key, self.world - len(excl), new_rank, memcpy=self.memcpy,
+                          timeout_s=self.timeout_s, stream_sync=self.stream_sync)
 
     def close(self) -> None:
         self._closed = True

@@ -111,7 +111,7 @@ def _count(exc):
 
 @app.errorhandler(Exception)
 def _error(e):
-    code = getattr(e, "code", 500)
+    code = getattr(e, "code", 400 if isinstance(e, ValueError) else 500)  # bad input: client error
     if not isinstance(code, int):
         code = 500
     if code >= 500:
@@ -202,22 +202,27 @@ def topk_np(p, k: int):
 def _predict_text(s, body):
     """BERT-style sequence classification: {"model", "input_ids", "token_type_ids"?,
     "attention_mask"?} -> class probabilities."""
-    import torch
     model = body.get("model") or "bert-base"
-    ids = torch.tensor(body["input_ids"], dtype=torch.long)
-    if ids.dim() == 1:
+    ids = np.asarray(body["input_ids"], dtype=np.int64)
+    if ids.ndim == 1:
         ids = ids[None]
     tt = body.get("token_type_ids")
     am = body.get("attention_mask")
-    tt = torch.tensor(tt, dtype=torch.long).reshape(ids.shape) if tt is not None else None
-    am = torch.tensor(am, dtype=torch.long).reshape(ids.shape) if am is not None else None
+    tt = np.asarray(tt, dtype=np.int64).reshape(ids.shape) if tt is not None else None
+    am = np.asarray(am, dtype=np.int64).reshape(ids.shape) if am is not None else None
     with phase("load"):
         backend = s.text(model)
     t0 = time.perf_counter()
     with phase("infer"):
-        logits = backend(ids, tt, am)
+        if hasattr(backend, "infer_np"):  # plan-backed: torch-free
+            logits = backend.infer_np(ids, tt, am)
+        else:
+            import torch
+            def tens(a):
+                return None if a is None else torch.from_numpy(a)
+            logits = backend(tens(ids), tens(tt), tens(am)).float().numpy()
     dt = (time.perf_counter() - t0) * 1e3
-    probs = torch.softmax(logits.float(), dim=-1)
+    probs = softmax_np(logits)
     return _json({"model": model, "backend": backend.backend, "batch": int(ids.shape[0]),
                   "probs": [[round(float(p), 6) for p in row] for row in probs],
                   "label": [int(i) for i in probs.argmax(-1)], "timing_ms": round(dt, 3)})

@@ -23,8 +23,12 @@ Shape (reference scale-out = Lambda's per-request container fan-out,
   polls ``ncclCommGetAsyncError`` with a deadline. A worker whose control connection drops, or
   that reports a collective failure, triggers a ``reform``: every live member drops its old
   communicator and joins a new one over the survivors (fresh unique id per epoch). Weights are
-  already resident, so bs=1 serving never stops; a restarted worker cold-starts from the plan
-  on disk and rejoins through the same path. Rank 0 hosts the sequencer: if it dies, batched
+  already resident, so bs=1 serving never stops. When the only change is a lost member (its
+  control connection dropped) the survivors SHRINK their communicator instead
+  (``ncclCommShrink`` with abort of the parent: no new unique id, no rendezvous, no bootstrap
+  of the survivors' connections); a reform after a failed collective, or a rejoin,
+  re-initialises. A restarted worker cold-starts from the plan on disk and rejoins through the
+  same path. Rank 0 hosts the sequencer: if it dies, batched
   requests fall back to the receiving worker's GPU alone until it is restarted; the other
   members then reconnect to the restarted sequencer and rejoin (one reform).
 """
@@ -82,6 +86,7 @@ class Coordinator:
         except (FileNotFoundError, ValueError):
             self.epoch = 0
         self.reforms: list = []
+        self.formed: list = list(range(world))  # members of the current communicator generation
         self._stop = threading.Event()
         try:
             os.unlink(path)
@@ -137,7 +142,7 @@ class Coordinator:
             else:
                 return
         if not self._stop.is_set():
-            self.reform(f"rank {r} lost")
+            self.reform(f"rank {r} lost", shrink_ok=True)
 
     def fanout(self, msg: dict) -> None:
         """Send ``msg`` to every live member, stamped with one global sequence number. Waits
@@ -155,7 +160,12 @@ class Coordinator:
             for r in dead:
                 self.members.pop(r, None)
 
-    def reform(self, reason: str) -> None:
+    def reform(self, reason: str, shrink_ok: bool = False) -> None:
+        """New communicator generation over the live members. ``shrink`` is offered only when the
+        members are a strict subset of the current generation (nobody joins), the trigger is a
+        lost control connection (the survivors' communicators were not aborted by a timed-out
+        collective). A member that cannot shrink re-initialises; the mismatch ends in a bounded
+        timeout -> ``fail`` -> a reform that always re-initialises."""
         with self.lock:
             self.epoch += 1
             tmp = f"{self._epoch_file}.{os.getpid()}"
@@ -163,9 +173,14 @@ class Coordinator:
                 f.write(str(self.epoch))
             os.replace(tmp, self._epoch_file)
             members = sorted(self.members)
-            self.reforms.append({"epoch": self.epoch, "members": members, "reason": reason})
-            log.warning("cluster reform epoch %d: members %s (%s)", self.epoch, members, reason)
-            msg = {"op": "reform", "epoch": self.epoch, "members": members, "reason": reason}
+            prev = list(self.formed)
+            shrink = bool(shrink_ok and members and set(members) < set(prev))
+            self.formed = members
+            self.reforms.append({"epoch": self.epoch, "members": members, "reason": reason, "shrink": shrink})
+            log.warning("cluster reform epoch %d: members %s (%s%s)", self.epoch, members, reason,
+                        ", shrink" if shrink else "")
+            msg = {"op": "reform", "epoch": self.epoch, "members": members, "reason": reason,
+                   "shrink": shrink, "prev": prev}
             self.seq += 1
             msg["seq"] = self.seq
             for r, (conn, f, lk) in list(self.members.items()):
@@ -374,24 +389,36 @@ class Member:
     def _reform(self, msg):
         members = msg["members"]
         old, self.comm = self.comm, None
+        self.epoch = msg["epoch"]
+        t0 = time.perf_counter()
+        how = "init"
+        if self.rank in members and msg.get("shrink") and old is not None and hasattr(old, "shrink") \
+                and list(self.members) == list(msg.get("prev", ())):
+            excl = [i for i, r in enumerate(self.members) if r not in members]
+            try:
+                self.comm = old.shrink(excl, abort_parent=True)
+                self.members = members
+                how = "shrink"
+            except CommError as e:  # the others shrank: this rank's init cannot match them; the
+                log.error("rank %d: shrink in epoch %d failed: %s", self.rank, self.epoch, e)  # timeout re-forms
         if old is not None:
             try:
                 old.abort()
                 old.close()
             except Exception:  # noqa: BLE001
                 pass
-        self.epoch = msg["epoch"]
         if self.rank not in members:
             return
-        t0 = time.perf_counter()
-        try:
-            self.comm = self.comm_factory(self.epoch, members) if len(members) > 0 else None
-            self.members = members
-        except CommError as e:
-            log.error("rank %d: reform epoch %d failed: %s", self.rank, self.epoch, e)
-            self._fail(str(e))
-            return
-        self.reforms.append({"epoch": self.epoch, "members": members, "ms": (time.perf_counter() - t0) * 1e3})
+        if self.comm is None:
+            try:
+                self.comm = self.comm_factory(self.epoch, members) if len(members) > 0 else None
+                self.members = members
+            except CommError as e:
+                log.error("rank %d: reform epoch %d failed: %s", self.rank, self.epoch, e)
+                self._fail(str(e))
+                return
+        self.reforms.append({"epoch": self.epoch, "members": members, "how": how,
+                             "ms": (time.perf_counter() - t0) * 1e3})
 
     def close(self):
         self.alive = False

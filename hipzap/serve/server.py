@@ -320,6 +320,16 @@ class ModelServer:
         return None
 
     def text(self, name: str):
+        plan = self._plan_for(name)
+        if plan is not None:
+            from ..lite import read_meta
+            if read_meta(plan).get("kind") == "text":
+                with self._lock:
+                    if name not in self._models:
+                        with trace_range(f"cold_start:{name}"):
+                            self._models[name] = PlanTextBackend(name, plan, self.settings.devices[0], self.spec(name))
+                        self.stats["cold_loads"] += 1
+                    return self._models[name]
         return self._load(name, TextBackend)
 
     def lm(self) -> LMBackend:
@@ -437,6 +447,70 @@ class PlanVisionBackend:
                                      f"{list(self.in_shape[1:])} (image_b64 or a uint8 .npy)")
                 self._torch = VisionBackend(self.name, ckpt, "gpu", f"cuda:{self.device}", self.spec, True)
         return self._torch(x)
+
+class PlanTextBackend:
+    """Torch-free BERT-style serving from a text plan image (``hipzap plan --model bert-base
+    --batch B``; meta ``kind: text``): a request is up to B sequences of token ids (+ optional
+    token types / attention mask), padded on the host to the captured (B, seq_len) -- padding
+    tokens are masked out with the additive mask, exactly as :class:`TextBackend` pads -- and one
+    hipGraph replay through the native per-request executor. Token ids outside the vocabulary
+    are rejected here (the embedding kernel also clamps them)."""
+    backend = "gpu"
+
+    def __init__(self, name: str, plan: str, device: int, spec: ModelSpec):
+        from ..lite import PlanEngine
+        t0 = time.perf_counter()
+        self.name, self.plan, self.spec, self.device = name, plan, spec, device
+        self.engine = PlanEngine(plan, device=device, contexts=max(1, spec.contexts), eager_contexts=1,
+                                 capture="lazy")
+        m = self.engine.meta
+        if m.get("kind") != "text":
+            raise ValueError(f"{plan} is not a text plan")
+        self.meta = m
+        self.batch, self.seq_len = int(m["batch"]), int(m["seq_len"])
+        self.vocab, self.type_vocab = int(m["vocab"]), int(m["type_vocab"])
+        self.num_labels = m["output"].get("num_labels") or m["output"]["shape"][-1]
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+        threading.Thread(target=self.engine.ensure_contexts, daemon=True, name=f"{name}-contexts").start()
+
+    def infer_np(self, ids, types=None, mask=None):
+        """``ids`` (and optional ``types`` / ``mask``): int arrays [n, L] with L <= seq_len ->
+        numpy float32 logits [n, num_labels]."""
+        import numpy as np
+        ids = np.asarray(ids)
+        if ids.ndim == 1:
+            ids = ids[None]
+        n, L = ids.shape
+        types = np.zeros_like(ids) if types is None else np.asarray(types).reshape(ids.shape)
+        mask = np.ones_like(ids) if mask is None else np.asarray(mask).reshape(ids.shape)
+        if L > self.seq_len:
+            raise ValueError(f"sequence length {L} exceeds the captured {self.seq_len}")
+        if ids.size and (ids.min() < 0 or ids.max() >= self.vocab):
+            raise ValueError(f"token ids must lie in [0, {self.vocab})")
+        if types.size and (types.min() < 0 or types.max() >= self.type_vocab):
+            raise ValueError(f"token type ids must lie in [0, {self.type_vocab})")
+        B, Lc = self.batch, self.seq_len
+        out = np.empty((n, self.num_labels), np.float32)
+        for i in range(0, n, B):
+            m = min(B, n - i)
+            ci = np.zeros((B, Lc), np.int32)
+            ct = np.zeros((B, Lc), np.int32)
+            cm = np.zeros((B, Lc), np.float32)  # padding tokens and rows: mask 0 -> additive -1e9
+            ci[:m, :L] = ids[i: i + m]
+            ct[:m, :L] = types[i: i + m]
+            cm[:m, :L] = mask[i: i + m]
+            madd = (np.float32(1.0) - cm) * np.float32(-1e9)
+            y = np.frombuffer(self.engine.infer_raw([ci, ct, madd]), np.float32).reshape(B, -1)
+            out[i: i + m] = y[:m, : self.num_labels]
+        return out
+
+    def __call__(self, ids, types=None, mask=None):
+        """torch-tensor entry (TextBackend's interface): logits as a torch tensor."""
+        import torch
+        def arr(t):
+            return None if t is None else t.cpu().numpy()
+        return torch.from_numpy(self.infer_np(arr(ids), arr(types), arr(mask)))
+
 
 def synthetic_vocab(n: int) -> list[str]:
     """fastai-style vocabulary for random-weight demos: specials first, then pseudo-words."""

@@ -44,7 +44,8 @@ def _worker(rank, world, rdzv, conn, join=False):
                 conn.send(("err", type(e).__name__))
         elif cmd == "state":
             conn.send({"members": m.members, "epoch": m.epoch, "health": dict(m.health), "alive": m.alive,
-                       "abandoned": m.abandoned, "reforms": coord.reforms if coord else None})
+                       "abandoned": m.abandoned, "reforms": coord.reforms if coord else None,
+                       "member_reforms": list(m.reforms)})
         elif cmd == "crash":
             os._exit(3)
 
@@ -103,6 +104,11 @@ def test_batched_jobs_from_any_rank_and_reform_after_a_worker_dies(cluster):
     np.testing.assert_array_equal(y, model_fn(x))
     coord = _call(pipes[0], "state")["reforms"]
     assert coord and coord[-1]["members"] == [0, 1] and "lost" in coord[-1]["reason"]
+    # a lost member only: the survivors shrank their communicator (no new rendezvous id)
+    assert coord[-1]["shrink"] is True
+    for r in (0, 1):
+        mr = _call(pipes[r], "state")["member_reforms"]
+        assert mr and mr[-1]["how"] == "shrink" and mr[-1]["members"] == [0, 1], mr
 
 
 @pytest.mark.timeout(240)

@@ -53,6 +53,48 @@ def test_rccl_world1_collectives(tmp_path):
     comm.close()
 
 
+def _allreduce_ok(comm, hip) -> bool:
+    buf = hip.DeviceBuffer(64)
+    host = (C.c_int * 16)(*range(16))
+    hip.memcpy(buf.ptr, C.addressof(host), 64, hip.H2D)
+    comm.allreduce_ptr(buf.ptr, 16, "int32", "sum")
+    back = (C.c_int * 16)()
+    hip.memcpy(C.addressof(back), buf.ptr, 64, hip.D2H)
+    return list(back) == [v * comm.world for v in range(16)]
+
+
+def test_rccl_world1_shrink_abort_and_reform(tmp_path):
+    """the RCCL (not socket) reform path. A Member's _reform with a shrink message
+    shrinks the live RCCL communicator (ncclCommShrink, parent aborted); an aborted communicator
+    reports -3 from poll and refuses to shrink (the member then re-initialises from a fresh
+    unique id through the rendezvous directory, as after a timed-out collective)."""
+    from hipzap import hip
+    from hipzap.parallel.base import CommError
+    from hipzap.parallel.rccl import RcclComm
+    from hipzap.serve.cluster import Member, make_comm_factory
+    factory = make_comm_factory("rccl", str(tmp_path), 0, 0, 30.0)
+    comm = factory(0, [0])
+    assert isinstance(comm, RcclComm) and _allreduce_ok(comm, hip)
+    # a Member without a control plane: only its sequenced-reform logic is exercised here
+    m = Member.__new__(Member)
+    m.rank, m.comm, m.comm_factory, m.members, m.epoch, m.reforms = 0, comm, factory, [0], 0, []
+    m._fail = lambda reason: (_ for _ in ()).throw(AssertionError(reason))
+    m._reform({"op": "reform", "epoch": 1, "members": [0], "shrink": True, "prev": [0]})
+    assert m.reforms[-1]["how"] == "shrink", m.reforms
+    assert m.comm is not comm and m.comm.world == 1 and m.comm.poll() == 0 and _allreduce_ok(m.comm, hip)
+    assert comm._h is None  # the parent was aborted and destroyed by the reform
+    # an aborted communicator: poll reports it, shrink is refused, a reform re-initialises
+    shrunk = m.comm
+    shrunk.abort()
+    assert shrunk.poll() == -3
+    with pytest.raises(CommError):
+        shrunk.shrink([])
+    m._reform({"op": "reform", "epoch": 2, "members": [0], "shrink": True, "prev": [0]})
+    assert m.reforms[-1]["how"] == "init", m.reforms
+    assert m.comm is not shrunk and m.comm.poll() == 0 and _allreduce_ok(m.comm, hip)
+    m.comm.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -115,7 +115,7 @@ def _mx_decode(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
     return q8.view(torch.float8_e4m3fn).float() * sc
 
 
-@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32])
+@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 40, 41, 42])
 @pytest.mark.parametrize("mx_in,mx_out", [(True, False), (False, True), (True, True)])
 def test_gemm_mx8_activations(cfg, mx_in, mx_out):
     """MX8 (e4m3 + E8M0 per 32 k) activations into the block-scaled MFMA, and MX8 output from
@@ -151,6 +151,45 @@ def test_gemm_mx8_activations(cfg, mx_in, mx_out):
         assert ((got - ref_q).abs().max() / ref_q.abs().max()).item() < 0.1  # <= one e4m3 step
     else:
         assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+
+
+@pytest.mark.parametrize("cfg", [33, 40, 41, 42])
+@pytest.mark.parametrize("mx_in,mx_out", [(False, False), (True, True)])
+def test_gemm_mx256_bitwise_vs_128(cfg, mx_in, mx_out):
+    """The 256-row MX kernels (plain 256x256 and the pipelined 256x256 / 256x128) sum every
+    output over the same k-steps in the same order with the same instruction and epilogue as the
+    8-wave 128x128 kernel (cfg 24): results are BITWISE equal, over several row tiles (one
+    partial) and column tiles, bf16 or MX8 output."""
+    import ctypes
+    from hipzap import _native as N
+    g = torch.Generator().manual_seed(11)
+    M, Nn, K = 700, 768, 1024
+    w = torch.randn(Nn, K, generator=g) * 0.05
+    b = torch.randn(Nn, generator=g)
+    x = torch.randn(M, K, generator=g) * torch.linspace(0.1, 8, K)
+    pw = F8.quantize_linear(C.pack_linear(w, b))
+    pwd = F8.PackedFp8(pw.w8.to(DEV), pw.sw.to(DEV), pw.bias.to(DEV), pw.cin, pw.cout, pw.w8mx.to(DEV))
+    if mx_in:
+        q8, s8, _ = _mx_encode(x)
+        x8, xs, sx = q8.to(DEV), s8.to(DEV), None
+    else:
+        x8, sx = F8.quant_rows(x.to(torch.bfloat16).to(DEV))
+        xs = None
+    outs = []
+    for c in (24, cfg):
+        out = torch.full((M, Nn), 7.0, device=DEV, dtype=torch.bfloat16)
+        o8 = torch.zeros(M, Nn, dtype=torch.uint8, device=DEV)
+        os8 = torch.zeros(M, Nn // 32, dtype=torch.uint8, device=DEV)
+        prm = F8.gemm_params(x8.data_ptr(), N.ptr(sx), pwd, M, 0 if mx_out else out.data_ptr(), 0, "gelu", False, c,
+                             1, xs_ptr=N.ptr(xs), out8_ptr=o8.data_ptr() if mx_out else 0,
+                             os8_ptr=os8.data_ptr() if mx_out else 0)
+        N.check(N.lib().hz_launch_kernel(F8.K_GEMM_FP8, ctypes.byref(prm), N.stream_ptr()), f"gemm cfg {c}")
+        torch.cuda.synchronize()
+        outs.append((o8.cpu(), os8.cpu()) if mx_out else (out.cpu(),))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_), f"cfg {cfg} differs from cfg 24"
+    if not mx_out:
+        assert not (outs[1][0] == 7.0).all(-1).any(), "rows left unwritten"
 
 
 def test_attention_mx8_output():

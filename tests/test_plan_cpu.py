@@ -148,3 +148,25 @@ def test_sampled_digest_detects_same_size_replacement(tmp_path):
     s2 = source_stamp(str(p))
     assert s1["size"] == s2["size"] and s1["mtime_ns"] == s2["mtime_ns"]
     assert s1["sampled_sha256"] != s2["sampled_sha256"]
+
+
+def test_bert_text_plan_meta(tmp_path):
+    """BERT exports as a TEXT plan: three adjacent host inputs (ids, token types,
+    additive mask) that PlanTextBackend fills in one copy, and the table sizes the server checks
+    request ids against."""
+    from hipzap.lite import read_meta
+    a = registry.get("bert-base")
+    torch.manual_seed(0)
+    from hipzap.models.bert import make_model
+    m = make_model(2, num_hidden_layers=2)
+    params, kw = a.pack(m.state_dict(), "cpu")
+    path = str(tmp_path / "bert.hzplan")
+    P.export_plan("bert-base", params, dict(kw), path, batch=4)
+    meta = read_meta(path)
+    assert meta["kind"] == "text" and meta["batch"] == 4 and meta["seq_len"] == 128
+    assert meta["vocab"] == 30522 and meta["type_vocab"] == 2
+    ins = meta["inputs"]
+    assert [i["dtype"] for i in ins] == ["int32", "int32", "float32"]
+    assert all(i["region"] == 2 for i in ins)
+    assert all(ins[k]["off"] + ins[k]["bytes"] == ins[k + 1]["off"] for k in range(2)), ins
+    assert meta["output"]["num_labels"] == 2

@@ -91,7 +91,7 @@ def test_predict_npy_and_image(client):
 
 def test_predict_bad_request_is_json_error(client):
     r = client.post("/predict", json={"nothing": 1})
-    assert r.status_code == 500 and r.json["error"] == "ValueError"
+    assert r.status_code == 400 and r.json["error"] == "ValueError"
 
 
 def test_metrics(client):
