@@ -68,6 +68,13 @@ def parse():
     ap.add_argument("--dyn-clients", type=int, default=96)
     ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
+    ap.add_argument("--http-clients", type=int, default=int(os.environ.get("HIPZAP_BENCH_HTTP_CLIENTS", 8)),
+                    help="secondary figure: HTTP client processes PER GPU against `hipzap serve --gpus N` "
+                         "(0 disables)")
+    ap.add_argument("--http-requests", type=int, default=800, help="requests per HTTP client process")
+    ap.add_argument("--bert-cold", type=int, default=1, help="also report the BERT-base text-plan cold start")
+    ap.add_argument("--sustained-s", type=float, default=2.0,
+                    help="secondary figure: served throughput over a self-timed window of at least this long")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
                     help="replica: independent bs=1 request streams per GPU (headline); scatter: rank 0 scatters "
                          "a global batch over ranks and gathers the logits (configs 3/5)")
@@ -177,7 +184,33 @@ def fresh_cold_start(args, device_index: int) -> dict:
         res["native"] = measure_fresh("native", plan, args.model, args.cold_trials, device=device_index)
     except Exception as e:  # noqa: BLE001 - not built: the Python plan path stays the headline
         print(f"native cold start skipped: {e}", file=sys.stderr)
+    if args.bert_cold:
+        try:  # BERT-base seq-cls (BASELINE config 4) from its text plan image: torch-free too
+            res["bert_plan"] = measure_fresh("plan", prepare_bert_plan(args.ckpt_dir), "bert-base",
+                                             min(3, args.cold_trials), device=device_index)
+        except Exception as e:  # noqa: BLE001 - secondary figure
+            print(f"BERT plan cold start skipped: {e}", file=sys.stderr)
     return res
+
+
+def prepare_bert_plan(ckpt_dir: str) -> str:
+    """Deploy-time BERT-base artifacts (untimed, CPU): a random-init checkpoint and its bs16 text
+    plan image (``hipzap plan --model bert-base --batch 16``); reused while up to date."""
+    from hipzap.engine.packfile import source_stamp
+    from hipzap.engine.plan import export_from_checkpoint, plan_path
+    from hipzap.lite import plan_usable, read_meta
+    from hipzap.models import registry
+    ckpt = os.path.join(ckpt_dir, "bert-base_seed0.pth")
+    if not os.path.exists(ckpt):
+        torch.manual_seed(0)
+        os.makedirs(ckpt_dir, exist_ok=True)
+        tmp = ckpt + f".tmp{os.getpid()}"
+        torch.save(registry.get("bert-base").make_model().eval().state_dict(), tmp)
+        os.replace(tmp, ckpt)
+    plan = plan_path(ckpt)
+    if not (plan_usable(plan) and read_meta(plan).get("source") == source_stamp(ckpt)):
+        export_from_checkpoint("bert-base", ckpt, plan, batch=16, contexts=1)
+    return plan
 
 
 def torch_reference_throughput(model, device, iters=200):
@@ -246,6 +279,37 @@ def dynamic_batching(args, eng, device, world):
     ex.close()
     del deng
     return out
+
+
+def http_figure(args, world: int, rank: int):
+    """Secondary figure: the serving SYSTEM over HTTP on the whole node -- ``python -m hipzap
+    serve --gpus N`` (serve/cluster.py: one worker process per GPU sharing the listening socket,
+    RCCL between the workers; N = 1: one server) from the plan image, loaded by
+    ``--http-clients`` x N client processes sending bs=1 uint8 images (npy bodies) over
+    keep-alive connections (hipzap/serve/loadtest.py). Run by rank 0 after the headline; the other
+    ranks wait on the process group's TCP store (a CPU wait: no collective kernel spins on the
+    GPUs the servers use). Returns the load result, or None if it could not run."""
+    from datetime import timedelta
+    from hipzap.parallel.comm import is_dist
+    res = None
+    if rank == 0:
+        try:
+            from hipzap.serve.loadtest import run_load
+            _, plan = prepare_artifacts(args.model, args.ckpt_dir)
+            res = run_load(plan, gpus=world, clients=args.http_clients * world, requests=args.http_requests,
+                           contexts=8, fmt="npy", ready_timeout=300.0)
+            if not res.get("errors"):
+                res.pop("server_log_tail", None)
+        except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
+            print(f"http serving figure skipped: {e!r}", file=sys.stderr)
+            res = None
+    if is_dist():
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("hipzap_http_done", "1")
+        else:
+            store.wait(["hipzap_http_done"], timedelta(seconds=1200))
+    return res
 
 
 def request_input(args, adapter):
@@ -501,6 +565,20 @@ def main():
     if is_dist():
         dist.barrier()
     dt = max_over_ranks(dt, device)
+    # a longer self-timed window of the same serving loop (>= --sustained-s), so box noise over the
+    # driver's short K-step region is not mistaken for kernel wins (same on every rank: dt is the max)
+    sustained = None
+    if args.sustained_s > 0:
+        n_long = int(min(50000, max(args.steps, -(-args.sustained_s * args.steps // dt))))
+        if is_dist():
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t_l = time.perf_counter()
+        run(n_long, args.serve)
+        torch.cuda.synchronize(device)
+        dt_l = max_over_ranks(time.perf_counter() - t_l, device)
+        sustained = {"inf_s": round(world * args.streams * args.batch * n_long / dt_l, 2), "steps": n_long,
+                     "window_s": round(dt_l, 3)}
     # the other serving mode, untimed for the headline (same K), for reference
     dt_other, lat_other = run(args.steps, other)
     dt_other = max_over_ranks(dt_other, device)
@@ -512,6 +590,7 @@ def main():
     from hipzap.engine.program import bench_contexts
     t_single = bench_contexts([single], [eng.streams[0]], 200)
     dyn = dynamic_batching(args, eng, device, world) if args.dyn_batch > 1 and args.batch == 1 else None
+    http = http_figure(args, world, rank) if args.http_clients > 0 and args.batch == 1 else None
     torch_ref = None
     if args.compare_torch and rank == 0:
         try:
@@ -548,6 +627,8 @@ def main():
             "cold_start_pth_torch_ms_p50": fresh["pth"]["p50_ms"] if fresh else None,
             # the Python-free server binary (hipzap-serve-plan --once) on the same plan image
             "cold_start_native_ms_p50": (fresh.get("native") or {}).get("p50_ms") if fresh else None,
+            # BERT-base bs16 seq-cls from its text plan image (torch-free)
+            "cold_start_bert_plan_ms_p50": (fresh.get("bert_plan") or {}).get("p50_ms") if fresh else None,
             "cold_start_fresh_process": fresh,
             "cold_start_inprocess_ms_first": round(cold_first, 2),
             "cold_start_inprocess_ms_p50": round(statistics.median(colds), 2),
@@ -568,6 +649,10 @@ def main():
         }
         if dyn is not None:
             res["dynamic_batching"] = dyn
+        if sustained is not None:
+            res["served_sustained"] = sustained
+        if http is not None:
+            res["http_serving"] = http
         if torch_ref is not None:
             res["torch_miopen_graph_inf_s_1gpu_1stream"] = round(torch_ref, 2)
         print(json.dumps(res), flush=True)

@@ -10,6 +10,7 @@
 // gfx950 converts with v_cvt_pk_fp8_f32, which on CDNA4 is the OCP e4m3fn encoding (NOT the
 // MI300 FNUZ variant) — checked against torch.float8_e4m3fn in tests/test_fp8_gpu.py.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "hipzap.h"
@@ -454,29 +455,27 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
-// ---- pipelined 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608) ----
-// The 128x128 tiles above move 32 KB per 128-deep k-step for 4 MFLOP: at M = 12,608 the
-// projections run at ~0.8 PF/s, bound by the L2 -> CU staging traffic (~7 TB/s chip-wide,
-// profiles/r3_tx_base), not by the MFMA. This kernel doubles the work per staged byte: a
-// 256 x BN tile (BN = 256: 64 KB per k-step for 16.8 MFLOP), ONE 8-wave workgroup per CU
-// (2 waves per SIMD), wave (wm, wn) owning 128 tokens x BN/4 features. Inside a k-step the wave
-// keeps its BN/64 weight fragments in registers and walks its 8 token fragments in 4 sub-blocks
-// of 2; the next sub-block's fragments are read from LDS while the current one's MFMAs issue
-// (register double buffer), and the NEXT stage's glds pieces are issued between the first two
-// sub-blocks rather than in one burst. Same LDS images, swizzle, hardware K order, block scales
-// and epilogue as gemm_mx_kernel; NS = 2 (BN 256, 132 KB) or 3 (BN 128, 150 KB) stages with
-// counted vmcnt + raw s_barrier.
+// ---- 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608): measured, never chosen ----
+// A 256 x BN tile moves half the staging bytes per FLOP of the 128x128 tiles (BN = 256: 64 KB per
+// k-step for 16.8 MFLOP) with ONE 8-wave workgroup per CU, wave (wm, wn) owning 128 tokens x BN/4
+// features. Same LDS images, swizzle, hardware K order, block scales and epilogue as
+// gemm_mx_kernel. The main k-loop is branch-free (the last NS-1 k-steps, which stage nothing, are
+// a peeled tail); per step: barrier -> the next stage's glds pieces -> token fragment 0, W, token
+// fragment 1 reads -> MFMAs of token fragment f while f+1 / f+2 reads are in flight;
+// sched_barrier(0) pins that order. Measured on the ViT shapes (profiles/r3_mx256): 1.3-1.5x
+// SLOWER than the 8-wave 128x128 tile at two workgroups per CU (QKV 65-74 vs 50 us): with one
+// workgroup per CU the staging latency is not hidden, whatever the in-step order; the tuner keeps
+// these as candidates (cfg 43-45) and never picks them.
 template <int BN, int NS, bool XS>
-__global__ __launch_bounds__(512) void gemm_mxp_kernel(const HzGemmFp8Params p, int group_m) {
+__global__ __launch_bounds__(512) void gemm_mxq_kernel(const HzGemmFp8Params p, int group_m) {
   constexpr int BM = 256, WM = 2, WN = 4, NW = 8;
-  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 4|2 weight, 8 token fragments per wave
-  constexpr int SB = 4, TPS = FPW / SB;                  // sub-blocks of 2 token fragments
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;
   constexpr int NWG = BN / 16;
   constexpr int XBYTES = BM * 128;
   constexpr int WBYTES = NWG * 2048;
   constexpr int SBYTES = XBYTES + WBYTES + (XS ? NW * 256 : 0);
   constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;
-  static_assert(XPW * 8 * NW == BM && WPW * NW == NWG * 2 && FCW >= 1 && TPS * SB == FPW, "tile / wave split");
+  static_assert(XPW * 8 * NW == BM && WPW * NW == NWG * 2 && FCW >= 1 && FCW * 2 + 6 <= 15, "tile / wave split");
   constexpr int G = XPW + WPW + (XS ? 1 : 0);
   static_assert(NS * SBYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
@@ -500,19 +499,16 @@ __global__ __launch_bounds__(512) void gemm_mxp_kernel(const HzGemmFp8Params p, 
   }
   const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
   const unsigned char* ssrc = XS ? p.xs + (long)min(m0 + (wave & 3) * 64 + lane, p.M - 1) * (p.K >> 5) : nullptr;
-  auto stage_x = [&](int buf, int st) {  // activations (+ block scales): XPW (+1) pieces
+  auto stage = [&](int buf, int st) {
     char* base = smem + buf * SBYTES;
-    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
 #pragma unroll
     for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
-  };
-  auto stage_w = [&](int buf, int st) {  // weights: WPW pieces
-    char* base = smem + buf * SBYTES;
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
       const int piece = wave + NW * i;
       glds16_8(wsrc + ((long)(piece >> 1) * kb + st) * 2048 + (piece & 1) * 1024, base + XBYTES + piece * 1024);
     }
+    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
   };
 
   const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
@@ -532,73 +528,74 @@ __global__ __launch_bounds__(512) void gemm_mxp_kernel(const HzGemmFp8Params p, 
 #pragma unroll
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < kb) {
-      stage_x(s0, s0);
-      stage_w(s0, s0);
+  // one k-step on buffer `cur`; STAGE: issue the glds pieces of step st + NS - 1 first. LDS reads
+  // are ordered [x0, W, x1] then x(f+2) after the MFMAs of token fragment f, so at most 14 reads
+  // are outstanding (the lgkm counter saturates at 15 -- beyond it hipcc falls back to
+  // lgkmcnt(0)) and every MFMA group waits only for its own operands.
+  auto kstep = [&](auto staged, int st, int cur) {
+    constexpr bool STAGE = decltype(staged)::value;
+    if constexpr (STAGE) {
+      stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
+      __builtin_amdgcn_sched_barrier(0);
     }
-  int cur = 0;
-  for (int st = 0; st < kb; ++st) {
-    const int ahead = min(NS - 2, kb - 1 - st);  // stages issued beyond st that may stay in flight
-    if (NS > 2 && ahead >= 1) wait_vm8<(NS > 2 ? G : 0)>();
-    else wait_vm8<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const bool pre = st + NS - 1 < kb;
-    const int nbuf = cur == 0 ? NS - 1 : cur - 1;
     const char* base = smem + cur * SBYTES;
-    i32x8 w[FCW], xa[TPS], xb[TPS];
+    i32x8 w[FCW], x[FPW];
+    int sc[FPW];
+    auto rdx = [&](int f) {
+      x[f] = rd(base + boff0 + f * 2048, base + boff1 + f * 2048);
+      if constexpr (XS) {
+        const int r = wm * (BM / WM) + f * 16 + lr;
+        sc[f] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
+                                                         (lane >> 4));
+      } else {
+        sc[f] = 0x7f7f7f7f;
+      }
+    };
+    rdx(0);
 #pragma unroll
     for (int i = 0; i < FCW; ++i) w[i] = rd(base + aoff + i * 2048, base + aoff + i * 2048 + 1024);
+    rdx(1);
 #pragma unroll
-    for (int j = 0; j < TPS; ++j) xa[j] = rd(base + boff0 + j * 2048, base + boff1 + j * 2048);
-#pragma unroll
-    for (int sb = 0; sb < SB; ++sb) {
-      if (sb + 1 < SB) {
-#pragma unroll
-        for (int j = 0; j < TPS; ++j)
-          xb[j] = rd(base + boff0 + ((sb + 1) * TPS + j) * 2048, base + boff1 + ((sb + 1) * TPS + j) * 2048);
-      }
-      if (pre && sb == 0) stage_x(nbuf, st + NS - 1);
-      if (pre && sb == 1) stage_w(nbuf, st + NS - 1);
-      int sc[TPS];
-#pragma unroll
-      for (int j = 0; j < TPS; ++j) {
-        if constexpr (XS) {
-          const int r = wm * (BM / WM) + (sb * TPS + j) * 16 + lr;
-          sc[j] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
-                                                           (lane >> 4));
-        } else {
-          sc[j] = 0x7f7f7f7f;
-        }
-      }
-      __builtin_amdgcn_s_setprio(1);
+    for (int f = 0; f < FPW; ++f) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FCW; ++i)
-#pragma unroll
-        for (int j = 0; j < TPS; ++j)
-          acc[i][sb * TPS + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w[i], xa[j], acc[i][sb * TPS + j], 0,
-                                                                                  0, 0, 0x7f7f7f7f, 0, sc[j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (sb + 1 < SB) {
-#pragma unroll
-        for (int j = 0; j < TPS; ++j) xa[j] = xb[j];
-      }
+        acc[i][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w[i], x[f], acc[i][f], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                     sc[f]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (f + 2 < FPW) rdx(f + 2);
     }
+  };
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < kb) stage(s0, s0);
+  int cur = 0, st = 0;
+  for (; st + NS - 1 < kb; ++st) {  // main loop: every step stages one (NS-2 further stages stay in flight)
+    wait_vm8<(NS - 2) * G>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    kstep(std::integral_constant<bool, true>{}, st, cur);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  for (; st < kb; ++st) {  // tail: nothing left to stage
+    wait_vm8<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    kstep(std::integral_constant<bool, false>{}, st, cur);
     cur = cur == NS - 1 ? 0 : cur + 1;
   }
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
 template <int BN, int NS>
-int launch_mxp(const HzGemmFp8Params& p, hipStream_t st) {
+int launch_mxq(const HzGemmFp8Params& p, hipStream_t st) {
   if (p.N % BN) return -4;
   const int tiles = (p.N / BN) * ((p.M + 255) / 256);
   static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
   const int group_m = group_env < 1 ? 1 : group_env;
-  if (p.xs) hipLaunchKernelGGL((gemm_mxp_kernel<BN, NS, true>), dim3(tiles), dim3(512), 0, st, p, group_m);
-  else hipLaunchKernelGGL((gemm_mxp_kernel<BN, NS, false>), dim3(tiles), dim3(512), 0, st, p, group_m);
+  if (p.xs) hipLaunchKernelGGL((gemm_mxq_kernel<BN, NS, true>), dim3(tiles), dim3(512), 0, st, p, group_m);
+  else hipLaunchKernelGGL((gemm_mxq_kernel<BN, NS, false>), dim3(tiles), dim3(512), 0, st, p, group_m);
   return (int)hipGetLastError();
 }
 
@@ -645,10 +642,11 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
-      // pipelined 256-row kernel: 256x256 / 2 stages, 256x128 / 2 and 3 stages
-      case 40: return launch_mxp<256, 2>(p, st);
-      case 41: return launch_mxp<128, 2>(p, st);
-      case 42: return launch_mxp<128, 3>(p, st);
+      // 256-row kernel (branch-free main loop, pinned read / MFMA order): 256x256 / 2 stages,
+      // 256x128 / 2 and 3 stages
+      case 43: return launch_mxq<256, 2>(p, st);
+      case 44: return launch_mxq<128, 2>(p, st);
+      case 45: return launch_mxq<128, 3>(p, st);
       default: return -2;
     }
   }

@@ -27,16 +27,32 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams 
   const bf16_t* x = p.x + (long)row * p.ldx;
   const bf16_t* r = p.res ? p.res + (long)row * p.ldr : nullptr;
   const int nch = p.D >> 3;
+  // every load of the row first -- x, residual, gamma, beta -- so the kernel pays ONE memory
+  // latency before the two reductions instead of a second one for gamma/beta after them
+  u32x4 xr[4], rr4[4];
+  f32x4 g4[4][2], b4[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int ch = c * 64 + lane;
+    if (ch < nch) {
+      xr[c] = *reinterpret_cast<const u32x4*>(x + ch * 8);
+      if (r) rr4[c] = *reinterpret_cast<const u32x4*>(r + ch * 8);
+      g4[c][0] = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8);
+      g4[c][1] = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8 + 4);
+      b4[c][0] = *reinterpret_cast<const f32x4*>(p.beta + ch * 8);
+      b4[c][1] = *reinterpret_cast<const f32x4*>(p.beta + ch * 8 + 4);
+    }
+  }
   float v[4][8];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int ch = c * 64 + lane;
     if (ch < nch) {
-      unpack8(*reinterpret_cast<const u32x4*>(x + ch * 8), v[c]);
+      unpack8(xr[c], v[c]);
       if (r) {
         float rr[8];
-        unpack8(*reinterpret_cast<const u32x4*>(r + ch * 8), rr);
+        unpack8(rr4[c], rr);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[c][e] += rr[e];
       }
@@ -63,10 +79,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams 
   for (int c = 0; c < 4; ++c) {
     const int ch = c * 64 + lane;
     if (ch < nch) {
-      const f32x4 g0 = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8);
-      const f32x4 g1 = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.beta + ch * 8);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.beta + ch * 8 + 4);
+      const f32x4 g0 = g4[c][0], g1 = g4[c][1], b0 = b4[c][0], b1 = b4[c][1];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[c][e] = (v[c][e] - mean) * rstd * g0[e] + b0[e];

@@ -102,9 +102,10 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256),
             # 30-32: 4 LDS stages (8-wave 128x128; 4-wave 64x128, 128x64)
             30: (128, 128), 31: (64, 128), 32: (128, 64),
-            # 33: 8-wave 256x256 (plain); 40-42: pipelined 256-row kernel (256x256 2 stages, 256x128 2 / 3)
-            33: (256, 256), 40: (256, 256), 41: (256, 128), 42: (256, 128)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 40, 41, 42)
+            # 33: 8-wave 256x256 (plain); 43-45: the 256-row kernel (256x256 2 stages, 256x128 2 / 3):
+            # measured slower than 24 at one workgroup per CU, kept as tuner candidates (profiles/r3_mx256)
+            33: (256, 256), 43: (256, 256), 44: (256, 128), 45: (256, 128)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 43, 44, 45)
 
 
 def mx_fits(cfg: int, n: int) -> bool:
