@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--dyn-clients", type=int, default=96)
     ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
-    ap.add_argument("--http-clients", type=int, default=int(os.environ.get("HIPZAP_BENCH_HTTP_CLIENTS", 8)),
+    ap.add_argument("--http-clients", type=int, default=int(os.environ.get("HIPZAP_BENCH_HTTP_CLIENTS", 12)),
                     help="secondary figure: HTTP client processes PER GPU against `hipzap serve --gpus N` "
                          "(0 disables)")
     ap.add_argument("--http-requests", type=int, default=800, help="requests per HTTP client process")

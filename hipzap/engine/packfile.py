@@ -58,6 +58,19 @@ def source_stamp(ckpt_path: str) -> dict:
     return {"size": st.st_size, "mtime_ns": st.st_mtime_ns, "sampled_sha256": sampled_digest(ckpt_path)}
 
 
+def same_source(stamp: dict | None, ckpt_path: str, content_only: bool = False) -> bool:
+    """``stamp`` (recorded when an artifact was derived) still describes ``ckpt_path``.
+    ``content_only``: compare size + sampled digest but not mtime -- for a checkpoint and its
+    derived artifact fetched together from an artifact store, where the local copies' mtimes are
+    the download times."""
+    if not stamp:
+        return False
+    cur = source_stamp(ckpt_path)
+    if content_only:
+        return stamp.get("size") == cur["size"] and stamp.get("sampled_sha256") == cur["sampled_sha256"]
+    return stamp == cur
+
+
 def find_packed(ckpt_path: str, model: str) -> str | None:
     """The packed file for ``ckpt_path`` if it exists, was packed for ``model`` and the source
     checkpoint is unchanged since; else None (the caller packs from the .pth)."""

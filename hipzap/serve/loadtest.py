@@ -27,7 +27,7 @@ _LAUNCH_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RA
                "TORCHELASTIC_MAX_RESTARTS", "HIPZAP_SELF_LAUNCHED")
 
 
-def client(port, n, fmt, q):
+def client(port, n, fmt, q, start=None):
     import numpy as np
     rng = np.random.default_rng(os.getpid())
     img = rng.integers(0, 256, (224, 224, 3), dtype=np.uint8)
@@ -39,7 +39,10 @@ def client(port, n, fmt, q):
         body = json.dumps({"image_b64": base64.b64encode(img.tobytes()).decode(), "shape": [224, 224, 3]})
         ctype = "application/json"
     conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+    conn.connect()
     lat, errors = [], 0
+    if start is not None:  # every client set up (interpreter, numpy, body, connection) before the window
+        start.wait()
     for _ in range(n):
         t = time.perf_counter()
         try:
@@ -138,9 +141,11 @@ def run_load(plan: str, gpus: int = 1, clients: int = 16, requests: int = 200, c
             [p.start() for p in ps]
             [q.get() for _ in ps]
             [p.join() for p in ps]
-        ps = [ctx.Process(target=client, args=(port, requests, fmt, q)) for _ in range(clients)]
-        t0 = time.perf_counter()
+        start = ctx.Barrier(clients + 1)
+        ps = [ctx.Process(target=client, args=(port, requests, fmt, q, start)) for _ in range(clients)]
         [p.start() for p in ps]
+        start.wait(timeout=120)  # the timed window opens once every client is connected
+        t0 = time.perf_counter()
         res = [q.get() for _ in ps]
         wall = time.perf_counter() - t0
         [p.join() for p in ps]

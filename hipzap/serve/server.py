@@ -299,7 +299,9 @@ class ModelServer:
 
     def _plan_for(self, name: str) -> str | None:
         """The up-to-date plan image of this model's checkpoint, if the GPU backend can use it
-        (``extra.plan`` names one explicitly; else ``<ckpt>.hzplan``; HIPZAP_PLAN=0 disables)."""
+        (``extra.plan`` names one explicitly; else ``<ckpt>.hzplan`` next to the fetched
+        checkpoint -- fetched from the artifact store too when it was published there,
+        ``hipzap plan`` + ``hipzap upload`` -- validated by content; HIPZAP_PLAN=0 disables)."""
         if self.backend != "gpu" or os.environ.get("HIPZAP_PLAN", "1") == "0":
             return None
         spec = self.spec(name)
@@ -308,12 +310,20 @@ class ModelServer:
         if spec.key in (None, "random") or os.environ.get("HIPZAP_RANDOM_WEIGHTS"):
             return None
         from ..lite import plan_usable, read_meta
-        from ..engine.packfile import source_stamp
+        from ..engine.packfile import same_source
         ckpt = self.store.fetch(spec.key)
         path = ckpt + ".hzplan"
+        fetched = False
+        if not os.path.exists(path):
+            try:  # published next to the checkpoint in the store (its cache path is <ckpt>.hzplan)
+                path = self.store.fetch(spec.key + ".hzplan")
+                fetched = True
+            except Exception:  # noqa: BLE001 - no plan in the store: the checkpoint path serves
+                return None
         try:
-            if plan_usable(path) and read_meta(path).get("source") == source_stamp(ckpt) \
-                    and read_meta(path).get("model") == name:
+            meta = read_meta(path)
+            if plan_usable(path) and meta.get("model") == name and \
+                    same_source(meta.get("source"), ckpt, content_only=fetched or self.store.bucket is not None):
                 return path
         except OSError:
             pass

@@ -102,7 +102,9 @@ def test_text_plan_served_by_the_app(bert, monkeypatch):
         assert r.status_code == 400 and r.json["error"] == "ValueError"
     finally:
         app_mod.set_server(None)
-        srv._models["bert-base"].engine.close()
+        be = srv._models.get("bert-base")
+        if be is not None and hasattr(be.engine, "close"):
+            be.engine.close()
 
 
 def test_text_plan_fresh_process_cold_start(bert):
