@@ -3,7 +3,7 @@
 # rocprofv3 --pmc run per pass (per-block counter limits), summaries -> gpurun_out/pmc8/
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc8
+OUT=gpurun_out/${TAG:-pmc8}
 mkdir -p $OUT
 P1="SQ_WAVES SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F8 SQ_INSTS_MFMA GRBM_GUI_ACTIVE GRBM_COUNT"
 P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F8"
