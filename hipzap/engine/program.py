@@ -108,7 +108,8 @@ class ExecContext:
                 # a conv with row-major output (ViT patch embedding) never runs as the LDS implicit GEMM
                 lds_pc = None if n.kind == "conv" and n.attrs.get("rowmajor") else pc
                 cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=lds_pc)
-            if _ln_folded(n) and cfg not in conv_ops.LDS_TILES:  # HzLnFold lives in the LDS GEMM epilogue
+            # HzLnFold lives in the 16x16 LDS GEMM epilogue (not in the 32x32x16 M32 tiles)
+            if _ln_folded(n) and (cfg not in conv_ops.LDS_TILES or cfg in conv_ops.M32_CFGS):
                 if not conv_ops.lds_ok(M, pc.K, True, pc):
                     raise ValueError(f"{n.attrs.get('name')}: folded LayerNorm needs the LDS GEMM (M={M} < 64?)")
                 cfg, kw = 19, 1

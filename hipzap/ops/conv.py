@@ -29,10 +29,15 @@ LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
              28: (128, 128), 29: (128, 128), 30: (256, 128), 31: (128, 64), 32: (64, 128),
              33: (256, 64),  # 28-33: 8-wave workgroups
              34: (64, 96), 35: (128, 192), 36: (128, 192), 37: (64, 288), 38: (64, 288), 39: (256, 96),
-             40: (64, 96)}  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
+             40: (64, 96),  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
+             # 64-77: the same LDS image read as mfma_f32_32x32x16_bf16 operands (csrc/gemm.hip M32)
+             64: (128, 128), 65: (128, 128), 66: (128, 128), 67: (256, 128), 68: (128, 256), 69: (64, 64),
+             70: (64, 64), 71: (128, 64), 72: (64, 128), 73: (64, 128), 74: (128, 192), 75: (64, 192),
+             76: (128, 64), 77: (256, 256)}
+M32_CFGS = tuple(range(64, 78))
 # LDS tiles that also run as an implicit-GEMM conv on channel-blocked activations (csrc/gemm.hip CV
 # mode; ResNet at batch >= 4): C % 64 == 0, Cout % BN == 0
-LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33)
+LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 64, 65, 66, 67, 69, 71, 72, 76)
 LDS_CONV_MIN_M = 4096  # heuristic: below this the register-ring conv kernel (bs=1 shapes) stays
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256

@@ -119,7 +119,8 @@ def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
 def candidates_fp8(M: int, pw: PackedFp8, mx_io: bool = False) -> list:
     from .conv import candidates
     out = [(cfg, 1) for cfg in MX_TILES if mx_fits(cfg, pw.cout)] if mx_ok(M, pw) else []
-    return out if mx_io else out + candidates(M, pw.cout, pw.K)
+    # the fp8 launcher reads cfg >= 16 as an MX tile: the bf16-only 32x32 LDS tiles do not exist there
+    return out if mx_io else out + [c for c in candidates(M, pw.cout, pw.K) if c[0] < 64]
 
 
 def choose_config_fp8(M: int, pw: PackedFp8, tuned: dict | None = None, key: str | None = None, mx_io=False):

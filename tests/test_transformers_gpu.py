@@ -77,6 +77,21 @@ def test_lds_gemm(cfg, M, N, K, act, res):
     assert _rel(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("m32,base", [(64, 20), (65, 16), (66, 29), (67, 30), (69, 23), (71, 31), (72, 21), (77, 16)])
+def test_lds_gemm_m32_matches_16x16(m32, base):
+    """The 32x32x16-MFMA tiles (csrc/gemm.hip M32) read the same LDS image through a different
+    lane map: against the 16x16x32 kernel in fp32 output they agree to summation-order rounding,
+    so a wrong operand or accumulator map (even one that permutes a few k) cannot hide."""
+    M, N, K = 520, 768, 1024
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(N, K, generator=g) * 0.03
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    pc = C.pack_linear(w, torch.randn(N, generator=g)).to(DEV)
+    ya = C.linear(x, pc, act="gelu", cfg=m32, kw=1, out_f32=True)
+    yb = C.linear(x, pc, act="gelu", cfg=base, kw=1, out_f32=True)
+    assert _rel(ya, yb) < 1e-5
+
+
 @pytest.mark.parametrize("ln_fold", ["1", "0"])
 def test_bert_engine_matches_hf(ln_fold, monkeypatch):
     """ln_fold=1: LayerNorms folded into the LDS GEMM epilogues (HzLnFold); LayerNorm affine
