@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <utility>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -588,6 +590,160 @@ __global__ __launch_bounds__(512) void gemm_mxq_kernel(const HzGemmFp8Params p, 
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
+template <class F, int... Ks>
+__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Ks...>) {
+  (f(std::integral_constant<int, Ks>{}), ...);
+}
+
+// ---- ring-pipelined 256-row MX GEMM, K fixed at compile time (cfg 46-48) ----
+// r3 (profiles/r3_mxs): the 2-stage loops above wait for the whole next stage at every k-step,
+// and a loop with data-dependent staging / read conditions let hipcc sink every MFMA below the
+// branches and insert vmcnt(0) between them. Here the K loop is fully unrolled (KB K-tiles of
+// 128, a template parameter: the LayerNorm-fed projections of BERT/ViT-base have K = 768), so
+// every buffer index, parity and wait count is static and the body is branch-free. Tile 256
+// tokens x BN features, 8 waves (wave (wm, wn): tokens wm*128.., features wn*BN/4..); a ring of
+// NB K-tile buffers; per K-tile 4 phases over the wave's quadrants (token half r, feature half c):
+//   phase 0: read W(cB) of k                 | MFMAs (r0, cA)
+//   phase 1: read X(r1) of k                 | MFMAs (r0, cB)
+//   phase 2: barrier [all W reads of k retired: consumed by phase-1 MFMAs]
+//            stage W of k+NB into k's buffer  | MFMAs (r1, cB)
+//   phase 3: vmcnt [own glds of k+1 landed; k+2.. may fly] + barrier [RAW for k+1, WAR for X
+//            of k's buffer], stage X of k+NB, read X(r0), W(cB) of k+1 | MFMAs (r1, cA)
+// cA alternates with k so phase 3 refills exactly the registers phases 0-2 are done with. Same
+// LDS images, swizzle, hardware K order, MFMA and epilogue as gemm_mx_kernel (bitwise equal to
+// cfg 24). Per-row activation scales only (XS = false).
+template <int BN, int NB, int KB>
+__global__ __launch_bounds__(512) void gemm_mxk_kernel(const HzGemmFp8Params p, int group_m) {
+  constexpr int BM = 256, WN = 4;
+  constexpr int FCW = BN / WN / 16, FPW = 8, FH = FCW / 2;
+  constexpr int XBYTES = BM * 128, WBYTES = (BN / 16) * 2048, TBYTES = XBYTES + WBYTES;
+  constexpr int GX = 4, GW = BN / 64;
+  static_assert(FH >= 1 && NB >= 2 && KB >= NB && NB * TBYTES <= 160 * 1024, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[NB * TBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int tiles_n = p.N / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
+  const int n0 = tile_n * BN, m0 = tile_m * BM;
+
+  // X piece q = wave + 8i: tile rows 8q..8q+7 (rows >= M clamped, never stored); W piece
+  // pc = wave + 8i: fragment pc >> 1 (+4 i), k half pc & 1
+  const unsigned char* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = min(m0 + 64 * i + wave * 8 + (lane >> 3), p.M - 1);
+    xsrc[i] = p.x + (long)row * p.ldx + ((lane & 7) ^ mx_swz(((wave & 1) << 2) + (lane >> 4))) * 16;
+  }
+  const unsigned char* wsrc = p.wmx + ((long)((n0 >> 4) + (wave >> 1)) * KB) * 2048 + (wave & 1) * 1024 + lane * 16;
+  auto stage_x = [&](int k, int buf) {
+    char* base = smem + buf * TBYTES + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16_8(xsrc[i] + k * 128, base + i * 8192);
+  };
+  auto stage_w = [&](int k, int buf) {
+    char* base = smem + buf * TBYTES + XBYTES + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < GW; ++i) glds16_8(wsrc + (long)(4 * i * KB + k) * 2048, base + i * 8192);
+  };
+
+  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
+  const int brow = (wm * 128 + lr) * 128;
+  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
+  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
+  auto rd = [](const char* b0, const char* b1) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(b0);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(b1);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+
+  f32x4 acc[FCW][FPW];
+#pragma unroll
+  for (int i = 0; i < FCW; ++i)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 x[2][4], w[2][FH];
+  auto rdx = [&](int buf, int r) {
+    const char* base = smem + buf * TBYTES;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) x[r][f] = rd(base + boff0 + (4 * r + f) * 2048, base + boff1 + (4 * r + f) * 2048);
+  };
+  auto rdw = [&](int buf, int c) {
+    const char* base = smem + buf * TBYTES;
+#pragma unroll
+    for (int f = 0; f < FH; ++f) {
+      const int o = aoff + (c * FH + f) * 2048;
+      w[c][f] = rd(base + o, base + o + 1024);
+    }
+  };
+  auto mma = [&](int r, int c) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int h = 0; h < FH; ++h)
+        acc[c * FH + h][4 * r + f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            w[c][h], x[r][f], acc[c * FH + h][4 * r + f], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    stage_w(k, k);
+    stage_x(k, k);
+  }
+  wait_vm8<(NB - 1) * (GW + GX)>();
+  __builtin_amdgcn_s_barrier();
+  rdx(0, 0);
+  rdw(0, 0);
+  auto kstep = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int cA = k & 1, cB = 1 - cA, buf = k % NB;
+    __builtin_amdgcn_sched_barrier(0);
+    rdw(buf, cB);  // phase 0
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, cA);
+    __builtin_amdgcn_sched_barrier(0);
+    rdx(buf, 1);  // phase 1
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, cB);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // phase 2
+    if (k + NB < KB) stage_w(k + NB, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, cB);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 3: in flight after k+1's glds: W + X of k+2 .. k+NB-1, and W of k+NB
+    if (k + NB < KB) wait_vm8<(NB - 2) * (GW + GX) + GW>();
+    else if (k + 2 < KB) wait_vm8<(KB - k - 2) * (GW + GX)>();
+    else wait_vm8<0>();
+    __builtin_amdgcn_s_barrier();
+    if (k + NB < KB) stage_x(k + NB, buf);
+    if (k + 1 < KB) {
+      rdx((k + 1) % NB, 0);
+      rdw((k + 1) % NB, cB);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, cA);
+  };
+  static_for(kstep, std::make_integer_sequence<int, KB>{});
+  __builtin_amdgcn_sched_barrier(0);
+  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * 128, n0 + wn * (BN / WN), lane);
+}
+
+template <int BN, int NB>
+int launch_mxk(const HzGemmFp8Params& p, hipStream_t st) {
+  if (p.N % BN || p.xs || p.K != 768) return -4;  // per-row activation scales, K = 768 (KB = 6)
+  const int tiles = (p.N / BN) * ((p.M + 255) / 256);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  hipLaunchKernelGGL((gemm_mxk_kernel<BN, NB, 6>), dim3(tiles), dim3(512), 0, st, p, group_m);
+  return (int)hipGetLastError();
+}
+
 template <int BN, int NS>
 int launch_mxq(const HzGemmFp8Params& p, hipStream_t st) {
   if (p.N % BN) return -4;
@@ -647,6 +803,10 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 43: return launch_mxq<256, 2>(p, st);
       case 44: return launch_mxq<128, 2>(p, st);
       case 45: return launch_mxq<128, 3>(p, st);
+      // ring-pipelined 256-row kernel, K = 768 unrolled: 256x128 with a 3- / 2-buffer ring (a
+      // 256x256 tile needs 128 accumulators + 96 operand registers per lane: it spills)
+      case 46: return launch_mxk<128, 3>(p, st);
+      case 47: return launch_mxk<128, 2>(p, st);
       default: return -2;
     }
   }

@@ -104,8 +104,11 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             30: (128, 128), 31: (64, 128), 32: (128, 64),
             # 33: 8-wave 256x256 (plain); 43-45: the 256-row kernel (256x256 2 stages, 256x128 2 / 3):
             # measured slower than 24 at one workgroup per CU, kept as tuner candidates (profiles/r3_mx256)
-            33: (256, 256), 43: (256, 256), 44: (256, 128), 45: (256, 128)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 43, 44, 45)
+            33: (256, 256), 43: (256, 256), 44: (256, 128), 45: (256, 128),
+            # 46 / 47: the ring-pipelined 256-row kernel, K = 768 unrolled (3- / 2-buffer ring; per-row
+            # activation scales only -- an MX8-input or other-K launch is refused)
+            46: (256, 128), 47: (256, 128)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 43, 44, 45, 46, 47)
 
 
 def mx_fits(cfg: int, n: int) -> bool:
