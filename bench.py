@@ -297,7 +297,7 @@ def http_figure(args, world: int, rank: int):
             from hipzap.serve.loadtest import run_load
             _, plan = prepare_artifacts(args.model, args.ckpt_dir)
             res = run_load(plan, gpus=world, clients=args.http_clients * world, requests=args.http_requests,
-                           contexts=8, fmt="npy", ready_timeout=300.0)
+                           contexts=8, fmt="npy", ready_timeout=150.0)
             if not res.get("errors"):
                 res.pop("server_log_tail", None)
         except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
