@@ -56,9 +56,23 @@ def _bf16_array_cls():
 
 
 class _StorageType:
+    """A storage dtype marker (``torch.FloatStorage`` ...). Immutable: a pickle BUILD opcode on it
+    cannot rewrite its dtype or item size (they are looked up from the name, which is fixed)."""
+    __slots__ = ("name",)
+
     def __init__(self, name: str):
-        self.name = name
-        self.dtype, self.itemsize = _STORAGE_DTYPES[name]
+        object.__setattr__(self, "name", name)
+
+    def __setattr__(self, k, v):
+        raise pickle.UnpicklingError("storage dtype markers are immutable")
+
+    @property
+    def dtype(self) -> str:
+        return _STORAGE_DTYPES[self.name][0]
+
+    @property
+    def itemsize(self) -> int:
+        return _STORAGE_DTYPES[self.name][1]
 
 
 class StorageRef:
@@ -104,9 +118,16 @@ class TensorRef:
 
 def _rebuild_tensor_v2(storage, storage_offset, size, stride, requires_grad=False, backward_hooks=None,
                        metadata=None):
+    if not isinstance(storage, StorageRef):
+        raise pickle.UnpicklingError("tensor rebuild without a storage record")
     size, stride = tuple(int(s) for s in size), tuple(int(s) for s in stride)
-    if storage.array is None:  # scan: geometry only
-        if size and min(size) > 0:
+    storage_offset = int(storage_offset)
+    # a view must stay inside its record: no negative offsets, sizes or strides (a negative one would
+    # address bytes before the record -- on the host through numpy, on the device through the packer)
+    if storage_offset < 0 or len(size) != len(stride) or any(n < 0 for n in size) or any(t < 0 for t in stride):
+        raise pickle.UnpicklingError("tensor view with a negative offset, size or stride")
+    if storage.array is None:  # scan: geometry only (a scalar spans one element)
+        if not size or min(size) > 0:
             span = 1 + sum((n - 1) * s for n, s in zip(size, stride))
             if storage_offset + span > storage.numel:
                 raise pickle.UnpicklingError("tensor view runs past its storage")
@@ -115,6 +136,8 @@ def _rebuild_tensor_v2(storage, storage_offset, size, stride, requires_grad=Fals
     base = storage.array
     item = base.itemsize
     if len(size) == 0:
+        if storage_offset >= base.size:
+            raise pickle.UnpicklingError("tensor view runs past its storage")
         t = base[storage_offset: storage_offset + 1].reshape(())
     else:
         span = 1 + sum((n - 1) * s for n, s in zip(size, stride) if n > 0)
@@ -158,6 +181,8 @@ class _RestrictedUnpickler(pickle.Unpickler):
         if not (isinstance(pid, tuple) and len(pid) == 5 and pid[0] == "storage" and isinstance(pid[1], _StorageType)):
             raise pickle.UnpicklingError(f"unsupported persistent id {pid!r}")
         _, st, key, _location, numel = pid
+        if int(numel) < 0:
+            raise pickle.UnpicklingError("negative storage size")
         return self._load_storage(str(key), st, int(numel))
 
 
@@ -199,7 +224,10 @@ def _read(path: str, with_arrays: bool):
                 raise pickle.UnpicklingError(f"storage {key}: missing or compressed record")
             if numel * st.itemsize > info.file_size:
                 raise pickle.UnpicklingError(f"storage {key}: record shorter than {numel} elements")
-            s = cache[key] = StorageRef(key, st, numel, _member_data_offset(mm, info))
+            s = StorageRef(key, st, numel, _member_data_offset(mm, info))
+            if s.file_off + s.nbytes > len(mm):
+                raise pickle.UnpicklingError(f"storage {key}: record runs past the end of the file")
+            cache[key] = s
             if with_arrays:
                 import numpy as np
                 s.array = np.frombuffer(mm, dtype=np.dtype(st.dtype), count=numel, offset=s.file_off)

@@ -116,3 +116,61 @@ def test_template_places_every_parameter_like_the_plan_image(tmp_path):
     assert bytes(mine) == blob
     # the recipe covers every packed parameter with its checkpoint sources
     assert set(tm["pack"]) == set(Q) and tm["pack"]["fc"]["kind"] == "linear" and tm["pack"]["conv1"]["cin_p"] == 8
+
+
+def _forged(tmp_path, off, size, stride, numel=16, name="forged.pth"):
+    """A torch.save-shaped archive whose one tensor view has the given geometry (written with the
+    real torch._utils rebuild global and storage marker, so only the geometry is hostile)."""
+    from collections import OrderedDict
+
+    class _S:
+        pass
+
+    class _T:
+        def __reduce__(self):
+            return torch._utils._rebuild_tensor_v2, (_S(), off, size, stride, False, OrderedDict())
+
+    class _P(pickle.Pickler):
+        def persistent_id(self, obj):
+            return ("storage", torch.FloatStorage, "0", "cpu", numel) if isinstance(obj, _S) else None
+
+    buf = io.BytesIO()
+    _P(buf, protocol=2).dump({"w": _T()})
+    p = tmp_path / name
+    with zipfile.ZipFile(p, "w", zipfile.ZIP_STORED) as z:
+        z.writestr("f/data.pkl", buf.getvalue())
+        z.writestr("f/byteorder", "little")
+        z.writestr("f/data/0", np.arange(16, dtype=np.float32).tobytes())
+    return str(p)
+
+
+@pytest.mark.parametrize("off,size,stride", [(-4, (4,), (1,)), (0, (4,), (-1,)), (8, (2, 2), (-4, 1)), (0, (-1,), (1,)),
+                                             (12, (8,), (1,)), (16, (), ())])
+def test_reader_refuses_views_outside_their_record(tmp_path, off, size, stride):
+    """Negative offsets / strides / sizes and views past the record would address bytes outside
+    the storage (numpy as_strided on the host, the device packer's staging pointer on the GPU):
+    refused in both modes, before any array or pointer is formed."""
+    p = _forged(tmp_path, off, size, stride)
+    with pytest.raises(pickle.UnpicklingError):
+        pthreader.load_state_dict(p)
+    with pytest.raises(pickle.UnpicklingError):
+        pthreader.scan(p)
+
+
+def test_reader_accepts_forged_but_valid_view(tmp_path):
+    p = _forged(tmp_path, 4, (2, 3), (3, 1))
+    assert np.array_equal(pthreader.load_state_dict(p)["w"], np.arange(4, 10, dtype=np.float32).reshape(2, 3))
+    r = pthreader.scan(p)["w"]
+    assert r.offset == 4 and r.shape == (2, 3) and r.is_contiguous()
+
+
+def test_reader_storage_marker_is_immutable(tmp_path):
+    """A BUILD opcode on a storage dtype marker (to rewrite its item size / dtype before a
+    persistent id uses it) fails instead of changing what the record is read as."""
+    for state in (b"}X\x05\x00\x00\x00dtypeX\x07\x00\x00\x00float64sb.",
+                  b"N}X\x04\x00\x00\x00nameX\r\x00\x00\x00DoubleStorages\x86b."):
+        p = tmp_path / "m.pth"
+        with zipfile.ZipFile(p, "w", zipfile.ZIP_STORED) as z:
+            z.writestr("m/data.pkl", b"\x80\x02ctorch\nFloatStorage\n" + state)
+        with pytest.raises((pickle.UnpicklingError, AttributeError)):
+            pthreader.load_state_dict(str(p))
