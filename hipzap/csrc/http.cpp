@@ -165,11 +165,18 @@ bool json_int_array(const char*& p, const char* e, std::vector<long>& v) {
       ++p;
       return true;
     }
-    char* q;
-    const long x = strtol(p, &q, 10);
-    if (q == p || q > e) return false;
-    v.push_back(x);
-    p = q;
+    // bounded decimal parse: never reads past e (strtol would run on into whatever follows the
+    // body in the connection buffer)
+    bool neg = false;
+    if (p < e && (*p == '-' || *p == '+')) neg = *p++ == '-';
+    const char* d0 = p;
+    long x = 0;
+    while (p < e && *p >= '0' && *p <= '9') {
+      if (x > 100000000L) return false;  // shapes are small; refuse instead of overflowing
+      x = x * 10 + (*p++ - '0');
+    }
+    if (p == d0) return false;
+    v.push_back(neg ? -x : x);
     skip_ws(p, e);
     if (p < e && *p == ',') {
       ++p;

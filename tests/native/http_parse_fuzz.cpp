@@ -1,0 +1,114 @@
+// Host ASan/UBSan fuzz of the native HTTP front end's parsers and request framing
+// (hipzap/csrc/http.cpp, tests/test_native_asan_cpu.py). The translation unit is included so the
+// anonymous-namespace parsers are reachable; every input lives in an exact-size heap buffer, so
+// any read past the body is an ASan heap-buffer-overflow. serve_conn() is driven over a
+// socketpair with random and mutated requests (no fast route, no Python handler: 404/400/413/411
+// answers), including pipelined requests and truncated bodies.
+#include "../../hipzap/csrc/http.cpp"
+
+#include <sys/socket.h>
+
+#include <cstdlib>
+#include <random>
+
+extern "C" int hz_exec_submit(void*, const void* const*, void*, double*) { return 1; }
+
+namespace {
+
+std::mt19937_64 rng(12345);
+
+std::string rnd_bytes(size_t n, const char* alphabet = nullptr) {
+  std::string s(n, '\0');
+  const size_t an = alphabet ? strlen(alphabet) : 0;
+  for (auto& c : s) c = alphabet ? alphabet[rng() % an] : (char)(rng() & 0xff);
+  return s;
+}
+
+std::string mutate(std::string s) {
+  const int k = 1 + (int)(rng() % 4);
+  for (int i = 0; i < k && !s.empty(); ++i) {
+    const size_t at = rng() % s.size();
+    switch (rng() % 4) {
+      case 0: s[at] = (char)(rng() & 0xff); break;
+      case 1: s.erase(at, 1 + rng() % 8); break;
+      case 2: s.insert(at, rnd_bytes(1 + rng() % 8, "0123456789[]{},:\"' -+")); break;
+      default: s.resize(at); break;
+    }
+  }
+  return s;
+}
+
+template <class F>
+void on_exact(const std::string& s, F f) {  // the input in a heap block of exactly its size
+  char* b = static_cast<char*>(malloc(s.size() ? s.size() : 1));
+  memcpy(b, s.data(), s.size());
+  f(b, s.size());
+  free(b);
+}
+
+void fuzz_parsers() {
+  const std::string seeds[] = {
+      "{\"image_b64\": \"AAECAwQF\", \"shape\": [1, 2, 3], \"model\": \"resnet50\"}",
+      "{\"shape\": [224, 224, 3], \"image_b64\": \"////\"}",
+      std::string("\x93NUMPY\x01\x00\x46\x00{'descr': '|u1', 'fortran_order': False, 'shape': (2, 3, 1), }      \n",
+                  80) + "abcdef",
+      std::string("\x93NUMPY\x02\x00\x10\x00\x00\x00{'shape': (5,", 26),
+  };
+  for (int it = 0; it < 200000; ++it) {
+    std::string in = it % 5 == 4 ? rnd_bytes(rng() % 96, nullptr) : mutate(seeds[rng() % 4]);
+    on_exact(in, [](const char* b, size_t n) {
+      const char* img;
+      size_t img_n;
+      std::vector<long> shape;
+      std::string model;
+      if (parse_json_image(b, n, &img, &img_n, shape, model)) {
+        if (img < b || img + img_n > b + n) abort();
+        std::vector<uint8_t> out(img_n);
+        b64decode(img, img_n, out.data(), (img_n * 3) / 4);
+      }
+      std::vector<long> s2;
+      const uint8_t* d;
+      size_t dn;
+      if (parse_npy_u8(b, n, s2, &d, &dn) && (reinterpret_cast<const char*>(d) < b || reinterpret_cast<const char*>(d) + dn != b + n))
+        abort();
+      const char* p = b;
+      std::vector<long> v;
+      json_int_array(p, b + n, v);
+      if (p < b || p > b + n) abort();
+    });
+  }
+}
+
+void fuzz_framing() {
+  Server S;  // no fast route, no Python handler
+  const std::string seeds[] = {
+      "GET /health HTTP/1.1\r\nHost: x\r\n\r\n",
+      "POST /predict HTTP/1.1\r\nContent-Type: application/json\r\nContent-Length: 13\r\n\r\n{\"a\": [1, 2]}",
+      "POST /p HTTP/1.1\r\nContent-Length: 4\r\nConnection: keep-alive\r\n\r\nabcdGET / HTTP/1.1\r\n\r\n",
+      "POST / HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n0\r\n\r\n",
+      "POST / HTTP/1.0\r\nContent-Length: -7\r\n\r\n",
+  };
+  for (int it = 0; it < 4000; ++it) {
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv)) abort();
+    std::string req = it % 7 == 6 ? rnd_bytes(rng() % 300, nullptr) : mutate(seeds[rng() % 5]);
+    if (rng() % 3 == 0) req += seeds[rng() % 5];
+    std::thread t(serve_conn, &S, sv[1]);  // closes sv[1] when it returns
+    send_all(sv[0], req.data(), req.size());
+    shutdown(sv[0], SHUT_WR);  // EOF: a truncated body ends the connection
+    char sink[4096];
+    while (recv(sv[0], sink, sizeof(sink), 0) > 0) {
+    }
+    t.join();
+    close(sv[0]);
+  }
+}
+
+}  // namespace
+
+int main() {
+  fuzz_parsers();
+  fuzz_framing();
+  printf("http parse fuzz: ok\n");
+  return 0;
+}

@@ -27,3 +27,22 @@ def test_runtime_host_asan_ubsan(tmp_path):
     run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert run.returncode == 0 and "runtime host asan: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
     assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_http_parsers_fuzz_asan_ubsan(tmp_path):
+    """The native HTTP front end's body parsers (JSON image, .npy, base64, int arrays) on 200k
+    mutated / random inputs held in exact-size heap blocks, and its request framing (serve_conn
+    over a socketpair: pipelined, truncated, chunked, negative lengths) under host ASan + UBSan."""
+    exe = tmp_path / "http_fuzz"
+    san = []
+    for f in ("-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
+        san += ["-Xarch_host", f]
+    cmd = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", os.path.join(ROOT, "hipzap", "csrc"),
+           os.path.join(ROOT, "tests", "native", "http_parse_fuzz.cpp"), "-lpthread", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert run.returncode == 0 and "http parse fuzz: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
