@@ -132,7 +132,9 @@ struct Plan {
     if (h.abi != hz_abi_version())
       return fail("plan: written for a different native ABI (" + std::to_string(h.abi) + " != " +
                   std::to_string(hz_abi_version()) + "); re-export it");
-    if (h.ops_off + h.ops_len > map_len || (!(h.flags & kFlagWeightless) && h.blob_off + h.blob_len > map_len))
+    // (subtractive bounds: a forged offset + length must not wrap around)
+    if (h.ops_off > map_len || h.ops_len > map_len - h.ops_off ||
+        (!(h.flags & kFlagWeightless) && (h.blob_off > map_len || h.blob_len > map_len - h.blob_off)))
       return fail("plan: truncated file");
     const uint8_t* p = map + h.ops_off;
     const uint8_t* end = p + h.ops_len;
@@ -142,15 +144,31 @@ struct Plan {
       PlanOp op;
       std::memcpy(&op.h, p, sizeof(OpHeader));
       p += sizeof(OpHeader);
+      const uint64_t rec = (((uint64_t)op.h.plen + 7u) & ~uint64_t(7)) + sizeof(Reloc) * (uint64_t)op.h.nrel;
+      if (rec > (uint64_t)(end - p)) return fail("plan: truncated op record");
       op.prm = p;
-      p += (op.h.plen + 7u) & ~7u;
-      op.rel = reinterpret_cast<const Reloc*>(p);
-      p += sizeof(Reloc) * op.h.nrel;
-      if (p > end) return fail("plan: truncated op record");
+      op.rel = reinterpret_cast<const Reloc*>(p + (((uint64_t)op.h.plen + 7u) & ~uint64_t(7)));
+      p += rec;
+      // every op reads a whole parameter struct from its record
+      size_t need = 0;
+      switch (op.h.type) {
+        case HZ_PLAN_OP_CONV: need = sizeof(HzConvParams); break;
+        case HZ_PLAN_OP_CONV2: need = 2 * sizeof(HzConvParams); break;
+        case HZ_PLAN_OP_MAXPOOL: need = sizeof(HzPoolParams); break;
+        case HZ_PLAN_OP_AVGPOOL: need = sizeof(HzAvgpoolArgs); break;
+        case HZ_PLAN_OP_PREPROCESS: need = sizeof(HzPreprocessArgs); break;
+        case HZ_PLAN_OP_MEMCPY: need = sizeof(HzMemcpyArgs); break;
+        case HZ_PLAN_OP_KERNEL: need = hz_kernel_param_size(op.h.arg); break;
+        case HZ_PLAN_OP_FORK:
+        case HZ_PLAN_OP_JOIN: need = 0; break;
+        default: return fail("plan: unknown op type " + std::to_string(op.h.type));
+      }
+      if ((op.h.type == HZ_PLAN_OP_KERNEL && !need) || op.h.plen < need)
+        return fail("plan: op " + std::to_string(i) + " record shorter than its parameters");
       for (uint32_t r = 0; r < op.h.nrel; ++r) {
         const Reloc& rl = op.rel[r];
         const uint64_t lim = rl.region == 0 ? h.blob_len : rl.region == 1 ? h.ctx_dev_bytes : h.ctx_host_bytes;
-        if (rl.region > 2 || rl.off + 8 > op.h.plen || rl.roff > lim)
+        if (rl.region > 2 || (uint64_t)rl.off + 8 > op.h.plen || rl.roff > lim)
           return fail("plan: relocation out of range in op " + std::to_string(i));
       }
       ops.push_back(op);

@@ -297,7 +297,34 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
   }
 }
 
+// bytes of the parameter struct hz_launch_kernel reads for `kind` (0: unknown kind)
+extern "C" size_t hz_kernel_param_size(int kind) {
+  switch (kind) {
+    case HZ_K_LAYERNORM: return sizeof(HzLayerNormParams);
+    case HZ_K_EMBED: return sizeof(HzEmbedParams);
+    case HZ_K_ATTENTION: return sizeof(HzAttentionParams);
+    case HZ_K_VIT_TOKENS: return sizeof(HzVitTokensParams);
+    case HZ_K_LSTM: return sizeof(HzLstmParams);
+    case HZ_K_DECODER: return sizeof(HzDecoderParams);
+    case HZ_K_SAMPLER: return sizeof(HzSamplerParams);
+    case HZ_K_MAXPOOL: return sizeof(HzPoolParams);
+    case HZ_K_QUANT: return sizeof(HzQuantParams);
+    case HZ_K_GEMM_FP8: return sizeof(HzGemmFp8Params);
+    case HZ_K_SOFTMAX: return sizeof(HzSoftmaxParams);
+    case HZ_K_POOL_FC: return sizeof(HzPoolFcParams);
+    case HZ_K_LMB_LAYER: return sizeof(HzLmbLayerParams);
+    case HZ_K_LMB_DEC: return sizeof(HzLmbDecParams);
+    case HZ_K_LMB_ADMIT: return sizeof(HzLmbAdmitParams);
+    case HZ_K_CONV_CHAIN: return sizeof(HzConvChainParams);
+    default: return 0;
+  }
+}
+
 extern "C" int hz_prog_add_kernel(HzProgram h, int kind, const void* params, size_t size, int slot) {
+  // the launcher reads a whole parameter struct: refuse unknown kinds and short records (a plan
+  // image's op record, for instance) instead of reading past them when the op is replayed
+  const size_t need = hz_kernel_param_size(kind);
+  if (!need || size < need) return -101;
   auto buf = std::make_shared<std::vector<char>>(static_cast<const char*>(params), static_cast<const char*>(params) + size);
   return add_op(static_cast<Program*>(h), slot, Op::LAUNCH,
                 [buf, kind](hipStream_t s) { return hz_launch_kernel(kind, buf->data(), s); });

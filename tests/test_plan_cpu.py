@@ -170,3 +170,54 @@ def test_bert_text_plan_meta(tmp_path):
     assert all(i["region"] == 2 for i in ins)
     assert all(ins[k]["off"] + ins[k]["bytes"] == ins[k + 1]["off"] for k in range(2)), ins
     assert meta["output"]["num_labels"] == 2
+
+
+def _plan_open_error(path) -> str:
+    """hz_plan_open on the CPU: parsing happens before the first HIP call, so a forged file is
+    refused with a parse error; a well-formed one gets as far as device initialisation."""
+    lib = N.lib()
+    lib.hz_plan_open.restype = C.c_void_p
+    lib.hz_plan_last_error.restype = C.c_char_p
+    h = lib.hz_plan_open(str(path).encode(), 0, 1, None)
+    if h:
+        lib.hz_plan_close(C.c_void_p(h))
+        return ""
+    return lib.hz_plan_last_error().decode()
+
+
+def test_plan_loader_refuses_forged_records(tmp_path, r18):
+    import struct
+    a, params, kw = r18
+    path = tmp_path / "r18.hzplan"
+    P.export_plan("resnet18", params, kw, str(path))
+    raw = bytes(path.read_bytes())
+    f = struct.unpack("<8s15Q", raw[:128])
+    ops_off, ops_len = f[6], f[7]
+    assert "truncated" not in _plan_open_error(path) and "shorter" not in _plan_open_error(path)
+
+    def forged(name, data):
+        p = tmp_path / name
+        p.write_bytes(bytes(data))
+        return _plan_open_error(p)
+
+    # the first op's parameter record claims 8 bytes (its struct is far larger)
+    b = bytearray(raw)
+    typ, arg, slot, plen, nrel, pad = struct.unpack("<IiiIII", b[ops_off: ops_off + 24])
+    b[ops_off + 12: ops_off + 16] = struct.pack("<I", 8)
+    b[ops_off + 16: ops_off + 20] = struct.pack("<I", 0)
+    assert "shorter than its parameters" in forged("short.hzplan", b) or "op record" in forged("short.hzplan", b)
+    # a relocation offset that would wrap a 32-bit bound check
+    b = bytearray(raw)
+    if nrel:
+        r0 = ops_off + 24 + ((plen + 7) & ~7)
+        b[r0: r0 + 4] = struct.pack("<I", 0xFFFFFFFC)
+        assert "relocation out of range" in forged("reloc.hzplan", b)
+    # an ops table whose offset + length wraps around 2^64
+    b = bytearray(raw)
+    b[8 + 8 * 5: 8 + 8 * 6] = struct.pack("<Q", 2 ** 64 - 64)  # ops_off
+    b[8 + 8 * 6: 8 + 8 * 7] = struct.pack("<Q", 128)           # ops_len
+    assert "truncated file" in forged("wrap.hzplan", b)
+    # an op whose record length runs past the table
+    b = bytearray(raw)
+    b[ops_off + 16: ops_off + 20] = struct.pack("<I", 0x7FFFFFFF)  # nrel
+    assert "truncated op record" in forged("nrel.hzplan", b)
