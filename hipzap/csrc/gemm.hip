@@ -419,15 +419,24 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
   static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
   const int group_m = group_env < 1 ? 1 : group_env;
   if (!p.x_rowmajor) {  // implicit-GEMM conv (CV): every feature tile lies inside Cout (rows padded to 64)
-    if (!CVOK || p.out_rowmajor || p.lnf || p.C % 64 || p.Cout % BN || p.Cout % 32 || p.K != p.R * p.S * p.C ||
-        (long)p.N * p.C * p.H * p.W * 2 >= (1L << 31))
+    // (instantiated only for the CV-capable tiles: every kernel variant is code the serving
+    // process loads at its first launch, i.e. part of the cold start)
+    if constexpr (CVOK) {
+      if (p.out_rowmajor || p.lnf || p.C % 64 || p.Cout % BN || p.Cout % 32 || p.K != p.R * p.S * p.C ||
+          (long)p.N * p.C * p.H * p.W * 2 >= (1L << 31))
+        return -1;
+      hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, true, M32>), dim3(tiles), block, 0, st, p, group_m);
+      return (int)hipGetLastError();
+    } else {
       return -1;
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, true, M32>), dim3(tiles), block, 0, st, p, group_m);
-    return (int)hipGetLastError();
+    }
   }
   if (p.lnf) {  // the folded-LayerNorm statistics slabs assume 2 feature halves per tile
-    if (WN != 2 || M32) return -3;
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
+    if constexpr (WN != 2 || M32) {
+      return -3;
+    } else {
+      hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
+    }
   } else {
     hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, false, M32>), dim3(tiles), block, 0, st, p, group_m);
   }
