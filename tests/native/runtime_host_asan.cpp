@@ -29,7 +29,11 @@ STUB(hz_layernorm_launch, HzLayerNormParams, 9, rows)
 STUB(hz_embed_ln_launch, HzEmbedParams, 10, L)
 STUB(hz_attention_launch, HzAttentionParams, 11, L)
 STUB(hz_vit_tokens_launch, HzVitTokensParams, 12, B)
-STUB(hz_softmax_launch, HzSoftmaxParams, 13, rows)
+extern "C" int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t) {
+  g_calls.push_back(13);
+  g_vals.push_back(p->rows);
+  return p->rows < 0 ? 7 : 0;  // a negative row count: a failing launch
+}
 STUB(hz_lmb_layer_launch, HzLmbLayerParams, 14, H)
 STUB(hz_lmb_dec_launch, HzLmbDecParams, 15, V)
 STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
@@ -97,16 +101,35 @@ int main() {
     CHECK(hz_prog_add_kernel(p, HZ_K_LAYERNORM, &ln, sizeof(ln), 0) == 0);
     ln.rows = -5;  // generic kernels also copy their parameter block
     std::vector<char> big(4096, 0);  // a parameter block larger than any struct
-    CHECK(hz_prog_add_kernel(p, 9999, big.data(), big.size(), 0) == 0);  // unknown kind: fails at run
+    CHECK(hz_prog_add_kernel(p, 9999, big.data(), big.size(), 0) == -101);  // unknown kind: refused at add
+    CHECK(hz_prog_add_kernel(p, HZ_K_LAYERNORM, &ln, sizeof(ln) - 8, 0) == -101);  // short record: refused
+    HzSoftmaxParams sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.rows = -7;
+    CHECK(hz_prog_add_kernel(p, HZ_K_SOFTMAX, big.data(), big.size(), 0) == 0);  // a longer record is fine
+    memcpy(big.data(), &sm, sizeof(sm));
+    CHECK(hz_prog_num_ops(p) == 5);
+    hz_prog_destroy(p);  // (discard: rebuild with the failing softmax as op 4)
+    p = hz_prog_create();
+    c.K = 576;
+    CHECK(hz_prog_add_conv(p, &c, 3, 0) == 0);
+    c.K = 1;
+    CHECK(hz_prog_add_conv2(p, &c, &d, 2, 0) == 0);
+    CHECK(hz_prog_add_lstm(p, &l, 0) == 0);
+    ln.rows = 2048;
+    CHECK(hz_prog_add_kernel(p, HZ_K_LAYERNORM, &ln, sizeof(ln), 0) == 0);
+    CHECK(hz_prog_add_kernel(p, HZ_K_SOFTMAX, big.data(), big.size(), 0) == 0);  // fails at run
     CHECK(hz_prog_add_avgpool(p, nullptr, nullptr, 7, 49, 2048, 1, 0) == 0);
     CHECK(hz_prog_add_conv(p, &c, 0, -1) == -4);  // slot out of range
     CHECK(hz_prog_add_conv(p, &c, 0, 9) == -4);
     CHECK(hz_prog_add_fork(p, 0) == -4);
     CHECK(hz_prog_num_ops(p) == 6);
     CHECK(hz_prog_is_captured(p) == 0);
-    const int rc = hz_prog_run(p, nullptr);  // op 4 (unknown kind) fails -> run stops there
-    CHECK(rc == -100);
-    CHECK(g_calls.size() == 4);
+    g_calls.clear();
+    g_vals.clear();
+    const int rc = hz_prog_run(p, nullptr);  // op 4 (the failing softmax) -> run stops there
+    CHECK(rc == 7);
+    CHECK(g_calls.size() == 5 && g_calls[4] == 13);
     CHECK(g_calls[0] == 1 && g_vals[0] == 576 * 100 + 3);
     CHECK(g_calls[1] == 14 && g_vals[1] == 1 + 64 + 2);
     CHECK(g_calls[2] == 4 && g_vals[2] == 1150);
