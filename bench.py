@@ -73,6 +73,8 @@ def parse():
                          "(0 disables)")
     ap.add_argument("--http-requests", type=int, default=800, help="requests per HTTP client process")
     ap.add_argument("--bert-cold", type=int, default=1, help="also report the BERT-base text-plan cold start")
+    ap.add_argument("--dp-figures", type=int, default=int(os.environ.get("HIPZAP_BENCH_DP", 1)),
+                    help="also measure BASELINE configs 3 / 5 (scatter-gather DP) in the same launch")
     ap.add_argument("--sustained-s", type=float, default=2.0,
                     help="secondary figure: served throughput over a self-timed window of at least this long")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
@@ -278,6 +280,71 @@ def dynamic_batching(args, eng, device, world):
            "latency_ms_p50": round(lat[len(lat) // 2], 4), "latency_ms_p99": round(lat[int(0.99 * (len(lat) - 1))], 4)}
     ex.close()
     del deng
+    return out
+
+
+def dp_figures(args, eng, device, world: int, rank: int, native_comm):
+    """Secondary figures: BASELINE configs 3 and 5 measured in the same N-rank launch. A global
+    batch is scattered from rank 0 over the N ranks (C2), every rank runs its captured shard
+    program, the logits are gathered back to rank 0 (C3); one step = scatter + forward + gather
+    (``parallel/dp.py`` DPExecutor), images/s over the whole job = global batch x K / the slowest
+    rank's wall. ResNet-50 at global batch 32 (uint8 images, the headline's broadcast weights)
+    and ViT-B/16 fp8 at global batch 64 (random-init weights packed on every rank from the same
+    seed). Collectives run on the native RCCL communicator when the headline uses it (bounded
+    waits: a stuck collective raises instead of hanging the launch), else torch.distributed.
+    Every rank builds first and all agree before the first collective; a failure skips the
+    figure (None), never the headline."""
+    from hipzap.engine.engine import Engine
+    from hipzap.models import registry
+    from hipzap.parallel.comm import is_dist, max_over_ranks
+    from hipzap.parallel.dp import DPExecutor
+    out = {}
+    for name, model, gb in (("resnet50_gb32", args.model, 32), ("vit_b16_fp8_gb64", "vit-b16-fp8", 64)):
+        ok, ex, xg = 1.0, None, None
+        try:
+            shard = gb // world
+            if shard * world != gb:
+                raise ValueError(f"global batch {gb} does not divide over {world} ranks")
+            if model == args.model:
+                params, arch_kw = eng.params, eng.arch_kw
+            else:
+                a = registry.get(model)
+                torch.manual_seed(0)
+                params, arch_kw = a.pack(a.make_model().eval().state_dict(), device)
+            seng = Engine(model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
+            cin, cout = seng.contexts[0].input, seng.contexts[0].output
+            ex = DPExecutor(lambda xs, e=seng: e.infer_device(xs), shard, tuple(cin.shape[1:]), tuple(cout.shape[1:]),
+                            device, in_dtype=cin.dtype, out_dtype=cout.dtype, comm=native_comm)
+            if rank == 0:
+                xg = (torch.randint(0, 256, (gb,) + tuple(cin.shape[1:]), dtype=torch.uint8, device=device)
+                      if cin.dtype == torch.uint8 else torch.randn((gb,) + tuple(cin.shape[1:]), device=device).to(cin.dtype))
+        except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
+            print(f"dp figure {name} skipped: {e!r}", file=sys.stderr)
+            ok = 0.0
+        if -max_over_ranks(-ok, device) < 1.0:
+            out[name] = None
+            continue
+        try:
+            for _ in range(max(1, args.warmup)):
+                ex.step(xg)
+            torch.cuda.synchronize(device)
+            if is_dist():
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ex.step(xg)
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            print(f"dp figure {name} failed: {e!r}", file=sys.stderr)
+            dt = float("inf")
+        dt = max_over_ranks(dt, device)
+        out[name] = None if dt == float("inf") else {
+            "img_s": round(gb * args.steps / dt, 2), "global_batch": gb, "per_rank_batch": gb // world,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "steps": args.steps, "model": model,
+            "comm": "native-rccl" if native_comm is not None else ("torch.distributed" if world > 1 else None),
+            "dtype": "fp8" if "fp8" in model else "bf16"}
+        del ex
     return out
 
 
@@ -591,6 +658,8 @@ def main():
     t_single = bench_contexts([single], [eng.streams[0]], 200)
     dyn = dynamic_batching(args, eng, device, world) if args.dyn_batch > 1 and args.batch == 1 else None
     http = http_figure(args, world, rank) if args.http_clients > 0 and args.batch == 1 else None
+    dpf = dp_figures(args, eng, device, world, rank, native_comm) \
+        if args.dp_figures and args.batch == 1 and args.model == "resnet50" else None
     torch_ref = None
     if args.compare_torch and rank == 0:
         try:
@@ -653,6 +722,8 @@ def main():
             res["served_sustained"] = sustained
         if http is not None:
             res["http_serving"] = http
+        if dpf is not None:  # BASELINE configs 3 and 5 (scatter / gather DP) in the same launch
+            res["dp_scatter"] = dpf
         if torch_ref is not None:
             res["torch_miopen_graph_inf_s_1gpu_1stream"] = round(torch_ref, 2)
         print(json.dumps(res), flush=True)
