@@ -123,6 +123,12 @@ class PackConvParams(C.Structure):  # csrc/pack.hip (torch-free checkpoint cold 
                 ("r", c_int), ("s", c_int), ("cin_p", c_int), ("rows", c_int), ("ksteps", c_int), ("pad_", c_int),
                 ("eps", c_double)]
 
+class FragPackParams(C.Structure):  # csrc/pack.hip hz_frag_pack_launch (batched AWD-LSTM packing)
+    _fields_ = [("a", c_void_p), ("b", c_void_p), ("out", c_void_p), ("bias_a", c_void_p), ("bias_b", c_void_p),
+                ("bias_out", c_void_p), ("R", c_int), ("K", c_int), ("nrows", c_int), ("interleave_h", c_int),
+                ("ka", c_int), ("acols", c_int), ("lda", c_int), ("bcols", c_int), ("ldb", c_int), ("pad_", c_int)]
+
+
 HH_ROWS = 16  # HZ_HH_ROWS (hipzap.h): rows per recurrent-partial workgroup of the decoder kernel
 
 
@@ -213,6 +219,7 @@ def _load():
     _sig(lib, "hz_http_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_http_stop", C.c_int, P)
     _sig(lib, "hz_pack_conv_launch", c_int, C.POINTER(PackConvParams), P)
+    _sig(lib, "hz_frag_pack_launch", c_int, C.POINTER(FragPackParams), P)
     _sig(lib, "hz_upload_file", c_int, C.c_char_p, c_int, C.POINTER(U64), C.POINTER(U64), C.POINTER(c_void_p), P)
     _sig(lib, "hz_lmb_layer_launch", c_int, C.POINTER(LmbLayerParams), P)
     _sig(lib, "hz_lmb_dec_launch", c_int, C.POINTER(LmbDecParams), P)

@@ -288,6 +288,21 @@ typedef struct HzPackConvParams {
   double eps;
 } HzPackConvParams;
 int hz_pack_conv_launch(const HzPackConvParams* p, hipStream_t st);
+// fp32 row-major source(s) -> bf16 fragment-major [R/16][K/32][64][8] (+ an fp32 bias row), the
+// batched AWD-LSTM packing (engine/lmbatch.py pack_lmb) on the device: output row r reads source
+// row r, or (interleave_h = H > 0) row (r & 3) * H + (r >> 2) (unit-major gates); output column k
+// reads a[src][k] for k < ka (zero at k >= acols) and b[src][k - ka] beyond (zero at >= bcols);
+// source rows >= nrows and absent segments are zeros. out == NULL: bias only.
+typedef struct HzFragPackParams {
+  const float* a;
+  const float* b;
+  unsigned short* out;
+  const float* bias_a;  // bias_out[r] = bias_a[src] (+ bias_b[src]), zero beyond the source rows
+  const float* bias_b;
+  float* bias_out;
+  int R, K, nrows, interleave_h, ka, acols, lda, bcols, ldb, pad_;
+} HzFragPackParams;
+int hz_frag_pack_launch(const HzFragPackParams* p, hipStream_t st);
 // file byte ranges -> device memory (csrc/plan.cpp): pread into two pinned staging buffers, DMA
 // chunk i while reading chunk i+1; synchronous on `st`
 int hz_upload_file(const char* path, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,

@@ -70,6 +70,50 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const HzPackConvParams p
   }
 }
 
+
+// ---- batched AWD-LSTM packing (hz_frag_pack_launch): gather + zero-pad + RNE bf16, one lane's
+// 16 bytes per thread; a second grid-stride pass writes the bias row (fp32 adds as torch does)
+__device__ __forceinline__ int frag_src_row(const HzFragPackParams& p, int r) {
+  if (p.interleave_h > 0) return r < 4 * p.interleave_h ? (r & 3) * p.interleave_h + (r >> 2) : -1;
+  return r < p.nrows ? r : -1;
+}
+
+__global__ __launch_bounds__(256) void frag_pack_kernel(const HzFragPackParams p) {
+#pragma clang fp contract(off)
+  const int ksteps = p.K / 32;
+  const long nchunk = p.out ? (long)(p.R / 16) * ksteps * 64 : 0;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < nchunk; idx += (long)gridDim.x * blockDim.x) {
+    const int lane = (int)(idx & 63);
+    const long fk = idx >> 6;
+    const int ks = (int)(fk % ksteps), t = (int)(fk / ksteps);
+    const int src = frag_src_row(p, t * 16 + (lane & 15));
+    const int k0 = ks * 32 + (lane >> 4) * 8;
+    unsigned short v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float x = 0.f;
+      if (src >= 0) {
+        if (k < p.ka) {
+          if (p.a && k < p.acols) x = p.a[(long)src * p.lda + k];
+        } else if (p.b && k - p.ka < p.bcols) {
+          x = p.b[(long)src * p.ldb + (k - p.ka)];
+        }
+      }
+      v[j] = bf16_rne(x);
+    }
+    *reinterpret_cast<u32x4*>(p.out + idx * 8) =
+        u32x4{v[0] | (unsigned)v[1] << 16, v[2] | (unsigned)v[3] << 16, v[4] | (unsigned)v[5] << 16, v[6] | (unsigned)v[7] << 16};
+  }
+  if (!p.bias_out) return;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < p.R; r += (long)gridDim.x * blockDim.x) {
+    const int src = frag_src_row(p, (int)r);
+    float x = 0.f;
+    if (src >= 0 && p.bias_a) x = p.bias_b ? p.bias_a[src] + p.bias_b[src] : p.bias_a[src];
+    p.bias_out[r] = x;
+  }
+}
+
 }  // namespace
 
 extern "C" int hz_pack_conv_launch(const HzPackConvParams* pp, hipStream_t st) {
@@ -81,5 +125,18 @@ extern "C" int hz_pack_conv_launch(const HzPackConvParams* pp, hipStream_t st) {
   const long nchunk = (long)(p.rows / 16) * p.ksteps * 64;
   const int blocks = (int)std::min<long>(2048, std::max<long>((nchunk + 255) / 256, (p.cout + 255) / 256));
   hipLaunchKernelGGL(pack_conv_kernel, dim3(blocks), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_frag_pack_launch(const HzFragPackParams* pp, hipStream_t st) {
+  const HzFragPackParams& p = *pp;
+  if (p.R % 16 || p.K % 32 || p.R <= 0 || p.K <= 0 || p.ka < 0 || p.ka > p.K || p.nrows < 0 || p.interleave_h < 0)
+    return -1;
+  if ((p.a && (p.acols < 0 || p.acols > p.ka || p.lda < p.acols)) || (p.b && (p.bcols < 0 || p.bcols > p.K - p.ka || p.ldb < p.bcols)))
+    return -1;
+  if (!p.out && !p.bias_out) return -1;
+  const long nchunk = p.out ? (long)(p.R / 16) * (p.K / 32) * 64 : p.R;
+  const long blocks = std::min<long>((nchunk + 255) / 256, 4096);
+  hipLaunchKernelGGL(frag_pack_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }

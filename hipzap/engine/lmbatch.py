@@ -49,15 +49,33 @@ def state_unpack(buf: torch.Tensor, K: int, Bp: int) -> torch.Tensor:
     return t.reshape(Bp, K)
 
 
-def pack_lmb(sd: dict, device) -> dict:
+def _native_pack_ok(dev: torch.device) -> bool:
+    if dev.type != "cuda":
+        return False
+    try:
+        return hasattr(N.lib(), "hz_frag_pack_launch")
+    except OSError:
+        return False
+
+
+def pack_lmb(sd: dict, device, native: bool | None = None) -> dict:
     """state_dict (reference key layout, awd_lstm.py:7-14) -> the batched engine's weights.
 
     Per layer l: ``W = [W_hh | W_ih]`` with rows unit-interleaved (row 4j + q = gate q of unit j,
     so one MFMA accumulator holds a unit's four gates), K segments padded to 32 (the last layer's
     recurrent segment to 256: it is also the decoder's K), fragment-major bf16; bias b_ih + b_hh.
     Embedding and decoder: [V, E] padded to [16, 256] multiples, fragment-major, stored once when
-    tied (awd_lstm.py:40)."""
+    tied (awd_lstm.py:40).
+
+    ``native`` (default on a GPU): the gathers, zero padding, RNE bf16 rounding and bias adds run
+    in one own kernel per matrix (csrc/pack.hip ``hz_frag_pack_launch``) on the raw fp32 tensors,
+    bitwise the torch ops' result. Measured cold in a fresh process (``scripts/diag_lm_build.py``):
+    the torch-op packing is ~280 ms of first-use kernel loading for ~1 ms of work."""
     dev = torch.device(device)
+    if native is None:
+        native = _native_pack_ok(dev)
+    if native:
+        return _pack_lmb_native(sd, dev)
     if any(k.endswith("_reverse") for k in sd):
         raise ValueError("bidirectional AWD-LSTM cannot drive token-by-token generation")
     emb = sd["0.encoder.weight"].float()
@@ -107,6 +125,90 @@ def pack_lmb(sd: dict, device) -> dict:
     bias = torch.zeros(Vp, device=dev)
     if dec_b is not None:
         bias[:V] = dec_b.float().to(dev)
+    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": bias, "V": V, "Vp": Vp, "E": E, "Ke": Ke}
+
+
+def _lmb_layers(sd: dict) -> list:
+    """(w_ih, w_hh, b_ih, b_hh, n_in, H) per layer, as stored (the effective W_hh rule of pack_lmb)."""
+    raw = []
+    l = 0
+    while f"0.rnns.{l}.module.weight_ih_l0" in sd:
+        pre = f"0.rnns.{l}"
+        w_ih = sd[f"{pre}.module.weight_ih_l0"]
+        w_hh = sd.get(f"{pre}.module.weight_hh_l0", sd.get(f"{pre}.weight_hh_l0_raw"))
+        raw.append((w_ih, w_hh, sd[f"{pre}.module.bias_ih_l0"], sd[f"{pre}.module.bias_hh_l0"], w_ih.shape[1],
+                    w_ih.shape[0] // 4))
+        l += 1
+    return raw
+
+
+def _pack_lmb_native(sd: dict, dev: torch.device) -> dict:
+    """pack_lmb's layout written by csrc/pack.hip (see pack_lmb); same checks, same bytes."""
+    if any(k.endswith("_reverse") for k in sd):
+        raise ValueError("bidirectional AWD-LSTM cannot drive token-by-token generation")
+    emb_src = sd["0.encoder.weight"]
+    V, E = emb_src.shape
+    Ke = _pad(E, 256)
+    if Ke > 1024:
+        raise ValueError(f"batched decode supports embedding widths <= 1024 (got {E})")
+    raw = _lmb_layers(sd)
+    if not raw:
+        raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
+    if len(raw) > 4:
+        raise ValueError("batched decode supports up to 4 layers")
+    if raw[0][4] != E or raw[-1][5] != E:
+        raise ValueError("batched decode needs layer 0 input and last hidden size = embedding width (tied model)")
+
+    def dev32(t):  # raw fp32 device copy (one H2D; a dtype conversion only for non-fp32 checkpoints)
+        t = t.to(dev, non_blocking=True)
+        return (t if t.dtype == torch.float32 else t.float()).contiguous()
+
+    lib = N.lib()
+    st = N.stream_ptr()
+
+    def launch(**kw):
+        p = N.FragPackParams()
+        for k, v in kw.items():
+            setattr(p, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+        N.check(lib.hz_frag_pack_launch(C.byref(p), st), "hz_frag_pack_launch")
+
+    layers = []
+    for i, (w_ih, w_hh, b_ih, b_hh, n_in, H) in enumerate(raw):
+        Kh = Ke if i == len(raw) - 1 else _pad(H, 32)
+        Kx = Ke if i == 0 else layers[-1]["Kh"]
+        R = _pad(4 * H, 16)
+        if (Kh + Kx) // 32 > 72:
+            raise ValueError(f"layer {i}: K = {Kh + Kx} exceeds the batched kernel's 2304")
+        a, b, ba, bb = dev32(w_hh), dev32(w_ih), dev32(b_ih), dev32(b_hh)
+        w = torch.empty(R // 16, (Kh + Kx) // 32, 64, 8, dtype=torch.bfloat16, device=dev)
+        bias = torch.empty(R, dtype=torch.float32, device=dev)
+        launch(a=a, b=b, out=w, bias_a=ba, bias_b=bb, bias_out=bias, R=R, K=Kh + Kx, nrows=4 * H, interleave_h=H,
+               ka=Kh, acols=H, lda=H, bcols=n_in, ldb=n_in)
+        layers.append({"w": w, "bias": bias, "H": H, "In": n_in, "Kh": Kh, "Kx": Kx, "R": R, "_src": (a, b, ba, bb)})
+    Vp = _pad(V, 16)
+    emb = dev32(emb_src)
+
+    def pack_vocab(m):
+        t = torch.empty(Vp // 16, Ke // 32, 64, 8, dtype=torch.bfloat16, device=dev)
+        launch(a=m, out=t, R=Vp, K=Ke, nrows=V, ka=Ke, acols=E, lda=E)
+        return t
+
+    embp = pack_vocab(emb)
+    dec_w = sd.get("1.decoder.weight")
+    tied = dec_w is None or (dec_w.device == emb_src.device and dec_w.data_ptr() == emb_src.data_ptr()
+                             and dec_w.shape == emb_src.shape and dec_w.stride() == emb_src.stride())
+    dec = None
+    if not tied:
+        dec = dev32(dec_w)
+        tied = torch.equal(dec, emb)
+    decp = embp if tied else pack_vocab(dec)
+    dec_b = sd.get("1.decoder.bias")
+    dbias = dev32(dec_b) if dec_b is not None else None
+    bias = torch.empty(Vp, dtype=torch.float32, device=dev)
+    launch(bias_a=dbias if dbias is not None else 0, bias_out=bias, R=Vp, K=32, nrows=V, ka=32)
+    torch.cuda.current_stream(dev).synchronize()  # the fp32 sources are released on return
+    for ly in layers:
+        del ly["_src"]
     return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": bias, "V": V, "Vp": Vp, "E": E, "Ke": Ke}
 
 

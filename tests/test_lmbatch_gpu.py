@@ -165,3 +165,36 @@ def test_untied_two_layer_model():
         assert (got - ref).abs().max().item() / ref.abs().max().item() < 3e-2
     finally:
         eng.close()
+
+
+def _packs_equal(a: dict, b: dict) -> None:
+    assert [k for k in a] == [k for k in b]
+    for k in ("V", "Vp", "E", "Ke"):
+        assert a[k] == b[k], k
+    for k in ("emb", "dec", "dec_bias"):
+        assert a[k].dtype == b[k].dtype and torch.equal(a[k].view(torch.int16) if a[k].dtype == torch.bfloat16 else a[k],
+                                                        b[k].view(torch.int16) if b[k].dtype == torch.bfloat16 else b[k]), k
+    assert (a["dec"] is a["emb"]) == (b["dec"] is b["emb"])  # tied stays stored once
+    for la, lb in zip(a["layers"], b["layers"]):
+        assert {k: v for k, v in la.items() if not torch.is_tensor(v)} == {k: v for k, v in lb.items() if not torch.is_tensor(v)}
+        assert torch.equal(la["w"].view(torch.int16), lb["w"].view(torch.int16)) and torch.equal(la["bias"], lb["bias"])
+
+
+@pytest.mark.parametrize("case", ["reference_tied", "untied_biased_two_layer", "bf16_checkpoint", "on_device_sd"])
+def test_native_pack_is_bitwise_the_torch_pack(model, case):
+    """csrc/pack.hip hz_frag_pack_launch (the GPU default) writes exactly pack_lmb's torch-op
+    bytes: unit-interleaved gate rows, [W_hh | W_ih] segments with zero padding, RNE bf16, b_ih +
+    b_hh in fp32, the vocabulary matrix padded to [16, 256] multiples, tied weights stored once."""
+    if case == "reference_tied":
+        sd = model.state_dict()
+    elif case == "untied_biased_two_layer":
+        torch.manual_seed(2)
+        m = get_language_model(vocab_sz=700, emb_sz=96, n_hid=160, n_layers=2, pad_token=1, tie_weights=False).eval()
+        sd = m.state_dict()
+        if "1.decoder.bias" in sd:
+            sd["1.decoder.bias"] = torch.randn_like(sd["1.decoder.bias"])
+    elif case == "bf16_checkpoint":
+        sd = {k: (v.to(torch.bfloat16) if v.is_floating_point() else v) for k, v in model.state_dict().items()}
+    else:
+        sd = {k: v.to(DEV) for k, v in model.state_dict().items()}
+    _packs_equal(pack_lmb(sd, DEV, native=False), pack_lmb(sd, DEV, native=True))
