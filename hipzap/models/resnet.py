@@ -158,21 +158,70 @@ def _bn(sd, prefix):
     return {k: sd[f"{prefix}.{k}"] for k in ("weight", "bias", "running_mean", "running_var")}
 
 
-def pack_resnet(sd: dict, device="cpu") -> dict[str, PackedConv]:
+def pack_resnet(sd: dict, device="cpu", native: bool | None = None) -> dict[str, PackedConv]:
     """state_dict -> {name: PackedConv} with BN folded (runs once at cold start). Which state_dict
     tensors feed which packed parameter: engine/nppack.py pack_sources (shared with the
-    torch-free packers)."""
+    torch-free packers).
+
+    ``native`` (default on a GPU): every conv / linear is folded and packed by one launch of the
+    device packer (csrc/pack.hip ``hz_pack_conv_launch``, the kernel of the torch-free .pth cold
+    start) instead of ~10 torch ops each -- bitwise the same bytes; in a fresh process the torch
+    ops cost 200-430 ms, almost all of it first-use kernel loading."""
     from ..engine.nppack import pack_sources
     sd = {k: v.to(device) for k, v in sd.items()}
     bottleneck = any(k.endswith("conv3.weight") for k in sd)
+    dev = torch.device(device)
+    if native is None:
+        native = dev.type == "cuda" and _native_pack_available()
     P = {}
     for name, kind, w, bn, b in pack_sources(sd):
         if kind == "linear":
-            P[name] = pack_linear(sd[w], sd[b] if b else None)
+            P[name] = _pack_native(sd[w], sd[b] if b else None, None, 1, 0, None, linear=True) if native \
+                else pack_linear(sd[w], sd[b] if b else None)
         else:
             stride, pad = _conv_stride_pad(name, sd[w].shape, bottleneck)
-            P[name] = pack_conv(sd[w], None, _bn(sd, bn), stride, pad, cin_pad=8 if name == "conv1" else None)
+            cin_pad = 8 if name == "conv1" else None
+            P[name] = _pack_native(sd[w], None, _bn(sd, bn), stride, pad, cin_pad) if native \
+                else pack_conv(sd[w], None, _bn(sd, bn), stride, pad, cin_pad=cin_pad)
+    if native:
+        torch.cuda.current_stream(dev).synchronize()  # the fp32 sources may be freed on return
     return P
+
+
+def _native_pack_available() -> bool:
+    try:
+        from .. import _native as N
+        return hasattr(N.lib(), "hz_pack_conv_launch")
+    except OSError:
+        return False
+
+
+def _pack_native(weight, bias, bn, stride, pad, cin_pad, linear=False) -> PackedConv:
+    """ops/conv.py pack_conv / pack_linear on the device (csrc/pack.hip): same layout, same bytes."""
+    import ctypes as C
+    import math
+    from .. import _native as N
+    from ..ops.conv import GEMM_ROW_PAD, ROW_PAD
+    f32 = lambda t: None if t is None else (t if t.dtype == torch.float32 else t.float()).contiguous()  # noqa: E731
+    w = f32(weight.detach())
+    cout, cin = w.shape[0], w.shape[1]
+    r, s = (1, 1) if linear else (w.shape[2], w.shape[3])
+    cin_p = cin if linear else (cin_pad or int(math.ceil(cin / 8) * 8))
+    if linear:
+        assert cin % 8 == 0
+    ksteps = int(math.ceil(r * s * cin_p / 32))
+    rows = int(math.ceil(cout / (GEMM_ROW_PAD if linear else ROW_PAD)) * (GEMM_ROW_PAD if linear else ROW_PAD))
+    wf = torch.empty(rows // 16, ksteps, 64, 8, dtype=torch.bfloat16, device=w.device)
+    bias_out = torch.empty(cout, dtype=torch.float32, device=w.device)
+    p = N.PackConvParams()
+    srcs = [w, f32(bias), *(f32(bn[k]) if bn is not None else None
+                            for k in ("weight", "bias", "running_mean", "running_var"))]
+    p.w, p.bias_in = w.data_ptr(), 0 if srcs[1] is None else srcs[1].data_ptr()
+    p.gamma, p.beta, p.mean, p.var = (0 if t is None else t.data_ptr() for t in srcs[2:])
+    p.wf, p.bias_out = wf.data_ptr(), bias_out.data_ptr()
+    p.cout, p.cin, p.r, p.s, p.cin_p, p.rows, p.ksteps, p.eps = cout, cin, r, s, cin_p, rows, ksteps, 1e-5
+    N.check(N.lib().hz_pack_conv_launch(C.byref(p), N.stream_ptr()), "hz_pack_conv_launch")
+    return PackedConv(wf, bias_out, cin_p, cout, r, s, stride, pad)
 
 
 def _conv_stride_pad(name: str, wshape, bottleneck: bool) -> tuple[int, int]:

@@ -189,3 +189,23 @@ def test_shared_context_streams_bitwise(monkeypatch):
     assert len({s.cuda_stream for s in eng.streams}) == 2
     outs = [eng.infer(x) for _ in range(12)]
     assert all(torch.equal(o, ref) for o in outs)
+
+
+@pytest.mark.parametrize("arch,dtype", [("resnet50", torch.float32), ("resnet18", torch.float32),
+                                        ("resnet50", torch.bfloat16)])
+def test_native_resnet_pack_is_bitwise_the_torch_pack(arch, dtype):
+    """pack_resnet's GPU default (csrc/pack.hip: BN fold in IEEE fp32 with the float64-rounded
+    scale, OIHW -> [cout][R*S*Cin_pad], RNE bf16, fragment-major) writes the torch-op packer's
+    bytes for every conv and the FC (also from a bf16 checkpoint)."""
+    from hipzap.models.resnet import pack_resnet, randomize_bn, resnet18, resnet50
+    torch.manual_seed(3)
+    m = randomize_bn((resnet50 if arch == "resnet50" else resnet18)()).eval()
+    sd = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in m.state_dict().items()}
+    a = pack_resnet(sd, "cuda:0", native=False)
+    b = pack_resnet(sd, "cuda:0", native=True)
+    assert list(a) == list(b)
+    for k in a:
+        pa, pb = a[k], b[k]
+        assert (pa.cin, pa.cout, pa.r, pa.s, pa.stride, pa.pad) == (pb.cin, pb.cout, pb.r, pb.s, pb.stride, pb.pad), k
+        assert pa.wf.shape == pb.wf.shape and torch.equal(pa.wf.view(torch.int16), pb.wf.view(torch.int16)), k
+        assert torch.equal(pa.bias, pb.bias), k

@@ -174,3 +174,16 @@ def test_reader_storage_marker_is_immutable(tmp_path):
             z.writestr("m/data.pkl", b"\x80\x02ctorch\nFloatStorage\n" + state)
         with pytest.raises((pickle.UnpicklingError, AttributeError)):
             pthreader.load_state_dict(str(p))
+
+
+def test_built_templates_match_the_current_code():
+    """A weightless plan template is valid only for the lowering code that wrote it (lite.code_stamp
+    over engine/, models/, ops/, tuning/): templates that exist in the tree must carry the current
+    stamp, else the torch-free .pth cold start refuses them (rebuild: python -m hipzap.build
+    --templates, which __graft_entry__.build() runs)."""
+    from hipzap import lite
+    for model in ("resnet50", "resnet18"):
+        p = lite.template_path(model)
+        if not os.path.exists(p):
+            continue
+        assert lite.read_meta(p).get("code_stamp") == lite.code_stamp(), f"{p} is stale"
