@@ -8,9 +8,60 @@ from ..ops.conv import GEMM_ROW_PAD, pack_matrix
 from ..ops.transformer import NormParams
 
 
+def _native_ok(*ts) -> bool:
+    """Device packing (csrc/pack.hip hz_frag_pack_launch) for tensors on a GPU: one launch per
+    matrix instead of ~6 torch ops whose first use in a fresh process is mostly kernel loading."""
+    import os
+    if os.environ.get("HIPZAP_NATIVE_PACK", "1") == "0":
+        return False
+    if not all(t is None or t.device.type == "cuda" for t in ts) or ts[0].device.type != "cuda":
+        return False
+    try:
+        from .. import _native as N
+        return hasattr(N.lib(), "hz_frag_pack_launch")
+    except OSError:
+        return False
+
+
+def _pack_rows_native(parts: list, npad: int):
+    """[(weight [n_j, K], bias [n_j] | None)] stacked by rows (each n_j % 16 == 0 but the last),
+    padded to ``npad`` rows and then to GEMM_ROW_PAD -> PackedConv, bitwise pack_matrix of the
+    row-concatenation (zero rows / columns, RNE bf16, fp32 bias)."""
+    import ctypes as C
+    import math
+    from .. import _native as N
+    from ..ops.conv import PackedConv
+    K = parts[0][0].shape[1]
+    dev = parts[0][0].device
+    ksteps = int(math.ceil(K / 32))
+    rows = int(math.ceil(npad / GEMM_ROW_PAD) * GEMM_ROW_PAD)
+    wf = torch.empty(rows // 16, ksteps, 64, 8, dtype=torch.bfloat16, device=dev)
+    bias = torch.empty(rows, dtype=torch.float32, device=dev)
+    f32 = lambda t: None if t is None else (t.detach() if t.dtype == torch.float32 else t.detach().float()).contiguous()  # noqa: E731
+    keep, r0 = [], 0
+    for j, (w, b) in enumerate(parts):
+        w, b = f32(w), f32(b)
+        keep += [w, b]
+        n = w.shape[0]
+        R = rows - r0 if j == len(parts) - 1 else n  # the last part also writes the zero padding rows
+        p = N.FragPackParams()
+        p.a, p.out = w.data_ptr(), wf.data_ptr() + (r0 // 16) * ksteps * 1024
+        p.bias_a, p.bias_out = (0 if b is None else b.data_ptr()), bias.data_ptr() + 4 * r0
+        p.R, p.K, p.nrows, p.ka, p.acols, p.lda = R, ksteps * 32, n, ksteps * 32, K, K
+        N.check(N.lib().hz_frag_pack_launch(C.byref(p), N.stream_ptr()), "hz_frag_pack_launch")
+        r0 += n
+    out_bias = bias[:npad].clone()  # its own storage (a D2D copy), as the torch path's bias
+    torch.cuda.current_stream(dev).synchronize()  # the fp32 sources may be temporaries
+    return PackedConv(wf, out_bias, K, npad, 1, 1, 1, 0)
+
+
 def pack_linear_padded(weight: torch.Tensor, bias: torch.Tensor | None, out_multiple: int = 4):
     """Pack a Linear for the GEMM kernel; output rows padded to ``out_multiple`` (the epilogue
-    stores 4 channels per lane) — logical width kept by the caller."""
+    stores 4 channels per lane) — logical width kept by the caller. On a GPU: the device packer
+    (bitwise the torch ops, tests/test_transformers_gpu.py)."""
+    if _native_ok(weight, bias):
+        n = weight.shape[0]
+        return _pack_rows_native([(weight, bias)], (n + out_multiple - 1) // out_multiple * out_multiple)
     w = weight.detach().float()
     b = bias.detach().float() if bias is not None else torch.zeros(w.shape[0], device=w.device)
     n = w.shape[0]
@@ -22,6 +73,9 @@ def pack_linear_padded(weight: torch.Tensor, bias: torch.Tensor | None, out_mult
 
 
 def pack_qkv(q_w, q_b, k_w, k_b, v_w, v_b):
+    if _native_ok(q_w, q_b, k_w, k_b, v_w, v_b) and q_w.shape[0] % 16 == 0 and k_w.shape[0] % 16 == 0:
+        n = q_w.shape[0] + k_w.shape[0] + v_w.shape[0]
+        return _pack_rows_native([(q_w, q_b), (k_w, k_b), (v_w, v_b)], (n + 3) // 4 * 4)
     return pack_linear_padded(torch.cat([q_w, k_w, v_w]), torch.cat([q_b, k_b, v_b]))
 
 

@@ -184,3 +184,27 @@ def test_bert_fp8_engine_matches_graph_oracle_and_hf():
     # picked the bf16 engine's 2nd class), never a class far down the bf16 ranking
     top3 = y16.topk(3, dim=1).indices
     assert all(int(y8[r].argmax()) in top3[r].tolist() for r in range(B)), (y8.argmax(1), top3)
+
+
+@pytest.mark.parametrize("n,k,bias", [(768, 768, True), (1000, 768, True), (2, 768, True), (3072, 768, False),
+                                      (768, 3072, True), (10, 100, True)])
+def test_native_linear_pack_is_bitwise_the_torch_pack(n, k, bias):
+    """models/_tx.py pack_linear_padded on a GPU (csrc/pack.hip hz_frag_pack_launch) writes the
+    torch path's bytes (row padding to 4 and to the GEMM tile, K padding, RNE bf16, fp32 bias)."""
+    from hipzap.models._tx import pack_linear_padded
+    g = torch.Generator().manual_seed(n + k)
+    w, b = torch.randn(n, k, generator=g), (torch.randn(n, generator=g) if bias else None)
+    ref = pack_linear_padded(w, b)  # CPU: the torch ops
+    got = pack_linear_padded(w.to(DEV), None if b is None else b.to(DEV))
+    assert (got.cin, got.cout, got.r, got.s) == (ref.cin, ref.cout, ref.r, ref.s)
+    assert torch.equal(got.wf.cpu().view(torch.int16), ref.wf.view(torch.int16)) and torch.equal(got.bias.cpu(), ref.bias)
+
+
+def test_native_qkv_pack_is_bitwise_the_torch_pack():
+    from hipzap.models._tx import pack_qkv
+    g = torch.Generator().manual_seed(7)
+    t = [torch.randn(768, 768, generator=g) if i % 2 == 0 else torch.randn(768, generator=g) for i in range(6)]
+    ref = pack_qkv(*t)
+    got = pack_qkv(*[x.to(DEV) for x in t])
+    assert got.cout == ref.cout == 2304 and got.wf.shape == ref.wf.shape
+    assert torch.equal(got.wf.cpu().view(torch.int16), ref.wf.view(torch.int16)) and torch.equal(got.bias.cpu(), ref.bias)
