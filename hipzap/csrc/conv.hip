@@ -583,3 +583,13 @@ extern "C" int hz_conv_chain_launch(const HzConvChainParams* cpp, hipStream_t st
   hipLaunchKernelGGL(conv_chain_kernel, dim3(cp.grid), dim3(kChainThreads), (size_t)cp.lds, st, cp);
   return (int)hipGetLastError();
 }
+
+// Load this translation unit's device code now (hipFuncGetAttributes makes the runtime load the
+// code object of the fatbin that holds the kernel, without a launch or a stream): the plan loader
+// calls it on a helper thread while the weight blob uploads, so the first request does not pay
+// the load (csrc/plan.cpp hz_plan_open).
+__global__ void hz_conv_code_warm_kernel() {}
+extern "C" int hz_conv_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_conv_code_warm_kernel));
+}

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hipzap.h"
@@ -519,6 +520,23 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   if (e == hipSuccess) e = hipFree(nullptr);
   double t2 = now_ms();
   p->t[HZ_PLAN_T_HIP_INIT] = t2 - t1;
+  // the first request's kernels live in conv.hip / vision.hip: have the runtime load that device
+  // code on a helper thread while this one uploads the weights (HIPZAP_PLAN_CODE_WARM=0: off)
+  std::thread warm;
+  const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
+  if (e == hipSuccess && !(cw && cw[0] == '0'))
+    warm = std::thread([device] {
+      if (hipSetDevice(device) == hipSuccess) {
+        (void)hz_conv_code_warm();
+        (void)hz_vision_code_warm();
+      }
+    });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{warm};
   if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);
   p->t[HZ_PLAN_T_BLOB_ALLOC] = now_ms() - t2;
   if (e != hipSuccess) {

@@ -355,3 +355,13 @@ extern "C" int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipSt
   hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, y, n);
   return (int)hipGetLastError();
 }
+
+// Load this translation unit's device code now (hipFuncGetAttributes makes the runtime load the
+// code object of the fatbin that holds the kernel, without a launch or a stream): the plan loader
+// calls it on a helper thread while the weight blob uploads, so the first request does not pay
+// the load (csrc/plan.cpp hz_plan_open).
+__global__ void hz_vision_code_warm_kernel() {}
+extern "C" int hz_vision_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_vision_code_warm_kernel));
+}
