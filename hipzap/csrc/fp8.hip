@@ -824,3 +824,10 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
     default: return -2;
   }
 }
+
+// Load this translation unit's device code without a launch (see hz_conv_code_warm in conv.hip).
+__global__ void hz_fp8_code_warm_kernel() {}
+extern "C" int hz_fp8_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_fp8_code_warm_kernel));
+}

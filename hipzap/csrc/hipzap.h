@@ -290,6 +290,10 @@ typedef struct HzPackConvParams {
 int hz_pack_conv_launch(const HzPackConvParams* p, hipStream_t st);
 int hz_conv_code_warm(void);    // load conv.hip / vision.hip device code (no launch)
 int hz_vision_code_warm(void);
+int hz_gemm_code_warm(void);
+int hz_transformer_code_warm(void);
+int hz_fp8_code_warm(void);
+int hz_pack_code_warm(void);
 // fp32 row-major source(s) -> bf16 fragment-major [R/16][K/32][64][8] (+ an fp32 bias row), the
 // batched AWD-LSTM packing (engine/lmbatch.py pack_lmb) on the device: output row r reads source
 // row r, or (interleave_h = H > 0) row (r & 3) * H + (r >> 2) (unit-major gates); output column k

@@ -140,3 +140,10 @@ extern "C" int hz_frag_pack_launch(const HzFragPackParams* pp, hipStream_t st) {
   hipLaunchKernelGGL(frag_pack_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
+
+// Load this translation unit's device code without a launch (see hz_conv_code_warm in conv.hip).
+__global__ void hz_pack_code_warm_kernel() {}
+extern "C" int hz_pack_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_pack_code_warm_kernel));
+}

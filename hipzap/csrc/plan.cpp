@@ -32,6 +32,7 @@ constexpr uint32_t kPlanVersion = 1;
 // is filled by the caller, e.g. by packing a .pth checkpoint on the device (csrc/pack.hip)
 constexpr uint64_t kFlagWeightless = 1;
 constexpr char kMagic[8] = {'H', 'Z', 'P', 'L', 'A', 'N', '0', '1'};
+enum : unsigned { kUnitConv = 1, kUnitVision = 2, kUnitGemm = 4, kUnitTransformer = 8, kUnitFp8 = 16, kUnitPack = 32 };
 
 // file header: magic + 15 little-endian u64 fields (see plan.py PlanHeader)
 struct FileHeader {
@@ -103,7 +104,10 @@ struct Plan {
                                 // ~10-25 ms of lazy runtime work in a fresh process)
   hipStream_t cap_st = nullptr;  // private capture stream for contexts on borrowed streams
   std::mutex cap_mu;
+  std::thread warm;  // device-code warm-up (hz_plan_open); outlives the open call so a weightless
+                     // template's warm-up overlaps the caller's checkpoint upload and packing
   ~Plan() {
+    if (warm.joinable()) warm.join();
     (void)hipSetDevice(device);
     // borrowed streams first: their owners' free_ctx destroys the stream
     for (auto& c : ctx)
@@ -123,6 +127,37 @@ struct Plan {
     if (c.dev) (void)hipFree(c.dev);
     if (c.host) (void)hipHostFree(c.host);
     c = PlanCtx{};
+  }
+
+  // translation units whose kernels the ops launch (bit set for hz_plan_open's code warm-up)
+  unsigned code_units() const {
+    unsigned u = 0;
+    for (const PlanOp& op : ops) {
+      switch (op.h.type) {
+        case HZ_PLAN_OP_CONV: u |= op.h.arg >= 16 ? kUnitGemm : kUnitConv; break;
+        case HZ_PLAN_OP_CONV2: u |= kUnitConv; break;
+        case HZ_PLAN_OP_MAXPOOL:
+        case HZ_PLAN_OP_AVGPOOL:
+        case HZ_PLAN_OP_PREPROCESS: u |= kUnitVision; break;
+        case HZ_PLAN_OP_KERNEL:
+          switch (op.h.arg) {
+            case HZ_K_LAYERNORM:
+            case HZ_K_EMBED:
+            case HZ_K_ATTENTION:
+            case HZ_K_VIT_TOKENS:
+            case HZ_K_SOFTMAX: u |= kUnitTransformer; break;
+            case HZ_K_GEMM_FP8:
+            case HZ_K_QUANT: u |= kUnitFp8; break;
+            case HZ_K_MAXPOOL:
+            case HZ_K_POOL_FC: u |= kUnitVision; break;
+            case HZ_K_CONV_CHAIN: u |= kUnitConv; break;
+            default: break;
+          }
+          break;
+        default: break;
+      }
+    }
+    return u;
   }
 
   int parse() {
@@ -520,23 +555,24 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   if (e == hipSuccess) e = hipFree(nullptr);
   double t2 = now_ms();
   p->t[HZ_PLAN_T_HIP_INIT] = t2 - t1;
-  // the first request's kernels live in conv.hip / vision.hip: have the runtime load that device
-  // code on a helper thread while this one uploads the weights (HIPZAP_PLAN_CODE_WARM=0: off)
-  std::thread warm;
+  // have the runtime load the device code of every translation unit the plan's ops launch (and
+  // the packer's, for a weightless template) on a helper thread while this one uploads the
+  // weights, instead of at the first request's first launches (HIPZAP_PLAN_CODE_WARM=0: off).
+  // Not joined here: the runtime serialises code-object loading against launches, and the
+  // thread is joined when the plan is closed.
   const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
-  if (e == hipSuccess && !(cw && cw[0] == '0'))
-    warm = std::thread([device] {
-      if (hipSetDevice(device) == hipSuccess) {
-        (void)hz_conv_code_warm();
-        (void)hz_vision_code_warm();
-      }
+  if (e == hipSuccess && !(cw && cw[0] == '0')) {
+    const unsigned units = p->code_units() | ((p->h.flags & kFlagWeightless) ? kUnitPack : 0u);
+    p->warm = std::thread([device, units] {
+      if (hipSetDevice(device) != hipSuccess) return;
+      if (units & kUnitConv) (void)hz_conv_code_warm();
+      if (units & kUnitVision) (void)hz_vision_code_warm();
+      if (units & kUnitGemm) (void)hz_gemm_code_warm();
+      if (units & kUnitTransformer) (void)hz_transformer_code_warm();
+      if (units & kUnitFp8) (void)hz_fp8_code_warm();
+      if (units & kUnitPack) (void)hz_pack_code_warm();
     });
-  struct Joiner {
-    std::thread& t;
-    ~Joiner() {
-      if (t.joinable()) t.join();
-    }
-  } joiner{warm};
+  }
   if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);
   p->t[HZ_PLAN_T_BLOB_ALLOC] = now_ms() - t2;
   if (e != hipSuccess) {

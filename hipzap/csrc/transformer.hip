@@ -446,3 +446,10 @@ extern "C" int hz_vit_tokens_launch(const HzVitTokensParams* pp, hipStream_t st)
   hipLaunchKernelGGL(vit_tokens_kernel, dim3((total + 255) / 256), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
+
+// Load this translation unit's device code without a launch (see hz_conv_code_warm in conv.hip).
+__global__ void hz_transformer_code_warm_kernel() {}
+extern "C" int hz_transformer_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_transformer_code_warm_kernel));
+}
