@@ -104,10 +104,12 @@ struct Plan {
                                 // ~10-25 ms of lazy runtime work in a fresh process)
   hipStream_t cap_st = nullptr;  // private capture stream for contexts on borrowed streams
   std::mutex cap_mu;
-  std::thread warm;  // device-code warm-up (hz_plan_open); outlives the open call so a weightless
-                     // template's warm-up overlaps the caller's checkpoint upload and packing
-  ~Plan() {
+  std::thread warm;  // device-code warm-up, joined before hz_plan_open returns
+  void join_warm() {
     if (warm.joinable()) warm.join();
+  }
+  ~Plan() {
+    join_warm();
     (void)hipSetDevice(device);
     // borrowed streams first: their owners' free_ctx destroys the stream
     for (auto& c : ctx)
@@ -558,8 +560,9 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   // have the runtime load the device code of every translation unit the plan's ops launch (and
   // the packer's, for a weightless template) on a helper thread while this one uploads the
   // weights, instead of at the first request's first launches (HIPZAP_PLAN_CODE_WARM=0: off).
-  // Not joined here: the runtime serialises code-object loading against launches, and the
-  // thread is joined when the plan is closed.
+  // Joined before returning: left running into the caller's context setup (stream creation,
+  // hipMemsetAsync), it crashed the runtime in a process that already held RCCL communicators
+  // (tests/test_cluster_gpu.py, profiles/r3_warm3/README.md).
   const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
   if (e == hipSuccess && !(cw && cw[0] == '0')) {
     const unsigned units = p->code_units() | ((p->h.flags & kFlagWeightless) ? kUnitPack : 0u);
@@ -593,6 +596,7 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
       return nullptr;
     }
   }
+  p->join_warm();
   p->t[HZ_PLAN_T_UPLOAD] = now_ms() - t2 - p->t[HZ_PLAN_T_BLOB_ALLOC];
   if (timings) std::memcpy(timings, p->t, sizeof(p->t));
   return p;
