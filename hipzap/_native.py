@@ -210,6 +210,7 @@ def _load():
     _sig(lib, "hz_exec_create_batched", P, PP_, PP_, PP_, C.POINTER(U64), c_int, PP_, U64, c_int, c_int, D, c_int)
     _sig(lib, "hz_exec_batches", None, P, C.POINTER(U64))
     _sig(lib, "hz_exec_submit", c_int, P, PP_, P, C.POINTER(D))
+    _sig(lib, "hz_exec_submit_rows", c_int, P, PP_, c_int, P, C.POINTER(D))
     _sig(lib, "hz_exec_stats", None, P, C.POINTER(U64), C.POINTER(U64))
     _sig(lib, "hz_exec_destroy", None, P)
     _sig(lib, "hz_exec_bench", c_int, P, c_int, c_int, PP_, C.POINTER(D), C.POINTER(D))

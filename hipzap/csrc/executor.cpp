@@ -24,6 +24,7 @@
 // GEMM (gemm.hip CV mode), so one batched replay costs far less than B single-image replays.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -193,13 +194,74 @@ struct Exec {
     return rc;
   }
 
-  int submit_wait(const void* const* in, void* out, double* lat_us) {
+  // m consecutive rows of one request (m <= rows) from ONE thread: each chunk claims what the open
+  // slot has left, copies it, waits for that replay and reads its rows back before the next chunk
+  // claims anything, so the thread never holds an unread slot while waiting for a free one
+  int submit_rows(const void* const* in, int m, void* out, double* lat_us) {
+    const double t0 = now_us();
+    int rc = 0;
+    for (int done = 0; done < m && !rc;) {
+      int s, r, k;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        while (open < 0) {
+          if (stop) return -10;
+          if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+            Slot& o = slots[s];
+            o.claimed = o.copied = o.read = 0;
+            o.sealed = o.done = false;
+            o.t_open = now_us();
+            open = s;
+            cv_work.notify_one();
+            cv_free.notify_all();
+            break;
+          }
+          cv_free.wait(lk);
+        }
+        s = open;
+        r = slots[s].claimed;
+        k = std::min(m - done, rows - r);
+        slots[s].claimed += k;
+        if (slots[s].claimed == rows) seal_open();
+      }
+      Slot& sl = slots[s];
+      for (int q = 0; q < n_in; ++q)
+        if (in && in[q] && row_in[q])
+          std::memcpy(static_cast<char*>(sl.in[q]) + r * row_in[q], static_cast<const char*>(in[q]) + done * row_in[q],
+                      k * row_in[q]);
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        sl.copied += k;
+        queue_if_ready(s);
+        sl.cv.wait(lk, [&] { return sl.done; });
+        rc = sl.rc;
+      }
+      if (!rc && out && row_out)
+        std::memcpy(static_cast<char*>(out) + done * row_out, static_cast<const char*>(sl.out) + r * row_out, k * row_out);
+      {
+        std::lock_guard<std::mutex> g(mu);
+        sl.read += k;
+        if (sl.read == sl.claimed) {
+          free_slots.push_back(s);
+          cv_free.notify_all();
+        }
+      }
+      done += k;
+    }
+    if (lat_us) *lat_us = now_us() - t0;
+    return rc;
+  }
+
+  int submit_wait(const void* const* in, void* out, double* lat_us, int m = 1) {
     {
       std::lock_guard<std::mutex> g(mu);
       if (stop) return -10;
       ++active;
     }
-    const int rc = rows > 1 ? submit_batched(in, out, lat_us) : submit_one(in, out, lat_us);
+    const int rc = rows > 1 ? (m > 1 ? submit_rows(in, m, out, lat_us) : submit_batched(in, out, lat_us))
+                            : submit_one(in, out, lat_us);
     {
       std::lock_guard<std::mutex> g(mu);
       if (--active == 0 && stop) cv_work.notify_all();
@@ -311,6 +373,14 @@ void hz_exec_batches(void* h, uint64_t* batches) {
 
 int hz_exec_submit(void* h, const void* const* in, void* out, double* lat_us) {
   return static_cast<Exec*>(h)->submit_wait(in, out, lat_us);
+}
+
+// dynamic-batching executor only: one request of m (1..rows) consecutive rows, in[k] / out holding
+// m rows each; the rows share replays with other requests' rows
+int hz_exec_submit_rows(void* h, const void* const* in, int m, void* out, double* lat_us) {
+  Exec* e = static_cast<Exec*>(h);
+  if (e->rows <= 1 || m < 1 || m > e->rows) return -1;
+  return e->submit_wait(in, out, lat_us, m);
 }
 
 void hz_exec_stats(void* h, uint64_t* served, uint64_t* polls) {

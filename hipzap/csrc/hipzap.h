@@ -498,6 +498,7 @@ void* hz_exec_create_batched(HzProgram* progs, hipStream_t* streams, void** host
                              int min_inflight);
 void hz_exec_batches(void* exec, uint64_t* batches);
 int hz_exec_submit(void* exec, const void* const* in, void* out, double* lat_us);
+int hz_exec_submit_rows(void* exec, const void* const* in, int m, void* out, double* lat_us);
 void hz_exec_stats(void* exec, uint64_t* served, uint64_t* polls);
 void hz_exec_destroy(void* exec);
 int hz_exec_bench(void* exec, int clients, int iters, const void* const* in, double* lat_us, double* wall_us);

@@ -50,6 +50,19 @@ class Executor:
             raise RuntimeError(f"executor request failed ({rc})")
         return lat.value * 1e-3
 
+    def submit_rows(self, in_ptrs: list, m: int, out_ptr: int) -> float:
+        """Dynamic batching only: one request of ``m`` (1..rows) consecutive rows from this one
+        thread (``in_ptrs[k]`` holds m rows of input k, ``out_ptr`` receives m output rows); the
+        rows join the open batch like single-row requests. Returns latency in ms."""
+        if self.rows <= 1 or not 1 <= m <= self.rows:
+            raise ValueError(f"submit_rows: m={m} needs a dynamic-batching executor with rows >= m ({self.rows})")
+        arr = (C.c_void_p * self.n_in)(*in_ptrs)
+        lat = C.c_double()
+        rc = N.lib().hz_exec_submit_rows(self._h, arr, int(m), out_ptr, C.byref(lat))
+        if rc:
+            raise RuntimeError(f"executor request failed ({rc})")
+        return lat.value * 1e-3
+
     def bench(self, clients: int, iters: int, in_ptrs: list) -> tuple[float, list]:
         """``clients`` native client threads x ``iters`` back-to-back requests each.
         Returns (wall seconds, per-request latencies in ms)."""

@@ -408,26 +408,13 @@ class PlanEngine:
             bex = self.batched_executor()
         if bex is not None:
             # the contexts belong to the dynamic-batching executor (native /predict): the real
-            # rows go through it as one-image requests, submitted together so they share a replay
-            ib, ob = bex.in_bytes[0], bex.out_bytes
+            # rows join its open batch from this thread (hz_exec_submit_rows), sharing replays
+            # with concurrent one-image requests
             m = bex.rows if rows is None else max(1, min(int(rows), bex.rows))
-            errs = []
-
-            def one(r):
-                try:
-                    bex.submit([addr + r * ib], oaddr + r * ob)
-                except Exception as e:  # noqa: BLE001 - re-raised below
-                    errs.append(e)
-
-            th = [threading.Thread(target=one, args=(r,)) for r in range(1, m)]
-            for t in th:
-                t.start()
-            one(0)
-            for t in th:
-                t.join()
-            del keep
-            if errs:
-                raise errs[0]
+            try:
+                bex.submit_rows([addr], m, oaddr)
+            finally:
+                del keep
             return out
         ex = self.executor() if ctx is None else None
         if ex is not None:

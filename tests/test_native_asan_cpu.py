@@ -46,3 +46,27 @@ def test_http_parsers_fuzz_asan_ubsan(tmp_path):
     run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert run.returncode == 0 and "http parse fuzz: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
     assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("sanitizer", ["address,undefined", "thread"])
+def test_executor_host_sanitizers(tmp_path, sanitizer):
+    """The request executor (csrc/executor.cpp) under host ASan+UBSan and under ThreadSanitizer:
+    concurrent single-row, dynamic-batching and multi-row (hz_exec_submit_rows) requests against a
+    fake program that computes each row at replay time, so a launch before the rows are copied or a
+    read before the replay is a wrong answer, and any unsynchronised slot access is a TSan report."""
+    exe = tmp_path / f"exec_{sanitizer.split(',')[0]}"
+    san = []
+    for f in (f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
+        san += ["-Xarch_host", f]
+    cmd = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", os.path.join(ROOT, "hipzap", "csrc"),
+           os.path.join(ROOT, "hipzap", "csrc", "executor.cpp"),
+           os.path.join(ROOT, "tests", "native", "executor_host_sanitize.cpp"), "-lpthread", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert run.returncode == 0 and "executor host sanitize: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
+    for marker in ("ERROR: AddressSanitizer", "runtime error", "WARNING: ThreadSanitizer"):
+        assert marker not in run.stderr, run.stderr[-4000:]
