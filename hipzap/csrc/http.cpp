@@ -372,8 +372,9 @@ bool try_fast(Server* S, const std::string& method, const std::string& target, c
 }
 
 // ---------------------------------------------------------------- connections
+// S->live was incremented by the spawner BEFORE this thread exists (hz_http_stop frees the server
+// once it reads live == 0: a count taken here could come after that read)
 void serve_conn(Server* S, int fd) {
-  S->live++;
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   std::string buf;
@@ -492,6 +493,7 @@ void accept_loop(Server* S) {
     if (pr <= 0) continue;
     const int fd = accept(S->lfd, nullptr, nullptr);
     if (fd < 0) continue;  // another process sharing the socket took it, or EINTR
+    S->live++;
     std::thread(serve_conn, S, fd).detach();
   }
 }

@@ -6,7 +6,13 @@
 // answers), including pipelined requests and truncated bodies.
 #include "../../hipzap/csrc/http.cpp"
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
 #include <sys/socket.h>
+#include <sys/time.h>
+
+#include <atomic>
+#include <vector>
 
 #include <cstdlib>
 #include <random>
@@ -93,6 +99,7 @@ void fuzz_framing() {
     if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv)) abort();
     std::string req = it % 7 == 6 ? rnd_bytes(rng() % 300, nullptr) : mutate(seeds[rng() % 5]);
     if (rng() % 3 == 0) req += seeds[rng() % 5];
+    S.live++;  // the spawner's count (accept_loop)
     std::thread t(serve_conn, &S, sv[1]);  // closes sv[1] when it returns
     send_all(sv[0], req.data(), req.size());
     shutdown(sv[0], SHUT_WR);  // EOF: a truncated body ends the connection
@@ -104,11 +111,68 @@ void fuzz_framing() {
   }
 }
 
+extern "C" void echo_handler(void* req, const char*, const char* target, const char*, uint64_t, const char*,
+                             uint64_t blen) {
+  const std::string body = std::string("{\"target\": \"") + target + "\", \"n\": " + std::to_string(blen) + "}";
+  const std::string hdr = "Content-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+  hz_http_respond(req, 200, hdr.data(), hdr.size(), body.data(), body.size());
+}
+
+// the whole server over loopback TCP: acceptor + one thread per connection + the handler
+// callback, with hz_http_stop racing clients that are still connecting (5 start/stop rounds on
+// one listening socket). Under ThreadSanitizer this is the race check of the connection
+// accounting that lets hz_http_stop free the server.
+void server_rounds() {
+  const int lfd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = 0;
+  if (lfd < 0 || bind(lfd, (sockaddr*)&a, sizeof(a)) || listen(lfd, 256)) abort();
+  socklen_t al = sizeof(a);
+  getsockname(lfd, (sockaddr*)&a, &al);
+  std::atomic<int> ok{0};
+  for (int round = 0; round < 5; ++round) {
+    void* srv = hz_http_start(lfd, echo_handler);
+    std::atomic<bool> quit{false};
+    std::vector<std::thread> cl;
+    for (int c = 0; c < 6; ++c)
+      cl.emplace_back([&, c] {
+        while (!quit.load()) {
+          const int fd = socket(AF_INET, SOCK_STREAM, 0);
+          timeval tv{0, 200000};
+          setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+          if (connect(fd, (sockaddr*)&a, sizeof(a)) == 0) {
+            const std::string req = "POST /c" + std::to_string(c) +
+                                    " HTTP/1.1\r\nContent-Length: 3\r\nConnection: close\r\n\r\nabc";
+            send_all(fd, req.data(), req.size());
+            char buf[512];
+            const ssize_t k = recv(fd, buf, sizeof(buf) - 1, 0);
+            if (k > 0) {
+              buf[k] = 0;
+              if (strstr(buf, "200 OK") && strstr(buf, "\"n\": 3")) ok++;
+            }
+          }
+          close(fd);
+        }
+      });
+    std::this_thread::sleep_for(std::chrono::milliseconds(60));
+    const int freed = hz_http_stop(srv);  // clients are still connecting
+    quit.store(true);
+    for (auto& t : cl) t.join();
+    if (!freed) abort();  // every connection here is short: the server must have been freed
+  }
+  close(lfd);
+  if (ok.load() < 10) abort();
+  printf("server rounds: %d answered\n", ok.load());
+}
+
 }  // namespace
 
 int main() {
   fuzz_parsers();
   fuzz_framing();
+  server_rounds();
   printf("http parse fuzz: ok\n");
   return 0;
 }

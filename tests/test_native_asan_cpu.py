@@ -30,22 +30,27 @@ def test_runtime_host_asan_ubsan(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_http_parsers_fuzz_asan_ubsan(tmp_path):
+@pytest.mark.parametrize("sanitizer", ["address,undefined", "thread"])
+def test_http_parsers_fuzz_asan_ubsan(tmp_path, sanitizer):
     """The native HTTP front end's body parsers (JSON image, .npy, base64, int arrays) on 200k
-    mutated / random inputs held in exact-size heap blocks, and its request framing (serve_conn
-    over a socketpair: pipelined, truncated, chunked, negative lengths) under host ASan + UBSan."""
-    exe = tmp_path / "http_fuzz"
+    mutated / random inputs held in exact-size heap blocks, its request framing (serve_conn
+    over a socketpair: pipelined, truncated, chunked, negative lengths), and the whole server over
+    loopback TCP with hz_http_stop racing connecting clients -- under host ASan + UBSan and
+    under ThreadSanitizer."""
+    exe = tmp_path / f"http_fuzz_{sanitizer.split(',')[0]}"
     san = []
-    for f in ("-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
+    for f in (f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
         san += ["-Xarch_host", f]
     cmd = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", os.path.join(ROOT, "hipzap", "csrc"),
            os.path.join(ROOT, "tests", "native", "http_parse_fuzz.cpp"), "-lpthread", "-o", str(exe)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1")
     run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert run.returncode == 0 and "http parse fuzz: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
-    assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
+    for marker in ("ERROR: AddressSanitizer", "runtime error", "WARNING: ThreadSanitizer"):
+        assert marker not in run.stderr, run.stderr[-4000:]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
