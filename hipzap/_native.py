@@ -198,6 +198,7 @@ def _load():
     _sig(lib, "hz_plan_host", P, P, c_int)
     _sig(lib, "hz_plan_device", P, P, c_int)
     _sig(lib, "hz_plan_stream", P, P, c_int)
+    _sig(lib, "hz_plan_upload_stream", P, P)
     _sig(lib, "hz_plan_replay", c_int, P, c_int)
     _sig(lib, "hz_plan_sync", c_int, P, c_int)
     _sig(lib, "hz_plan_infer", c_int, P, c_int, P, U64, U64, P, U64, U64)

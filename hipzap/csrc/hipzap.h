@@ -480,6 +480,7 @@ void* hz_plan_blob(void* plan, uint64_t* bytes);
 void* hz_plan_host(void* plan, int ctx);
 void* hz_plan_device(void* plan, int ctx);
 void* hz_plan_stream(void* plan, int ctx);
+void* hz_plan_upload_stream(void* plan);
 int hz_plan_replay(void* plan, int ctx);
 int hz_plan_sync(void* plan, int ctx);
 int hz_plan_infer(void* plan, int ctx, const void* in, uint64_t in_off, uint64_t in_bytes, void* out,

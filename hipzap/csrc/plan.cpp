@@ -583,15 +583,16 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
     delete p;
     return nullptr;
   }
-  if (read_blob) {
+  {  // the upload stream: kept, it becomes the first context's stream (a weightless template's
+     // caller fills the blob on it, hz_plan_upload_stream, instead of creating a stream of its own)
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       fail("plan: stream creation failed");
       delete p;
       return nullptr;
     }
-    p->spare = s;  // kept: becomes the first context's stream
-    if (p->upload_blob(s)) {
+    p->spare = s;
+    if (read_blob && p->upload_blob(s)) {
       delete p;
       return nullptr;
     }
@@ -618,6 +619,13 @@ void hz_plan_timings(void* h, double* out) { std::memcpy(out, P(h)->t, sizeof(P(
 void* hz_plan_blob(void* h, uint64_t* bytes) {
   if (bytes) *bytes = P(h)->h.blob_len;
   return P(h)->blob;
+}
+
+// the stream hz_plan_open created for the blob upload until the first context takes it over
+// (NULL afterwards): fill a weightless template's blob on it before adding contexts
+void* hz_plan_upload_stream(void* h) {
+  std::lock_guard<std::mutex> g(P(h)->mu);
+  return (void*)P(h)->spare;
 }
 
 void* hz_plan_host(void* h, int ctx) {

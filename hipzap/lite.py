@@ -120,6 +120,16 @@ def no_sdma_default() -> None:
         os.environ.setdefault("HSA_ENABLE_SDMA", "0")
 
 
+_fill_tls = threading.local()
+
+
+def upload_stream() -> int | None:
+    """Inside a ``fill_blob`` callback: the plan's upload stream, which becomes the first
+    context's stream (a fill that runs on it creates no stream of its own, ~10-20 ms of lazy
+    runtime work in a fresh process); None outside a fill."""
+    return getattr(_fill_tls, "stream", None)
+
+
 class PlanEngine:
     """One plan image on one GPU. ``read_blob=False`` + ``fill_blob(address, nbytes)`` lets a DP
     rank receive the weights by RCCL broadcast instead of reading the file."""
@@ -148,7 +158,11 @@ class PlanEngine:
             nb = C.c_uint64()
             addr = L.hz_plan_blob(h, C.byref(nb))
             ta = time.perf_counter()
-            fill_blob(addr, nb.value)
+            _fill_tls.stream = L.hz_plan_upload_stream(h) or None
+            try:
+                fill_blob(addr, nb.value)
+            finally:
+                _fill_tls.stream = None
             self.timings["broadcast_ms"] = (time.perf_counter() - ta) * 1e3
         self.num_contexts = contexts
         self._capture = bool(capture)
@@ -234,7 +248,7 @@ class PlanEngine:
             n = len(stores)
             U64 = C.c_uint64 * n
             keys = list(stores)
-            stream = hip._private_stream()
+            stream = upload_stream() or hip._private_stream()
             rc = lib().hz_upload_file(ckpt.encode(), n, U64(*[stores[k].file_off for k in keys]),
                                       U64(*[stores[k].nbytes for k in keys]),
                                       (C.c_void_p * n)(*[staging.ptr + offs[k] for k in keys]), stream)
