@@ -1,9 +1,9 @@
 #!/bin/bash
-# self-launched 2-rank rehearsal on ONE GPU (gloo, ranks folded onto cuda:0) with every secondary
+# self-launched 4-rank rehearsal on ONE GPU (gloo, ranks folded onto cuda:0) with every secondary
 # figure on (sustained window, BERT plan cold start, HTTP serving through hipzap serve --gpus 2)
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-O=gpurun_out/r3_launch2
+O=gpurun_out/r3_launch2_final
 mkdir -p $O
 HIPZAP_DIST_BACKEND=gloo HIPZAP_SHARE_GPU=1 timeout -k 10 900 python bench.py --gpus 2 --steps 20 --warmup 5 \
   > $O/self_launch_2.log 2>&1 || { tail -40 $O/self_launch_2.log; exit 1; }
