@@ -187,3 +187,22 @@ def test_built_templates_match_the_current_code():
         if not os.path.exists(p):
             continue
         assert lite.read_meta(p).get("code_stamp") == lite.code_stamp(), f"{p} is stale"
+
+
+def test_upload_stream_only_inside_a_fill():
+    """lite.upload_stream() hands a fill_blob callback the plan's upload stream (set by PlanEngine
+    around the callback) and is None everywhere else, including other threads during a fill."""
+    import threading
+    from hipzap import lite
+    assert lite.upload_stream() is None
+    seen = {}
+    lite._fill_tls.stream = 0x1234
+    try:
+        t = threading.Thread(target=lambda: seen.setdefault("other", lite.upload_stream()))
+        t.start()
+        t.join()
+        seen["self"] = lite.upload_stream()
+    finally:
+        lite._fill_tls.stream = None
+    assert seen == {"other": None, "self": 0x1234}
+    assert lite.upload_stream() is None
