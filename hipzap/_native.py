@@ -17,7 +17,7 @@ DEBUG = os.environ.get("HIPZAP_DEBUG") == "1"
 _LIB_PATH = Path(__file__).resolve().parent / "_lib" / ("libhipzap_debug.so" if DEBUG else "libhipzap.so")
 if os.environ.get("HIPZAP_LIB"):  # same-box A/B of two builds (scripts/ab_lib.sh)
     _LIB_PATH = Path(os.environ["HIPZAP_LIB"]).resolve()
-DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch", "pack")
+DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch", "pack", "block")
 _lock = threading.Lock()
 _lib = None
 

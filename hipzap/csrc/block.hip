@@ -1,0 +1,416 @@
+// Fused ResNet-50 stages for bs=1 serving (VERDICT r3 "next round" 1): fewer, fatter dispatches.
+//
+// At bs=1 every conv of ResNet-50 is a ~5 us latency chain (launch ramp, operand round trips,
+// epilogue, end-of-kernel release) and the served rate is bounded by dispatches x that latency on
+// HIP's 4 hardware queues. These kernels remove dispatches WITHOUT any in-launch
+// cross-workgroup dependency (the persistent chain, profiles/r3_chain, lost to its fences): every
+// workgroup owns a spatial output tile and recomputes the 1-pixel halo it needs, so it never reads
+// another workgroup's output.
+//
+// * stem_kernel: image bytes (uint8 HWC, read zero-copy from the pinned request buffer) or fp32 NCHW
+//   -> normalise -> 7x7/2 conv + folded BN + ReLU -> 3x3/2 max-pool, one launch instead of three
+//   (preprocess, conv, maxpool). A workgroup computes a 9 x 17 patch of stem outputs (the 4 x 8
+//   pooled tile plus its halo) from a 23 x 39 input patch staged in LDS.
+// * bneck_kernel: one whole bottleneck block of layer1 (56 x 56, 64 mid channels): conv1 1x1 ->
+//   conv2 3x3 -> conv3 1x1 + residual (identity, or the downsample 1x1 computed into the same
+//   accumulators) + ReLU, one launch instead of three. A workgroup owns an 8 x 8 output tile:
+//   the 10 x 10 x Cin input patch goes to LDS, conv1 runs over the halo (zero outside the image,
+//   conv2's padding), conv2 and conv3 read their operands from LDS.
+//
+// Both read the SAME packed weights as the per-conv kernels (fragment-major [Cout/16][ksteps][64][8],
+// csrc/conv.hip), so plan images, templates and the device packer are unchanged. MFMA orientation
+// as conv.hip: A = weights (rows = output channels), B = activations (columns = pixels), so a lane's
+// accumulator is 4 consecutive channels of one pixel. LDS images are XOR-swizzled per 16-B chunk so
+// every B-fragment ds_read_b128 is conflict-free (checked with the lane-group model of
+// MI355X_MICROARCH.md § LDS for every read pattern below).
+#include "common.h"
+#include "hipzap.h"
+
+HZ_DEBUG_UNIT(block)
+
+namespace {
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 ldw(const bf16_t* w, int frag, int ksteps, int s, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + (((long)frag * ksteps + s) * 64 + lane) * 8);
+}
+
+// ------------------------------------------------------------------------------------------------
+// stem
+constexpr int kStemPH = 4, kStemPW = 8;                                  // pooled output tile
+constexpr int kStemSH = 2 * kStemPH + 1, kStemSW = 2 * kStemPW + 1;      // 9 x 17 stem outputs
+constexpr int kStemNP = kStemSH * kStemSW;                               // 153
+constexpr int kStemNF = (kStemNP + 15) / 16;                             // 10 pixel fragments
+constexpr int kStemIH = 2 * (kStemSH - 1) + 7, kStemIW = 2 * (kStemSW - 1) + 7;  // 23 x 39 input patch
+constexpr int kStemKS = 13;                                              // ceil(49 taps * 8 ch / 32)
+constexpr int kStemRawRow = 128;                                         // bytes per staged uint8 row
+
+__global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned raw[kStemIH * kStemRawRow / 4];  // uint8 rows (mode 1)
+  __shared__ __attribute__((aligned(16))) bf16_t img[kStemIH * kStemIW * 8];       // 8 ch / pixel, 3 real
+  __shared__ __attribute__((aligned(16))) bf16_t so[kStemNP * 64];                 // stem outputs, bf16
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tx_n = (p.PW + kStemPW - 1) / kStemPW, ty_n = (p.PH + kStemPH - 1) / kStemPH;
+  const int per_img = tx_n * ty_n;
+  const int b = blockIdx.x, n = b / per_img, rem = b - n * per_img;
+  const int ty = rem / tx_n, tx = rem - ty * tx_n;
+  const int py0 = ty * kStemPH, px0 = tx * kStemPW;
+  const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;  // stem-output origin of the patch
+  const int iy0 = 2 * sy0 - 3, ix0 = 2 * sx0 - 3;  // input origin
+
+  // ---- weights first (L2/MALL-resident, back before the input bytes cross PCIe): wave ->
+  // output-channel fragments {2cp, 2cp+1}, all 13 k-steps (26 x 16 B per lane) ----
+  const int cp = wave & 1, fgrp = wave >> 1;
+  bf16x8 wa[2][kStemKS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < kStemKS; ++s) wa[i][s] = ldw(p.w, 2 * cp + i, kStemKS, s, lane);
+  // ---- input patch (in zero-copy mode it is read straight from the pinned request buffer) ----
+  if (p.mode == 1) {
+    // per row: the dwords covering bytes [(row, c_lo), (row, c_hi)) of the HWC image. An image is a
+    // multiple of 4 bytes (launcher), so the rounded-up end never leaves the buffer.
+    const int c_lo = max(ix0, 0), c_hi = min(ix0 + kStemIW, p.W);
+    const unsigned* src = static_cast<const unsigned*>(p.src);
+    for (int q = tid; q < kStemIH * 32; q += 512) {
+      const int row = q >> 5, j = q & 31, iy = iy0 + row;
+      if ((unsigned)iy >= (unsigned)p.H || c_lo >= c_hi) continue;
+      const long rb = ((long)n * p.H + iy) * p.W;
+      const long d0 = ((rb + c_lo) * 3) >> 2, d1 = ((rb + c_hi) * 3 + 3) >> 2;
+      if (d0 + j < d1) raw[row * (kStemRawRow / 4) + j] = src[d0 + j];
+    }
+    __syncthreads();
+  }
+  // ---- normalised bf16 patch [23][39][8] (channels 3..7 and out-of-image pixels are zero) ----
+  for (int q = tid; q < kStemIH * kStemIW; q += 512) {
+    const int row = q / kStemIW, col = q - row * kStemIW;
+    const int iy = iy0 + row, ix = ix0 + col;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) {
+      if (p.mode == 1) {
+        const long rb = ((long)n * p.H + iy) * p.W;
+        const long d0 = ((rb + max(ix0, 0)) * 3) >> 2;
+        const int off = (int)((rb + ix) * 3 - d0 * 4);  // byte offset inside the staged row
+        const unsigned char* rr = reinterpret_cast<const unsigned char*>(raw) + row * kStemRawRow;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = (float)rr[off + c] * (1.0f / 255.0f);
+      } else {
+        const float* src = static_cast<const float*>(p.src);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = src[(((long)n * 3 + c) * p.H + iy) * p.W + ix];
+      }
+      if (p.norm) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = (v[c] - p.mean[c]) * p.inv_std[c];
+      }
+    }
+    *reinterpret_cast<u32x4*>(img + q * 8) = pack8(v);
+  }
+  __syncthreads();
+
+  // ---- 7x7/2 conv: wave -> pixel fragments fgrp, fgrp+4, fgrp+8 x channel fragments 2cp, 2cp+1 ----
+  // k-step s, lane group g = lane>>4: tap 4s+g = (r, c) of the 7x7 window, 8 channels (pack_conv
+  // cin_pad 8: k = (r*7 + c)*8 + ch) = one 16-B pixel of the LDS patch.
+  constexpr int FPW = (kStemNF + 3) / 4;  // 3
+  int poff[FPW];
+#pragma unroll
+  for (int fi = 0; fi < FPW; ++fi) {
+    const int j = min(16 * (fgrp + 4 * fi) + (lane & 15), kStemNP - 1);
+    const int ly = j / kStemSW, lx = j - ly * kStemSW;
+    poff[fi] = (2 * ly * kStemIW + 2 * lx) * 8;
+  }
+  f32x4 acc[FPW][2];
+#pragma unroll
+  for (int fi = 0; fi < FPW; ++fi) acc[fi][0] = acc[fi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < kStemKS; ++s) {
+    const int tap = 4 * s + g, tp = min(tap, 48);  // (taps >= 49: zero weights, operand zeroed below)
+    const int r = tp / 7, c = tp - 7 * r;
+    const int toff = (r * kStemIW + c) * 8;
+#pragma unroll
+    for (int fi = 0; fi < FPW; ++fi) {
+      if (fgrp + 4 * fi >= kStemNF) continue;  // wave-uniform
+      bf16x8 bv = *reinterpret_cast<const bf16x8*>(img + poff[fi] + toff);
+      if (tap >= 49) bv = bf16x8{};  // K padding: zero weights, but the LDS bytes need not be finite
+      acc[fi][0] = mfma16(wa[0][s], bv, acc[fi][0]);
+      acc[fi][1] = mfma16(wa[1][s], bv, acc[fi][1]);
+    }
+  }
+  // ---- bias + ReLU -> stem outputs in LDS (zero outside the stem image: the pool's padding) ----
+#pragma unroll
+  for (int fi = 0; fi < FPW; ++fi) {
+    const int j = 16 * (fgrp + 4 * fi) + (lane & 15);
+    if (fgrp + 4 * fi >= kStemNF || j >= kStemNP) continue;
+    const int ly = j / kStemSW, lx = j - ly * kStemSW;
+    const bool in = (unsigned)(sy0 + ly) < (unsigned)p.SH && (unsigned)(sx0 + lx) < (unsigned)p.SW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ch = 16 * (2 * cp + i) + 4 * g;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + ch);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][i][e] + bb[e], 0.f) : 0.f;
+      *reinterpret_cast<u32x2*>(so + j * 64 + ch) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  __syncthreads();
+  // ---- 3x3/2 max-pool (pad 1): every value is >= 0 after the ReLU and every window holds a real
+  // output, so the zeros written for out-of-image positions never win ----
+  {
+    const int q = tid >> 4, cg = tid & 15;  // pooled pixel (of 32), 4-channel group (of 16)
+    const int qy = q >> 3, qx = q & 7;
+    const int py = py0 + qy, px = px0 + qx;
+    if (py < p.PH && px < p.PW) {
+      float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int j = (2 * qy + dy) * kStemSW + 2 * qx + dx;
+          const u32x2 v = *reinterpret_cast<const u32x2*>(so + j * 64 + cg * 4);
+          m[0] = fmaxf(m[0], __uint_as_float(v[0] << 16));
+          m[1] = fmaxf(m[1], __uint_as_float(v[0] & 0xffff0000u));
+          m[2] = fmaxf(m[2], __uint_as_float(v[1] << 16));
+          m[3] = fmaxf(m[3], __uint_as_float(v[1] & 0xffff0000u));
+        }
+      const long o = ((((long)n * 2 + (cg >> 3)) * p.PH + py) * p.PW + px) * 32 + (cg & 7) * 4;
+      *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(m[0], m[1]), pack2(m[2], m[3])};
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bottleneck block (layer1 geometry: Cmid 64, Cout 256, stride 1)
+constexpr int kBnTH = 8, kBnTW = 8;                              // output tile
+constexpr int kBnHT = kBnTH + 2, kBnWT = kBnTW + 2;             // conv1 halo tile
+constexpr int kBnNP = kBnHT * kBnWT;                             // 100 halo pixels
+constexpr int kBnNF1 = (kBnNP + 15) / 16;                        // 7 fragments
+constexpr int kBnCM = 64, kBnCO = 256;
+
+// LDS images: [pixel][channels] bf16, 16-B chunks XOR-swizzled per pixel
+__device__ __forceinline__ int x_chunk(int p, int c, int nch) { return p * nch + (c ^ (p & (nch - 1))); }
+// conv1 output (read only by the 3x3 conv, whose 16 pixels are two 8-pixel rows of the halo tile)
+__device__ __forceinline__ int t1_chunk(int hy, int hx, int c) {
+  return (hy * kBnWT + hx) * 8 + (c ^ ((2 * hx + 2 * hy) & 7));
+}
+
+template <int CIN, bool DS>
+__global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
+  constexpr int XCH = CIN / 8;                       // 16-B chunks per input pixel
+  constexpr int KS1 = CIN / 32, KS2 = 9 * kBnCM / 32, KS3 = kBnCM / 32, KSD = CIN / 32;
+  constexpr int NQ = kBnNP * XCH, NL = (NQ + 511) / 512;
+  __shared__ __attribute__((aligned(16))) bf16_t X[kBnNP * CIN];
+  __shared__ __attribute__((aligned(16))) bf16_t T1[kBnNP * kBnCM];
+  __shared__ __attribute__((aligned(16))) bf16_t T2[kBnTH * kBnTW * kBnCM];
+  __shared__ __attribute__((aligned(16))) f32x4 RED[8][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int tx_n = p.W / kBnTW, ty_n = p.H / kBnTH, per_img = tx_n * ty_n;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = b / per_img, rem = b - n * per_img;
+  const int ty = rem / tx_n, tx = rem - ty * tx_n;
+  const int y0 = ty * kBnTH, x0 = tx * kBnTW;
+  const int CB = CIN / 32;
+
+  // ---- input patch loads (10 x 10 x Cin, zero outside the image); chunk order keeps a halo row of
+  // one 32-channel block contiguous in global memory ----
+  u32x4 xv[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    xv[i] = u32x4{0u, 0u, 0u, 0u};
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kBnNP, pp = pc - cb * kBnNP;
+      const int hy = pp / kBnWT, hx = pp - hy * kBnWT;
+      const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+      if ((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)
+        xv[i] = *reinterpret_cast<const u32x4*>(p.x + ((((long)n * CB + cb) * p.H + gy) * p.W + gx) * 32 + sub * 8);
+    }
+  }
+  // ---- every weight fragment this wave will use, issued up front (L2-resident across requests) ----
+  const int cf1 = wave & 3, fg1 = wave >> 2;  // conv1: channel fragment, pixel-fragment parity
+  const int cf2 = wave & 3, kh = wave >> 2;   // conv2: channel fragment, K half
+  bf16x8 a1[KS1], a2[KS2 / 2], a3[2][KS3], ad[2][DS ? KSD : 1];
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) a1[s] = ldw(p.w1, cf1, KS1, s, lane);
+#pragma unroll
+  for (int s = 0; s < KS2 / 2; ++s) a2[s] = ldw(p.w2, cf2, KS2, kh * (KS2 / 2) + s, lane);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < KS3; ++s) a3[i][s] = ldw(p.w3, 2 * wave + i, KS3, s, lane);
+  if constexpr (DS) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) ad[i][s] = ldw(p.wd, 2 * wave + i, KSD, s, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kBnNP, pp = pc - cb * kBnNP;
+      *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
+    }
+  }
+  __syncthreads();
+
+  // ---- conv1 (1x1, Cin -> 64) over the 100 halo pixels: wave -> fragments fg1, fg1+2, .. x cf1 ----
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) acc[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS1; ++s)
+#pragma unroll
+      for (int fi = 0; fi < 4; ++fi) {
+        const int f = fg1 + 2 * fi;
+        if (f >= kBnNF1) continue;  // wave-uniform
+        const int pp = min(16 * f + l16, kBnNP - 1);
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
+        acc[fi] = mfma16(a1[s], bv, acc[fi]);
+      }
+    const int ch = 16 * cf1 + 4 * g;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b1 + ch);
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      const int f = fg1 + 2 * fi, pp = 16 * f + l16;
+      if (f >= kBnNF1 || pp >= kBnNP) continue;
+      const int hy = pp / kBnWT, hx = pp - hy * kBnWT;
+      const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)p.H && (unsigned)(x0 - 1 + hx) < (unsigned)p.W;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][e] + bb[e], 0.f) : 0.f;  // conv2's zero padding
+      *reinterpret_cast<u32x2*>(T1 + t1_chunk(hy, hx, ch >> 3) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  __syncthreads();
+
+  // ---- conv2 (3x3, 64 -> 64): wave -> channel fragment cf2, K half kh (9 of 18 k-steps), all 4
+  // pixel fragments; the two halves meet through LDS (kh 0 finishes fragments 0-1, kh 1 2-3) ----
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS2 / 2; ++s) {
+      const int ks = kh * (KS2 / 2) + s;  // k-step: tap ks>>1 (r, c), channel half ks&1
+      const int tap = ks >> 1, r = tap / 3, c = tap - 3 * (tap / 3);
+      const int chunk = (ks & 1) * 4 + g;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int j = 16 * f + l16, hy = (j >> 3) + r, hx = (j & 7) + c;
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + t1_chunk(hy, hx, chunk) * 8);
+        acc[f] = mfma16(a2[s], bv, acc[f]);
+      }
+    }
+    const int give = kh ? 0 : 2, keep = kh ? 2 : 0;
+    RED[wave][0][lane] = acc[give];
+    RED[wave][1][lane] = acc[give + 1];
+    __syncthreads();
+    const int ch = 16 * cf2 + 4 * g;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + ch);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 o = RED[wave ^ 4][i][lane];
+      const int j = 16 * (keep + i) + l16;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[keep + i][e] + o[e] + bb[e], 0.f);
+      *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 8) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  __syncthreads();
+
+  // ---- conv3 (1x1, 64 -> 256) + residual (identity or the downsample 1x1 in the same
+  // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments ----
+  {
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS3; ++s)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int j = 16 * f + l16;
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 8) * 8);
+        acc[0][f] = mfma16(a3[0][s], bv, acc[0][f]);
+        acc[1][f] = mfma16(a3[1][s], bv, acc[1][f]);
+      }
+    if constexpr (DS) {
+#pragma unroll
+      for (int s = 0; s < KSD; ++s)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int j = 16 * f + l16, pp = ((j >> 3) + 1) * kBnWT + (j & 7) + 1;
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
+          acc[0][f] = mfma16(ad[0][s], bv, acc[0][f]);
+          acc[1][f] = mfma16(ad[1][s], bv, acc[1][f]);
+        }
+    }
+    const int CO32 = kBnCO / 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ch = 16 * (2 * wave + i) + 4 * g;
+      f32x4 bb = *reinterpret_cast<const f32x4*>(p.b3 + ch);
+      if constexpr (DS) bb += *reinterpret_cast<const f32x4*>(p.bd + ch);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int j = 16 * f + l16, jy = j >> 3, jx = j & 7;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][f][e] + bb[e];
+        if constexpr (!DS) {  // identity residual: the centre of the staged input patch (Cin == 256)
+          const int pp = (jy + 1) * kBnWT + jx + 1;
+          const u32x2 rr = *reinterpret_cast<const u32x2*>(X + x_chunk(pp, ch >> 3, XCH) * 8 + (ch & 4));
+          v[0] += __uint_as_float(rr[0] << 16);
+          v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+          v[2] += __uint_as_float(rr[1] << 16);
+          v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        const long o = ((((long)n * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
+        *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
+  const HzStemParams& p = *pp;
+  if (p.N < 1 || p.H < 8 || p.W < 8 || (p.mode != 0 && p.mode != 1)) return -1;
+  if (p.SH != (p.H + 6 - 7) / 2 + 1 || p.SW != (p.W + 6 - 7) / 2 + 1) return -1;  // 7x7/2 pad 3
+  if (p.PH != (p.SH + 2 - 3) / 2 + 1 || p.PW != (p.SW + 2 - 3) / 2 + 1) return -1;  // 3x3/2 pad 1
+  if (p.mode == 1 && ((long)p.H * p.W * 3) % 4) return -1;  // whole-dword image rows (see the kernel)
+  if (p.mode == 1 && ((uintptr_t)p.src & 3)) return -1;
+  const int tiles = ((p.PW + kStemPW - 1) / kStemPW) * ((p.PH + kStemPH - 1) / kStemPH) * p.N;
+  hipLaunchKernelGGL(stem_kernel, dim3(tiles), dim3(512), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
+  const HzBneckParams& p = *pp;
+  if (p.N < 1 || p.H % kBnTH || p.W % kBnTW || p.Cmid != kBnCM || p.Cout != kBnCO) return -1;
+  const int tiles = (p.H / kBnTH) * (p.W / kBnTW) * p.N;
+  if (p.Cin == 64 && p.wd && p.bd) hipLaunchKernelGGL((bneck_kernel<64, true>), dim3(tiles), dim3(512), 0, st, p);
+  else if (p.Cin == 256 && !p.wd) hipLaunchKernelGGL((bneck_kernel<256, false>), dim3(tiles), dim3(512), 0, st, p);
+  else return -1;
+  return (int)hipGetLastError();
+}
+
+// Load this translation unit's device code now (see hz_conv_code_warm, csrc/conv.hip).
+__global__ void hz_block_code_warm_kernel() {}
+extern "C" int hz_block_code_warm(void) {
+  hipFuncAttributes a;
+  return (int)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hz_block_code_warm_kernel));
+}

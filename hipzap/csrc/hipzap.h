@@ -397,11 +397,44 @@ typedef struct HzSoftmaxParams {
 } HzSoftmaxParams;
 int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t st);
 
+// ---- fused ResNet stages (csrc/block.hip; bs=1 dispatch count) ----
+// stem: image -> normalise -> 7x7/2 conv (packed like conv1: cin_pad 8, 13 k-steps) + bias + ReLU ->
+// 3x3/2 max-pool pad 1, channel-blocked output; one launch instead of preprocess + conv + maxpool
+typedef struct HzStemParams {
+  const void* src;            // uint8 NHWC [N][H][W][3] (mode 1) or fp32 NCHW [N][3][H][W] (mode 0)
+  const unsigned short* w;    // fragment-major [4][13][64][8], k = (r*7 + s)*8 + c
+  const float* bias;          // [64]
+  unsigned short* out;        // [N][2][PH][PW][32]
+  int N, H, W, mode;
+  int SH, SW, PH, PW;         // stem output / pooled sizes
+  int norm, pad_;             // norm: (x - mean) * inv_std (mode 1 scales bytes by 1/255 first)
+  float mean[4], inv_std[4];
+} HzStemParams;
+// one bottleneck block at layer1 geometry (Cmid 64, Cout 256, stride 1): conv1 1x1 -> conv2 3x3 ->
+// conv3 1x1 + residual (identity when wd == NULL, else the 1x1 downsample) + ReLU, each workgroup an
+// 8x8 output tile recomputing its conv1 halo; H, W multiples of 8
+typedef struct HzBneckParams {
+  const unsigned short* x;    // [N][Cin/32][H][W][32]
+  const unsigned short* w1;   // packed as the per-conv kernels (fragment-major, K order (r, s, c))
+  const float* b1;
+  const unsigned short* w2;
+  const float* b2;
+  const unsigned short* w3;
+  const float* b3;
+  const unsigned short* wd;   // downsample (Cin 64) or NULL (Cin 256, identity residual)
+  const float* bd;
+  unsigned short* out;        // [N][Cout/32][H][W][32]
+  int N, H, W, Cin, Cmid, Cout;
+} HzBneckParams;
+int hz_stem_launch(const HzStemParams* p, hipStream_t st);
+int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);
+int hz_block_code_warm(void);
+
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
-       HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17 };
+       HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17, HZ_K_STEM = 18, HZ_K_BNECK = 19 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);

@@ -32,7 +32,7 @@ constexpr uint32_t kPlanVersion = 1;
 // is filled by the caller, e.g. by packing a .pth checkpoint on the device (csrc/pack.hip)
 constexpr uint64_t kFlagWeightless = 1;
 constexpr char kMagic[8] = {'H', 'Z', 'P', 'L', 'A', 'N', '0', '1'};
-enum : unsigned { kUnitConv = 1, kUnitVision = 2, kUnitGemm = 4, kUnitTransformer = 8, kUnitFp8 = 16, kUnitPack = 32 };
+enum : unsigned { kUnitConv = 1, kUnitVision = 2, kUnitGemm = 4, kUnitTransformer = 8, kUnitFp8 = 16, kUnitPack = 32, kUnitBlock = 64 };
 
 // file header: magic + 15 little-endian u64 fields (see plan.py PlanHeader)
 struct FileHeader {
@@ -153,6 +153,8 @@ struct Plan {
             case HZ_K_MAXPOOL:
             case HZ_K_POOL_FC: u |= kUnitVision; break;
             case HZ_K_CONV_CHAIN: u |= kUnitConv; break;
+            case HZ_K_STEM:
+            case HZ_K_BNECK: u |= kUnitBlock; break;
             default: break;
           }
           break;
@@ -464,6 +466,8 @@ uint64_t hz_abi_version(void) {
                             sizeof(HzAvgpoolArgs),
                             sizeof(HzPreprocessArgs),
                             sizeof(HzMemcpyArgs),
+                            sizeof(HzStemParams),
+                            sizeof(HzBneckParams),
                             HZ_ABI_EPOCH};
   uint64_t x = 1469598103934665603ull;
   for (uint64_t v : parts) {
@@ -574,6 +578,7 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
       if (units & kUnitTransformer) (void)hz_transformer_code_warm();
       if (units & kUnitFp8) (void)hz_fp8_code_warm();
       if (units & kUnitPack) (void)hz_pack_code_warm();
+      if (units & kUnitBlock) (void)hz_block_code_warm();
     });
   }
   if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);

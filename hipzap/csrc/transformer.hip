@@ -416,6 +416,7 @@ extern "C" int hz_layernorm_launch(const HzLayerNormParams* pp, hipStream_t st) 
 extern "C" int hz_embed_ln_launch(const HzEmbedParams* pp, hipStream_t st) {
   const HzEmbedParams& p = *pp;
   if (p.D % 8 || p.D > 2048) return -1;
+  if (p.vocab < 1 || (p.types && p.ntypes < 1)) return -1;  // the id clamps need non-empty tables
   hipLaunchKernelGGL(embed_ln_kernel, dim3((p.rows + 3) / 4), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }

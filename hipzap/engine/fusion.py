@@ -1,0 +1,211 @@
+"""Bind-time fusion of ResNet stages into single launches (csrc/block.hip).
+
+The graph IR keeps one node per conv (the fp32 oracle, ``engine/reference.py``, interprets it
+unchanged); :class:`~hipzap.engine.program.ExecContext` asks :func:`plan` which node runs it may
+bind as ONE fused kernel instead:
+
+* ``stem``: preprocess -> conv1 (7x7/2, BN folded, ReLU) -> maxpool 3x3/2 -> ``hz_stem_launch``;
+* ``bneck``: a layer1-geometry bottleneck (1x1 Cin -> 64, 3x3 64 -> 64, 1x1 64 -> 256 + residual,
+  optionally with its 1x1 downsample) -> ``hz_bneck_launch``.
+
+Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
+fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
+(comma list of ``stem``, ``bneck``; ``none`` disables; default both) -- the A/B switch of
+``profiles/r4_fuse``. Reference: the per-conv contract these replace is SURVEY.md §2e N1/N2/N14.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .. import _native as N
+
+HZ_K_STEM, HZ_K_BNECK = 18, 19
+KINDS = ("stem", "bneck")
+
+
+class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
+    _fields_ = [("src", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("out", C.c_void_p),
+                ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
+                ("SH", C.c_int), ("SW", C.c_int), ("PH", C.c_int), ("PW", C.c_int),
+                ("norm", C.c_int), ("pad_", C.c_int), ("mean", C.c_float * 4), ("inv_std", C.c_float * 4)]
+
+
+class BneckParams(C.Structure):  # HzBneckParams
+    _fields_ = [("x", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p),
+                ("b2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("wd", C.c_void_p),
+                ("bd", C.c_void_p), ("out", C.c_void_p), ("N", C.c_int), ("H", C.c_int), ("W", C.c_int),
+                ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int)]
+
+
+@dataclass
+class Fused:
+    kind: str
+    start: int
+    end: int      # exclusive node index
+    nodes: list   # the graph nodes it replaces
+
+
+def enabled_kinds(spec: str | None = None) -> set:
+    v = os.environ.get("HIPZAP_FUSE", "stem,bneck") if spec is None else spec
+    v = v.strip().lower()
+    if v in ("", "0", "none", "off"):
+        return set()
+    if v in ("1", "all", "on"):
+        return set(KINDS)
+    return {k for k in v.split(",") if k in KINDS}
+
+
+def _conv(n, kind="conv"):
+    return n is not None and n.kind == kind
+
+
+def _geom(pc, cin, cout, k, stride, pad) -> bool:
+    return (pc.cin == cin and pc.cout == cout and pc.r == k and pc.s == k and pc.stride == stride
+            and pc.pad == pad)
+
+
+def match_stem(g, params, i: int) -> Fused | None:
+    nodes = g.nodes
+    if i + 3 > len(nodes):
+        return None
+    pre, cv, mp = nodes[i:i + 3]
+    if pre.kind != "preprocess" or not _conv(cv) or mp.kind != "maxpool":
+        return None
+    if cv.inputs != [pre.outputs[0]] or mp.inputs != [cv.outputs[0]] or len({pre.slot, cv.slot, mp.slot}) != 1:
+        return None
+    pc = params.get(cv.attrs.get("w"))
+    if pc is None or not _geom(pc, 8, 64, 7, 2, 3) or pc.ksteps != 13 or cv.attrs.get("act", "relu") != "relu":
+        return None
+    if cv.attrs.get("out_f32") or (mp.attrs.get("k"), mp.attrs.get("stride"), mp.attrs.get("pad")) != (3, 2, 1):
+        return None
+    src = g.tensors[pre.inputs[0]]
+    import torch
+    if src.dtype == torch.uint8:
+        if src.shape[-1] != 3 or (src.shape[1] * src.shape[2] * 3) % 4:
+            return None
+    elif src.dtype != torch.float32 or src.shape[1] != 3:
+        return None
+    return Fused("stem", i, i + 3, [pre, cv, mp])
+
+
+def match_bneck(g, params, i: int) -> Fused | None:
+    nodes = g.nodes
+    run = nodes[i:i + 4]
+    if len(run) < 3 or not all(_conv(n) for n in run[:3]):
+        return None
+    ds = None
+    if len(run) == 4 and _conv(run[3]) and run[0].inputs == run[1].inputs and len(run[0].inputs) == 1:
+        ds, c1, c2, c3 = run
+    else:
+        c1, c2, c3 = run[:3]
+    x = c1.inputs[0]
+    if len(c1.inputs) != 1 or c2.inputs != [c1.outputs[0]]:
+        return None
+    res = ds.outputs[0] if ds is not None else x
+    if c3.inputs != [c2.outputs[0], res]:
+        return None
+    grp = [n for n in (ds, c1, c2, c3) if n is not None]
+    if len({n.slot for n in grp}) != 1 or any(n.attrs.get("out_f32") or n.attrs.get("rowmajor") for n in grp):
+        return None
+    if any(n.attrs.get("act", "relu") != "relu" for n in (c1, c2, c3)):
+        return None
+    p1, p2, p3 = (params.get(n.attrs.get("w")) for n in (c1, c2, c3))
+    if p1 is None or p2 is None or p3 is None:
+        return None
+    cin = 64 if ds is not None else 256
+    if not (_geom(p1, cin, 64, 1, 1, 0) and _geom(p2, 64, 64, 3, 1, 1) and _geom(p3, 64, 256, 1, 1, 0)):
+        return None
+    if ds is not None:
+        pd = params.get(ds.attrs.get("w"))
+        if pd is None or not _geom(pd, 64, 256, 1, 1, 0) or ds.attrs.get("act", "relu") != "none":
+            return None
+    nb, h, w, c = g.shape(x)
+    if c != cin or h % 8 or w % 8:
+        return None
+    return Fused("bneck", i, i + len(grp), grp)
+
+
+def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
+    """{first node index: Fused} for every fusible run of ``g`` (non-overlapping, in order)."""
+    kinds = enabled_kinds() if kinds is None else kinds
+    out: dict[int, Fused] = {}
+    if not kinds:
+        return out
+    i = 0
+    while i < len(g.nodes):
+        f = None
+        if "stem" in kinds:
+            f = match_stem(g, params, i)
+        if f is None and "bneck" in kinds:
+            f = match_bneck(g, params, i)
+        if f is not None:
+            out[i] = f
+            i = f.end
+        else:
+            i += 1
+    return out
+
+
+def stem_params(g, params, f: Fused, addr) -> StemParams:
+    pre, cv, mp = f.nodes
+    import torch
+    src = g.tensors[pre.inputs[0]]
+    pc = params[cv.attrs["w"]]
+    p = StemParams()
+    p.src, p.w, p.bias, p.out = addr(pre.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), addr(mp.outputs[0])
+    if src.dtype == torch.uint8:
+        p.N, p.H, p.W, _ = src.shape
+        p.mode = 1
+    else:
+        p.N, _, p.H, p.W = src.shape
+        p.mode = 0
+    _, p.SH, p.SW, _ = g.shape(cv.outputs[0])
+    _, p.PH, p.PW, _ = g.shape(mp.outputs[0])
+    mean, std = pre.attrs.get("mean"), pre.attrs.get("std")
+    p.norm = int(mean is not None)
+    if mean is not None:
+        # the same float32 constants as the standalone preprocess kernel (inv_std = 1/std in fp32)
+        inv = (np.float32(1.0) / np.asarray(std, dtype=np.float32)).astype(np.float32)
+        for c in range(3):
+            p.mean[c] = float(np.float32(mean[c]))
+            p.inv_std[c] = float(inv[c])
+    return p
+
+
+def bneck_params(g, params, f: Fused, addr) -> BneckParams:
+    grp = f.nodes
+    ds = grp[0] if len(grp) == 4 else None
+    c1, c2, c3 = grp[-3:]
+    p1, p2, p3 = (params[n.attrs["w"]] for n in (c1, c2, c3))
+    p = BneckParams()
+    p.x, p.out = addr(c1.inputs[0]), addr(c3.outputs[0])
+    p.w1, p.b1 = p1.wf.data_ptr(), p1.bias.data_ptr()
+    p.w2, p.b2 = p2.wf.data_ptr(), p2.bias.data_ptr()
+    p.w3, p.b3 = p3.wf.data_ptr(), p3.bias.data_ptr()
+    if ds is not None:
+        pd = params[ds.attrs["w"]]
+        p.wd, p.bd = pd.wf.data_ptr(), pd.bias.data_ptr()
+    p.N, p.H, p.W, p.Cin = g.shape(c1.inputs[0])
+    p.Cmid, p.Cout = p1.cout, p3.cout
+    return p
+
+
+def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
+    """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
+    if f.kind == "stem":
+        prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
+    else:
+        prm, kind = bneck_params(g, params, f, addr), HZ_K_BNECK
+    N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(prm), C.sizeof(prm), f.nodes[0].slot), f"add_{f.kind}")
+    names = "+".join(str(n.attrs.get("name", n.kind)) for n in f.nodes)
+    return (names, f"fused:{f.kind}", -1, 0)
+
+
+def launch(kind: str, prm, stream=None) -> None:
+    """Eager launch of a fused kernel (tests)."""
+    k = HZ_K_STEM if kind == "stem" else HZ_K_BNECK
+    N.check(N.lib().hz_launch_kernel(k, C.byref(prm), N.stream_ptr(stream)), f"launch_{kind}")

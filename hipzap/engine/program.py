@@ -18,6 +18,7 @@ from ..ops import conv as conv_ops
 from ..ops import fp8
 from ..ops import transformer as tx
 from ..ops import vision
+from . import fusion
 from .graph import Graph, plan_memory
 
 
@@ -49,10 +50,11 @@ def _ln_folded(n) -> bool:
 class ExecContext:
     def __init__(self, g: Graph, params: dict, device: torch.device, tuned: dict | None = None,
                  host_io: bool = False, pair_convs: bool | None = None, zero_copy: str | None = None,
-                 lib=None):
+                 lib=None, fuse: str | None = None):
         """``lib``: the native library (default) or a recorder with the same ``hz_prog_add_*``
         surface (engine/plan.py ``PlanRecorder``: binds against CPU tensors and serialises the
-        program as a plan image instead of launching it)."""
+        program as a plan image instead of launching it). ``fuse``: which ResNet stage fusions to
+        bind (engine/fusion.py; default: env ``HIPZAP_FUSE``, else all)."""
         self.graph = g
         self.recording = lib is not None and getattr(lib, "recording", False)
         self.device = torch.device(device)
@@ -141,9 +143,18 @@ class ExecContext:
         self.pairs = conv_pairs(g) if pair_convs else {}
         chain = self._chain_range(os.environ.get("HIPZAP_CONV_CHAIN", ""))
         self.chain_sync = None
+        # fused ResNet stages (engine/fusion.py, csrc/block.hip): runs of nodes bound as ONE launch
+        self.fused = fusion.plan(g, params, fusion.enabled_kinds(fuse) if fuse is not None else None)
+        if chain is not None:
+            self.fused = {k: f for k, f in self.fused.items() if f.end <= chain[0]}
         i = 0
         while i < len(g.nodes):
             n = g.nodes[i]
+            if i in self.fused:
+                f = self.fused[i]
+                self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib))
+                i = f.end
+                continue
             if chain is not None and i == chain[0]:
                 self._add_conv_chain(lib, chain[0], chain[1], conv_plans)
                 i = chain[1]

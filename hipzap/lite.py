@@ -231,6 +231,11 @@ class PlanEngine:
             want = (e["cout"], e["cin"]) if e["kind"] == "linear" else (e["cout"], e["cin"], e["r"], e["s"])
             if tuple(src["w"].shape) != want:
                 raise PlanError(f"{ckpt}: {e['w']} is {src['w'].shape}, template expects {want}")
+            # the pack kernel reads cout elements of every BN vector and of the bias: a short one
+            # would read into the next staged tensor (or past the staging buffer)
+            for f, r in src.items():
+                if f != "w" and tuple(r.shape) != (e["cout"],):
+                    raise PlanError(f"{ckpt}: {keys[f]} is {tuple(r.shape)}, template expects ({e['cout']},)")
             jobs.append((name, e, src))
         stores = {}
         for _, _, src in jobs:

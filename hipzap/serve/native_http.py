@@ -94,6 +94,7 @@ class NativeHTTPServer:
         eng = backend.engine
         b, h, w, c = backend.in_shape
         self._exec = ex  # keep alive
+        self._fast_engine = eng
         out = eng.out_spec
         rc = N.lib().hz_http_set_fast(self._h, ex._h, h, w, c, out["bytes"] // b // 4, int(backend.num_labels),
                                       int(backend.probs), backend.name.encode())
@@ -135,6 +136,13 @@ class NativeHTTPServer:
         h, self._h = getattr(self, "_h", None), None
         self._stopped.set()
         if h and not N.lib().hz_http_stop(h):
-            # a connection thread is still live and may be inside the executor: never free it
-            _LEAKED.append(getattr(self, "_exec", None))
-            log.warning("native http: connections still open at stop; executor kept alive")
+            # a connection thread is still live and may be inside the executor: never free it, nor
+            # the plan whose contexts and pinned slots it submits to. Disarm both handles so a later
+            # engine close() (PlanEngine.close -> ex.close, hz_plan_close) cannot destroy them.
+            ex, eng = getattr(self, "_exec", None), getattr(self, "_fast_engine", None)
+            if ex is not None:
+                ex._h = None
+            if eng is not None and hasattr(eng, "_h"):
+                eng._h = None
+            _LEAKED.append((ex, eng))
+            log.warning("native http: connections still open at stop; executor and plan kept alive")

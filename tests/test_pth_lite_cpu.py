@@ -206,3 +206,20 @@ def test_upload_stream_only_inside_a_fill():
         lite._fill_tls.stream = None
     assert seen == {"other": None, "self": 0x1234}
     assert lite.upload_stream() is None
+
+
+@pytest.mark.parametrize("key", ["bn1.weight", "layer1.0.bn2.running_var", "fc.bias"])
+def test_from_checkpoint_refuses_short_vectors(tmp_path, key):
+    """Every BN vector and bias the device packer reads must hold exactly cout elements: a short
+    one (which still fits its own storage) is refused before anything is uploaded, instead of the
+    pack kernel reading the next staged tensor."""
+    from hipzap import lite
+    if not os.path.exists(lite.template_path("resnet18")):
+        pytest.skip("resnet18 template not built")
+    torch.manual_seed(0)
+    sd = randomize_bn(resnet18()).eval().state_dict()
+    sd[key] = sd[key][:10].clone()
+    p = str(tmp_path / "short.pth")
+    torch.save(sd, p)
+    with pytest.raises(lite.PlanError, match=key.replace(".", r"\.")):
+        lite.PlanEngine.from_checkpoint(p)
