@@ -5,6 +5,9 @@
     python -m hipzap.coldstart hzpack <ckpt.pth> --model resnet50        packed safetensors path
     python -m hipzap.coldstart pth-lite <ckpt.pth>                       the .pth without torch:
         weights-only zip reader + plan template + device-side packing (PlanEngine.from_checkpoint)
+    python -m hipzap.coldstart lm <ckpt.pth> [--vocab itos.pkl]          GET /inference without torch:
+        AWD-LSTM .pth -> raw upload -> device packing -> batched decode engine (hipzap/lmlite.py),
+        then one 200-word response (the reference's request, main.py:84-112)
 
 ``measure_fresh("native", plan)`` spawns the Python-free ``hipzap-serve-plan PLAN --once IMAGE``
 (csrc/tools/serve_plan.cpp) instead: exec -> HIP init -> plan upload -> one eager request.
@@ -66,6 +69,31 @@ def run_pth_lite(ckpt: str, device: int) -> dict:
                           "engine_total": (t_ready - t_lib) * 1e3, "first_request": (t_first - t_ready) * 1e3}}
 
 
+def run_lm(ckpt: str, device: int, vocab: str | None, words: int = 200) -> dict:
+    t_imp = time.time()
+    from hipzap.lmlite import LMLiteEngine
+    from hipzap.serve.text import load_itos, make_stoi
+    t_lib = time.time()
+    if vocab:
+        itos = load_itos(vocab)
+    else:  # ids as words (the checkpoint's vocabulary size is read from the file)
+        from hipzap.pthreader import scan
+        itos = [f"w{i}" for i in range(scan(ckpt)["0.encoder.weight"].shape[0])]
+    stoi = make_stoi(itos)
+    t_vocab = time.time()
+    eng = LMLiteEngine.for_vocab(ckpt, stoi, device=device)
+    t_ready = time.time()
+    text = eng.generate([""], words, itos, stoi, seed=1)
+    t_first = time.time()
+    return {"mode": "lm", "t_first": t_first, "ok": len(text.split()) >= words // 2, "words": words,
+            "torch_imported": "torch" in sys.modules, "numpy_imported": "numpy" in sys.modules,
+            "vocab": eng.V, "decode_ms": eng.last_latency_ms,
+            "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3, "import_lmlite": (t_lib - t_imp) * 1e3,
+                          "vocab_ms": (t_vocab - t_lib) * 1e3,
+                          **{k: round(v, 3) for k, v in eng.timings.items()},
+                          "engine_total": (t_ready - t_vocab) * 1e3, "first_response": (t_first - t_ready) * 1e3}}
+
+
 def run_torch(ckpt: str, model: str, device: int, packed: bool) -> dict:
     t_imp = time.time()
     import torch
@@ -103,7 +131,7 @@ def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:
 
 
 def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5, device: int = 0,
-                  timeout: float = 300.0, env: dict | None = None) -> dict:
+                  timeout: float = 300.0, env: dict | None = None, extra_args: list | None = None) -> dict:
     """Spawn ``trials`` fresh processes of this module; p50/min/max of spawn -> first logits and
     the child-reported phases of the median trial. Raises if any child fails."""
     import statistics
@@ -123,7 +151,8 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
             f.write(os.urandom(nbytes))
         cmd = [exe, path, "--once", img, "--device", str(device)]
     else:
-        cmd = [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device)]
+        cmd = [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device),
+               *(extra_args or [])]
     for _ in range(trials):
         t = time.time()
         r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout, env=env)
@@ -139,21 +168,25 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
             "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2),
             "all_ms": [round(w, 1) for w in walls],
             "median_trial_phases_ms": {k: round(v, 2) for k, v in med["phases_ms"].items()},
-            "torch_imported": med.get("torch_imported", mode not in ("plan", "native", "pth-lite"))}
+            "torch_imported": med.get("torch_imported", mode not in ("plan", "native", "pth-lite", "lm"))}
 
 
 def main(argv=None) -> int:
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite"])
+    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite", "lm"])
     ap.add_argument("path")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--vocab", default=None, help="lm mode: the pickled itos list")
+    ap.add_argument("--words", type=int, default=200, help="lm mode: words to generate")
     a = ap.parse_args(argv)
     if a.mode == "plan":
         res = run_plan(a.path, a.device)
     elif a.mode == "pth-lite":
         res = run_pth_lite(a.path, a.device)
+    elif a.mode == "lm":
+        res = run_lm(a.path, a.device, a.vocab, a.words)
     else:
         res = run_torch(a.path, a.model, a.device, packed=a.mode == "hzpack")
     res["t_interp"] = T0

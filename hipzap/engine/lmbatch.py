@@ -25,6 +25,7 @@ import math
 import torch
 
 from .. import _native as N
+from . import lmcore
 from ..serve.text import EXCLUDE_TOKENS, Detokenizer
 from .lm import _interleave
 
@@ -143,73 +144,61 @@ def _lmb_layers(sd: dict) -> list:
 
 
 def _pack_lmb_native(sd: dict, dev: torch.device) -> dict:
-    """pack_lmb's layout written by csrc/pack.hip (see pack_lmb); same checks, same bytes."""
-    if any(k.endswith("_reverse") for k in sd):
-        raise ValueError("bidirectional AWD-LSTM cannot drive token-by-token generation")
-    emb_src = sd["0.encoder.weight"]
-    V, E = emb_src.shape
-    Ke = _pad(E, 256)
-    if Ke > 1024:
-        raise ValueError(f"batched decode supports embedding widths <= 1024 (got {E})")
-    raw = _lmb_layers(sd)
-    if not raw:
-        raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
-    if len(raw) > 4:
-        raise ValueError("batched decode supports up to 4 layers")
-    if raw[0][4] != E or raw[-1][5] != E:
-        raise ValueError("batched decode needs layer 0 input and last hidden size = embedding width (tied model)")
-
-    def dev32(t):  # raw fp32 device copy (one H2D; a dtype conversion only for non-fp32 checkpoints)
-        t = t.to(dev, non_blocking=True)
-        return (t if t.dtype == torch.float32 else t.float()).contiguous()
-
-    lib = N.lib()
-    st = N.stream_ptr()
-
-    def launch(**kw):
-        p = N.FragPackParams()
-        for k, v in kw.items():
-            setattr(p, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
-        N.check(lib.hz_frag_pack_launch(C.byref(p), st), "hz_frag_pack_launch")
-
-    layers = []
-    for i, (w_ih, w_hh, b_ih, b_hh, n_in, H) in enumerate(raw):
-        Kh = Ke if i == len(raw) - 1 else _pad(H, 32)
-        Kx = Ke if i == 0 else layers[-1]["Kh"]
-        R = _pad(4 * H, 16)
-        if (Kh + Kx) // 32 > 72:
-            raise ValueError(f"layer {i}: K = {Kh + Kx} exceeds the batched kernel's 2304")
-        a, b, ba, bb = dev32(w_hh), dev32(w_ih), dev32(b_ih), dev32(b_hh)
-        w = torch.empty(R // 16, (Kh + Kx) // 32, 64, 8, dtype=torch.bfloat16, device=dev)
-        bias = torch.empty(R, dtype=torch.float32, device=dev)
-        launch(a=a, b=b, out=w, bias_a=ba, bias_b=bb, bias_out=bias, R=R, K=Kh + Kx, nrows=4 * H, interleave_h=H,
-               ka=Kh, acols=H, lda=H, bcols=n_in, ldb=n_in)
-        layers.append({"w": w, "bias": bias, "H": H, "In": n_in, "Kh": Kh, "Kx": Kx, "R": R, "_src": (a, b, ba, bb)})
-    Vp = _pad(V, 16)
-    emb = dev32(emb_src)
-
-    def pack_vocab(m):
-        t = torch.empty(Vp // 16, Ke // 32, 64, 8, dtype=torch.bfloat16, device=dev)
-        launch(a=m, out=t, R=Vp, K=Ke, nrows=V, ka=Ke, acols=E, lda=E)
-        return t
-
-    embp = pack_vocab(emb)
+    """pack_lmb's layout written by csrc/pack.hip through the torch-free core (engine/lmcore.py
+    ``pack``, shared with the .pth-lite engine hipzap/lmlite.py); same checks, same bytes."""
+    emb_src = sd.get("0.encoder.weight")
     dec_w = sd.get("1.decoder.weight")
-    tied = dec_w is None or (dec_w.device == emb_src.device and dec_w.data_ptr() == emb_src.data_ptr()
-                             and dec_w.shape == emb_src.shape and dec_w.stride() == emb_src.stride())
-    dec = None
+    tied = dec_w is None or emb_src is None or (
+        dec_w.device == emb_src.device and dec_w.data_ptr() == emb_src.data_ptr()
+        and dec_w.shape == emb_src.shape and dec_w.stride() == emb_src.stride())
+    srcs: dict = {}
+
+    def dev32(k):  # raw fp32 device copy (one H2D; a dtype conversion only for non-fp32 checkpoints)
+        if k not in srcs:
+            t = sd[k].to(dev, non_blocking=True)
+            srcs[k] = (t if t.dtype == torch.float32 else t.float()).contiguous()
+        return srcs[k]
+
     if not tied:
-        dec = dev32(dec_w)
-        tied = torch.equal(dec, emb)
-    decp = embp if tied else pack_vocab(dec)
-    dec_b = sd.get("1.decoder.bias")
-    dbias = dev32(dec_b) if dec_b is not None else None
-    bias = torch.empty(Vp, dtype=torch.float32, device=dev)
-    launch(bias_a=dbias if dbias is not None else 0, bias_out=bias, R=Vp, K=32, nrows=V, ka=32)
+        tied = torch.equal(dev32("1.decoder.weight"), dev32("0.encoder.weight"))
+    geo = lmcore.geometry({k: tuple(v.shape) for k, v in sd.items() if hasattr(v, "shape")}, tied=tied)
+    layers = []
+    for ly in geo.layers:
+        w = torch.empty(ly.R // 16, (ly.Kh + ly.Kx) // 32, 64, 8, dtype=torch.bfloat16, device=dev)
+        layers.append({"w": w, "bias": torch.empty(ly.R, dtype=torch.float32, device=dev), "H": ly.H, "In": ly.In,
+                       "Kh": ly.Kh, "Kx": ly.Kx, "R": ly.R})
+    vocab = lambda: torch.empty(geo.Vp // 16, geo.Ke // 32, 64, 8, dtype=torch.bfloat16, device=dev)  # noqa: E731
+    embp = vocab()
+    decp = embp if geo.dec_key is None else vocab()
+    bias = torch.empty(geo.Vp, dtype=torch.float32, device=dev)
+    dst = {"layers": [(ly["w"].data_ptr(), ly["bias"].data_ptr()) for ly in layers], "emb": embp.data_ptr(),
+           "dec": decp.data_ptr(), "dec_bias": bias.data_ptr()}
+    lmcore.pack(geo, lambda k: dev32(k).data_ptr() if k else 0, dst, N.stream_ptr())
     torch.cuda.current_stream(dev).synchronize()  # the fp32 sources are released on return
-    for ly in layers:
-        del ly["_src"]
-    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": bias, "V": V, "Vp": Vp, "E": E, "Ke": Ke}
+    return {"layers": layers, "emb": embp, "dec": decp, "dec_bias": bias, "V": geo.V, "Vp": geo.Vp, "E": geo.E,
+            "Ke": geo.Ke}
+
+
+class _TorchAlloc:
+    """lmcore allocator over torch tensors (zero-filled device / pinned host bytes)."""
+
+    def __init__(self, dev: torch.device):
+        self.dev, self.keep = dev, []
+
+    def device(self, nbytes: int) -> int:
+        t = torch.zeros(max(1, nbytes), dtype=torch.uint8, device=self.dev)
+        self.keep.append(t)
+        return t.data_ptr()
+
+    def pinned(self, nbytes: int) -> int:
+        t = torch.zeros(max(1, nbytes), dtype=torch.uint8, pin_memory=True)
+        self.keep.append(t)
+        return t.data_ptr()
+
+
+def geometry_of(packed: dict) -> lmcore.LmbGeometry:
+    layers = [lmcore.LmbLayer(ly["H"], ly["In"], ly["Kh"], ly["Kx"], ly["R"], ()) for ly in packed["layers"]]
+    return lmcore.LmbGeometry(layers, packed["V"], packed["E"], packed["Ke"], packed["Vp"], None, None)
 
 
 class LMBatchEngine:
@@ -220,75 +209,21 @@ class LMBatchEngine:
 
     def __init__(self, packed: dict, device="cuda:0", rows: int = 32, unroll: int = 8, exclude_ids=(),
                  max_words: int = 1024, record_logits: bool = False, capture: bool = True):
-        if rows not in (16, 32):
-            raise ValueError("rows must be 16 or 32")
-        if not 1 <= unroll <= 32:
-            raise ValueError("unroll must be in 1..32")
         self.p = packed
         self.device = torch.device(device)
-        self.rows, self.unroll, self.max_words = rows, unroll, max_words
         self.V = packed["V"]
-        lib = N.lib()
-        dev, Bp, U = self.device, rows, unroll
-        L = packed["layers"]
-        with torch.cuda.device(dev):
-            self.stream = torch.cuda.Stream(dev)
-            self.h = [torch.zeros(4 * ly["Kh"] * Bp, dtype=torch.int16, device=dev) for ly in L]
-            self.c = [torch.zeros(Bp * ly["H"], device=dev) for ly in L]
-            self.gpar = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.ctl = torch.zeros(U * Bp * 4, dtype=torch.int32, device=dev)
-            self.seed = torch.zeros(Bp, dtype=torch.int64, device=dev)
-            self.outp = torch.zeros(Bp, dtype=torch.int64, device=dev)
-            self.nblk = lib.hz_lmb_dec_blocks(self.V)
-            self.dbest = torch.zeros(2 * Bp, dtype=torch.int64, device=dev)  # [parity][row]
-            self.tok = torch.zeros(Bp, dtype=torch.int32, device=dev)
-            self.block = torch.zeros(8 + Bp * (8 + 4 * U), dtype=torch.int32, pin_memory=True)
-            self.out_pool = torch.zeros(Bp * max_words, dtype=torch.int32, pin_memory=True)
-            self.logits = torch.zeros(Bp * self.V, dtype=torch.float32, pin_memory=True) if record_logits else None
-            ex = [int(e) for e in exclude_ids][:8]
-
-            a = N.LmbAdmitParams()
-            a.block, a.ctl, a.seed, a.outp, a.gpar = (self.block.data_ptr(), self.ctl.data_ptr(),
-                                                      self.seed.data_ptr(), self.outp.data_ptr(), self.gpar.data_ptr())
-            a.Bp, a.U, a.n_layers = Bp, U, len(L)
-            for i, ly in enumerate(L):
-                a.h[i], a.c[i], a.Kh[i], a.H[i] = self.h[i].data_ptr(), self.c[i].data_ptr(), ly["Kh"], ly["H"]
-            layer_prms = []
-            for i, ly in enumerate(L):
-                q = N.LmbLayerParams()
-                q.w, q.bias, q.h, q.c = ly["w"].data_ptr(), ly["bias"].data_ptr(), self.h[i].data_ptr(), self.c[i].data_ptr()
-                q.x = 0 if i == 0 else self.h[i - 1].data_ptr()
-                q.gpar, q.ctl = self.gpar.data_ptr(), self.ctl.data_ptr()
-                q.H, q.Kh, q.Kx, q.R, q.Bp = ly["H"], ly["Kh"], ly["Kx"], ly["R"], Bp
-                if i == 0:
-                    q.emb, q.dbest, q.V = packed["emb"].data_ptr(), self.dbest.data_ptr(), self.V
-                    q.outp, q.tok = self.outp.data_ptr(), self.tok.data_ptr()
-                layer_prms.append(q)
-            d = N.LmbDecParams()
-            d.w, d.bias, d.h = packed["dec"].data_ptr(), packed["dec_bias"].data_ptr(), self.h[-1].data_ptr()
-            d.gpar, d.ctl, d.seed, d.dbest = self.gpar.data_ptr(), self.ctl.data_ptr(), self.seed.data_ptr(), self.dbest.data_ptr()
-            d.logits = self.logits.data_ptr() if self.logits is not None else 0
-            d.V, d.Vp, d.K, d.Bp, d.nblk = self.V, packed["Vp"], L[-1]["Kh"], Bp, self.nblk
-            d.n_exclude = len(ex)
-            for i, e in enumerate(ex):
-                d.exclude[i] = e
-            self._ops = [(N.HZ_K_LMB_LAYER, q) for q in layer_prms] + [(N.HZ_K_LMB_DEC, d)]
-            prog = lib.hz_prog_create()
-            N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(a), C.sizeof(a), 0), "add lmb admit")
-            for u in range(U):
-                for kind, prm in self._ops:
-                    q = type(prm).from_buffer_copy(prm)
-                    q.step_off = u
-                    N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
-            self._admit = a
-            self.prog = prog
-            if capture:
-                N.check(lib.hz_prog_capture(prog, self.stream.cuda_stream), "capture lmb")
-            torch.cuda.synchronize(dev)
-        self._sched = lib.hz_lmb_create(prog, self.stream.cuda_stream, self.block.data_ptr(), Bp, U, 0, max_words,
-                                        self.out_pool.data_ptr(), d.logits, self.V)
-        if not self._sched:
-            raise RuntimeError("hz_lmb_create failed")
+        with torch.cuda.device(self.device):
+            self.stream = torch.cuda.Stream(self.device)
+            self._alloc = _TorchAlloc(self.device)
+            w = {"layers": [(ly["w"].data_ptr(), ly["bias"].data_ptr()) for ly in packed["layers"]],
+                 "emb": packed["emb"].data_ptr(), "dec": packed["dec"].data_ptr(),
+                 "dec_bias": packed["dec_bias"].data_ptr()}
+            self.core = lmcore.LmbCore(geometry_of(packed), w, self._alloc, self.stream.cuda_stream, rows=rows,
+                                       unroll=unroll, exclude_ids=exclude_ids, max_words=max_words,
+                                       record_logits=record_logits, capture=capture)
+            torch.cuda.synchronize(self.device)
+        self.rows, self.unroll, self.max_words = rows, unroll, max_words
+        self._ops = self.core._ops
 
     @classmethod
     def from_state_dict(cls, sd: dict, device="cuda:0", **kw) -> "LMBatchEngine":
@@ -302,26 +237,12 @@ class LMBatchEngine:
     def run_tokens(self, prompt_ids: list, n_words: int, seed: int = 0, logits: bool = False):
         """Feed ``prompt_ids``, sample ``n_words`` tokens; returns the sampled ids (and, with
         ``logits``, the fp32 logits after the last prompt token)."""
-        P = len(prompt_ids)
-        if P < 1:
-            raise ValueError("need at least one prompt token")
-        if not 1 <= n_words <= self.max_words:
-            raise ValueError(f"n_words must be in 1..{self.max_words}")
-        if logits and self.logits is None:
-            raise ValueError("engine built without record_logits")
-        prompt = (C.c_int * P)(*[int(t) for t in prompt_ids])
-        out = (C.c_int * n_words)()
-        lg = (C.c_float * self.V)() if logits else None
-        lat = C.c_double()
-        rc = N.lib().hz_lmb_submit(self._sched, prompt, P, n_words, int(seed) & ((1 << 62) - 1), out,
-                                   lg, C.byref(lat))
-        if rc:
-            raise RuntimeError(f"batched decode request failed ({rc})")
-        self.last_latency_ms = lat.value / 1e3
-        toks = list(out)
+        r = self.core.run_tokens(prompt_ids, n_words, seed, logits)
+        self.last_latency_ms = self.core.last_latency_ms
         if logits:
+            toks, lg = r
             return toks, torch.frombuffer(bytearray(lg), dtype=torch.float32)
-        return toks
+        return r
 
     def generate(self, prompt_words, n_words, itos, stoi, seed=None) -> str:
         ids = [stoi.get(w, 0) for w in prompt_words]
@@ -336,21 +257,9 @@ class LMBatchEngine:
         return det.text
 
     def stats(self) -> dict:
-        a = (C.c_uint64 * 4)()
-        N.lib().hz_lmb_stats(self._sched, a)
-        return {"replays": a[0], "served": a[1], "row_steps_used": a[2], "row_steps": a[3],
-                "row_utilisation": round(a[2] / a[3], 4) if a[3] else None}
+        return self.core.stats()
 
     def close(self) -> None:
-        s, self._sched = getattr(self, "_sched", None), None
-        if s:
-            N.lib().hz_lmb_destroy(s)
-        prog, self.prog = getattr(self, "prog", None), None
-        if prog:
-            N.lib().hz_prog_destroy(prog)
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        core = getattr(self, "core", None)
+        if core is not None:
+            core.close()

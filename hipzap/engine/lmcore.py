@@ -1,0 +1,259 @@
+"""Torch-free core of the batched AWD-LSTM decode engine (csrc/lmbatch.hip + csrc/lmserve.cpp).
+
+Everything the batched engine does between "the fp32 weights are on the device" and "a request
+gets its tokens" is plain pointers and ctypes: the packing launches (csrc/pack.hip
+``hz_frag_pack_launch``), the decode program (admit kernel + ``unroll`` x (layers, decoder)),
+its hipGraph capture and the native row scheduler. Two front ends share it:
+
+* ``engine/lmbatch.py`` :class:`LMBatchEngine` -- torch tensors as storage (the state_dict path);
+* ``hipzap/lmlite.py`` :class:`LMLiteEngine` -- the reference's ``.pth`` read by the weights-only
+  zip reader and uploaded raw (``hz_upload_file``), HIP allocations through ctypes: the
+  ``GET /inference`` cold start without ``import torch`` (VERDICT r3 "next round" 2).
+
+Checkpoint rules (/root/reference/pytorch_models/awd_lstm.py:140-168): the
+effective recurrent weight is ``module.weight_hh_l0`` (loaded after ``weight_hh_l0_raw`` into the
+shared storage), ``_raw`` only when the module key is absent; the decoder is tied to the encoder
+embedding when ``1.decoder.weight`` is absent or is the same tensor.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+
+from .. import _native as N
+
+
+def _pad(n: int, m: int) -> int:
+    return int(math.ceil(n / m) * m)
+
+
+@dataclass
+class LmbLayer:
+    H: int
+    In: int
+    Kh: int
+    Kx: int
+    R: int
+    keys: tuple  # (w_ih, w_hh, b_ih, b_hh) state_dict keys
+
+
+@dataclass
+class LmbGeometry:
+    layers: list
+    V: int
+    E: int
+    Ke: int
+    Vp: int
+    dec_key: str | None   # untied decoder weight key (None: tied to the embedding)
+    dec_bias_key: str | None
+    extra: dict = field(default_factory=dict)
+
+    def layer_bytes(self, i: int) -> tuple[int, int]:
+        ly = self.layers[i]
+        return ly.R * (ly.Kh + ly.Kx) * 2, ly.R * 4
+
+    def vocab_bytes(self) -> int:
+        return self.Vp * self.Ke * 2
+
+
+def layer_keys(keys) -> list[tuple]:
+    """(w_ih, effective w_hh, b_ih, b_hh) key names per layer, in order."""
+    ks = set(keys)
+    out, l = [], 0
+    while f"0.rnns.{l}.module.weight_ih_l0" in ks:
+        pre = f"0.rnns.{l}"
+        hh = f"{pre}.module.weight_hh_l0" if f"{pre}.module.weight_hh_l0" in ks else f"{pre}.weight_hh_l0_raw"
+        out.append((f"{pre}.module.weight_ih_l0", hh, f"{pre}.module.bias_ih_l0", f"{pre}.module.bias_hh_l0"))
+        l += 1
+    return out
+
+
+def geometry(shapes: dict, tied: bool | None = None) -> LmbGeometry:
+    """Batched-engine geometry from ``{state_dict key: shape}``; raises ValueError for checkpoints
+    the batched kernels cannot run (same checks as the torch packer always had)."""
+    if any(k.endswith("_reverse") for k in shapes):
+        raise ValueError("bidirectional AWD-LSTM cannot drive token-by-token generation")
+    if "0.encoder.weight" not in shapes:
+        raise ValueError("not an AWD-LSTM state_dict (no 0.encoder.weight)")
+    V, E = shapes["0.encoder.weight"]
+    Ke = _pad(E, 256)
+    if Ke > 1024:
+        raise ValueError(f"batched decode supports embedding widths <= 1024 (got {E})")
+    lk = layer_keys(shapes)
+    if not lk:
+        raise ValueError("not an AWD-LSTM state_dict (no 0.rnns.{l}.module.weight_ih_l0)")
+    if len(lk) > 4:
+        raise ValueError("batched decode supports up to 4 layers")
+    for keys in lk:
+        for k in keys:
+            if k not in shapes:
+                raise ValueError(f"missing {k}")
+    raw = [(shapes[k[0]][1], shapes[k[0]][0] // 4) for k in lk]  # (In, H)
+    if raw[0][0] != E or raw[-1][1] != E:
+        raise ValueError("batched decode needs layer 0 input and last hidden size = embedding width (tied model)")
+    layers = []
+    for i, (keys, (n_in, H)) in enumerate(zip(lk, raw)):
+        if tuple(shapes[keys[0]]) != (4 * H, n_in) or tuple(shapes[keys[1]]) != (4 * H, H) or \
+                tuple(shapes[keys[2]]) != (4 * H,) or tuple(shapes[keys[3]]) != (4 * H,):
+            raise ValueError(f"layer {i}: inconsistent LSTM parameter shapes")
+        if i > 0 and n_in != raw[i - 1][1]:
+            raise ValueError(f"layer {i}: input width {n_in} != previous hidden {raw[i - 1][1]}")
+        Kh = Ke if i == len(raw) - 1 else _pad(H, 32)
+        Kx = Ke if i == 0 else layers[-1].Kh
+        if (Kh + Kx) // 32 > 72:
+            raise ValueError(f"layer {i}: K = {Kh + Kx} exceeds the batched kernel's 2304")
+        layers.append(LmbLayer(H, n_in, Kh, Kx, _pad(4 * H, 16), keys))
+    dec = "1.decoder.weight" if "1.decoder.weight" in shapes and tied is False else None
+    if dec is not None and tuple(shapes[dec]) != (V, E):
+        raise ValueError(f"1.decoder.weight is {shapes[dec]}, expected {(V, E)}")
+    db = "1.decoder.bias" if "1.decoder.bias" in shapes else None
+    if db is not None and tuple(shapes[db]) != (V,):
+        raise ValueError(f"1.decoder.bias is {shapes[db]}, expected ({V},)")
+    return LmbGeometry(layers, V, E, Ke, _pad(V, 16), dec, db)
+
+
+def pack(geo: LmbGeometry, src, dst: dict, stream: int, lib=None) -> None:
+    """Issue the packing launches on ``stream``: ``src(key) -> device address`` of the raw fp32
+    contiguous tensor of that state_dict key (0 for absent); ``dst``: ``{"layers": [(w, bias)...],
+    "emb", "dec" (may equal emb), "dec_bias"}`` device addresses of the packed outputs.
+    Layout (bitwise the torch packer's, engine/lmbatch.py): per layer W = [W_hh | W_ih], rows
+    unit-interleaved (4j + q = gate q of unit j), K segments zero-padded, RNE bf16, fragment-major
+    [R/16][K/32][64][8]; bias b_ih + b_hh; vocabulary matrices [Vp, Ke]; decoder bias [Vp]."""
+    lib = lib or N.lib()
+
+    def launch(**kw):
+        p = N.FragPackParams()
+        for k, v in kw.items():
+            setattr(p, k, v)
+        N.check(lib.hz_frag_pack_launch(C.byref(p), stream), "hz_frag_pack_launch")
+
+    for ly, (w, bias) in zip(geo.layers, dst["layers"]):
+        w_ih, w_hh, b_ih, b_hh = ly.keys
+        launch(a=src(w_hh), b=src(w_ih), out=w, bias_a=src(b_ih), bias_b=src(b_hh), bias_out=bias, R=ly.R,
+               K=ly.Kh + ly.Kx, nrows=4 * ly.H, interleave_h=ly.H, ka=ly.Kh, acols=ly.H, lda=ly.H, bcols=ly.In,
+               ldb=ly.In)
+    launch(a=src("0.encoder.weight"), out=dst["emb"], R=geo.Vp, K=geo.Ke, nrows=geo.V, ka=geo.Ke, acols=geo.E,
+           lda=geo.E)
+    if dst["dec"] != dst["emb"]:
+        launch(a=src(geo.dec_key), out=dst["dec"], R=geo.Vp, K=geo.Ke, nrows=geo.V, ka=geo.Ke, acols=geo.E,
+               lda=geo.E)
+    launch(bias_a=src(geo.dec_bias_key) if geo.dec_bias_key else 0, bias_out=dst["dec_bias"], R=geo.Vp, K=32,
+           nrows=geo.V, ka=32)
+
+
+class LmbCore:
+    """The decode program and its scheduler over packed weights at device addresses ``w``
+    (``{"layers": [(w, bias)], "emb", "dec", "dec_bias"}``). ``alloc`` provides storage:
+    ``alloc.device(nbytes) -> address`` (zero-filled) and ``alloc.pinned(nbytes) -> address``
+    (zero-filled, page-locked); it owns the allocations (the caller keeps it alive).
+    ``stream``: the HIP stream the program is captured on and replayed by the scheduler."""
+
+    def __init__(self, geo: LmbGeometry, w: dict, alloc, stream: int, rows: int = 32, unroll: int = 8,
+                 exclude_ids=(), max_words: int = 1024, record_logits: bool = False, capture: bool = True,
+                 lib=None):
+        if rows not in (16, 32):
+            raise ValueError("rows must be 16 or 32")
+        if not 1 <= unroll <= 32:
+            raise ValueError("unroll must be in 1..32")
+        lib = lib or N.lib()
+        self.lib, self.geo = lib, geo
+        self.rows, self.unroll, self.max_words, self.V = rows, unroll, max_words, geo.V
+        Bp, U, L = rows, unroll, geo.layers
+        self.h = [alloc.device(4 * ly.Kh * Bp * 2) for ly in L]       # [2 par][2 hi/lo][Kh/32][Bp/16][64][8] bf16
+        self.c = [alloc.device(Bp * ly.H * 4) for ly in L]
+        self.gpar = alloc.device(4)
+        self.ctl = alloc.device(U * Bp * 4 * 4)
+        self.seed = alloc.device(Bp * 8)
+        self.outp = alloc.device(Bp * 8)
+        self.nblk = lib.hz_lmb_dec_blocks(geo.V)
+        self.dbest = alloc.device(2 * Bp * 8)
+        self.tok = alloc.device(Bp * 4)
+        self.block = alloc.pinned((8 + Bp * (8 + 4 * U)) * 4)
+        self.out_pool = alloc.pinned(Bp * max_words * 4)
+        self.logits = alloc.pinned(Bp * geo.V * 4) if record_logits else 0
+        ex = [int(e) for e in exclude_ids][:8]
+
+        a = N.LmbAdmitParams()
+        a.block, a.ctl, a.seed, a.outp, a.gpar = self.block, self.ctl, self.seed, self.outp, self.gpar
+        a.Bp, a.U, a.n_layers = Bp, U, len(L)
+        for i, ly in enumerate(L):
+            a.h[i], a.c[i], a.Kh[i], a.H[i] = self.h[i], self.c[i], ly.Kh, ly.H
+        layer_prms = []
+        for i, ly in enumerate(L):
+            q = N.LmbLayerParams()
+            q.w, q.bias = w["layers"][i]
+            q.h, q.c = self.h[i], self.c[i]
+            q.x = 0 if i == 0 else self.h[i - 1]
+            q.gpar, q.ctl = self.gpar, self.ctl
+            q.H, q.Kh, q.Kx, q.R, q.Bp = ly.H, ly.Kh, ly.Kx, ly.R, Bp
+            if i == 0:
+                q.emb, q.dbest, q.V = w["emb"], self.dbest, geo.V
+                q.outp, q.tok = self.outp, self.tok
+            layer_prms.append(q)
+        d = N.LmbDecParams()
+        d.w, d.bias, d.h = w["dec"], w["dec_bias"], self.h[-1]
+        d.gpar, d.ctl, d.seed, d.dbest = self.gpar, self.ctl, self.seed, self.dbest
+        d.logits = self.logits
+        d.V, d.Vp, d.K, d.Bp, d.nblk = geo.V, geo.Vp, L[-1].Kh, Bp, self.nblk
+        d.n_exclude = len(ex)
+        for i, e in enumerate(ex):
+            d.exclude[i] = e
+        self._ops = [(N.HZ_K_LMB_LAYER, q) for q in layer_prms] + [(N.HZ_K_LMB_DEC, d)]
+        prog = lib.hz_prog_create()
+        N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(a), C.sizeof(a), 0), "add lmb admit")
+        for u in range(U):
+            for kind, prm in self._ops:
+                q = type(prm).from_buffer_copy(prm)
+                q.step_off = u
+                N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
+        self._admit = a
+        self.prog = prog
+        self.stream = stream
+        if capture:
+            N.check(lib.hz_prog_capture(prog, stream), "capture lmb")
+        self._sched = lib.hz_lmb_create(prog, stream, self.block, Bp, U, 0, max_words, self.out_pool, d.logits, geo.V)
+        if not self._sched:
+            raise RuntimeError("hz_lmb_create failed")
+        self.last_latency_ms = None
+
+    def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
+        """Feed ``prompt_ids``, sample ``n_words`` tokens (blocking, thread-safe); the sampled ids,
+        and with ``logits`` the fp32 logits after the last prompt token as a ctypes float array."""
+        P = len(prompt_ids)
+        if P < 1:
+            raise ValueError("need at least one prompt token")
+        if not 1 <= n_words <= self.max_words:
+            raise ValueError(f"n_words must be in 1..{self.max_words}")
+        if logits and not self.logits:
+            raise ValueError("engine built without record_logits")
+        prompt = (C.c_int * P)(*[int(t) for t in prompt_ids])
+        out = (C.c_int * n_words)()
+        lg = (C.c_float * self.V)() if logits else None
+        lat = C.c_double()
+        rc = self.lib.hz_lmb_submit(self._sched, prompt, P, n_words, int(seed) & ((1 << 62) - 1), out, lg,
+                                    C.byref(lat))
+        if rc:
+            raise RuntimeError(f"batched decode request failed ({rc})")
+        self.last_latency_ms = lat.value / 1e3
+        return (list(out), lg) if logits else list(out)
+
+    def stats(self) -> dict:
+        a = (C.c_uint64 * 4)()
+        self.lib.hz_lmb_stats(self._sched, a)
+        return {"replays": a[0], "served": a[1], "row_steps_used": a[2], "row_steps": a[3],
+                "row_utilisation": round(a[2] / a[3], 4) if a[3] else None}
+
+    def close(self) -> None:
+        s, self._sched = getattr(self, "_sched", None), None
+        if s:
+            self.lib.hz_lmb_destroy(s)
+        prog, self.prog = getattr(self, "prog", None), None
+        if prog:
+            self.lib.hz_prog_destroy(prog)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

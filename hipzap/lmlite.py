@@ -1,0 +1,193 @@
+"""``GET /inference`` without torch: the batched AWD-LSTM engine built straight from the
+reference's ``.pth`` (VERDICT r3 "next round" 2).
+
+The reference cold-loads its checkpoint with ``torch.load`` on every request
+(/root/reference/main.py:84-103, :99). Here a fresh process never imports torch:
+
+1. ``pthreader.scan`` -- the weights-only zip reader: where each tensor of the state_dict lives
+   in the file (a restricted unpickler; nothing from the file runs);
+2. ``hz_upload_file`` (csrc/plan.cpp) -- the raw fp32 records pread into pinned staging and DMA'd
+   to one device buffer, chunk i in flight while chunk i+1 is read;
+3. ``lmcore.pack`` -- the device packer (csrc/pack.hip ``hz_frag_pack_launch``) writes the batched
+   engine's fragment-major bf16 layouts, bitwise the torch packer's;
+4. ``lmcore.LmbCore`` -- the decode program, its hipGraph and the native row scheduler
+   (csrc/lmserve.cpp), exactly the object the torch-built :class:`LMBatchEngine` drives.
+
+Checkpoint rules: engine/lmcore.py (effective W_hh = ``module.weight_hh_l0``; tied decoder when
+``1.decoder.weight`` is the encoder's storage). The vocabulary is the reference's pickled
+``list[str]`` read by a no-globals unpickler (serve/text.py ``load_itos``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+import time
+
+from . import _native as N
+from . import hip
+from .engine import lmcore
+from .pthreader import scan
+from .serve.text import EXCLUDE_TOKENS, Detokenizer, load_itos, make_stoi
+
+
+class LMLiteError(RuntimeError):
+    pass
+
+
+class _HipAlloc:
+    """lmcore allocator over ctypes HIP allocations (zero-filled)."""
+
+    def __init__(self, stream: int):
+        self.stream, self.keep = stream, []
+
+    def device(self, nbytes: int) -> int:
+        b = hip.DeviceBuffer(max(1, nbytes))
+        hip.check(hip.hip().hipMemsetAsync(b.ptr, 0, max(1, nbytes), self.stream), "hipMemsetAsync")
+        self.keep.append(b)
+        return b.ptr
+
+    def pinned(self, nbytes: int) -> int:
+        b = hip.PinnedBuffer(max(1, nbytes))
+        C.memset(b.ptr, 0, max(1, nbytes))
+        self.keep.append(b)
+        return b.ptr
+
+
+def _stream() -> int:
+    p = C.c_void_p()
+    hip.check(hip.hip().hipStreamCreateWithFlags(C.byref(p), 1), "hipStreamCreateWithFlags")  # non-blocking
+    return p.value
+
+
+class LMLiteEngine:
+    """Batched AWD-LSTM decode from a ``.pth`` with no torch in the process. Same request API as
+    :class:`hipzap.engine.lmbatch.LMBatchEngine` (``run_tokens`` / ``generate``, thread-safe,
+    concurrent requests share decode steps); ``timings`` holds the cold-start phases (ms)."""
+
+    def __init__(self, ckpt: str, device: int = 0, rows: int = 32, unroll: int = 8, exclude_ids=(),
+                 max_words: int = 1024, record_logits: bool = False, capture: bool = True):
+        t0 = time.perf_counter()
+        refs = scan(ckpt)
+        enc, dec = refs.get("0.encoder.weight"), refs.get("1.decoder.weight")
+        if enc is None:
+            raise LMLiteError(f"{ckpt}: not an AWD-LSTM checkpoint (no 0.encoder.weight)")
+        tied = dec is None or (dec.storage is enc.storage and dec.offset == enc.offset and
+                               tuple(dec.shape) == tuple(enc.shape) and tuple(dec.stride) == tuple(enc.stride))
+        try:
+            geo = lmcore.geometry({k: tuple(r.shape) for k, r in refs.items()}, tied=tied)
+        except ValueError as e:
+            raise LMLiteError(f"{ckpt}: {e}") from None
+        need = ["0.encoder.weight"] + [k for ly in geo.layers for k in ly.keys]
+        need += [k for k in (geo.dec_key, geo.dec_bias_key) if k]
+        for k in need:
+            r = refs[k]
+            if r.dtype != "float32" or not r.is_contiguous():
+                raise LMLiteError(f"{ckpt}: {k} is {r.dtype}{'' if r.is_contiguous() else ' (non-contiguous)'}: "
+                                  f"the torch-free path packs contiguous fp32 records")
+        t_scan = time.perf_counter()
+        hip.set_device(device)
+        self.device, self.geo, self.ckpt = device, geo, ckpt
+        self.stream = _stream()
+        t_init = time.perf_counter()
+        # raw records -> one staging buffer (each shared storage once)
+        stores = {}
+        for k in need:
+            stores.setdefault(refs[k].storage.key, refs[k].storage)
+        offs, total = {}, 0
+        for key, st in stores.items():
+            offs[key] = total
+            total += (st.nbytes + 255) // 256 * 256
+        staging = hip.DeviceBuffer(total)
+        keys = list(stores)
+        n = len(keys)
+        U64 = C.c_uint64 * n
+        rc = N.lib().hz_upload_file(ckpt.encode(), n, U64(*[stores[k].file_off for k in keys]),
+                                    U64(*[stores[k].nbytes for k in keys]),
+                                    (C.c_void_p * n)(*[staging.ptr + offs[k] for k in keys]), self.stream)
+        if rc:
+            raise LMLiteError(f"checkpoint upload failed: {N.lib().hz_plan_last_error().decode()}")
+        t_up = time.perf_counter()
+        # packed weights
+        self._alloc = _HipAlloc(self.stream)
+        dev = self._alloc.device
+        layers = []
+        for i in range(len(geo.layers)):
+            wb, bb = geo.layer_bytes(i)
+            layers.append((dev(wb), dev(bb)))
+        emb = dev(geo.vocab_bytes())
+        w = {"layers": layers, "emb": emb, "dec": emb if geo.dec_key is None else dev(geo.vocab_bytes()),
+             "dec_bias": dev(geo.Vp * 4)}
+        src = lambda k: staging.ptr + offs[refs[k].storage.key] + refs[k].offset * 4 if k else 0  # noqa: E731
+        lmcore.pack(geo, src, w, self.stream)
+        hip.sync(self.stream)
+        staging.free()
+        t_pack = time.perf_counter()
+        self.core = lmcore.LmbCore(geo, w, self._alloc, self.stream, rows=rows, unroll=unroll,
+                                   exclude_ids=exclude_ids, max_words=max_words, record_logits=record_logits,
+                                   capture=capture)
+        hip.sync(self.stream)
+        t_ready = time.perf_counter()
+        self.V, self.rows, self.unroll, self.max_words = geo.V, rows, unroll, max_words
+        self.timings = {"scan_ms": (t_scan - t0) * 1e3, "hip_init_ms": (t_init - t_scan) * 1e3,
+                        "upload_ms": (t_up - t_init) * 1e3, "pack_ms": (t_pack - t_up) * 1e3,
+                        "program_ms": (t_ready - t_pack) * 1e3, "raw_MB": round(total / 2 ** 20, 1)}
+        self._seed_lock = threading.Lock()
+        self._seed_ctr = int.from_bytes(os.urandom(8), "little")
+
+    @classmethod
+    def for_vocab(cls, ckpt: str, stoi: dict, **kw) -> "LMLiteEngine":
+        return cls(ckpt, exclude_ids=[stoi[w] for w in EXCLUDE_TOKENS if w in stoi], **kw)
+
+    def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
+        return self.core.run_tokens(prompt_ids, n_words, seed, logits)
+
+    @property
+    def last_latency_ms(self):
+        return self.core.last_latency_ms
+
+    def _fresh_seed(self) -> int:
+        with self._seed_lock:
+            self._seed_ctr = (self._seed_ctr * 6364136223846793005 + 1442695040888963407) & ((1 << 64) - 1)
+            return self._seed_ctr >> 2
+
+    def generate(self, prompt_words, n_words, itos, stoi, seed=None) -> str:
+        """The reference's loop semantics (main.py:40-81) on the device: prompt fed token by
+        token (unknown -> 0), ``n_words`` samples, detokenized on the host."""
+        ids = [stoi.get(w, 0) for w in prompt_words]
+        toks = self.run_tokens(ids, n_words, self._fresh_seed() if seed is None else seed)
+        det = Detokenizer()
+        for w_ in prompt_words:
+            det.add_prompt(w_)
+        for t in toks:
+            det.add(itos[t])
+        return det.text
+
+    def stats(self) -> dict:
+        return self.core.stats()
+
+    def close(self) -> None:
+        core = getattr(self, "core", None)
+        if core is not None:
+            core.close()
+
+
+class LMLiteBackend:
+    """``GET /inference`` backend over :class:`LMLiteEngine` (serve/server.py ``ModelServer.lm``
+    picks it for a GPU server whose checkpoint is a zip ``.pth``; HIPZAP_LM_LITE=0 disables)."""
+    backend = "gpu"
+    engine_kind = "batch-lite"
+
+    def __init__(self, ckpt: str, itos_path: str, device: int = 0):
+        t0 = time.perf_counter()
+        self.itos = load_itos(itos_path)
+        self.stoi = make_stoi(self.itos)
+        self.engine = LMLiteEngine.for_vocab(ckpt, self.stoi, device=device,
+                                             rows=int(os.environ.get("HIPZAP_LM_ROWS", 32)),
+                                             unroll=int(os.environ.get("HIPZAP_LM_UNROLL", 8)))
+        if self.engine.V > len(self.itos):
+            raise LMLiteError(f"vocabulary has {len(self.itos)} words, the checkpoint {self.engine.V} rows")
+        self.cold_ms = (time.perf_counter() - t0) * 1e3
+
+    def generate(self, prompt_words, n_words, seed=None) -> str:
+        return self.engine.generate(prompt_words, n_words, self.itos, self.stoi, seed=seed)

@@ -342,22 +342,36 @@ class ModelServer:
                     return self._models[name]
         return self._load(name, TextBackend)
 
-    def lm(self) -> LMBackend:
-        import torch
+    def lm(self):
+        """The GET /inference backend, loaded once. A GPU server whose checkpoint is a zip ``.pth``
+        builds the batched engine WITHOUT torch (hipzap/lmlite.py: weights-only reader, raw upload,
+        device packing); anything that path refuses (legacy files, non-fp32 records) and the random
+        demo weights go through torch (LMBackend)."""
         from .text import load_itos
         key = "__lm__"
         with self._lock:
             if key not in self._models:
                 st = self.settings
+                be = None
                 if os.environ.get("HIPZAP_RANDOM_WEIGHTS") or st.models_bucket is None:
+                    import torch
                     from ..models.awd_lstm import reference_lm
                     itos = synthetic_vocab(int(os.environ.get("HIPZAP_LM_VOCAB", 2000)))
                     torch.manual_seed(0)
-                    sd = reference_lm(len(itos)).state_dict()
+                    be = LMBackend(reference_lm(len(itos)).state_dict(), itos, self.backend, self.device)
                 else:
-                    itos = load_itos(self.store.fetch(st.lm_vocab_key))
-                    sd = load_checkpoint(self.store.fetch(st.lm_model_key))
-                self._models[key] = LMBackend(sd, itos, self.backend, self.device)
+                    ckpt, vocab = self.store.fetch(st.lm_model_key), self.store.fetch(st.lm_vocab_key)
+                    if self.backend == "gpu" and os.environ.get("HIPZAP_LM_LITE", "1") != "0":
+                        import zipfile
+                        from ..lmlite import LMLiteBackend, LMLiteError
+                        if zipfile.is_zipfile(ckpt):
+                            try:
+                                be = LMLiteBackend(ckpt, vocab, st.devices[0])
+                            except LMLiteError as e:
+                                log.warning("torch-free LM path refused %s (%s); loading it with torch", ckpt, e)
+                    if be is None:
+                        be = LMBackend(load_checkpoint(ckpt), load_itos(vocab), self.backend, self.device)
+                self._models[key] = be
                 self.stats["cold_loads"] += 1
             return self._models[key]
 

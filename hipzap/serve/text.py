@@ -19,9 +19,10 @@ from __future__ import annotations
 import io
 import json
 import pickle
-from typing import Callable, Sequence
+from typing import TYPE_CHECKING, Callable, Sequence
 
-import torch
+if TYPE_CHECKING:  # torch-free at import: the plan / lite LM servers never load torch
+    import torch
 
 NO_SPACE = ["'s", "'ll", ",", "?", ".", "'t", "'m", "n't", "!", "'", "'ve", ";", "http", ":", "/", "\\"]
 CAPITALIZE_AFTER = [".", "!", "\n"]
@@ -65,6 +66,7 @@ def make_stoi(itos: Sequence[str]) -> dict[str, int]:
 
 def gumbel_topk(logits: torch.Tensor, k: int, generator: torch.Generator | None = None) -> torch.Tensor:
     """k draws without replacement, P ∝ exp(logits) (Plackett-Luce), in log space."""
+    import torch
     lg = logits.float().reshape(-1)
     u = torch.rand(lg.shape, generator=generator, device=lg.device).clamp_(1e-20, 1.0)
     g = -torch.log(-torch.log(u))
