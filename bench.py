@@ -73,6 +73,8 @@ def parse():
                          "(0 disables)")
     ap.add_argument("--http-requests", type=int, default=800, help="requests per HTTP client process")
     ap.add_argument("--bert-cold", type=int, default=1, help="also report the BERT-base text-plan cold start")
+    ap.add_argument("--lm-cold", type=int, default=1,
+                    help="also report the GET /inference (AWD-LSTM V=60000, 200 words) torch-free cold start")
     ap.add_argument("--dp-figures", type=int, default=int(os.environ.get("HIPZAP_BENCH_DP", 1)),
                     help="also measure BASELINE configs 3 / 5 (scatter-gather DP) in the same launch")
     ap.add_argument("--sustained-s", type=float, default=2.0,
@@ -172,11 +174,43 @@ def prepare_artifacts(model: str, ckpt_dir: str, plan_contexts: int = 1) -> tupl
     return ckpt, plan
 
 
-def fresh_cold_start(args, device_index: int) -> dict:
+def prepare_lm_artifacts(ckpt_dir: str, vocab: int = 60000) -> tuple[str, str]:
+    """Deploy-time AWD-LSTM artifacts of the reference's route (untimed, CPU): a random-init
+    checkpoint of the reference's dimensions (main.py:96: emb 1000, hidden 1150, 3 layers, tied,
+    V = 60000 as SURVEY §2d assumes; ~357 MB fp32, torch.save) and its pickled itos list."""
+    import pickle
+    from hipzap.models.awd_lstm import reference_lm
+    ckpt = os.path.join(ckpt_dir, f"awd_lstm_v{vocab}_seed0.pth")
+    itos = os.path.join(ckpt_dir, f"awd_lstm_v{vocab}.itos.pkl")
+    if not os.path.exists(ckpt):
+        torch.manual_seed(0)
+        os.makedirs(ckpt_dir, exist_ok=True)
+        tmp = ckpt + f".tmp{os.getpid()}"
+        torch.save(reference_lm(vocab).eval().state_dict(), tmp)
+        os.replace(tmp, ckpt)
+    if not os.path.exists(itos):
+        words = ["xxunk", "xxpad", "xxbos", "xxfld", "xxmaj", "xxup", "xxrep", ".", ",", "!", "\n", "'s"]
+        with open(itos, "wb") as f:
+            pickle.dump(words + [f"w{i}" for i in range(vocab - len(words))], f)
+    return ckpt, itos
+
+
+def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
     """Cold start over fresh processes (hipzap/coldstart.py), before this process uses a GPU."""
-    from hipzap.coldstart import measure_fresh
+    from hipzap.coldstart import measure_fresh, measure_node
     ckpt, plan = prepare_artifacts(args.model, args.ckpt_dir)
     res = {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index)}
+    try:  # the node: N torch-free workers, RCCL rendezvous, C1 weight broadcast, first logits on every rank
+        res["node"] = measure_node(plan, world, trials=max(3, min(5, args.cold_trials)))
+    except Exception as e:  # noqa: BLE001 - secondary to the one-GPU figure
+        print(f"node cold start skipped: {e}", file=sys.stderr)
+    if args.lm_cold:
+        try:  # the reference's own route: GET /inference (AWD-LSTM, 200 words) from its .pth, no torch
+            lm_ckpt, itos = prepare_lm_artifacts(args.ckpt_dir)
+            res["lm"] = measure_fresh("lm", lm_ckpt, "awd-lstm", args.cold_trials, device=device_index,
+                                      extra_args=["--vocab", itos])
+        except Exception as e:  # noqa: BLE001 - secondary figure
+            print(f"LM cold start skipped: {e}", file=sys.stderr)
     try:  # the .pth itself without torch: weights-only reader + plan template + device-side packing
         res["pth_lite"] = measure_fresh("pth-lite", ckpt, args.model, args.cold_trials, device=device_index)
     except Exception as e:  # noqa: BLE001 - template not built: the torch path stays the .pth figure
@@ -331,8 +365,9 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
             if is_dist():
                 dist.barrier()
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                ex.step(xg)
+            for i in range(args.steps):  # one bounded host sync per 8 steps (DPExecutor.step docstring)
+                ex.step(xg, sync=i % 8 == 7)
+            ex.sync()
             torch.cuda.synchronize(device)
             dt = time.perf_counter() - t0
         except Exception as e:  # noqa: BLE001
@@ -488,7 +523,7 @@ def main():
         if args.mode == "replica" and args.cold_trials > 0 and args.model.startswith("resnet"):
             dev_index = local % max(1, torch.cuda.device_count()) if os.environ.get("HIPZAP_SHARE_GPU") == "1" \
                 else local
-            fresh = fresh_cold_start(args, dev_index)
+            fresh = fresh_cold_start(args, dev_index, world)
         else:
             prepare_artifacts(args.model, args.ckpt_dir)
 
@@ -574,7 +609,6 @@ def main():
 
     # 2. in-process cold starts (secondary figures: warm torch, warm HIP runtime)
     eng, out, cold_first = cold_start()
-    cold_process_ms = (time.time() - T_PROC0) * 1e3
     colds = [cold_first]
     for _ in range(args.cold_runs):
         del eng
@@ -698,13 +732,16 @@ def main():
             "cold_start_native_ms_p50": (fresh.get("native") or {}).get("p50_ms") if fresh else None,
             # BERT-base bs16 seq-cls from its text plan image (torch-free)
             "cold_start_bert_plan_ms_p50": (fresh.get("bert_plan") or {}).get("p50_ms") if fresh else None,
+            # the node: spawn N torch-free workers -> RCCL init -> C1 broadcast -> first logits on EVERY rank
+            "cold_start_node_ms_p50": (fresh.get("node") or {}).get("p50_ms") if fresh else None,
+            # the reference's route: fresh process -> first 200-word GET /inference response, torch-free
+            "cold_start_lm_ms_p50": (fresh.get("lm") or {}).get("p50_ms") if fresh else None,
             "cold_start_fresh_process": fresh,
             "cold_start_inprocess_ms_first": round(cold_first, 2),
             "cold_start_inprocess_ms_p50": round(statistics.median(colds), 2),
             "cold_start_inprocess_breakdown_ms": {k: round(v, 2) for k, v in breakdown_pth.items()},
             "cold_start_inprocess_packed_ms_p50": round(statistics.median(colds_packed), 2) if colds_packed else None,
             "cold_start_inprocess_packed_breakdown_ms": {k: round(v, 2) for k, v in breakdown_packed.items()},
-            "bench_process_first_request_ms": round(cold_process_ms, 2),
             "deferred_contexts_ms": round(deferred_ms, 2),
             "served_closed_loop_inf_s": round(inf / (dt if args.serve != "pipelined" else dt_other), 2),
             "device_pipelined_inf_s": round(inf / (dt if args.serve == "pipelined" else dt_other), 2),

@@ -9,6 +9,13 @@
         AWD-LSTM .pth -> raw upload -> device packing -> batched decode engine (hipzap/lmlite.py),
         then one 200-word response (the reference's request, main.py:84-112)
 
+``measure_node(plan, N)`` is the node-level cold start of N GPUs (VERDICT r3 "next round" 3a):
+N fresh torch-free worker processes, one per GPU, spawned together; each joins the RCCL
+communicator through a file rendezvous, rank 0 reads the plan's weight blob and broadcasts it to
+the others (C1), every rank serves one request, and a 1-int all-reduce (C4) checks
+that all of them produced finite logits. Timed from the launcher: spawn -> the LAST rank's first
+logits.
+
 ``measure_fresh("native", plan)`` spawns the Python-free ``hipzap-serve-plan PLAN --once IMAGE``
 (csrc/tools/serve_plan.cpp) instead: exec -> HIP init -> plan upload -> one eager request.
 
@@ -94,6 +101,99 @@ def run_lm(ckpt: str, device: int, vocab: str | None, words: int = 200) -> dict:
                           "engine_total": (t_ready - t_vocab) * 1e3, "first_response": (t_first - t_ready) * 1e3}}
 
 
+def run_node(plan: str, rank: int, world: int, rdzv_dir: str, device: int, timeout_s: float = 60.0,
+             dry: bool = False) -> dict:
+    """One worker of a node cold start (see :func:`measure_node`). ``dry``: the launcher and
+    rendezvous plumbing only (no GPU: every rank publishes its arrival and waits for all)."""
+    t_imp = time.time()
+    from hipzap.parallel.rccl import FileRendezvous
+    rdzv = FileRendezvous(rdzv_dir)
+    if dry:
+        rdzv.publish(f"arrived{rank}", b"1")
+        for r in range(world):
+            rdzv.wait(f"arrived{r}", timeout=timeout_s)
+        t_first = time.time()
+        return {"mode": "node", "rank": rank, "world": world, "t_first": t_first, "ok": True, "healthy": world,
+                "torch_imported": "torch" in sys.modules, "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3}}
+    from hipzap import hip
+    from hipzap.lite import PlanEngine
+    from hipzap.parallel.rccl import RcclComm
+    t_lib = time.time()
+    hip.set_device(device)
+    comm = RcclComm.from_rendezvous(rdzv, world, rank, device, timeout_s=timeout_s) if world > 1 else None
+    t_comm = time.time()
+    fill = (lambda addr, n: comm.broadcast_ptr(addr, n, 0)) if comm is not None else None  # noqa: E731
+    eng = PlanEngine(plan, device=device, contexts=1, read_blob=comm is None or rank == 0, fill_blob=fill,
+                     capture="lazy")
+    t_ready = time.time()
+    out = eng.infer_raw(os.urandom(eng.in_specs[0]["bytes"]))
+    t_first = time.time()
+    import math
+    ok = all(math.isfinite(v) for v in out)
+    healthy = int(ok)
+    if comm is not None:  # C4: how many ranks served a finite first request
+        import ctypes as C
+        buf = hip.DeviceBuffer(4)
+        v = C.c_int(healthy)
+        hip.memcpy(buf.ptr, C.addressof(v), 4, hip.H2D)
+        comm.allreduce_ptr(buf.ptr, 1, "int32", "sum")
+        hip.memcpy(C.addressof(v), buf.ptr, 4, hip.D2H)
+        healthy = v.value
+        comm.close()
+    return {"mode": "node", "rank": rank, "world": world, "t_first": t_first, "ok": ok and healthy == world,
+            "healthy": healthy, "torch_imported": "torch" in sys.modules,
+            "phases_ms": {"interp_to_main": (t_imp - T0) * 1e3, "import": (t_lib - t_imp) * 1e3,
+                          "rccl_init": (t_comm - t_lib) * 1e3,
+                          **{k: round(v, 3) for k, v in eng.timings.items()},
+                          "first_request": (t_first - t_ready) * 1e3}}
+
+
+def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0, dry: bool = False,
+                 env: dict | None = None) -> dict:
+    """Node-level cold start: ``trials`` launches of ``world`` fresh workers (device = rank), each
+    timed from the spawn of the first worker to the first logits of the LAST one."""
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    walls, res = [], []
+    for _ in range(trials):
+        rdzv = tempfile.mkdtemp(prefix="hzcold_node_")
+        procs = []
+        t = time.time()
+        for r in range(world):
+            cmd = [sys.executable, "-m", "hipzap.coldstart", "node", plan, "--device", str(r), "--rank", str(r),
+                   "--world", str(world), "--rdzv", rdzv] + (["--dry"] if dry else [])
+            procs.append(subprocess.Popen(cmd, cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                          text=True))
+        outs, err = [], None
+        for r, p in enumerate(procs):
+            try:
+                so, se = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise RuntimeError(f"node cold start: rank {r} did not finish within {timeout:.0f} s")
+            lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+            if p.returncode != 0 or not lines:
+                err = err or f"rank {r} rc={p.returncode}: {se[-2000:]}"
+                continue
+            outs.append(json.loads(lines[-1]))
+        shutil.rmtree(rdzv, ignore_errors=True)
+        if err or len(outs) != world or not all(o["ok"] for o in outs):
+            raise RuntimeError(f"node cold start failed: {err or [o.get('healthy') for o in outs]}")
+        walls.append((max(o["t_first"] for o in outs) - t) * 1e3)
+        res.append(outs)
+    order = sorted(range(trials), key=lambda i: walls[i])
+    med = res[order[len(order) // 2]]
+    slow = max(med, key=lambda o: o["t_first"])
+    return {"mode": "node", "world": world, "trials": trials, "p50_ms": round(statistics.median(walls), 2),
+            "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2), "all_ms": [round(w, 1) for w in walls],
+            "slowest_rank_phases_ms": {k: round(v, 2) for k, v in slow["phases_ms"].items()},
+            "slowest_rank": slow["rank"], "torch_imported": any(o["torch_imported"] for o in med)}
+
+
 def run_torch(ckpt: str, model: str, device: int, packed: bool) -> dict:
     t_imp = time.time()
     import torch
@@ -174,12 +274,16 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
 def main(argv=None) -> int:
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite", "lm"])
+    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite", "lm", "node"])
     ap.add_argument("path")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--vocab", default=None, help="lm mode: the pickled itos list")
     ap.add_argument("--words", type=int, default=200, help="lm mode: words to generate")
+    ap.add_argument("--rank", type=int, default=0, help="node mode")
+    ap.add_argument("--world", type=int, default=1, help="node mode")
+    ap.add_argument("--rdzv", default=None, help="node mode: rendezvous directory")
+    ap.add_argument("--dry", action="store_true", help="node mode: launcher/rendezvous only, no GPU")
     a = ap.parse_args(argv)
     if a.mode == "plan":
         res = run_plan(a.path, a.device)
@@ -187,6 +291,8 @@ def main(argv=None) -> int:
         res = run_pth_lite(a.path, a.device)
     elif a.mode == "lm":
         res = run_lm(a.path, a.device, a.vocab, a.words)
+    elif a.mode == "node":
+        res = run_node(a.path, a.rank, a.world, a.rdzv, a.device, dry=a.dry)
     else:
         res = run_torch(a.path, a.model, a.device, packed=a.mode == "hzpack")
     res["t_interp"] = T0

@@ -17,3 +17,9 @@ class Comm:
     def gather(self, t, outs: list | None, dst: int = 0) -> None: ...
     def all_reduce(self, t, op: str = "sum") -> None: ...
     def barrier(self) -> None: ...
+
+    # asynchronous communicators (RcclComm) set this and accept scatter/gather(..., wait=False)
+    # plus sync(stream): the collective is stream-ordered and the host waits once, in sync()
+    supports_async: bool = False
+
+    def sync(self, stream=None) -> None: ...

@@ -39,8 +39,15 @@ class DPExecutor:
             self.x_all = torch.zeros((self.global_batch,) + tuple(in_shape), dtype=in_dtype, device=self.device)
             self.y_all = torch.zeros((self.global_batch,) + tuple(out_shape), dtype=out_dtype, device=self.device)
 
-    def step(self, x: torch.Tensor | None = None) -> torch.Tensor | None:
-        """Collective: every rank calls it; rank 0 passes the global batch (<= world*shard)."""
+    def step(self, x: torch.Tensor | None = None, sync: bool = True) -> torch.Tensor | None:
+        """Collective: every rank calls it; rank 0 passes the global batch (<= world*shard).
+
+        On a communicator that can enqueue without waiting (``supports_async``: the native RCCL
+        one), scatter -> shard replay -> gather are all stream-ordered on the caller's current
+        stream and the host synchronises at most ONCE per step (``sync``: a bounded wait on that
+        stream that also polls the communicator's asynchronous errors); ``sync=False`` leaves the
+        step in flight (a bench loop syncs every K steps). Blocking communicators (torch.distributed,
+        loopback) keep their own semantics."""
         n = 0
         if self.rank == 0:
             n = x.shape[0]
@@ -49,17 +56,29 @@ class DPExecutor:
             self.x_all[:n].copy_(x, non_blocking=True)
             if n < self.global_batch:
                 self.x_all[n:].zero_()
+        aio = bool(getattr(self.comm, "supports_async", False)) and self.world > 1
+        kw = {"wait": False} if aio else {}
         if self.world > 1:
             chunks = list(self.x_all.chunk(self.world)) if self.rank == 0 else None
-            self.comm.scatter(self.x_shard, chunks, src=0)
+            self.comm.scatter(self.x_shard, chunks, src=0, **kw)
         else:
             self.x_shard.copy_(self.x_all)
         y = self.runner(self.x_shard)
         self.y_shard.copy_(y.reshape(self.y_shard.shape))
         if self.world > 1:
             outs = list(self.y_all.chunk(self.world)) if self.rank == 0 else None
-            self.comm.gather(self.y_shard, outs, dst=0)
+            self.comm.gather(self.y_shard, outs, dst=0, **kw)
         else:
             self.y_all.copy_(self.y_shard)
         # a copy: the gather buffer is reused by the next step
-        return self.y_all[:n].clone() if self.rank == 0 else None
+        out = self.y_all[:n].clone() if self.rank == 0 else None
+        if aio and sync:
+            self.comm.sync(torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else None)
+        return out
+
+    def sync(self) -> None:
+        """Wait for the steps left in flight by ``step(sync=False)`` (bounded on RCCL)."""
+        if getattr(self.comm, "supports_async", False) and self.world > 1:
+            self.comm.sync(torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else None)
+        elif self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()

@@ -203,26 +203,33 @@ class RcclComm(Comm):
         self._check(lib().hz_comm_allreduce(self._h, ptr, count, dt, o, stream, int(wait)), "allreduce")
 
     # ------------------------------------------------------------------ loopback.Comm (torch tensors)
+    supports_async = True  # scatter / gather(wait=False) + sync(stream): DPExecutor's one-sync step
+
     def broadcast(self, t, src: int = 0) -> None:
         self.broadcast_ptr(_ptr(t), _nbytes(t), src, _stream_of(t))
 
-    def scatter(self, out, chunks, src: int = 0) -> None:
+    def scatter(self, out, chunks, src: int = 0, wait: bool = True) -> None:
         send = 0
         if self.rank == src:
             nb = _nbytes(out)
             send = chunks[0].data_ptr()
             if any(c.data_ptr() != send + i * nb or _nbytes(c) != nb for i, c in enumerate(chunks)):
                 raise ValueError("scatter chunks must be equal, contiguous slices of one buffer")
-        self.scatter_ptr(send, out.data_ptr(), _nbytes(out), src, _stream_of(out))
+        self.scatter_ptr(send, out.data_ptr(), _nbytes(out), src, _stream_of(out), wait=wait)
 
-    def gather(self, t, outs, dst: int = 0) -> None:
+    def gather(self, t, outs, dst: int = 0, wait: bool = True) -> None:
         recv = 0
         if self.rank == dst:
             nb = _nbytes(t)
             recv = outs[0].data_ptr()
             if any(o.data_ptr() != recv + i * nb or _nbytes(o) != nb for i, o in enumerate(outs)):
                 raise ValueError("gather outputs must be equal, contiguous slices of one buffer")
-        self.gather_ptr(t.data_ptr(), recv, _nbytes(t), dst, _stream_of(t))
+        self.gather_ptr(t.data_ptr(), recv, _nbytes(t), dst, _stream_of(t), wait=wait)
+
+    def sync(self, stream=None) -> None:
+        """Bounded wait for ``stream`` (default: the communicator's): polls the asynchronous
+        error state against the deadline; raises CommError on timeout or a transport error."""
+        self._check(lib().hz_comm_sync(self._h, stream), "sync")
 
     def all_reduce(self, t, op: str = "sum") -> None:
         dt = str(t.dtype).replace("torch.", "")

@@ -76,3 +76,52 @@ def test_failing_rank_aborts_peers_instead_of_hanging():
         return ex.step(torch.ones(4, 1) if c.rank == 0 else None)
     res = run_ranks(4, fn, timeout_s=10)
     assert all(isinstance(e, CommError) for e in res), res
+
+
+class _CountingAsyncComm:
+    """A loopback rank that advertises asynchronous collectives and counts host waits: a
+    collective called with wait=True (or without ``wait``) is a host sync, and so is sync()."""
+    supports_async = True
+
+    def __init__(self, inner):
+        self.inner, self.rank, self.world = inner, inner.rank, inner.world
+        self.host_syncs, self.async_calls = 0, 0
+
+    def scatter(self, out, chunks, src=0, wait=True):
+        self.host_syncs += int(wait)
+        self.async_calls += int(not wait)
+        self.inner.scatter(out, chunks, src)
+
+    def gather(self, t, outs, dst=0, wait=True):
+        self.host_syncs += int(wait)
+        self.async_calls += int(not wait)
+        self.inner.gather(t, outs, dst)
+
+    def sync(self, stream=None):
+        self.host_syncs += 1
+
+
+def test_dp_step_one_host_sync_per_step():
+    """VERDICT r3 "next round" 7: on an asynchronous communicator a DP step enqueues scatter and
+    gather without waiting and synchronises the host exactly once (sync=False: not at all), and the
+    results are the blocking step's, bitwise."""
+    from hipzap.parallel.loopback import run_ranks
+
+    def runner(xs):
+        return xs.sum(dim=1) * 2.0
+
+    x = torch.arange(4 * 3 * 5, dtype=torch.float32).reshape(12, 5)
+
+    def body(comm):
+        c = _CountingAsyncComm(comm)
+        ex = DPExecutor(runner, shard_batch=3, in_shape=(5,), out_shape=(), device="cpu", comm=c)
+        outs = [ex.step(x if c.rank == 0 else None) for _ in range(3)]
+        syncs_after_3 = c.host_syncs
+        ex.step(x if c.rank == 0 else None, sync=False)
+        return outs, syncs_after_3, c.host_syncs, c.async_calls
+
+    res = run_ranks(4, body)
+    for r, (outs, s3, s4, a) in enumerate(res):
+        assert s3 == 3 and s4 == 3 and a == 8, (r, s3, s4, a)  # 1 sync per step; 2 async collectives per step
+    for y in res[0][0]:
+        assert torch.equal(y, runner(x))
