@@ -176,6 +176,7 @@ def _load():
     _sig(lib, "hz_prog_add_diag", c_int, P, c_int, c_int, c_int, P, P, c_long, c_int)
     _sig(lib, "hz_prog_replay_n", c_int, P, P, c_int)
     _sig(lib, "hz_launch_kernel", c_int, c_int, P, P)
+    _sig(lib, "hz_experiments", c_int)
     _sig(lib, "hz_prog_add_kernel", c_int, P, c_int, P, C.c_size_t, c_int)
     _sig(lib, "hz_lstm_cell_launch", c_int, C.POINTER(LstmParams), P)
     _sig(lib, "hz_decoder_launch", c_int, C.POINTER(DecoderParams), P)
@@ -261,6 +262,12 @@ def lib():
                 _b.build(verbose=False, debug=DEBUG)
             _lib = _load()
     return _lib
+
+
+def experiments() -> bool:
+    """The loaded library carries the HZ_EXPERIMENTS kernels (chain conv, M32 / LN-fold GEMM tiles,
+    256-row MX pipelines): ``python -m hipzap.build --experiments``, ``HIPZAP_LIB=.../libhipzap_exp.so``."""
+    return bool(lib().hz_experiments())
 
 
 def check(rc: int, what: str) -> None:

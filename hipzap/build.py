@@ -22,6 +22,9 @@ CSRC = PKG / "csrc"
 LIBDIR = PKG / "_lib"
 LIB = LIBDIR / "libhipzap.so"
 LIB_DEBUG = LIBDIR / "libhipzap_debug.so"  # -DHZ_DEBUG: device-side HZ_DCHECK contracts (csrc/common.h)
+# -DHZ_EXPERIMENTS=1: the measured-negative kernel variants (csrc/common.h); not part of the product
+# build, built on demand for re-measurement and selected with HIPZAP_LIB
+LIB_EXP = LIBDIR / "libhipzap_exp.so"
 # the RCCL communicator is its own library: only multi-GPU processes map the 570 MB librccl
 LIB_COMM = LIBDIR / "libhipzap_comm.so"
 COMM_SRC = CSRC / "comm"
@@ -39,25 +42,29 @@ def sources() -> list[Path]:
     return sorted([p for p in CSRC.iterdir() if p.suffix in (".hip", ".cpp")])
 
 
-def _flags(debug: bool) -> list[str]:
-    return COMMON + (["-DHZ_DEBUG"] if debug else [])
+def _flags(debug: bool, exp: bool = False) -> list[str]:
+    return COMMON + (["-DHZ_DEBUG"] if debug else []) + (["-DHZ_EXPERIMENTS=1"] if exp else [])
 
 
-def _hash(src: Path, debug: bool = False) -> str:
+def _variant(debug: bool, exp: bool) -> str:
+    return "-dbg" if debug else "-exp" if exp else ""
+
+
+def _hash(src: Path, debug: bool = False, exp: bool = False) -> str:
     h = hashlib.sha1()
-    h.update(" ".join(_flags(debug)).encode())
+    h.update(" ".join(_flags(debug, exp)).encode())
     h.update(src.read_bytes())
     for hdr in sorted(CSRC.glob("*.h")):  # headers are shared: any change invalidates all
         h.update(hdr.read_bytes())
     return h.hexdigest()[:16]
 
 
-def _compile(src: Path, debug: bool = False) -> Path:
-    obj = OBJDIR / f"{src.stem}{'-dbg' if debug else ''}-{_hash(src, debug)}.o"
+def _compile(src: Path, debug: bool = False, exp: bool = False) -> Path:
+    obj = OBJDIR / f"{src.stem}{_variant(debug, exp)}-{_hash(src, debug, exp)}.o"
     if obj.exists():
         return obj
     tmp = obj.with_suffix(".o.tmp")
-    cmd = [HIPCC, *_flags(debug), "-c", str(src), "-o", str(tmp)]
+    cmd = [HIPCC, *_flags(debug, exp), "-c", str(src), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
@@ -65,24 +72,28 @@ def _compile(src: Path, debug: bool = False) -> Path:
     return obj
 
 
-def build(verbose: bool = True, jobs: int | None = None, debug: bool = False) -> Path:
-    """Release library (``libhipzap.so``) or, with ``debug``, the HZ_DEBUG variant
-    (``libhipzap_debug.so``, loaded when ``HIPZAP_DEBUG=1``)."""
+def build(verbose: bool = True, jobs: int | None = None, debug: bool = False, experiments: bool = False) -> Path:
+    """Release library (``libhipzap.so``); with ``debug`` the HZ_DEBUG variant
+    (``libhipzap_debug.so``, loaded when ``HIPZAP_DEBUG=1``); with ``experiments`` the
+    HZ_EXPERIMENTS variant (``libhipzap_exp.so``, ``HIPZAP_LIB=...``)."""
     OBJDIR.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     srcs = sources()
-    lib = LIB_DEBUG if debug else LIB
+    exp = experiments and not debug
+    lib = LIB_DEBUG if debug else LIB_EXP if exp else LIB
+    var = _variant(debug, exp)
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, debug), srcs))
+        objs = list(ex.map(lambda s: _compile(s, debug, exp), srcs))
     live = {o.name for o in objs}
     stems = {s.stem for s in srcs}
     for stale in OBJDIR.glob("*.o"):  # objects of older source versions (of this variant)
-        stem = stale.name.rsplit("-", 2 if "-dbg-" in stale.name else 1)[0]
-        if stale.name not in live and ("-dbg-" in stale.name) == debug and stem in stems:
+        v = next((x for x in ("-dbg", "-exp") if f"{x}-" in stale.name), "")
+        stem = stale.name.rsplit("-", 2 if v else 1)[0]
+        if stale.name not in live and v == var and stem in stems:
             stale.unlink(missing_ok=True)
     key = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
-    stamp = LIBDIR / (".buildkey_debug" if debug else ".buildkey")
+    stamp = LIBDIR / (".buildkey_debug" if debug else ".buildkey_exp" if exp else ".buildkey")
     if lib.exists() and stamp.exists() and stamp.read_text() == key:
         if verbose:
             print(f"hipzap: {lib} up to date")
@@ -186,6 +197,9 @@ def build_templates(verbose: bool = True) -> list[Path]:
 if __name__ == "__main__":
     if "--templates" in sys.argv[1:]:
         build_templates(verbose=True)
+        sys.exit(0)
+    if "--experiments" in sys.argv[1:]:
+        build(verbose=True, experiments=True)
         sys.exit(0)
     build(verbose=True, debug="--debug" in sys.argv[1:])
     if "--debug" not in sys.argv[1:]:

@@ -69,23 +69,57 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int s = 0; s < kStemKS; ++s) wa[i][s] = ldw(p.w, 2 * cp + i, kStemKS, s, lane);
-  // ---- input patch (in zero-copy mode it is read straight from the pinned request buffer) ----
+  // ---- input patch (in zero-copy mode it is read straight from the pinned request buffer): every
+  // load of a thread issued before the first wait, one PCIe round trip ----
+  constexpr int RAWQ = kStemIH * 32, RAWL = (RAWQ + 511) / 512;                 // dword slots
+  constexpr int PIX = kStemIH * kStemIW, PIXL = (PIX + 511) / 512;               // patch pixels
+  float fv[PIXL][3];
   if (p.mode == 1) {
     // per row: the dwords covering bytes [(row, c_lo), (row, c_hi)) of the HWC image. An image is a
     // multiple of 4 bytes (launcher), so the rounded-up end never leaves the buffer.
     const int c_lo = max(ix0, 0), c_hi = min(ix0 + kStemIW, p.W);
     const unsigned* src = static_cast<const unsigned*>(p.src);
-    for (int q = tid; q < kStemIH * 32; q += 512) {
-      const int row = q >> 5, j = q & 31, iy = iy0 + row;
-      if ((unsigned)iy >= (unsigned)p.H || c_lo >= c_hi) continue;
-      const long rb = ((long)n * p.H + iy) * p.W;
-      const long d0 = ((rb + c_lo) * 3) >> 2, d1 = ((rb + c_hi) * 3 + 3) >> 2;
-      if (d0 + j < d1) raw[row * (kStemRawRow / 4) + j] = src[d0 + j];
+    unsigned rv[RAWL];
+    int rdst[RAWL];
+#pragma unroll
+    for (int i = 0; i < RAWL; ++i) {
+      const int q = tid + 512 * i, row = q >> 5, j = q & 31, iy = iy0 + row;
+      rdst[i] = -1;
+      rv[i] = 0u;
+      if (q < RAWQ && (unsigned)iy < (unsigned)p.H && c_lo < c_hi) {
+        const long rb = ((long)n * p.H + iy) * p.W;
+        const long d0 = ((rb + c_lo) * 3) >> 2, d1 = ((rb + c_hi) * 3 + 3) >> 2;
+        if (d0 + j < d1) {
+          rv[i] = src[d0 + j];
+          rdst[i] = row * (kStemRawRow / 4) + j;
+        }
+      }
     }
+#pragma unroll
+    for (int i = 0; i < RAWL; ++i)
+      if (rdst[i] >= 0) raw[rdst[i]] = rv[i];
     __syncthreads();
+  } else {
+    const float* src = static_cast<const float*>(p.src);
+#pragma unroll
+    for (int i = 0; i < PIXL; ++i) {
+      const int q = min(tid + 512 * i, PIX - 1), row = q / kStemIW, col = q - row * kStemIW;
+      const int iy = iy0 + row, ix = ix0 + col;
+      const bool in = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) fv[i][c] = in ? src[(((long)n * 3 + c) * p.H + iy) * p.W + ix] : 0.f;
+    }
   }
+  // folded-BN bias of this wave's channels, loaded now (off the epilogue's critical path)
+  const int g = lane >> 4;
+  f32x4 bias_r[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) bias_r[i] = *reinterpret_cast<const f32x4*>(p.bias + 16 * (2 * cp + i) + 4 * g);
   // ---- normalised bf16 patch [23][39][8] (channels 3..7 and out-of-image pixels are zero) ----
-  for (int q = tid; q < kStemIH * kStemIW; q += 512) {
+#pragma unroll
+  for (int i = 0; i < PIXL; ++i) {
+    const int q = tid + 512 * i;
+    if (q >= PIX) continue;
     const int row = q / kStemIW, col = q - row * kStemIW;
     const int iy = iy0 + row, ix = ix0 + col;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -98,9 +132,8 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) v[c] = (float)rr[off + c] * (1.0f / 255.0f);
       } else {
-        const float* src = static_cast<const float*>(p.src);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) v[c] = src[(((long)n * 3 + c) * p.H + iy) * p.W + ix];
+        for (int c = 0; c < 3; ++c) v[c] = fv[i][c];
       }
       if (p.norm) {
 #pragma unroll
@@ -113,7 +146,9 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
 
   // ---- 7x7/2 conv: wave -> pixel fragments fgrp, fgrp+4, fgrp+8 x channel fragments 2cp, 2cp+1 ----
   // k-step s, lane group g = lane>>4: tap 4s+g = (r, c) of the 7x7 window, 8 channels (pack_conv
-  // cin_pad 8: k = (r*7 + c)*8 + ch) = one 16-B pixel of the LDS patch.
+  // cin_pad 8: k = (r*7 + c)*8 + ch) = one 16-B pixel of the LDS patch. Waves with only two real
+  // fragments compute a clamped third one and discard it (no divergent branch in the loop); the B
+  // fragments of step s+1 are read while step s's MFMAs run.
   constexpr int FPW = (kStemNF + 3) / 4;  // 3
   int poff[FPW];
 #pragma unroll
@@ -125,19 +160,29 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
   f32x4 acc[FPW][2];
 #pragma unroll
   for (int fi = 0; fi < FPW; ++fi) acc[fi][0] = acc[fi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int g = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < kStemKS; ++s) {
-    const int tap = 4 * s + g, tp = min(tap, 48);  // (taps >= 49: zero weights, operand zeroed below)
+  auto load_b = [&](int s, bf16x8(&bv)[FPW]) {
+    const int tap = 4 * s + g, tp = min(tap, 48);  // taps >= 49: zero weights; the operand is zeroed
     const int r = tp / 7, c = tp - 7 * r;
     const int toff = (r * kStemIW + c) * 8;
 #pragma unroll
     for (int fi = 0; fi < FPW; ++fi) {
-      if (fgrp + 4 * fi >= kStemNF) continue;  // wave-uniform
-      bf16x8 bv = *reinterpret_cast<const bf16x8*>(img + poff[fi] + toff);
-      if (tap >= 49) bv = bf16x8{};  // K padding: zero weights, but the LDS bytes need not be finite
-      acc[fi][0] = mfma16(wa[0][s], bv, acc[fi][0]);
-      acc[fi][1] = mfma16(wa[1][s], bv, acc[fi][1]);
+      bv[fi] = *reinterpret_cast<const bf16x8*>(img + poff[fi] + toff);
+      if (tap >= 49) bv[fi] = bf16x8{};  // the LDS bytes need not be finite
+    }
+  };
+  bf16x8 bc[FPW], bn[FPW];
+  load_b(0, bc);
+#pragma unroll
+  for (int s = 0; s < kStemKS; ++s) {
+    if (s + 1 < kStemKS) load_b(s + 1, bn);
+#pragma unroll
+    for (int fi = 0; fi < FPW; ++fi) {
+      acc[fi][0] = mfma16(wa[0][s], bc[fi], acc[fi][0]);
+      acc[fi][1] = mfma16(wa[1][s], bc[fi], acc[fi][1]);
+    }
+    if (s + 1 < kStemKS) {
+#pragma unroll
+      for (int fi = 0; fi < FPW; ++fi) bc[fi] = bn[fi];
     }
   }
   // ---- bias + ReLU -> stem outputs in LDS (zero outside the stem image: the pool's padding) ----
@@ -150,7 +195,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ch = 16 * (2 * cp + i) + 4 * g;
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + ch);
+      const f32x4 bb = bias_r[i];
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][i][e] + bb[e], 0.f) : 0.f;
@@ -258,25 +303,45 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
       *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
     }
   }
+
+  // ---- folded-BN biases of every epilogue, loaded while the patch lands (not after the MFMAs) ----
+  const f32x4 bias1 = *reinterpret_cast<const f32x4*>(p.b1 + 16 * cf1 + 4 * g);
+  const f32x4 bias2 = *reinterpret_cast<const f32x4*>(p.b2 + 16 * cf2 + 4 * g);
+  f32x4 bias3[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    bias3[i] = *reinterpret_cast<const f32x4*>(p.b3 + 16 * (2 * wave + i) + 4 * g);
+    if constexpr (DS) bias3[i] += *reinterpret_cast<const f32x4*>(p.bd + 16 * (2 * wave + i) + 4 * g);
+  }
   __syncthreads();
 
-  // ---- conv1 (1x1, Cin -> 64) over the 100 halo pixels: wave -> fragments fg1, fg1+2, .. x cf1 ----
+  // ---- conv1 (1x1, Cin -> 64) over the 100 halo pixels: wave -> fragments fg1, fg1+2, .. x cf1.
+  // Waves with three real fragments compute a clamped fourth and discard it (no branch in the
+  // loop); the B fragments of k-step s+1 are read while step s's MFMAs run. ----
   {
+    int pp1[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) pp1[fi] = min(16 * (fg1 + 2 * fi) + l16, kBnNP - 1);
     f32x4 acc[4];
 #pragma unroll
     for (int fi = 0; fi < 4; ++fi) acc[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 bc[4], bn[4];
+    auto load_b = [&](int s, bf16x8(&bv)[4]) {
 #pragma unroll
-    for (int s = 0; s < KS1; ++s)
+      for (int fi = 0; fi < 4; ++fi) bv[fi] = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp1[fi], 4 * s + g, XCH) * 8);
+    };
+    load_b(0, bc);
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) {
-        const int f = fg1 + 2 * fi;
-        if (f >= kBnNF1) continue;  // wave-uniform
-        const int pp = min(16 * f + l16, kBnNP - 1);
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
-        acc[fi] = mfma16(a1[s], bv, acc[fi]);
+    for (int s = 0; s < KS1; ++s) {
+      if (s + 1 < KS1) load_b(s + 1, bn);
+#pragma unroll
+      for (int fi = 0; fi < 4; ++fi) acc[fi] = mfma16(a1[s], bc[fi], acc[fi]);
+      if (s + 1 < KS1) {
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi) bc[fi] = bn[fi];
       }
+    }
     const int ch = 16 * cf1 + 4 * g;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b1 + ch);
 #pragma unroll
     for (int fi = 0; fi < 4; ++fi) {
       const int f = fg1 + 2 * fi, pp = 16 * f + l16;
@@ -285,7 +350,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
       const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)p.H && (unsigned)(x0 - 1 + hx) < (unsigned)p.W;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][e] + bb[e], 0.f) : 0.f;  // conv2's zero padding
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][e] + bias1[e], 0.f) : 0.f;  // conv2's zero padding
       *reinterpret_cast<u32x2*>(T1 + t1_chunk(hy, hx, ch >> 3) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
     }
   }
@@ -297,16 +362,26 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     f32x4 acc[4];
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KS2 / 2; ++s) {
+    auto load_b = [&](int s, bf16x8(&bv)[4]) {
       const int ks = kh * (KS2 / 2) + s;  // k-step: tap ks>>1 (r, c), channel half ks&1
       const int tap = ks >> 1, r = tap / 3, c = tap - 3 * (tap / 3);
       const int chunk = (ks & 1) * 4 + g;
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         const int j = 16 * f + l16, hy = (j >> 3) + r, hx = (j & 7) + c;
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + t1_chunk(hy, hx, chunk) * 8);
-        acc[f] = mfma16(a2[s], bv, acc[f]);
+        bv[f] = *reinterpret_cast<const bf16x8*>(T1 + t1_chunk(hy, hx, chunk) * 8);
+      }
+    };
+    bf16x8 bc[4], bn[4];
+    load_b(0, bc);
+#pragma unroll
+    for (int s = 0; s < KS2 / 2; ++s) {
+      if (s + 1 < KS2 / 2) load_b(s + 1, bn);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] = mfma16(a2[s], bc[f], acc[f]);
+      if (s + 1 < KS2 / 2) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) bc[f] = bn[f];
       }
     }
     const int give = kh ? 0 : 2, keep = kh ? 2 : 0;
@@ -314,66 +389,84 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     RED[wave][1][lane] = acc[give + 1];
     __syncthreads();
     const int ch = 16 * cf2 + 4 * g;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + ch);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const f32x4 o = RED[wave ^ 4][i][lane];
       const int j = 16 * (keep + i) + l16;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[keep + i][e] + o[e] + bb[e], 0.f);
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[keep + i][e] + o[e] + bias2[e], 0.f);
       *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 8) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
     }
   }
   __syncthreads();
 
   // ---- conv3 (1x1, 64 -> 256) + residual (identity or the downsample 1x1 in the same
-  // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments ----
+  // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments. Every LDS
+  // operand (and the identity residual) is read before the first MFMA. ----
   {
-    f32x4 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 b3[KS3][4];
 #pragma unroll
     for (int s = 0; s < KS3; ++s)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const int j = 16 * f + l16;
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 8) * 8);
-        acc[0][f] = mfma16(a3[0][s], bv, acc[0][f]);
-        acc[1][f] = mfma16(a3[1][s], bv, acc[1][f]);
-      }
+      for (int f = 0; f < 4; ++f)
+        b3[s][f] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(16 * f + l16, 4 * s + g, 8) * 8);
+    bf16x8 bd[DS ? KSD : 1][4];
+    u32x2 rr[2][4];
     if constexpr (DS) {
 #pragma unroll
       for (int s = 0; s < KSD; ++s)
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           const int j = 16 * f + l16, pp = ((j >> 3) + 1) * kBnWT + (j & 7) + 1;
-          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
-          acc[0][f] = mfma16(ad[0][s], bv, acc[0][f]);
-          acc[1][f] = mfma16(ad[1][s], bv, acc[1][f]);
+          bd[s][f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
+        }
+    } else {  // identity residual: the centre of the staged input patch (Cin == 256)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int ch = 16 * (2 * wave + i) + 4 * g, j = 16 * f + l16;
+          const int pp = ((j >> 3) + 1) * kBnWT + (j & 7) + 1;
+          rr[i][f] = *reinterpret_cast<const u32x2*>(X + x_chunk(pp, ch >> 3, XCH) * 8 + (ch & 4));
+        }
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[i][f] = bias3[i];
+#pragma unroll
+    for (int s = 0; s < KS3; ++s)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        acc[0][f] = mfma16(a3[0][s], b3[s][f], acc[0][f]);
+        acc[1][f] = mfma16(a3[1][s], b3[s][f], acc[1][f]);
+      }
+    if constexpr (DS) {
+#pragma unroll
+      for (int s = 0; s < KSD; ++s)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          acc[0][f] = mfma16(ad[0][s], bd[s][f], acc[0][f]);
+          acc[1][f] = mfma16(ad[1][s], bd[s][f], acc[1][f]);
         }
     }
     const int CO32 = kBnCO / 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ch = 16 * (2 * wave + i) + 4 * g;
-      f32x4 bb = *reinterpret_cast<const f32x4*>(p.b3 + ch);
-      if constexpr (DS) bb += *reinterpret_cast<const f32x4*>(p.bd + ch);
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         const int j = 16 * f + l16, jy = j >> 3, jx = j & 7;
         float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][f][e] + bb[e];
-        if constexpr (!DS) {  // identity residual: the centre of the staged input patch (Cin == 256)
-          const int pp = (jy + 1) * kBnWT + jx + 1;
-          const u32x2 rr = *reinterpret_cast<const u32x2*>(X + x_chunk(pp, ch >> 3, XCH) * 8 + (ch & 4));
-          v[0] += __uint_as_float(rr[0] << 16);
-          v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-          v[2] += __uint_as_float(rr[1] << 16);
-          v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][f][e];
+        if constexpr (!DS) {
+          v[0] += __uint_as_float(rr[i][f][0] << 16);
+          v[1] += __uint_as_float(rr[i][f][0] & 0xffff0000u);
+          v[2] += __uint_as_float(rr[i][f][1] << 16);
+          v[3] += __uint_as_float(rr[i][f][1] & 0xffff0000u);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);

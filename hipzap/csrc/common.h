@@ -13,6 +13,16 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 #define HZ_WAVE 64
 
+// HZ_EXPERIMENTS=1 (python -m hipzap.build --experiments -> libhipzap_exp.so, selected with
+// HIPZAP_LIB): kernel variants that were built, measured and LOST against the defaults, kept for
+// re-measurement but not shipped in the product library: the persistent conv
+// chain (conv.hip, profiles/r3_chain), the 32x32x16 LDS-GEMM tiles cfg 64-77 (gemm.hip,
+// profiles/r3_m32), the folded-LayerNorm GEMM epilogue (gemm.hip, profiles/r1_ab/bert_lnfold.txt)
+// and the 256-row MX pipelines cfg 43-47 (fp8.hip, profiles/r3_mxk).
+#ifndef HZ_EXPERIMENTS
+#define HZ_EXPERIMENTS 0
+#endif
+
 // ---- DEBUG kernel variant (SURVEY.md §5 "bounds-check asserts in a DEBUG kernel variant") ----
 // `python -m hipzap.build --debug` compiles every source with -DHZ_DEBUG into
 // hipzap/_lib/libhipzap_debug.so; HIPZAP_DEBUG=1 makes hipzap._native load that library.

@@ -448,6 +448,7 @@ extern "C" int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int
   }
 }
 
+#if HZ_EXPERIMENTS
 // ---------------------------------------------------------------------------------------------
 // Persistent conv chain (HzConvChainParams, hipzap.h): a run of dependent convs -- e.g. ResNet-50
 // layer3 + layer4 at bs=1, 26 convs in 17 stages -- as ONE launch instead of one launch per conv.
@@ -583,6 +584,11 @@ extern "C" int hz_conv_chain_launch(const HzConvChainParams* cpp, hipStream_t st
   hipLaunchKernelGGL(conv_chain_kernel, dim3(cp.grid), dim3(kChainThreads), (size_t)cp.lds, st, cp);
   return (int)hipGetLastError();
 }
+
+#else   // !HZ_EXPERIMENTS: the chain kernel is not in the product library
+extern "C" int hz_conv_chain_prepare(HzChainLayer*, int, int*, int) { return -99; }
+extern "C" int hz_conv_chain_launch(const HzConvChainParams*, hipStream_t) { return -99; }
+#endif
 
 // Load this translation unit's device code now (hipFuncGetAttributes makes the runtime load the
 // code object of the fatbin that holds the kernel, without a launch or a stream): the plan loader

@@ -798,6 +798,7 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
+#if HZ_EXPERIMENTS
       // 256-row kernel (branch-free main loop, pinned read / MFMA order): 256x256 / 2 stages,
       // 256x128 / 2 and 3 stages
       case 43: return launch_mxq<256, 2>(p, st);
@@ -807,6 +808,7 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       // 256x256 tile needs 128 accumulators + 96 operand registers per lane: it spills)
       case 46: return launch_mxk<128, 3>(p, st);
       case 47: return launch_mxk<128, 2>(p, st);
+#endif
       default: return -2;
     }
   }

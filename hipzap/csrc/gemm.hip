@@ -432,8 +432,8 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
     }
   }
   if (p.lnf) {  // the folded-LayerNorm statistics slabs assume 2 feature halves per tile
-    if constexpr (WN != 2 || M32) {
-      return -3;
+    if constexpr (WN != 2 || M32 || !HZ_EXPERIMENTS) {
+      return -3;  // (the LN-fold epilogue is an experiment: not in the product library)
     } else {
       hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
     }
@@ -469,6 +469,7 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
       case 31: return launch_lds<128, 64, 3, 4, 2, true>(p, st);
       case 32: return launch_lds<64, 128, 3, 2, 4, true>(p, st);
       case 33: return launch_lds<256, 64, 2, 4, 2, true>(p, st);
+#if HZ_EXPERIMENTS
       // 64-77: mfma_f32_32x32x16_bf16 tiles (M32)
       case 64: return launch_lds<128, 128, 2, 2, 2, true, true>(p, st);
       case 65: return launch_lds<128, 128, 3, 2, 2, true, true>(p, st);
@@ -478,6 +479,7 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
       case 71: return launch_lds<128, 64, 3, 4, 2, true, true>(p, st);
       case 72: return launch_lds<64, 128, 2, 2, 2, true, true>(p, st);
       case 76: return launch_lds<128, 64, 2, 2, 2, true, true>(p, st);
+#endif
       default: return -2;
     }
   }
@@ -511,6 +513,7 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
     case 38: return launch_lds<64, 288, 3, 2, 2>(p, st);
     case 39: return launch_lds<256, 96, 2, 2, 2>(p, st);
     case 40: return launch_lds<64, 96, 4, 2, 2>(p, st);
+#if HZ_EXPERIMENTS
     // 64-77: the LDS image read as mfma_f32_32x32x16_bf16 operands (32-aligned wave tiles)
     case 64: return launch_lds<128, 128, 2, 2, 2, false, true>(p, st);
     case 65: return launch_lds<128, 128, 3, 2, 2, false, true>(p, st);
@@ -526,6 +529,7 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
     case 75: return launch_lds<64, 192, 2, 2, 2, false, true>(p, st);
     case 76: return launch_lds<128, 64, 2, 2, 2, false, true>(p, st);
     case 77: return launch_lds<256, 256, 2, 4, 2, false, true>(p, st);
+#endif
     default: return -2;
   }
 }

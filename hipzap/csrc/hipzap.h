@@ -436,6 +436,7 @@ enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
        HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17, HZ_K_STEM = 18, HZ_K_BNECK = 19 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
+int hz_experiments(void);  // 1: built with HZ_EXPERIMENTS (measured-negative kernel variants)
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind
 int hz_prog_add_kernel(HzProgram p, int kind, const void* params, size_t size, int slot);
 

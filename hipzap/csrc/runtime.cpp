@@ -16,6 +16,7 @@
 #include <thread>
 #include <vector>
 
+#include "common.h"
 #include "hipzap.h"
 
 namespace {
@@ -266,6 +267,9 @@ int hz_serve_bench(HzProgram* progs, hipStream_t* streams, void** in_dst, void**
 }
 
 }  // extern "C"
+
+// 1 when this library was built with the measured-negative experiment kernels (HZ_EXPERIMENTS)
+extern "C" int hz_experiments(void) { return HZ_EXPERIMENTS; }
 
 extern "C" int hz_prog_replay_n(HzProgram h, hipStream_t st, int n) {
   for (int i = 0; i < n; ++i) {

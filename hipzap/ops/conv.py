@@ -196,10 +196,11 @@ def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv
     """All legal (cfg, kw) launch choices worth timing for one conv / GEMM shape."""
     steps = max(1, math.ceil(K / 32))
     out = []
+    exp = N.experiments()  # the 32x32 (M32) tiles exist only in the HZ_EXPERIMENTS library
     if lds_ok(M, K, rowmajor, pc):
-        out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout)]
+        out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout) and (exp or cfg not in M32_CFGS)]
     elif not rowmajor and lds_conv_ok(M, pc):
-        out += [(cfg, 1) for cfg in LDS_CONV_CFGS if lds_conv_fits(cfg, cout)]
+        out += [(cfg, 1) for cfg in LDS_CONV_CFGS if lds_conv_fits(cfg, cout) and (exp or cfg not in M32_CFGS)]
     for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue

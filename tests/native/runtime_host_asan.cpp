@@ -38,6 +38,8 @@ STUB(hz_lmb_layer_launch, HzLmbLayerParams, 14, H)
 STUB(hz_lmb_dec_launch, HzLmbDecParams, 15, V)
 STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
 STUB(hz_conv_chain_launch, HzConvChainParams, 17, n_layers)
+STUB(hz_stem_launch, HzStemParams, 18, N)
+STUB(hz_bneck_launch, HzBneckParams, 19, N)
 extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
   g_calls.push_back(18);
   g_vals.push_back(n);

@@ -13,6 +13,14 @@ from hipzap.models import registry
 from hipzap.models.resnet import randomize_bn
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _experiments_lib():
+    """The chain kernel is a measured negative (profiles/r3_chain): HZ_EXPERIMENTS library only."""
+    from hipzap import _native as N
+    if not N.experiments():
+        pytest.skip("conv chain: build with python -m hipzap.build --experiments, run with HIPZAP_LIB")
 DEV = "cuda:0"
 
 

@@ -47,7 +47,8 @@ def _fused_tensors(ctx):
 
 
 @pytest.mark.parametrize("uint8,batch", [(True, 1), (False, 1), (True, 3)])
-def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch):
+def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, monkeypatch):
+    monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")  # every intermediate stays readable after the run
     a, params, params_cpu, kw = r50
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=uint8))
     fused = ExecContext(g, params, torch.device(DEV), fuse="all")

@@ -82,6 +82,9 @@ def test_lds_gemm_m32_matches_16x16(m32, base):
     """The 32x32x16-MFMA tiles (csrc/gemm.hip M32) read the same LDS image through a different
     lane map: against the 16x16x32 kernel in fp32 output they agree to summation-order rounding,
     so a wrong operand or accumulator map (even one that permutes a few k) cannot hide."""
+    from hipzap import _native as NN
+    if not NN.experiments():
+        pytest.skip("M32 tiles are a measured negative: python -m hipzap.build --experiments")
     M, N, K = 520, 768, 1024
     g = torch.Generator().manual_seed(5)
     w = torch.randn(N, K, generator=g) * 0.03
@@ -96,6 +99,9 @@ def test_lds_gemm_m32_matches_16x16(m32, base):
 def test_bert_engine_matches_hf(ln_fold, monkeypatch):
     """ln_fold=1: LayerNorms folded into the LDS GEMM epilogues (HzLnFold); LayerNorm affine
     params randomised so a wrong fold cannot hide behind gamma=1, beta=0."""
+    from hipzap import _native as N
+    if ln_fold == "1" and not N.experiments():
+        pytest.skip("the LN-fold GEMM epilogue is a measured negative: python -m hipzap.build --experiments")
     monkeypatch.setenv("HIPZAP_LN_FOLD", ln_fold)
     torch.manual_seed(0)
     m = bert.make_model(num_labels=2)
