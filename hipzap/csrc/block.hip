@@ -28,6 +28,14 @@
 
 HZ_DEBUG_UNIT(block)
 
+// phase timestamps for scripts/native/block_stamps.hip (which defines them before including this
+// file); empty in the library
+#ifndef HZ_BSTAMP
+#define HZ_BSTAMP_DECL
+#define HZ_BSTAMP(i)
+#define HZ_BSTAMP_FLUSH(kind)
+#endif
+
 namespace {
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -60,6 +68,8 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
   const int py0 = ty * kStemPH, px0 = tx * kStemPW;
   const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;  // stem-output origin of the patch
   const int iy0 = 2 * sy0 - 3, ix0 = 2 * sx0 - 3;  // input origin
+  HZ_BSTAMP_DECL
+  HZ_BSTAMP(0);
 
   // ---- weights first (L2/MALL-resident, back before the input bytes cross PCIe): wave ->
   // output-channel fragments {2cp, 2cp+1}, all 13 k-steps (26 x 16 B per lane) ----
@@ -143,6 +153,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
     *reinterpret_cast<u32x4*>(img + q * 8) = pack8(v);
   }
   __syncthreads();
+  HZ_BSTAMP(1);
 
   // ---- 7x7/2 conv: wave -> pixel fragments fgrp, fgrp+4, fgrp+8 x channel fragments 2cp, 2cp+1 ----
   // k-step s, lane group g = lane>>4: tap 4s+g = (r, c) of the 7x7 window, 8 channels (pack_conv
@@ -185,6 +196,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
       for (int fi = 0; fi < FPW; ++fi) bc[fi] = bn[fi];
     }
   }
+  HZ_BSTAMP(2);
   // ---- bias + ReLU -> stem outputs in LDS (zero outside the stem image: the pool's padding) ----
 #pragma unroll
   for (int fi = 0; fi < FPW; ++fi) {
@@ -203,6 +215,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
     }
   }
   __syncthreads();
+  HZ_BSTAMP(3);
   // ---- 3x3/2 max-pool (pad 1): every value is >= 0 after the ReLU and every window holds a real
   // output, so the zeros written for out-of-image positions never win ----
   {
@@ -226,6 +239,8 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
       *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(m[0], m[1]), pack2(m[2], m[3])};
     }
   }
+  HZ_BSTAMP(4);
+  HZ_BSTAMP_FLUSH(0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -259,6 +274,8 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   const int ty = rem / tx_n, tx = rem - ty * tx_n;
   const int y0 = ty * kBnTH, x0 = tx * kBnTW;
   const int CB = CIN / 32;
+  HZ_BSTAMP_DECL
+  HZ_BSTAMP(0);
 
   // ---- input patch loads (10 x 10 x Cin, zero outside the image); chunk order keeps a halo row of
   // one 32-channel block contiguous in global memory ----
@@ -314,6 +331,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     if constexpr (DS) bias3[i] += *reinterpret_cast<const f32x4*>(p.bd + 16 * (2 * wave + i) + 4 * g);
   }
   __syncthreads();
+  HZ_BSTAMP(1);
 
   // ---- conv1 (1x1, Cin -> 64) over the 100 halo pixels: wave -> fragments fg1, fg1+2, .. x cf1.
   // Waves with three real fragments compute a clamped fourth and discard it (no branch in the
@@ -355,6 +373,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     }
   }
   __syncthreads();
+  HZ_BSTAMP(2);
 
   // ---- conv2 (3x3, 64 -> 64): wave -> channel fragment cf2, K half kh (9 of 18 k-steps), all 4
   // pixel fragments; the two halves meet through LDS (kh 0 finishes fragments 0-1, kh 1 2-3) ----
@@ -400,6 +419,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     }
   }
   __syncthreads();
+  HZ_BSTAMP(3);
 
   // ---- conv3 (1x1, 64 -> 256) + residual (identity or the downsample 1x1 in the same
   // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments. Every LDS
@@ -452,6 +472,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
           acc[1][f] = mfma16(ad[1][s], bd[s][f], acc[1][f]);
         }
     }
+    HZ_BSTAMP(4);
     const int CO32 = kBnCO / 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -475,6 +496,8 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
       }
     }
   }
+  HZ_BSTAMP(5);
+  HZ_BSTAMP_FLUSH(CIN == 64 ? 1 : 2);
 }
 
 }  // namespace
