@@ -245,10 +245,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
 
 // ------------------------------------------------------------------------------------------------
 // bottleneck block (layer1 geometry: Cmid 64, Cout 256, stride 1)
-constexpr int kBnTH = 8, kBnTW = 8;                              // output tile
-constexpr int kBnHT = kBnTH + 2, kBnWT = kBnTW + 2;             // conv1 halo tile
-constexpr int kBnNP = kBnHT * kBnWT;                             // 100 halo pixels
-constexpr int kBnNF1 = (kBnNP + 15) / 16;                        // 7 fragments
+constexpr int kBnTW = 8, kBnWT = kBnTW + 2;  // output tile width, conv1 halo width (TH rows: template)
 constexpr int kBnCM = 64, kBnCO = 256;
 
 // LDS images: [pixel][channels] bf16, 16-B chunks XOR-swizzled per pixel
@@ -258,8 +255,14 @@ __device__ __forceinline__ int t1_chunk(int hy, int hx, int c) {
   return (hy * kBnWT + hx) * 8 + (c ^ ((2 * hx + 2 * hy) & 7));
 }
 
-template <int CIN, bool DS>
+template <int CIN, bool DS, int TH>
 __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
+  constexpr int kBnTH = TH;                          // output tile rows (8 or 4)
+  constexpr int kBnNP = (TH + 2) * kBnWT;            // conv1 halo pixels: 100 / 60
+  constexpr int kBnNF1 = (kBnNP + 15) / 16;          // 7 / 4 fragments
+  constexpr int FI1 = (kBnNF1 + 1) / 2;              // conv1 fragments per wave (parity split)
+  constexpr int NF2 = TH * kBnTW / 16;               // output-pixel fragments: 4 / 2
+  constexpr int HALF = NF2 / 2;                      // conv2 fragments finished per K half
   constexpr int XCH = CIN / 8;                       // 16-B chunks per input pixel
   constexpr int KS1 = CIN / 32, KS2 = 9 * kBnCM / 32, KS3 = kBnCM / 32, KSD = CIN / 32;
   constexpr int NQ = kBnNP * XCH, NL = (NQ + 511) / 512;
@@ -337,31 +340,31 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   // Waves with three real fragments compute a clamped fourth and discard it (no branch in the
   // loop); the B fragments of k-step s+1 are read while step s's MFMAs run. ----
   {
-    int pp1[4];
+    int pp1[FI1];
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) pp1[fi] = min(16 * (fg1 + 2 * fi) + l16, kBnNP - 1);
-    f32x4 acc[4];
+    for (int fi = 0; fi < FI1; ++fi) pp1[fi] = min(16 * (fg1 + 2 * fi) + l16, kBnNP - 1);
+    f32x4 acc[FI1];
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) acc[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 bc[4], bn[4];
-    auto load_b = [&](int s, bf16x8(&bv)[4]) {
+    for (int fi = 0; fi < FI1; ++fi) acc[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 bc[FI1], bn[FI1];
+    auto load_b = [&](int s, bf16x8(&bv)[FI1]) {
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) bv[fi] = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp1[fi], 4 * s + g, XCH) * 8);
+      for (int fi = 0; fi < FI1; ++fi) bv[fi] = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp1[fi], 4 * s + g, XCH) * 8);
     };
     load_b(0, bc);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       if (s + 1 < KS1) load_b(s + 1, bn);
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) acc[fi] = mfma16(a1[s], bc[fi], acc[fi]);
+      for (int fi = 0; fi < FI1; ++fi) acc[fi] = mfma16(a1[s], bc[fi], acc[fi]);
       if (s + 1 < KS1) {
 #pragma unroll
-        for (int fi = 0; fi < 4; ++fi) bc[fi] = bn[fi];
+        for (int fi = 0; fi < FI1; ++fi) bc[fi] = bn[fi];
       }
     }
     const int ch = 16 * cf1 + 4 * g;
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) {
+    for (int fi = 0; fi < FI1; ++fi) {
       const int f = fg1 + 2 * fi, pp = 16 * f + l16;
       if (f >= kBnNF1 || pp >= kBnNP) continue;
       const int hy = pp / kBnWT, hx = pp - hy * kBnWT;
@@ -378,38 +381,38 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   // ---- conv2 (3x3, 64 -> 64): wave -> channel fragment cf2, K half kh (9 of 18 k-steps), all 4
   // pixel fragments; the two halves meet through LDS (kh 0 finishes fragments 0-1, kh 1 2-3) ----
   {
-    f32x4 acc[4];
+    f32x4 acc[NF2];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto load_b = [&](int s, bf16x8(&bv)[4]) {
+    for (int f = 0; f < NF2; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto load_b = [&](int s, bf16x8(&bv)[NF2]) {
       const int ks = kh * (KS2 / 2) + s;  // k-step: tap ks>>1 (r, c), channel half ks&1
       const int tap = ks >> 1, r = tap / 3, c = tap - 3 * (tap / 3);
       const int chunk = (ks & 1) * 4 + g;
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < NF2; ++f) {
         const int j = 16 * f + l16, hy = (j >> 3) + r, hx = (j & 7) + c;
         bv[f] = *reinterpret_cast<const bf16x8*>(T1 + t1_chunk(hy, hx, chunk) * 8);
       }
     };
-    bf16x8 bc[4], bn[4];
+    bf16x8 bc[NF2], bn[NF2];
     load_b(0, bc);
 #pragma unroll
     for (int s = 0; s < KS2 / 2; ++s) {
       if (s + 1 < KS2 / 2) load_b(s + 1, bn);
 #pragma unroll
-      for (int f = 0; f < 4; ++f) acc[f] = mfma16(a2[s], bc[f], acc[f]);
+      for (int f = 0; f < NF2; ++f) acc[f] = mfma16(a2[s], bc[f], acc[f]);
       if (s + 1 < KS2 / 2) {
 #pragma unroll
-        for (int f = 0; f < 4; ++f) bc[f] = bn[f];
+        for (int f = 0; f < NF2; ++f) bc[f] = bn[f];
       }
     }
-    const int give = kh ? 0 : 2, keep = kh ? 2 : 0;
-    RED[wave][0][lane] = acc[give];
-    RED[wave][1][lane] = acc[give + 1];
+    const int give = kh ? 0 : HALF, keep = kh ? HALF : 0;
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) RED[wave][i][lane] = acc[give + i];
     __syncthreads();
     const int ch = 16 * cf2 + 4 * g;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < HALF; ++i) {
       const f32x4 o = RED[wave ^ 4][i][lane];
       const int j = 16 * (keep + i) + l16;
       float v[4];
@@ -425,19 +428,19 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments. Every LDS
   // operand (and the identity residual) is read before the first MFMA. ----
   {
-    bf16x8 b3[KS3][4];
+    bf16x8 b3[KS3][NF2];
 #pragma unroll
     for (int s = 0; s < KS3; ++s)
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int f = 0; f < NF2; ++f)
         b3[s][f] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(16 * f + l16, 4 * s + g, 8) * 8);
-    bf16x8 bd[DS ? KSD : 1][4];
-    u32x2 rr[2][4];
+    bf16x8 bd[DS ? KSD : 1][NF2];
+    u32x2 rr[2][NF2];
     if constexpr (DS) {
 #pragma unroll
       for (int s = 0; s < KSD; ++s)
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
+        for (int f = 0; f < NF2; ++f) {
           const int j = 16 * f + l16, pp = ((j >> 3) + 1) * kBnWT + (j & 7) + 1;
           bd[s][f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(pp, 4 * s + g, XCH) * 8);
         }
@@ -445,21 +448,21 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
+        for (int f = 0; f < NF2; ++f) {
           const int ch = 16 * (2 * wave + i) + 4 * g, j = 16 * f + l16;
           const int pp = ((j >> 3) + 1) * kBnWT + (j & 7) + 1;
           rr[i][f] = *reinterpret_cast<const u32x2*>(X + x_chunk(pp, ch >> 3, XCH) * 8 + (ch & 4));
         }
     }
-    f32x4 acc[2][4];
+    f32x4 acc[2][NF2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) acc[i][f] = bias3[i];
+      for (int f = 0; f < NF2; ++f) acc[i][f] = bias3[i];
 #pragma unroll
     for (int s = 0; s < KS3; ++s)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < NF2; ++f) {
         acc[0][f] = mfma16(a3[0][s], b3[s][f], acc[0][f]);
         acc[1][f] = mfma16(a3[1][s], b3[s][f], acc[1][f]);
       }
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
 #pragma unroll
       for (int s = 0; s < KSD; ++s)
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
+        for (int f = 0; f < NF2; ++f) {
           acc[0][f] = mfma16(ad[0][s], bd[s][f], acc[0][f]);
           acc[1][f] = mfma16(ad[1][s], bd[s][f], acc[1][f]);
         }
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     for (int i = 0; i < 2; ++i) {
       const int ch = 16 * (2 * wave + i) + 4 * g;
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < NF2; ++f) {
         const int j = 16 * f + l16, jy = j >> 3, jx = j & 7;
         float v[4];
 #pragma unroll
@@ -516,11 +519,20 @@ extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
 
 extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   const HzBneckParams& p = *pp;
-  if (p.N < 1 || p.H % kBnTH || p.W % kBnTW || p.Cmid != kBnCM || p.Cout != kBnCO) return -1;
-  const int tiles = (p.H / kBnTH) * (p.W / kBnTW) * p.N;
-  if (p.Cin == 64 && p.wd && p.bd) hipLaunchKernelGGL((bneck_kernel<64, true>), dim3(tiles), dim3(512), 0, st, p);
-  else if (p.Cin == 256 && !p.wd) hipLaunchKernelGGL((bneck_kernel<256, false>), dim3(tiles), dim3(512), 0, st, p);
-  else return -1;
+  const int th = p.tile_h ? p.tile_h : 8;
+  if (p.N < 1 || (th != 8 && th != 4) || p.H % th || p.W % kBnTW || p.Cmid != kBnCM || p.Cout != kBnCO) return -1;
+  const int tiles = (p.H / th) * (p.W / kBnTW) * p.N;
+#define HZ_BNL(CIN, DS)                                                                               \
+  if (th == 8) hipLaunchKernelGGL((bneck_kernel<CIN, DS, 8>), dim3(tiles), dim3(512), 0, st, p);     \
+  else hipLaunchKernelGGL((bneck_kernel<CIN, DS, 4>), dim3(tiles), dim3(512), 0, st, p);
+  if (p.Cin == 64 && p.wd && p.bd) {
+    HZ_BNL(64, true)
+  } else if (p.Cin == 256 && !p.wd) {
+    HZ_BNL(256, false)
+  } else {
+    return -1;
+  }
+#undef HZ_BNL
   return (int)hipGetLastError();
 }
 

@@ -425,6 +425,7 @@ typedef struct HzBneckParams {
   const float* bd;
   unsigned short* out;        // [N][Cout/32][H][W][32]
   int N, H, W, Cin, Cmid, Cout;
+  int tile_h, pad_;           // output tile rows: 8 (default when 0) or 4 (twice the workgroups)
 } HzBneckParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);

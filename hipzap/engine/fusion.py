@@ -38,7 +38,7 @@ class BneckParams(C.Structure):  # HzBneckParams
     _fields_ = [("x", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p),
                 ("b2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("wd", C.c_void_p),
                 ("bd", C.c_void_p), ("out", C.c_void_p), ("N", C.c_int), ("H", C.c_int), ("W", C.c_int),
-                ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int)]
+                ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int), ("tile_h", C.c_int), ("pad_", C.c_int)]
 
 
 @dataclass
@@ -124,7 +124,7 @@ def match_bneck(g, params, i: int) -> Fused | None:
         if pd is None or not _geom(pd, 64, 256, 1, 1, 0) or ds.attrs.get("act", "relu") != "none":
             return None
     nb, h, w, c = g.shape(x)
-    if c != cin or h % 8 or w % 8:
+    if c != cin or h % 8 or w % 8:  # (8x8 or 4x8 output tiles)
         return None
     return Fused("bneck", i, i + len(grp), grp)
 
@@ -191,6 +191,7 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
         p.wd, p.bd = pd.wf.data_ptr(), pd.bias.data_ptr()
     p.N, p.H, p.W, p.Cin = g.shape(c1.inputs[0])
     p.Cmid, p.Cout = p1.cout, p3.cout
+    p.tile_h = int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # output tile rows (8: 49 workgroups at 56x56)
     return p
 
 

@@ -14,13 +14,18 @@
 #include <vector>
 
 __device__ unsigned long long g_bstamps[3][512][6];
+__device__ unsigned long long g_bclock[3][512][2];  // s_memtime (shader clock) at the first / last stamp
 #define HZ_BSTAMP 1
-#define HZ_BSTAMP_DECL unsigned long long hz_bst[6] = {0, 0, 0, 0, 0, 0};
+#define HZ_BSTAMP_DECL unsigned long long hz_bst[6] = {0, 0, 0, 0, 0, 0}, hz_clk0 = __builtin_amdgcn_s_memtime();
 #define HZ_BSTAMP(i) hz_bst[i] = __builtin_amdgcn_s_memrealtime()
 #define HZ_BSTAMP_FLUSH(kind)                                                            \
   do {                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < 512)                                            \
+    const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                      \
+    if (threadIdx.x == 0 && blockIdx.x < 512) {                                          \
       for (int i_ = 0; i_ < 6; ++i_) g_bstamps[kind][blockIdx.x][i_] = hz_bst[i_];       \
+      g_bclock[kind][blockIdx.x][0] = hz_clk0;                                           \
+      g_bclock[kind][blockIdx.x][1] = clk1_;                                             \
+    }                                                                                    \
   } while (0)
 #include "../../hipzap/csrc/block.hip"
 
@@ -50,8 +55,13 @@ static void* dev_random(size_t bytes, unsigned seed, bool bf16) {
 }
 
 static int report(const char* name, int kind, int nwg, int nph, double launch_us) {
-  unsigned long long h[512][6];
+  unsigned long long h[512][6], ck[512][2];
   CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bstamps), sizeof(h), (size_t)kind * sizeof(h), hipMemcpyDeviceToHost));
+  CK(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_bclock), sizeof(ck), (size_t)kind * sizeof(ck), hipMemcpyDeviceToHost));
+  std::vector<double> mhz;
+  for (int b = 0; b < nwg; ++b)
+    if (h[b][nph - 1] > h[b][0]) mhz.push_back((double)(ck[b][1] - ck[b][0]) / (double)(h[b][nph - 1] - h[b][0]) * 100.0);
+  std::sort(mhz.begin(), mhz.end());
   std::printf("{\"kernel\": \"%s\", \"workgroups\": %d, \"graph_launch_us\": %.2f, \"phase_us_median\": [", name, nwg,
               launch_us);
   for (int ph = 1; ph < nph; ++ph) {
@@ -68,8 +78,8 @@ static int report(const char* name, int kind, int nwg, int nph, double launch_us
   std::vector<double> st;
   for (int b = 0; b < nwg; ++b) st.push_back((double)(h[b][0] - t0) * 0.01);
   std::sort(st.begin(), st.end());
-  std::printf("], \"first_to_last_us\": %.2f, \"start_skew_us_p50_max\": [%.2f, %.2f]}\n", (double)(t1 - t0) * 0.01,
-              st[st.size() / 2], st.back());
+  std::printf("], \"first_to_last_us\": %.2f, \"start_skew_us_p50_max\": [%.2f, %.2f], \"shader_mhz_p50\": %.0f}\n",
+              (double)(t1 - t0) * 0.01, st[st.size() / 2], st.back(), mhz.empty() ? 0.0 : mhz[mhz.size() / 2]);
   return 0;
 }
 
@@ -81,7 +91,7 @@ static double graph_us(F launch, hipStream_t st, int n) {
   for (int i = 0; i < n; ++i) launch();
   (void)hipStreamEndCapture(st, &g);
   (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-  (void)hipGraphLaunch(ge, st);
+  for (int w = 0; w < 30; ++w) (void)hipGraphLaunch(ge, st);  // ~clock ramp before the timed replays
   (void)hipStreamSynchronize(st);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
@@ -114,6 +124,7 @@ int main() {
   const double t_stem = graph_us([&] { hz_stem_launch(&sp, st); }, st, 64);
   report("stem", 0, 98, 5, t_stem);
   // ---- layer1 bottlenecks at 56x56
+  for (int th : {8, 4})
   for (int cin : {64, 256}) {
     HzBneckParams bp{};
     bp.x = (const unsigned short*)dev_random((size_t)cin * 56 * 56 * 2, 4, true);
@@ -130,11 +141,13 @@ int main() {
       CK(hipMemset((void*)bp.bd, 0, 1024));
     }
     CK(hipMalloc((void**)&bp.out, (size_t)256 * 56 * 56 * 2));
-    bp.N = 1, bp.H = 56, bp.W = 56, bp.Cin = cin, bp.Cmid = 64, bp.Cout = 256;
+    bp.N = 1, bp.H = 56, bp.W = 56, bp.Cin = cin, bp.Cmid = 64, bp.Cout = 256, bp.tile_h = th;
     CK((hipError_t)hz_bneck_launch(&bp, st));
     CK(hipStreamSynchronize(st));
     const double t = graph_us([&] { hz_bneck_launch(&bp, st); }, st, 64);
-    report(cin == 64 ? "bneck_cin64_ds" : "bneck_cin256", cin == 64 ? 1 : 2, 49, 6, t);
+    char name[64];
+    snprintf(name, sizeof name, "bneck_cin%d%s_th%d", cin, cin == 64 ? "_ds" : "", th);
+    report(name, cin == 64 ? 1 : 2, 56 / th * 7, 6, t);
   }
   return 0;
 }

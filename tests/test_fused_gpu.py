@@ -46,9 +46,10 @@ def _fused_tensors(ctx):
             for f in ctx.fused.values()]
 
 
-@pytest.mark.parametrize("uint8,batch", [(True, 1), (False, 1), (True, 3)])
-def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, monkeypatch):
+@pytest.mark.parametrize("uint8,batch,th", [(True, 1, 8), (False, 1, 8), (True, 3, 8), (True, 1, 4), (True, 2, 4)])
+def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, monkeypatch):
     monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")  # every intermediate stays readable after the run
+    monkeypatch.setenv("HIPZAP_BNECK_TH", str(th))  # 8x8 or 4x8 bottleneck output tiles
     a, params, params_cpu, kw = r50
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=uint8))
     fused = ExecContext(g, params, torch.device(DEV), fuse="all")
