@@ -9,7 +9,9 @@
 //
 // * stem_kernel: image bytes (uint8 HWC, read zero-copy from the pinned request buffer) or fp32 NCHW
 //   -> normalise -> 7x7/2 conv + folded BN + ReLU -> 3x3/2 max-pool, one launch instead of three
-//   (preprocess, conv, maxpool). A workgroup computes a 9 x 17 patch of stem outputs (the 4 x 8
+//   (preprocess, conv, maxpool); mode 2 starts from the preprocess kernel's bf16 NHWC8 output
+//   (conv + max-pool in one launch: the PCIe read of a zero-copy request then stays in the light
+//   preprocess kernel instead of holding 98 conv workgroups, profiles/r4_fuse). A workgroup computes a 9 x 17 patch of stem outputs (the 4 x 8
 //   pooled tile plus its halo) from a 23 x 39 input patch staged in LDS.
 // * bneck_kernel: one whole bottleneck block of layer1 (56 x 56, 64 mid channels): conv1 1x1 ->
 //   conv2 3x3 -> conv3 1x1 + residual (identity, or the downsample 1x1 computed into the same
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
     for (int i = 0; i < RAWL; ++i)
       if (rdst[i] >= 0) raw[rdst[i]] = rv[i];
     __syncthreads();
-  } else {
+  } else if (p.mode == 0) {
     const float* src = static_cast<const float*>(p.src);
 #pragma unroll
     for (int i = 0; i < PIXL; ++i) {
@@ -118,6 +120,19 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
       const bool in = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
 #pragma unroll
       for (int c = 0; c < 3; ++c) fv[i][c] = in ? src[(((long)n * 3 + c) * p.H + iy) * p.W + ix] : 0.f;
+    }
+  }
+  // mode 2 (the standalone preprocess kernel's bf16 NHWC8 output): 16-B pixels straight into the patch
+  u32x4 pv[PIXL];
+  if (p.mode == 2) {
+    const bf16_t* src = static_cast<const bf16_t*>(p.src);
+#pragma unroll
+    for (int i = 0; i < PIXL; ++i) {
+      const int q = min(tid + 512 * i, PIX - 1), row = q / kStemIW, col = q - row * kStemIW;
+      const int iy = iy0 + row, ix = ix0 + col;
+      pv[i] = u32x4{0u, 0u, 0u, 0u};
+      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+        pv[i] = *reinterpret_cast<const u32x4*>(src + (((long)n * p.H + iy) * p.W + ix) * 8);
     }
   }
   // folded-BN bias of this wave's channels, loaded now (off the epilogue's critical path)
@@ -130,6 +145,10 @@ __global__ __launch_bounds__(512) void stem_kernel(const HzStemParams p) {
   for (int i = 0; i < PIXL; ++i) {
     const int q = tid + 512 * i;
     if (q >= PIX) continue;
+    if (p.mode == 2) {
+      *reinterpret_cast<u32x4*>(img + q * 8) = pv[i];
+      continue;
+    }
     const int row = q / kStemIW, col = q - row * kStemIW;
     const int iy = iy0 + row, ix = ix0 + col;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -406,6 +425,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
         for (int f = 0; f < NF2; ++f) bc[f] = bn[f];
       }
     }
+    HZ_BSTAMP(3);
     const int give = kh ? 0 : HALF, keep = kh ? HALF : 0;
 #pragma unroll
     for (int i = 0; i < HALF; ++i) RED[wave][i][lane] = acc[give + i];
@@ -422,7 +442,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
     }
   }
   __syncthreads();
-  HZ_BSTAMP(3);
+  HZ_BSTAMP(4);
 
   // ---- conv3 (1x1, 64 -> 256) + residual (identity or the downsample 1x1 in the same
   // accumulators) + ReLU: wave -> channel fragments 2w, 2w+1, all 4 pixel fragments. Every LDS
@@ -475,7 +495,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
           acc[1][f] = mfma16(ad[1][s], bd[s][f], acc[1][f]);
         }
     }
-    HZ_BSTAMP(4);
+    HZ_BSTAMP(5);
     const int CO32 = kBnCO / 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -499,7 +519,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
       }
     }
   }
-  HZ_BSTAMP(5);
+  HZ_BSTAMP(6);
   HZ_BSTAMP_FLUSH(CIN == 64 ? 1 : 2);
 }
 
@@ -507,7 +527,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
 
 extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
   const HzStemParams& p = *pp;
-  if (p.N < 1 || p.H < 8 || p.W < 8 || (p.mode != 0 && p.mode != 1)) return -1;
+  if (p.N < 1 || p.H < 8 || p.W < 8 || p.mode < 0 || p.mode > 2) return -1;
   if (p.SH != (p.H + 6 - 7) / 2 + 1 || p.SW != (p.W + 6 - 7) / 2 + 1) return -1;  // 7x7/2 pad 3
   if (p.PH != (p.SH + 2 - 3) / 2 + 1 || p.PW != (p.SW + 2 - 3) / 2 + 1) return -1;  // 3x3/2 pad 1
   if (p.mode == 1 && ((long)p.H * p.W * 3) % 4) return -1;  // whole-dword image rows (see the kernel)

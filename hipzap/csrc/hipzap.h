@@ -401,7 +401,8 @@ int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t st);
 // stem: image -> normalise -> 7x7/2 conv (packed like conv1: cin_pad 8, 13 k-steps) + bias + ReLU ->
 // 3x3/2 max-pool pad 1, channel-blocked output; one launch instead of preprocess + conv + maxpool
 typedef struct HzStemParams {
-  const void* src;            // uint8 NHWC [N][H][W][3] (mode 1) or fp32 NCHW [N][3][H][W] (mode 0)
+  const void* src;            // uint8 NHWC [N][H][W][3] (mode 1), fp32 NCHW [N][3][H][W] (mode 0), or bf16
+                              // NHWC [N][H][W][8] already normalised (mode 2: after the preprocess kernel)
   const unsigned short* w;    // fragment-major [4][13][64][8], k = (r*7 + s)*8 + c
   const float* bias;          // [64]
   unsigned short* out;        // [N][2][PH][PW][32]

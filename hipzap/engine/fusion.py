@@ -5,6 +5,9 @@ unchanged); :class:`~hipzap.engine.program.ExecContext` asks :func:`plan` which 
 bind as ONE fused kernel instead:
 
 * ``stem``: preprocess -> conv1 (7x7/2, BN folded, ReLU) -> maxpool 3x3/2 -> ``hz_stem_launch``;
+* ``convpool``: the same kernel after a standalone preprocess (conv1 + maxpool only, bf16 NHWC8
+  input): the default, since a zero-copy request read inside the 98-workgroup stem cost served
+  throughput (profiles/r4_fuse/README.md);
 * ``bneck``: a layer1-geometry bottleneck (1x1 Cin -> 64, 3x3 64 -> 64, 1x1 64 -> 256 + residual,
   optionally with its 1x1 downsample) -> ``hz_bneck_launch``.
 
@@ -24,7 +27,7 @@ import numpy as np
 from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK = 18, 19
-KINDS = ("stem", "bneck")
+KINDS = ("stem", "convpool", "bneck")
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -50,12 +53,12 @@ class Fused:
 
 
 def enabled_kinds(spec: str | None = None) -> set:
-    v = os.environ.get("HIPZAP_FUSE", "stem,bneck") if spec is None else spec
+    v = os.environ.get("HIPZAP_FUSE", "convpool,bneck") if spec is None else spec
     v = v.strip().lower()
     if v in ("", "0", "none", "off"):
         return set()
     if v in ("1", "all", "on"):
-        return set(KINDS)
+        return {"stem", "bneck"}
     return {k for k in v.split(",") if k in KINDS}
 
 
@@ -90,6 +93,23 @@ def match_stem(g, params, i: int) -> Fused | None:
     elif src.dtype != torch.float32 or src.shape[1] != 3:
         return None
     return Fused("stem", i, i + 3, [pre, cv, mp])
+
+
+def match_convpool(g, params, i: int) -> Fused | None:
+    nodes = g.nodes
+    if i + 2 > len(nodes):
+        return None
+    cv, mp = nodes[i:i + 2]
+    if not _conv(cv) or mp.kind != "maxpool" or mp.inputs != [cv.outputs[0]] or cv.slot != mp.slot:
+        return None
+    pc = params.get(cv.attrs.get("w"))
+    if pc is None or not _geom(pc, 8, 64, 7, 2, 3) or pc.ksteps != 13 or cv.attrs.get("act", "relu") != "relu":
+        return None
+    if cv.attrs.get("out_f32") or (mp.attrs.get("k"), mp.attrs.get("stride"), mp.attrs.get("pad")) != (3, 2, 1):
+        return None
+    if len(cv.inputs) != 1 or g.shape(cv.inputs[0])[-1] != 8:
+        return None
+    return Fused("convpool", i, i + 2, [cv, mp])
 
 
 def match_bneck(g, params, i: int) -> Fused | None:
@@ -140,6 +160,8 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
         f = None
         if "stem" in kinds:
             f = match_stem(g, params, i)
+        if f is None and "convpool" in kinds:
+            f = match_convpool(g, params, i)
         if f is None and "bneck" in kinds:
             f = match_bneck(g, params, i)
         if f is not None:
@@ -151,6 +173,16 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
 
 
 def stem_params(g, params, f: Fused, addr) -> StemParams:
+    if f.kind == "convpool":
+        cv, mp = f.nodes
+        pc = params[cv.attrs["w"]]
+        p = StemParams()
+        p.src, p.w, p.bias, p.out = addr(cv.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), addr(mp.outputs[0])
+        p.N, p.H, p.W, _ = g.shape(cv.inputs[0])
+        p.mode = 2
+        _, p.SH, p.SW, _ = g.shape(cv.outputs[0])
+        _, p.PH, p.PW, _ = g.shape(mp.outputs[0])
+        return p
     pre, cv, mp = f.nodes
     import torch
     src = g.tensors[pre.inputs[0]]
@@ -197,7 +229,7 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
 
 def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
     """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
-    if f.kind == "stem":
+    if f.kind in ("stem", "convpool"):
         prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
     else:
         prm, kind = bneck_params(g, params, f, addr), HZ_K_BNECK

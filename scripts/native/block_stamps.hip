@@ -13,16 +13,16 @@
 #include <cstring>
 #include <vector>
 
-__device__ unsigned long long g_bstamps[3][512][6];
+__device__ unsigned long long g_bstamps[3][512][8];
 __device__ unsigned long long g_bclock[3][512][2];  // s_memtime (shader clock) at the first / last stamp
 #define HZ_BSTAMP 1
-#define HZ_BSTAMP_DECL unsigned long long hz_bst[6] = {0, 0, 0, 0, 0, 0}, hz_clk0 = __builtin_amdgcn_s_memtime();
+#define HZ_BSTAMP_DECL unsigned long long hz_bst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hz_clk0 = __builtin_amdgcn_s_memtime();
 #define HZ_BSTAMP(i) hz_bst[i] = __builtin_amdgcn_s_memrealtime()
 #define HZ_BSTAMP_FLUSH(kind)                                                            \
   do {                                                                                   \
     const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                      \
     if (threadIdx.x == 0 && blockIdx.x < 512) {                                          \
-      for (int i_ = 0; i_ < 6; ++i_) g_bstamps[kind][blockIdx.x][i_] = hz_bst[i_];       \
+      for (int i_ = 0; i_ < 8; ++i_) g_bstamps[kind][blockIdx.x][i_] = hz_bst[i_];       \
       g_bclock[kind][blockIdx.x][0] = hz_clk0;                                           \
       g_bclock[kind][blockIdx.x][1] = clk1_;                                             \
     }                                                                                    \
@@ -55,7 +55,7 @@ static void* dev_random(size_t bytes, unsigned seed, bool bf16) {
 }
 
 static int report(const char* name, int kind, int nwg, int nph, double launch_us) {
-  unsigned long long h[512][6], ck[512][2];
+  unsigned long long h[512][8], ck[512][2];
   CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bstamps), sizeof(h), (size_t)kind * sizeof(h), hipMemcpyDeviceToHost));
   CK(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_bclock), sizeof(ck), (size_t)kind * sizeof(ck), hipMemcpyDeviceToHost));
   std::vector<double> mhz;
@@ -147,7 +147,7 @@ int main() {
     const double t = graph_us([&] { hz_bneck_launch(&bp, st); }, st, 64);
     char name[64];
     snprintf(name, sizeof name, "bneck_cin%d%s_th%d", cin, cin == 64 ? "_ds" : "", th);
-    report(name, cin == 64 ? 1 : 2, 56 / th * 7, 6, t);
+    report(name, cin == 64 ? 1 : 2, 56 / th * 7, 7, t);
   }
   return 0;
 }

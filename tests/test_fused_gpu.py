@@ -46,16 +46,18 @@ def _fused_tensors(ctx):
             for f in ctx.fused.values()]
 
 
-@pytest.mark.parametrize("uint8,batch,th", [(True, 1, 8), (False, 1, 8), (True, 3, 8), (True, 1, 4), (True, 2, 4)])
-def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, monkeypatch):
+@pytest.mark.parametrize("uint8,batch,th,fuse", [(True, 1, 8, "all"), (False, 1, 8, "all"), (True, 3, 8, "all"),
+                                                (True, 1, 4, "all"), (True, 2, 4, "all"),
+                                                (True, 1, 8, "convpool,bneck"), (False, 2, 8, "convpool,bneck")])
+def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, fuse, monkeypatch):
     monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")  # every intermediate stays readable after the run
     monkeypatch.setenv("HIPZAP_BNECK_TH", str(th))  # 8x8 or 4x8 bottleneck output tiles
     a, params, params_cpu, kw = r50
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=uint8))
-    fused = ExecContext(g, params, torch.device(DEV), fuse="all")
+    fused = ExecContext(g, params, torch.device(DEV), fuse=fuse)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     kinds = [f.kind for f in fused.fused.values()]
-    assert kinds == ["stem", "bneck", "bneck", "bneck"], kinds
+    assert kinds == ["stem" if fuse == "all" else "convpool", "bneck", "bneck", "bneck"], kinds
     assert plain.fused == {}
     gen = torch.Generator().manual_seed(batch)
     if uint8:
@@ -70,7 +72,7 @@ def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, monkey
         # same bf16 operands, fp32 accumulation in a different order: within a few bf16 ulps
         assert _rel(yf, yp) < 2e-2, (label, _rel(yf, yp))
         assert _rel(yf, yr) < 2e-2, (label, _rel(yf, yr))
-        if label.startswith("stem"):  # same K order as the per-conv kernel: at most 1 ulp apart
+        if label.startswith(("stem", "convpool")):  # same K order as the per-conv kernel: at most 1 ulp apart
             d = (yf - yp).abs() / yp.abs().clamp_min(1e-3)
             assert d.max().item() <= 2 ** -7, label
     lf, lp = fused.output.float().cpu().reshape(batch, -1), plain.output.float().cpu().reshape(batch, -1)
@@ -86,6 +88,7 @@ def test_fused_dispatch_count_and_replay(r50):
     ctx = ExecContext(g, params, torch.device(DEV), fuse="all")
     assert plain.num_ops() - ctx.num_ops() == 8  # stem 3 -> 1, three layer1 blocks 3 -> 1 each
     assert ctx.num_ops() <= 45
+    assert plain.num_ops() - ExecContext(g, params, torch.device(DEV)).num_ops() == 7  # default: convpool
     s = torch.cuda.Stream()
     ctx.capture(s)
     eager = ExecContext(g, params, torch.device(DEV), fuse="all")
