@@ -25,6 +25,8 @@
 // accumulator is 4 consecutive channels of one pixel. LDS images are XOR-swizzled per 16-B chunk so
 // every B-fragment ds_read_b128 is conflict-free (checked with the lane-group model of
 // MI355X_MICROARCH.md § LDS for every read pattern below).
+#include <type_traits>
+
 #include "common.h"
 #include "hipzap.h"
 
@@ -269,10 +271,11 @@ constexpr int kBnCM = 64, kBnCO = 256;
 
 // LDS images: [pixel][channels] bf16, 16-B chunks XOR-swizzled per pixel
 __device__ __forceinline__ int x_chunk(int p, int c, int nch) { return p * nch + (c ^ (p & (nch - 1))); }
-// conv1 output (read only by the 3x3 conv, whose 16 pixels are two 8-pixel rows of the halo tile)
-__device__ __forceinline__ int t1_chunk(int hy, int hx, int c) {
-  return (hy * kBnWT + hx) * 8 + (c ^ ((2 * hx + 2 * hy) & 7));
-}
+// conv1 output, read only by the 3x3 conv (16 pixels = two 8-pixel rows of the halo tile): rows of
+// 16 pixel slots, 160-B (10-chunk) pixel stride, no swizzle -- conflict-free for every tap, and the
+// per-tap offset (r * 16 + c) * 160 is an immediate of the ds_read (r, c compile-time per K half)
+constexpr int kT1Row = 16, kT1Pix = 80;  // pixel slots per row, bf16 elements per pixel slot (160 B)
+__device__ __forceinline__ int t1_off(int hy, int hx) { return (hy * kT1Row + hx) * kT1Pix; }
 
 template <int CIN, bool DS, int TH>
 __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   constexpr int KS1 = CIN / 32, KS2 = 9 * kBnCM / 32, KS3 = kBnCM / 32, KSD = CIN / 32;
   constexpr int NQ = kBnNP * XCH, NL = (NQ + 511) / 512;
   __shared__ __attribute__((aligned(16))) bf16_t X[kBnNP * CIN];
-  __shared__ __attribute__((aligned(16))) bf16_t T1[kBnNP * kBnCM];
+  __shared__ __attribute__((aligned(16))) bf16_t T1[(TH + 2) * kT1Row * kT1Pix];
   __shared__ __attribute__((aligned(16))) bf16_t T2[kBnTH * kBnTW * kBnCM];
   __shared__ __attribute__((aligned(16))) f32x4 RED[8][2][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
@@ -391,55 +394,66 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[fi][e] + bias1[e], 0.f) : 0.f;  // conv2's zero padding
-      *reinterpret_cast<u32x2*>(T1 + t1_chunk(hy, hx, ch >> 3) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      *reinterpret_cast<u32x2*>(T1 + t1_off(hy, hx) + ch) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
     }
   }
   __syncthreads();
   HZ_BSTAMP(2);
 
-  // ---- conv2 (3x3, 64 -> 64): wave -> channel fragment cf2, K half kh (9 of 18 k-steps), all 4
-  // pixel fragments; the two halves meet through LDS (kh 0 finishes fragments 0-1, kh 1 2-3) ----
+  // ---- conv2 (3x3, 64 -> 64): wave -> channel fragment cf2, K half kh (9 of 18 k-steps), all
+  // pixel fragments; the two halves meet through LDS (kh 0 finishes the first half of the
+  // fragments, kh 1 the second). The K half is a template argument of the body (a wave-uniform
+  // branch picks it), so every tap offset is a compile-time immediate and no accumulator is
+  // indexed at run time. ----
   {
-    f32x4 acc[NF2];
+    int base2[NF2];  // this lane's pixel of fragment f at tap (0, 0), plus its 8-channel group
 #pragma unroll
-    for (int f = 0; f < NF2; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto load_b = [&](int s, bf16x8(&bv)[NF2]) {
-      const int ks = kh * (KS2 / 2) + s;  // k-step: tap ks>>1 (r, c), channel half ks&1
-      const int tap = ks >> 1, r = tap / 3, c = tap - 3 * (tap / 3);
-      const int chunk = (ks & 1) * 4 + g;
+    for (int f = 0; f < NF2; ++f) {
+      const int j = 16 * f + l16;
+      base2[f] = t1_off(j >> 3, j & 7) + 8 * g;
+    }
+    auto conv2_half = [&](auto kh_c) {
+      constexpr int KH = decltype(kh_c)::value;
+      f32x4 acc[NF2];
 #pragma unroll
-      for (int f = 0; f < NF2; ++f) {
-        const int j = 16 * f + l16, hy = (j >> 3) + r, hx = (j & 7) + c;
-        bv[f] = *reinterpret_cast<const bf16x8*>(T1 + t1_chunk(hy, hx, chunk) * 8);
+      for (int f = 0; f < NF2; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto load_b = [&](int s, bf16x8(&bv)[NF2]) {
+        const int ks = KH * (KS2 / 2) + s;  // k-step: tap ks>>1 = (r, c), channel half ks&1
+        const int tap = ks >> 1, r = tap / 3, c = tap % 3;
+        const int off = t1_off(r, c) + (ks & 1) * 32;
+#pragma unroll
+        for (int f = 0; f < NF2; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(T1 + base2[f] + off);
+      };
+      bf16x8 bc[NF2], bn[NF2];
+      load_b(0, bc);
+#pragma unroll
+      for (int s = 0; s < KS2 / 2; ++s) {
+        if (s + 1 < KS2 / 2) load_b(s + 1, bn);
+#pragma unroll
+        for (int f = 0; f < NF2; ++f) acc[f] = mfma16(a2[s], bc[f], acc[f]);
+        if (s + 1 < KS2 / 2) {
+#pragma unroll
+          for (int f = 0; f < NF2; ++f) bc[f] = bn[f];
+        }
+      }
+      HZ_BSTAMP(3);
+      constexpr int give = KH ? 0 : HALF, keep = KH ? HALF : 0;
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) RED[wave][i][lane] = acc[give + i];
+      __syncthreads();
+      const int ch = 16 * cf2 + 4 * g;
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) {
+        const f32x4 o = RED[wave ^ 4][i][lane];
+        const int j = 16 * (keep + i) + l16;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[keep + i][e] + o[e] + bias2[e], 0.f);
+        *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 8) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
       }
     };
-    bf16x8 bc[NF2], bn[NF2];
-    load_b(0, bc);
-#pragma unroll
-    for (int s = 0; s < KS2 / 2; ++s) {
-      if (s + 1 < KS2 / 2) load_b(s + 1, bn);
-#pragma unroll
-      for (int f = 0; f < NF2; ++f) acc[f] = mfma16(a2[s], bc[f], acc[f]);
-      if (s + 1 < KS2 / 2) {
-#pragma unroll
-        for (int f = 0; f < NF2; ++f) bc[f] = bn[f];
-      }
-    }
-    HZ_BSTAMP(3);
-    const int give = kh ? 0 : HALF, keep = kh ? HALF : 0;
-#pragma unroll
-    for (int i = 0; i < HALF; ++i) RED[wave][i][lane] = acc[give + i];
-    __syncthreads();
-    const int ch = 16 * cf2 + 4 * g;
-#pragma unroll
-    for (int i = 0; i < HALF; ++i) {
-      const f32x4 o = RED[wave ^ 4][i][lane];
-      const int j = 16 * (keep + i) + l16;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[keep + i][e] + o[e] + bias2[e], 0.f);
-      *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 8) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
+    if (kh == 0) conv2_half(std::integral_constant<int, 0>{});
+    else conv2_half(std::integral_constant<int, 1>{});
   }
   __syncthreads();
   HZ_BSTAMP(4);

@@ -3,7 +3,7 @@
 // the two layer1 bottleneck kernels at bs=1 (random operands), next to the per-launch time of 64
 // back-to-back launches captured in a hipGraph. Stem phases: 0 start, 1 patch in LDS, 2 MFMAs
 // done, 3 stem outputs in LDS, 4 pooled stores issued. Bottleneck phases: 0 start, 1 input patch
-// in LDS, 2 conv1 done, 3 conv2 done, 4 conv3 MFMAs done, 5 stores issued.
+// in LDS, 2 conv1 done, 3 conv2 MFMAs done, 4 conv2 epilogue done, 5 conv3 MFMAs done, 6 stores.
 // Build + run: scripts/sessions/gpu_r4_stamps.sh (hipcc --offload-arch=gfx950 -I hipzap/csrc).
 #include <hip/hip_runtime.h>
 
