@@ -504,7 +504,11 @@ typedef struct HzMemcpyArgs {
 // load-phase timings (ms) reported by hz_plan_open / hz_plan_timings
 enum { HZ_PLAN_T_PARSE = 0, HZ_PLAN_T_HIP_INIT = 1, HZ_PLAN_T_UPLOAD = 2, HZ_PLAN_T_CTX_ALLOC = 3,
        HZ_PLAN_T_BIND = 4, HZ_PLAN_T_CAPTURE = 5, HZ_PLAN_T_BLOB_ALLOC = 6,
-       HZ_PLAN_T_FIRST_COPY = 7, HZ_PLAN_NT = 8 };
+       HZ_PLAN_T_FIRST_COPY = 7,
+       // sub-phases of HZ_PLAN_T_UPLOAD (cold-start phase table): stream creation, the blob's
+       // read + DMA, the wait for the device-code warm thread; and that thread's own duration
+       HZ_PLAN_T_STREAM = 8, HZ_PLAN_T_UPLOAD_DMA = 9, HZ_PLAN_T_WARM_WAIT = 10, HZ_PLAN_T_WARM_THREAD = 11,
+       HZ_PLAN_NT = 12 };
 uint64_t hz_abi_version(void);
 const char* hz_plan_last_error(void);
 // read_blob = 0: allocate the weight blob but leave it unfilled (an RCCL broadcast fills it)

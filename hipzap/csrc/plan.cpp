@@ -570,7 +570,9 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
   if (e == hipSuccess && !(cw && cw[0] == '0')) {
     const unsigned units = p->code_units() | ((p->h.flags & kFlagWeightless) ? kUnitPack : 0u);
-    p->warm = std::thread([device, units] {
+    double* t_warm = &p->t[HZ_PLAN_T_WARM_THREAD];  // written by the thread, read after the join
+    p->warm = std::thread([device, units, t_warm] {
+      const double w0 = now_ms();
       if (hipSetDevice(device) != hipSuccess) return;
       if (units & kUnitConv) (void)hz_conv_code_warm();
       if (units & kUnitVision) (void)hz_vision_code_warm();
@@ -579,6 +581,7 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
       if (units & kUnitFp8) (void)hz_fp8_code_warm();
       if (units & kUnitPack) (void)hz_pack_code_warm();
       if (units & kUnitBlock) (void)hz_block_code_warm();
+      *t_warm = now_ms() - w0;
     });
   }
   if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);
@@ -591,18 +594,24 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   {  // the upload stream: kept, it becomes the first context's stream (a weightless template's
      // caller fills the blob on it, hz_plan_upload_stream, instead of creating a stream of its own)
     hipStream_t s = nullptr;
+    const double ts = now_ms();
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       fail("plan: stream creation failed");
       delete p;
       return nullptr;
     }
     p->spare = s;
+    const double tu = now_ms();
+    p->t[HZ_PLAN_T_STREAM] = tu - ts;
     if (read_blob && p->upload_blob(s)) {
       delete p;
       return nullptr;
     }
+    p->t[HZ_PLAN_T_UPLOAD_DMA] = now_ms() - tu;
   }
+  const double tw = now_ms();
   p->join_warm();
+  p->t[HZ_PLAN_T_WARM_WAIT] = now_ms() - tw;
   p->t[HZ_PLAN_T_UPLOAD] = now_ms() - t2 - p->t[HZ_PLAN_T_BLOB_ALLOC];
   if (timings) std::memcpy(timings, p->t, sizeof(p->t));
   return p;

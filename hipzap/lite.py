@@ -24,7 +24,9 @@ from . import _native as N
 
 HEADER = struct.Struct("<8s15Q")
 PHASES = ("parse_ms", "hip_init_ms", "upload_ms", "ctx_alloc_ms", "bind_ms", "capture_ms", "blob_alloc_ms",
-          "first_copy_ms")
+          "first_copy_ms",
+          # upload_ms = stream_ms + upload_dma_ms + warm_wait_ms; warm_thread_ms runs beside them
+          "stream_ms", "upload_dma_ms", "warm_wait_ms", "warm_thread_ms")
 _TYPECODE = {"float32": "f", "uint8": "B", "int32": "i", "int64": "q", "bfloat16": "H", "float16": "H"}
 
 
@@ -148,7 +150,7 @@ class PlanEngine:
             raise PlanError(f"{path}: plan written for native ABI {self.meta['abi']}, library is "
                             f"{L.hz_abi_version()} (re-export with `hipzap plan`)")
         no_sdma_default()
-        tm = (C.c_double * 8)()
+        tm = (C.c_double * len(PHASES))()
         h = L.hz_plan_open(path.encode(), device, int(read_blob), tm)
         if not h:
             raise PlanError(L.hz_plan_last_error().decode())
