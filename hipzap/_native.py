@@ -85,14 +85,14 @@ class LmbLayerParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("x", c_void_p), ("c", c_void_p),
                 ("gpar", c_void_p), ("ctl", c_void_p), ("H", c_int), ("Kh", c_int), ("Kx", c_int), ("R", c_int),
                 ("Bp", c_int), ("step_off", c_int), ("emb", c_void_p), ("dbest", c_void_p), ("V", c_int),
-                ("pad_", c_int), ("outp", c_void_p), ("tok", c_void_p)]
+                ("nb_act", c_int), ("outp", c_void_p), ("tok", c_void_p)]
 
 
 class LmbDecParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("gpar", c_void_p), ("ctl", c_void_p),
                 ("seed", c_void_p), ("dbest", c_void_p), ("logits", c_void_p), ("V", c_int), ("Vp", c_int),
                 ("K", c_int), ("Bp", c_int), ("nblk", c_int), ("step_off", c_int), ("n_exclude", c_int),
-                ("pad_", c_int), ("exclude", c_int * 8)]
+                ("nb_act", c_int), ("exclude", c_int * 8)]
 
 
 class LmbAdmitParams(C.Structure):
@@ -231,6 +231,8 @@ def _load():
     _sig(lib, "hz_lmb_create", P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int)
     _sig(lib, "hz_lmb_submit", c_int, P, P, c_int, c_int, C.c_uint64, P, P, C.POINTER(D))
     _sig(lib, "hz_lmb_stats", None, P, C.POINTER(U64))
+    _sig(lib, "hz_lmb_set_lowload", c_int, P, P, c_int)
+    _sig(lib, "hz_lmb_lo_replays", U64, P)
     _sig(lib, "hz_lmb_destroy", None, P)
     if DEBUG:
         for unit in DEBUG_UNITS:

@@ -234,7 +234,9 @@ typedef struct HzLmbLayerParams {
   // and its embedding as the x operand
   const unsigned short* emb;  // [Vp/16][Kx/32][64][8] fragment-major embedding (NULL: not first)
   unsigned long long* dbest;  // [2 parity][Bp] running maxima (packed key, row) of the decoder; the
-  int V, pad_;                //   first layer reads the other parity and clears its own
+  int V;                      //   first layer reads the other parity and clears its own
+  int nb_act;                 // row blocks (of 16) computed: 0 = all Bp/16; 1 = rows 0..15 only (the
+                              //   low-load program: every busy row is below 16)
   int* const* outp;           // [Bp] request output arrays (pinned host, written by workgroup 0)
   int* tok;                   // [Bp] this step's tokens (device, diagnostics)
 } HzLmbLayerParams;
@@ -247,7 +249,8 @@ typedef struct HzLmbDecParams {
   const unsigned long long* seed;  // [Bp]
   unsigned long long* dbest;  // [2 parity][Bp]: atomic max over acceptable ids -> the next first layer
   float* logits;              // [Bp][V] (recorded rows only) or NULL
-  int V, Vp, K, Bp, nblk, step_off, n_exclude, pad_;
+  int V, Vp, K, Bp, nblk, step_off, n_exclude;
+  int nb_act;                 // as HzLmbLayerParams::nb_act
   int exclude[8];
 } HzLmbDecParams;
 typedef struct HzLmbAdmitParams {
@@ -272,6 +275,8 @@ void* hz_lmb_create(HzProgram prog, hipStream_t st, int* host_block, int Bp, int
 int hz_lmb_submit(void* s, const int* prompt, int P, int n, unsigned long long seed, int* out, float* logits_out,
                   double* lat_us);
 void hz_lmb_stats(void* s, unsigned long long* out4);  // replays, served, row-steps used, row-steps total
+int hz_lmb_set_lowload(void* s, HzProgram lo, int rows);  // program for replays whose busy rows are < rows
+unsigned long long hz_lmb_lo_replays(void* s);
 void hz_lmb_destroy(void* s);
 
 // ---- device-side packing of raw checkpoint tensors (csrc/pack.hip; torch-free .pth cold start) ----

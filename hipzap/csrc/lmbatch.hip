@@ -72,7 +72,8 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   const int k0 = wave * spw;
   const int cnt = max(0, min(spw, KS - k0));
   const int Bp = NB * 16;
-  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile0 < ntile)) return;
+  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
+  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile0 < ntile && nba <= NB)) return;
   // ---- loads that need nothing: this sub-step's control + the decoder maxima (FIRST), then the
   // weight stream; vmcnt retires in issue order, so what the token selection waits for goes first
   HzLmbCtl cl = {};
@@ -108,8 +109,10 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     const size_t lo_off = (size_t)(hk ? KSH : KSX) * NB * 512;
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
-      ah[s][cb] = *reinterpret_cast<const u32x4*>(src + cb * 512 + lane * 8);
-      al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + cb * 512 + lane * 8);
+      if (cb < nba) {
+        ah[s][cb] = *reinterpret_cast<const u32x4*>(src + cb * 512 + lane * 8);
+        al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + cb * 512 + lane * 8);
+      }
     }
   }
   if constexpr (FIRST) {
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       if (ks >= KSH) {  // wave-uniform
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) {
+          if (cb >= nba) continue;
           const int tk = s_tok[cb * 16 + (lane & 15)];
           ah[s][cb] = *reinterpret_cast<const u32x4*>(
               p.emb + ((size_t)(tk >> 4) * KSX + (ks - KSH)) * 512 + ((lane >> 4) * 16 + (tk & 15)) * 8);
@@ -158,6 +162,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) {
+          if (cb >= nba) continue;
           acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(ah[s][cb]), acc[tt][cb], 0, 0, 0);
           if (lo)
             acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(al[s][cb]), acc[tt][cb], 0, 0, 0);
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   __syncthreads();
   // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row cb*16 + (l & 15);
   // its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows 4(l>>4) .. +3)
-  if (tid < TPW * NB * 64) {
+  if (tid < TPW * NB * 64 && (tid >> 6) % NB < nba) {
     const int tt = tid / (NB * 64), cb = (tid >> 6) % NB, l = tid & 63;
     f32x4 g = part[0][tt][cb][l];
 #pragma unroll
@@ -206,6 +211,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int CH = 8;         // k-steps per chunk
   constexpr int KS = NCH * CH;  // K = 256 * NCH
   constexpr int Bp = NB * 16;
+  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
   __shared__ unsigned long long s_best[DW][32];
   __shared__ __attribute__((aligned(16))) HzLmbCtl s_ctl[32];
@@ -238,7 +244,8 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       const int f = f0 + wave;
       const int ks = f / (2 * NB), rem = f - ks * 2 * NB, hl = rem / NB, cb = rem - hl * NB;
       const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
+      if (cb < nba)  // (the vmcnt wait below counts only the weight chunk issued after the staging)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
     }
   }
   // the rows' control and seeds go to LDS the same way (an ordinary load here would make hipcc
@@ -294,6 +301,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       const int ks = c * CH + s;
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) {
+        if (cb >= nba) continue;
         const bf16x8 hi = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 0) * NB + cb) * 512 + lane * 8));
         const bf16x8 lo = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 1) * NB + cb) * 512 + lane * 8));
         acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wa[cur][s]), hi, acc[0][cb], 0, 0, 0);
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int v0 = (tile0 + t) * 16 + (lane >> 4) * 4;
-      if (tile0 + t >= t_hi || v0 >= p.V) continue;
+      if (cb >= nba || tile0 + t >= t_hi || v0 >= p.V) continue;
       f32x4 lg = acc[t][cb];
       if (p.bias) lg += *reinterpret_cast<const f32x4*>(p.bias + v0);
       if (p.logits && rec[cb])
@@ -397,7 +405,7 @@ extern "C" int hz_lmb_dec_blocks(int V) {
 extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
   const HzLmbLayerParams& p = *pp;
   const bool first = p.emb != nullptr;
-  if (p.Bp != 16 && p.Bp != 32) return -1;
+  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < 0 || p.nb_act > p.Bp / 16) return -1;
   if (p.Kh % 32 || p.Kx % 32 || p.Kh < p.H || p.R % 16 || p.R < 4 * p.H || !p.w || !p.bias || !p.h || !p.c || !p.gpar)
     return -1;
   const int KS = (p.Kh + p.Kx) / 32;
@@ -431,7 +439,7 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
 
 extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   const HzLmbDecParams& p = *pp;
-  if (p.Bp != 16 && p.Bp != 32) return -1;
+  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < 0 || p.nb_act > p.Bp / 16) return -1;
   if (p.K % 256 || p.K < 256 || p.K > DKMAX * 32 || p.Vp % 16 || p.Vp < p.V || p.n_exclude < 0 || p.n_exclude > 8)
     return -1;
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;

@@ -10,6 +10,10 @@
 // A request of P prompt tokens and n words occupies its row for P + n sub-steps (its last token
 // is chosen at sub-step P + n - 1); rows are refilled at the next replay boundary, so a request
 // waits at most one replay (U steps) to join.
+// Low load: with a second program captured for the first row block only (hz_lmb_set_lowload), a
+// replay whose busy rows are all below lo_rows runs that one instead: the same per-row arithmetic
+// (a row's tokens never depend on the program), half the state traffic and MFMAs at Bp = 32.
+// Requests take the lowest free row, so a lone request always qualifies.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -42,6 +46,8 @@ struct Req {
 
 struct Sched {
   HzProgram prog;
+  HzProgram lo = nullptr;  // low-load program (rows < lo_rows only) or null
+  int lo_rows = 0;
   hipStream_t st;
   hipEvent_t ev = nullptr;
   int* block;
@@ -56,7 +62,7 @@ struct Sched {
   bool stop = false;
   std::thread worker;
   long long gstep = 0;
-  unsigned long long replays = 0, served = 0, used = 0, offered = 0;
+  unsigned long long replays = 0, served = 0, used = 0, offered = 0, lo_replays = 0;
 
   int row_stride() const { return 8 + 4 * U; }
 
@@ -90,6 +96,7 @@ struct Sched {
   void run() {
     std::vector<char> admitted(Bp, 0);
     for (;;) {
+      bool low = false;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv_work.wait(lk, [&] { return stop || !waiting.empty() || busy > 0; });
@@ -112,9 +119,12 @@ struct Sched {
             ++busy;
           }
         }
+        low = lo != nullptr;
+        for (int r = lo_rows; low && r < Bp; ++r) low = rows[r] == nullptr;
       }
       write_block(admitted);
-      int rc = hz_prog_replay(prog, st);
+      int rc = hz_prog_replay(low ? lo : prog, st);
+      lo_replays += low;
       if (!rc) rc = (int)hipEventRecord(ev, st);
       if (!rc) {
         for (;;) {
@@ -201,6 +211,23 @@ int hz_lmb_submit(void* h, const int* prompt, int P, int n, unsigned long long s
   q.cv.wait(lk, [&] { return q.done; });
   if (lat_us) *lat_us = now_us() - t0;
   return q.rc;
+}
+
+// optional low-load program over the same buffers (kernels with nb_act = rows / 16); call before
+// the first submit
+int hz_lmb_set_lowload(void* h, HzProgram lo, int rows) {
+  auto* s = static_cast<Sched*>(h);
+  if (!s || (lo && (rows < 16 || rows % 16 || rows >= s->Bp))) return -1;
+  std::lock_guard<std::mutex> g(s->mu);
+  s->lo = lo;
+  s->lo_rows = lo ? rows : 0;
+  return 0;
+}
+
+unsigned long long hz_lmb_lo_replays(void* h) {
+  auto* s = static_cast<Sched*>(h);
+  std::lock_guard<std::mutex> g(s->mu);
+  return s->lo_replays;
 }
 
 void hz_lmb_stats(void* h, unsigned long long* out4) {

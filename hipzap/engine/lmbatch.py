@@ -208,7 +208,8 @@ class LMBatchEngine:
     ``run_tokens(..., logits=True)`` also returns the logits after the last prompt token."""
 
     def __init__(self, packed: dict, device="cuda:0", rows: int = 32, unroll: int = 8, exclude_ids=(),
-                 max_words: int = 1024, record_logits: bool = False, capture: bool = True):
+                 max_words: int = 1024, record_logits: bool = False, capture: bool = True,
+                 lowload: bool | None = None):
         self.p = packed
         self.device = torch.device(device)
         self.V = packed["V"]
@@ -220,7 +221,7 @@ class LMBatchEngine:
                  "dec_bias": packed["dec_bias"].data_ptr()}
             self.core = lmcore.LmbCore(geometry_of(packed), w, self._alloc, self.stream.cuda_stream, rows=rows,
                                        unroll=unroll, exclude_ids=exclude_ids, max_words=max_words,
-                                       record_logits=record_logits, capture=capture)
+                                       record_logits=record_logits, capture=capture, lowload=lowload)
             torch.cuda.synchronize(self.device)
         self.rows, self.unroll, self.max_words = rows, unroll, max_words
         self._ops = self.core._ops

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass, field
 
 from .. import _native as N
@@ -151,12 +152,14 @@ class LmbCore:
 
     def __init__(self, geo: LmbGeometry, w: dict, alloc, stream: int, rows: int = 32, unroll: int = 8,
                  exclude_ids=(), max_words: int = 1024, record_logits: bool = False, capture: bool = True,
-                 lib=None):
+                 lowload: bool | None = None, lib=None):
         if rows not in (16, 32):
             raise ValueError("rows must be 16 or 32")
         if not 1 <= unroll <= 32:
             raise ValueError("unroll must be in 1..32")
         lib = lib or N.lib()
+        if lowload is None:
+            lowload = os.environ.get("HIPZAP_LM_LOWLOAD", "1") != "0"
         self.lib, self.geo = lib, geo
         self.rows, self.unroll, self.max_words, self.V = rows, unroll, max_words, geo.V
         Bp, U, L = rows, unroll, geo.layers
@@ -200,21 +203,31 @@ class LmbCore:
         for i, e in enumerate(ex):
             d.exclude[i] = e
         self._ops = [(N.HZ_K_LMB_LAYER, q) for q in layer_prms] + [(N.HZ_K_LMB_DEC, d)]
-        prog = lib.hz_prog_create()
-        N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(a), C.sizeof(a), 0), "add lmb admit")
-        for u in range(U):
-            for kind, prm in self._ops:
-                q = type(prm).from_buffer_copy(prm)
-                q.step_off = u
-                N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
+
+        def build(nb_act: int):
+            prog = lib.hz_prog_create()
+            N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(a), C.sizeof(a), 0), "add lmb admit")
+            for u in range(U):
+                for kind, prm in self._ops:
+                    q = type(prm).from_buffer_copy(prm)
+                    q.step_off, q.nb_act = u, nb_act
+                    N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
+            if capture:
+                N.check(lib.hz_prog_capture(prog, stream), "capture lmb")
+            return prog
+
         self._admit = a
-        self.prog = prog
         self.stream = stream
-        if capture:
-            N.check(lib.hz_prog_capture(prog, stream), "capture lmb")
-        self._sched = lib.hz_lmb_create(prog, stream, self.block, Bp, U, 0, max_words, self.out_pool, d.logits, geo.V)
+        self.prog = build(0)
+        # low load (HIPZAP_LM_LOWLOAD, default on at 32 rows): a second program over the first 16
+        # rows, replayed while every busy row is below 16 (csrc/lmserve.cpp)
+        self.prog_lo = build(1) if lowload and Bp > 16 else None
+        self._sched = lib.hz_lmb_create(self.prog, stream, self.block, Bp, U, 0, max_words, self.out_pool, d.logits,
+                                        geo.V)
         if not self._sched:
             raise RuntimeError("hz_lmb_create failed")
+        if self.prog_lo:
+            N.check(lib.hz_lmb_set_lowload(self._sched, self.prog_lo, 16), "hz_lmb_set_lowload")
         self.last_latency_ms = None
 
     def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
@@ -242,15 +255,18 @@ class LmbCore:
         a = (C.c_uint64 * 4)()
         self.lib.hz_lmb_stats(self._sched, a)
         return {"replays": a[0], "served": a[1], "row_steps_used": a[2], "row_steps": a[3],
-                "row_utilisation": round(a[2] / a[3], 4) if a[3] else None}
+                "row_utilisation": round(a[2] / a[3], 4) if a[3] else None,
+                "lowload_replays": int(self.lib.hz_lmb_lo_replays(self._sched))}
 
     def close(self) -> None:
         s, self._sched = getattr(self, "_sched", None), None
         if s:
             self.lib.hz_lmb_destroy(s)
-        prog, self.prog = getattr(self, "prog", None), None
-        if prog:
-            self.lib.hz_prog_destroy(prog)
+        for attr in ("prog", "prog_lo"):
+            prog = getattr(self, attr, None)
+            setattr(self, attr, None)
+            if prog:
+                self.lib.hz_prog_destroy(prog)
 
     def __del__(self):
         try:

@@ -115,6 +115,23 @@ def test_requests_are_independent_of_the_batch(engine):
     assert st["served"] >= 80 and st["row_utilisation"] > 0
 
 
+def test_lowload_program_is_bitwise_the_full_one(model):
+    """A lone request (every busy row below 16) replays the 16-row program (csrc/lmserve.cpp
+    low load); its tokens and logits are bitwise those of the full 32-row program."""
+    pk = pack_lmb(model.state_dict(), DEV)
+    full = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=False)
+    low = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=True)
+    try:
+        for seed, (ids, n) in enumerate([([4, 7], 30), ([9] * 9, 17), ([123], 1)]):
+            a, la = full.run_tokens(ids, n, seed=seed, logits=True)
+            b, lb = low.run_tokens(ids, n, seed=seed, logits=True)
+            assert a == b and torch.equal(la, lb)
+        assert low.stats()["lowload_replays"] > 0 and full.stats()["lowload_replays"] == 0
+    finally:
+        full.close()
+        low.close()
+
+
 def test_tokens_track_the_single_request_engine(model):
     """Same seed, same rule, same noise: the batched engine's tokens agree with the single-request
     engine's (fp32 state) except where two keys are closer than the small state rounding."""
