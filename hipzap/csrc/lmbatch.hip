@@ -17,6 +17,7 @@
 // output element depends only on its own row's operands, so a request's tokens do not depend on
 // which other requests share the batch (tests/test_lmbatch_gpu.py checks bitwise).
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "hipzap.h"
@@ -204,12 +205,23 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
 // ------------------------------------------------------------------------ decoder kernel
 // Workgroup = 256 vocabulary rows x all Bp request rows. The whole last-layer state (hi/lo, K <=
 // 1024) is staged once into LDS (fragment-major, lane-linear: 16-B global_load_lds per lane) while
-// the first weight chunk streams in; each wave owns 2 vocabulary tiles and walks K in chunks of 8
-// k-steps with the next chunk's 16 weight fragments in flight.
-template <int NB, int NCH>
+// the first weight chunk streams in; each wave owns 2 vocabulary tiles and walks K in chunks of CH
+// k-steps through a ring of R register chunks: chunk c + R is issued into chunk c's registers as
+// soon as chunk c is multiplied, so R - 1 chunks stream during every chunk's MFMAs (the
+// compiler's vmcnt counts retire in issue order). (CH, R) = (8, 2) is the round-3 schedule.
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int NB, int KS, int CH, int R>
 __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
-  constexpr int CH = 8;         // k-steps per chunk
-  constexpr int KS = NCH * CH;  // K = 256 * NCH
+  constexpr int NCH = KS / CH;  // K = 32 * KS
+  constexpr int RR = R < NCH ? R : NCH;  // chunks issued before the first MFMA
+  static_assert(KS % CH == 0, "k-steps per chunk");
   constexpr int Bp = NB * 16;
   const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
@@ -225,15 +237,15 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   const int tile0 = t_lo + wave * 2;
   const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
   const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
-  // weight chunks of 8 k-steps (16 fragments per wave), two in flight: chunk c + 2 is issued
-  // into chunk c's registers as soon as chunk c is multiplied, so every wait leaves the next
-  // chunk streaming (the compiler's vmcnt counts retire in issue order)
-  u32x4 wa[2][CH], wb[2][CH];
+  u32x4 wa[RR][CH], wb[RR][CH];
+  auto issue = [&](int slot, int c) {
 #pragma unroll
-  for (int s = 0; s < CH; ++s) {
-    wa[0][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)s * 512);
-    wb[0][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)s * 512);
-  }
+    for (int s = 0; s < CH; ++s) {
+      wa[slot][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512);
+      wb[slot][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512);
+    }
+  };
+  issue(0, 0);
   const int par = (*p.gpar + p.step_off) & 1;
   // stage the state: KS * 2 * NB fragments of 1 KiB, wave w takes fragments w, w + 8, ...
   {
@@ -244,7 +256,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       const int f = f0 + wave;
       const int ks = f / (2 * NB), rem = f - ks * 2 * NB, hl = rem / NB, cb = rem - hl * NB;
       const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
-      if (cb < nba)  // (the vmcnt wait below counts only the weight chunk issued after the staging)
+      if (cb < nba)  // (the vmcnt wait below counts only the weight chunks issued after the staging)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
     }
   }
@@ -257,22 +269,16 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     if (lane < Bp / 2)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p.seed + 2 * lane), (lds_void*)s_seed, 16, 0, 0);
   }
-  if constexpr (NCH > 1) {
 #pragma unroll
-    for (int s = 0; s < CH; ++s) {
-      wa[1][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)(CH + s) * 512);
-      wb[1][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)(CH + s) * 512);
-    }
-  }
+  for (int c = 1; c < RR; ++c) issue(c, c);
   __builtin_amdgcn_sched_barrier(0);
-  // the staged state is complete once everything issued before chunk 1 has landed (every wave),
-  // chunk 1 keeps streaming across the barrier
-  if constexpr (NCH > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the staged state is complete once everything issued before chunk 1 has landed (every wave);
+  // chunks 1 .. RR - 1 keep streaming across the barrier
+  wait_vmcnt<(RR - 1) * 2 * CH>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   // the Gumbel noise of this wave's rows does not depend on the logits: compute it (VALU) while
-  // chunk 1 streams (after the barrier: with a global_load_lds in flight hipcc would wait for
+  // the chunks stream (after the barrier: with a global_load_lds in flight hipcc would wait for
   // vmcnt(0) at the first use of the control loads)
   int dt[NB];
   bool rec[NB];
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     for (int cb = 0; cb < NB; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int cur = c & 1;  // compile-time after unrolling: register arrays stay registers
+    const int cur = c % RR;  // compile-time after unrolling: register arrays stay registers
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       const int ks = c * CH + s;
@@ -311,13 +317,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // chunk c's MFMAs are done with its registers
-    if (c + 2 < NCH) {  // refill this chunk's registers with chunk c + 2
-#pragma unroll
-      for (int s = 0; s < CH; ++s) {
-        wa[cur][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)((c + 2) * CH + s) * 512);
-        wb[cur][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)((c + 2) * CH + s) * 512);
-      }
-    }
+    if (c + RR < NCH) issue(cur, c + RR);  // refill them with chunk c + RR
     __builtin_amdgcn_sched_barrier(0);
   }
   // ---- epilogue: lane l holds vocabulary rows 16*tile + 4(l>>4) + i of request row cb*16 + (l&15)
@@ -437,6 +437,19 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// decoder weight pipeline: HIPZAP_LMB_DEC_PIPE = "8x2" (default: 8 k-steps per chunk, 2 chunks in
+// the ring), "4x5" or "4x6" (K = 1024 only; the A/B of profiles/r4_lmb)
+static int lmb_dec_pipe() {
+  static const int v = [] {
+    const char* e = getenv("HIPZAP_LMB_DEC_PIPE");
+    if (!e) return 0;
+    if (!strcmp(e, "4x5")) return 1;
+    if (!strcmp(e, "4x6")) return 2;
+    return 0;
+  }();
+  return v;
+}
+
 extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   const HzLmbDecParams& p = *pp;
   if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < 0 || p.nb_act > p.Bp / 16) return -1;
@@ -444,13 +457,26 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
     return -1;
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
   const dim3 grid(p.nblk), block(512);
-#define HZ_LMBD(NB, NCH) \
-  case NCH: hipLaunchKernelGGL((lmb_dec_kernel<NB, NCH>), grid, block, 0, st, p); break;
-  if (p.Bp == 16) {
-    switch (p.K / 256) { HZ_LMBD(1, 1) HZ_LMBD(1, 2) HZ_LMBD(1, 3) HZ_LMBD(1, 4) default: return -1; }
-  } else {
-    switch (p.K / 256) { HZ_LMBD(2, 1) HZ_LMBD(2, 2) HZ_LMBD(2, 3) HZ_LMBD(2, 4) default: return -1; }
+  const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
+#define HZ_LMBD(NB, KS, CH, R) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R>), grid, block, 0, st, p)
+#define HZ_LMBD_K(NB)                               \
+  switch (p.K / 256) {                              \
+    case 1: HZ_LMBD(NB, 8, 8, 2); break;            \
+    case 2: HZ_LMBD(NB, 16, 8, 2); break;           \
+    case 3: HZ_LMBD(NB, 24, 8, 2); break;           \
+    case 4:                                         \
+      if (pipe == 1) HZ_LMBD(NB, 32, 4, 5);         \
+      else if (pipe == 2) HZ_LMBD(NB, 32, 4, 6);    \
+      else HZ_LMBD(NB, 32, 8, 2);                   \
+      break;                                        \
+    default: return -1;                             \
   }
+  if (p.Bp == 16) {
+    HZ_LMBD_K(1)
+  } else {
+    HZ_LMBD_K(2)
+  }
+#undef HZ_LMBD_K
 #undef HZ_LMBD
   return (int)hipGetLastError();
 }
