@@ -58,23 +58,37 @@ __device__ __forceinline__ int st_off(int j, int r, int NB) {
 }
 
 // ------------------------------------------------------------------------ layer kernel
-// One workgroup per 16-row tile (4 hidden units x 4 gates) x all Bp rows; the 8 waves split K.
-// Every load of a wave (its weight fragments, its state fragments) is issued before the first
-// MFMA; partial tiles meet in LDS and 4 x Bp threads apply the cell update.
-template <int NB, bool FIRST, int TPW>
+// One workgroup per TPW 16-row tiles (4 hidden units x 4 gates each) x NBW row blocks of 16
+// request rows; the 8 waves split K. Every load of a wave (its weight fragments, its state
+// fragments) is issued before the first MFMA; partial tiles meet in LDS and TPW x NBW x 64 threads
+// apply the cell update.
+// NBW = NB: every workgroup reads all Bp rows' state (128 B per k at Bp 32 against 32 B of weights
+// per tile): the layer is bound by what each CU fetches, not by HBM. NBW = 1 (Bp 32): twin
+// workgroups b and b + 8 (one XCD under round-robin placement: the twin's weight read hits L2)
+// take one row block each, so a CU fetches TPW * 32 + 64 B per k instead of TPW * 32 + 128.
+template <int NB, bool FIRST, int TPW, int NBW>
 __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p) {
-  __shared__ f32x4 part[LW][TPW][NB][64];
+  static_assert(NBW == NB || NBW == 1, "row blocks per workgroup");
+  __shared__ f32x4 part[LW][TPW][NBW][64];
   __shared__ int s_tok[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile0 = blockIdx.x * TPW;  // this workgroup's row tiles tile0 .. tile0 + TPW - 1
+  int grp = blockIdx.x, cb0 = 0;  // tile group, first row block
+  if constexpr (NBW != NB) {
+    const int idx = blockIdx.x >> 3;
+    grp = (idx >> 1) * 8 + (blockIdx.x & 7);
+    cb0 = idx & 1;
+  }
+  const int tile0 = grp * TPW;  // this workgroup's row tiles tile0 .. tile0 + TPW - 1
   const int ntile = p.R >> 4;
+  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
+  if (tile0 >= ntile || cb0 >= nba) return;      // (grid padding of the twin mapping; low-load program)
+  const int nbw = min(NBW, nba - cb0);           // row blocks this workgroup computes
   const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;
   const int spw = (KS + LW - 1) / LW;
   const int k0 = wave * spw;
   const int cnt = max(0, min(spw, KS - k0));
   const int Bp = NB * 16;
-  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
-  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && tile0 < ntile && nba <= NB)) return;
+  if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && nba <= NB)) return;
   // ---- loads that need nothing: this sub-step's control + the decoder maxima (FIRST), then the
   // weight stream; vmcnt retires in issue order, so what the token selection waits for goes first
   HzLmbCtl cl = {};
@@ -97,7 +111,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   const int par = (*p.gpar + p.step_off) & 1;
   // state operands: h_prev (own, parity par) for k < Kh; x for k >= Kh (previous layer's output
   // of this step, parity par ^ 1; FIRST: the embedding rows of the tokens, after selection)
-  u32x4 ah[SPW][NB], al[SPW][NB];
+  u32x4 ah[SPW][NBW], al[SPW][NBW];
 #pragma unroll
   for (int s = 0; s < SPW; ++s) {
     const int ks = min(k0 + s, KS - 1);
@@ -109,17 +123,17 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
                            : p.x + ((size_t)((par ^ 1) * 2) * KSX + (ks - KSH)) * NB * 512;
     const size_t lo_off = (size_t)(hk ? KSH : KSX) * NB * 512;
 #pragma unroll
-    for (int cb = 0; cb < NB; ++cb) {
-      if (cb < nba) {
-        ah[s][cb] = *reinterpret_cast<const u32x4*>(src + cb * 512 + lane * 8);
-        al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + cb * 512 + lane * 8);
+    for (int cb = 0; cb < NBW; ++cb) {
+      if (cb < nbw) {
+        ah[s][cb] = *reinterpret_cast<const u32x4*>(src + (cb0 + cb) * 512 + lane * 8);
+        al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + (cb0 + cb) * 512 + lane * 8);
       }
     }
   }
   if constexpr (FIRST) {
     // ---- token of every row: the argmax of the acceptable keys of the last decoder (its
-    // workgroups' atomic maxima, buffer of the other parity); workgroup 0 clears this parity's
-    // buffer for this step's decoder
+    // workgroups' atomic maxima, buffer of the other parity); the first workgroup clears this
+    // parity's buffer for this step's decoder
     if (tid < Bp) {
       // (measured: sharding these maxima over 8 atomic slots made this kernel 1.3 us slower and
       // the decoder no faster, profiles/r3_lmbatch)
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       int tok = cl.tok >= 0 ? cl.tok : (cl.tok == -1 && best ? key_row(best) : 0);
       tok = min(max(tok, 0), p.V - 1);
       s_tok[tid] = tok;
-      if (tile0 == 0) {
+      if (tile0 == 0 && cb0 == 0) {
         p.dbest[(size_t)par * Bp + tid] = 0ull;  // for this step's decoder
         if (p.tok) p.tok[tid] = tok;
         if (cl.tok == -1 && cl.out >= 0 && p.outp[tid]) p.outp[tid][cl.out] = tok;
@@ -140,9 +154,9 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       const int ks = min(k0 + s, KS - 1);
       if (ks >= KSH) {  // wave-uniform
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) {
-          if (cb >= nba) continue;
-          const int tk = s_tok[cb * 16 + (lane & 15)];
+        for (int cb = 0; cb < NBW; ++cb) {
+          if (cb >= nbw) continue;
+          const int tk = s_tok[(cb0 + cb) * 16 + (lane & 15)];
           ah[s][cb] = *reinterpret_cast<const u32x4*>(
               p.emb + ((size_t)(tk >> 4) * KSX + (ks - KSH)) * 512 + ((lane >> 4) * 16 + (tk & 15)) * 8);
         }
@@ -150,11 +164,11 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     }
   }
   // ---- MFMAs over this wave's k-steps
-  f32x4 acc[TPW][NB];
+  f32x4 acc[TPW][NBW];
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
-    for (int cb = 0; cb < NB; ++cb) acc[tt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cb = 0; cb < NBW; ++cb) acc[tt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < SPW; ++s) {
     if (s < cnt) {  // wave-uniform
@@ -162,8 +176,8 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
 #pragma unroll
       for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) {
-          if (cb >= nba) continue;
+        for (int cb = 0; cb < NBW; ++cb) {
+          if (cb >= nbw) continue;
           acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(ah[s][cb]), acc[tt][cb], 0, 0, 0);
           if (lo)
             acc[tt][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wf[tt][s]), as_frag(al[s][cb]), acc[tt][cb], 0, 0, 0);
@@ -173,17 +187,18 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
-    for (int cb = 0; cb < NB; ++cb) part[wave][tt][cb][lane] = acc[tt][cb];
+    for (int cb = 0; cb < NBW; ++cb) part[wave][tt][cb][lane] = acc[tt][cb];
   __syncthreads();
-  // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row cb*16 + (l & 15);
-  // its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows 4(l>>4) .. +3)
-  if (tid < TPW * NB * 64 && (tid >> 6) % NB < nba) {
-    const int tt = tid / (NB * 64), cb = (tid >> 6) % NB, l = tid & 63;
+  // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row
+  // (cb0+cb)*16 + (l & 15); its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows
+  // 4(l>>4) .. +3)
+  if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw) {
+    const int tt = tid / (NBW * 64), cb = (tid >> 6) % NBW, l = tid & 63;
     f32x4 g = part[0][tt][cb][l];
 #pragma unroll
     for (int w = 1; w < LW; ++w) g += part[w][tt][cb][l];  // fixed order: deterministic
-    const int j = (tile0 + tt) * 4 + (l >> 4), r = cb * 16 + (l & 15);
-    if (j < p.H) {
+    const int j = (tile0 + tt) * 4 + (l >> 4), r = (cb0 + cb) * 16 + (l & 15);
+    if (tile0 + tt < ntile && j < p.H) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + 4 * j);
       g += b;
       const float si = 1.f / (1.f + __expf(-g[0]));
@@ -412,26 +427,31 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
   if ((KS + LW - 1) / LW > SPW) return -1;
   if (first && (!p.ctl || !p.dbest || !p.outp || p.V < 16)) return -1;
   if (!first && !p.x) return -1;
-  // tiles per workgroup: 2 halves the state operand each weight byte is paired with (every
-  // workgroup reads all Bp rows' state over its K) and fits the grid in one pass of the CUs
-  const char* tpw_env = getenv("HIPZAP_LMB_TPW");
-  const int tpw = tpw_env && tpw_env[0] == '1' ? 1 : 2;
-  const dim3 grid((p.R / 16 + tpw - 1) / tpw), block(512);
-#define HZ_LMBL(NB, T)                                                                        \
-  if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T>), grid, block, 0, st, p);     \
-  else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T>), grid, block, 0, st, p);
+  // workgroup shape: HIPZAP_LMB_LAYER = "t2" (round 3: 2 tiles x all rows), "t1" (1 tile x all
+  // rows) or, at Bp 32, "t3h" (default: 3 tiles x one row block, twin workgroups)
+  static const int shape = [] {
+    const char* e = getenv("HIPZAP_LMB_LAYER");
+    if (e && !strcmp(e, "t1")) return 1;
+    if (e && !strcmp(e, "t2")) return 2;
+    return 3;
+  }();
+  const int ntile = p.R / 16;
+#define HZ_LMBL(NB, T, NBW)                                                                    \
+  do {                                                                                         \
+    const int groups = (ntile + T - 1) / T;                                                    \
+    const dim3 grid(NBW == NB ? groups : 2 * ((groups + 7) / 8 * 8)), block(512);              \
+    if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW>), grid, block, 0, st, p); \
+    else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T, NBW>), grid, block, 0, st, p);     \
+  } while (0)
   if (p.Bp == 16) {
-    if (tpw == 1) {
-      HZ_LMBL(1, 1)
-    } else {
-      HZ_LMBL(1, 2)
-    }
+    if (shape == 1) HZ_LMBL(1, 1, 1);
+    else HZ_LMBL(1, 2, 1);
+  } else if (p.nb_act == 1) {
+    HZ_LMBL(2, 2, 2);  // low-load program: 2 tiles x the first row block (64 + 64 B per k)
   } else {
-    if (tpw == 1) {
-      HZ_LMBL(2, 1)
-    } else {
-      HZ_LMBL(2, 2)
-    }
+    if (shape == 1) HZ_LMBL(2, 1, 2);
+    else if (shape == 2) HZ_LMBL(2, 2, 2);
+    else HZ_LMBL(2, 3, 1);
   }
 #undef HZ_LMBL
   return (int)hipGetLastError();

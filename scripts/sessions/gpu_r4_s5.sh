@@ -11,8 +11,9 @@ for lo in 0 1; do
   HIPZAP_LM_LOWLOAD=$lo timeout -k 10 200 python scripts/bench_lm_batch.py --clients 1 32 --requests 12 > $O/lm_lo$lo.json 2> $O/lm_err.log || { tail -20 $O/lm_err.log; exit 1; }
   tail -c 600 $O/lm_lo$lo.json; echo
 done
-for pipe in 4x5 4x6 8x2; do
-  HIPZAP_LMB_DEC_PIPE=$pipe timeout -k 10 200 python scripts/bench_lm_batch.py --clients 1 32 --requests 12 > $O/lm_pipe$pipe.json 2> $O/lm_err.log || { tail -20 $O/lm_err.log; exit 1; }
+for pipe in 4x5 4x6 8x2 t2 t1; do
+  lay=t3h; dp=$pipe; case $pipe in t*) lay=$pipe; dp=8x2;; esac
+  HIPZAP_LMB_LAYER=$lay HIPZAP_LMB_DEC_PIPE=$dp timeout -k 10 200 python scripts/bench_lm_batch.py --clients 1 32 --requests 12 > $O/lm_pipe$pipe.json 2> $O/lm_err.log || { tail -20 $O/lm_err.log; exit 1; }
   tail -c 600 $O/lm_pipe$pipe.json; echo
 done
 B="--steps 300 --warmup 30 --cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
