@@ -537,6 +537,176 @@ __global__ __launch_bounds__(512) void bneck_kernel(const HzBneckParams p) {
   HZ_BSTAMP_FLUSH(CIN == 64 ? 1 : 2);
 }
 
+// ------------------------------------------------------------------------------------------------
+// bottleneck block, layer2 geometry (28 x 28, Cin = Cout = 512, Cmid 128, stride 1, identity
+// residual): 544 KB of weights per workgroup, far more than registers hold, so every wave STREAMS
+// its weight fragments in use order (conv1 16, conv2 36, conv3 4 x 4 k-steps) through a ring of
+// kB2D registers fragments: fragment i + kB2D is issued as soon as fragment i has been multiplied,
+// and the LDS barriers between the convs wait for LDS traffic only, so the stream never drains.
+// A workgroup owns a 4 x 4 output tile (49 workgroups at 28 x 28): the 6 x 6 x 512 input patch
+// goes to LDS, conv1 (wave = one of the 8 mid-channel fragments) runs over the 36 halo pixels,
+// conv2 (wave = one mid-channel fragment, all 36 k-steps) over the 16 output pixels, conv3 (wave =
+// 4 of the 32 output-channel fragments) adds the identity residual from the staged patch.
+constexpr int kB2T = 4, kB2HW = kB2T + 2, kB2NP = kB2HW * kB2HW;  // 4 x 4 tile, 6 x 6 halo, 36 px
+constexpr int kB2NF1 = 3;                                           // conv1 pixel fragments (48 slots)
+constexpr int kB2CI = 512, kB2CM = 128, kB2CO = 512;
+constexpr int kB2KS1 = kB2CI / 32, kB2KS2 = 9 * kB2CM / 32, kB2KS3 = kB2CM / 32;  // 16, 36, 4
+constexpr int kB2NW = kB2KS1 + kB2KS2 + 4 * kB2KS3;                 // 68 fragments per wave
+constexpr int kB2D = 20;                                            // fragments in flight per wave
+// conv1 output image: rows of 12 pixel slots, 288-B pixel stride, no swizzle (conflict-free for
+// every conv2 tap with the tap offset an immediate; MI355X_MICROARCH.md lane-group model)
+constexpr int kB2T1Row = 12, kB2T1Pix = 144;
+__device__ __forceinline__ int b2_t1(int hy, int hx) { return (hy * kB2T1Row + hx) * kB2T1Pix; }
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
+  constexpr int XCH = kB2CI / 8, NQ = kB2NP * XCH, NL = (NQ + 511) / 512;
+  __shared__ __attribute__((aligned(16))) bf16_t X[16 * kB2NF1 * kB2CI];          // 48 pixel slots
+  __shared__ __attribute__((aligned(16))) bf16_t T1[(5 * kB2T1Row + 6) * kB2T1Pix];
+  __shared__ __attribute__((aligned(16))) bf16_t T2[16 * kB2CM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int tx_n = p.W / kB2T, ty_n = p.H / kB2T, per_img = tx_n * ty_n;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = b / per_img, rem = b - n * per_img;
+  const int ty = rem / tx_n, tx = rem - ty * tx_n;
+  const int y0 = ty * kB2T, x0 = tx * kB2T;
+  HZ_BSTAMP_DECL
+  HZ_BSTAMP(0);
+  // ---- input patch loads (6 x 6 x 512, zero outside the image) ----
+  u32x4 xv[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    xv[i] = u32x4{0u, 0u, 0u, 0u};
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
+      const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
+      const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+      if ((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)
+        xv[i] = *reinterpret_cast<const u32x4*>(p.x + ((((long)n * (kB2CI / 32) + cb) * p.H + gy) * p.W + gx) * 32 + sub * 8);
+    }
+  }
+  // ---- folded-BN biases ----
+  const f32x4 bias1 = *reinterpret_cast<const f32x4*>(p.b1 + 16 * wave + 4 * g);
+  const f32x4 bias2 = *reinterpret_cast<const f32x4*>(p.b2 + 16 * wave + 4 * g);
+  f32x4 bias3[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias3[i] = *reinterpret_cast<const f32x4*>(p.b3 + 16 * (4 * wave + i) + 4 * g);
+  // ---- the weight stream: fragment i of this wave's use order ----
+  bf16x8 wr[kB2NW];
+  auto fetch = [&](int i) {
+    if (i < kB2KS1) wr[i] = ldw(p.w1, wave, kB2KS1, i, lane);
+    else if (i < kB2KS1 + kB2KS2) wr[i] = ldw(p.w2, wave, kB2KS2, i - kB2KS1, lane);
+    else {
+      const int j = i - kB2KS1 - kB2KS2;  // conv3: k-step j / 4 of output fragment 4 * wave + j % 4
+      wr[i] = ldw(p.w3, 4 * wave + (j & 3), kB2KS3, j >> 2, lane);
+    }
+  };
+  auto consumed = [&](int i) {  // fragment i has been multiplied: refill its ring slot
+    if (i + kB2D < kB2NW) fetch(i + kB2D);
+  };
+#pragma unroll
+  for (int i = 0; i < kB2D; ++i) fetch(i);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
+      *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
+    }
+  }
+  lds_sync();
+  HZ_BSTAMP(1);
+  // ---- conv1 (1x1, 512 -> 128) over the 36 halo pixels (3 fragments; slots 36..47 are computed
+  // from unwritten LDS and discarded) ----
+  {
+    f32x4 acc[kB2NF1];
+#pragma unroll
+    for (int f = 0; f < kB2NF1; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kB2KS1; ++s) {
+      bf16x8 bv[kB2NF1];
+#pragma unroll
+      for (int f = 0; f < kB2NF1; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+#pragma unroll
+      for (int f = 0; f < kB2NF1; ++f) acc[f] = mfma16(wr[s], bv[f], acc[f]);
+      consumed(s);
+    }
+    const int ch = 16 * wave + 4 * g;
+#pragma unroll
+    for (int f = 0; f < kB2NF1; ++f) {
+      const int pp = 16 * f + l16;
+      if (pp >= kB2NP) continue;
+      const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
+      const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)p.H && (unsigned)(x0 - 1 + hx) < (unsigned)p.W;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[f][e] + bias1[e], 0.f) : 0.f;  // conv2's zero padding
+      *reinterpret_cast<u32x2*>(T1 + b2_t1(hy, hx) + ch) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  lds_sync();
+  HZ_BSTAMP(2);
+  // ---- conv2 (3x3, 128 -> 128) over the 16 output pixels: k-step ks = tap ks / 4, channel
+  // quarter ks % 4; the tap offset is an immediate ----
+  {
+    const int j = l16, base = b2_t1(j >> 2, j & 3) + 8 * g;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < kB2KS2; ++ks) {
+      const int tap = ks >> 2, r = tap / 3, c = tap % 3;
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + base + b2_t1(r, c) + (ks & 3) * 32);
+      acc = mfma16(wr[kB2KS1 + ks], bv, acc);
+      consumed(kB2KS1 + ks);
+    }
+    const int ch = 16 * wave + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[e] + bias2[e], 0.f);
+    *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  }
+  lds_sync();
+  HZ_BSTAMP(3);
+  // ---- conv3 (1x1, 128 -> 512) + identity residual (centre of the staged patch) + ReLU: wave ->
+  // output fragments 4w .. 4w+3 ----
+  {
+    const int j = l16, jy = j >> 2, jx = j & 3, cp = (jy + 1) * kB2HW + jx + 1;
+    bf16x8 b3[kB2KS3];
+#pragma unroll
+    for (int s = 0; s < kB2KS3; ++s) b3[s] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 16) * 8);
+    u32x2 rr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 16 * (4 * wave + i) + 4 * g;
+      rr[i] = *reinterpret_cast<const u32x2*>(X + x_chunk(cp, ch >> 3, XCH) * 8 + (ch & 4));
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = bias3[i];
+#pragma unroll
+    for (int s = 0; s < kB2KS3; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = mfma16(wr[kB2KS1 + kB2KS2 + 4 * s + i], b3[s], acc[i]);
+    HZ_BSTAMP(4);
+    const int CO32 = kB2CO / 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 16 * (4 * wave + i) + 4 * g;
+      float v[4] = {acc[i][0] + __uint_as_float(rr[i][0] << 16), acc[i][1] + __uint_as_float(rr[i][0] & 0xffff0000u),
+                    acc[i][2] + __uint_as_float(rr[i][1] << 16), acc[i][3] + __uint_as_float(rr[i][1] & 0xffff0000u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      const long o = ((((long)n * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
+      *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  HZ_BSTAMP(5);
+  HZ_BSTAMP_FLUSH(3);
+}
+
 }  // namespace
 
 extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
@@ -553,6 +723,11 @@ extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
 
 extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   const HzBneckParams& p = *pp;
+  if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles, identity residual
+    if (p.N < 1 || p.Cin != kB2CI || p.Cout != kB2CO || p.wd || p.H % kB2T || p.W % kB2T) return -1;
+    hipLaunchKernelGGL(bneck2_kernel, dim3((p.H / kB2T) * (p.W / kB2T) * p.N), dim3(512), 0, st, p);
+    return (int)hipGetLastError();
+  }
   const int th = p.tile_h ? p.tile_h : 8;
   if (p.N < 1 || (th != 8 && th != 4) || p.H % th || p.W % kBnTW || p.Cmid != kBnCM || p.Cout != kBnCO) return -1;
   const int tiles = (p.H / th) * (p.W / kBnTW) * p.N;

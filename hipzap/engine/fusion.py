@@ -9,7 +9,9 @@ bind as ONE fused kernel instead:
   input): the default, since a zero-copy request read inside the 98-workgroup stem cost served
   throughput (profiles/r4_fuse/README.md);
 * ``bneck``: a layer1-geometry bottleneck (1x1 Cin -> 64, 3x3 64 -> 64, 1x1 64 -> 256 + residual,
-  optionally with its 1x1 downsample) -> ``hz_bneck_launch``.
+  optionally with its 1x1 downsample) -> ``hz_bneck_launch``;
+* ``bneck2``: a layer2 identity bottleneck (1x1 512 -> 128, 3x3 128 -> 128, 1x1 128 -> 512 +
+  residual) -> ``hz_bneck_launch`` (the weight-streaming ``bneck2_kernel``).
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
@@ -27,7 +29,7 @@ import numpy as np
 from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK = 18, 19
-KINDS = ("stem", "convpool", "bneck")
+KINDS = ("stem", "convpool", "bneck", "bneck2")
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -58,7 +60,7 @@ def enabled_kinds(spec: str | None = None) -> set:
     if v in ("", "0", "none", "off"):
         return set()
     if v in ("1", "all", "on"):
-        return {"stem", "bneck"}
+        return {"stem", "bneck", "bneck2"}
     return {k for k in v.split(",") if k in KINDS}
 
 
@@ -112,7 +114,9 @@ def match_convpool(g, params, i: int) -> Fused | None:
     return Fused("convpool", i, i + 2, [cv, mp])
 
 
-def match_bneck(g, params, i: int) -> Fused | None:
+def match_bneck(g, params, i: int, layer2: bool = False) -> Fused | None:
+    """layer1 geometry (``bneck``: Cmid 64, Cout 256, optional downsample) or, with ``layer2``,
+    the identity blocks of layer2 (``bneck2``: Cin = Cout = 512, Cmid 128)."""
     nodes = g.nodes
     run = nodes[i:i + 4]
     if len(run) < 3 or not all(_conv(n) for n in run[:3]):
@@ -136,6 +140,14 @@ def match_bneck(g, params, i: int) -> Fused | None:
     p1, p2, p3 = (params.get(n.attrs.get("w")) for n in (c1, c2, c3))
     if p1 is None or p2 is None or p3 is None:
         return None
+    if layer2:
+        if ds is not None or not (_geom(p1, 512, 128, 1, 1, 0) and _geom(p2, 128, 128, 3, 1, 1)
+                                  and _geom(p3, 128, 512, 1, 1, 0)):
+            return None
+        nb, h, w, c = g.shape(x)
+        if c != 512 or h % 4 or w % 4:  # (4x4 output tiles)
+            return None
+        return Fused("bneck2", i, i + 3, [c1, c2, c3])
     cin = 64 if ds is not None else 256
     if not (_geom(p1, cin, 64, 1, 1, 0) and _geom(p2, 64, 64, 3, 1, 1) and _geom(p3, 64, 256, 1, 1, 0)):
         return None
@@ -164,6 +176,8 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
             f = match_convpool(g, params, i)
         if f is None and "bneck" in kinds:
             f = match_bneck(g, params, i)
+        if f is None and "bneck2" in kinds:
+            f = match_bneck(g, params, i, layer2=True)
         if f is not None:
             out[i] = f
             i = f.end
@@ -223,7 +237,7 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
         p.wd, p.bd = pd.wf.data_ptr(), pd.bias.data_ptr()
     p.N, p.H, p.W, p.Cin = g.shape(c1.inputs[0])
     p.Cmid, p.Cout = p1.cout, p3.cout
-    p.tile_h = int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # output tile rows (8: 49 workgroups at 56x56)
+    p.tile_h = 0 if p.Cmid == 128 else int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # layer1 tile rows
     return p
 
 

@@ -4,6 +4,8 @@
 // back-to-back launches captured in a hipGraph. Stem phases: 0 start, 1 patch in LDS, 2 MFMAs
 // done, 3 stem outputs in LDS, 4 pooled stores issued. Bottleneck phases: 0 start, 1 input patch
 // in LDS, 2 conv1 done, 3 conv2 MFMAs done, 4 conv2 epilogue done, 5 conv3 MFMAs done, 6 stores.
+// Layer2 bottleneck (weight-streaming): 0 start, 1 patch in LDS, 2 conv1 done, 3 conv2 done,
+// 4 conv3 MFMAs done, 5 stores issued.
 // Build + run: scripts/sessions/gpu_r4_stamps.sh (hipcc --offload-arch=gfx950 -I hipzap/csrc).
 #include <hip/hip_runtime.h>
 
@@ -13,8 +15,8 @@
 #include <cstring>
 #include <vector>
 
-__device__ unsigned long long g_bstamps[3][512][8];
-__device__ unsigned long long g_bclock[3][512][2];  // s_memtime (shader clock) at the first / last stamp
+__device__ unsigned long long g_bstamps[4][512][8];
+__device__ unsigned long long g_bclock[4][512][2];  // s_memtime (shader clock) at the first / last stamp
 #define HZ_BSTAMP 1
 #define HZ_BSTAMP_DECL unsigned long long hz_bst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hz_clk0 = __builtin_amdgcn_s_memtime();
 #define HZ_BSTAMP(i) hz_bst[i] = __builtin_amdgcn_s_memrealtime()
@@ -148,6 +150,24 @@ int main() {
     char name[64];
     snprintf(name, sizeof name, "bneck_cin%d%s_th%d", cin, cin == 64 ? "_ds" : "", th);
     report(name, cin == 64 ? 1 : 2, 56 / th * 7, 7, t);
+  }
+  // ---- layer2 identity bottleneck at 28x28 (Cin = Cout = 512, Cmid 128)
+  {
+    HzBneckParams bp{};
+    bp.x = (const unsigned short*)dev_random((size_t)512 * 28 * 28 * 2, 14, true);
+    bp.w1 = (const unsigned short*)dev_random((size_t)128 * 512 * 2, 15, true);
+    bp.b1 = (const float*)dev_random(2048, 16, false);
+    bp.w2 = (const unsigned short*)dev_random((size_t)128 * 1152 * 2, 17, true);
+    bp.b2 = (const float*)dev_random(2048, 18, false);
+    bp.w3 = (const unsigned short*)dev_random((size_t)512 * 128 * 2, 19, true);
+    bp.b3 = (const float*)dev_random(2048, 20, false);
+    for (const float* b : {bp.b1, bp.b2, bp.b3}) CK(hipMemset((void*)b, 0, 2048));
+    CK(hipMalloc((void**)&bp.out, (size_t)512 * 28 * 28 * 2));
+    bp.N = 1, bp.H = 28, bp.W = 28, bp.Cin = 512, bp.Cmid = 128, bp.Cout = 512;
+    CK((hipError_t)hz_bneck_launch(&bp, st));
+    CK(hipStreamSynchronize(st));
+    const double t = graph_us([&] { hz_bneck_launch(&bp, st); }, st, 64);
+    report("bneck2_cin512", 3, 49, 6, t);
   }
   return 0;
 }

@@ -18,7 +18,7 @@ for pipe in 4x5 4x6 8x2 t2 t1; do
 done
 B="--steps 300 --warmup 30 --cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
 for rep in 1 2; do
-  for v in none bneck convpool,bneck convpool,bneck:out; do
+  for v in none convpool,bneck convpool,bneck,bneck2 convpool,bneck,bneck2:out; do
     f=${v%%:*}; zc=all; [ "$v" != "$f" ] && zc=${v##*:}
     tag=${v//[,:]/_}
     HIPZAP_FUSE=$f HIPZAP_ZERO_COPY=$zc timeout -k 10 200 python bench.py $B > $O/bench_${tag}_$rep.json 2> $O/bench_err.log \

@@ -1,5 +1,6 @@
 """Fused ResNet stages (csrc/block.hip, engine/fusion.py) on MI355X: the stem kernel (image ->
-normalise -> 7x7/2 conv -> max-pool) and the layer1 bottleneck kernel against (a) the per-conv
+normalise -> 7x7/2 conv -> max-pool), the layer1 bottleneck kernel and the weight-streaming
+layer2 bottleneck kernel against (a) the per-conv
 program of the same packed weights and (b) the fp32 graph oracle, tensor by tensor; graph replay,
 batch > 1 and the dispatch count."""
 import pytest
@@ -48,7 +49,8 @@ def _fused_tensors(ctx):
 
 @pytest.mark.parametrize("uint8,batch,th,fuse", [(True, 1, 8, "all"), (False, 1, 8, "all"), (True, 3, 8, "all"),
                                                 (True, 1, 4, "all"), (True, 2, 4, "all"),
-                                                (True, 1, 8, "convpool,bneck"), (False, 2, 8, "convpool,bneck")])
+                                                (True, 1, 8, "convpool,bneck"), (False, 2, 8, "convpool,bneck"),
+                                                (True, 1, 8, "convpool,bneck,bneck2"), (True, 2, 8, "bneck2")])
 def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, fuse, monkeypatch):
     monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")  # every intermediate stays readable after the run
     monkeypatch.setenv("HIPZAP_BNECK_TH", str(th))  # 8x8 or 4x8 bottleneck output tiles
@@ -57,7 +59,10 @@ def test_fused_matches_per_conv_program_and_oracle(r50, uint8, batch, th, fuse, 
     fused = ExecContext(g, params, torch.device(DEV), fuse=fuse)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     kinds = [f.kind for f in fused.fused.values()]
-    assert kinds == ["stem" if fuse == "all" else "convpool", "bneck", "bneck", "bneck"], kinds
+    want = fusion.enabled_kinds(fuse)
+    expect = (["stem"] if "stem" in want else ["convpool"] if "convpool" in want else []) + \
+        ["bneck"] * 3 * ("bneck" in want) + ["bneck2"] * 3 * ("bneck2" in want)
+    assert kinds == expect, kinds
     assert plain.fused == {}
     gen = torch.Generator().manual_seed(batch)
     if uint8:
@@ -86,8 +91,9 @@ def test_fused_dispatch_count_and_replay(r50):
     g = a.build_graph(batch=1, **dict(kw, input_uint8=True))
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     ctx = ExecContext(g, params, torch.device(DEV), fuse="all")
-    assert plain.num_ops() - ctx.num_ops() == 8  # stem 3 -> 1, three layer1 blocks 3 -> 1 each
-    assert ctx.num_ops() <= 45
+    # stem 3 -> 1, three layer1 blocks and three layer2 identity blocks 3 -> 1 each
+    assert plain.num_ops() - ctx.num_ops() == 14
+    assert ctx.num_ops() <= 39
     assert plain.num_ops() - ExecContext(g, params, torch.device(DEV)).num_ops() == 7  # default: convpool
     s = torch.cuda.Stream()
     ctx.capture(s)
