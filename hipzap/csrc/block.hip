@@ -707,6 +707,169 @@ __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
   HZ_BSTAMP_FLUSH(3);
 }
 
+// ------------------------------------------------------------------------------------------------
+// first block of layer2 (56 x 56 x 256 -> 28 x 28 x 512: conv1 1x1 256 -> 128, conv2 3x3 stride 2,
+// conv3 1x1 128 -> 512 + the 1x1 stride-2 downsample 256 -> 512 into the same accumulators):
+// the same weight stream as bneck2_kernel (8 + 36 + 16 + 32 = 92 fragments per wave). A 4 x 4
+// output tile reads a 9 x 9 halo of conv1 outputs (81 pixels, 6 fragments); the downsample reads
+// the staged input at the odd halo positions.
+constexpr int kB2dHW = 2 * kB2T + 1, kB2dNP = kB2dHW * kB2dHW;  // 9 x 9 halo, 81 px
+constexpr int kB2dNF1 = 6, kB2dCI = 256;
+constexpr int kB2dKS1 = kB2dCI / 32, kB2dKSD = kB2dCI / 32;          // 8, 8
+constexpr int kB2dNW = kB2dKS1 + kB2KS2 + 4 * kB2KS3 + 4 * kB2dKSD;  // 92
+// conv1 output image: rows of 10 pixel slots, 288-B pixel stride, chunk ^= halo column (stride-2
+// taps: conflict-free by the lane-group model)
+constexpr int kB2dRow = 10, kB2dPix = 144;
+__device__ __forceinline__ int b2d_t1(int hy, int hx, int chunk) {
+  return (hy * kB2dRow + hx) * kB2dPix + ((chunk ^ (hx & 15)) << 3);
+}
+
+__global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
+  constexpr int XCH = kB2dCI / 8, NQ = kB2dNP * XCH, NL = (NQ + 511) / 512;
+  __shared__ __attribute__((aligned(16))) bf16_t X[16 * kB2dNF1 * kB2dCI];        // 96 pixel slots
+  __shared__ __attribute__((aligned(16))) bf16_t T1[(8 * kB2dRow + 9) * kB2dPix];
+  __shared__ __attribute__((aligned(16))) bf16_t T2[16 * kB2CM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int tx_n = p.W / kB2T, ty_n = p.H / kB2T, per_img = tx_n * ty_n;  // OUTPUT geometry (28 x 28)
+  const int IH = 2 * p.H, IW = 2 * p.W;                                   // input 56 x 56
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = b / per_img, rem = b - n * per_img;
+  const int ty = rem / tx_n, tx = rem - ty * tx_n;
+  const int y0 = ty * kB2T, x0 = tx * kB2T;
+  const int iy0 = 2 * y0 - 1, ix0 = 2 * x0 - 1;  // halo origin in the input
+  HZ_BSTAMP_DECL
+  HZ_BSTAMP(0);
+  u32x4 xv[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    xv[i] = u32x4{0u, 0u, 0u, 0u};
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
+      const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
+      const int gy = iy0 + hy, gx = ix0 + hx;
+      if ((unsigned)gy < (unsigned)IH && (unsigned)gx < (unsigned)IW)
+        xv[i] = *reinterpret_cast<const u32x4*>(p.x + ((((long)n * (kB2dCI / 32) + cb) * IH + gy) * IW + gx) * 32 + sub * 8);
+    }
+  }
+  const f32x4 bias1 = *reinterpret_cast<const f32x4*>(p.b1 + 16 * wave + 4 * g);
+  const f32x4 bias2 = *reinterpret_cast<const f32x4*>(p.b2 + 16 * wave + 4 * g);
+  f32x4 bias3[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    bias3[i] = *reinterpret_cast<const f32x4*>(p.b3 + 16 * (4 * wave + i) + 4 * g) +
+               *reinterpret_cast<const f32x4*>(p.bd + 16 * (4 * wave + i) + 4 * g);
+  constexpr int O2 = kB2dKS1, O3 = O2 + kB2KS2, OD = O3 + 4 * kB2KS3;  // stream offsets
+  bf16x8 wr[kB2dNW];
+  auto fetch = [&](int i) {
+    if (i < O2) wr[i] = ldw(p.w1, wave, kB2dKS1, i, lane);
+    else if (i < O3) wr[i] = ldw(p.w2, wave, kB2KS2, i - O2, lane);
+    else if (i < OD) wr[i] = ldw(p.w3, 4 * wave + ((i - O3) & 3), kB2KS3, (i - O3) >> 2, lane);
+    else wr[i] = ldw(p.wd, 4 * wave + ((i - OD) & 3), kB2dKSD, (i - OD) >> 2, lane);
+  };
+  auto consumed = [&](int i) {
+    if (i + kB2D < kB2dNW) fetch(i + kB2D);
+  };
+#pragma unroll
+  for (int i = 0; i < kB2D; ++i) fetch(i);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int q = tid + 512 * i;
+    if (q < NQ) {
+      const int sub = q & 3, pc = q >> 2;
+      const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
+      *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
+    }
+  }
+  lds_sync();
+  HZ_BSTAMP(1);
+  // ---- conv1 (1x1, 256 -> 128) over the 81 halo pixels ----
+  {
+    f32x4 acc[kB2dNF1];
+#pragma unroll
+    for (int f = 0; f < kB2dNF1; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kB2dKS1; ++s) {
+      bf16x8 bv[kB2dNF1];
+#pragma unroll
+      for (int f = 0; f < kB2dNF1; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+#pragma unroll
+      for (int f = 0; f < kB2dNF1; ++f) acc[f] = mfma16(wr[s], bv[f], acc[f]);
+      consumed(s);
+    }
+    const int ch = 16 * wave + 4 * g;
+#pragma unroll
+    for (int f = 0; f < kB2dNF1; ++f) {
+      const int pp = 16 * f + l16;
+      if (pp >= kB2dNP) continue;
+      const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
+      const bool in = (unsigned)(iy0 + hy) < (unsigned)IH && (unsigned)(ix0 + hx) < (unsigned)IW;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[f][e] + bias1[e], 0.f) : 0.f;
+      *reinterpret_cast<u32x2*>(T1 + b2d_t1(hy, hx, ch >> 3) + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  lds_sync();
+  HZ_BSTAMP(2);
+  // ---- conv2 (3x3 stride 2, 128 -> 128): output (jy, jx) reads halo (2jy + r, 2jx + c) ----
+  {
+    const int j = l16, jy = j >> 2, jx = j & 3;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < kB2KS2; ++ks) {
+      const int tap = ks >> 2, r = tap / 3, c = tap % 3;
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + b2d_t1(2 * jy + r, 2 * jx + c, 4 * (ks & 3) + g));
+      acc = mfma16(wr[O2 + ks], bv, acc);
+      consumed(O2 + ks);
+    }
+    const int ch = 16 * wave + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[e] + bias2[e], 0.f);
+    *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  }
+  lds_sync();
+  HZ_BSTAMP(3);
+  // ---- conv3 (1x1, 128 -> 512) + downsample (1x1 stride 2, 256 -> 512) + ReLU ----
+  {
+    const int j = l16, jy = j >> 2, jx = j & 3, dp = (2 * jy + 1) * kB2dHW + 2 * jx + 1;
+    bf16x8 b3[kB2KS3], bd[kB2dKSD];
+#pragma unroll
+    for (int s = 0; s < kB2KS3; ++s) b3[s] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 16) * 8);
+#pragma unroll
+    for (int s = 0; s < kB2dKSD; ++s) bd[s] = *reinterpret_cast<const bf16x8*>(X + x_chunk(dp, 4 * s + g, XCH) * 8);
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = bias3[i];
+#pragma unroll
+    for (int s = 0; s < kB2KS3; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i] = mfma16(wr[O3 + 4 * s + i], b3[s], acc[i]);
+        consumed(O3 + 4 * s + i);
+      }
+#pragma unroll
+    for (int s = 0; s < kB2dKSD; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = mfma16(wr[OD + 4 * s + i], bd[s], acc[i]);
+    HZ_BSTAMP(4);
+    const int CO32 = kB2CO / 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 16 * (4 * wave + i) + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[i][e], 0.f);
+      const long o = ((((long)n * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
+      *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
+  }
+  HZ_BSTAMP(5);
+  HZ_BSTAMP_FLUSH(4);
+}
+
 }  // namespace
 
 extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
@@ -723,9 +886,12 @@ extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
 
 extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   const HzBneckParams& p = *pp;
-  if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles, identity residual
-    if (p.N < 1 || p.Cin != kB2CI || p.Cout != kB2CO || p.wd || p.H % kB2T || p.W % kB2T) return -1;
-    hipLaunchKernelGGL(bneck2_kernel, dim3((p.H / kB2T) * (p.W / kB2T) * p.N), dim3(512), 0, st, p);
+  if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles (H, W: the block's OUTPUT size)
+    if (p.N < 1 || p.Cout != kB2CO || p.H % kB2T || p.W % kB2T) return -1;
+    const dim3 grid((p.H / kB2T) * (p.W / kB2T) * p.N);
+    if (p.Cin == kB2CI && !p.wd) hipLaunchKernelGGL(bneck2_kernel, grid, dim3(512), 0, st, p);
+    else if (p.Cin == kB2dCI && p.wd && p.bd) hipLaunchKernelGGL(bneck2d_kernel, grid, dim3(512), 0, st, p);
+    else return -1;
     return (int)hipGetLastError();
   }
   const int th = p.tile_h ? p.tile_h : 8;

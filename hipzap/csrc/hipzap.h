@@ -427,11 +427,12 @@ typedef struct HzBneckParams {
   const float* b2;
   const unsigned short* w3;
   const float* b3;
-  const unsigned short* wd;   // downsample (Cin 64) or NULL (Cin 256, identity residual)
+  const unsigned short* wd;   // downsample (layer1: Cin 64; layer2: Cin 256, stride 2) or NULL (identity)
   const float* bd;
   unsigned short* out;        // [N][Cout/32][H][W][32]
-  int N, H, W, Cin, Cmid, Cout;
-  int tile_h, pad_;           // output tile rows: 8 (default when 0) or 4 (twice the workgroups)
+  int N, H, W, Cin, Cmid, Cout;  // H, W: the block's OUTPUT size (the input is 2H x 2W for the
+                                 //   stride-2 first block of layer2)
+  int tile_h, pad_;           // layer1 output tile rows: 8 (default when 0) or 4 (twice the workgroups)
 } HzBneckParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);

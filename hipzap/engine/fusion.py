@@ -10,8 +10,9 @@ bind as ONE fused kernel instead:
   throughput (profiles/r4_fuse/README.md);
 * ``bneck``: a layer1-geometry bottleneck (1x1 Cin -> 64, 3x3 64 -> 64, 1x1 64 -> 256 + residual,
   optionally with its 1x1 downsample) -> ``hz_bneck_launch``;
-* ``bneck2``: a layer2 identity bottleneck (1x1 512 -> 128, 3x3 128 -> 128, 1x1 128 -> 512 +
-  residual) -> ``hz_bneck_launch`` (the weight-streaming ``bneck2_kernel``).
+* ``bneck2``: a layer2 bottleneck (1x1 512 -> 128, 3x3 128 -> 128, 1x1 128 -> 512 + residual;
+  or the first block: 1x1 256 -> 128, 3x3/2, 1x1 -> 512 + the 1x1/2 downsample) ->
+  ``hz_bneck_launch`` (the weight-streaming ``bneck2_kernel`` / ``bneck2d_kernel``).
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
@@ -141,13 +142,19 @@ def match_bneck(g, params, i: int, layer2: bool = False) -> Fused | None:
     if p1 is None or p2 is None or p3 is None:
         return None
     if layer2:
-        if ds is not None or not (_geom(p1, 512, 128, 1, 1, 0) and _geom(p2, 128, 128, 3, 1, 1)
-                                  and _geom(p3, 128, 512, 1, 1, 0)):
-            return None
-        nb, h, w, c = g.shape(x)
-        if c != 512 or h % 4 or w % 4:  # (4x4 output tiles)
-            return None
-        return Fused("bneck2", i, i + 3, [c1, c2, c3])
+        if ds is None:
+            if not (_geom(p1, 512, 128, 1, 1, 0) and _geom(p2, 128, 128, 3, 1, 1) and _geom(p3, 128, 512, 1, 1, 0)):
+                return None
+        else:  # the first block: stride-2 3x3 and the stride-2 downsample
+            pd = params.get(ds.attrs.get("w"))
+            if pd is None or ds.attrs.get("act", "relu") != "none" or not (
+                    _geom(pd, 256, 512, 1, 2, 0) and _geom(p1, 256, 128, 1, 1, 0) and _geom(p2, 128, 128, 3, 2, 1)
+                    and _geom(p3, 128, 512, 1, 1, 0)):
+                return None
+        nb, h, w, c = g.shape(c3.outputs[0])
+        if c != 512 or h % 4 or w % 4 or g.shape(x)[1:3] != ((h, w) if ds is None else (2 * h, 2 * w)):
+            return None  # (4x4 output tiles)
+        return Fused("bneck2", i, i + len(grp), grp)
     cin = 64 if ds is not None else 256
     if not (_geom(p1, cin, 64, 1, 1, 0) and _geom(p2, 64, 64, 3, 1, 1) and _geom(p3, 64, 256, 1, 1, 0)):
         return None
@@ -237,6 +244,8 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
         p.wd, p.bd = pd.wf.data_ptr(), pd.bias.data_ptr()
     p.N, p.H, p.W, p.Cin = g.shape(c1.inputs[0])
     p.Cmid, p.Cout = p1.cout, p3.cout
+    if p.Cmid == 128:  # layer2 kernels take the block's OUTPUT size (the first block halves it)
+        _, p.H, p.W, _ = g.shape(c3.outputs[0])
     p.tile_h = 0 if p.Cmid == 128 else int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # layer1 tile rows
     return p
 

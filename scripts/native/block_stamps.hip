@@ -15,8 +15,8 @@
 #include <cstring>
 #include <vector>
 
-__device__ unsigned long long g_bstamps[4][512][8];
-__device__ unsigned long long g_bclock[4][512][2];  // s_memtime (shader clock) at the first / last stamp
+__device__ unsigned long long g_bstamps[5][512][8];
+__device__ unsigned long long g_bclock[5][512][2];  // s_memtime (shader clock) at the first / last stamp
 #define HZ_BSTAMP 1
 #define HZ_BSTAMP_DECL unsigned long long hz_bst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hz_clk0 = __builtin_amdgcn_s_memtime();
 #define HZ_BSTAMP(i) hz_bst[i] = __builtin_amdgcn_s_memrealtime()
@@ -168,6 +168,26 @@ int main() {
     CK(hipStreamSynchronize(st));
     const double t = graph_us([&] { hz_bneck_launch(&bp, st); }, st, 64);
     report("bneck2_cin512", 3, 49, 6, t);
+  }
+  // ---- first layer2 block: 56x56x256 -> 28x28x512 (stride-2 3x3 and downsample)
+  {
+    HzBneckParams bp{};
+    bp.x = (const unsigned short*)dev_random((size_t)256 * 56 * 56 * 2, 24, true);
+    bp.w1 = (const unsigned short*)dev_random((size_t)128 * 256 * 2, 25, true);
+    bp.b1 = (const float*)dev_random(2048, 26, false);
+    bp.w2 = (const unsigned short*)dev_random((size_t)128 * 1152 * 2, 27, true);
+    bp.b2 = (const float*)dev_random(2048, 28, false);
+    bp.w3 = (const unsigned short*)dev_random((size_t)512 * 128 * 2, 29, true);
+    bp.b3 = (const float*)dev_random(2048, 30, false);
+    bp.wd = (const unsigned short*)dev_random((size_t)512 * 256 * 2, 31, true);
+    bp.bd = (const float*)dev_random(2048, 32, false);
+    for (const float* b : {bp.b1, bp.b2, bp.b3, bp.bd}) CK(hipMemset((void*)b, 0, 2048));
+    CK(hipMalloc((void**)&bp.out, (size_t)512 * 28 * 28 * 2));
+    bp.N = 1, bp.H = 28, bp.W = 28, bp.Cin = 256, bp.Cmid = 128, bp.Cout = 512;
+    CK((hipError_t)hz_bneck_launch(&bp, st));
+    CK(hipStreamSynchronize(st));
+    const double t = graph_us([&] { hz_bneck_launch(&bp, st); }, st, 64);
+    report("bneck2d_cin256_ds", 4, 49, 6, t);
   }
   return 0;
 }

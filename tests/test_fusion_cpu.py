@@ -25,9 +25,9 @@ def _plan(a, params, kw, spec, **gkw):
 @pytest.mark.parametrize("spec,expect", [
     ("none", []),
     ("convpool,bneck", ["convpool"] + ["bneck"] * 3),
-    ("all", ["stem"] + ["bneck"] * 3 + ["bneck2"] * 3),
-    ("bneck2", ["bneck2"] * 3),
-    ("convpool,bneck,bneck2", ["convpool"] + ["bneck"] * 3 + ["bneck2"] * 3),
+    ("all", ["stem"] + ["bneck"] * 3 + ["bneck2"] * 4),
+    ("bneck2", ["bneck2"] * 4),
+    ("convpool,bneck,bneck2", ["convpool"] + ["bneck"] * 3 + ["bneck2"] * 4),
 ])
 def test_resnet50_runs(r50, spec, expect):
     a, params, kw = r50
@@ -46,8 +46,10 @@ def test_resnet50_block_shapes(r50):
     b1 = [f for f in fz.values() if f.kind == "bneck"]
     b2 = [f for f in fz.values() if f.kind == "bneck2"]
     assert [len(f.nodes) for f in b1] == [4, 3, 3]  # the first layer1 block carries its downsample
-    for f in b2:  # layer2 identity blocks only: 28 x 28 x 512 in and out
-        assert g.shape(f.nodes[0].inputs[0]) == (2, 28, 28, 512) and g.shape(f.nodes[-1].outputs[0]) == (2, 28, 28, 512)
+    assert [len(f.nodes) for f in b2] == [4, 3, 3, 3]  # layer2: the first block with its downsample
+    assert g.shape(b2[0].nodes[1].inputs[0]) == (2, 56, 56, 256)
+    for f in b2:
+        assert g.shape(f.nodes[-1].outputs[0]) == (2, 28, 28, 512)
     assert fz[min(fz)].kind == "stem"
 
 
