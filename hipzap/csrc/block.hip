@@ -689,7 +689,10 @@ __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
 #pragma unroll
     for (int s = 0; s < kB2KS3; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = mfma16(wr[kB2KS1 + kB2KS2 + 4 * s + i], b3[s], acc[i]);
+      for (int i = 0; i < 4; ++i) {
+        acc[i] = mfma16(wr[kB2KS1 + kB2KS2 + 4 * s + i], b3[s], acc[i]);
+        consumed(kB2KS1 + kB2KS2 + 4 * s + i);
+      }
     HZ_BSTAMP(4);
     const int CO32 = kB2CO / 32;
 #pragma unroll
@@ -768,7 +771,7 @@ __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
     else if (i < OD) wr[i] = ldw(p.w3, 4 * wave + ((i - O3) & 3), kB2KS3, (i - O3) >> 2, lane);
     else wr[i] = ldw(p.wd, 4 * wave + ((i - OD) & 3), kB2dKSD, (i - OD) >> 2, lane);
   };
-  auto consumed = [&](int i) {
+  auto consumed = [&](int i) {  // (every fragment is consumed in order, so every one is fetched)
     if (i + kB2D < kB2dNW) fetch(i + kB2D);
   };
 #pragma unroll
@@ -853,7 +856,10 @@ __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
 #pragma unroll
     for (int s = 0; s < kB2dKSD; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = mfma16(wr[OD + 4 * s + i], bd[s], acc[i]);
+      for (int i = 0; i < 4; ++i) {
+        acc[i] = mfma16(wr[OD + 4 * s + i], bd[s], acc[i]);
+        consumed(OD + 4 * s + i);
+      }
     HZ_BSTAMP(4);
     const int CO32 = kB2CO / 32;
 #pragma unroll
