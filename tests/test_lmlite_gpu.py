@@ -58,12 +58,20 @@ def test_whh_quirk_and_untied_decoder(ckpt, tmp_path):
     raw_sd = dict(sd)
     for l in range(3):
         raw_sd.pop(f"0.rnns.{l}.module.weight_hh_l0")  # a loader that took _raw (zeros) would compute this
-    raw = LMBatchEngine(pack_lmb(raw_sd, "cuda:0"), "cuda:0", rows=16, unroll=4)
-    lite = LMLiteEngine(p, rows=16, unroll=4)
+    ref = LMBatchEngine(pack_lmb(sd, "cuda:0"), "cuda:0", rows=16, unroll=4, record_logits=True)
+    raw = LMBatchEngine(pack_lmb(raw_sd, "cuda:0"), "cuda:0", rows=16, unroll=4, record_logits=True)
+    lite = LMLiteEngine(p, rows=16, unroll=4, record_logits=True)
     try:
-        a, b = lite.run_tokens([0], 30, seed=3), raw.run_tokens([0], 30, seed=3)
-        assert a != b
+        # logits after a multi-token prompt (the recurrent term matters; sampled tokens of a
+        # random-init model are decided by the Gumbel noise, not by the nearly flat logits)
+        prompt = [5, 9, 11, 13]
+        la = torch.frombuffer(bytearray(lite.run_tokens(prompt, 1, seed=3, logits=True)[1]), dtype=torch.float32)
+        lr = raw.run_tokens(prompt, 1, seed=3, logits=True)[1]
+        lm = ref.run_tokens(prompt, 1, seed=3, logits=True)[1]
+        assert torch.equal(la, lm)  # the module weight, as the torch packer takes it
+        assert (la - lr).abs().max().item() > 1e-3 * la.abs().max().item()  # not the zeroed _raw decoy
     finally:
+        ref.close()
         raw.close()
         lite.close()
     # untied: a decoder weight in its own storage (different values) is packed separately
