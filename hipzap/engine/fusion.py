@@ -16,7 +16,8 @@ bind as ONE fused kernel instead:
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
-(comma list of ``stem``, ``bneck``; ``none`` disables; default both) -- the A/B switch of
+(comma list of ``stem``, ``convpool``, ``bneck``, ``bneck2``; ``none`` disables; default
+``convpool,bneck,bneck2``) -- the A/B switch of
 ``profiles/r4_fuse``. Reference: the per-conv contract these replace is SURVEY.md §2e N1/N2/N14.
 """
 from __future__ import annotations
@@ -31,6 +32,8 @@ from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK = 18, 19
 KINDS = ("stem", "convpool", "bneck", "bneck2")
+# measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box)
+DEFAULT = "convpool,bneck,bneck2"
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -56,7 +59,7 @@ class Fused:
 
 
 def enabled_kinds(spec: str | None = None) -> set:
-    v = os.environ.get("HIPZAP_FUSE", "convpool,bneck") if spec is None else spec
+    v = os.environ.get("HIPZAP_FUSE", DEFAULT) if spec is None else spec
     v = v.strip().lower()
     if v in ("", "0", "none", "off"):
         return set()
