@@ -23,3 +23,9 @@ db=$(find $O/lmb -name '*results.db' | head -1)
 python3 scripts/rocpd_stats.py "$db" 12 > $O/kernel_stats_lmb_c32.txt
 rm -rf $O/lmb
 cat $O/kernel_stats_lmb_c32.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/lmb1 -o run -- python3 scripts/bench_lm_batch.py --clients 1 --requests 8 > $O/lmb1.log 2>&1 || { tail -20 $O/lmb1.log; exit 1; }
+db=$(find $O/lmb1 -name '*results.db' | head -1)
+python3 scripts/rocpd_stats.py "$db" 12 > $O/kernel_stats_lmb_c1.txt
+python3 scripts/rocpd_stats.py "$db" --timeline lmb_admit lmb_dec_kernel > $O/lmb_c1_timeline.txt
+rm -rf $O/lmb1
+cat $O/kernel_stats_lmb_c1.txt; tail -12 $O/lmb_c1_timeline.txt
