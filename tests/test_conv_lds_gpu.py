@@ -4,6 +4,7 @@ fp32 PyTorch conv2d on bf16-rounded operands (MI355X only)."""
 import pytest
 import torch
 
+from hipzap import _native as N
 from hipzap.ops import conv as C
 
 from test_vision_gpu import _case
@@ -23,6 +24,8 @@ SHAPES = [
 
 @pytest.mark.parametrize("cfg", C.LDS_CONV_CFGS)
 def test_lds_conv_every_tile(cfg):
+    if cfg in C.M32_CFGS and not N.experiments():
+        pytest.skip("M32 tiles are a measured negative, built only with --experiments")
     for n, cin, h, cout, k, stride, pad, res in SHAPES:
         if not C.lds_conv_fits(cfg, cout):
             continue

@@ -5,6 +5,7 @@ import torch
 from hipzap.engine.engine import Engine
 from hipzap.engine.reference import run_graph_reference
 from hipzap.models import bert, registry, vit
+from hipzap import _native as NN
 from hipzap.ops import conv as C
 from hipzap.ops import transformer as T
 
@@ -62,6 +63,8 @@ def test_linear_gemm(M, N, K, act):
                                             (64, 132, 64, "none", False)])
 def test_lds_gemm(cfg, M, N, K, act, res):
     """LDS-tiled GEMM (csrc/gemm.hip) vs fp32: ragged M and N tails, all tiles."""
+    if cfg in C.M32_CFGS and not NN.experiments():
+        pytest.skip("M32 tiles are a measured negative, built only with --experiments")
     g = torch.Generator().manual_seed(3)
     w = torch.randn(N, K, generator=g) * 0.03
     b = torch.randn(N, generator=g)
