@@ -96,13 +96,22 @@ def lifetimes(g: Graph) -> dict[int, list[int]]:
     return life
 
 
-def plan_memory(g: Graph, reuse: bool | None = None) -> tuple[dict[int, int], int]:
+def plan_memory(g: Graph, reuse: bool | None = None, groups=()) -> tuple[dict[int, int], int]:
     """Return ({tensor id: arena byte offset}, arena bytes). ``reuse=False`` (or env
     ``HIPZAP_ARENA_NOREUSE=1``) gives every tensor its own slot, so every intermediate stays
-    readable after a run (per-node debugging, ``scripts/debug_nodes.py``)."""
+    readable after a run (per-node debugging, ``scripts/debug_nodes.py``).
+    ``groups``: (first, end) node ranges that run as ONE launch (engine/fusion.py): every tensor
+    the range reads or writes is live over the whole range, so a fused kernel's output never
+    shares memory with an input its other workgroups still read (a halo) -- the per-node
+    lifetimes would let the block output reuse the block input of a downsample block."""
     if reuse is None:
         reuse = os.environ.get("HIPZAP_ARENA_NOREUSE", "0") != "1"
     life = lifetimes(g)
+    for first, end in groups:
+        for n in g.nodes[first:end]:
+            for t in list(n.inputs) + list(n.outputs):
+                if t is not None and t in life:
+                    life[t] = [min(life[t][0], first), max(life[t][1], end - 1)]
     if not reuse:
         life = {t: [0, len(g.nodes)] for t in life}
     order = sorted(life.keys(), key=lambda t: -g.tensors[t].nbytes)

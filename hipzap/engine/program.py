@@ -63,7 +63,13 @@ class ExecContext:
         self._nslab: dict[int, int] = {}  # stats tensor -> slabs written by its producer (HzLnFold)
         lib = lib if lib is not None else N.lib()
         self._lib = lib
-        offsets, arena_bytes = plan_memory(g)
+        # fused ResNet stages (engine/fusion.py, csrc/block.hip): runs of nodes bound as ONE launch;
+        # the arena plan keeps each run's tensors live over the whole run
+        chain = self._chain_range(os.environ.get("HIPZAP_CONV_CHAIN", ""))
+        self.fused = fusion.plan(g, params, fusion.enabled_kinds(fuse) if fuse is not None else None)
+        if chain is not None:
+            self.fused = {k: f for k, f in self.fused.items() if f.end <= chain[0]}
+        offsets, arena_bytes = plan_memory(g, groups=[(f.start, f.end) for f in self.fused.values()])
         self.arena_bytes = arena_bytes
         self.arena = torch.empty(max(arena_bytes, 256), dtype=torch.uint8, device=self.device)
         base = self.arena.data_ptr()
@@ -141,12 +147,7 @@ class ExecContext:
         if pair_convs is None:
             pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
         self.pairs = conv_pairs(g) if pair_convs else {}
-        chain = self._chain_range(os.environ.get("HIPZAP_CONV_CHAIN", ""))
         self.chain_sync = None
-        # fused ResNet stages (engine/fusion.py, csrc/block.hip): runs of nodes bound as ONE launch
-        self.fused = fusion.plan(g, params, fusion.enabled_kinds(fuse) if fuse is not None else None)
-        if chain is not None:
-            self.fused = {k: f for k, f in self.fused.items() if f.end <= chain[0]}
         i = 0
         while i < len(g.nodes):
             n = g.nodes[i]

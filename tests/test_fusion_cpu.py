@@ -60,3 +60,32 @@ def test_unknown_kinds_are_ignored_and_resnet18_has_no_bottleneck():
     params, kw = a.pack(randomize_bn(a.make_model()).eval().state_dict(), "cpu")
     g, fz = _plan(a, params, kw, "all", batch=1, input_uint8=True)
     assert [f.kind for f in fz.values()] == ["stem"]
+
+
+def test_arena_never_aliases_a_fused_runs_tensors(r50):
+    """A fused kernel reads its input's halo from other workgroups' tiles while it writes its
+    output: the arena plan must keep the run's input and output apart (per-node lifetimes let the
+    output of a downsample block reuse the block input, whose last reader is the run's 2nd node)."""
+    from hipzap.engine.graph import plan_memory
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, "all", batch=1, input_uint8=True)
+    offsets, _ = plan_memory(g, groups=[(f.start, f.end) for f in fz.values()])
+    naive, _ = plan_memory(g)
+
+    def overlap(off, t, u):
+        a0, a1 = off[t], off[t] + g.tensors[t].nbytes
+        b0, b1 = off[u], off[u] + g.tensors[u].nbytes
+        return a0 < b1 and b0 < a1
+
+    hit_naive = False
+    for f in fz.values():
+        ins = {t for n in f.nodes for t in n.inputs if t in offsets}
+        outs = {t for n in f.nodes for t in n.outputs if t in offsets}
+        ext_in = ins - outs
+        last = f.nodes[-1].outputs[0]
+        if last not in offsets:
+            continue
+        for t in ext_in:
+            assert not overlap(offsets, t, last), (f.kind, g.tensors[t].name)
+            hit_naive |= overlap(naive, t, last)
+    assert hit_naive  # the hazard is real without the groups
