@@ -228,7 +228,7 @@ def _load():
     _sig(lib, "hz_lmb_dec_launch", c_int, C.POINTER(LmbDecParams), P)
     _sig(lib, "hz_lmb_admit_launch", c_int, C.POINTER(LmbAdmitParams), P)
     _sig(lib, "hz_lmb_dec_blocks", c_int, c_int)
-    _sig(lib, "hz_lmb_create", P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int)
+    _sig(lib, "hz_lmb_create", P, P, c_int, P, P, c_int, c_int, c_int, c_int, P, P, c_int)
     _sig(lib, "hz_lmb_submit", c_int, P, P, c_int, c_int, C.c_uint64, P, P, C.POINTER(D))
     _sig(lib, "hz_lmb_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_lmb_set_lowload", c_int, P, P, c_int)

@@ -268,14 +268,15 @@ int hz_lmb_layer_launch(const HzLmbLayerParams* p, hipStream_t st);
 int hz_lmb_dec_launch(const HzLmbDecParams* p, hipStream_t st);
 int hz_lmb_admit_launch(const HzLmbAdmitParams* p, hipStream_t st);
 int hz_lmb_dec_blocks(int V);  // decoder workgroups (256 vocabulary rows each)
-// scheduler: one worker thread replays the captured U-step program; requests join free rows
-// at replay boundaries and leave when their last token is out (csrc/lmserve.cpp)
-void* hz_lmb_create(HzProgram prog, hipStream_t st, int* host_block, int Bp, int U, int maxp, int maxn,
-                    int* out_pool, float* logits, int V);
+// scheduler: one worker thread replays the captured U-step program(s); requests join free rows
+// at replay boundaries and leave when their last token is out (csrc/lmserve.cpp). Two programs
+// (each reading its own host block and recording into its own logits buffer): pipelined replays.
+void* hz_lmb_create(const HzProgram* progs, int nprog, hipStream_t st, int* const* blocks, int Bp, int U, int maxp,
+                    int maxn, int* out_pool, float* const* logits, int V);
 int hz_lmb_submit(void* s, const int* prompt, int P, int n, unsigned long long seed, int* out, float* logits_out,
                   double* lat_us);
 void hz_lmb_stats(void* s, unsigned long long* out4);  // replays, served, row-steps used, row-steps total
-int hz_lmb_set_lowload(void* s, HzProgram lo, int rows);  // program for replays whose busy rows are < rows
+int hz_lmb_set_lowload(void* s, const HzProgram* lo, int rows);  // programs for replays whose busy rows are < rows
 unsigned long long hz_lmb_lo_replays(void* s);
 void hz_lmb_destroy(void* s);
 

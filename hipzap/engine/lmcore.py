@@ -152,7 +152,7 @@ class LmbCore:
 
     def __init__(self, geo: LmbGeometry, w: dict, alloc, stream: int, rows: int = 32, unroll: int = 8,
                  exclude_ids=(), max_words: int = 1024, record_logits: bool = False, capture: bool = True,
-                 lowload: bool | None = None, lib=None):
+                 lowload: bool | None = None, pipeline: bool | None = None, lib=None):
         if rows not in (16, 32):
             raise ValueError("rows must be 16 or 32")
         if not 1 <= unroll <= 32:
@@ -172,13 +172,18 @@ class LmbCore:
         self.nblk = lib.hz_lmb_dec_blocks(geo.V)
         self.dbest = alloc.device(2 * Bp * 8)
         self.tok = alloc.device(Bp * 4)
-        self.block = alloc.pinned((8 + Bp * (8 + 4 * U)) * 4)
-        self.out_pool = alloc.pinned(Bp * max_words * 4)
-        self.logits = alloc.pinned(Bp * geo.V * 4) if record_logits else 0
+        if pipeline is None:
+            pipeline = os.environ.get("HIPZAP_LM_PIPELINE", "1") != "0"
+        self.nprog = 2 if pipeline else 1  # pipelined replays: one host block / logits buffer per program
+        self.blocks = [alloc.pinned((8 + Bp * (8 + 4 * U)) * 4) for _ in range(self.nprog)]
+        self.block = self.blocks[0]
+        self.out_pool = alloc.pinned(2 * Bp * max_words * 4)  # two output slots per row
+        self.logits_bufs = [alloc.pinned(Bp * geo.V * 4) for _ in range(self.nprog)] if record_logits else []
+        self.logits = self.logits_bufs[0] if record_logits else 0
         ex = [int(e) for e in exclude_ids][:8]
 
         a = N.LmbAdmitParams()
-        a.block, a.ctl, a.seed, a.outp, a.gpar = self.block, self.ctl, self.seed, self.outp, self.gpar
+        a.block, a.ctl, a.seed, a.outp, a.gpar = self.blocks[0], self.ctl, self.seed, self.outp, self.gpar
         a.Bp, a.U, a.n_layers = Bp, U, len(L)
         for i, ly in enumerate(L):
             a.h[i], a.c[i], a.Kh[i], a.H[i] = self.h[i], self.c[i], ly.Kh, ly.H
@@ -204,13 +209,17 @@ class LmbCore:
             d.exclude[i] = e
         self._ops = [(N.HZ_K_LMB_LAYER, q) for q in layer_prms] + [(N.HZ_K_LMB_DEC, d)]
 
-        def build(nb_act: int):
+        def build(nb_act: int, k: int):
             prog = lib.hz_prog_create()
-            N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(a), C.sizeof(a), 0), "add lmb admit")
+            ak = N.LmbAdmitParams.from_buffer_copy(a)
+            ak.block = self.blocks[k]
+            N.check(lib.hz_prog_add_kernel(prog, N.HZ_K_LMB_ADMIT, C.byref(ak), C.sizeof(ak), 0), "add lmb admit")
             for u in range(U):
                 for kind, prm in self._ops:
                     q = type(prm).from_buffer_copy(prm)
                     q.step_off, q.nb_act = u, nb_act
+                    if kind == N.HZ_K_LMB_DEC and self.logits_bufs:
+                        q.logits = self.logits_bufs[k]
                     N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
             if capture:
                 N.check(lib.hz_prog_capture(prog, stream), "capture lmb")
@@ -218,16 +227,21 @@ class LmbCore:
 
         self._admit = a
         self.stream = stream
-        self.prog = build(0)
-        # low load (HIPZAP_LM_LOWLOAD, default on at 32 rows): a second program over the first 16
-        # rows, replayed while every busy row is below 16 (csrc/lmserve.cpp)
-        self.prog_lo = build(1) if lowload and Bp > 16 else None
-        self._sched = lib.hz_lmb_create(self.prog, stream, self.block, Bp, U, 0, max_words, self.out_pool, d.logits,
-                                        geo.V)
+        self.progs = [build(0, k) for k in range(self.nprog)]
+        self.prog = self.progs[0]
+        # low load (HIPZAP_LM_LOWLOAD, default on at 32 rows): programs over the first 16 rows,
+        # replayed while every busy row is below 16 (csrc/lmserve.cpp)
+        self.progs_lo = [build(1, k) for k in range(self.nprog)] if lowload and Bp > 16 else []
+        P2 = C.c_void_p * 2
+        lg = P2(*(self.logits_bufs + [0] * (2 - len(self.logits_bufs)))) if self.logits_bufs else None
+        self._sched = lib.hz_lmb_create(P2(*(self.progs + [0] * (2 - self.nprog))), self.nprog, stream,
+                                        P2(*(self.blocks + [0] * (2 - self.nprog))), Bp, U, 0, max_words,
+                                        self.out_pool, lg, geo.V)
         if not self._sched:
             raise RuntimeError("hz_lmb_create failed")
-        if self.prog_lo:
-            N.check(lib.hz_lmb_set_lowload(self._sched, self.prog_lo, 16), "hz_lmb_set_lowload")
+        if self.progs_lo:
+            N.check(lib.hz_lmb_set_lowload(self._sched, P2(*(self.progs_lo + [0] * (2 - self.nprog))), 16),
+                    "hz_lmb_set_lowload")
         self.last_latency_ms = None
 
     def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
@@ -262,9 +276,9 @@ class LmbCore:
         s, self._sched = getattr(self, "_sched", None), None
         if s:
             self.lib.hz_lmb_destroy(s)
-        for attr in ("prog", "prog_lo"):
-            prog = getattr(self, attr, None)
-            setattr(self, attr, None)
+        progs = list(getattr(self, "progs", []) or []) + list(getattr(self, "progs_lo", []) or [])
+        self.progs, self.progs_lo, self.prog = [], [], None
+        for prog in progs:
             if prog:
                 self.lib.hz_prog_destroy(prog)
 

@@ -75,3 +75,26 @@ def test_executor_host_sanitizers(tmp_path, sanitizer):
     assert run.returncode == 0 and "executor host sanitize: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
     for marker in ("ERROR: AddressSanitizer", "runtime error", "WARNING: ThreadSanitizer"):
         assert marker not in run.stderr, run.stderr[-4000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("sanitizer", ["address,undefined", "thread"])
+def test_lmserve_host_sanitizers(tmp_path, sanitizer):
+    """The batched-decode scheduler (csrc/lmserve.cpp): pipelined program pair, alternating output
+    slots, low-load switch, logits recording, under host ASan+UBSan and ThreadSanitizer against an
+    in-order fake device that reads each host block only when its replay runs."""
+    exe = tmp_path / f"lmserve_{sanitizer.split(',')[0]}"
+    san = []
+    for f in (f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"):
+        san += ["-Xarch_host", f]
+    cmd = [HIPCC, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", os.path.join(ROOT, "hipzap", "csrc"),
+           os.path.join(ROOT, "hipzap", "csrc", "lmserve.cpp"),
+           os.path.join(ROOT, "tests", "native", "lmserve_host_sanitize.cpp"), "-lpthread", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert run.returncode == 0 and "lmserve host sanitize: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-4000:])
+    for marker in ("ERROR: AddressSanitizer", "runtime error", "WARNING: ThreadSanitizer"):
+        assert marker not in run.stderr, run.stderr[-4000:]
