@@ -1,0 +1,21 @@
+#!/bin/bash
+# r4: (1) 2-rank torchrun rehearsal of the multi-GPU bench path (gloo, both ranks on cuda:0);
+# (2) PMC pass over the batched LM decode at 32 rows: L2 hits / misses and memory-side read
+# requests per kernel (is the 182 MB weight set served on-die?), plus the counter list.
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/r4_s10; mkdir -p $O
+rocprofv3 -L > $O/counters_avail.txt 2>&1 || true
+grep -i -E "mall|_EA0_|TCC_EA|infinity" $O/counters_avail.txt | head -40 > $O/counters_mall.txt || true
+P1="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"
+timeout -s KILL 120 rocprofv3 --pmc $P1 -d $O/P1 -o run --output-format csv -- python3 scripts/bench_lm_batch.py --clients 32 --requests 2 > $O/P1.log 2>&1
+rc=$?; echo "pmc P1 rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/P1.log; exit $rc; }
+python3 scripts/pmc_summary.py $O/P1 $O/P1.json > /dev/null && rm -rf $O/P1
+python3 -c "
+import json; d=json.load(open('$O/P1.json'))['P1']['per_kernel']
+for k,v in d.items():
+    if 'lmb' in k: print(k[:80], v)
+"
+HIPZAP_DIST_BACKEND=gloo HIPZAP_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 100 --warmup 10 > $O/rehearse_dp2.log 2>&1 || { tail -30 $O/rehearse_dp2.log; exit 1; }
+grep '^{' $O/rehearse_dp2.log > $O/rehearse_dp2.json && tail -c 1200 $O/rehearse_dp2.json
