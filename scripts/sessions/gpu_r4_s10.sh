@@ -6,6 +6,8 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r4_s10; mkdir -p $O
+timeout -k 10 240 python3 scripts/diag_stream_init.py --trials 5 > $O/stream_init.jsonl 2>&1 || { tail -5 $O/stream_init.jsonl; exit 1; }
+tail -1 $O/stream_init.jsonl
 rocprofv3 -L > $O/counters_avail.txt 2>&1 || true
 grep -i -E "mall|_EA0_|TCC_EA|infinity" $O/counters_avail.txt | head -40 > $O/counters_mall.txt || true
 P1="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"
