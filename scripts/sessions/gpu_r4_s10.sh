@@ -21,3 +21,13 @@ for k,v in d.items():
 "
 HIPZAP_DIST_BACKEND=gloo HIPZAP_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 100 --warmup 10 > $O/rehearse_dp2.log 2>&1 || { tail -30 $O/rehearse_dp2.log; exit 1; }
 grep '^{' $O/rehearse_dp2.log > $O/rehearse_dp2.json && tail -c 1200 $O/rehearse_dp2.json
+# (3) request input through the SDMA engines instead of a zero-copy PCIe read inside the
+# preprocess kernel (which holds a compute-queue slot for the whole transfer): same-box A/B
+B="--steps 300 --warmup 30 --cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
+for rep in 1 2; do
+  for v in all:0 out:0 out:1 all:1; do
+    zc=${v%%:*}; sd=${v##*:}
+    HSA_ENABLE_SDMA=$sd HIPZAP_KEEP_SDMA=$sd HIPZAP_ZERO_COPY=$zc timeout -k 10 200 python bench.py $B > $O/bench_${zc}_sdma${sd}_$rep.json 2> $O/bench_err.log || { tail -20 $O/bench_err.log; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/bench_${zc}_sdma${sd}_$rep.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['served_sustained']['inf_s'], d['latency_ms_p50_single'])"
+  done
+done
