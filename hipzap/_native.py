@@ -85,7 +85,12 @@ class LmbLayerParams(C.Structure):
     _fields_ = [("w", c_void_p), ("bias", c_void_p), ("h", c_void_p), ("x", c_void_p), ("c", c_void_p),
                 ("gpar", c_void_p), ("ctl", c_void_p), ("H", c_int), ("Kh", c_int), ("Kx", c_int), ("R", c_int),
                 ("Bp", c_int), ("step_off", c_int), ("emb", c_void_p), ("dbest", c_void_p), ("V", c_int),
-                ("nb_act", c_int), ("outp", c_void_p), ("tok", c_void_p)]
+                ("nb_act", c_int), ("outp", c_void_p), ("tok", c_void_p), ("embproj", c_void_p)]
+
+
+class LmbEmbProjParams(C.Structure):
+    _fields_ = [("w", c_void_p), ("emb", c_void_p), ("out", c_void_p), ("R", c_int), ("Kh", c_int), ("Kx", c_int),
+                ("Vp", c_int)]
 
 
 class LmbDecParams(C.Structure):
@@ -232,6 +237,7 @@ def _load():
     _sig(lib, "hz_lmb_submit", c_int, P, P, c_int, c_int, C.c_uint64, P, P, C.POINTER(D))
     _sig(lib, "hz_lmb_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_lmb_set_lowload", c_int, P, P, c_int)
+    _sig(lib, "hz_lmb_embproj_launch", c_int, P, P)
     _sig(lib, "hz_lmb_lo_replays", U64, P)
     _sig(lib, "hz_lmb_destroy", None, P)
     if DEBUG:

@@ -239,7 +239,14 @@ typedef struct HzLmbLayerParams {
                               //   low-load program: every busy row is below 16)
   int* const* outp;           // [Bp] request output arrays (pinned host, written by workgroup 0)
   int* tok;                   // [Bp] this step's tokens (device, diagnostics)
+  const float* embproj;       // first layer: [Vp][R] fp32 W_ih E[v] (hz_lmb_embproj_launch) or NULL
 } HzLmbLayerParams;
+typedef struct HzLmbEmbProjParams {  // P[v][r] = sum_k W[r][Kh + k] emb[v][k]
+  const unsigned short* w;    // the first layer's packed weights [R/16][(Kh+Kx)/32][64][8]
+  const unsigned short* emb;  // [Vp/16][Kx/32][64][8]
+  float* out;                 // [Vp][R]
+  int R, Kh, Kx, Vp;
+} HzLmbEmbProjParams;
 typedef struct HzLmbDecParams {
   const unsigned short* w;    // [Vp/16][K/32][64][8] bf16 (tied embedding when untied weights are absent)
   const float* bias;          // [Vp] or NULL
@@ -267,6 +274,7 @@ typedef struct HzLmbAdmitParams {
 int hz_lmb_layer_launch(const HzLmbLayerParams* p, hipStream_t st);
 int hz_lmb_dec_launch(const HzLmbDecParams* p, hipStream_t st);
 int hz_lmb_admit_launch(const HzLmbAdmitParams* p, hipStream_t st);
+int hz_lmb_embproj_launch(const HzLmbEmbProjParams* p, hipStream_t st);
 int hz_lmb_dec_blocks(int V);  // decoder workgroups (256 vocabulary rows each)
 // scheduler: one worker thread replays the captured U-step program(s); requests join free rows
 // at replay boundaries and leave when their last token is out (csrc/lmserve.cpp). Two programs

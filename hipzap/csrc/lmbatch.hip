@@ -66,9 +66,13 @@ __device__ __forceinline__ int st_off(int j, int r, int NB) {
 // per tile): the layer is bound by what each CU fetches, not by HBM. NBW = 1 (Bp 32): twin
 // workgroups b and b + 8 (one XCD under round-robin placement: the twin's weight read hits L2)
 // take one row block each, so a CU fetches TPW * 32 + 64 B per k instead of TPW * 32 + 128.
-template <int NB, bool FIRST, int TPW, int NBW>
+// EP (first layer, p.embproj): the embedding half of the layer's K is precomputed per vocabulary
+// id (lmb_embproj_kernel: P[v] = W_ih E[v], fp32), so the workgroup multiplies W_hh h only and the
+// cell update adds P[token] -- half the weight bytes on the step's critical path.
+template <int NB, bool FIRST, int TPW, int NBW, bool EP = false>
 __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p) {
   static_assert(NBW == NB || NBW == 1, "row blocks per workgroup");
+  static_assert(!EP || FIRST, "the projected embedding is the first layer's input");
   __shared__ f32x4 part[LW][TPW][NBW][64];
   __shared__ int s_tok[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -83,15 +87,17 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   if (tile0 >= ntile || cb0 >= nba) return;      // (grid padding of the twin mapping; low-load program)
   const int nbw = min(NBW, nba - cb0);           // row blocks this workgroup computes
-  const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;
-  const int spw = (KS + LW - 1) / LW;
+  const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;  // KS: the packed row stride
+  const int KSE = EP ? KSH : KS;                                  // k-steps multiplied here
+  const int spw = (KSE + LW - 1) / LW;
   const int k0 = wave * spw;
-  const int cnt = max(0, min(spw, KS - k0));
+  const int cnt = max(0, min(spw, KSE - k0));
   const int Bp = NB * 16;
   if (!HZ_DCHECK(spw <= SPW && p.Bp == Bp && p.R % 16 == 0 && nba <= NB)) return;
   // ---- loads that need nothing: this sub-step's control + the decoder maxima (FIRST), then the
   // weight stream; vmcnt retires in issue order, so what the token selection waits for goes first
   HzLmbCtl cl = {};
+  f32x4 pe = f32x4{0.f, 0.f, 0.f, 0.f};  // EP: this thread's unit's projected embedding (4 gates)
   unsigned long long best0 = 0, best1 = 0;  // both parities: no wait on the step parity before the weight stream
   if constexpr (FIRST) {
     if (tid < Bp) {
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   for (int tt = 0; tt < TPW; ++tt) {
     const bf16_t* wt = p.w + (size_t)min(tile0 + tt, ntile - 1) * KS * 512 + lane * 8;
 #pragma unroll
-    for (int s = 0; s < SPW; ++s) wf[tt][s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KS - 1) * 512);
+    for (int s = 0; s < SPW; ++s) wf[tt][s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KSE - 1) * 512);
   }
   __builtin_amdgcn_sched_barrier(0);
   const int par = (*p.gpar + p.step_off) & 1;
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   u32x4 ah[SPW][NBW], al[SPW][NBW];
 #pragma unroll
   for (int s = 0; s < SPW; ++s) {
-    const int ks = min(k0 + s, KS - 1);
+    const int ks = min(k0 + s, KSE - 1);
     // FIRST: k-steps past Kh are the embedding, loaded after the token selection (a harmless
     // in-range h fragment here keeps the loop branch-free)
     const bool hk = FIRST || ks < KSH;
@@ -148,9 +154,16 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       }
     }
     lds_barrier();  // LDS only: the weight and state loads stay in flight
-    // embedding fragments of the chosen tokens: lane l holds emb[tok(row l&15)][k 8(l>>4)..+7]
+    if constexpr (EP) {
+      // the cell-update threads fetch their rows' projected embedding now (consumed after the MFMAs)
+      if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw) {
+        const int tt = tid / (NBW * 64), cb = (tid >> 6) % NBW, l = tid & 63;
+        const int j = min((tile0 + tt) * 4 + (l >> 4), p.R / 4 - 1);
+        pe = *reinterpret_cast<const f32x4*>(p.embproj + (size_t)s_tok[(cb0 + cb) * 16 + (l & 15)] * p.R + 4 * j);
+      }
+    }
 #pragma unroll
-    for (int s = 0; s < SPW; ++s) {
+    for (int s = 0; s < SPW && !EP; ++s) {
       const int ks = min(k0 + s, KS - 1);
       if (ks >= KSH) {  // wave-uniform
 #pragma unroll
@@ -201,6 +214,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     if (tile0 + tt < ntile && j < p.H) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + 4 * j);
       g += b;
+      if constexpr (EP) g += pe;
       const float si = 1.f / (1.f + __expf(-g[0]));
       const float sf = 1.f / (1.f + __expf(-g[1]));
       const float so = 1.f / (1.f + __expf(-g[3]));
@@ -214,6 +228,48 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       dst[0] = __builtin_bit_cast(bf16_t, hi);
       dst[(size_t)KSH * NB * 512] = __builtin_bit_cast(bf16_t, lo);
     }
+  }
+}
+
+// ------------------------------------------------------------------------ projected embedding
+// P[v][r] = sum_k W0[r][Kh + k] E[v][k] (fp32, [Vp][R]): the first layer's input half for every
+// vocabulary id, once per engine build. Workgroup = 8 vocabulary tiles (one per wave, its 16 ids'
+// embedding fragments held in registers); the W_ih fragments of each 16-row gate tile are staged
+// once per workgroup in LDS (double-buffered, global_load_lds) and shared by the 8 waves.
+constexpr int EPKS = 32;  // Kx / 32 <= 32 (K <= 1024, the batched engine's embedding limit)
+
+__global__ __launch_bounds__(512) void lmb_embproj_kernel(const HzLmbEmbProjParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t A[2][EPKS * 512];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int KSX = p.Kx >> 5, KS = (p.Kh + p.Kx) >> 5, KSH = p.Kh >> 5;
+  const int nvt = p.Vp >> 4, ngt = p.R >> 4;
+  const int vt = blockIdx.x * 8 + wave;
+  if (!HZ_DCHECK(KSX <= EPKS && KSX >= 1)) return;
+  const bool live = vt < nvt;  // (waves past the vocabulary keep the barriers)
+  bf16x8 b[EPKS];
+#pragma unroll
+  for (int s = 0; s < EPKS; ++s)
+    if (s < KSX) b[s] = as_frag(*reinterpret_cast<const u32x4*>(p.emb + ((size_t)min(vt, nvt - 1) * KSX + s) * 512 + lane * 8));
+  // stage gate tile g's KSX fragments: fragment s = 1 KiB, wave w takes s = w, w + 8, ...
+  auto stage = [&](int buf, int g) {
+    const bf16_t* src = p.w + ((size_t)g * KS + KSH) * 512 + lane * 8;
+    for (int s = wave; s < KSX; s += 8)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (size_t)s * 512),
+                                       (lds_void*)(&A[buf][s * 512]), 16, 0, 0);
+  };
+  stage(0, 0);
+  for (int g = 0; g < ngt; ++g) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile g staged by every wave; buffer (g + 1) & 1 free (tile g - 1 read)
+    if (g + 1 < ngt) stage((g + 1) & 1, g + 1);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* a = &A[g & 1][lane * 8];
+#pragma unroll
+    for (int s = 0; s < EPKS; ++s)
+      if (s < KSX) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(*reinterpret_cast<const u32x4*>(a + s * 512)), b[s], acc, 0, 0, 0);
+    // lane l: gate rows 16g + 4(l>>4) .. +3 of vocabulary id 16vt + (l&15)
+    if (live)
+      *reinterpret_cast<f32x4*>(p.out + (size_t)(vt * 16 + (lane & 15)) * p.R + g * 16 + 4 * (lane >> 4)) = acc;
   }
 }
 
@@ -436,12 +492,13 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
     return 3;
   }();
   const int ntile = p.R / 16;
-#define HZ_LMBL(NB, T, NBW)                                                                    \
-  do {                                                                                         \
-    const int groups = (ntile + T - 1) / T;                                                    \
-    const dim3 grid(NBW == NB ? groups : 2 * ((groups + 7) / 8 * 8)), block(512);              \
-    if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW>), grid, block, 0, st, p); \
-    else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T, NBW>), grid, block, 0, st, p);     \
+#define HZ_LMBL(NB, T, NBW)                                                                          \
+  do {                                                                                               \
+    const int groups = (ntile + T - 1) / T;                                                          \
+    const dim3 grid(NBW == NB ? groups : 2 * ((groups + 7) / 8 * 8)), block(512);                    \
+    if (first && p.embproj) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW, true>), grid, block, 0, st, p); \
+    else if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW>), grid, block, 0, st, p); \
+    else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T, NBW>), grid, block, 0, st, p);           \
   } while (0)
   if (p.Bp == 16) {
     if (shape == 1) HZ_LMBL(1, 1, 1);
@@ -498,6 +555,15 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   }
 #undef HZ_LMBD_K
 #undef HZ_LMBD
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_lmb_embproj_launch(const HzLmbEmbProjParams* pp, hipStream_t st) {
+  const HzLmbEmbProjParams& p = *pp;
+  if (!p.w || !p.emb || !p.out || p.Kh % 32 || p.Kx % 32 || p.Kx < 32 || p.Kx > EPKS * 32 || p.R % 16 || p.Vp % 16 ||
+      p.Vp < 16)
+    return -1;
+  hipLaunchKernelGGL(lmb_embproj_kernel, dim3((p.Vp / 16 + 7) / 8), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 

@@ -152,7 +152,8 @@ class LmbCore:
 
     def __init__(self, geo: LmbGeometry, w: dict, alloc, stream: int, rows: int = 32, unroll: int = 8,
                  exclude_ids=(), max_words: int = 1024, record_logits: bool = False, capture: bool = True,
-                 lowload: bool | None = None, pipeline: bool | None = None, lib=None):
+                 lowload: bool | None = None, pipeline: bool | None = None, embproj: bool | None = None,
+                 lib=None):
         if rows not in (16, 32):
             raise ValueError("rows must be 16 or 32")
         if not 1 <= unroll <= 32:
@@ -187,6 +188,17 @@ class LmbCore:
         a.Bp, a.U, a.n_layers = Bp, U, len(L)
         for i, ly in enumerate(L):
             a.h[i], a.c[i], a.Kh[i], a.H[i] = self.h[i], self.c[i], ly.Kh, ly.H
+        # the first layer's embedding half, precomputed per vocabulary id (HIPZAP_LM_EMBPROJ, default
+        # on): P[v] = W_ih0 E[v] in fp32, so a step multiplies only W_hh0 h0 in the first layer
+        if embproj is None:
+            embproj = os.environ.get("HIPZAP_LM_EMBPROJ", "1") != "0"
+        self.embproj = 0
+        if embproj:
+            self.embproj = alloc.device(geo.Vp * L[0].R * 4)
+            ep = N.LmbEmbProjParams()
+            ep.w, ep.emb, ep.out = w["layers"][0][0], w["emb"], self.embproj
+            ep.R, ep.Kh, ep.Kx, ep.Vp = L[0].R, L[0].Kh, L[0].Kx, geo.Vp
+            N.check(lib.hz_lmb_embproj_launch(C.byref(ep), stream), "hz_lmb_embproj_launch")
         layer_prms = []
         for i, ly in enumerate(L):
             q = N.LmbLayerParams()
@@ -198,6 +210,7 @@ class LmbCore:
             if i == 0:
                 q.emb, q.dbest, q.V = w["emb"], self.dbest, geo.V
                 q.outp, q.tok = self.outp, self.tok
+                q.embproj = self.embproj
             layer_prms.append(q)
         d = N.LmbDecParams()
         d.w, d.bias, d.h = w["dec"], w["dec_bias"], self.h[-1]

@@ -6,6 +6,15 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r4_s10; mkdir -p $O
+# (0) the projected-embedding first layer: LM tests, then the decode bench with / without it
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lmbatch_gpu.py tests/test_lmlite_gpu.py > $O/pytest_lm.log 2>&1 || { tail -30 $O/pytest_lm.log; exit 1; }
+tail -1 $O/pytest_lm.log
+for rep in 1 2; do
+for ep in 1 0; do
+  HIPZAP_LM_EMBPROJ=$ep timeout -k 10 200 python scripts/bench_lm_batch.py --clients 1 32 64 --requests 12 > $O/lm_ep${ep}_$rep.json 2> $O/lm_err.log || { tail -20 $O/lm_err.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('$O/lm_ep${ep}_$rep.json').read().strip().splitlines()[-1]); print('embproj=$ep', d.get('build_ms'), [(l['clients'], l['us_per_step'], l['p50_ms'], l['req_per_s']) for l in d['load']])"
+done
+done
 timeout -k 10 240 python3 scripts/diag_stream_init.py --trials 5 > $O/stream_init.jsonl 2>&1 || { tail -5 $O/stream_init.jsonl; exit 1; }
 tail -1 $O/stream_init.jsonl
 rocprofv3 -L > $O/counters_avail.txt 2>&1 || true

@@ -132,6 +132,26 @@ def test_lowload_program_is_bitwise_the_full_one(model):
         low.close()
 
 
+def test_projected_embedding_matches_the_fused_first_layer(model):
+    """HIPZAP_LM_EMBPROJ: the first layer's embedding half precomputed per vocabulary id (fp32
+    W_ih E[v], lmb_embproj_kernel) gives the logits of the engine that multiplies it every step,
+    up to fp32 summation order."""
+    pk = pack_lmb(model.state_dict(), DEV)
+    a = LMBatchEngine(pk, DEV, rows=32, unroll=8, record_logits=True, embproj=False)
+    b = LMBatchEngine(pk, DEV, rows=32, unroll=8, record_logits=True, embproj=True)
+    try:
+        assert b.core.embproj and not a.core.embproj
+        for ids in ([5], [5, 17, 200, 3, 2999], [9, 8, 7, 6, 5, 4, 3, 2, 1, 11, 12]):
+            _, la = a.run_tokens(ids, 1, seed=1, logits=True)
+            _, lb = b.run_tokens(ids, 1, seed=1, logits=True)
+            assert (la - lb).abs().max().item() / la.abs().max().item() < 2e-3
+        agree = sum(a.run_tokens([4, 7], 10, seed=s) == b.run_tokens([4, 7], 10, seed=s) for s in range(10))
+        assert agree >= 9, agree
+    finally:
+        a.close()
+        b.close()
+
+
 def test_tokens_track_the_single_request_engine(model):
     """Same seed, same rule, same noise: the batched engine's tokens agree with the single-request
     engine's (fp32 state) except where two keys are closer than the small state rounding."""
