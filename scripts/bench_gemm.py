@@ -41,10 +41,15 @@ def time_torch(x, w, reps=20):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default=None, help="M,N,K;M,N,K;... (default: the BERT / ViT projections)")
+    a = ap.parse_args()
+    shapes = [tuple(int(v) for v in t.split(",")) for t in a.shapes.split(";")] if a.shapes else SHAPES
     dev = torch.device("cuda:0")
     lib = N.lib()
     gen = torch.Generator(device=dev).manual_seed(0)
-    for M, Nn, K in SHAPES:
+    for M, Nn, K in shapes:
         w = (torch.rand(Nn, K, device=dev, generator=gen) - 0.5).to(torch.bfloat16)
         x = (torch.rand(M, K, device=dev, generator=gen) - 0.5).to(torch.bfloat16)
         t_torch = time_torch(x, w)

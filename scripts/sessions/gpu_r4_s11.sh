@@ -23,3 +23,12 @@ import json; d=json.load(open('$O/P2.json'))['P2']['per_kernel']
 for k,v in d.items():
     if 'lmb' in k: print(k[:70], {c: v[c] for c in v}, 'dram/ea=%.3f' % (v.get('TCC_EA0_RDREQ_DRAM_sum',0)/max(1,v.get('TCC_EA0_RDREQ_sum',1))))
 "
+# (3) would split-K help the BERT bs16 projections? Each split-K-s GEMM (M, N, K) runs like one GEMM
+# (s*M, N, K/s) -- same workgroups, same bytes per workgroup -- plus a reduction
+timeout -k 10 300 python3 scripts/bench_gemm.py --shapes "2048,768,3072;4096,768,1536;6144,768,1024;8192,768,768;2048,768,768;4096,768,384;6144,768,256;2048,2304,768;4096,2304,384;6144,2304,256;2048,3072,768;4096,3072,384;6144,3072,256" > $O/gemm_splitk.jsonl 2>&1 || { tail -5 $O/gemm_splitk.jsonl; exit 1; }
+python3 -c "
+import json
+for l in open('$O/gemm_splitk.jsonl'):
+    if l.startswith('{'):
+        d=json.loads(l); print(d['M'], d['N'], d['K'], d['hipzap_us'], d['hipzap_cfg'], d['hipblaslt_us'])
+"
