@@ -25,7 +25,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -50,6 +52,7 @@ struct Slot {
   void* out = nullptr;
   hipEvent_t ev = nullptr;
   bool done = false;
+  std::atomic<bool> done_a{false};  // = done, for the low-load spin of submit_one (set after rc)
   int rc = 0;
   std::condition_variable cv;
   // dynamic batching: rows claimed / payloads copied / outputs read; sealed = no more rows
@@ -77,11 +80,18 @@ struct Exec {
   double max_wait_us = 0;
   uint64_t row_in[kMaxIn] = {};
   uint64_t row_out = 0;
+  // low load (HIPZAP_EXEC_SPIN_US, default 300; 0 = off): an idle worker polls for new work and a
+  // request thread that is alone (or one of two) polls for its completion for up to this long
+  // before sleeping on a condition variable -- two futex wake-ups off a single request's latency.
+  // Under load nobody spins: the worker always has replays in flight and requesters sleep.
+  double spin_us = 300.0;
+  std::atomic<int> work_hint{0};  // bumped whenever work is queued for the worker
 
   void complete(int s, int rc) {
     std::lock_guard<std::mutex> g(mu);
     slots[s].rc = rc;
     slots[s].done = true;
+    slots[s].done_a.store(true, std::memory_order_release);
     slots[s].cv.notify_all();
     served += rows == 1 ? 1 : slots[s].claimed;
     ++batches;
@@ -92,6 +102,7 @@ struct Exec {
     Slot& sl = slots[s];
     if (sl.sealed && sl.copied == sl.claimed) {
       to_launch.push_back(s);
+      work_hint.fetch_add(1, std::memory_order_release);
       cv_work.notify_one();
     }
   }
@@ -106,7 +117,19 @@ struct Exec {
 
   void run() {
     std::vector<int> launch;
+    double last_busy = now_us();
     for (;;) {
+      if (inflight.empty() && spin_us > 0 && now_us() - last_busy < spin_us) {
+        // idle but recently busy: poll for new work without the lock instead of sleeping
+        const int h0 = work_hint.load(std::memory_order_acquire);
+        bool empty;
+        {
+          std::lock_guard<std::mutex> g(mu);
+          empty = to_launch.empty() && open < 0 && !stop;
+        }
+        while (empty && work_hint.load(std::memory_order_acquire) == h0 && now_us() - last_busy < spin_us)
+          std::this_thread::yield();
+      }
       {
         std::unique_lock<std::mutex> lk(mu);
         // at shutdown a request may still be copying into a sealed slot (not yet queued): keep
@@ -129,6 +152,7 @@ struct Exec {
           inflight.push_back(s);
       }
       bool progressed = !launch.empty();
+      if (progressed || !inflight.empty()) last_busy = now_us();
       for (size_t i = 0; i < inflight.size();) {
         const int s = inflight[i];
         const hipError_t q = hipEventQuery(slots[s].ev);
@@ -161,6 +185,7 @@ struct Exec {
           o.sealed = o.done = false;
           o.t_open = now_us();
           open = s;
+          work_hint.fetch_add(1, std::memory_order_release);
           cv_work.notify_one();  // the worker decides when to seal
           cv_free.notify_all();  // waiting requests may join this batch
           break;
@@ -214,6 +239,7 @@ struct Exec {
             o.sealed = o.done = false;
             o.t_open = now_us();
             open = s;
+            work_hint.fetch_add(1, std::memory_order_release);
             cv_work.notify_one();
             cv_free.notify_all();
             break;
@@ -283,11 +309,22 @@ struct Exec {
     for (int k = 0; k < n_in; ++k)
       if (in && in[k] && in_bytes[k]) std::memcpy(sl.in[k], in[k], in_bytes[k]);
     int rc;
+    bool spin;
     {
       std::unique_lock<std::mutex> lk(mu);
       sl.done = false;
+      sl.done_a.store(false, std::memory_order_relaxed);
       to_launch.push_back(s);
+      work_hint.fetch_add(1, std::memory_order_release);
       cv_work.notify_one();
+      spin = spin_us > 0 && active <= 2;
+    }
+    if (spin) {  // low load: poll for the completion before sleeping
+      const double ts = now_us();
+      while (!sl.done_a.load(std::memory_order_acquire) && now_us() - ts < 4.0 * spin_us) std::this_thread::yield();
+    }
+    {
+      std::unique_lock<std::mutex> lk(mu);
       sl.cv.wait(lk, [&] { return sl.done; });
       rc = sl.rc;
     }
@@ -306,6 +343,7 @@ struct Exec {
       std::lock_guard<std::mutex> g(mu);
       stop = true;
     }
+    work_hint.fetch_add(1, std::memory_order_release);
     cv_work.notify_all();
     cv_free.notify_all();
     if (worker.joinable()) worker.join();  // returns once no request thread is inside submit_wait
@@ -325,6 +363,7 @@ void* hz_exec_create(HzProgram* progs, hipStream_t* streams, void** host_in, con
   if (n <= 0 || n_in < 0 || n_in > kMaxIn) return nullptr;
   auto* e = new Exec();
   e->slots = std::vector<Slot>(n);
+  if (const char* sp = getenv("HIPZAP_EXEC_SPIN_US")) e->spin_us = atof(sp);
   e->n_in = n_in;
   for (int k = 0; k < n_in; ++k) e->in_bytes[k] = in_bytes[k];
   e->out_bytes = out_bytes;
