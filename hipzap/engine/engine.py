@@ -241,7 +241,14 @@ class Engine:
         ex = self.executor()
         if ex is not None:
             c0 = self.contexts[0]
-            ins = [xi.to(hb.dtype).reshape(hb.shape).contiguous() for hb, xi in zip(c0.host_inputs, xs)]
+            # fast path (the common one-tensor request already in the payload's dtype and layout):
+            # no per-request tensor views (~2 us each of the single-request latency)
+            hbs = c0.host_inputs
+            if all(xi.dtype == hb.dtype and xi.is_contiguous() and xi.numel() == hb.numel() and xi.device.type == "cpu"
+                   for hb, xi in zip(hbs, xs)):
+                ins = xs
+            else:
+                ins = [xi.to(hb.dtype).reshape(hb.shape).contiguous() for hb, xi in zip(hbs, xs)]
             out = torch.empty_like(c0.host_output)
             ex.submit([t.data_ptr() for t in ins], out.data_ptr())
             if _native.DEBUG:
@@ -268,10 +275,17 @@ class Engine:
         return self._post(out)
 
     def _post(self, out):
-        try:
+        takes_meta = getattr(self, "_post_meta", None)
+        if takes_meta is None:  # decided once (a TypeError per request cost ~1 us)
+            import inspect
+            try:
+                takes_meta = len(inspect.signature(self.adapter.postprocess_output).parameters) >= 2
+            except (TypeError, ValueError):
+                takes_meta = True
+            self._post_meta = takes_meta
+        if takes_meta:
             return self.adapter.postprocess_output(out, getattr(self.graph, "meta", None))
-        except TypeError:
-            return self.adapter.postprocess_output(out)
+        return self.adapter.postprocess_output(out)
 
     def infer_device(self, x: torch.Tensor, ctx_index: int = 0) -> torch.Tensor:
         """Device-resident variant (no host copies); output aliases the static buffer.
