@@ -457,6 +457,137 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
+// ---- ping-pong MX GEMM (VERDICT r3 "next round" 6; cdna_hip_programming.md ping-pong) ----
+// cfg 24's 128x128 tile and wave map (wave (wm, wn): tokens wm*64.., features wn*32..) with the two
+// wave groups a phase apart: group 0 (wm = 0, one wave per SIMD) reads its operands of K-step t
+// from LDS while group 1 (the other wave on each SIMD) issues its MFMAs of t - 1, then they swap,
+// so on every SIMD one wave's LDS reads overlap the other's MFMAs instead of both waiting on
+// their reads together. Two barriers per K-step; the MFMA group raises its issue priority. NS LDS
+// stages: stage t + NS - 1 is issued right after the barrier that retires the last reads of
+// buffer (t - 1) % NS; counted vmcnt waits keep the later stages in flight across barriers. Same
+// LDS images, swizzle, hardware K order, per-wave accumulation order and epilogue as cfg 24:
+// bitwise equal to it (tests/test_fp8_gpu.py). Per-row activation scales only (XS = false).
+template <int NS>
+__global__ __launch_bounds__(512) void gemm_mxpp_kernel(const HzGemmFp8Params p, int group_m) {
+  constexpr int BM = 128, BN = 128, WM = 2, WN = 4, NW = 8;
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 2, 4
+  constexpr int NWG = BN / 16;
+  constexpr int XBYTES = BM * 128, WBYTES = NWG * 2048, SBYTES = XBYTES + WBYTES;
+  constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;  // 2, 2
+  constexpr int G = XPW + WPW;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;  // wm = the wave's group
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
+  const int n0 = tile_n * BN, m0 = tile_m * BM;
+  const int kb = p.K >> 7;
+
+  const unsigned char* xsrc[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int q = wave + NW * i;
+    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
+    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
+    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
+  }
+  const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
+  auto stage = [&](int buf, int st) {
+    char* base = smem + buf * SBYTES;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int piece = wave + NW * i;
+      const int g = piece >> 1, h = piece & 1;
+      glds16_8(wsrc + ((long)g * kb + st) * 2048 + h * 1024, base + XBYTES + piece * 1024);
+    }
+  };
+  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
+  const int brow = (wm * (BM / WM) + lr) * 128;
+  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
+  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
+
+  f32x4 acc[FCW][FPW];
+#pragma unroll
+  for (int i = 0; i < FCW; ++i)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 a[FCW], b[FPW];
+  auto read = [&](int st) {
+    const char* base = smem + (st % NS) * SBYTES;
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048 + 1024);
+      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + boff0 + j * 16 * 128);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + j * 16 * 128);
+      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+  };
+  auto mfma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FCW; ++i)
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                      0x7f7f7f7f);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < kb) stage(s0, s0);
+  // K-step t: phase 0 = group 0 reads t | group 1 multiplies t - 1; phase 1 = group 0 multiplies
+  // t | group 1 reads t. One extra round lets group 1 multiply the last K-step.
+  for (int st = 0; st <= kb; ++st) {
+    if (st < kb) {  // this wave's pieces of stage st landed (later stages may stay in flight)
+      const int ahead = min(NS - 2, kb - 1 - st);
+      if (NS > 3 && ahead >= 2) wait_vm8<(NS > 3 ? 2 * G : 0)>();
+      else if (NS > 2 && ahead >= 1) wait_vm8<(NS > 2 ? G : 0)>();
+      else wait_vm8<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage st complete; buffer (st - 1) % NS read by both groups
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + NS - 1 < kb) stage((st + NS - 1) % NS, st + NS - 1);
+    if (wm == 0) {
+      if (st < kb) read(st);
+    } else if (st >= 1) {
+      mfma();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st < kb) {
+      if (wm == 0) mfma();
+      else read(st);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
+}
+
+template <int NS>
+int launch_mxpp(const HzGemmFp8Params& p, hipStream_t st) {
+  if (p.N % 128 || p.xs) return -4;  // full 128-wide feature tiles, per-row activation scales only
+  const int tiles = (p.N / 128) * ((p.M + 127) / 128);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  hipLaunchKernelGGL(gemm_mxpp_kernel<NS>, dim3(tiles), dim3(512), 0, st, p, group_m);
+  return (int)hipGetLastError();
+}
+
 // ---- 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608): measured, never chosen ----
 // A 256 x BN tile moves half the staging bytes per FLOP of the 128x128 tiles (BN = 256: 64 KB per
 // k-step for 16.8 MFLOP) with ONE 8-wave workgroup per CU, wave (wm, wn) owning 128 tokens x BN/4
@@ -798,6 +929,10 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
+      // ping-pong 128x128 (two wave groups a phase apart): 2 / 3 / 4 LDS stages
+      case 34: return launch_mxpp<2>(p, st);
+      case 35: return launch_mxpp<3>(p, st);
+      case 36: return launch_mxpp<4>(p, st);
 #if HZ_EXPERIMENTS
       // 256-row kernel (branch-free main loop, pinned read / MFMA order): 256x256 / 2 stages,
       // 256x128 / 2 and 3 stages

@@ -107,8 +107,12 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             33: (256, 256), 43: (256, 256), 44: (256, 128), 45: (256, 128),
             # 46 / 47: the ring-pipelined 256-row kernel, K = 768 unrolled (3- / 2-buffer ring; per-row
             # activation scales only -- an MX8-input or other-K launch is refused)
-            46: (256, 128), 47: (256, 128)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 43, 44, 45, 46, 47)
+            46: (256, 128), 47: (256, 128),
+            # 34-36: cfg 24's tile with the two wave groups a phase apart (ping-pong), 2 / 3 / 4 stages;
+            # per-row activation scales only (an MX8-input launch is refused)
+            34: (128, 128), 35: (128, 128), 36: (128, 128)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 34, 35, 36, 43, 44, 45, 46, 47)
+MX_PERROW_ONLY = (34, 35, 36, 46, 47)
 MX_EXPERIMENTS = (43, 44, 45, 46, 47)  # only in the HZ_EXPERIMENTS library (csrc/common.h)
 
 
@@ -123,8 +127,8 @@ def mx_ok(M: int, pw: PackedFp8, ldx: int | None = None) -> bool:
 def candidates_fp8(M: int, pw: PackedFp8, mx_io: bool = False) -> list:
     from .conv import candidates
     exp = N.experiments()
-    out = [(cfg, 1) for cfg in MX_TILES if mx_fits(cfg, pw.cout) and (exp or cfg not in MX_EXPERIMENTS)] \
-        if mx_ok(M, pw) else []
+    out = [(cfg, 1) for cfg in MX_TILES if mx_fits(cfg, pw.cout) and (exp or cfg not in MX_EXPERIMENTS)
+           and not (mx_io and cfg in MX_PERROW_ONLY)] if mx_ok(M, pw) else []
     # the fp8 launcher reads cfg >= 16 as an MX tile: the bf16-only 32x32 LDS tiles do not exist there
     return out if mx_io else out + [c for c in candidates(M, pw.cout, pw.K) if c[0] < 64]
 

@@ -236,6 +236,39 @@ def test_gemm_mx_phased_bitwise_vs_128(cfg, K, mx_out):
         assert not (outs[1][0] == 7.0).all(-1).any(), "rows left unwritten"
 
 
+@pytest.mark.parametrize("cfg", [34, 35, 36])
+@pytest.mark.parametrize("K", [768, 3072])
+@pytest.mark.parametrize("mx_out", [False, True])
+def test_gemm_mx_pingpong_bitwise_vs_128(cfg, K, mx_out):
+    """The ping-pong MX kernel (two wave groups a phase apart, 2-4 LDS stages) reads the same LDS
+    images and sums every output over the same k-steps in the same order as cfg 24: BITWISE equal
+    (partial last row tile, bf16 or MX8 output)."""
+    import ctypes
+    from hipzap import _native as N
+    g = torch.Generator().manual_seed(13)
+    M, Nn = 12608 - 64, 768
+    w = torch.randn(Nn, K, generator=g) * 0.05
+    b = torch.randn(Nn, generator=g)
+    x = torch.randn(M, K, generator=g) * torch.linspace(0.1, 8, K)
+    pw = F8.quantize_linear(C.pack_linear(w, b))
+    pwd = F8.PackedFp8(pw.w8.to(DEV), pw.sw.to(DEV), pw.bias.to(DEV), pw.cin, pw.cout, pw.w8mx.to(DEV))
+    x8, sx = F8.quant_rows(x.to(torch.bfloat16).to(DEV))
+    outs = []
+    for c in (24, cfg):
+        out = torch.full((M, Nn), 7.0, device=DEV, dtype=torch.bfloat16)
+        o8 = torch.zeros(M, Nn, dtype=torch.uint8, device=DEV)
+        os8 = torch.zeros(M, Nn // 32, dtype=torch.uint8, device=DEV)
+        prm = F8.gemm_params(x8.data_ptr(), N.ptr(sx), pwd, M, 0 if mx_out else out.data_ptr(), 0, "gelu", False, c,
+                             1, out8_ptr=o8.data_ptr() if mx_out else 0, os8_ptr=os8.data_ptr() if mx_out else 0)
+        N.check(N.lib().hz_launch_kernel(F8.K_GEMM_FP8, ctypes.byref(prm), N.stream_ptr()), f"gemm cfg {c}")
+        torch.cuda.synchronize()
+        outs.append((o8.cpu(), os8.cpu()) if mx_out else (out.cpu(),))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_), f"cfg {cfg} differs from cfg 24"
+    if not mx_out:
+        assert not (outs[1][0] == 7.0).all(-1).any(), "rows left unwritten"
+
+
 def test_gemm_mx_phased_refuses_mx8_input():
     _need_exp(46)
     import ctypes
