@@ -457,6 +457,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
+#if HZ_EXPERIMENTS
 // ---- ping-pong MX GEMM (VERDICT r3 "next round" 6; cdna_hip_programming.md ping-pong) ----
 // cfg 24's 128x128 tile and wave map (wave (wm, wn): tokens wm*64.., features wn*32..) with the two
 // wave groups a phase apart: group 0 (wm = 0, one wave per SIMD) reads its operands of K-step t
@@ -587,6 +588,8 @@ int launch_mxpp(const HzGemmFp8Params& p, hipStream_t st) {
   hipLaunchKernelGGL(gemm_mxpp_kernel<NS>, dim3(tiles), dim3(512), 0, st, p, group_m);
   return (int)hipGetLastError();
 }
+
+#endif  // HZ_EXPERIMENTS
 
 // ---- 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608): measured, never chosen ----
 // A 256 x BN tile moves half the staging bytes per FLOP of the 128x128 tiles (BN = 256: 64 KB per
@@ -929,10 +932,13 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
-      // ping-pong 128x128 (two wave groups a phase apart): 2 / 3 / 4 LDS stages
+#if HZ_EXPERIMENTS
+      // ping-pong 128x128 (two wave groups a phase apart): 2 / 3 / 4 LDS stages. Measured 1.4x
+      // SLOWER than cfg 24 on the ViT bs64 QKV / FC1 shapes (profiles/r4_mx): experiments only
       case 34: return launch_mxpp<2>(p, st);
       case 35: return launch_mxpp<3>(p, st);
       case 36: return launch_mxpp<4>(p, st);
+#endif
 #if HZ_EXPERIMENTS
       // 256-row kernel (branch-free main loop, pinned read / MFMA order): 256x256 / 2 stages,
       // 256x128 / 2 and 3 stages

@@ -109,11 +109,12 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             # activation scales only -- an MX8-input or other-K launch is refused)
             46: (256, 128), 47: (256, 128),
             # 34-36: cfg 24's tile with the two wave groups a phase apart (ping-pong), 2 / 3 / 4 stages;
-            # per-row activation scales only (an MX8-input launch is refused)
+            # per-row activation scales only; measured 1.4x slower than cfg 24 (profiles/r4_mx):
+            # experiments build only
             34: (128, 128), 35: (128, 128), 36: (128, 128)}
 MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 34, 35, 36, 43, 44, 45, 46, 47)
 MX_PERROW_ONLY = (34, 35, 36, 46, 47)
-MX_EXPERIMENTS = (43, 44, 45, 46, 47)  # only in the HZ_EXPERIMENTS library (csrc/common.h)
+MX_EXPERIMENTS = (34, 35, 36, 43, 44, 45, 46, 47)  # only in the HZ_EXPERIMENTS library (csrc/common.h)
 
 
 def mx_fits(cfg: int, n: int) -> bool:

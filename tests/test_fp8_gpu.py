@@ -12,7 +12,7 @@ DEV = "cuda:0"
 
 
 def _need_exp(cfg):
-    """cfg 43-47 (256-row MX pipelines) exist only in the HZ_EXPERIMENTS library."""
+    """cfg 34-36 (ping-pong) and 43-47 (256-row MX pipelines) exist only in the HZ_EXPERIMENTS library."""
     from hipzap import _native as N
     if cfg in F8.MX_EXPERIMENTS and not N.experiments():
         pytest.skip("measured-negative MX pipeline: build with python -m hipzap.build --experiments")
@@ -243,6 +243,7 @@ def test_gemm_mx_pingpong_bitwise_vs_128(cfg, K, mx_out):
     """The ping-pong MX kernel (two wave groups a phase apart, 2-4 LDS stages) reads the same LDS
     images and sums every output over the same k-steps in the same order as cfg 24: BITWISE equal
     (partial last row tile, bf16 or MX8 output)."""
+    _need_exp(cfg)
     import ctypes
     from hipzap import _native as N
     g = torch.Generator().manual_seed(13)
