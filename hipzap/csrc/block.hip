@@ -880,6 +880,7 @@ __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
 
 extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
   const HzStemParams& p = *pp;
+  if (!p.src || !p.w || !p.bias || !p.out) return -1;
   if (p.N < 1 || p.H < 8 || p.W < 8 || p.mode < 0 || p.mode > 2) return -1;
   if (p.SH != (p.H + 6 - 7) / 2 + 1 || p.SW != (p.W + 6 - 7) / 2 + 1) return -1;  // 7x7/2 pad 3
   if (p.PH != (p.SH + 2 - 3) / 2 + 1 || p.PW != (p.SW + 2 - 3) / 2 + 1) return -1;  // 3x3/2 pad 1
@@ -892,6 +893,8 @@ extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
 
 extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   const HzBneckParams& p = *pp;
+  if (!p.x || !p.w1 || !p.b1 || !p.w2 || !p.b2 || !p.w3 || !p.b3 || !p.out || (!p.wd) != (!p.bd)) return -1;
+  if (p.N < 1 || p.H < 1 || p.W < 1) return -1;
   if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles (H, W: the block's OUTPUT size)
     if (p.N < 1 || p.Cout != kB2CO || p.H % kB2T || p.W % kB2T) return -1;
     const dim3 grid((p.H / kB2T) * (p.W / kB2T) * p.N);

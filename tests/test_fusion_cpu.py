@@ -89,3 +89,42 @@ def test_arena_never_aliases_a_fused_runs_tensors(r50):
             assert not overlap(offsets, t, last), (f.kind, g.tensors[t].name)
             hit_naive |= overlap(naive, t, last)
     assert hit_naive  # the hazard is real without the groups
+
+
+def test_launchers_refuse_malformed_params_before_any_hip_call():
+    """The fused launchers validate geometry and pointers on the host (returning -1 before any
+    HIP call, so this runs without a GPU): a kernel launched on a shape its tiles do not assume
+    would read out of bounds."""
+    import ctypes as C
+    from hipzap import _native as N
+    lib = N.lib()
+    fake = 1 << 20  # never dereferenced: every case below is refused first
+
+    def bneck(**kw):
+        p = fusion.BneckParams(x=fake, w1=fake, b1=fake, w2=fake, b2=fake, w3=fake, b3=fake, out=fake,
+                               N=1, H=28, W=28, Cin=512, Cmid=128, Cout=512)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return lib.hz_bneck_launch(C.byref(p), None)
+
+    assert bneck(x=None) == -1
+    assert bneck(out=None) == -1
+    assert bneck(wd=fake) == -1                     # downsample weights without its bias
+    assert bneck(H=0) == -1 and bneck(N=0) == -1
+    assert bneck(H=30) == -1                        # layer2 tiles are 4x4
+    assert bneck(Cin=256) == -1                     # layer2 first block needs its downsample
+    assert bneck(Cout=256) == -1
+    assert bneck(Cmid=64, Cin=256, Cout=256, H=56, W=56, tile_h=6) == -1
+    assert bneck(Cmid=64, Cin=64, Cout=256, H=56, W=56) == -1  # layer1 first block without downsample
+
+    def stem(**kw):
+        p = fusion.StemParams(src=fake, w=fake, bias=fake, out=fake, N=1, H=224, W=224, mode=1,
+                              SH=112, SW=112, PH=56, PW=56)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return lib.hz_stem_launch(C.byref(p), None)
+
+    assert stem(w=None) == -1
+    assert stem(SH=111) == -1 and stem(PH=55) == -1
+    assert stem(mode=3) == -1
+    assert stem(src=fake + 2) == -1                 # uint8 rows are read as dwords
