@@ -35,6 +35,10 @@ LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
              70: (64, 64), 71: (128, 64), 72: (64, 128), 73: (64, 128), 74: (128, 192), 75: (64, 192),
              76: (128, 64), 77: (256, 256)}
 M32_CFGS = tuple(range(64, 78))
+# the folded-LayerNorm epilogue (HzLnFold, experiments build) writes its statistics slabs per
+# (feature tile, wave column) of a 2-column wave grid: LDS tiles with 4 wave columns map to the
+# same tile with 2 (128x192 has none: 128x128)
+LNF_REMAP = {28: 16, 29: 20, 32: 17, 35: 16, 36: 16}
 # LDS tiles that also run as an implicit-GEMM conv on channel-blocked activations (csrc/gemm.hip CV
 # mode; ResNet at batch >= 4): C % 64 == 0, Cout % BN == 0
 LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 64, 65, 66, 67, 69, 71, 72, 76)
