@@ -20,7 +20,6 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
-from dataclasses import dataclass, field
 
 from .. import _native as N
 
@@ -29,26 +28,34 @@ def _pad(n: int, m: int) -> int:
     return int(math.ceil(n / m) * m)
 
 
-@dataclass
-class LmbLayer:
-    H: int
-    In: int
-    Kh: int
-    Kx: int
-    R: int
-    keys: tuple  # (w_ih, w_hh, b_ih, b_hh) state_dict keys
+class _Record:
+    """Plain value record (``dataclasses`` costs ~7-10 ms of import through ``inspect`` on the
+    torch-free LM cold-start path, coldstart.py ``import_lmlite``)."""
+    __slots__ = ()
+
+    def __repr__(self) -> str:
+        return f"{type(self).__name__}({', '.join(f'{k}={getattr(self, k)!r}' for k in self.__slots__)})"
+
+    def __eq__(self, other) -> bool:
+        return type(other) is type(self) and all(getattr(self, k) == getattr(other, k) for k in self.__slots__)
 
 
-@dataclass
-class LmbGeometry:
-    layers: list
-    V: int
-    E: int
-    Ke: int
-    Vp: int
-    dec_key: str | None   # untied decoder weight key (None: tied to the embedding)
-    dec_bias_key: str | None
-    extra: dict = field(default_factory=dict)
+class LmbLayer(_Record):
+    __slots__ = ("H", "In", "Kh", "Kx", "R", "keys")  # keys: (w_ih, w_hh, b_ih, b_hh) state_dict keys
+
+    def __init__(self, H: int, In: int, Kh: int, Kx: int, R: int, keys: tuple):
+        self.H, self.In, self.Kh, self.Kx, self.R, self.keys = H, In, Kh, Kx, R, keys
+
+
+class LmbGeometry(_Record):
+    # dec_key: untied decoder weight key (None: tied to the embedding)
+    __slots__ = ("layers", "V", "E", "Ke", "Vp", "dec_key", "dec_bias_key", "extra")
+
+    def __init__(self, layers: list, V: int, E: int, Ke: int, Vp: int, dec_key: str | None,
+                 dec_bias_key: str | None, extra: dict | None = None):
+        self.layers, self.V, self.E, self.Ke, self.Vp = layers, V, E, Ke, Vp
+        self.dec_key, self.dec_bias_key = dec_key, dec_bias_key
+        self.extra = {} if extra is None else extra
 
     def layer_bytes(self, i: int) -> tuple[int, int]:
         ly = self.layers[i]
