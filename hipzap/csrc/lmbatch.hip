@@ -288,7 +288,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int NB, int KS, int CH, int R>
+template <int NB, int KS, int CH, int R, bool NT = false>
 __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int NCH = KS / CH;  // K = 32 * KS
   constexpr int RR = R < NCH ? R : NCH;  // chunks issued before the first MFMA
@@ -312,8 +312,15 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   auto issue = [&](int slot, int c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
-      wa[slot][s] = *reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512);
-      wb[slot][s] = *reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512);
+      const u32x4* a = reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512);
+      const u32x4* b = reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512);
+      if constexpr (NT) {  // non-temporal weight stream (MI355X_MICROARCH.md "nt-weights")
+        wa[slot][s] = __builtin_nontemporal_load(a);
+        wb[slot][s] = __builtin_nontemporal_load(b);
+      } else {
+        wa[slot][s] = *a;
+        wb[slot][s] = *b;
+      }
     }
   };
   issue(0, 0);
@@ -515,13 +522,15 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
 }
 
 // decoder weight pipeline: HIPZAP_LMB_DEC_PIPE = "8x2" (default: 8 k-steps per chunk, 2 chunks in
-// the ring), "4x5" or "4x6" (K = 1024 only; the A/B of profiles/r4_lmb)
+// the ring), "4x5" or "4x6" (K = 1024 only; the A/B of profiles/r4_lmb), "8x2nt" (the default ring
+// with non-temporal weight loads)
 static int lmb_dec_pipe() {
   static const int v = [] {
     const char* e = getenv("HIPZAP_LMB_DEC_PIPE");
     if (!e) return 0;
     if (!strcmp(e, "4x5")) return 1;
     if (!strcmp(e, "4x6")) return 2;
+    if (!strcmp(e, "8x2nt")) return 3;
     return 0;
   }();
   return v;
@@ -535,7 +544,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
   const dim3 grid(p.nblk), block(512);
   const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
-#define HZ_LMBD(NB, KS, CH, R) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R>), grid, block, 0, st, p)
+#define HZ_LMBD(NB, KS, CH, R, ...) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R, ##__VA_ARGS__>), grid, block, 0, st, p)
 #define HZ_LMBD_K(NB)                               \
   switch (p.K / 256) {                              \
     case 1: HZ_LMBD(NB, 8, 8, 2); break;            \
@@ -544,6 +553,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
     case 4:                                         \
       if (pipe == 1) HZ_LMBD(NB, 32, 4, 5);         \
       else if (pipe == 2) HZ_LMBD(NB, 32, 4, 6);    \
+      else if (pipe == 3) HZ_LMBD(NB, 32, 8, 2, true); \
       else HZ_LMBD(NB, 32, 8, 2);                   \
       break;                                        \
     default: return -1;                             \
