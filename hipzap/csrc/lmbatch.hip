@@ -522,8 +522,8 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
 }
 
 // decoder weight pipeline: HIPZAP_LMB_DEC_PIPE = "8x2" (default: 8 k-steps per chunk, 2 chunks in
-// the ring), "4x5" or "4x6" (K = 1024 only; the A/B of profiles/r4_lmb), "8x2nt" (the default ring
-// with non-temporal weight loads)
+// the ring); experiments build only (measured negatives, profiles/r4_lmb): "4x5" or "4x6" (K = 1024)
+// and "8x2nt" (the default ring with non-temporal weight loads)
 static int lmb_dec_pipe() {
   static const int v = [] {
     const char* e = getenv("HIPZAP_LMB_DEC_PIPE");
@@ -544,17 +544,24 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
   const dim3 grid(p.nblk), block(512);
   const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
+  (void)pipe;
 #define HZ_LMBD(NB, KS, CH, R, ...) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R, ##__VA_ARGS__>), grid, block, 0, st, p)
+#if HZ_EXPERIMENTS  // measured negatives (profiles/r4_lmb): deeper rings, non-temporal weight loads
+#define HZ_LMBD_EXP(NB)                                                   \
+  if (pipe == 1) { HZ_LMBD(NB, 32, 4, 5); break; }                         \
+  if (pipe == 2) { HZ_LMBD(NB, 32, 4, 6); break; }                         \
+  if (pipe == 3) { HZ_LMBD(NB, 32, 8, 2, true); break; }
+#else
+#define HZ_LMBD_EXP(NB)
+#endif
 #define HZ_LMBD_K(NB)                               \
   switch (p.K / 256) {                              \
     case 1: HZ_LMBD(NB, 8, 8, 2); break;            \
     case 2: HZ_LMBD(NB, 16, 8, 2); break;           \
     case 3: HZ_LMBD(NB, 24, 8, 2); break;           \
     case 4:                                         \
-      if (pipe == 1) HZ_LMBD(NB, 32, 4, 5);         \
-      else if (pipe == 2) HZ_LMBD(NB, 32, 4, 6);    \
-      else if (pipe == 3) HZ_LMBD(NB, 32, 8, 2, true); \
-      else HZ_LMBD(NB, 32, 8, 2);                   \
+      HZ_LMBD_EXP(NB)                               \
+      HZ_LMBD(NB, 32, 8, 2);                        \
       break;                                        \
     default: return -1;                             \
   }
@@ -564,6 +571,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
     HZ_LMBD_K(2)
   }
 #undef HZ_LMBD_K
+#undef HZ_LMBD_EXP
 #undef HZ_LMBD
   return (int)hipGetLastError();
 }
