@@ -239,6 +239,8 @@ def _load():
     _sig(lib, "hz_lmb_set_lowload", c_int, P, P, c_int)
     _sig(lib, "hz_lmb_embproj_launch", c_int, P, P)
     _sig(lib, "hz_lmb_lo_replays", U64, P)
+    _sig(lib, "hz_lmb_set_solo", c_int, P, P)
+    _sig(lib, "hz_lmb_solo_replays", U64, P)
     _sig(lib, "hz_lmb_destroy", None, P)
     if DEBUG:
         for unit in DEBUG_UNITS:

@@ -236,7 +236,8 @@ typedef struct HzLmbLayerParams {
   unsigned long long* dbest;  // [2 parity][Bp] running maxima (packed key, row) of the decoder; the
   int V;                      //   first layer reads the other parity and clears its own
   int nb_act;                 // row blocks (of 16) computed: 0 = all Bp/16; 1 = rows 0..15 only (the
-                              //   low-load program: every busy row is below 16)
+                              //   low-load program: every busy row is below 16); -1 = request row 0
+                              //   only (the one-request program: no other row's state read or written)
   int* const* outp;           // [Bp] request output arrays (pinned host, written by workgroup 0)
   int* tok;                   // [Bp] this step's tokens (device, diagnostics)
   const float* embproj;       // first layer: [Vp][R] fp32 W_ih E[v] (hz_lmb_embproj_launch) or NULL
@@ -286,6 +287,8 @@ int hz_lmb_submit(void* s, const int* prompt, int P, int n, unsigned long long s
 void hz_lmb_stats(void* s, unsigned long long* out4);  // replays, served, row-steps used, row-steps total
 int hz_lmb_set_lowload(void* s, const HzProgram* lo, int rows);  // programs for replays whose busy rows are < rows
 unsigned long long hz_lmb_lo_replays(void* s);
+int hz_lmb_set_solo(void* s, const HzProgram* solo);  // programs for replays whose only busy row is row 0
+unsigned long long hz_lmb_solo_replays(void* s);
 void hz_lmb_destroy(void* s);
 
 // ---- device-side packing of raw checkpoint tensors (csrc/pack.hip; torch-free .pth cold start) ----

@@ -69,9 +69,14 @@ __device__ __forceinline__ int st_off(int j, int r, int NB) {
 // EP (first layer, p.embproj): the embedding half of the layer's K is precomputed per vocabulary
 // id (lmb_embproj_kernel: P[v] = W_ih E[v], fp32), so the workgroup multiplies W_hh h only and the
 // cell update adds P[token] -- half the weight bytes on the step's critical path.
-template <int NB, bool FIRST, int TPW, int NBW, bool EP = false>
+// SOLO (p.nb_act == -1, the one-request program): request row 0 alone is busy; the other rows'
+// state is neither read (their operand lanes are zero) nor written, so a wave fetches 1/16 of
+// each 1 KiB state fragment (the lanes of row 0: 0, 16, 32, 48). Each MFMA output column depends
+// on its own row's operand only: row 0 is bitwise the full program's.
+template <int NB, bool FIRST, int TPW, int NBW, bool EP = false, bool SOLO = false>
 __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p) {
   static_assert(NBW == NB || NBW == 1, "row blocks per workgroup");
+  static_assert(!SOLO || NBW == NB, "the one-request program uses the all-row-block shape");
   static_assert(!EP || FIRST, "the projected embedding is the first layer's input");
   __shared__ f32x4 part[LW][TPW][NBW][64];
   __shared__ int s_tok[32];
@@ -84,8 +89,9 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   }
   const int tile0 = grp * TPW;  // this workgroup's row tiles tile0 .. tile0 + TPW - 1
   const int ntile = p.R >> 4;
-  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
+  const int nba = SOLO ? 1 : p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   if (tile0 >= ntile || cb0 >= nba) return;      // (grid padding of the twin mapping; low-load program)
+  const bool row_lane = !SOLO || (lane & 15) == 0;  // this lane carries a busy row's operand
   const int nbw = min(NBW, nba - cb0);           // row blocks this workgroup computes
   const int KSH = p.Kh >> 5, KSX = p.Kx >> 5, KS = KSH + KSX;  // KS: the packed row stride
   const int KSE = EP ? KSH : KS;                                  // k-steps multiplied here
@@ -131,8 +137,12 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
 #pragma unroll
     for (int cb = 0; cb < NBW; ++cb) {
       if (cb < nbw) {
-        ah[s][cb] = *reinterpret_cast<const u32x4*>(src + (cb0 + cb) * 512 + lane * 8);
-        al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + (cb0 + cb) * 512 + lane * 8);
+        if (row_lane) {
+          ah[s][cb] = *reinterpret_cast<const u32x4*>(src + (cb0 + cb) * 512 + lane * 8);
+          al[s][cb] = *reinterpret_cast<const u32x4*>(src + lo_off + (cb0 + cb) * 512 + lane * 8);
+        } else {
+          ah[s][cb] = al[s][cb] = u32x4{0u, 0u, 0u, 0u};
+        }
       }
     }
   }
@@ -156,7 +166,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
     lds_barrier();  // LDS only: the weight and state loads stay in flight
     if constexpr (EP) {
       // the cell-update threads fetch their rows' projected embedding now (consumed after the MFMAs)
-      if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw) {
+      if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw && row_lane) {
         const int tt = tid / (NBW * 64), cb = (tid >> 6) % NBW, l = tid & 63;
         const int j = min((tile0 + tt) * 4 + (l >> 4), p.R / 4 - 1);
         pe = *reinterpret_cast<const f32x4*>(p.embproj + (size_t)s_tok[(cb0 + cb) * 16 + (l & 15)] * p.R + 4 * j);
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       if (ks >= KSH) {  // wave-uniform
 #pragma unroll
         for (int cb = 0; cb < NBW; ++cb) {
-          if (cb >= nbw) continue;
+          if (cb >= nbw || !row_lane) continue;  // (SOLO: the other lanes stay zero)
           const int tk = s_tok[(cb0 + cb) * 16 + (lane & 15)];
           ah[s][cb] = *reinterpret_cast<const u32x4*>(
               p.emb + ((size_t)(tk >> 4) * KSX + (ks - KSH)) * 512 + ((lane >> 4) * 16 + (tk & 15)) * 8);
@@ -205,7 +215,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row
   // (cb0+cb)*16 + (l & 15); its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows
   // 4(l>>4) .. +3)
-  if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw) {
+  if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw && row_lane) {
     const int tt = tid / (NBW * 64), cb = (tid >> 6) % NBW, l = tid & 63;
     f32x4 g = part[0][tt][cb][l];
 #pragma unroll
@@ -288,13 +298,13 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int NB, int KS, int CH, int R, bool NT = false>
+template <int NB, int KS, int CH, int R, bool NT = false, bool SOLO = false>
 __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int NCH = KS / CH;  // K = 32 * KS
   constexpr int RR = R < NCH ? R : NCH;  // chunks issued before the first MFMA
   static_assert(KS % CH == 0, "k-steps per chunk");
   constexpr int Bp = NB * 16;
-  const int nba = p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
+  const int nba = SOLO ? 1 : p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
   __shared__ unsigned long long s_best[DW][32];
   __shared__ __attribute__((aligned(16))) HzLmbCtl s_ctl[32];
@@ -334,7 +344,9 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
       const int f = f0 + wave;
       const int ks = f / (2 * NB), rem = f - ks * 2 * NB, hl = rem / NB, cb = rem - hl * NB;
       const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
-      if (cb < nba)  // (the vmcnt wait below counts only the weight chunks issued after the staging)
+      // (the vmcnt wait below counts only the weight chunks issued after the staging; SOLO: the
+      // lanes of row 0 only -- the other rows' logits are garbage nobody reads: their dec_t is -1)
+      if (cb < nba && (!SOLO || (lane & 15) == 0))
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
     }
   }
@@ -483,7 +495,8 @@ extern "C" int hz_lmb_dec_blocks(int V) {
 extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
   const HzLmbLayerParams& p = *pp;
   const bool first = p.emb != nullptr;
-  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < 0 || p.nb_act > p.Bp / 16) return -1;
+  // nb_act: 0 all row blocks, 1 the first one (low-load program), -1 request row 0 only (SOLO)
+  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < -1 || p.nb_act > p.Bp / 16) return -1;
   if (p.Kh % 32 || p.Kx % 32 || p.Kh < p.H || p.R % 16 || p.R < 4 * p.H || !p.w || !p.bias || !p.h || !p.c || !p.gpar)
     return -1;
   const int KS = (p.Kh + p.Kx) / 32;
@@ -499,23 +512,37 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
     return 3;
   }();
   const int ntile = p.R / 16;
-#define HZ_LMBL(NB, T, NBW)                                                                          \
+#define HZ_LMBL(NB, T, NBW, S)                                                                       \
   do {                                                                                               \
     const int groups = (ntile + T - 1) / T;                                                          \
     const dim3 grid(NBW == NB ? groups : 2 * ((groups + 7) / 8 * 8)), block(512);                    \
-    if (first && p.embproj) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW, true>), grid, block, 0, st, p); \
-    else if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW>), grid, block, 0, st, p); \
-    else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T, NBW>), grid, block, 0, st, p);           \
+    if (first && p.embproj) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW, true, S>), grid, block, 0, st, p); \
+    else if (first) hipLaunchKernelGGL((lmb_layer_kernel<NB, true, T, NBW, false, S>), grid, block, 0, st, p); \
+    else hipLaunchKernelGGL((lmb_layer_kernel<NB, false, T, NBW, false, S>), grid, block, 0, st, p); \
   } while (0)
-  if (p.Bp == 16) {
-    if (shape == 1) HZ_LMBL(1, 1, 1);
-    else HZ_LMBL(1, 2, 1);
+  // one tile per workgroup when the tiles fit the CUs (the last layer, R = 4000: 250 tiles): at low
+  // load a workgroup's fetch is its weight tiles plus one row block of state, so fewer tiles per
+  // CU is a shorter step
+  const bool one = ntile <= 256;
+  if (p.nb_act == -1) {
+    if (p.Bp == 16) {
+      if (one) HZ_LMBL(1, 1, 1, true);
+      else HZ_LMBL(1, 2, 1, true);
+    } else {
+      if (one) HZ_LMBL(2, 1, 2, true);
+      else HZ_LMBL(2, 2, 2, true);
+    }
+  } else if (p.Bp == 16) {
+    if (shape == 1) HZ_LMBL(1, 1, 1, false);
+    else HZ_LMBL(1, 2, 1, false);
   } else if (p.nb_act == 1) {
-    HZ_LMBL(2, 2, 2);  // low-load program: 2 tiles x the first row block (64 + 64 B per k)
+    // low-load program: the first row block (64 B of state per k)
+    if (one) HZ_LMBL(2, 1, 2, false);
+    else HZ_LMBL(2, 2, 2, false);
   } else {
-    if (shape == 1) HZ_LMBL(2, 1, 2);
-    else if (shape == 2) HZ_LMBL(2, 2, 2);
-    else HZ_LMBL(2, 3, 1);
+    if (shape == 1) HZ_LMBL(2, 1, 2, false);
+    else if (shape == 2) HZ_LMBL(2, 2, 2, false);
+    else HZ_LMBL(2, 3, 1, false);
   }
 #undef HZ_LMBL
   return (int)hipGetLastError();
@@ -538,7 +565,7 @@ static int lmb_dec_pipe() {
 
 extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   const HzLmbDecParams& p = *pp;
-  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < 0 || p.nb_act > p.Bp / 16) return -1;
+  if ((p.Bp != 16 && p.Bp != 32) || p.nb_act < -1 || p.nb_act > p.Bp / 16) return -1;
   if (p.K % 256 || p.K < 256 || p.K > DKMAX * 32 || p.Vp % 16 || p.Vp < p.V || p.n_exclude < 0 || p.n_exclude > 8)
     return -1;
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
@@ -554,21 +581,27 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
 #else
 #define HZ_LMBD_EXP(NB)
 #endif
-#define HZ_LMBD_K(NB)                               \
+#define HZ_LMBD_K(NB, S)                            \
   switch (p.K / 256) {                              \
-    case 1: HZ_LMBD(NB, 8, 8, 2); break;            \
-    case 2: HZ_LMBD(NB, 16, 8, 2); break;           \
-    case 3: HZ_LMBD(NB, 24, 8, 2); break;           \
+    case 1: HZ_LMBD(NB, 8, 8, 2, false, S); break;  \
+    case 2: HZ_LMBD(NB, 16, 8, 2, false, S); break; \
+    case 3: HZ_LMBD(NB, 24, 8, 2, false, S); break; \
     case 4:                                         \
-      HZ_LMBD_EXP(NB)                               \
-      HZ_LMBD(NB, 32, 8, 2);                        \
+      if (!S) { HZ_LMBD_EXP(NB) }                   \
+      HZ_LMBD(NB, 32, 8, 2, false, S);              \
       break;                                        \
     default: return -1;                             \
   }
-  if (p.Bp == 16) {
-    HZ_LMBD_K(1)
+  if (p.nb_act == -1) {  // the one-request program
+    if (p.Bp == 16) {
+      HZ_LMBD_K(1, true)
+    } else {
+      HZ_LMBD_K(2, true)
+    }
+  } else if (p.Bp == 16) {
+    HZ_LMBD_K(1, false)
   } else {
-    HZ_LMBD_K(2)
+    HZ_LMBD_K(2, false)
   }
 #undef HZ_LMBD_K
 #undef HZ_LMBD_EXP

@@ -13,7 +13,9 @@
 // Low load: with a second program captured for the first row block only (hz_lmb_set_lowload), a
 // replay whose busy rows are all below lo_rows runs that one instead: the same per-row arithmetic
 // (a row's tokens never depend on the program), half the state traffic and MFMAs at Bp = 32.
-// Requests take the lowest free row, so a lone request always qualifies.
+// Requests take the lowest free row, so a lone request always qualifies. One request: with the
+// programs of hz_lmb_set_solo (kernels with nb_act = -1), a replay whose only busy row is row 0
+// reads and writes that row's state alone (bitwise the same tokens).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -57,6 +59,7 @@ struct Flight {
 struct Sched {
   HzProgram prog[2] = {nullptr, nullptr};
   HzProgram lo[2] = {nullptr, nullptr};  // low-load programs (rows < lo_rows only) or null
+  HzProgram solo[2] = {nullptr, nullptr};  // one-request programs (row 0 only) or null
   int nprog = 1, lo_rows = 0;
   hipStream_t st;
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -72,7 +75,7 @@ struct Sched {
   int busy = 0;             // rows holding a request with sub-steps still to issue
   bool stop = false;
   std::thread worker;
-  unsigned long long replays = 0, served = 0, used = 0, offered = 0, lo_replays = 0;
+  unsigned long long replays = 0, served = 0, used = 0, offered = 0, lo_replays = 0, solo_replays = 0;
 
   int row_stride() const { return 8 + 4 * U; }
 
@@ -126,7 +129,7 @@ struct Sched {
     long long seq = 0, gstep = 0;
     int next_k = 0;
     for (;;) {
-      bool launch = false, low = false;
+      bool launch = false, low = false, one = false;
       {
         std::unique_lock<std::mutex> lk(mu);
         if (inflight.empty() && busy == 0) {
@@ -159,15 +162,18 @@ struct Sched {
           launch = busy > 0;
           low = launch && lo[next_k] != nullptr;
           for (int r = lo_rows; low && r < Bp; ++r) low = rows[r] == nullptr;
+          one = launch && solo[next_k] != nullptr && rows[0] != nullptr;
+          for (int r = 1; one && r < Bp; ++r) one = rows[r] == nullptr;
         }
       }
       if (launch) {
         const int k = next_k;
         write_block(k, gstep, admitted);
-        int rc = hz_prog_replay(low ? lo[k] : prog[k], st);
+        int rc = hz_prog_replay(one ? solo[k] : low ? lo[k] : prog[k], st);
         if (!rc) rc = (int)hipEventRecord(ev[k], st);
         std::lock_guard<std::mutex> g(mu);
-        lo_replays += low;
+        lo_replays += low && !one;
+        solo_replays += one;
         ++replays;
         offered += (unsigned long long)Bp * U;
         for (int r = 0; r < Bp; ++r) {
@@ -306,6 +312,22 @@ int hz_lmb_set_lowload(void* h, const HzProgram* lo, int rows) {
   for (int k = 0; k < s->nprog; ++k) s->lo[k] = lo ? lo[k] : nullptr;
   s->lo_rows = lo ? rows : 0;
   return 0;
+}
+
+// optional one-request programs over the same buffers (kernels with nb_act = -1), one per
+// program of hz_lmb_create; call before the first submit
+int hz_lmb_set_solo(void* h, const HzProgram* solo) {
+  auto* s = static_cast<Sched*>(h);
+  if (!s) return -1;
+  std::lock_guard<std::mutex> g(s->mu);
+  for (int k = 0; k < s->nprog; ++k) s->solo[k] = solo ? solo[k] : nullptr;
+  return 0;
+}
+
+unsigned long long hz_lmb_solo_replays(void* h) {
+  auto* s = static_cast<Sched*>(h);
+  std::lock_guard<std::mutex> g(s->mu);
+  return s->solo_replays;
 }
 
 unsigned long long hz_lmb_lo_replays(void* h) {

@@ -209,7 +209,7 @@ class LMBatchEngine:
 
     def __init__(self, packed: dict, device="cuda:0", rows: int = 32, unroll: int = 8, exclude_ids=(),
                  max_words: int = 1024, record_logits: bool = False, capture: bool = True,
-                 lowload: bool | None = None, embproj: bool | None = None):
+                 lowload: bool | None = None, embproj: bool | None = None, solo: bool | None = None):
         self.p = packed
         self.device = torch.device(device)
         self.V = packed["V"]
@@ -222,7 +222,7 @@ class LMBatchEngine:
             self.core = lmcore.LmbCore(geometry_of(packed), w, self._alloc, self.stream.cuda_stream, rows=rows,
                                        unroll=unroll, exclude_ids=exclude_ids, max_words=max_words,
                                        record_logits=record_logits, capture=capture, lowload=lowload,
-                                       embproj=embproj)
+                                       embproj=embproj, solo=solo)
             torch.cuda.synchronize(self.device)
         self.rows, self.unroll, self.max_words = rows, unroll, max_words
         self._ops = self.core._ops

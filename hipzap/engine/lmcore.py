@@ -160,7 +160,7 @@ class LmbCore:
     def __init__(self, geo: LmbGeometry, w: dict, alloc, stream: int, rows: int = 32, unroll: int = 8,
                  exclude_ids=(), max_words: int = 1024, record_logits: bool = False, capture: bool = True,
                  lowload: bool | None = None, pipeline: bool | None = None, embproj: bool | None = None,
-                 lib=None):
+                 solo: bool | None = None, lib=None):
         if rows not in (16, 32):
             raise ValueError("rows must be 16 or 32")
         if not 1 <= unroll <= 32:
@@ -168,6 +168,8 @@ class LmbCore:
         lib = lib or N.lib()
         if lowload is None:
             lowload = os.environ.get("HIPZAP_LM_LOWLOAD", "1") != "0"
+        if solo is None:
+            solo = os.environ.get("HIPZAP_LM_SOLO", "1") != "0"
         self.lib, self.geo = lib, geo
         self.rows, self.unroll, self.max_words, self.V = rows, unroll, max_words, geo.V
         Bp, U, L = rows, unroll, geo.layers
@@ -252,6 +254,9 @@ class LmbCore:
         # low load (HIPZAP_LM_LOWLOAD, default on at 32 rows): programs over the first 16 rows,
         # replayed while every busy row is below 16 (csrc/lmserve.cpp)
         self.progs_lo = [build(1, k) for k in range(self.nprog)] if lowload and Bp > 16 else []
+        # one request (HIPZAP_LM_SOLO, default on): programs that read and write row 0's state only,
+        # replayed while row 0 is the only busy row (a lone request always sits in row 0)
+        self.progs_solo = [build(-1, k) for k in range(self.nprog)] if solo else []
         P2 = C.c_void_p * 2
         lg = P2(*(self.logits_bufs + [0] * (2 - len(self.logits_bufs)))) if self.logits_bufs else None
         self._sched = lib.hz_lmb_create(P2(*(self.progs + [0] * (2 - self.nprog))), self.nprog, stream,
@@ -262,6 +267,9 @@ class LmbCore:
         if self.progs_lo:
             N.check(lib.hz_lmb_set_lowload(self._sched, P2(*(self.progs_lo + [0] * (2 - self.nprog))), 16),
                     "hz_lmb_set_lowload")
+        if self.progs_solo:
+            N.check(lib.hz_lmb_set_solo(self._sched, P2(*(self.progs_solo + [0] * (2 - self.nprog)))),
+                    "hz_lmb_set_solo")
         self.last_latency_ms = None
 
     def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
@@ -290,14 +298,16 @@ class LmbCore:
         self.lib.hz_lmb_stats(self._sched, a)
         return {"replays": a[0], "served": a[1], "row_steps_used": a[2], "row_steps": a[3],
                 "row_utilisation": round(a[2] / a[3], 4) if a[3] else None,
-                "lowload_replays": int(self.lib.hz_lmb_lo_replays(self._sched))}
+                "lowload_replays": int(self.lib.hz_lmb_lo_replays(self._sched)),
+                "solo_replays": int(self.lib.hz_lmb_solo_replays(self._sched))}
 
     def close(self) -> None:
         s, self._sched = getattr(self, "_sched", None), None
         if s:
             self.lib.hz_lmb_destroy(s)
-        progs = list(getattr(self, "progs", []) or []) + list(getattr(self, "progs_lo", []) or [])
-        self.progs, self.progs_lo, self.prog = [], [], None
+        progs = (list(getattr(self, "progs", []) or []) + list(getattr(self, "progs_lo", []) or []) +
+                 list(getattr(self, "progs_solo", []) or []))
+        self.progs, self.progs_lo, self.progs_solo, self.prog = [], [], [], None
         for prog in progs:
             if prog:
                 self.lib.hz_prog_destroy(prog)

@@ -119,8 +119,10 @@ def test_lowload_program_is_bitwise_the_full_one(model):
     """A lone request (every busy row below 16) replays the 16-row program (csrc/lmserve.cpp
     low load); its tokens and logits are bitwise those of the full 32-row program."""
     pk = pack_lmb(model.state_dict(), DEV)
-    full = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=False)
-    low = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=True)
+    full = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=False,
+                         solo=False)
+    low = LMBatchEngine(pk, DEV, rows=32, unroll=8, exclude_ids=[2], record_logits=True, lowload=True,
+                        solo=False)
     try:
         for seed, (ids, n) in enumerate([([4, 7], 30), ([9] * 9, 17), ([123], 1)]):
             a, la = full.run_tokens(ids, n, seed=seed, logits=True)
@@ -130,6 +132,45 @@ def test_lowload_program_is_bitwise_the_full_one(model):
     finally:
         full.close()
         low.close()
+
+
+@pytest.mark.parametrize("rows", [16, 32])
+def test_one_request_program_is_bitwise_the_full_one(model, rows):
+    """A lone request (row 0 the only busy row) replays the one-request program (nb_act = -1:
+    the kernels read and write row 0's state only); its tokens and logits are bitwise those of
+    the full program, and requests that join while it runs switch programs without a change."""
+    pk = pack_lmb(model.state_dict(), DEV)
+    full = LMBatchEngine(pk, DEV, rows=rows, unroll=8, exclude_ids=[2], record_logits=True, lowload=False,
+                         solo=False)
+    one = LMBatchEngine(pk, DEV, rows=rows, unroll=8, exclude_ids=[2], record_logits=True, solo=True)
+    try:
+        for seed, (ids, n) in enumerate([([4, 7], 30), ([9] * 9, 17), ([123], 1)]):
+            a, la = full.run_tokens(ids, n, seed=seed, logits=True)
+            b, lb = one.run_tokens(ids, n, seed=seed, logits=True)
+            assert a == b and torch.equal(la, lb)
+        assert one.stats()["solo_replays"] > 0 and full.stats()["solo_replays"] == 0
+        # a long request alone, then others joining (and leaving) while it runs
+        jobs = [([5, 6], 120, 100)] + [([int(3 + i)], 20 + 3 * i, 200 + i) for i in range(6)]
+        ref = [full.run_tokens(p, n, seed=s) for p, n, s in jobs]
+        out = [None] * len(jobs)
+
+        def go(i):
+            p, n, s = jobs[i]
+            out[i] = one.run_tokens(p, n, seed=s)
+
+        th = [threading.Thread(target=go, args=(0,))]
+        th[0].start()
+        import time
+        time.sleep(0.002)
+        th += [threading.Thread(target=go, args=(i,)) for i in range(1, len(jobs))]
+        for t in th[1:]:
+            t.start()
+        for t in th:
+            t.join()
+        assert out == ref
+    finally:
+        full.close()
+        one.close()
 
 
 def test_projected_embedding_matches_the_fused_first_layer(model):
