@@ -77,6 +77,16 @@ def _geom(pc, cin, cout, k, stride, pad) -> bool:
             and pc.pad == pad)
 
 
+def _internal_only(g, grp) -> bool:
+    """The fused kernel writes only the run's last output: every other output of the run must be
+    read inside the run alone (and not be a graph output)."""
+    inner = {t for n in grp[:-1] for t in n.outputs}
+    if inner & set(g.outputs):
+        return False
+    ids = {id(n) for n in grp}
+    return not any(t in inner for n in g.nodes if id(n) not in ids for t in n.inputs)
+
+
 def match_stem(g, params, i: int) -> Fused | None:
     nodes = g.nodes
     if i + 3 > len(nodes):
@@ -98,7 +108,7 @@ def match_stem(g, params, i: int) -> Fused | None:
             return None
     elif src.dtype != torch.float32 or src.shape[1] != 3:
         return None
-    return Fused("stem", i, i + 3, [pre, cv, mp])
+    return Fused("stem", i, i + 3, [pre, cv, mp]) if _internal_only(g, [pre, cv, mp]) else None
 
 
 def match_convpool(g, params, i: int) -> Fused | None:
@@ -115,7 +125,7 @@ def match_convpool(g, params, i: int) -> Fused | None:
         return None
     if len(cv.inputs) != 1 or g.shape(cv.inputs[0])[-1] != 8:
         return None
-    return Fused("convpool", i, i + 2, [cv, mp])
+    return Fused("convpool", i, i + 2, [cv, mp]) if _internal_only(g, [cv, mp]) else None
 
 
 def match_bneck(g, params, i: int, layer2: bool = False) -> Fused | None:
@@ -137,6 +147,8 @@ def match_bneck(g, params, i: int, layer2: bool = False) -> Fused | None:
     if c3.inputs != [c2.outputs[0], res]:
         return None
     grp = [n for n in (ds, c1, c2, c3) if n is not None]
+    if not _internal_only(g, grp):
+        return None
     if len({n.slot for n in grp}) != 1 or any(n.attrs.get("out_f32") or n.attrs.get("rowmajor") for n in grp):
         return None
     if any(n.attrs.get("act", "relu") != "relu" for n in (c1, c2, c3)):

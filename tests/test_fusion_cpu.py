@@ -128,3 +128,17 @@ def test_launchers_refuse_malformed_params_before_any_hip_call():
     assert stem(SH=111) == -1 and stem(PH=55) == -1
     assert stem(mode=3) == -1
     assert stem(src=fake + 2) == -1                 # uint8 rows are read as dwords
+
+
+def test_a_run_whose_intermediate_is_read_elsewhere_is_not_fused(r50):
+    """The fused kernels write only the run's last output: a block whose conv2 output is also a
+    graph output (a debugging tap) stays per-conv, the other blocks still fuse."""
+    a, params, kw = r50
+    g = a.build_graph(batch=1, input_uint8=True)
+    fz = fusion.plan(g, params, fusion.enabled_kinds("all"))
+    b2 = [f for f in fz.values() if f.kind == "bneck2"]
+    tap = b2[1].nodes[1].outputs[0]  # conv2 of the second layer2 block
+    g.outputs.append(tap)
+    fz2 = fusion.plan(g, params, fusion.enabled_kinds("all"))
+    assert [f.kind for f in fz2.values()].count("bneck2") == 3
+    assert b2[1].start not in fz2
