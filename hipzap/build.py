@@ -203,6 +203,10 @@ if __name__ == "__main__":
         sys.exit(0)
     build(verbose=True, debug="--debug" in sys.argv[1:])
     if "--debug" not in sys.argv[1:]:
+        # an in-tree debug library is loaded by the GPU tests (HIPZAP_DEBUG=1): keep it on the
+        # same sources as the product one (a stale one misses new entry points)
+        if LIB_DEBUG.exists():
+            build(verbose=True, debug=True)
         build_comm(verbose=True)
         build_tools(verbose=True)
         build_templates(verbose=True)
