@@ -201,6 +201,8 @@ def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
     ckpt, plan = prepare_artifacts(args.model, args.ckpt_dir)
     res = {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index)}
     try:  # the node: N torch-free workers, RCCL rendezvous, C1 weight broadcast, first logits on every rank
+        if world > torch.cuda.device_count():  # (a shared-GPU rehearsal: one RCCL rank per GPU only)
+            raise RuntimeError(f"{world} workers need {world} visible GPUs, {torch.cuda.device_count()} visible")
         res["node"] = measure_node(plan, world, trials=max(3, min(5, args.cold_trials)), timeout=120)
     except Exception as e:  # noqa: BLE001 - secondary to the one-GPU figure
         print(f"node cold start skipped: {e}", file=sys.stderr)

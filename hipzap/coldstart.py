@@ -109,6 +109,8 @@ def run_node(plan: str, rank: int, world: int, rdzv_dir: str, device: int, timeo
     from hipzap.parallel.rccl import FileRendezvous
     rdzv = FileRendezvous(rdzv_dir)
     if dry:
+        if os.environ.get("HIPZAP_COLD_FAIL_RANK") == str(rank):  # tests: a worker that dies early
+            raise SystemExit(3)
         rdzv.publish(f"arrived{rank}", b"1")
         for r in range(world):
             rdzv.wait(f"arrived{r}", timeout=timeout_s)
@@ -168,13 +170,28 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
             procs.append(subprocess.Popen(cmd, cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                           text=True))
         outs, err = [], None
-        for r, p in enumerate(procs):
-            try:
-                so, se = p.communicate(timeout=timeout)
-            except subprocess.TimeoutExpired:
+        # a worker that fails (e.g. its device is not visible) leaves the others blocked in the
+        # RCCL rendezvous: stop the launch as soon as any worker exits non-zero, not at the timeout
+        deadline = time.time() + timeout
+        while True:
+            rcs = [p.poll() for p in procs]
+            if all(rc is not None for rc in rcs):
+                break
+            bad = [r for r, rc in enumerate(rcs) if rc not in (None, 0)]
+            if bad or time.time() > deadline:
                 for q in procs:
                     q.kill()
+                for q in procs:
+                    q.wait()
+                shutil.rmtree(rdzv, ignore_errors=True)
+                if bad:
+                    se = procs[bad[0]].stderr.read()
+                    raise RuntimeError(f"node cold start: rank {bad[0]} exited {rcs[bad[0]]}: {se[-1500:]}")
+                r = next(r for r, rc in enumerate(rcs) if rc is None)
                 raise RuntimeError(f"node cold start: rank {r} did not finish within {timeout:.0f} s")
+            time.sleep(0.01)
+        for r, p in enumerate(procs):
+            so, se = p.communicate()
             lines = [ln for ln in so.splitlines() if ln.startswith("{")]
             if p.returncode != 0 or not lines:
                 err = err or f"rank {r} rc={p.returncode}: {se[-2000:]}"

@@ -20,3 +20,16 @@ def test_node_cold_start_fails_loudly_on_a_bad_rank():
     # not dry: every worker tries to open a plan that does not exist
     with pytest.raises(RuntimeError, match="node cold start"):
         measure_node("/nonexistent.hzplan", 2, trials=1, dry=False, timeout=120)
+
+
+def test_a_dead_worker_stops_the_launch_at_once():
+    """A worker that exits early leaves the others waiting in the rendezvous: the launcher stops
+    the launch when it sees the exit, not at its timeout (on a real node: a rank whose device is
+    not visible)."""
+    import os
+    import time
+    t = time.time()
+    with pytest.raises(RuntimeError, match="rank 1 exited 3"):
+        measure_node("/nonexistent.hzplan", 3, trials=1, dry=True, timeout=120,
+                     env=dict(os.environ, HIPZAP_COLD_FAIL_RANK="1"))
+    assert time.time() - t < 30
