@@ -316,20 +316,28 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   const int ntile = p.Vp >> 4;
   const int t_lo = (int)((long)blk * ntile / p.nblk), t_hi = (int)((long)(blk + 1) * ntile / p.nblk);
   const int tile0 = t_lo + wave * 2;
-  const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
-  const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
+  // A workgroup owns 14-15 tiles (3750 over 256 at V = 60000) but its 8 waves have 16 tile slots:
+  // a slot past t_hi loads through a range-checked buffer descriptor at an out-of-range offset --
+  // no memory traffic, zeros in the registers, and the load still counts in vmcnt, so the counted
+  // waits below hold for every wave (these slots used to re-read the next workgroup's tiles: 8 %
+  // of the decoder's bytes)
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long)ntile * KS * 1024), 0x00020000);
+  constexpr int kOOB = 0x7ff00000;  // > every descriptor's size (the launcher bounds it)
+  const int woff0 = (tile0 < t_hi ? tile0 * KS * 1024 : kOOB) + lane * 16;
+  const int woff1 = (tile0 + 1 < t_hi ? (tile0 + 1) * KS * 1024 : kOOB) + lane * 16;
   u32x4 wa[RR][CH], wb[RR][CH];
   auto issue = [&](int slot, int c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
-      const u32x4* a = reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512);
-      const u32x4* b = reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512);
       if constexpr (NT) {  // non-temporal weight stream (MI355X_MICROARCH.md "nt-weights")
-        wa[slot][s] = __builtin_nontemporal_load(a);
-        wb[slot][s] = __builtin_nontemporal_load(b);
+        const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
+        const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
+        wa[slot][s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512));
+        wb[slot][s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512));
       } else {
-        wa[slot][s] = *a;
-        wb[slot][s] = *b;
+        wa[slot][s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff0 + (c * CH + s) * 1024, 0, 0));
+        wb[slot][s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff1 + (c * CH + s) * 1024, 0, 0));
       }
     }
   };
@@ -569,6 +577,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if (p.K % 256 || p.K < 256 || p.K > DKMAX * 32 || p.Vp % 16 || p.Vp < p.V || p.n_exclude < 0 || p.n_exclude > 8)
     return -1;
   if (!p.w || !p.h || !p.gpar || !p.ctl || !p.seed || !p.dbest || p.nblk != hz_lmb_dec_blocks(p.V)) return -1;
+  if ((long)p.Vp * p.K * 2 > 0x70000000L) return -1;  // the weight descriptor's 32-bit range (see the kernel)
   const dim3 grid(p.nblk), block(512);
   const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
   (void)pipe;
