@@ -112,12 +112,15 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       best1 = p.dbest[Bp + tid];
     }
   }
+  const auto kcl = [&](int s) { return min(k0 + min(s, max(cnt - 1, 0)), KSE - 1); };
   u32x4 wf[TPW][SPW];
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt) {
     const bf16_t* wt = p.w + (size_t)min(tile0 + tt, ntile - 1) * KS * 512 + lane * 8;
 #pragma unroll
-    for (int s = 0; s < SPW; ++s) wf[tt][s] = *reinterpret_cast<const u32x4*>(wt + (size_t)min(k0 + s, KSE - 1) * 512);
+    for (int s = 0; s < SPW; ++s)  // (slots past this wave's cnt re-load its own last k-step, not the
+                                   // next wave's: straight-line loads keep the counted vmcnt waits)
+      wf[tt][s] = *reinterpret_cast<const u32x4*>(wt + (size_t)kcl(s) * 512);
   }
   __builtin_amdgcn_sched_barrier(0);
   const int par = (*p.gpar + p.step_off) & 1;
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   u32x4 ah[SPW][NBW], al[SPW][NBW];
 #pragma unroll
   for (int s = 0; s < SPW; ++s) {
-    const int ks = min(k0 + s, KSE - 1);
+    const int ks = kcl(s);
     // FIRST: k-steps past Kh are the embedding, loaded after the token selection (a harmless
     // in-range h fragment here keeps the loop branch-free)
     const bool hk = FIRST || ks < KSH;
