@@ -1,5 +1,5 @@
 #!/bin/bash
-# r4: decoder weight slots past a workgroup's tiles dropped by the buffer range check (they used
+# r4: LM decoder OOB slots + layer k-step clamp: LM tests, decode bench 1 / 32 / 64 clients x 2, profile
 # to re-read the next workgroup's tiles): LM tests, decode bench 1 / 32 / 64 clients x 2, profile
 set -u
 cd "$GRAFT_REPO_ROOT"
