@@ -28,7 +28,7 @@ namespace {
 
 constexpr int LW = 8;      // waves per layer workgroup (K split over them)
 constexpr int SPW = 9;     // k-steps (of 32) per wave: K <= 8 * 9 * 32 = 2304
-constexpr int DW = 8;      // decoder waves; 2 vocabulary tiles (32 rows) each
+constexpr int DW = 8;      // decoder tile slots per workgroup / 2 (8 waves x 2 tiles or 4 x 4)
 constexpr int DROWS = DW * 32;  // vocabulary rows per decoder workgroup
 constexpr int DKMAX = 32;  // decoder k-steps (K <= 1024, a multiple of 256)
 
@@ -301,57 +301,66 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int NB, int KS, int CH, int R, bool NT = false, bool SOLO = false>
-__global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
+// TW vocabulary tiles per wave, 16 / TW waves per workgroup (the 16 tile slots of a workgroup
+// either way): every wave reads each state fragment from LDS once per k-step, so TW = 4 halves
+// the LDS reads per tile of TW = 2 (128 KiB of ds_read_b128 per wave at Bp 32) with half the waves
+template <int NB, int KS, int CH, int R, bool NT = false, bool SOLO = false, int TW = 2>
+__global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int NCH = KS / CH;  // K = 32 * KS
   constexpr int RR = R < NCH ? R : NCH;  // chunks issued before the first MFMA
+  constexpr int NW = 16 / TW;            // waves
   static_assert(KS % CH == 0, "k-steps per chunk");
+  static_assert(TW == 2 || TW == 4, "tiles per wave");
+  static_assert((RR - 1) * TW * CH < 64, "vmcnt range");
   constexpr int Bp = NB * 16;
   const int nba = SOLO ? 1 : p.nb_act > 0 ? p.nb_act : NB;  // row blocks computed (wave-uniform)
   __shared__ __attribute__((aligned(16))) bf16_t act[KS * 2 * NB * 512];  // [KS][2 hi/lo][NB][512]: 128 KiB at Bp 32, K 1024
-  __shared__ unsigned long long s_best[DW][32];
+  __shared__ unsigned long long s_best[NW][32];
   __shared__ __attribute__((aligned(16))) HzLmbCtl s_ctl[32];
   __shared__ __attribute__((aligned(16))) unsigned long long s_seed[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int blk = blockIdx.x;
   if (!HZ_DCHECK(p.K == KS * 32 && p.Bp == Bp)) return;
-  // this workgroup's vocabulary tiles [t_lo, t_hi) (<= 16: 2 per wave)
+  // this workgroup's vocabulary tiles [t_lo, t_hi) (<= 16: TW per wave)
   const int ntile = p.Vp >> 4;
   const int t_lo = (int)((long)blk * ntile / p.nblk), t_hi = (int)((long)(blk + 1) * ntile / p.nblk);
-  const int tile0 = t_lo + wave * 2;
-  // A workgroup owns 14-15 tiles (3750 over 256 at V = 60000) but its 8 waves have 16 tile slots:
-  // a slot past t_hi loads through a range-checked buffer descriptor at an out-of-range offset --
-  // no memory traffic, zeros in the registers, and the load still counts in vmcnt, so the counted
-  // waits below hold for every wave (these slots used to re-read the next workgroup's tiles: 8 %
-  // of the decoder's bytes)
+  const int tile0 = t_lo + wave * TW;
+  // A workgroup owns 14-15 tiles (3750 over 256 at V = 60000) but has 16 tile slots: a slot past
+  // t_hi loads through a range-checked buffer descriptor at an out-of-range offset -- no memory
+  // traffic, zeros in the registers, and the load still counts in vmcnt, so the counted waits
+  // below hold for every wave (these slots used to re-read the next workgroup's tiles: 8 % of
+  // the decoder's bytes)
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long)ntile * KS * 1024), 0x00020000);
   constexpr int kOOB = 0x7ff00000;  // > every descriptor's size (the launcher bounds it)
-  const int woff0 = (tile0 < t_hi ? tile0 * KS * 1024 : kOOB) + lane * 16;
-  const int woff1 = (tile0 + 1 < t_hi ? (tile0 + 1) * KS * 1024 : kOOB) + lane * 16;
-  u32x4 wa[RR][CH], wb[RR][CH];
+  int woff[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) woff[t] = (tile0 + t < t_hi ? (tile0 + t) * KS * 1024 : kOOB) + lane * 16;
+  u32x4 wr[TW][RR][CH];
   auto issue = [&](int slot, int c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
-      if constexpr (NT) {  // non-temporal weight stream (MI355X_MICROARCH.md "nt-weights")
-        const bf16_t* wt0 = p.w + (size_t)min(tile0, ntile - 1) * KS * 512 + lane * 8;
-        const bf16_t* wt1 = p.w + (size_t)min(tile0 + 1, ntile - 1) * KS * 512 + lane * 8;
-        wa[slot][s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wt0 + (size_t)(c * CH + s) * 512));
-        wb[slot][s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wt1 + (size_t)(c * CH + s) * 512));
-      } else {
-        wa[slot][s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff0 + (c * CH + s) * 1024, 0, 0));
-        wb[slot][s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff1 + (c * CH + s) * 1024, 0, 0));
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        if constexpr (NT) {  // non-temporal weight stream (MI355X_MICROARCH.md "nt-weights")
+          const bf16_t* wt = p.w + (size_t)min(tile0 + t, ntile - 1) * KS * 512 + lane * 8;
+          wr[t][slot][s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wt + (size_t)(c * CH + s) * 512));
+        } else {
+          wr[t][slot][s] =
+              __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, woff[t] + (c * CH + s) * 1024, 0, 0));
+        }
       }
     }
   };
   issue(0, 0);
   const int par = (*p.gpar + p.step_off) & 1;
-  // stage the state: KS * 2 * NB fragments of 1 KiB, wave w takes fragments w, w + 8, ...
+  // stage the state: KS * 2 * NB fragments of 1 KiB, wave w takes fragments w, w + NW, ...
   {
     const bf16_t* src = p.h + (size_t)((par ^ 1) * 2) * KS * NB * 512;  // this step's output of the last layer
     constexpr int NFRAG = KS * 2 * NB;
+    static_assert(NFRAG % NW == 0, "state fragments per wave");
 #pragma unroll
-    for (int f0 = 0; f0 < NFRAG; f0 += DW) {
+    for (int f0 = 0; f0 < NFRAG; f0 += NW) {
       const int f = f0 + wave;
       const int ks = f / (2 * NB), rem = f - ks * 2 * NB, hl = rem / NB, cb = rem - hl * NB;
       const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
@@ -363,7 +372,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   }
   // the rows' control and seeds go to LDS the same way (an ordinary load here would make hipcc
   // wait for vmcnt(0) at its first use while the global_load_lds are in flight)
-  if (wave == DW - 1) {
+  if (wave == NW - 1) {
     if (lane < Bp)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p.ctl + p.step_off * Bp + lane), (lds_void*)s_ctl,
                                        16, 0, 0);
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   __builtin_amdgcn_sched_barrier(0);
   // the staged state is complete once everything issued before chunk 1 has landed (every wave);
   // chunks 1 .. RR - 1 keep streaming across the barrier
-  wait_vmcnt<(RR - 1) * 2 * CH>();
+  wait_vmcnt<(RR - 1) * TW * CH>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   // the Gumbel noise of this wave's rows does not depend on the logits: compute it (VALU) while
@@ -383,7 +392,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   // vmcnt(0) at the first use of the control loads)
   int dt[NB];
   bool rec[NB];
-  f32x4 gn[2][NB];
+  f32x4 gn[TW][NB];
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb) {
     const int r = cb * 16 + (lane & 15);
@@ -392,12 +401,12 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     rec[cb] = cl.rec != 0;
     const unsigned long long sd = s_seed[r];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TW; ++t)
       gn[t][cb] = dt[cb] >= 0 ? gumbel4(sd, dt[cb], (tile0 + t) * 16 + (lane >> 4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  f32x4 acc[2][NB];
+  f32x4 acc[TW][NB];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TW; ++t)
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -411,10 +420,11 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
         if (cb >= nba) continue;
         const bf16x8 hi = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 0) * NB + cb) * 512 + lane * 8));
         const bf16x8 lo = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 1) * NB + cb) * 512 + lane * 8));
-        acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wa[cur][s]), hi, acc[0][cb], 0, 0, 0);
-        acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wa[cur][s]), lo, acc[0][cb], 0, 0, 0);
-        acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wb[cur][s]), hi, acc[1][cb], 0, 0, 0);
-        acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wb[cur][s]), lo, acc[1][cb], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wr[t][cur][s]), hi, acc[t][cb], 0, 0, 0);
+          acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wr[t][cur][s]), lo, acc[t][cb], 0, 0, 0);
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // chunk c's MFMAs are done with its registers
@@ -429,7 +439,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
     const int r = cb * 16 + (lane & 15);
     unsigned long long b = 0;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TW; ++t) {
       const int v0 = (tile0 + t) * 16 + (lane >> 4) * 4;
       if (cb >= nba || tile0 + t >= t_hi || v0 >= p.V) continue;
       f32x4 lg = acc[t][cb];
@@ -459,7 +469,7 @@ __global__ __launch_bounds__(512) void lmb_dec_kernel(const HzLmbDecParams p) {
   if (tid < Bp) {  // this workgroup's best per request row -> the row's running maximum
     unsigned long long b = s_best[0][tid];
 #pragma unroll
-    for (int w = 1; w < DW; ++w) b = umax64(b, s_best[w][tid]);
+    for (int w = 1; w < NW; ++w) b = umax64(b, s_best[w][tid]);
     if (b) atomicMax(p.dbest + (size_t)par * Bp + tid, b);
   }
 }
@@ -562,6 +572,15 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
 // decoder weight pipeline: HIPZAP_LMB_DEC_PIPE = "8x2" (default: 8 k-steps per chunk, 2 chunks in
 // the ring); experiments build only (measured negatives, profiles/r4_lmb): "4x5" or "4x6" (K = 1024)
 // and "8x2nt" (the default ring with non-temporal weight loads)
+// HIPZAP_LMB_DEC_TW = 4: four vocabulary tiles per wave, four waves (K = 1024), default 2
+static int lmb_dec_tw() {
+  static const int v = [] {
+    const char* e = getenv("HIPZAP_LMB_DEC_TW");
+    return e && !strcmp(e, "4") ? 4 : 2;
+  }();
+  return v;
+}
+
 static int lmb_dec_pipe() {
   static const int v = [] {
     const char* e = getenv("HIPZAP_LMB_DEC_PIPE");
@@ -583,6 +602,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if ((long)p.Vp * p.K * 2 > 0x70000000L) return -1;  // the weight descriptor's 32-bit range (see the kernel)
   const dim3 grid(p.nblk), block(512);
   const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
+  const int tw = lmb_dec_tw();
   (void)pipe;
 #define HZ_LMBD(NB, KS, CH, R, ...) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R, ##__VA_ARGS__>), grid, block, 0, st, p)
 #if HZ_EXPERIMENTS  // measured negatives (profiles/r4_lmb): deeper rings, non-temporal weight loads
@@ -600,6 +620,10 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
     case 3: HZ_LMBD(NB, 24, 8, 2, false, S); break; \
     case 4:                                         \
       if (!S) { HZ_LMBD_EXP(NB) }                   \
+      if (tw == 4) {                                \
+        hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 4, 2, false, S, 4>), grid, dim3(256), 0, st, p); \
+        break;                                      \
+      }                                             \
       HZ_LMBD(NB, 32, 8, 2, false, S);              \
       break;                                        \
     default: return -1;                             \
