@@ -572,7 +572,8 @@ extern "C" int hz_lmb_layer_launch(const HzLmbLayerParams* pp, hipStream_t st) {
 // decoder weight pipeline: HIPZAP_LMB_DEC_PIPE = "8x2" (default: 8 k-steps per chunk, 2 chunks in
 // the ring); experiments build only (measured negatives, profiles/r4_lmb): "4x5" or "4x6" (K = 1024)
 // and "8x2nt" (the default ring with non-temporal weight loads)
-// HIPZAP_LMB_DEC_TW = 4: four vocabulary tiles per wave, four waves (K = 1024), default 2
+// HIPZAP_LMB_DEC_TW = 4 (experiments build, measured slower: profiles/r4_lmb): four vocabulary
+// tiles per wave, four waves (K = 1024); default 2
 static int lmb_dec_tw() {
   static const int v = [] {
     const char* e = getenv("HIPZAP_LMB_DEC_TW");
@@ -604,14 +605,22 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   const int pipe = p.K == 1024 ? lmb_dec_pipe() : 0;
   const int tw = lmb_dec_tw();
   (void)pipe;
+  (void)tw;
 #define HZ_LMBD(NB, KS, CH, R, ...) hipLaunchKernelGGL((lmb_dec_kernel<NB, KS, CH, R, ##__VA_ARGS__>), grid, block, 0, st, p)
 #if HZ_EXPERIMENTS  // measured negatives (profiles/r4_lmb): deeper rings, non-temporal weight loads
 #define HZ_LMBD_EXP(NB)                                                   \
   if (pipe == 1) { HZ_LMBD(NB, 32, 4, 5); break; }                         \
   if (pipe == 2) { HZ_LMBD(NB, 32, 4, 6); break; }                         \
   if (pipe == 3) { HZ_LMBD(NB, 32, 8, 2, true); break; }
+// four tiles per wave, four waves: +5 us per step (fewer waves hide less of the weight stream)
+#define HZ_LMBD_TW4(NB, S)                                                                          \
+  if (tw == 4) {                                                                                   \
+    hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 4, 2, false, S, 4>), grid, dim3(256), 0, st, p);    \
+    break;                                                                                         \
+  }
 #else
 #define HZ_LMBD_EXP(NB)
+#define HZ_LMBD_TW4(NB, S)
 #endif
 #define HZ_LMBD_K(NB, S)                            \
   switch (p.K / 256) {                              \
@@ -620,10 +629,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
     case 3: HZ_LMBD(NB, 24, 8, 2, false, S); break; \
     case 4:                                         \
       if (!S) { HZ_LMBD_EXP(NB) }                   \
-      if (tw == 4) {                                \
-        hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 4, 2, false, S, 4>), grid, dim3(256), 0, st, p); \
-        break;                                      \
-      }                                             \
+      HZ_LMBD_TW4(NB, S)                            \
       HZ_LMBD(NB, 32, 8, 2, false, S);              \
       break;                                        \
     default: return -1;                             \
@@ -641,6 +647,7 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   }
 #undef HZ_LMBD_K
 #undef HZ_LMBD_EXP
+#undef HZ_LMBD_TW4
 #undef HZ_LMBD
   return (int)hipGetLastError();
 }
