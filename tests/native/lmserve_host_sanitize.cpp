@@ -1,6 +1,6 @@
 // Host-side sanitizer check of the batched-decode scheduler (csrc/lmserve.cpp): continuous
 // batching, the pipelined pair of programs (host blocks written while the other replay runs,
-// alternating per-row output slots), the low-load program switch and teardown, under
+// alternating per-row output slots), the low-load and one-request program switches and teardown, under
 // AddressSanitizer+UBSan or ThreadSanitizer (tests/test_native_asan_cpu.py builds it both ways).
 //
 // No GPU: hz_prog_replay and the HIP event calls are defined here. A fake "GPU" thread executes the
@@ -34,6 +34,7 @@ struct FakeProg {
   float* logits;  // [Bp][kV] or null
   int Bp, U;
   bool low;
+  bool solo = false;
 };
 
 struct FakeEvent {
@@ -92,6 +93,10 @@ struct FakeGpu {
           fprintf(stderr, "low-load replay with a busy row %d\n", r);
           abort();
         }
+        if (p->solo && r != 0) {  // the one-request program computes row 0 only
+          fprintf(stderr, "one-request replay with a busy row %d\n", r);
+          abort();
+        }
         if (c[u].tok == -1 && c[u].out >= 0) outp[c[u].out] = (int)((seed * 2654435761ull + c[u].out * 97ull) % 100003ull);
         if (c[u].rec && p->logits)
           for (int v = 0; v < kV; ++v) p->logits[(size_t)r * kV + v] = (float)((seed + v) % 1009);
@@ -145,20 +150,22 @@ hipError_t hipEventDestroy(hipEvent_t ev) {
     }                                                              \
   } while (0)
 
-static int run_mode(int nprog, bool lowload, int clients, int iters) {
+static int run_mode(int nprog, bool lowload, int clients, int iters, bool solo = false) {
   const int Bp = 32, U = 4, maxn = 64;
   std::vector<std::vector<int>> blocks(2, std::vector<int>(8 + Bp * (8 + 4 * U), 0));
   std::vector<int> out_pool(2 * Bp * maxn, 0);
   std::vector<std::vector<float>> logits(2, std::vector<float>(Bp * kV, 0.f));
-  FakeProg progs[2], lo[2];
-  HzProgram hp[2] = {nullptr, nullptr}, hl[2] = {nullptr, nullptr};
+  FakeProg progs[2], lo[2], so[2];
+  HzProgram hp[2] = {nullptr, nullptr}, hl[2] = {nullptr, nullptr}, hs[2] = {nullptr, nullptr};
   int* bl[2] = {nullptr, nullptr};
   float* lg[2] = {nullptr, nullptr};
   for (int k = 0; k < nprog; ++k) {
     progs[k] = FakeProg{blocks[k].data(), logits[k].data(), Bp, U, false};
     lo[k] = FakeProg{blocks[k].data(), logits[k].data(), Bp, U, true};
+    so[k] = FakeProg{blocks[k].data(), logits[k].data(), Bp, U, false, true};
     hp[k] = &progs[k];
     hl[k] = &lo[k];
+    hs[k] = &so[k];
     bl[k] = blocks[k].data();
     lg[k] = logits[k].data();
   }
@@ -166,6 +173,7 @@ static int run_mode(int nprog, bool lowload, int clients, int iters) {
   void* s = hz_lmb_create(hp, nprog, nullptr, bl, Bp, U, 0, maxn, out_pool.data(), lg, kV);
   CHECK(s != nullptr);
   if (lowload) CHECK(hz_lmb_set_lowload(s, hl, 16) == 0);
+  if (solo) CHECK(hz_lmb_set_solo(s, hs) == 0);
   std::atomic<int> bad{0};
   std::vector<std::thread> th;
   for (int c = 0; c < clients; ++c)
@@ -194,14 +202,17 @@ static int run_mode(int nprog, bool lowload, int clients, int iters) {
   for (auto& t : th) t.join();
   unsigned long long st[4];
   hz_lmb_stats(s, st);
-  const unsigned long long lo_rep = hz_lmb_lo_replays(s);
+  const unsigned long long lo_rep = hz_lmb_lo_replays(s), solo_rep = hz_lmb_solo_replays(s);
   hz_lmb_destroy(s);
   CHECK(bad.load() == 0);
   CHECK(st[1] == (unsigned long long)clients * iters);
   CHECK(st[2] <= st[3]);
-  if (lowload) CHECK(lo_rep > 0 && lo_rep < st[0]);
-  else CHECK(lo_rep == 0);
-  printf("mode nprog=%d lowload=%d: replays %llu served %llu low %llu\n", nprog, (int)lowload, st[0], st[1], lo_rep);
+  if (lowload && clients > 1) CHECK(lo_rep > 0 && lo_rep < st[0]);
+  if (!lowload) CHECK(lo_rep == 0);
+  if (solo && clients == 1) CHECK(solo_rep == st[0]);  // a lone client always sits in row 0
+  if (!solo) CHECK(solo_rep == 0);
+  printf("mode nprog=%d lowload=%d solo=%d clients=%d: replays %llu served %llu low %llu solo %llu\n", nprog,
+         (int)lowload, (int)solo, clients, st[0], st[1], lo_rep, solo_rep);
   return 0;
 }
 
@@ -211,6 +222,10 @@ int main() {
   for (int nprog : {1, 2})
     for (bool lowload : {false, true})
       if (!rc) rc = run_mode(nprog, lowload, lowload ? 40 : 12, 25);
+  for (int nprog : {1, 2}) {  // the one-request program: alone, then under concurrency
+    if (!rc) rc = run_mode(nprog, true, 1, 20, true);
+    if (!rc) rc = run_mode(nprog, true, 24, 15, true);
+  }
   // a lone client mostly runs the low-load program
   g_gpu.halt();
   if (rc) return rc;
