@@ -304,7 +304,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // TW vocabulary tiles per wave, 16 / TW waves per workgroup (the 16 tile slots of a workgroup
 // either way): every wave reads each state fragment from LDS once per k-step, so TW = 4 halves
 // the LDS reads per tile of TW = 2 (128 KiB of ds_read_b128 per wave at Bp 32) with half the waves
-template <int NB, int KS, int CH, int R, bool NT = false, bool SOLO = false, int TW = 2>
+// DIAG (experiments build, timing only -- the tokens are garbage): 1 skips the state staging,
+// 2 skips the lo-half MFMAs and LDS reads; what each costs at Bp 32 (profiles/r4_lmb)
+template <int NB, int KS, int CH, int R, bool NT = false, bool SOLO = false, int TW = 2, int DIAG = 0>
 __global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecParams p) {
   constexpr int NCH = KS / CH;  // K = 32 * KS
   constexpr int RR = R < NCH ? R : NCH;  // chunks issued before the first MFMA
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecP
       const bf16_t* g = src + ((size_t)hl * KS * NB + (size_t)ks * NB + cb) * 512 + lane * 8;
       // (the vmcnt wait below counts only the weight chunks issued after the staging; SOLO: the
       // lanes of row 0 only -- the other rows' logits are garbage nobody reads: their dec_t is -1)
-      if (cb < nba && (!SOLO || (lane & 15) == 0))
+      if (cb < nba && (!SOLO || (lane & 15) == 0) && DIAG != 1)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g), (lds_void*)(act + (size_t)f * 512), 16, 0, 0);
     }
   }
@@ -419,11 +421,14 @@ __global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecP
       for (int cb = 0; cb < NB; ++cb) {
         if (cb >= nba) continue;
         const bf16x8 hi = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 0) * NB + cb) * 512 + lane * 8));
-        const bf16x8 lo = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 1) * NB + cb) * 512 + lane * 8));
 #pragma unroll
-        for (int t = 0; t < TW; ++t) {
+        for (int t = 0; t < TW; ++t)
           acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wr[t][cur][s]), hi, acc[t][cb], 0, 0, 0);
-          acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wr[t][cur][s]), lo, acc[t][cb], 0, 0, 0);
+        if constexpr (DIAG != 2) {
+          const bf16x8 lo = as_frag(*reinterpret_cast<const u32x4*>(act + ((size_t)(ks * 2 + 1) * NB + cb) * 512 + lane * 8));
+#pragma unroll
+          for (int t = 0; t < TW; ++t)
+            acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(wr[t][cur][s]), lo, acc[t][cb], 0, 0, 0);
         }
       }
     }
@@ -582,6 +587,14 @@ static int lmb_dec_tw() {
   return v;
 }
 
+static int lmb_dec_diag() {
+  static const int v = [] {
+    const char* e = getenv("HIPZAP_LMB_DEC_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static int lmb_dec_pipe() {
   static const int v = [] {
     const char* e = getenv("HIPZAP_LMB_DEC_PIPE");
@@ -612,10 +625,19 @@ extern "C" int hz_lmb_dec_launch(const HzLmbDecParams* pp, hipStream_t st) {
   if (pipe == 1) { HZ_LMBD(NB, 32, 4, 5); break; }                         \
   if (pipe == 2) { HZ_LMBD(NB, 32, 4, 6); break; }                         \
   if (pipe == 3) { HZ_LMBD(NB, 32, 8, 2, true); break; }
-// four tiles per wave, four waves: +5 us per step (fewer waves hide less of the weight stream)
+// four tiles per wave, four waves: +5 us per step (fewer waves hide less of the weight stream);
+// HIPZAP_LMB_DEC_DIAG = 1 / 2: the timing-only variants of the kernel's DIAG parameter
 #define HZ_LMBD_TW4(NB, S)                                                                          \
   if (tw == 4) {                                                                                   \
     hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 4, 2, false, S, 4>), grid, dim3(256), 0, st, p);    \
+    break;                                                                                         \
+  }                                                                                                \
+  if (lmb_dec_diag() == 1) {                                                                       \
+    hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 8, 2, false, S, 2, 1>), grid, dim3(512), 0, st, p); \
+    break;                                                                                         \
+  }                                                                                                \
+  if (lmb_dec_diag() == 2) {                                                                       \
+    hipLaunchKernelGGL((lmb_dec_kernel<NB, 32, 8, 2, false, S, 2, 2>), grid, dim3(512), 0, st, p); \
     break;                                                                                         \
   }
 #else
