@@ -49,8 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 24)),
-                    help="concurrent bs=1 request contexts per GPU")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 16)),
+                    help="concurrent bs=1 request contexts per GPU (16: the 24-48 rate at 2/3 of the 24-stream latency, profiles/r4_final/streams)")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
     ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 5)),
                     help="fresh processes per cold-start path (0: skip)")
