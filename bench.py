@@ -13,7 +13,7 @@ cold start (headline ``cold_start_ms_p50``): measured FIRST, before this process
   of the real ResNet-50 architecture, their plan image) are written untimed beforehand, on the
   CPU, as ``hipzap plan`` does at deploy time. In-process rebuilds inside this warm process are
   reported separately (``cold_start_inprocess_*``).
-warm path: every rank serves ``--streams`` (default 24: same throughput as 32-48 with the executor at lower latency, profiles/r2_serving/streams_sweep.md)
+warm path: every rank serves ``--streams`` (default 16: the rate of 24-48 streams at a third less latency under load, profiles/r4_final/streams16v24)
   concurrent bs=1 request streams; each request is one hipGraph replay (zero-copy pinned uint8
   image -> preprocess -> 53 fused conv kernels -> pool+FC -> logits in pinned memory).
   ``--serve executor`` (default): one native client thread per stream sends requests back to
