@@ -15,7 +15,7 @@ cold start (headline ``cold_start_ms_p50``): measured FIRST, before this process
   reported separately (``cold_start_inprocess_*``).
 warm path: every rank serves ``--streams`` (default 16: the rate of 24-48 streams at a third less latency under load, profiles/r4_final/streams16v24)
   concurrent bs=1 request streams; each request is one hipGraph replay (zero-copy pinned uint8
-  image -> preprocess -> 53 fused conv kernels -> pool+FC -> logits in pinned memory).
+  image -> preprocess -> 37 kernels: conv+maxpool, fused layer1/layer2 bottlenecks, layer3/layer4 convs -> pool+FC -> logits in pinned memory).
   ``--serve executor`` (default): one native client thread per stream sends requests back to
   back through the request executor (csrc/executor.cpp, the serving path of Engine.infer):
   payload copied into a pinned input, one replay, the client sleeps until ITS result is done,
