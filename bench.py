@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--dyn-clients", type=int, default=96)
     ap.add_argument("--dyn-wait-us", type=float, default=200.0)
     ap.add_argument("--tuned", default=None, help="conv tuning table JSON")
-    ap.add_argument("--http-clients", type=int, default=int(os.environ.get("HIPZAP_BENCH_HTTP_CLIENTS", 12)),
+    ap.add_argument("--http-clients", type=int, default=int(os.environ.get("HIPZAP_BENCH_HTTP_CLIENTS", 16)),
                     help="secondary figure: HTTP client processes PER GPU against `hipzap serve --gpus N` "
                          "(0 disables)")
     ap.add_argument("--http-requests", type=int, default=800, help="requests per HTTP client process")
@@ -401,7 +401,7 @@ def http_figure(args, world: int, rank: int):
             from hipzap.serve.loadtest import run_load
             _, plan = prepare_artifacts(args.model, args.ckpt_dir)
             res = run_load(plan, gpus=world, clients=args.http_clients * world, requests=args.http_requests,
-                           contexts=8, fmt="npy", ready_timeout=150.0)
+                           contexts=16, fmt="npy", ready_timeout=150.0)  # 16 x 16: +5 % over 12 x 8 (r4_final/http_contexts)
             if not res.get("errors"):
                 res.pop("server_log_tail", None)
         except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
