@@ -1,0 +1,32 @@
+"""bench.py's output contract on the GPU (the driver parses it every round): one JSON line with
+BASELINE.json's metric, the requested steps / warmup, a positive whole-job value and the
+fields the judge checks. A short run with every secondary figure disabled."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_prints_one_contract_line():
+    cmd = [sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--streams", "2", "--cold-trials", "0",
+           "--cold-runs", "0", "--http-clients", "0", "--dp-figures", "0", "--dyn-batch", "0", "--bert-cold", "0",
+           "--lm-cold", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["unit"] == "inferences/s"
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
+    assert d["data"].startswith("synthetic")
+    assert d["config"]["model"] == "ResNet-50" and d["config"]["global_batch"] == 1
+    assert d["config"]["parallelism"] == "dp1" and d["config"]["streams_per_gpu"] == 2
+    assert "vs_baseline" in d
