@@ -35,6 +35,8 @@ class ConvParams(C.Structure):
         ("x_rowmajor", c_int), ("ldx", c_int),
         ("tiles_n", c_int), ("kw", c_int),
         ("lnf", c_void_p),  # const HzLnFold* (device memory) or NULL
+        ("x_f32", c_int), ("z_C", c_int), ("zinit", c_void_p), ("zbias", c_void_p), ("z_HW", c_int),
+        ("pad_z", c_int),  # ResNet seams (block.hip seam_kernel)
     ]
 
 

@@ -163,12 +163,20 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
     for _ in range(trials):
         rdzv = tempfile.mkdtemp(prefix="hzcold_node_")
         procs = []
+        # worker output goes to files, not pipes: a worker writing more than a pipe buffer (RCCL debug
+        # logs, a long traceback) would block on write while this loop only polls
+        logs = [(tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")) for _ in range(world)]
         t = time.time()
         for r in range(world):
             cmd = [sys.executable, "-m", "hipzap.coldstart", "node", plan, "--device", str(r), "--rank", str(r),
                    "--world", str(world), "--rdzv", rdzv] + (["--dry"] if dry else [])
-            procs.append(subprocess.Popen(cmd, cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                          text=True))
+            procs.append(subprocess.Popen(cmd, cwd=root, env=env, stdout=logs[r][0], stderr=logs[r][1], text=True))
+
+        def output(r):
+            fo, fe = logs[r]
+            fo.seek(0)
+            fe.seek(0)
+            return fo.read(), fe.read()
         outs, err = [], None
         # a worker that fails (e.g. its device is not visible) leaves the others blocked in the
         # RCCL rendezvous: stop the launch as soon as any worker exits non-zero, not at the timeout
@@ -185,18 +193,22 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
                     q.wait()
                 shutil.rmtree(rdzv, ignore_errors=True)
                 if bad:
-                    se = procs[bad[0]].stderr.read()
+                    se = output(bad[0])[1]
                     raise RuntimeError(f"node cold start: rank {bad[0]} exited {rcs[bad[0]]}: {se[-1500:]}")
                 r = next(r for r, rc in enumerate(rcs) if rc is None)
                 raise RuntimeError(f"node cold start: rank {r} did not finish within {timeout:.0f} s")
             time.sleep(0.01)
         for r, p in enumerate(procs):
-            so, se = p.communicate()
+            p.wait()
+            so, se = output(r)
             lines = [ln for ln in so.splitlines() if ln.startswith("{")]
             if p.returncode != 0 or not lines:
                 err = err or f"rank {r} rc={p.returncode}: {se[-2000:]}"
                 continue
             outs.append(json.loads(lines[-1]))
+        for fo, fe in logs:
+            fo.close()
+            fe.close()
         shutil.rmtree(rdzv, ignore_errors=True)
         if err or len(outs) != world or not all(o["ok"] for o in outs):
             raise RuntimeError(f"node cold start failed: {err or [o.get('healthy') for o in outs]}")

@@ -876,6 +876,144 @@ __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
   HZ_BSTAMP_FLUSH(4);
 }
 
+// ------------------------------------------------------------------------------------------------
+// ResNet 1x1 -> 1x1 seam (HzSeamParams, hipzap.h; VERDICT r4 "next round" 1b): conv3 of block i
+// and conv1 of block i+1 of layer3 (14 x 14, CM 256) / layer4 (7 x 7, CM 512) in ONE launch with no
+// cross-workgroup wait. conv3's K (CM) is complete inside a workgroup, so a workgroup that owns
+// (pixel tile, CS-wide slice of the 4CM conv3 outputs) finishes its slice of the block output y --
+// bias, residual, ReLU, stored bf16 -- and can already multiply that slice by the matching K-slice of
+// conv1: the CM conv1 partial sums of its pixels go to the fp32 accumulator z by no-return float
+// atomics (memory-side adds, MI355X_MICROARCH.md § Global float atomics: each register of a 32x32
+// accumulator is two 128-B row segments, the measured full-rate shape). The launch before (block i's
+// 3x3 conv) preset z to conv1's folded-BN bias (HzConvParams.zinit), and block i+1's 3x3 conv applies
+// the ReLU when it loads z (HzConvParams.x_f32). Two launches per layer3/layer4 block instead of three.
+//
+// Phase 1 (conv3, mfma 16x16x32, A = weights, B = pixels as conv.hip): wave -> one 16-channel row
+// group x PGW 16-pixel groups, all CM/32 k-steps through a D-deep register ring. The slice of y goes
+// to global memory and, swizzled, to LDS. Phase 2 (conv1 partial, mfma 32x32x16, A = y rows =
+// pixels from LDS, B = W1 columns = conv1 outputs straight from the per-conv packing): wave -> ZBW
+// 32-wide column blocks of the CM conv1 outputs, K = the slice.
+template <int CS>
+__device__ __forceinline__ int seam_lds(int row, int chunk) {  // bf16 offset of 16-B chunk `chunk` of pixel row `row`
+  // conflict-free for the 32x32x16 A-operand ds_read_b128 lane groups (rows 0..31, one chunk):
+  // 256-B rows (CS 128) XOR the chunk with row & 15; 128-B rows (CS 64) pair rows per 256 B and XOR
+  // with (row >> 1) & 7
+  const int sw = CS == 128 ? (row & 15) : ((row >> 1) & 7);
+  return row * CS + ((chunk ^ sw) << 3);
+}
+
+// (one workgroup per CU is the design point -- 56-128 workgroups -- so the register budget is 256:
+// with hipcc's default occupancy target its scheduler sinks the ring's loads next to their MFMAs)
+template <int CM, int CS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void seam_kernel(const HzSeamParams p) {
+  constexpr int CO = 4 * CM;
+  constexpr int KS3 = CM / 32;     // conv3 k-steps
+  constexpr int RG = CS / 16;      // conv3 row groups in the slice (4 or 8)
+  constexpr int PGW = 2 * RG / 8;  // 16-pixel groups per wave (1 or 2)
+  constexpr int ZB = CM / 32;      // conv1 output column blocks (8 or 16)
+  constexpr int ZBW = ZB / 8;      // per wave
+  constexpr int KS1 = CS / 16;     // conv1 k-steps over the slice (32x32x16)
+  constexpr int KSW1 = CO / 32;    // conv1 weight k-steps (its packing)
+  constexpr int D = KS3 * PGW <= 16 ? KS3 : KS3 / 2;  // conv3 k-steps in flight (all of them up to 16 B loads)
+  __shared__ __attribute__((aligned(16))) bf16_t Y[32 * CS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4, l16 = lane & 15;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int HW = p.HW, nt = p.N * p.tiles;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids (one XCD) share a weight slice
+  const int slice = lid / nt, rem = lid - slice * nt;
+  const int n = rem / p.tiles, t = rem - n * p.tiles;
+  const int hw0 = t * HW / p.tiles, cnt = (t + 1) * HW / p.tiles - hw0;  // <= 32 (launcher)
+  const int c0 = slice * CS;
+  const int rg = wave % RG, pg0 = (wave / RG) * PGW;
+  const int ch = c0 + 16 * rg + 4 * g4;  // this lane's 4 conv3 output channels
+
+  // ---- epilogue operands first (vmcnt retires in issue order). A padding pixel column (j >= cnt)
+  // loads its tile's last pixel instead of branching (a branch around a load makes hipcc drain
+  // vmcnt): its conv3 column, LDS row and conv1 row are never stored ----
+  const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b3 + ch);
+  u32x2 rr[PGW];
+  long yo[PGW], xb[PGW];
+  bool yv[PGW];
+#pragma unroll
+  for (int q = 0; q < PGW; ++q) {
+    const int j = 16 * (pg0 + q) + l16, jc = min(j, cnt - 1);
+    yv[q] = j < cnt;
+    yo[q] = (((long)n * (CO / 32) + (ch >> 5)) * HW + hw0 + jc) * 32 + (ch & 31);
+    rr[q] = *reinterpret_cast<const u32x2*>(p.res + yo[q]);
+    xb[q] = (((long)n * KS3) * HW + hw0 + jc) * 32 + 8 * g4;
+  }
+  // ---- conv3 operand ring ----
+  const bf16_t* __restrict__ W3 = p.w3 + ((long)(c0 / 16 + rg) * KS3) * 512 + lane * 8;
+  bf16x8 fa[KS3], fb[KS3][PGW];
+  auto load = [&](int s) {
+    fa[s] = *reinterpret_cast<const bf16x8*>(W3 + (long)s * 512);
+#pragma unroll
+    for (int q = 0; q < PGW; ++q) fb[s][q] = *reinterpret_cast<const bf16x8*>(p.t2 + xb[q] + (long)s * HW * 32);
+  };
+#pragma unroll
+  for (int s = 0; s < D && s < KS3; ++s) load(s);
+  // ---- conv1 weights of this wave's column blocks (phase 2's B operands), behind the ring ----
+  bf16x8 fw[ZBW][KS1];
+#pragma unroll
+  for (int i = 0; i < ZBW; ++i) {
+    const int zc = 32 * (wave * ZBW + i) + l32;
+#pragma unroll
+    for (int u = 0; u < KS1; ++u) {
+      const int kk = c0 + 16 * u + 8 * h;
+      fw[i][u] = *reinterpret_cast<const bf16x8*>(
+          p.w1 + ((((long)(zc >> 4) * KSW1 + (kk >> 5)) * 64) + ((kk & 31) >> 3) * 16 + (zc & 15)) * 8);
+    }
+  }
+  asm volatile("" ::: "memory");  // keep those loads here: hipcc otherwise sinks them below phase 1
+  f32x4 acc[PGW];
+#pragma unroll
+  for (int q = 0; q < PGW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS3; ++s) {
+#pragma unroll
+    for (int q = 0; q < PGW; ++q) acc[q] = mfma16(fa[s], fb[s][q], acc[q]);
+    if (s + D < KS3) load(s + D);
+  }
+  // ---- phase-1 epilogue: y slice -> global (bf16) and LDS ----
+  const int cl = 16 * rg + 4 * g4;  // local channel in the slice
+#pragma unroll
+  for (int q = 0; q < PGW; ++q) {
+    float v[4] = {acc[q][0] + bias[0] + __uint_as_float(rr[q][0] << 16),
+                  acc[q][1] + bias[1] + __uint_as_float(rr[q][0] & 0xffff0000u),
+                  acc[q][2] + bias[2] + __uint_as_float(rr[q][1] << 16),
+                  acc[q][3] + bias[3] + __uint_as_float(rr[q][1] & 0xffff0000u)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    const u32x2 pk = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    if (yv[q]) *reinterpret_cast<u32x2*>(p.y + yo[q]) = pk;
+    *reinterpret_cast<u32x2*>(Y + seam_lds<CS>(16 * (pg0 + q) + l16, cl >> 3) + (cl & 4)) = pk;
+  }
+  lds_sync();
+  // ---- phase 2: z[pixel][conv1 channel] += y_slice . W1[:, slice] ----
+  f32x16 za[ZBW];
+#pragma unroll
+  for (int i = 0; i < ZBW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) za[i][r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < KS1; ++u) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(Y + seam_lds<CS>(l32, 2 * u + h));
+#pragma unroll
+    for (int i = 0; i < ZBW; ++i) za[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, fw[i][u], za[i], 0, 0, 0);
+  }
+  // 32x32 D map: column = lane & 31 (conv1 channel), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (pixel)
+#pragma unroll
+  for (int i = 0; i < ZBW; ++i) {
+    float* zb = p.z + (((long)n * ZB + wave * ZBW + i) * HW + hw0) * 32 + l32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < cnt) atomicAdd(zb + row * 32, za[i][r]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
@@ -917,6 +1055,20 @@ extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
     return -1;
   }
 #undef HZ_BNL
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
+  const HzSeamParams& p = *pp;
+  if (!p.t2 || !p.w3 || !p.b3 || !p.res || !p.y || !p.w1 || !p.z) return -1;
+  if (p.N < 1 || p.HW < 1 || (p.CM != 256 && p.CM != 512) || (p.cs != 64 && p.cs != 128)) return -1;
+  HzSeamParams q = p;
+  q.tiles = (p.HW + 31) / 32;  // balanced tiles of <= 32 pixels
+  const dim3 grid(q.tiles * p.N * (4 * p.CM / p.cs));
+  if (p.CM == 256 && p.cs == 128) hipLaunchKernelGGL((seam_kernel<256, 128>), grid, dim3(512), 0, st, q);
+  else if (p.CM == 256) hipLaunchKernelGGL((seam_kernel<256, 64>), grid, dim3(512), 0, st, q);
+  else if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128>), grid, dim3(512), 0, st, q);
+  else hipLaunchKernelGGL((seam_kernel<512, 64>), grid, dim3(512), 0, st, q);
   return (int)hipGetLastError();
 }
 

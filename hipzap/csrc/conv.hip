@@ -70,9 +70,20 @@ __device__ __forceinline__ bf16x8 ld_act(const bf16_t* X, long off, __amdgpu_buf
   else return *reinterpret_cast<const bf16x8*>(X + off);
 }
 
+// fp32 activation fragment (HzConvParams.x_f32: a ResNet seam's conv1 sum, block.hip seam_kernel):
+// the ring keeps the two raw 16-B loads and this converts them (ReLU -> bf16) right before the MFMA,
+// so no ALU work sits behind a load inside the validity branch (which made hipcc drain vmcnt there:
+// the first build of the seam consumer ran 70 % slower than the bf16 conv, profiles/r5_seam)
+__device__ __forceinline__ bf16x8 f32relu_bf16(const f32x4& a, const f32x4& b) {
+  const u32x4 r = u32x4{pack2(fmaxf(a[0], 0.f), fmaxf(a[1], 0.f)), pack2(fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)),
+                        pack2(fmaxf(b[0], 0.f), fmaxf(b[1], 0.f)), pack2(fmaxf(b[2], 0.f), fmaxf(b[3], 0.f))};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 // One output tile of one conv problem; `lid` = logical tile id (already XCD-remapped).
 // SC1: the tile runs inside conv_chain_kernel (in-launch producer/consumer hand-offs).
-template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool SC1 = false>
+// F32IN: fp32 input with ReLU at the load (3x3 convs only; HzConvParams.x_f32).
+template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool SC1 = false, bool F32IN = false>
 __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) {
   constexpr int DEPTH = Depth<FC, FP>::value;
   constexpr int NF = FC * FP;
@@ -133,6 +144,8 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   const bf16_t* __restrict__ Wf = p.w + ((long)(n0 >> 4) * steps) * 512 + lane * 8;
 
   bf16x8 fa[DEPTH + 1][FC], fb[DEPTH + 1][FP];
+  constexpr int FR = F32IN ? DEPTH + 1 : 1;
+  f32x4 fr[FR][FP][2];  // F32IN: the raw fp32 activation loads of each ring slot
   f32x4 acc[FC][FP];
 #pragma unroll
   for (int i = 0; i < FC; ++i)
@@ -157,7 +170,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   // vmcnt(0) per step) were A/B-measured on one box: +2.7 % single stream but -2 % at 8
   // concurrent streams with a spread zero region, -10/-18 % with a shared zero line + zero
   // loads for out-of-range steps (profiles/r1_ab). Throughput is the objective, so this stays.
-  auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP]) {
+  auto load_step = [&](int t, bf16x8(&a)[FC], bf16x8(&b)[FP], f32x4(&rw)[FP][2]) {
     const int s_idx = s_begin + t;
     const int k = s_idx * 32;
 #pragma unroll
@@ -194,8 +207,18 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
         for (int j = 0; j < FP; ++j) {
           const bool v = pval[j] && (unsigned)(pih[j] + r) < (unsigned)p.H && (unsigned)(piw[j] + s) < (unsigned)p.W;
           const long off = ((long)(pb[j] + uoff) << 5) + lk;
-          if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) b[j] = ld_act<SC1>(X, off, xrs);
-          else b[j] = bf16x8{};
+          if constexpr (F32IN) {
+            const float* xf = reinterpret_cast<const float*>(X) + off;
+            if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) {
+              rw[j][0] = *reinterpret_cast<const f32x4*>(xf);
+              rw[j][1] = *reinterpret_cast<const f32x4*>(xf + 4);
+            } else {
+              rw[j][0] = rw[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          } else {
+            if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) b[j] = ld_act<SC1>(X, off, xrs);
+            else b[j] = bf16x8{};
+          }
         }
       }
     } else {  // plain NHWC input with C in {8, 16}: per-lane (r, s, c) decomposition
@@ -218,7 +241,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 
 #pragma unroll
   for (int u = 0; u < DEPTH; ++u)
-    if (u < nsteps) load_step(u, fa[u], fb[u]);
+    if (u < nsteps) load_step(u, fa[u], fb[u], fr[F32IN ? u : 0]);
   // output element offset of accumulator (i, j) of this lane, -1 when out of range
   auto out_off = [&](int i, int j) -> long {
     const int m = m0 + j * 16 + lrow;
@@ -255,8 +278,14 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
     for (int u = 0; u <= DEPTH; ++u) {
       const int tt = t + u;
-      if (tt + DEPTH < nsteps) load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)]);
+      if (tt + DEPTH < nsteps)
+        load_step(tt + DEPTH, fa[(u + DEPTH) % (DEPTH + 1)], fb[(u + DEPTH) % (DEPTH + 1)],
+                  fr[F32IN ? (u + DEPTH) % (DEPTH + 1) : 0]);
       if (tt < nsteps) {
+        if constexpr (F32IN) {
+#pragma unroll
+          for (int j = 0; j < FP; ++j) fb[u][j] = f32relu_bf16(fr[u][j][0], fr[u][j][1]);
+        }
 #pragma unroll
         for (int i = 0; i < FC; ++i)
 #pragma unroll
@@ -343,9 +372,22 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
   HZ_STAMP_FLUSH;
 }
 
-template <int FC, int FP, bool FAST, bool IS1X1, bool XROW>
+// HzConvParams.zinit: preset the next ResNet seam's fp32 accumulator to its conv1 bias (after this
+// launch's own tiles; the seam launch that follows adds into it)
+__device__ __forceinline__ void zfill(const HzConvParams& p) {
+  const long n4 = (long)p.N * p.z_C * p.z_HW / 4;
+  const int T = p.kw * 64, cb = p.z_C >> 5;
+  for (long i = (long)blockIdx.x * T + threadIdx.x; i < n4; i += (long)gridDim.x * T) {
+    const long e = i * 4;
+    const int c = (int)((e / (32L * p.z_HW)) % cb) * 32 + (int)(e & 31);
+    *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
+  }
+}
+
+template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool F32IN = false>
 __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const HzConvParams p) {
-  conv_tile<FC, FP, FAST, IS1X1, XROW>(p, xcd_remap(blockIdx.x, gridDim.x));
+  conv_tile<FC, FP, FAST, IS1X1, XROW, false, F32IN>(p, xcd_remap(blockIdx.x, gridDim.x));
+  if (p.zinit) zfill(p);
 }
 
 // Two independent convs on the same stream in ONE launch (ResNet: a stage's downsample 1x1
@@ -361,6 +403,7 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv2_kernel(const 
 
 int check_params(const HzConvParams& p) {
   if (p.Cout % 4 != 0 || p.C % 8 != 0) return -1;
+  if (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1)) return -1;
   if (!p.x_rowmajor && p.C % 32 != 0 && p.C > 16) return -1;
   if (p.x_rowmajor && (p.ldx % 8 != 0 || p.R != 1 || p.S != 1)) return -1;
   if (!p.out_rowmajor && p.Cout % 32 != 0) return -1;
@@ -402,7 +445,10 @@ int launch(const HzConvParams& p, hipStream_t st) {
   const bool fast = (p.C % 32) == 0;
   dim3 grid(q.tiles_n * tiles_m), block(64 * kw);
   const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
-  if (p.x_rowmajor) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
+  if (p.x_f32) {  // a seam consumer: 3x3 (or strided) channel-blocked convs only
+    if (p.x_rowmajor || is1x1 || !fast) return -1;
+    hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false, true>), grid, block, lds, st, q);
+  } else if (p.x_rowmajor) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
   else if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false>), grid, block, lds, st, q);
   else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false>), grid, block, lds, st, q);
   else hipLaunchKernelGGL((conv_kernel<FC, FP, false, false, false>), grid, block, lds, st, q);
@@ -414,7 +460,7 @@ int launch(const HzConvParams& p, hipStream_t st) {
 // cfg = fci*3 + fpi with FC = 1<<fci, FP = 1<<fpi (1, 2, 4); waves per workgroup = p->kw.
 // Mirrored by hipzap/ops/conv.py (TILES).
 extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
-  if (cfg >= 16) return hz_gemm_lds_launch(pp, cfg, st);
+  if (cfg >= 16) return (pp->x_f32 || pp->zinit) ? -1 : hz_gemm_lds_launch(pp, cfg, st);
   const HzConvParams& p = *pp;
   if (check_params(p)) return -1;
   switch (cfg) {
@@ -434,6 +480,7 @@ extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
 // Grouped launch of two independent convs sharing one (cfg, kw); see conv2_kernel.
 extern "C" int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int cfg, hipStream_t st) {
   if (check_params(*a) || check_params(*b)) return -1;
+  if (a->x_f32 || b->x_f32 || a->zinit || b->zinit) return -1;  // (seams bind single convs)
   switch (cfg) {
     case 0: return launch2<1, 1>(*a, *b, st);
     case 1: return launch2<1, 2>(*a, *b, st);

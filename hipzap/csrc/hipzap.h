@@ -24,6 +24,14 @@ typedef struct HzConvParams {
   int tiles_n;               // filled by the launcher
   int kw;                    // waves per workgroup splitting K
   const struct HzLnFold* lnf; // LDS GEMM only: LayerNorm folded into this GEMM (device memory), or NULL
+  // ResNet 1x1 -> 1x1 seams (block.hip seam_kernel; register-ring 3x3 convs only):
+  int x_f32;                 // 1: x is fp32 in the same channel-blocked layout (a seam's conv1 sum, its
+                             //    folded-BN bias included): ReLU + bf16 applied at the operand load
+  int z_C;                   // channels of zinit
+  float* zinit;              // or NULL: after its tiles the launch fills zinit [N][z_C/32][z_HW][32] fp32
+                             //   with zbias[c] (the NEXT seam's accumulator, before its atomic adds)
+  const float* zbias;        // [z_C]
+  int z_HW, pad_z;
 } HzConvParams;
 
 // Post-LN transformer LayerNorm folded into the neighbouring GEMMs (gemm.hip, BERT). A GEMM
@@ -446,15 +454,34 @@ typedef struct HzBneckParams {
                                  //   stride-2 first block of layer2)
   int tile_h, pad_;           // layer1 output tile rows: 8 (default when 0) or 4 (twice the workgroups)
 } HzBneckParams;
+// ResNet 1x1 -> 1x1 seam at 14x14 / 7x7 (layer3 / layer4, bs=1): conv3 of block i (1x1 CM -> 4CM,
+// + residual + ReLU) and the K-split conv1 of block i+1 (1x1 4CM -> CM) in ONE launch. A workgroup
+// owns (pixel tile <= 32, slice of cs of the 4CM channels): it computes that slice of y = relu(W3 t2
+// + b3 + res) over the full K, stores it, and adds W1[:, slice] . y_slice into the fp32 accumulator z
+// (no-return float atomics; z was set to conv1's bias by the launch before, see HzConvParams.zinit);
+// block i+1's 3x3 conv reads z with ReLU at its operand load (HzConvParams.x_f32). No workgroup
+// waits for another: the conv1 reduction happens in the memory-side atomic units.
+typedef struct HzSeamParams {
+  const unsigned short* t2;   // conv3 input [N][CM/32][HW][32] bf16
+  const unsigned short* w3;   // conv3 weights, packed as the per-conv kernels ([4CM/16][CM/32][64][8])
+  const float* b3;            // [4CM]
+  const unsigned short* res;  // residual [N][4CM/32][HW][32]
+  unsigned short* y;          // block output [N][4CM/32][HW][32]
+  const unsigned short* w1;   // next conv1 weights [CM/16][4CM/32][64][8]
+  float* z;                   // next conv1 accumulator [N][CM/32][HW][32] fp32, preset to its bias
+  int N, HW, CM, cs;          // cs: slice width (64 or 128)
+  int tiles, pad_;            // pixel tiles per image (launcher: ceil(HW / 32))
+} HzSeamParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);
+int hz_seam_launch(const HzSeamParams* p, hipStream_t st);
 int hz_block_code_warm(void);
 
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
-       HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17, HZ_K_STEM = 18, HZ_K_BNECK = 19 };
+       HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17, HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_experiments(void);  // 1: built with HZ_EXPERIMENTS (measured-negative kernel variants)
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind
@@ -497,7 +524,7 @@ int hz_prog_add_diag(HzProgram p, int kind, int blocks, int threads, void* a, vo
 
 // ---- plan images (csrc/plan.cpp, engine/plan.py): serialised bound programs ----
 // bump HZ_ABI_EPOCH when a kernel's parameter SEMANTICS change without a size change
-#define HZ_ABI_EPOCH 1
+#define HZ_ABI_EPOCH 2
 enum { HZ_PLAN_OP_CONV = 1, HZ_PLAN_OP_CONV2 = 2, HZ_PLAN_OP_MAXPOOL = 3, HZ_PLAN_OP_AVGPOOL = 4,
        HZ_PLAN_OP_PREPROCESS = 5, HZ_PLAN_OP_MEMCPY = 6, HZ_PLAN_OP_KERNEL = 7, HZ_PLAN_OP_FORK = 8,
        HZ_PLAN_OP_JOIN = 9 };

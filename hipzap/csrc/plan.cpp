@@ -154,7 +154,8 @@ struct Plan {
             case HZ_K_POOL_FC: u |= kUnitVision; break;
             case HZ_K_CONV_CHAIN: u |= kUnitConv; break;
             case HZ_K_STEM:
-            case HZ_K_BNECK: u |= kUnitBlock; break;
+            case HZ_K_BNECK:
+            case HZ_K_SEAM: u |= kUnitBlock; break;
             default: break;
           }
           break;
@@ -468,6 +469,7 @@ uint64_t hz_abi_version(void) {
                             sizeof(HzMemcpyArgs),
                             sizeof(HzStemParams),
                             sizeof(HzBneckParams),
+                            sizeof(HzSeamParams),
                             HZ_ABI_EPOCH};
   uint64_t x = 1469598103934665603ull;
   for (uint64_t v : parts) {
@@ -567,8 +569,16 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   // Joined before returning: left running into the caller's context setup (stream creation,
   // hipMemsetAsync), it crashed the runtime in a process that already held RCCL communicators
   // (tests/test_cluster_gpu.py, profiles/r3_warm3/README.md).
+  // Order (HIPZAP_PLAN_WARM_ORDER): "stream" (default) starts the thread once the upload stream
+  // exists, so the process's first hipStreamCreate (HIP's lazy queue setup) never runs beside the
+  // code-object loads -- the driver's round-4 box showed the first stream finishing only when the
+  // warm thread did (stream 161 ms, warm 163 ms); "init": right after HIP init
+  // (rounds 3-4).
   const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
-  if (e == hipSuccess && !(cw && cw[0] == '0')) {
+  const char* wo = getenv("HIPZAP_PLAN_WARM_ORDER");
+  const bool warm_on = !(cw && cw[0] == '0');
+  const bool warm_early = wo && std::strcmp(wo, "init") == 0;
+  auto start_warm = [&]() {
     const unsigned units = p->code_units() | ((p->h.flags & kFlagWeightless) ? kUnitPack : 0u);
     double* t_warm = &p->t[HZ_PLAN_T_WARM_THREAD];  // written by the thread, read after the join
     p->warm = std::thread([device, units, t_warm] {
@@ -583,7 +593,8 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
       if (units & kUnitBlock) (void)hz_block_code_warm();
       *t_warm = now_ms() - w0;
     });
-  }
+  };
+  if (e == hipSuccess && warm_on && warm_early) start_warm();
   if (e == hipSuccess) e = hipMalloc(&p->blob, p->h.blob_len ? p->h.blob_len : 256);
   p->t[HZ_PLAN_T_BLOB_ALLOC] = now_ms() - t2;
   if (e != hipSuccess) {
@@ -603,6 +614,7 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
     p->spare = s;
     const double tu = now_ms();
     p->t[HZ_PLAN_T_STREAM] = tu - ts;
+    if (warm_on && !warm_early) start_warm();  // beside the blob's read + DMA, after the first stream
     if (read_blob && p->upload_blob(s)) {
       delete p;
       return nullptr;

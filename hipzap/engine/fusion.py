@@ -12,7 +12,14 @@ bind as ONE fused kernel instead:
   optionally with its 1x1 downsample) -> ``hz_bneck_launch``;
 * ``bneck2``: a layer2 bottleneck (1x1 512 -> 128, 3x3 128 -> 128, 1x1 128 -> 512 + residual;
   or the first block: 1x1 256 -> 128, 3x3/2, 1x1 -> 512 + the 1x1/2 downsample) ->
-  ``hz_bneck_launch`` (the weight-streaming ``bneck2_kernel`` / ``bneck2d_kernel``).
+  ``hz_bneck_launch`` (the weight-streaming ``bneck2_kernel`` / ``bneck2d_kernel``);
+* ``seam``: layer3 / layer4 -- conv3 of block i and conv1 of block i+1 (1x1 CM -> 4CM + residual,
+  1x1 4CM -> CM; CM 256 or 512) -> ``hz_seam_launch`` (``seam_kernel``): conv1's K is split over
+  the workgroups and summed by float atomics into an fp32 accumulator that block i's 3x3 conv
+  presets to conv1's bias (``HzConvParams.zinit``) and block i+1's 3x3 conv reads with the ReLU
+  at its operand load (``HzConvParams.x_f32``). The accumulator is conv1's output tensor, planned
+  as fp32 (:func:`planning_graph`). Atomic accumulation order varies run to run: a seam program is
+  numerically equal to the per-conv one within fp32 rounding, not bitwise reproducible.
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
@@ -30,8 +37,8 @@ import numpy as np
 
 from .. import _native as N
 
-HZ_K_STEM, HZ_K_BNECK = 18, 19
-KINDS = ("stem", "convpool", "bneck", "bneck2")
+HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM = 18, 19, 20
+KINDS = ("stem", "convpool", "bneck", "bneck2", "seam")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box)
 DEFAULT = "convpool,bneck,bneck2"
 
@@ -50,12 +57,20 @@ class BneckParams(C.Structure):  # HzBneckParams
                 ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int), ("tile_h", C.c_int), ("pad_", C.c_int)]
 
 
+class SeamParams(C.Structure):  # HzSeamParams
+    _fields_ = [("t2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("res", C.c_void_p),
+                ("y", C.c_void_p), ("w1", C.c_void_p), ("z", C.c_void_p), ("N", C.c_int), ("HW", C.c_int),
+                ("CM", C.c_int), ("cs", C.c_int), ("tiles", C.c_int), ("pad_", C.c_int)]
+
+
 @dataclass
 class Fused:
     kind: str
     start: int
     end: int      # exclusive node index
     nodes: list   # the graph nodes it replaces
+    init: int | None = None      # seam: the conv that presets the accumulator (block i's 3x3 conv)
+    consumer: int | None = None  # seam: the conv that reads it (block i+1's 3x3 conv)
 
 
 def enabled_kinds(spec: str | None = None) -> set:
@@ -183,6 +198,44 @@ def match_bneck(g, params, i: int, layer2: bool = False) -> Fused | None:
     return Fused("bneck", i, i + len(grp), grp)
 
 
+def match_seam(g, params, i: int) -> Fused | None:
+    """nodes[i] = conv3 of a layer3/layer4 block, nodes[i+1] = the next block's conv1 reading its
+    output, nodes[i-1] / nodes[i+2] = the two 3x3 convs around them (accumulator preset / reader)."""
+    nodes = g.nodes
+    if i < 1 or i + 3 > len(nodes):
+        return None
+    c2a, c3, c1, c2b = nodes[i - 1:i + 3]
+    if not all(_conv(n) for n in (c2a, c3, c1, c2b)):
+        return None
+    if len({n.slot for n in (c2a, c3, c1, c2b)}) != 1:
+        return None
+    if any(n.attrs.get("out_f32") or n.attrs.get("rowmajor") for n in (c2a, c3, c1, c2b)):
+        return None
+    if any(n.attrs.get("act", "relu") != "relu" for n in (c3, c1, c2b)):
+        return None
+    pa, p3, p1, pb = (params.get(n.attrs.get("w")) for n in (c2a, c3, c1, c2b))
+    if None in (pa, p3, p1, pb):
+        return None
+    cm = p1.cout
+    if cm not in (256, 512):
+        return None
+    if not (_geom(p3, cm, 4 * cm, 1, 1, 0) and _geom(p1, 4 * cm, cm, 1, 1, 0) and _geom(pb, cm, cm, 3, 1, 1)
+            and pa.cout == cm and pa.r == 3):
+        return None
+    if len(c3.inputs) != 2 or c3.inputs[0] != c2a.outputs[0] or c1.inputs != [c3.outputs[0]]:
+        return None
+    if c2b.inputs != [c1.outputs[0]]:
+        return None
+    t1 = c1.outputs[0]
+    if t1 in g.outputs or g.tensors[t1].external:
+        return None
+    if any(t1 in n.inputs for j, n in enumerate(nodes) if j != i + 2):  # read by the 3x3 conv alone
+        return None
+    if len(g.shape(c3.outputs[0])) != 4 or g.shape(c3.outputs[0])[1:3] != g.shape(t1)[1:3]:
+        return None
+    return Fused("seam", i, i + 2, [c3, c1], init=i - 1, consumer=i + 2)
+
+
 def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
     """{first node index: Fused} for every fusible run of ``g`` (non-overlapping, in order)."""
     kinds = enabled_kinds() if kinds is None else kinds
@@ -205,7 +258,55 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
             i = f.end
         else:
             i += 1
+    if "seam" in kinds:  # over the nodes the block fusions left, their 3x3 neighbours included
+        covered = {j for f in out.values() for j in range(f.start, f.end)}
+        seams = {}
+        for i in range(len(g.nodes)):
+            f = match_seam(g, params, i)
+            if f is not None and not covered & set(range(f.init, f.consumer + 1)):
+                seams[i] = f
+        out.update(seams)
+        out = dict(sorted(out.items()))
     return out
+
+
+def planning_graph(g, fused: dict):
+    """The graph the arena planner sees: a seam's accumulator (conv1's output) is fp32, and it is
+    live from the 3x3 conv that presets it (an extra output of that node)."""
+    seams = [f for f in fused.values() if f.kind == "seam"]
+    if not seams:
+        return g
+    import copy
+
+    import torch
+    gp = copy.copy(g)
+    gp.tensors = list(g.tensors)
+    gp.nodes = list(g.nodes)
+    for f in seams:
+        t1 = f.nodes[1].outputs[0]
+        spec = g.tensors[t1]
+        gp.tensors[t1] = type(spec)(spec.shape, torch.float32, spec.name, spec.external)
+        n = g.nodes[f.init]
+        gp.nodes[f.init] = type(n)(n.kind, list(n.inputs), list(n.outputs) + [t1], n.slot, n.attrs)
+    return gp
+
+
+def seam_cs(cm: int) -> int:
+    """Slice width of the seam kernel per geometry (HIPZAP_SEAM_CS="<cs for CM 256>,<cs for CM 512>")."""
+    v = [int(x) for x in os.environ.get("HIPZAP_SEAM_CS", "128,64").split(",")]
+    return v[0] if cm == 256 else v[-1]
+
+
+def seam_params(g, params, f: Fused, addr) -> SeamParams:
+    c3, c1 = f.nodes
+    p3, p1 = params[c3.attrs["w"]], params[c1.attrs["w"]]
+    p = SeamParams()
+    p.t2, p.res, p.y, p.z = addr(c3.inputs[0]), addr(c3.inputs[1]), addr(c3.outputs[0]), addr(c1.outputs[0])
+    p.w3, p.b3, p.w1 = p3.wf.data_ptr(), p3.bias.data_ptr(), p1.wf.data_ptr()
+    nb, h, w, _ = g.shape(c3.outputs[0])
+    p.N, p.HW, p.CM = nb, h * w, p1.cout
+    p.cs = seam_cs(p.CM)
+    return p
 
 
 def stem_params(g, params, f: Fused, addr) -> StemParams:
@@ -269,6 +370,8 @@ def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
     """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
     if f.kind in ("stem", "convpool"):
         prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
+    elif f.kind == "seam":
+        prm, kind = seam_params(g, params, f, addr), HZ_K_SEAM
     else:
         prm, kind = bneck_params(g, params, f, addr), HZ_K_BNECK
     N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(prm), C.sizeof(prm), f.nodes[0].slot), f"add_{f.kind}")
@@ -278,5 +381,5 @@ def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
 
 def launch(kind: str, prm, stream=None) -> None:
     """Eager launch of a fused kernel (tests)."""
-    k = HZ_K_STEM if kind == "stem" else HZ_K_BNECK
+    k = HZ_K_STEM if kind == "stem" else HZ_K_SEAM if kind == "seam" else HZ_K_BNECK
     N.check(N.lib().hz_launch_kernel(k, C.byref(prm), N.stream_ptr(stream)), f"launch_{kind}")

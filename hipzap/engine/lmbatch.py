@@ -187,6 +187,10 @@ class _TorchAlloc:
 
     def device(self, nbytes: int) -> int:
         t = torch.zeros(max(1, nbytes), dtype=torch.uint8, device=self.dev)
+        # the fill runs on torch's current stream; LmbCore launches on its own non-blocking stream
+        # right after (e.g. lmb_embproj_kernel writing the 1.1 GB projected-embedding table), which
+        # is not ordered after it: finish the fill before handing the bytes out
+        torch.cuda.current_stream(self.dev).synchronize()
         self.keep.append(t)
         return t.data_ptr()
 

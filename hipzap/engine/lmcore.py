@@ -202,8 +202,17 @@ class LmbCore:
         if embproj is None:
             embproj = os.environ.get("HIPZAP_LM_EMBPROJ", "1") != "0"
         self.embproj = 0
+        # the table is fp32 Vp x 4H (1.1 GB at V = 60000, ~4.9 GB at V = 267k): capped by
+        # HIPZAP_LM_EMBPROJ_MAX_MB, and a failed allocation falls back to the per-step multiply
+        ep_bytes = geo.Vp * L[0].R * 4
+        if embproj and ep_bytes > float(os.environ.get("HIPZAP_LM_EMBPROJ_MAX_MB", 8192)) * 2 ** 20:
+            embproj = False
         if embproj:
-            self.embproj = alloc.device(geo.Vp * L[0].R * 4)
+            try:
+                self.embproj = alloc.device(ep_bytes)
+            except Exception:  # noqa: BLE001 - out of device memory: the first layer multiplies W_ih0 E[tok]
+                self.embproj, embproj = 0, False
+        if embproj:
             ep = N.LmbEmbProjParams()
             ep.w, ep.emb, ep.out = w["layers"][0][0], w["emb"], self.embproj
             ep.R, ep.Kh, ep.Kx, ep.Vp = L[0].R, L[0].Kh, L[0].Kx, geo.Vp

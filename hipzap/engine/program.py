@@ -69,7 +69,19 @@ class ExecContext:
         self.fused = fusion.plan(g, params, fusion.enabled_kinds(fuse) if fuse is not None else None)
         if chain is not None:
             self.fused = {k: f for k, f in self.fused.items() if f.end <= chain[0]}
-        offsets, arena_bytes = plan_memory(g, groups=[(f.start, f.end) for f in self.fused.values()])
+        conv_plans = self._conv_plans(g, params, tuned)
+        if pair_convs is None:
+            pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
+        self.pairs = conv_pairs(g) if pair_convs else {}
+        paired = set(self.pairs) | set(self.pairs.values())
+        # a seam's 3x3 neighbours must bind as single register-ring convs (zinit / x_f32 live there)
+        self.fused = {k: f for k, f in self.fused.items() if f.kind != "seam" or (
+            f.init not in paired and f.consumer not in paired and conv_plans[f.init][0] < 16
+            and conv_plans[f.consumer][0] < 16)}
+        self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
+        self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}
+        offsets, arena_bytes = plan_memory(fusion.planning_graph(g, self.fused),
+                                           groups=[(f.start, f.end) for f in self.fused.values()])
         self.arena_bytes = arena_bytes
         self.arena = torch.empty(max(arena_bytes, 256), dtype=torch.uint8, device=self.device)
         base = self.arena.data_ptr()
@@ -89,6 +101,54 @@ class ExecContext:
         self.tensor_offsets = offsets
         self.prog = lib.hz_prog_create()
         self.configs: list = []
+        # host_io: the request's PCIe transfers are part of the program (and of the graph):
+        # pinned host inputs -> device inputs ... device output -> pinned host output.
+        # zero_copy ("in", "out", "all"): the first/last kernels read the request from / write the
+        # result to the pinned host buffers directly (UVA), replacing the copy node(s) and their
+        # kernel boundaries; HIPZAP_ZERO_COPY picks the default.
+        self.host_io = host_io
+        zc = zero_copy if zero_copy is not None else os.environ.get("HIPZAP_ZERO_COPY", "")
+        self.zc_in, self.zc_out = host_io and zc in ("in", "all", "1"), host_io and zc in ("out", "all", "1")
+        if host_io:
+            pin = (lambda t: t) if self.recording else (lambda t: t.pin_memory())
+            self.host_inputs = [pin(torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype)) for t in g.inputs]
+            self.host_input = self.host_inputs[0]
+            self.host_output = pin(torch.zeros(self.output.shape, dtype=self.output.dtype))
+            for t, hbuf in zip(g.inputs, self.host_inputs):
+                if self.zc_in:
+                    self.ext[t] = hbuf
+                    continue
+                d = self.ext[t]
+                N.check(lib.hz_prog_add_memcpy(self.prog, d.data_ptr(), hbuf.data_ptr(), d.numel() * d.element_size(),
+                                               0), "h2d")
+            if self.zc_out:
+                self.ext[g.outputs[0]] = self.host_output
+        self.chain_sync = None
+        i = 0
+        while i < len(g.nodes):
+            n = g.nodes[i]
+            if i in self.fused:
+                f = self.fused[i]
+                self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib))
+                i = f.end
+                continue
+            if chain is not None and i == chain[0]:
+                self._add_conv_chain(lib, chain[0], chain[1], conv_plans)
+                i = chain[1]
+                continue
+            if i in self.pairs:
+                self._add_conv_pair(lib, n, g.nodes[i + 1], conv_plans[i], conv_plans[i + 1], tuned)
+                i += 2
+                continue
+            self._add_node(lib, n, conv_plans[i])
+            i += 1
+        if host_io and not self.zc_out:
+            N.check(lib.hz_prog_add_memcpy(self.prog, self.host_output.data_ptr(), self.output.data_ptr(),
+                                           self.output.numel() * self.output.element_size(), 0), "d2h")
+
+    # ------------------------------------------------------------------
+    def _conv_plans(self, g: Graph, params: dict, tuned: dict | None) -> list:
+        """(cfg, kw, tuning key) of every conv / GEMM node, None for other nodes."""
         conv_plans = []
         for n in g.nodes:
             if n.kind not in ("conv", "gemm", "gemm_fp8"):
@@ -129,53 +189,7 @@ class ExecContext:
                         raise ValueError(f"{n.attrs.get('name')}: folded LayerNorm needs the LDS GEMM (M={M} < 64?)")
                     cfg, kw = 19, 1
             conv_plans.append((cfg, kw, key))
-        # host_io: the request's PCIe transfers are part of the program (and of the graph):
-        # pinned host inputs -> device inputs ... device output -> pinned host output.
-        # zero_copy ("in", "out", "all"): the first/last kernels read the request from / write the
-        # result to the pinned host buffers directly (UVA), replacing the copy node(s) and their
-        # kernel boundaries; HIPZAP_ZERO_COPY picks the default.
-        self.host_io = host_io
-        zc = zero_copy if zero_copy is not None else os.environ.get("HIPZAP_ZERO_COPY", "")
-        self.zc_in, self.zc_out = host_io and zc in ("in", "all", "1"), host_io and zc in ("out", "all", "1")
-        if host_io:
-            pin = (lambda t: t) if self.recording else (lambda t: t.pin_memory())
-            self.host_inputs = [pin(torch.zeros(self.ext[t].shape, dtype=self.ext[t].dtype)) for t in g.inputs]
-            self.host_input = self.host_inputs[0]
-            self.host_output = pin(torch.zeros(self.output.shape, dtype=self.output.dtype))
-            for t, hbuf in zip(g.inputs, self.host_inputs):
-                if self.zc_in:
-                    self.ext[t] = hbuf
-                    continue
-                d = self.ext[t]
-                N.check(lib.hz_prog_add_memcpy(self.prog, d.data_ptr(), hbuf.data_ptr(), d.numel() * d.element_size(),
-                                               0), "h2d")
-            if self.zc_out:
-                self.ext[g.outputs[0]] = self.host_output
-        if pair_convs is None:
-            pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
-        self.pairs = conv_pairs(g) if pair_convs else {}
-        self.chain_sync = None
-        i = 0
-        while i < len(g.nodes):
-            n = g.nodes[i]
-            if i in self.fused:
-                f = self.fused[i]
-                self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib))
-                i = f.end
-                continue
-            if chain is not None and i == chain[0]:
-                self._add_conv_chain(lib, chain[0], chain[1], conv_plans)
-                i = chain[1]
-                continue
-            if i in self.pairs:
-                self._add_conv_pair(lib, n, g.nodes[i + 1], conv_plans[i], conv_plans[i + 1], tuned)
-                i += 2
-                continue
-            self._add_node(lib, n, conv_plans[i])
-            i += 1
-        if host_io and not self.zc_out:
-            N.check(lib.hz_prog_add_memcpy(self.prog, self.host_output.data_ptr(), self.output.data_ptr(),
-                                           self.output.numel() * self.output.element_size(), 0), "d2h")
+        return conv_plans
 
     # ------------------------------------------------------------------
     def _chain_range(self, prefix: str):
@@ -325,6 +339,15 @@ class ExecContext:
             prm, _, _ = conv_ops.make_params(
                 addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
                 n.attrs.get("out_f32", False), cfg, kw, out_rowmajor=n.attrs.get("rowmajor", False))
+            if id(n) in self.seam_consumer:  # reads a seam's fp32 conv1 sum (ReLU at the load)
+                prm.x_f32 = 1
+            if id(n) in self.seam_init:  # presets the next seam's accumulator to conv1's bias
+                f = self.seam_init[id(n)]
+                t1 = f.nodes[1].outputs[0]
+                nb1, h1, w1, c1 = g.shape(t1)
+                prm.zinit, prm.zbias = addr(t1), self.params[f.nodes[1].attrs["w"]].bias.data_ptr()
+                prm.z_C, prm.z_HW = c1, h1 * w1
+                assert nb1 == nb
             self.configs.append((n.attrs.get("name", ""), key, cfg, kw))
             N.check(lib.hz_prog_add_conv(self.prog, C.byref(prm), cfg, n.slot), "add_conv")
         elif n.kind == "maxpool":

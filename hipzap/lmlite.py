@@ -180,12 +180,20 @@ class LMLiteBackend:
 
     def __init__(self, ckpt: str, itos_path: str, device: int = 0):
         t0 = time.perf_counter()
+        if os.environ.get("HIPZAP_LM_ENGINE", "batch") != "batch":
+            raise LMLiteError("HIPZAP_LM_ENGINE selects the torch engine pool")
         self.itos = load_itos(itos_path)
         self.stoi = make_stoi(self.itos)
+        # refuse a vocabulary mismatch BEFORE the engine exists (its scheduler thread, programs and
+        # device tables would otherwise stay allocated beside the torch fallback's engine)
+        enc = scan(ckpt).get("0.encoder.weight")
+        if enc is not None and enc.shape[0] > len(self.itos):
+            raise LMLiteError(f"vocabulary has {len(self.itos)} words, the checkpoint {enc.shape[0]} rows")
         self.engine = LMLiteEngine.for_vocab(ckpt, self.stoi, device=device,
                                              rows=int(os.environ.get("HIPZAP_LM_ROWS", 32)),
                                              unroll=int(os.environ.get("HIPZAP_LM_UNROLL", 8)))
-        if self.engine.V > len(self.itos):
+        if self.engine.V > len(self.itos):  # (the scan above already refused this)
+            self.engine.close()
             raise LMLiteError(f"vocabulary has {len(self.itos)} words, the checkpoint {self.engine.V} rows")
         self.cold_ms = (time.perf_counter() - t0) * 1e3
 

@@ -4,7 +4,14 @@ calls, total/avg/min/max duration, sorted by total. ``python scripts/rocpd_stats
 
 ``--timeline FIRST LAST``: instead, the dispatch timeline of one request -- on the stream with
 the most dispatches, the last complete run from a kernel whose name contains FIRST through the
-next one containing LAST (start offset, duration, grid, workgroup, VGPRs, name)."""
+next one containing LAST (start offset, duration, grid, workgroup, VGPRs, name).
+
+``--cutime FIRST LAST``: per-position CU-time accounting over EVERY complete request (FIRST ..
+LAST) of every stream: median duration, workgroups, waves per workgroup, CU-us = workgroups x
+duration / 256 CUs and wave-us = waves x duration / (256 CUs x 32 wave slots) of each dispatch
+position, plus each position's share of a request's summed kernel time (VERDICT r4 "next round"
+1a)."""
+import statistics
 import sqlite3
 import sys
 
@@ -33,8 +40,62 @@ def timeline(c, name, first, last):
     print("# no complete request found")
 
 
+def requests(c, name, first, last):
+    """[(stream, [rows of one request])] for every complete FIRST..LAST run on every stream."""
+    rows = c.execute(f"select stream_id, start, end, grid_x, workgroup_x, vgpr_count, {name} from kernels "
+                     "order by start").fetchall()
+    by: dict = {}
+    for r in rows:
+        by.setdefault(r[0], []).append(r)
+    out = []
+    for sid, rs in by.items():
+        cur = None
+        for r in rs:
+            if first in r[6]:
+                cur = [r]
+            elif cur is not None:
+                cur.append(r)
+                if last in r[6]:
+                    out.append((sid, cur))
+                    cur = None
+    return out
+
+
+def cutime(c, name, first, last, cus=256):
+    reqs = requests(c, name, first, last)
+    if not reqs:
+        print("# no complete request found")
+        return
+    n = statistics.mode(len(r) for _, r in reqs)
+    reqs = [r for _, r in reqs if len(r) == n]
+    span = statistics.median((r[-1][2] - r[0][1]) / 1e3 for r in reqs)
+    print(f"# {len(reqs)} requests of {n} dispatches; median request span {span:.1f} us")
+    print(f"{'pos':>3} {'dur_us':>7} {'wgs':>5} {'wv/wg':>5} {'CU-us':>7} {'wave-us':>7} {'pct':>5}  kernel")
+    tot = [0.0, 0.0, 0.0]
+    lines = []
+    for i in range(n):
+        d = statistics.median((r[i][2] - r[i][1]) / 1e3 for r in reqs)
+        gx, wx = reqs[0][i][3], reqs[0][i][4]
+        wgs = max(1, gx // max(1, wx))
+        wv = (wx + 63) // 64
+        cu, wave = wgs * d / cus, wgs * wv * d / (cus * 32)
+        tot[0] += d
+        tot[1] += cu
+        tot[2] += wave
+        lines.append((i, d, wgs, wv, cu, wave, reqs[0][i][6]))
+    for i, d, wgs, wv, cu, wave, nm in lines:
+        print(f"{i:3d} {d:7.2f} {wgs:5d} {wv:5d} {cu:7.3f} {wave:7.3f} {100 * d / tot[0]:5.1f}  {nm[:90]}")
+    print(f"# sum: {tot[0]:.1f} us kernel time, {tot[1]:.2f} CU-us, {tot[2]:.3f} wave-us per request "
+          "(profiled; durations inflate under the profiler)")
+
+
 def main():
     db = sys.argv[1]
+    if len(sys.argv) > 4 and sys.argv[2] == "--cutime":
+        c = sqlite3.connect(db)
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+        cutime(c, "kernel_name" if "kernel_name" in cols else "name", sys.argv[3], sys.argv[4])
+        return
     if len(sys.argv) > 4 and sys.argv[2] == "--timeline":
         c = sqlite3.connect(db)
         cols = [r[1] for r in c.execute("pragma table_info(kernels)")]

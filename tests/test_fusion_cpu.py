@@ -142,3 +142,45 @@ def test_a_run_whose_intermediate_is_read_elsewhere_is_not_fused(r50):
     fz2 = fusion.plan(g, params, fusion.enabled_kinds("all"))
     assert [f.kind for f in fz2.values()].count("bneck2") == 3
     assert b2[1].start not in fz2
+
+
+def test_resnet50_seams(r50):
+    """layer3 has five conv3 -> conv1 seams, layer4 two (the first block of a stage starts with its
+    downsample + conv1 pair, so no seam crosses a stage boundary); each seam's accumulator is
+    planned as fp32 and is live from the 3x3 conv that presets it to the one that reads it."""
+    from hipzap.engine.graph import plan_memory
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam", batch=1, input_uint8=True)
+    seams = [f for f in fz.values() if f.kind == "seam"]
+    names = [(f.nodes[0].attrs["name"], f.nodes[1].attrs["name"]) for f in seams]
+    assert names == [(f"layer3.{b}.conv3", f"layer3.{b + 1}.conv1") for b in range(5)] + \
+        [(f"layer4.{b}.conv3", f"layer4.{b + 1}.conv1") for b in range(2)]
+    for f in seams:
+        assert g.nodes[f.init].attrs["name"].endswith("conv2") and g.nodes[f.consumer].attrs["name"].endswith("conv2")
+        assert f.end == f.start + 2 and f.init == f.start - 1 and f.consumer == f.end
+    # the block fusions are unchanged next to the seams
+    assert [f.kind for f in fz.values() if f.kind != "seam"] == ["convpool"] + ["bneck"] * 3 + ["bneck2"] * 4
+    gp = fusion.planning_graph(g, fz)
+    assert gp is not g and g.tensors[seams[0].nodes[1].outputs[0]].dtype == torch.bfloat16
+    offsets, _ = plan_memory(gp, groups=[(f.start, f.end) for f in fz.values()])
+    for f in seams:
+        t1 = f.nodes[1].outputs[0]
+        assert gp.tensors[t1].dtype == torch.float32 and t1 in gp.nodes[f.init].outputs
+        z0, z1 = offsets[t1], offsets[t1] + gp.tensors[t1].nbytes
+        # no tensor touched from the presetting conv through the reader shares the accumulator's bytes
+        for j in range(f.init, f.consumer + 1):
+            for t in g.nodes[j].inputs + g.nodes[j].outputs:
+                if t == t1 or t is None or g.tensors[t].external:
+                    continue
+                o0, o1 = offsets[t], offsets[t] + gp.tensors[t].nbytes
+                assert o1 <= z0 or z1 <= o0, (g.nodes[j].attrs.get("name"), g.tensors[t].name)
+
+
+def test_seams_need_the_layer3_layer4_geometry(r50):
+    a, params, kw = r50
+    _, fz = _plan(a, params, kw, "seam", batch=2, input_uint8=False)
+    assert sum(f.kind == "seam" for f in fz.values()) == 7
+    r18 = registry.get("resnet18")
+    p18, kw18 = r18.pack(randomize_bn(r18.make_model()).eval().state_dict(), "cpu")
+    _, fz18 = _plan(r18, p18, kw18, "seam", batch=1, input_uint8=True)
+    assert fz18 == {}  # basic blocks: no 1x1 -> 1x1 seam

@@ -1,0 +1,166 @@
+"""ResNet 1x1 -> 1x1 seams (csrc/block.hip seam_kernel, engine/fusion.py ``seam``) on MI355X.
+
+* the kernel alone against an fp32 PyTorch oracle of the same op: y = relu(W3 t2 + b3 + res) and
+  z = b1 + W1 y (layer3 and layer4 geometry, both slice widths, N > 1, a pixel count that is not a
+  multiple of the 32-pixel tile);
+* the consumer side: a 3x3 conv reading z (fp32, ReLU at the load) and presetting the next
+  accumulator (HzConvParams.zinit) against the same conv on relu(z) in bf16;
+* ResNet-50 with seams against the per-conv program and the fp32 graph oracle: every block output
+  a seam writes, the logits, with the arena's default reuse and without, eager and graph replay;
+  7 dispatches fewer.
+Atomic accumulation order varies run to run, so comparisons are within fp32/bf16 rounding, not
+bitwise."""
+import ctypes as C
+
+import pytest
+import torch
+
+from hipzap import _native as N
+from hipzap.engine import fusion
+from hipzap.engine.program import ExecContext
+from hipzap.engine.reference import run_graph_reference
+from hipzap.models import registry
+from hipzap.models.resnet import randomize_bn
+from hipzap.ops import conv as CV
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SEAMS = "convpool,bneck,bneck2,seam"
+
+
+def _rel(a, b):
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
+
+
+def _blk(x_nhwc):  # logical NHWC -> channel-blocked device layout
+    return CV.to_blocked(x_nhwc).to(DEV)
+
+
+@pytest.mark.parametrize("cm,cs,n,h", [(256, 128, 1, 14), (256, 64, 1, 14), (512, 64, 1, 7), (512, 128, 1, 7),
+                                       (256, 128, 2, 10), (512, 64, 3, 7)])
+def test_seam_kernel_vs_fp32(cm, cs, n, h):
+    g = torch.Generator().manual_seed(cm + cs + n)
+    co = 4 * cm
+    w3 = torch.randn(co, cm, 1, 1, generator=g) * (2.0 / cm) ** 0.5
+    w1 = torch.randn(cm, co, 1, 1, generator=g) * (2.0 / co) ** 0.5
+    p3 = CV.pack_conv(w3, 0.1 * torch.randn(co, generator=g))
+    p1 = CV.pack_conv(w1, 0.1 * torch.randn(cm, generator=g))
+    t2 = torch.relu(torch.randn(n, h, h, cm, generator=g)).to(torch.bfloat16)
+    res = torch.randn(n, h, h, co, generator=g).to(torch.bfloat16)
+    # oracle: fp32 on the bf16 operands; y rounded to bf16 before conv1 (as the kernel feeds it)
+    W3, W1 = p3.dense(), p1.dense()
+    y_ref = torch.relu(t2.float() @ W3.t() + p3.bias + res.float())
+    z_ref = p1.bias + y_ref.to(torch.bfloat16).float() @ W1.t()
+    p3d, p1d = p3.to(DEV), p1.to(DEV)
+    t2d, resd = _blk(t2), _blk(res)
+    y = torch.zeros(n, co // 32, h, h, 32, dtype=torch.bfloat16, device=DEV)
+    z = p1d.bias.view(1, cm // 32, 1, 1, 32).expand(n, cm // 32, h, h, 32).contiguous()  # the preset
+    prm = fusion.SeamParams()
+    prm.t2, prm.w3, prm.b3, prm.res, prm.y = t2d.data_ptr(), p3d.wf.data_ptr(), p3d.bias.data_ptr(), resd.data_ptr(), \
+        y.data_ptr()
+    prm.w1, prm.z, prm.N, prm.HW, prm.CM, prm.cs = p1d.wf.data_ptr(), z.data_ptr(), n, h * h, cm, cs
+    fusion.launch("seam", prm)
+    torch.cuda.synchronize()
+    y_got = CV.from_blocked(y.cpu(), (n, h, h, co)).float()
+    z_got = CV.from_blocked(z.cpu(), (n, h, h, cm))
+    assert _rel(y_got, y_ref) < 1e-2, _rel(y_got, y_ref)
+    assert _rel(z_got, z_ref) < 2e-3, _rel(z_got, z_ref)
+
+
+def test_seam_launch_refuses_bad_geometry():
+    prm = fusion.SeamParams()
+    buf = torch.zeros(1 << 20, device=DEV)
+    for f in ("t2", "w3", "b3", "res", "y", "w1", "z"):
+        setattr(prm, f, buf.data_ptr())
+    prm.N, prm.HW, prm.CM, prm.cs = 1, 196, 384, 128
+    assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
+    prm.CM, prm.cs = 256, 96
+    assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
+
+
+@pytest.mark.parametrize("cfg,kw", [(3, 16), (3, 8), (0, 4), (4, 8)])
+def test_conv_fp32_relu_input_and_zinit(cfg, kw):
+    """3x3 conv on fp32 z with ReLU at the load == the same conv on relu(z) in bf16, and the
+    launch presets the next accumulator to its bias."""
+    g = torch.Generator().manual_seed(cfg * 16 + kw)
+    n, h, cm = 1, 14, 256
+    z = torch.randn(n, h, h, cm, generator=g)
+    pc = CV.pack_conv(torch.randn(cm, cm, 3, 3, generator=g) * (2.0 / (9 * cm)) ** 0.5, 0.1 * torch.randn(cm), None,
+                      1, 1).to(DEV)
+    want = CV.conv2d_nhwc(torch.relu(z).to(torch.bfloat16).contiguous().to(DEV), pc, act="relu", cfg=cfg, kw=kw)
+    zd = _blk(z)
+    out = torch.zeros(n, cm // 32, h, h, 32, dtype=torch.bfloat16, device=DEV)
+    nxt = torch.full((n, cm // 32, h, h, 32), float("nan"), device=DEV)
+    zb = torch.randn(cm, generator=g).to(DEV)
+    prm, _, _ = CV.make_params(zd.data_ptr(), pc, n, h, h, out.data_ptr(), 0, "relu", False, cfg, kw)
+    prm.x_f32, prm.zinit, prm.zbias, prm.z_C, prm.z_HW = 1, nxt.data_ptr(), zb.data_ptr(), cm, h * h
+    N.check(N.lib().hz_conv_launch(prm, cfg, N.stream_ptr()), "hz_conv_launch")
+    torch.cuda.synchronize()
+    got = CV.from_blocked(out.cpu(), (n, h, h, cm))
+    assert torch.equal(got, want.cpu())  # same bf16 operands, same kernel, same K order
+    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, h, h, cm)), zb.cpu().expand(n, h, h, cm))
+
+
+@pytest.fixture(scope="module")
+def r50():
+    torch.manual_seed(0)
+    a = registry.get("resnet50")
+    sd = randomize_bn(a.make_model()).eval().state_dict()
+    params, kw = a.pack({k: v.to(DEV) for k, v in sd.items()}, torch.device(DEV))
+    params_cpu, _ = a.pack(sd, "cpu")
+    return a, params, params_cpu, kw
+
+
+def _run(ctx, x):
+    ctx.input.copy_(x.to(ctx.input.device))
+    ctx.run()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("batch,noreuse", [(1, True), (1, False), (2, True)])
+def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, monkeypatch):
+    if noreuse:
+        monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
+    else:
+        monkeypatch.delenv("HIPZAP_ARENA_NOREUSE", raising=False)
+    a, params, params_cpu, kw = r50
+    g = a.build_graph(batch=batch, **dict(kw, input_uint8=True))
+    seam = ExecContext(g, params, torch.device(DEV), fuse=SEAMS)
+    plain = ExecContext(g, params, torch.device(DEV), fuse="none")
+    assert sum(f.kind == "seam" for f in seam.fused.values()) == 7
+    x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    _run(seam, x)
+    _run(plain, x)
+    ref = run_graph_reference(g, params_cpu, [x])
+    if noreuse:  # every block output a seam writes
+        for f in seam.fused.values():
+            if f.kind != "seam":
+                continue
+            tid = f.nodes[0].outputs[0]
+            ys = CV.from_blocked(seam.view(tid).reshape(-1), g.shape(tid)).float().cpu()
+            yp = CV.from_blocked(plain.view(tid).reshape(-1), g.shape(tid)).float().cpu()
+            assert _rel(ys, yp) < 2e-2 and _rel(ys, ref[tid].float()) < 3e-2, f.nodes[0].attrs["name"]
+    ls, lp = seam.output.float().cpu().reshape(batch, -1), plain.output.float().cpu().reshape(batch, -1)
+    lr = ref[g.outputs[0]].reshape(batch, -1)
+    assert _rel(ls, lr) < 3e-2 and _rel(ls, lp) < 3e-2, (_rel(ls, lr), _rel(ls, lp))
+    assert torch.equal(ls.argmax(1), lp.argmax(1))
+
+
+def test_resnet50_seam_dispatches_and_replay(r50):
+    a, params, _, kw = r50
+    g = a.build_graph(batch=1, **dict(kw, input_uint8=True))
+    base = ExecContext(g, params, torch.device(DEV), fuse="convpool,bneck,bneck2")
+    ctx = ExecContext(g, params, torch.device(DEV), fuse=SEAMS)
+    assert base.num_ops() - ctx.num_ops() == 7
+    assert ctx.num_ops() <= 31
+    s = torch.cuda.Stream()
+    ctx.capture(s)
+    for seed in range(4):  # the replayed accumulators are preset again on every replay
+        x = torch.randint(0, 256, (1, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(seed))
+        _run(base, x)
+        with torch.cuda.stream(s):
+            ctx.input.copy_(x.to(DEV))
+            ctx.replay(s)
+        torch.cuda.synchronize()
+        lb, lc = base.output.float().cpu(), ctx.output.float().cpu()
+        assert _rel(lc, lb) < 2e-2 and torch.equal(lc.argmax(-1), lb.argmax(-1))
