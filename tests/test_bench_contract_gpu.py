@@ -30,3 +30,8 @@ def test_bench_prints_one_contract_line():
     assert d["config"]["model"] == "ResNet-50" and d["config"]["global_batch"] == 1
     assert d["config"]["parallelism"] == "dp1" and d["config"]["streams_per_gpu"] == 2
     assert "vs_baseline" in d
+    # one step = requests_per_stream_per_step requests on every stream: value is those requests over
+    # exactly the timed region (steps x ms_per_step)
+    rps = d["config"]["requests_per_stream_per_step"]
+    assert rps >= 1
+    assert abs(d["value"] - 2 * rps * 1e3 / d["ms_per_step"]) / d["value"] < 0.01

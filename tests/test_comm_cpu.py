@@ -92,3 +92,21 @@ def test_dp_scatter_gather_world2_uneven():
     expect = (x.sum(dim=(1, 2)) + torch.tensor([0, 0, 0, 1000, 1000])).tolist()
     assert y == expect
     assert sorted(m[2] for m in msgs if m[0] == "shard") == [3, 3]
+
+
+def test_mapped_rccl_report_parses_maps():
+    """The bench's per-rank RCCL report: the librccl paths a process mapped (torch's bundled copy
+    flagged), read from /proc/self/maps."""
+    from hipzap.parallel.rccl import mapped_rccl
+    maps = "\n".join([
+        "7f00-7f10 r-xp 00000000 08:01 1 /usr/lib/libc.so.6",
+        "7f10-7f20 r-xp 00000000 08:01 2 /usr/local/lib/python3.10/dist-packages/torch/lib/librccl.so",
+        "7f20-7f30 r--p 00100000 08:01 2 /usr/local/lib/python3.10/dist-packages/torch/lib/librccl.so",
+        "7f30-7f40 rw-p 00000000 00:00 0 ",
+    ])
+    r = mapped_rccl(maps)
+    assert r["paths"] == ["/usr/local/lib/python3.10/dist-packages/torch/lib/librccl.so"]
+    assert r["torch_bundled"] is True
+    assert mapped_rccl("7f00-7f10 r-xp 00000000 08:01 1 /opt/rocm/lib/librccl.so.1")["torch_bundled"] is False
+    live = mapped_rccl()  # this process: whatever is mapped, a well-formed report
+    assert set(live) == {"paths", "version", "torch_bundled", "has_comm_shrink"}
