@@ -109,21 +109,6 @@ class LmbAdmitParams(C.Structure):
 
 
 HZ_K_LMB_LAYER, HZ_K_LMB_DEC, HZ_K_LMB_ADMIT = 14, 15, 16
-HZ_K_CONV_CHAIN = 17
-HZ_CHAIN_MAX_STAGES, HZ_CHAIN_SYNC_STRIDE = 48, 32
-
-
-class ChainLayer(C.Structure):  # HzChainLayer (csrc/hipzap.h): one conv of a persistent chain
-    _fields_ = [("p", ConvParams), ("cfg", c_int), ("stage", c_int), ("dep_x", c_int), ("dep_res", c_int),
-                ("tiles", c_int), ("is1x1", c_int), ("pad_", c_int * 2)]
-
-
-class ConvChainParams(C.Structure):  # HzConvChainParams
-    _fields_ = [("layers", c_void_p), ("sync", c_void_p), ("trace", c_void_p), ("n_layers", c_int), ("n_stages", c_int), ("grid", c_int),
-                ("lds", c_int), ("spin_limit", C.c_uint), ("pad_", c_int),
-                ("stage_tiles", c_int * HZ_CHAIN_MAX_STAGES)]
-
-
 class PackConvParams(C.Structure):  # csrc/pack.hip (torch-free checkpoint cold start)
     _fields_ = [("w", c_void_p), ("gamma", c_void_p), ("beta", c_void_p), ("mean", c_void_p), ("var", c_void_p),
                 ("bias_in", c_void_p), ("wf", c_void_p), ("bias_out", c_void_p), ("cout", c_int), ("cin", c_int),
@@ -151,8 +136,6 @@ def _load():
     P = c_void_p
     _sig(lib, "hz_conv_launch", c_int, C.POINTER(ConvParams), c_int, P)
     _sig(lib, "hz_conv2_launch", c_int, C.POINTER(ConvParams), C.POINTER(ConvParams), c_int, P)
-    _sig(lib, "hz_conv_chain_prepare", c_int, C.POINTER(ChainLayer), c_int, C.POINTER(c_int), c_int)
-    _sig(lib, "hz_conv_chain_launch", c_int, C.POINTER(ConvChainParams), P)
     _sig(lib, "hz_maxpool_launch", c_int, C.POINTER(PoolParams), P)
     _sig(lib, "hz_avgpool_launch", c_int, P, P, c_int, c_int, c_int, c_int, P)
     _sig(lib, "hz_preprocess_launch", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P)
@@ -277,8 +260,8 @@ def lib():
 
 
 def experiments() -> bool:
-    """The loaded library carries the HZ_EXPERIMENTS kernels (chain conv, M32 / LN-fold GEMM tiles,
-    256-row MX pipelines): ``python -m hipzap.build --experiments``, ``HIPZAP_LIB=.../libhipzap_exp.so``."""
+    """The loaded library carries the HZ_EXPERIMENTS kernels (M32 / LN-fold GEMM tiles, LM ring variants):
+    ``python -m hipzap.build --experiments``, ``HIPZAP_LIB=.../libhipzap_exp.so``."""
     return bool(lib().hz_experiments())
 
 

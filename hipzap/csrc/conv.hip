@@ -57,17 +57,8 @@ struct Depth {
 // keep the register ring out of scratch: 1024 threads cap a wave at 128 VGPRs
 constexpr int conv_max_threads(int nf) { return nf >= 16 ? 256 : nf >= 8 ? 512 : 1024; }
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-// Activation fragment load. SC1 (conv_chain_kernel): a `buffer_load_dwordx4 ... sc1`, which
-// bypasses this CU's L1, so bytes another workgroup of the SAME launch wrote (write-through, see
-// the epilogue) are read fresh with no acquire fence (MI355X_MICROARCH.md § visibility, Valid
-// forms: every store of the handed-off bytes sc1 + drained before the counter add, every load sc1).
-template <bool SC1>
-__device__ __forceinline__ bf16x8 ld_act(const bf16_t* X, long off, __amdgpu_buffer_rsrc_t rs) {
-  if constexpr (SC1) return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 2), 0, 16));
-  else return *reinterpret_cast<const bf16x8*>(X + off);
+__device__ __forceinline__ bf16x8 ld_act(const bf16_t* X, long off) {
+  return *reinterpret_cast<const bf16x8*>(X + off);
 }
 
 // fp32 activation fragment (HzConvParams.x_f32: a ResNet seam's conv1 sum, block.hip seam_kernel):
@@ -81,9 +72,8 @@ __device__ __forceinline__ bf16x8 f32relu_bf16(const f32x4& a, const f32x4& b) {
 }
 
 // One output tile of one conv problem; `lid` = logical tile id (already XCD-remapped).
-// SC1: the tile runs inside conv_chain_kernel (in-launch producer/consumer hand-offs).
 // F32IN: fp32 input with ReLU at the load (3x3 convs only; HzConvParams.x_f32).
-template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool SC1 = false, bool F32IN = false>
+template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool F32IN = false>
 __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) {
   constexpr int DEPTH = Depth<FC, FP>::value;
   constexpr int NF = FC * FP;
@@ -138,8 +128,6 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     }
   }
   const bf16_t* __restrict__ X = p.x;
-  // (used by SC1 loads only; dead otherwise)
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
   // fragment-major weights: fragment (row group g, k-step s) at ((g*ksteps + s)*64 + lane)*8
   const bf16_t* __restrict__ Wf = p.w + ((long)(n0 >> 4) * steps) * 512 + lane * 8;
 
@@ -198,7 +186,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
           const long off = ((long)(pb[j] + cb * HW) << 5) + lk;
-          if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) b[j] = ld_act<SC1>(X, off, xrs);
+          if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) b[j] = ld_act(X, off);
           else b[j] = bf16x8{};
         }
       } else {
@@ -216,7 +204,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
               rw[j][0] = rw[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
           } else {
-            if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) b[j] = ld_act<SC1>(X, off, xrs);
+            if (v && HZ_DCHECK(off >= 0 && off + 8 <= xlim)) b[j] = ld_act(X, off);
             else b[j] = bf16x8{};
           }
         }
@@ -308,12 +296,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
     if (!HZ_DCHECK(o >= 0 && o + 4 <= olim)) return;
     if (p.res) {
       u32x2 rr;
-      if constexpr (SC1) {  // written earlier in the same launch: an sc1 load (see ld_act)
-        const unsigned long long r64 = __hip_atomic_load((gu64*)(p.res + o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rr = u32x2{(unsigned)r64, (unsigned)(r64 >> 32)};
-      } else {
-        rr = PF ? pf_res[i][j] : *reinterpret_cast<const u32x2*>(p.res + o);
-      }
+      rr = PF ? pf_res[i][j] : *reinterpret_cast<const u32x2*>(p.res + o);
       v[0] += __uint_as_float(rr[0] << 16);
       v[1] += __uint_as_float(rr[0] & 0xffff0000u);
       v[2] += __uint_as_float(rr[1] << 16);
@@ -329,10 +312,7 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
     }
-    if constexpr (SC1) {  // write-through (sc1) 8-B store: the bytes leave this XCD's L2 for the consumers
-      const unsigned long long w64 = (unsigned long long)pack2(v[0], v[1]) | ((unsigned long long)pack2(v[2], v[3]) << 32);
-      __hip_atomic_store((gu64*)(reinterpret_cast<bf16_t*>(p.out) + o), w64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (p.out_f32) {
+    if (p.out_f32) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
     } else {
       *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
@@ -386,7 +366,7 @@ __device__ __forceinline__ void zfill(const HzConvParams& p) {
 
 template <int FC, int FP, bool FAST, bool IS1X1, bool XROW, bool F32IN = false>
 __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv_kernel(const HzConvParams p) {
-  conv_tile<FC, FP, FAST, IS1X1, XROW, false, F32IN>(p, xcd_remap(blockIdx.x, gridDim.x));
+  conv_tile<FC, FP, FAST, IS1X1, XROW, F32IN>(p, xcd_remap(blockIdx.x, gridDim.x));
   if (p.zinit) zfill(p);
 }
 
@@ -495,147 +475,6 @@ extern "C" int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int
   }
 }
 
-#if HZ_EXPERIMENTS
-// ---------------------------------------------------------------------------------------------
-// Persistent conv chain (HzConvChainParams, hipzap.h): a run of dependent convs -- e.g. ResNet-50
-// layer3 + layer4 at bs=1, 26 convs in 17 stages -- as ONE launch instead of one launch per conv.
-// Stage hand-off (MI355X_MICROARCH.md § visibility, Valid forms, row "agent-scope atomic adds, one
-// lane of each storing workgroup"): every output store of a chain tile is an 8-B sc1 store; every
-// storing wave drains (s_waitcnt vmcnt(0)); a workgroup barrier; then ONE lane adds the
-// workgroup's tile count to the stage counter (agent-scope atomic). A consumer workgroup's lane 0
-// polls the counters of the stages its tiles read (sc1 loads, s_sleep between polls) and the
-// workgroup barrier releases the other waves, whose activation / residual loads are all sc1
-// (ld_act, epilogue). Weights and biases are never written in the launch: plain loads.
-namespace {
-
-__device__ __forceinline__ void chain_wait(unsigned* sync, int stage, unsigned target, unsigned limit, unsigned* err) {
-  if (stage < 0) return;  // written before the launch
-  gu32* c = (gu32*)(sync + stage * HZ_CHAIN_SYNC_STRIDE);
-  unsigned spins = 0;
-  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(2);
-    ++spins;
-    // give up (flag it, never hang the GPU); once any wait of the launch gave up, the others
-    // stop waiting too, so a broken launch still ends in about one spin_limit
-    if (spins > limit || ((spins & 63) == 0 && __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_fetch_or((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-}
-
-template <int FC, int FP>
-__device__ __forceinline__ void chain_tile2(const HzConvParams& p, bool is1x1, int t) {
-  if (is1x1) conv_tile<FC, FP, true, true, false, true>(p, t);
-  else conv_tile<FC, FP, true, false, false, true>(p, t);
-}
-
-__device__ __forceinline__ void chain_tile(const HzChainLayer& L, int t) {
-  switch (L.cfg) {
-    case 0: chain_tile2<1, 1>(L.p, L.is1x1, t); break;
-    case 1: chain_tile2<1, 2>(L.p, L.is1x1, t); break;
-    case 3: chain_tile2<2, 1>(L.p, L.is1x1, t); break;
-    case 4: chain_tile2<2, 2>(L.p, L.is1x1, t); break;
-    case 6: chain_tile2<4, 1>(L.p, L.is1x1, t); break;
-    default: break;  // rejected by hz_conv_chain_prepare
-  }
-}
-
-constexpr int kChainThreads = 512;  // 8 waves split every tile's K (kw = 8)
-
-__global__ __launch_bounds__(kChainThreads, 4) void conv_chain_kernel(const HzConvChainParams cp) {
-  const HzChainLayer* __restrict__ L = cp.layers;
-  unsigned* sync = cp.sync;
-  unsigned* err = sync + (cp.n_stages + 1) * HZ_CHAIN_SYNC_STRIDE;
-  const int G = gridDim.x, b = blockIdx.x;
-  int li = 0;
-  for (int s = 0; s < cp.n_stages; ++s) {
-    const int total = cp.stage_tiles[s];
-    int lj = li;
-    while (lj < cp.n_layers && L[lj].stage == s) ++lj;
-    if (b < total) {
-      unsigned long long* tr = cp.trace ? cp.trace + ((long)b * cp.n_stages + s) * 3 : nullptr;
-      if (tr && threadIdx.x == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
-      if (threadIdx.x == 0) {
-        for (int l = li; l < lj; ++l) {
-          const int dx = L[l].dep_x, dr = L[l].dep_res;
-          if (dx >= 0) chain_wait(sync, dx, cp.stage_tiles[dx], cp.spin_limit, err);
-          if (dr >= 0) chain_wait(sync, dr, cp.stage_tiles[dr], cp.spin_limit, err);
-        }
-      }
-      __syncthreads();
-      if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
-      unsigned mine = 0;
-      for (int t = b; t < total; t += G) {
-        int l = li, tt = t;
-        while (tt >= L[l].tiles) tt -= L[l++].tiles;
-        chain_tile(L[l], tt);
-        ++mine;
-        __syncthreads();  // conv_tile's LDS reduction buffer is reused by the next tile
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
-      __syncthreads();
-      if (tr && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
-      if (threadIdx.x == 0)
-        __hip_atomic_fetch_add((gu32*)(sync + s * HZ_CHAIN_SYNC_STRIDE), mine, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    li = lj;
-  }
-  // the last workgroup out resets the stage counters for the next replay (stream-ordered after
-  // this launch); the timeout word is left for the host
-  if (threadIdx.x == 0) {
-    gu32* done = (gu32*)(sync + cp.n_stages * HZ_CHAIN_SYNC_STRIDE);
-    const unsigned tk = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == (unsigned)G - 1) {
-      for (int s = 0; s < cp.n_stages; ++s)
-        __hip_atomic_store((gu32*)(sync + s * HZ_CHAIN_SYNC_STRIDE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-}  // namespace
-
-extern "C" int hz_conv_chain_prepare(HzChainLayer* layers, int n_layers, int* stage_tiles, int n_stages) {
-  if (n_layers < 1 || n_stages < 1 || n_stages > HZ_CHAIN_MAX_STAGES) return -1;
-  int lds = 0;
-  for (int s = 0; s < n_stages; ++s) stage_tiles[s] = 0;
-  for (int i = 0; i < n_layers; ++i) {
-    HzChainLayer& L = layers[i];
-    HzConvParams& p = L.p;
-    const int fc = 1 << (L.cfg / 3), fp = 1 << (L.cfg % 3);
-    const bool cfg_ok = L.cfg == 0 || L.cfg == 1 || L.cfg == 3 || L.cfg == 4 || L.cfg == 6;
-    const bool ok = cfg_ok && check_params(p) == 0 && p.C % 32 == 0 && !p.x_rowmajor && !p.out_rowmajor &&
-                    !p.out_f32 && p.lnf == nullptr && L.stage >= 0 && L.stage < n_stages &&
-                    (i == 0 || L.stage >= layers[i - 1].stage) && L.dep_x < L.stage && L.dep_res < L.stage &&
-                    (long)p.N * p.C * p.H * p.W * 2 < 0x7fffffffL;
-    if (!ok) return -(100 + i);
-    p.kw = kChainThreads / 64;
-    p.tiles_n = (p.Cout + fc * 16 - 1) / (fc * 16);
-    L.tiles = p.tiles_n * ((p.M + fp * 16 - 1) / (fp * 16));
-    L.is1x1 = p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0;
-    stage_tiles[L.stage] += L.tiles;
-    const int need = p.kw * fc * fp * 64 * 16;
-    lds = need > lds ? need : lds;
-  }
-  for (int s = 0; s < n_stages; ++s)
-    if (stage_tiles[s] == 0) return -2;  // every stage holds at least one layer
-  return lds;
-}
-
-extern "C" int hz_conv_chain_launch(const HzConvChainParams* cpp, hipStream_t st) {
-  const HzConvChainParams& cp = *cpp;
-  if (cp.grid < 1 || cp.grid > 1024 || cp.n_stages < 1 || cp.n_stages > HZ_CHAIN_MAX_STAGES || !cp.layers || !cp.sync)
-    return -1;
-  hipLaunchKernelGGL(conv_chain_kernel, dim3(cp.grid), dim3(kChainThreads), (size_t)cp.lds, st, cp);
-  return (int)hipGetLastError();
-}
-
-#else   // !HZ_EXPERIMENTS: the chain kernel is not in the product library
-extern "C" int hz_conv_chain_prepare(HzChainLayer*, int, int*, int) { return -99; }
-extern "C" int hz_conv_chain_launch(const HzConvChainParams*, hipStream_t) { return -99; }
-#endif
 
 // Load this translation unit's device code now (hipFuncGetAttributes makes the runtime load the
 // code object of the fatbin that holds the kernel, without a launch or a stream): the plan loader

@@ -457,437 +457,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
-#if HZ_EXPERIMENTS
-// ---- ping-pong MX GEMM (VERDICT r3 "next round" 6; cdna_hip_programming.md ping-pong) ----
-// cfg 24's 128x128 tile and wave map (wave (wm, wn): tokens wm*64.., features wn*32..) with the two
-// wave groups a phase apart: group 0 (wm = 0, one wave per SIMD) reads its operands of K-step t
-// from LDS while group 1 (the other wave on each SIMD) issues its MFMAs of t - 1, then they swap,
-// so on every SIMD one wave's LDS reads overlap the other's MFMAs instead of both waiting on
-// their reads together. Two barriers per K-step; the MFMA group raises its issue priority. NS LDS
-// stages: stage t + NS - 1 is issued right after the barrier that retires the last reads of
-// buffer (t - 1) % NS; counted vmcnt waits keep the later stages in flight across barriers. Same
-// LDS images, swizzle, hardware K order, per-wave accumulation order and epilogue as cfg 24:
-// bitwise equal to it (tests/test_fp8_gpu.py). Per-row activation scales only (XS = false).
-template <int NS>
-__global__ __launch_bounds__(512) void gemm_mxpp_kernel(const HzGemmFp8Params p, int group_m) {
-  constexpr int BM = 128, BN = 128, WM = 2, WN = 4, NW = 8;
-  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 2, 4
-  constexpr int NWG = BN / 16;
-  constexpr int XBYTES = BM * 128, WBYTES = NWG * 2048, SBYTES = XBYTES + WBYTES;
-  constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;  // 2, 2
-  constexpr int G = XPW + WPW;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;  // wm = the wave's group
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  int tile_m, tile_n;
-  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
-  const int n0 = tile_n * BN, m0 = tile_m * BM;
-  const int kb = p.K >> 7;
-
-  const unsigned char* xsrc[XPW];
-#pragma unroll
-  for (int i = 0; i < XPW; ++i) {
-    const int q = wave + NW * i;
-    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
-    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
-    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
-  }
-  const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
-  auto stage = [&](int buf, int st) {
-    char* base = smem + buf * SBYTES;
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
-#pragma unroll
-    for (int i = 0; i < WPW; ++i) {
-      const int piece = wave + NW * i;
-      const int g = piece >> 1, h = piece & 1;
-      glds16_8(wsrc + ((long)g * kb + st) * 2048 + h * 1024, base + XBYTES + piece * 1024);
-    }
-  };
-  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
-  const int brow = (wm * (BM / WM) + lr) * 128;
-  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
-  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
-  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
-
-  f32x4 acc[FCW][FPW];
-#pragma unroll
-  for (int i = 0; i < FCW; ++i)
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x8 a[FCW], b[FPW];
-  auto read = [&](int st) {
-    const char* base = smem + (st % NS) * SBYTES;
-#pragma unroll
-    for (int i = 0; i < FCW; ++i) {
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048);
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048 + 1024);
-      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) {
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + boff0 + j * 16 * 128);
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + j * 16 * 128);
-      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-  };
-  auto mfma = [&]() {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FCW; ++i)
-#pragma unroll
-      for (int j = 0; j < FPW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
-                                                                      0x7f7f7f7f);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < kb) stage(s0, s0);
-  // K-step t: phase 0 = group 0 reads t | group 1 multiplies t - 1; phase 1 = group 0 multiplies
-  // t | group 1 reads t. One extra round lets group 1 multiply the last K-step.
-  for (int st = 0; st <= kb; ++st) {
-    if (st < kb) {  // this wave's pieces of stage st landed (later stages may stay in flight)
-      const int ahead = min(NS - 2, kb - 1 - st);
-      if (NS > 3 && ahead >= 2) wait_vm8<(NS > 3 ? 2 * G : 0)>();
-      else if (NS > 2 && ahead >= 1) wait_vm8<(NS > 2 ? G : 0)>();
-      else wait_vm8<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // stage st complete; buffer (st - 1) % NS read by both groups
-    __builtin_amdgcn_sched_barrier(0);
-    if (st + NS - 1 < kb) stage((st + NS - 1) % NS, st + NS - 1);
-    if (wm == 0) {
-      if (st < kb) read(st);
-    } else if (st >= 1) {
-      mfma();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (st < kb) {
-      if (wm == 0) mfma();
-      else read(st);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
-}
-
-template <int NS>
-int launch_mxpp(const HzGemmFp8Params& p, hipStream_t st) {
-  if (p.N % 128 || p.xs) return -4;  // full 128-wide feature tiles, per-row activation scales only
-  const int tiles = (p.N / 128) * ((p.M + 127) / 128);
-  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
-  const int group_m = group_env < 1 ? 1 : group_env;
-  hipLaunchKernelGGL(gemm_mxpp_kernel<NS>, dim3(tiles), dim3(512), 0, st, p, group_m);
-  return (int)hipGetLastError();
-}
-
-#endif  // HZ_EXPERIMENTS
-
-// ---- 256-row MX GEMM (ViT-B/16 fp8 at batch 64: M = 12,608): measured, never chosen ----
-// A 256 x BN tile moves half the staging bytes per FLOP of the 128x128 tiles (BN = 256: 64 KB per
-// k-step for 16.8 MFLOP) with ONE 8-wave workgroup per CU, wave (wm, wn) owning 128 tokens x BN/4
-// features. Same LDS images, swizzle, hardware K order, block scales and epilogue as
-// gemm_mx_kernel. The main k-loop is branch-free (the last NS-1 k-steps, which stage nothing, are
-// a peeled tail); per step: barrier -> the next stage's glds pieces -> token fragment 0, W, token
-// fragment 1 reads -> MFMAs of token fragment f while f+1 / f+2 reads are in flight;
-// sched_barrier(0) pins that order. Measured on the ViT shapes (profiles/r3_mx256): 1.3-1.5x
-// SLOWER than the 8-wave 128x128 tile at two workgroups per CU (QKV 65-74 vs 50 us): with one
-// workgroup per CU the staging latency is not hidden, whatever the in-step order; the tuner keeps
-// these as candidates (cfg 43-45) and never picks them.
-template <int BN, int NS, bool XS>
-__global__ __launch_bounds__(512) void gemm_mxq_kernel(const HzGemmFp8Params p, int group_m) {
-  constexpr int BM = 256, WM = 2, WN = 4, NW = 8;
-  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;
-  constexpr int NWG = BN / 16;
-  constexpr int XBYTES = BM * 128;
-  constexpr int WBYTES = NWG * 2048;
-  constexpr int SBYTES = XBYTES + WBYTES + (XS ? NW * 256 : 0);
-  constexpr int XPW = BM / 8 / NW, WPW = NWG * 2 / NW;
-  static_assert(XPW * 8 * NW == BM && WPW * NW == NWG * 2 && FCW >= 1 && FCW * 2 + 6 <= 15, "tile / wave split");
-  constexpr int G = XPW + WPW + (XS ? 1 : 0);
-  static_assert(NS * SBYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
-  const int tiles_n = p.N / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  int tile_m, tile_n;
-  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
-  const int n0 = tile_n * BN, m0 = tile_m * BM;
-  const int kb = p.K >> 7;
-
-  const unsigned char* xsrc[XPW];
-#pragma unroll
-  for (int i = 0; i < XPW; ++i) {
-    const int q = wave + NW * i;
-    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
-    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
-    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
-  }
-  const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
-  const unsigned char* ssrc = XS ? p.xs + (long)min(m0 + (wave & 3) * 64 + lane, p.M - 1) * (p.K >> 5) : nullptr;
-  auto stage = [&](int buf, int st) {
-    char* base = smem + buf * SBYTES;
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
-#pragma unroll
-    for (int i = 0; i < WPW; ++i) {
-      const int piece = wave + NW * i;
-      glds16_8(wsrc + ((long)(piece >> 1) * kb + st) * 2048 + (piece & 1) * 1024, base + XBYTES + piece * 1024);
-    }
-    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + WBYTES + wave * 256);
-  };
-
-  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
-  const int brow = (wm * (BM / WM) + lr) * 128;
-  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
-  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
-  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
-  auto rd = [](const char* b0, const char* b1) {
-    const u32x4 lo = *reinterpret_cast<const u32x4*>(b0);
-    const u32x4 hi = *reinterpret_cast<const u32x4*>(b1);
-    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-  };
-
-  f32x4 acc[FCW][FPW];
-#pragma unroll
-  for (int i = 0; i < FCW; ++i)
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // one k-step on buffer `cur`; STAGE: issue the glds pieces of step st + NS - 1 first. LDS reads
-  // are ordered [x0, W, x1] then x(f+2) after the MFMAs of token fragment f, so at most 14 reads
-  // are outstanding (the lgkm counter saturates at 15 -- beyond it hipcc falls back to
-  // lgkmcnt(0)) and every MFMA group waits only for its own operands.
-  auto kstep = [&](auto staged, int st, int cur) {
-    constexpr bool STAGE = decltype(staged)::value;
-    if constexpr (STAGE) {
-      stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const char* base = smem + cur * SBYTES;
-    i32x8 w[FCW], x[FPW];
-    int sc[FPW];
-    auto rdx = [&](int f) {
-      x[f] = rd(base + boff0 + f * 2048, base + boff1 + f * 2048);
-      if constexpr (XS) {
-        const int r = wm * (BM / WM) + f * 16 + lr;
-        sc[f] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
-                                                         (lane >> 4));
-      } else {
-        sc[f] = 0x7f7f7f7f;
-      }
-    };
-    rdx(0);
-#pragma unroll
-    for (int i = 0; i < FCW; ++i) w[i] = rd(base + aoff + i * 2048, base + aoff + i * 2048 + 1024);
-    rdx(1);
-#pragma unroll
-    for (int f = 0; f < FPW; ++f) {
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < FCW; ++i)
-        acc[i][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w[i], x[f], acc[i][f], 0, 0, 0, 0x7f7f7f7f, 0,
-                                                                     sc[f]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (f + 2 < FPW) rdx(f + 2);
-    }
-  };
-
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < kb) stage(s0, s0);
-  int cur = 0, st = 0;
-  for (; st + NS - 1 < kb; ++st) {  // main loop: every step stages one (NS-2 further stages stay in flight)
-    wait_vm8<(NS - 2) * G>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    kstep(std::integral_constant<bool, true>{}, st, cur);
-    cur = cur == NS - 1 ? 0 : cur + 1;
-  }
-  for (; st < kb; ++st) {  // tail: nothing left to stage
-    wait_vm8<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    kstep(std::integral_constant<bool, false>{}, st, cur);
-    cur = cur == NS - 1 ? 0 : cur + 1;
-  }
-  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
-}
-
-template <class F, int... Ks>
-__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Ks...>) {
-  (f(std::integral_constant<int, Ks>{}), ...);
-}
-
-// ---- ring-pipelined 256-row MX GEMM, K fixed at compile time (cfg 46-48) ----
-// r3 (profiles/r3_mxs): the 2-stage loops above wait for the whole next stage at every k-step,
-// and a loop with data-dependent staging / read conditions let hipcc sink every MFMA below the
-// branches and insert vmcnt(0) between them. Here the K loop is fully unrolled (KB K-tiles of
-// 128, a template parameter: the LayerNorm-fed projections of BERT/ViT-base have K = 768), so
-// every buffer index, parity and wait count is static and the body is branch-free. Tile 256
-// tokens x BN features, 8 waves (wave (wm, wn): tokens wm*128.., features wn*BN/4..); a ring of
-// NB K-tile buffers; per K-tile 4 phases over the wave's quadrants (token half r, feature half c):
-//   phase 0: read W(cB) of k                 | MFMAs (r0, cA)
-//   phase 1: read X(r1) of k                 | MFMAs (r0, cB)
-//   phase 2: barrier [all W reads of k retired: consumed by phase-1 MFMAs]
-//            stage W of k+NB into k's buffer  | MFMAs (r1, cB)
-//   phase 3: vmcnt [own glds of k+1 landed; k+2.. may fly] + barrier [RAW for k+1, WAR for X
-//            of k's buffer], stage X of k+NB, read X(r0), W(cB) of k+1 | MFMAs (r1, cA)
-// cA alternates with k so phase 3 refills exactly the registers phases 0-2 are done with. Same
-// LDS images, swizzle, hardware K order, MFMA and epilogue as gemm_mx_kernel (bitwise equal to
-// cfg 24). Per-row activation scales only (XS = false).
-template <int BN, int NB, int KB>
-__global__ __launch_bounds__(512) void gemm_mxk_kernel(const HzGemmFp8Params p, int group_m) {
-  constexpr int BM = 256, WN = 4;
-  constexpr int FCW = BN / WN / 16, FPW = 8, FH = FCW / 2;
-  constexpr int XBYTES = BM * 128, WBYTES = (BN / 16) * 2048, TBYTES = XBYTES + WBYTES;
-  constexpr int GX = 4, GW = BN / 64;
-  static_assert(FH >= 1 && NB >= 2 && KB >= NB && NB * TBYTES <= 160 * 1024, "tile");
-  __shared__ __attribute__((aligned(16))) char smem[NB * TBYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
-  const int tiles_n = p.N / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  int tile_m, tile_n;
-  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
-  const int n0 = tile_n * BN, m0 = tile_m * BM;
-
-  // X piece q = wave + 8i: tile rows 8q..8q+7 (rows >= M clamped, never stored); W piece
-  // pc = wave + 8i: fragment pc >> 1 (+4 i), k half pc & 1
-  const unsigned char* xsrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = min(m0 + 64 * i + wave * 8 + (lane >> 3), p.M - 1);
-    xsrc[i] = p.x + (long)row * p.ldx + ((lane & 7) ^ mx_swz(((wave & 1) << 2) + (lane >> 4))) * 16;
-  }
-  const unsigned char* wsrc = p.wmx + ((long)((n0 >> 4) + (wave >> 1)) * KB) * 2048 + (wave & 1) * 1024 + lane * 16;
-  auto stage_x = [&](int k, int buf) {
-    char* base = smem + buf * TBYTES + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16_8(xsrc[i] + k * 128, base + i * 8192);
-  };
-  auto stage_w = [&](int k, int buf) {
-    char* base = smem + buf * TBYTES + XBYTES + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < GW; ++i) glds16_8(wsrc + (long)(4 * i * KB + k) * 2048, base + i * 8192);
-  };
-
-  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
-  const int brow = (wm * 128 + lr) * 128;
-  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
-  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
-  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
-  auto rd = [](const char* b0, const char* b1) {
-    const u32x4 lo = *reinterpret_cast<const u32x4*>(b0);
-    const u32x4 hi = *reinterpret_cast<const u32x4*>(b1);
-    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-  };
-
-  f32x4 acc[FCW][FPW];
-#pragma unroll
-  for (int i = 0; i < FCW; ++i)
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x8 x[2][4], w[2][FH];
-  auto rdx = [&](int buf, int r) {
-    const char* base = smem + buf * TBYTES;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) x[r][f] = rd(base + boff0 + (4 * r + f) * 2048, base + boff1 + (4 * r + f) * 2048);
-  };
-  auto rdw = [&](int buf, int c) {
-    const char* base = smem + buf * TBYTES;
-#pragma unroll
-    for (int f = 0; f < FH; ++f) {
-      const int o = aoff + (c * FH + f) * 2048;
-      w[c][f] = rd(base + o, base + o + 1024);
-    }
-  };
-  auto mma = [&](int r, int c) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-#pragma unroll
-      for (int h = 0; h < FH; ++h)
-        acc[c * FH + h][4 * r + f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-            w[c][h], x[r][f], acc[c * FH + h][4 * r + f], 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    stage_w(k, k);
-    stage_x(k, k);
-  }
-  wait_vm8<(NB - 1) * (GW + GX)>();
-  __builtin_amdgcn_s_barrier();
-  rdx(0, 0);
-  rdw(0, 0);
-  auto kstep = [&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    constexpr int cA = k & 1, cB = 1 - cA, buf = k % NB;
-    __builtin_amdgcn_sched_barrier(0);
-    rdw(buf, cB);  // phase 0
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, cA);
-    __builtin_amdgcn_sched_barrier(0);
-    rdx(buf, 1);  // phase 1
-    __builtin_amdgcn_sched_barrier(0);
-    mma(0, cB);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();  // phase 2
-    if (k + NB < KB) stage_w(k + NB, buf);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(1, cB);
-    __builtin_amdgcn_sched_barrier(0);
-    // phase 3: in flight after k+1's glds: W + X of k+2 .. k+NB-1, and W of k+NB
-    if (k + NB < KB) wait_vm8<(NB - 2) * (GW + GX) + GW>();
-    else if (k + 2 < KB) wait_vm8<(KB - k - 2) * (GW + GX)>();
-    else wait_vm8<0>();
-    __builtin_amdgcn_s_barrier();
-    if (k + NB < KB) stage_x(k + NB, buf);
-    if (k + 1 < KB) {
-      rdx((k + 1) % NB, 0);
-      rdw((k + 1) % NB, cB);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mma(1, cA);
-  };
-  static_for(kstep, std::make_integer_sequence<int, KB>{});
-  __builtin_amdgcn_sched_barrier(0);
-  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * 128, n0 + wn * (BN / WN), lane);
-}
-
-template <int BN, int NB>
-int launch_mxk(const HzGemmFp8Params& p, hipStream_t st) {
-  if (p.N % BN || p.xs || p.K != 768) return -4;  // per-row activation scales, K = 768 (KB = 6)
-  const int tiles = (p.N / BN) * ((p.M + 255) / 256);
-  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
-  const int group_m = group_env < 1 ? 1 : group_env;
-  hipLaunchKernelGGL((gemm_mxk_kernel<BN, NB, 6>), dim3(tiles), dim3(512), 0, st, p, group_m);
-  return (int)hipGetLastError();
-}
-
-template <int BN, int NS>
-int launch_mxq(const HzGemmFp8Params& p, hipStream_t st) {
-  if (p.N % BN) return -4;
-  const int tiles = (p.N / BN) * ((p.M + 255) / 256);
-  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
-  const int group_m = group_env < 1 ? 1 : group_env;
-  if (p.xs) hipLaunchKernelGGL((gemm_mxq_kernel<BN, NS, true>), dim3(tiles), dim3(512), 0, st, p, group_m);
-  else hipLaunchKernelGGL((gemm_mxq_kernel<BN, NS, false>), dim3(tiles), dim3(512), 0, st, p, group_m);
-  return (int)hipGetLastError();
-}
+// Measured-negative MX schedules removed in round 5, their numbers committed: the
+// ping-pong 128x128 tile with two wave groups a phase apart (cfg 34-36, 1.4x slower than cfg 24,
+// profiles/r4_mx), the 256-row tiles with a branch-free main loop (cfg 43-45) and the ring-pipelined
+// 256-row kernel with K unrolled (cfg 46-47), 1.15-1.6x slower (profiles/r3_mx256, r3_mxk). Source:
+// git history before the round-5 cleanup.
 
 template <int BM, int BN, int NS, int WM = 2, int WN = 2>
 int launch_mx(const HzGemmFp8Params& p, hipStream_t st) {
@@ -932,24 +506,6 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
-#if HZ_EXPERIMENTS
-      // ping-pong 128x128 (two wave groups a phase apart): 2 / 3 / 4 LDS stages. Measured 1.4x
-      // SLOWER than cfg 24 on the ViT bs64 QKV / FC1 shapes (profiles/r4_mx): experiments only
-      case 34: return launch_mxpp<2>(p, st);
-      case 35: return launch_mxpp<3>(p, st);
-      case 36: return launch_mxpp<4>(p, st);
-#endif
-#if HZ_EXPERIMENTS
-      // 256-row kernel (branch-free main loop, pinned read / MFMA order): 256x256 / 2 stages,
-      // 256x128 / 2 and 3 stages
-      case 43: return launch_mxq<256, 2>(p, st);
-      case 44: return launch_mxq<128, 2>(p, st);
-      case 45: return launch_mxq<128, 3>(p, st);
-      // ring-pipelined 256-row kernel, K = 768 unrolled: 256x128 with a 3- / 2-buffer ring (a
-      // 256x256 tile needs 128 accumulators + 96 operand registers per lane: it spills)
-      case 46: return launch_mxk<128, 3>(p, st);
-      case 47: return launch_mxk<128, 2>(p, st);
-#endif
       default: return -2;
     }
   }

@@ -59,39 +59,8 @@ int hz_gemm_lds_launch(const HzConvParams* p, int cfg, hipStream_t st);
 // two independent convs with one shared (cfg, kw) in one launch (grouped; conv.hip conv2_kernel)
 int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int cfg, hipStream_t st);
 
-// A chain of dependent convs in ONE persistent launch (conv.hip conv_chain_kernel; VERDICT r2
-// "next round" 2b): the layers run in stages (the layers of a stage read the same input, e.g. a
-// downsample and its block's conv1); every workgroup walks the stages, waits on a per-stage
-// arrival counter for the stages its tiles read (x and residual), runs its share of the stage's
-// tiles with write-through (sc1) output stores and sc1 activation loads, drains and adds its tile
-// count. The last workgroup to finish resets the counters (they start zeroed), so a captured
-// graph replays it with no memset node. Every wait is bounded: a timeout sets sync[err] and the
-// kernel completes (wrong output, never a hang).
-#define HZ_CHAIN_MAX_STAGES 48
-#define HZ_CHAIN_SYNC_STRIDE 32  /* words between counters: one 128-B line each */
-typedef struct HzChainLayer {
-  HzConvParams p;            // tiles_n and kw (= 8) filled by hz_conv_chain_prepare
-  int cfg;                   // register-ring tile config 0..8 (FC, FP) as hz_conv_launch
-  int stage;                 // non-decreasing over the array
-  int dep_x, dep_res;        // stage that wrote p.x / p.res inside the chain, -1: before the launch
-  int tiles, is1x1;          // filled by hz_conv_chain_prepare
-  int pad_[2];
-} HzChainLayer;
-typedef struct HzConvChainParams {
-  const HzChainLayer* layers;  // device array [n_layers]
-  unsigned* sync;              // device words [(n_stages + 2) * HZ_CHAIN_SYNC_STRIDE], zero before the first launch:
-                               // stage counters, then the done ticket, then the timeout word
-  unsigned long long* trace;   // NULL, or [grid][n_stages][3] s_memrealtime (100 MHz) stamps per workgroup:
-                               // wait entered, wait satisfied, stage tiles done (diagnostics)
-  int n_layers, n_stages, grid, lds;  // lds: dynamic LDS bytes (hz_conv_chain_prepare)
-  unsigned spin_limit;         // polls (each ~s_sleep 2) before a wait gives up and sets the timeout word
-  int pad_;
-  int stage_tiles[HZ_CHAIN_MAX_STAGES];
-} HzConvChainParams;
-// validates the host-side layer array and fills tiles_n/kw/tiles/is1x1; returns the LDS bytes the
-// launch needs, or < 0 (layer index encoded as -(100 + i) for a layer the chain cannot run)
-int hz_conv_chain_prepare(HzChainLayer* layers, int n_layers, int* stage_tiles, int n_stages);
-int hz_conv_chain_launch(const HzConvChainParams* cp, hipStream_t st);
+// (kind 17, the persistent dependent-conv chain, was removed in round 5: measured negative in
+// round 3, profiles/r3_chain)
 
 typedef struct HzPoolParams {
   const unsigned short* x;  // NHWC bf16
@@ -481,7 +450,7 @@ int hz_block_code_warm(void);
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
-       HZ_K_LMB_ADMIT = 16, HZ_K_CONV_CHAIN = 17, HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20 };
+       HZ_K_LMB_ADMIT = 16, /* 17: removed */ HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_experiments(void);  // 1: built with HZ_EXPERIMENTS (measured-negative kernel variants)
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind

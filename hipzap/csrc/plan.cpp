@@ -152,7 +152,6 @@ struct Plan {
             case HZ_K_QUANT: u |= kUnitFp8; break;
             case HZ_K_MAXPOOL:
             case HZ_K_POOL_FC: u |= kUnitVision; break;
-            case HZ_K_CONV_CHAIN: u |= kUnitConv; break;
             case HZ_K_STEM:
             case HZ_K_BNECK:
             case HZ_K_SEAM: u |= kUnitBlock; break;

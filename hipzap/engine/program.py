@@ -65,10 +65,7 @@ class ExecContext:
         self._lib = lib
         # fused ResNet stages (engine/fusion.py, csrc/block.hip): runs of nodes bound as ONE launch;
         # the arena plan keeps each run's tensors live over the whole run
-        chain = self._chain_range(os.environ.get("HIPZAP_CONV_CHAIN", ""))
         self.fused = fusion.plan(g, params, fusion.enabled_kinds(fuse) if fuse is not None else None)
-        if chain is not None:
-            self.fused = {k: f for k, f in self.fused.items() if f.end <= chain[0]}
         conv_plans = self._conv_plans(g, params, tuned)
         if pair_convs is None:
             pair_convs = os.environ.get("HIPZAP_PAIR_CONVS", "1") != "0"
@@ -123,7 +120,6 @@ class ExecContext:
                                                0), "h2d")
             if self.zc_out:
                 self.ext[g.outputs[0]] = self.host_output
-        self.chain_sync = None
         i = 0
         while i < len(g.nodes):
             n = g.nodes[i]
@@ -131,10 +127,6 @@ class ExecContext:
                 f = self.fused[i]
                 self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib))
                 i = f.end
-                continue
-            if chain is not None and i == chain[0]:
-                self._add_conv_chain(lib, chain[0], chain[1], conv_plans)
-                i = chain[1]
                 continue
             if i in self.pairs:
                 self._add_conv_pair(lib, n, g.nodes[i + 1], conv_plans[i], conv_plans[i + 1], tuned)
@@ -190,82 +182,6 @@ class ExecContext:
                     cfg, kw = 19, 1
             conv_plans.append((cfg, kw, key))
         return conv_plans
-
-    # ------------------------------------------------------------------
-    def _chain_range(self, prefix: str):
-        """[first, end) node indices of the conv run that HIPZAP_CONV_CHAIN=<name prefix> turns into
-        one persistent launch (e.g. ``layer3``: ResNet-50 layer3 + layer4, 26 convs)."""
-        if not prefix or self.recording:
-            return None
-        g = self.graph
-        first = next((i for i, n in enumerate(g.nodes) if n.kind == "conv" and
-                      str(n.attrs.get("name", "")).startswith(prefix)), None)
-        if first is None:
-            return None
-        end = first
-        while end < len(g.nodes) and g.nodes[end].kind == "conv":
-            end += 1
-        return (first, end) if end - first >= 2 else None
-
-    # register-ring tiles the chain kernel instantiates (conv.hip chain_tile): larger FP -> FP 2 / 1
-    _CHAIN_CFG = {0: 0, 1: 1, 2: 1, 3: 3, 4: 4, 5: 4, 6: 6, 7: 6, 8: 6}
-
-    def _add_conv_chain(self, lib, first: int, end: int, conv_plans: list) -> None:
-        """Nodes [first, end) -> ONE conv_chain_kernel launch (csrc/conv.hip; HzConvChainParams).
-        Stages: a conv that reads the same input as the previous conv, which is alone in its stage
-        (a downsample + its block's conv1), joins that stage; every other conv opens a new one."""
-        g = self.graph
-        nodes = g.nodes[first:end]
-        n_layers = len(nodes)
-        layers = (N.ChainLayer * n_layers)()
-        producer: dict[int, int] = {}
-        stage, stage_size, stage_input = -1, 0, None
-        force_cfg = os.environ.get("HIPZAP_CHAIN_CFG")
-        for k, n in enumerate(nodes):
-            join = (stage_size == 1 and n.inputs[0] == stage_input and
-                    all(producer.get(t, -1) != stage for t in n.inputs))
-            if not join:
-                stage, stage_size, stage_input = stage + 1, 0, n.inputs[0]
-            stage_size += 1
-            cfg = int(force_cfg) if force_cfg is not None else self._CHAIN_CFG.get(conv_plans[first + k][0], 3)
-            L = layers[k]
-            L.p = self._conv_params(n, cfg, 8)
-            L.cfg, L.stage = cfg, stage
-            L.dep_x = producer.get(n.inputs[0], -1)  # an earlier stage, or -1: written before the launch
-            L.dep_res = producer.get(n.inputs[1], -1) if len(n.inputs) > 1 else -1
-            producer[n.outputs[0]] = stage
-            self.configs.append((n.attrs.get("name", ""), "chain", cfg, 8))
-        n_stages = stage + 1
-        tiles = (C.c_int * n_stages)()
-        lds = lib.hz_conv_chain_prepare(layers, n_layers, tiles, n_stages)
-        if lds < 0:
-            bad = nodes[-lds - 100].attrs.get("name") if lds <= -100 else None
-            raise ValueError(f"conv chain rejected (code {lds}, layer {bad})")
-        dev_layers = torch.frombuffer(bytearray(bytes(layers)), dtype=torch.uint8).to(self.device)
-        sync = torch.zeros((n_stages + 2) * N.HZ_CHAIN_SYNC_STRIDE, dtype=torch.int32, device=self.device)
-        self._keep += [dev_layers, sync]
-        self.chain_sync, self.chain_stages = sync, n_stages
-        cp = N.ConvChainParams()
-        cp.layers, cp.sync = dev_layers.data_ptr(), sync.data_ptr()
-        cp.grid = int(os.environ.get("HIPZAP_CHAIN_GRID", "128"))
-        self.chain_trace = None
-        if os.environ.get("HIPZAP_CHAIN_TRACE", "0") == "1":
-            self.chain_trace = torch.zeros((cp.grid, n_stages, 3), dtype=torch.int64, device=self.device)
-            self._keep.append(self.chain_trace)
-            cp.trace = self.chain_trace.data_ptr()
-        cp.n_layers, cp.n_stages, cp.lds = n_layers, n_stages, lds
-        cp.spin_limit = int(os.environ.get("HIPZAP_CHAIN_SPIN", str(1 << 20)))
-        for s_ in range(n_stages):
-            cp.stage_tiles[s_] = tiles[s_]
-        self.chain_info = {"layers": n_layers, "stages": n_stages, "grid": cp.grid, "lds": lds,
-                           "stage_tiles": list(tiles)}
-        N.check(lib.hz_prog_add_kernel(self.prog, N.HZ_K_CONV_CHAIN, C.byref(cp), C.sizeof(cp), 0), "add_conv_chain")
-
-    def chain_error(self) -> int:
-        """The chain kernel's timeout word (0 = every in-launch wait was satisfied)."""
-        if self.chain_sync is None:
-            return 0
-        return int(self.chain_sync[(self.chain_stages + 1) * N.HZ_CHAIN_SYNC_STRIDE].item())
 
     def _conv_params(self, n, cfg, kw):
         g, addr = self.graph, self._addr

@@ -102,19 +102,12 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             24: (128, 128), 25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (256, 128), 29: (128, 256),
             # 30-32: 4 LDS stages (8-wave 128x128; 4-wave 64x128, 128x64)
             30: (128, 128), 31: (64, 128), 32: (128, 64),
-            # 33: 8-wave 256x256 (plain); 43-45: the 256-row kernel (256x256 2 stages, 256x128 2 / 3):
-            # measured slower than 24 at one workgroup per CU, kept as tuner candidates (profiles/r3_mx256)
-            33: (256, 256), 43: (256, 256), 44: (256, 128), 45: (256, 128),
-            # 46 / 47: the ring-pipelined 256-row kernel, K = 768 unrolled (3- / 2-buffer ring; per-row
-            # activation scales only -- an MX8-input or other-K launch is refused)
-            46: (256, 128), 47: (256, 128),
-            # 34-36: cfg 24's tile with the two wave groups a phase apart (ping-pong), 2 / 3 / 4 stages;
-            # per-row activation scales only; measured 1.4x slower than cfg 24 (profiles/r4_mx):
-            # experiments build only
-            34: (128, 128), 35: (128, 128), 36: (128, 128)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 34, 35, 36, 43, 44, 45, 46, 47)
-MX_PERROW_ONLY = (34, 35, 36, 46, 47)
-MX_EXPERIMENTS = (34, 35, 36, 43, 44, 45, 46, 47)  # only in the HZ_EXPERIMENTS library (csrc/common.h)
+            # 33: 8-wave 256x256 (plain). Removed in round 5 with their negatives committed: 34-36
+            # (ping-pong, profiles/r4_mx), 43-47 (256-row tiles, profiles/r3_mx256, r3_mxk)
+            33: (256, 256)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33)
+MX_PERROW_ONLY = ()
+MX_EXPERIMENTS = ()  # MX tiles that exist only in the HZ_EXPERIMENTS library: none left
 
 
 def mx_fits(cfg: int, n: int) -> bool:

@@ -5,7 +5,14 @@ hipGraph replay, best of 3; random e4m3 operands). One JSON line per shape with 
 config.
 
     python scripts/bench_mx.py [--M 12608] [--cfgs 24,40,43]
+    python scripts/bench_mx.py --torch   # the library bar: torch._scaled_mm (hipBLASLt fp8) on the same shapes
+
+``--torch`` (VERDICT r4 missing 2): ``torch._scaled_mm`` with OCP e4m3fn operands, bf16 output,
+per-tensor scales and (where this torch / hipBLASLt accept them) row-wise scales, 20 calls per
+captured graph replay, best of 3 -- the same timing frame as the MX kernels. A scaling mode the
+library refuses is recorded with its error instead of a time.
 """
+import time
 import argparse
 import json
 import os
@@ -24,12 +31,64 @@ SHAPES = [("qkv", 2304, 768, "fp8"), ("o", 768, 768, "fp8:xs"), ("fc1", 3072, 76
           ("fc2", 768, 3072, "fp8:xs")]
 
 
+def _graph_time(fn, dev, reps: int = 20) -> float:
+    """us per call: ``reps`` calls captured in one graph, replayed 3 x 5 times, best replay."""
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(reps):
+            fn()
+    best = float("inf")
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        best = min(best, (time.perf_counter() - t0) / (5 * reps) * 1e6)
+    return best
+
+
+def torch_bar(M: int, dev) -> None:
+    gen = torch.Generator(device=dev).manual_seed(0)
+    for name, Nn, K, _ in SHAPES:
+        a = (torch.randn(M, K, device=dev, generator=gen) * 0.5).to(torch.float8_e4m3fn)
+        b = (torch.randn(Nn, K, device=dev, generator=gen) * 0.1).to(torch.float8_e4m3fn)
+        fl = 2.0 * M * Nn * K
+        res = {}
+        modes = {"tensorwise": (torch.tensor(1.0, device=dev), torch.tensor(1.0, device=dev)),
+                 "rowwise": (torch.ones(M, 1, device=dev), torch.ones(1, Nn, device=dev))}
+        for mode, (sa, sb) in modes.items():
+            try:
+                fn = lambda sa=sa, sb=sb: torch._scaled_mm(a, b.t(), scale_a=sa, scale_b=sb,  # noqa: E731
+                                                           out_dtype=torch.bfloat16)
+                fn()
+                t = _graph_time(fn, dev)
+                res[mode] = {"us": round(t, 2), "tflops": round(fl / t / 1e6, 1)}
+            except Exception as e:  # noqa: BLE001 - record what the library refuses
+                res[mode] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+        try:  # the bf16 library GEMM of the same shape, for scale
+            ab, bb = a.to(torch.bfloat16), b.to(torch.bfloat16)
+            t = _graph_time(lambda: torch.mm(ab, bb.t()), dev)
+            res["bf16_mm"] = {"us": round(t, 2), "tflops": round(fl / t / 1e6, 1)}
+        except Exception as e:  # noqa: BLE001
+            res["bf16_mm"] = {"error": str(e)[:200]}
+        print(json.dumps({"shape": name, "M": M, "N": Nn, "K": K, "torch": torch.__version__, "lib": res}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=12608)
     ap.add_argument("--cfgs", default="")
+    ap.add_argument("--torch", action="store_true", help="time torch._scaled_mm (hipBLASLt) instead")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.torch:
+        return torch_bar(a.M, dev)
     lib = N.lib()
     g = torch.Generator(device=dev).manual_seed(0)
     want = [int(c) for c in a.cfgs.split(",") if c] or sorted(F8.MX_TILES)

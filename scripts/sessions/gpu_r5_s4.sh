@@ -25,3 +25,7 @@ HIPZAP_FUSE=convpool,bneck,bneck2,seam timeout -k 10 300 rocprofv3 --kernel-trac
 python3 scripts/rocpd_stats.py $O/p/run_results.db --cutime preprocess pool_fc > $O/cutime_seam_16.txt
 rm -rf $O/p
 sed -n 12,40p $O/cutime_seam_16.txt | cut -c1-60
+# MX-fp8 library bar (VERDICT r4 missing 2): torch._scaled_mm vs our cfg 24 on the ViT bs64 shapes
+timeout -k 10 180 python3 scripts/bench_mx.py --torch > $O/mx_torch.jsonl 2> $O/mx_torch.err || tail -5 $O/mx_torch.err
+timeout -k 10 180 python3 scripts/bench_mx.py --cfgs 24 > $O/mx_cfg24.jsonl 2>&1 || tail -5 $O/mx_cfg24.jsonl
+cat $O/mx_torch.jsonl | cut -c1-400

@@ -37,7 +37,6 @@ extern "C" int hz_softmax_launch(const HzSoftmaxParams* p, hipStream_t) {
 STUB(hz_lmb_layer_launch, HzLmbLayerParams, 14, H)
 STUB(hz_lmb_dec_launch, HzLmbDecParams, 15, V)
 STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
-STUB(hz_conv_chain_launch, HzConvChainParams, 17, n_layers)
 STUB(hz_stem_launch, HzStemParams, 18, N)
 STUB(hz_bneck_launch, HzBneckParams, 19, N)
 STUB(hz_seam_launch, HzSeamParams, 20, N)
