@@ -904,7 +904,7 @@ __device__ __forceinline__ int seam_lds(int row, int chunk) {  // bf16 offset of
 
 // (one workgroup per CU is the design point -- 56-128 workgroups -- so the register budget is 256:
 // with hipcc's default occupancy target its scheduler sinks the ring's loads next to their MFMAs)
-template <int CM, int CS>
+template <int CM, int CS, bool T2F32>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void seam_kernel(const HzSeamParams p) {
   constexpr int CO = 4 * CM;
   constexpr int KS3 = CM / 32;     // conv3 k-steps
@@ -914,8 +914,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   constexpr int ZBW = ZB / 8;      // per wave
   constexpr int KS1 = CS / 16;     // conv1 k-steps over the slice (32x32x16)
   constexpr int KSW1 = CO / 32;    // conv1 weight k-steps (its packing)
-  constexpr int D = KS3 * PGW <= 16 ? KS3 : KS3 / 2;  // conv3 k-steps in flight (all of them up to 16 B loads)
+  constexpr int D = KS3;  // conv3 weight k-steps in flight
   __shared__ __attribute__((aligned(16))) bf16_t Y[32 * CS];
+  // the tile's t2 (32 pixels x CM) is staged ONCE per workgroup in LDS as bf16 (fp32 t2: with the
+  // ReLU applied), [CM/8 chunks][32 pixels][8]: every wave's B fragment is then one conflict-free
+  // ds_read_b128 (16 consecutive pixels of one chunk) instead of every wave re-reading the tile from
+  // L1/L2 -- fp32 t2 read that way took 2x the seam's time, and staging also took the bf16 seam
+  // from 7.1 to ~6 us (profiles/r5_seam)
+  __shared__ __attribute__((aligned(16))) bf16_t T2S[CM * 32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4, l16 = lane & 15;
   const int h = lane >> 5, l32 = lane & 31;
@@ -928,12 +934,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int rg = wave % RG, pg0 = (wave / RG) * PGW;
   const int ch = c0 + 16 * rg + 4 * g4;  // this lane's 4 conv3 output channels
 
-  // ---- epilogue operands first (vmcnt retires in issue order). A padding pixel column (j >= cnt)
+  // ---- the staging loads first of all (the wait before the LDS writes then covers them only)
+  constexpr int NSE = CM * 32 / 8 / 512;
+  f32x4 sf[T2F32 ? NSE : 1][2];
+  u32x4 sb[T2F32 ? 1 : NSE];
+#pragma unroll
+  for (int i = 0; i < NSE; ++i) {
+    // entry e -> (32-channel block cb, pixel px, 8-channel sub-chunk): consecutive threads read
+    // consecutive 16 / 32 B of one pixel's line, then the next pixel's
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    const long off = (((long)n * KS3 + cb) * HW + hw0 + min(px, cnt - 1)) * 32 + sub * 8;
+    if constexpr (T2F32) {
+      const float* xf = reinterpret_cast<const float*>(p.t2) + off;
+      sf[i][0] = *reinterpret_cast<const f32x4*>(xf);
+      sf[i][1] = *reinterpret_cast<const f32x4*>(xf + 4);
+    } else {
+      sb[i] = *reinterpret_cast<const u32x4*>(p.t2 + off);
+    }
+  }
+  // ---- epilogue operands next (vmcnt retires in issue order). A padding pixel column (j >= cnt)
   // loads its tile's last pixel instead of branching (a branch around a load makes hipcc drain
   // vmcnt): its conv3 column, LDS row and conv1 row are never stored ----
   const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b3 + ch);
   u32x2 rr[PGW];
-  long yo[PGW], xb[PGW];
+  long yo[PGW];
   bool yv[PGW];
 #pragma unroll
   for (int q = 0; q < PGW; ++q) {
@@ -941,16 +965,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     yv[q] = j < cnt;
     yo[q] = (((long)n * (CO / 32) + (ch >> 5)) * HW + hw0 + jc) * 32 + (ch & 31);
     rr[q] = *reinterpret_cast<const u32x2*>(p.res + yo[q]);
-    xb[q] = (((long)n * KS3) * HW + hw0 + jc) * 32 + 8 * g4;
   }
   // ---- conv3 operand ring ----
   const bf16_t* __restrict__ W3 = p.w3 + ((long)(c0 / 16 + rg) * KS3) * 512 + lane * 8;
   bf16x8 fa[KS3], fb[KS3][PGW];
-  auto load = [&](int s) {
-    fa[s] = *reinterpret_cast<const bf16x8*>(W3 + (long)s * 512);
-#pragma unroll
-    for (int q = 0; q < PGW; ++q) fb[s][q] = *reinterpret_cast<const bf16x8*>(p.t2 + xb[q] + (long)s * HW * 32);
-  };
+  auto load = [&](int s) { fa[s] = *reinterpret_cast<const bf16x8*>(W3 + (long)s * 512); };
 #pragma unroll
   for (int s = 0; s < D && s < KS3; ++s) load(s);
   // ---- conv1 weights of this wave's column blocks (phase 2's B operands), behind the ring ----
@@ -966,13 +985,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
   }
   asm volatile("" ::: "memory");  // keep those loads here: hipcc otherwise sinks them below phase 1
+#pragma unroll
+  for (int i = 0; i < NSE; ++i) {
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    u32x4 v;
+    if constexpr (T2F32) {
+      const f32x4 a = sf[i][0], b = sf[i][1];
+      v = u32x4{pack2(fmaxf(a[0], 0.f), fmaxf(a[1], 0.f)), pack2(fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)),
+                pack2(fmaxf(b[0], 0.f), fmaxf(b[1], 0.f)), pack2(fmaxf(b[2], 0.f), fmaxf(b[3], 0.f))};
+    } else {
+      v = sb[i];
+    }
+    *reinterpret_cast<u32x4*>(T2S + ((cb * 4 + sub) * 32 + px) * 8) = v;
+  }
+  lds_sync();
   f32x4 acc[PGW];
 #pragma unroll
   for (int q = 0; q < PGW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KS3; ++s) {
 #pragma unroll
-    for (int q = 0; q < PGW; ++q) acc[q] = mfma16(fa[s], fb[s][q], acc[q]);
+    for (int q = 0; q < PGW; ++q) {
+      fb[s][q] = *reinterpret_cast<const bf16x8*>(T2S + ((s * 4 + g4) * 32 + 16 * (pg0 + q) + l16) * 8);
+      acc[q] = mfma16(fa[s], fb[s][q], acc[q]);
+    }
     if (s + D < KS3) load(s + D);
   }
   // ---- phase-1 epilogue: y slice -> global (bf16) and LDS ----
@@ -1010,6 +1046,155 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
       if (row < cnt) atomicAdd(zb + row * 32, za[i][r]);
+    }
+  }
+  if (p.zinit) {  // preset the next K-split 3x3 conv's accumulator (HzSeamParams.zinit)
+    const long n4 = (long)p.N * p.z_C * p.z_HW / 4;
+    const int cbz = p.z_C >> 5;
+    for (long i = (long)blockIdx.x * 512 + tid; i < n4; i += (long)gridDim.x * 512) {
+      const long e = i * 4;
+      const int c = (int)((e / (32L * p.z_HW)) % cbz) * 32 + (int)(e & 31);
+      *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K-split 3x3 conv into an fp32 accumulator (HzKconvParams, hipzap.h), layer3 / layer4 at bs=1.
+// Workgroup = (image n, 32 output channels ct, input-channel slice of CK). The slice of the whole
+// image goes to LDS once, chunk-major ([8-channel chunk][padded pixel], 16 B per entry, zero halo),
+// converted to bf16 (fp32 inputs get their ReLU here). Wave w owns pixel group w % PG (32 pixels)
+// and the k-part w / PG of the slice's 9 * CK reduction; mfma_f32_32x32x16_bf16 with the PIXELS on
+// the A rows and the output channels on the B columns, so one accumulator register is one pixel's
+// 32 consecutive channels = a 128-B row of the channel-blocked output: the no-return float atomics
+// go out as full 128-B segments (MI355X_MICROARCH.md § Global float atomics). k-parts > 1 are summed
+// through LDS first.
+template <int CK, int PG, bool XF32>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void kconv_kernel(const HzKconvParams p) {
+  constexpr int QK = 8 / PG;         // k-parts per pixel group
+  constexpr int T = 9 * CK / 16;     // 32x32x16 k-steps of the slice
+  constexpr int TW = T / QK;         // per wave
+  constexpr int D = TW < 12 ? TW : 12;  // weight ring depth
+  static_assert(T % QK == 0, "k-steps must split evenly over the k-parts");
+  extern __shared__ __attribute__((aligned(16))) char kc_smem[];
+  bf16_t* X = reinterpret_cast<bf16_t*>(kc_smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int H = p.H, W = p.W, HW = H * W, W2 = W + 2, NPOS = (H + 2) * W2;
+  const int nct = p.Cout >> 5, nsl = p.C / CK;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids: one input slice, all channel tiles
+  const int ct = lid % nct, rest = lid / nct, slice = rest % nsl, n = rest / nsl;
+  const int c0 = slice * CK;
+  const int pg = wave % PG, q = wave / PG;
+  const bool active = wave < PG * QK;
+  const int KS = 9 * p.C / 32;  // weight k-steps (packing)
+
+  // ---- stage the slice: entry (chunk, padded pixel) at X[(chunk * NPOS + pos) * 8]. Every load of
+  // the staging is issued first (a fixed, unrolled count per thread; out-of-image entries read the
+  // pixel at 0 and are written as zeros), then the weight ring behind them, so the wait before the
+  // LDS writes covers the staging loads only (vmcnt retires in issue order) ----
+  constexpr int NPMAX = PG == 7 ? 256 : 100;       // padded pixels: (14+2)^2 / (8+2)^2
+  constexpr int NST = ((CK / 8) * NPMAX + 511) / 512;
+  const int nent = (CK / 8) * NPOS;
+  u32x4 sv[NST];
+  f32x4 sf[XF32 ? NST : 1][2];
+  int sdst[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    // u -> (32-channel block, padded pixel, 8-channel sub-chunk): consecutive threads read
+    // consecutive 16 / 32 B of the channel-blocked input
+    const int u = min(tid + 512 * i, nent - 1);
+    const int sub = u & 3, bp = u >> 2, cb = bp / NPOS, pos = bp - cb * NPOS;
+    const int py = pos / W2, px = pos - py * W2;
+    const bool in = (unsigned)(py - 1) < (unsigned)H && (unsigned)(px - 1) < (unsigned)W;
+    sdst[i] = tid + 512 * i >= nent ? -1 : in ? ((cb * 4 + sub) * NPOS + pos) * 8 : -2 - ((cb * 4 + sub) * NPOS + pos) * 8;
+    const long off = ((((long)n * (p.C >> 5) + (c0 >> 5) + cb) * HW) + (in ? (py - 1) * W + (px - 1) : 0)) * 32 + sub * 8;
+    if constexpr (XF32) {
+      const float* xf = static_cast<const float*>(p.x) + off;
+      sf[i][0] = *reinterpret_cast<const f32x4*>(xf);
+      sf[i][1] = *reinterpret_cast<const f32x4*>(xf + 4);
+    } else {
+      sv[i] = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(p.x) + off);
+    }
+  }
+  // ---- this wave's weight ring (B operand: column = output channel, 8 consecutive k per lane) ----
+  const int co = ct * 32 + l32;
+  const bf16_t* __restrict__ Wg = p.w + ((long)(co >> 4) * KS) * 512 + (co & 15) * 8;
+  auto wofs = [&](int t) {  // element offset (past Wg) of k-step t's 8 k for this lane
+    const int kl = 16 * t + 8 * h, tap = kl / CK, k = tap * p.C + c0 + (kl - tap * CK);
+    return (long)(k >> 5) * 512 + ((k & 31) >> 3) * 128;
+  };
+  const int t0 = (active ? q : 0) * TW;  // (an idle wave loads k-part 0 and multiplies nothing)
+  bf16x8 wr[TW];
+#pragma unroll
+  for (int u = 0; u < D; ++u) wr[u] = *reinterpret_cast<const bf16x8*>(Wg + wofs(t0 + u));
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    if (sdst[i] == -1) continue;
+    u32x4 v;
+    if constexpr (XF32) {
+      const f32x4 a = sf[i][0], b = sf[i][1];
+      v = u32x4{pack2(fmaxf(a[0], 0.f), fmaxf(a[1], 0.f)), pack2(fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)),
+                pack2(fmaxf(b[0], 0.f), fmaxf(b[1], 0.f)), pack2(fmaxf(b[2], 0.f), fmaxf(b[3], 0.f))};
+    } else {
+      v = sv[i];
+    }
+    const int d = sdst[i] >= 0 ? sdst[i] : -2 - sdst[i];
+    if (sdst[i] < -1) v = u32x4{0u, 0u, 0u, 0u};  // zero halo
+    *reinterpret_cast<u32x4*>(X + d) = v;
+  }
+  __syncthreads();
+  // ---- MFMAs from LDS ----
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int pix = min(pg * 32 + l32, HW - 1);  // (padding rows re-read the last pixel; never stored)
+  const int oy = pix / W, ox = pix - oy * W, base = oy * W2 + ox;
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      const int kl = 16 * (t0 + u) + 8 * h, tap = kl / CK, cc = kl - tap * CK;
+      const int r = tap / 3, s = tap - 3 * r;
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + ((cc >> 3) * NPOS + base + r * W2 + s) * 8);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wr[u], acc, 0, 0, 0);
+      if (u + D < TW) wr[u + D] = *reinterpret_cast<const bf16x8*>(Wg + wofs(t0 + u + D));
+    }
+  }
+  // ---- k-parts summed through LDS (after the staging image is dead), then the atomic adds ----
+  int r_lo = 0, r_hi = 16;
+  if constexpr (QK > 1) {
+    float* red = reinterpret_cast<float*>(kc_smem);
+    __syncthreads();  // every wave's LDS operand reads are done
+    if (active) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((pg * QK + q) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    r_lo = q * (16 / QK), r_hi = r_lo + 16 / QK;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r < r_lo || r >= r_hi) continue;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < QK; ++j) sum += red[((pg * QK + j) * 16 + r) * 64 + lane];
+      acc[r] = sum;
+    }
+  }
+  if (active) {
+    float* ob = p.out + (((long)n * nct + ct) * HW) * 32 + l32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r < r_lo || r >= r_hi) continue;
+      const int px = pg * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (px < HW) atomicAdd(ob + px * 32, acc[r]);
+    }
+  }
+  if (p.zinit) {  // preset the next accumulator (HzConvParams.zinit)
+    const long n4 = (long)p.N * p.z_C * p.z_HW / 4;
+    const int cbz = p.z_C >> 5;
+    for (long i = (long)blockIdx.x * 512 + tid; i < n4; i += (long)gridDim.x * 512) {
+      const long e = i * 4;
+      const int c = (int)((e / (32L * p.z_HW)) % cbz) * 32 + (int)(e & 31);
+      *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
     }
   }
 }
@@ -1065,10 +1250,44 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
   HzSeamParams q = p;
   q.tiles = (p.HW + 31) / 32;  // balanced tiles of <= 32 pixels
   const dim3 grid(q.tiles * p.N * (4 * p.CM / p.cs));
-  if (p.CM == 256 && p.cs == 128) hipLaunchKernelGGL((seam_kernel<256, 128>), grid, dim3(512), 0, st, q);
-  else if (p.CM == 256) hipLaunchKernelGGL((seam_kernel<256, 64>), grid, dim3(512), 0, st, q);
-  else if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128>), grid, dim3(512), 0, st, q);
-  else hipLaunchKernelGGL((seam_kernel<512, 64>), grid, dim3(512), 0, st, q);
+  if (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1)) return -1;
+#define HZ_SEAM(CM, CS)                                                                                    \
+  if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<CM, CS, true>), grid, dim3(512), 0, st, q);               \
+  else hipLaunchKernelGGL((seam_kernel<CM, CS, false>), grid, dim3(512), 0, st, q);
+  if (p.CM == 256 && p.cs == 128) { HZ_SEAM(256, 128) }
+  else if (p.CM == 256) { HZ_SEAM(256, 64) }
+  else if (p.cs == 128) { HZ_SEAM(512, 128) }
+  else { HZ_SEAM(512, 64) }
+#undef HZ_SEAM
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_kconv_launch(const HzKconvParams* pp, hipStream_t st) {
+  const HzKconvParams& p = *pp;
+  if (!p.x || !p.w || !p.out || (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1))) return -1;
+  if (p.N < 1 || p.H < 1 || p.W < 1 || p.C % 32 || p.Cout % 32 || p.C % p.ck) return -1;
+  const int HW = p.H * p.W;
+  const int pg = (HW + 31) / 32;
+  const dim3 grid(p.N * (p.Cout / 32) * (p.C / p.ck));
+  const size_t stage = (size_t)(p.ck / 8) * (p.H + 2) * (p.W + 2) * 16;
+#define HZ_KC(CK, PG, XF)                                                                            \
+  do {                                                                                               \
+    const size_t red = (8 / PG) > 1 ? (size_t)PG * (8 / PG) * 16 * 64 * 4 : 0;                       \
+    const size_t lds = stage > red ? stage : red;                                                    \
+    if (lds > 160 * 1024) return -1;                                                                 \
+    hipLaunchKernelGGL((kconv_kernel<CK, PG, XF>), grid, dim3(512), lds, st, p);                     \
+  } while (0)
+#define HZ_KC_X(CK, PG)              \
+  if (p.x_f32) HZ_KC(CK, PG, true);  \
+  else HZ_KC(CK, PG, false);
+  if ((pg == 7 && (p.H + 2) * (p.W + 2) > 256) || (pg == 2 && (p.H + 2) * (p.W + 2) > 100)) return -1;  // NPMAX
+  if (pg == 7 && p.ck == 64) { HZ_KC_X(64, 7) }        // 14 x 14 (layer3)
+  else if (pg == 7 && p.ck == 32) { HZ_KC_X(32, 7) }
+  else if (pg == 2 && p.ck == 128) { HZ_KC_X(128, 2) }  // 7 x 7 (layer4)
+  else if (pg == 2 && p.ck == 64) { HZ_KC_X(64, 2) }
+  else return -2;
+#undef HZ_KC_X
+#undef HZ_KC
   return (int)hipGetLastError();
 }
 

@@ -186,8 +186,18 @@ __device__ __forceinline__ void conv_tile(const HzConvParams& p, const int lid) 
 #pragma unroll
         for (int j = 0; j < FP; ++j) {
           const long off = ((long)(pb[j] + cb * HW) << 5) + lk;
-          if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) b[j] = ld_act(X, off);
-          else b[j] = bf16x8{};
+          if constexpr (F32IN) {
+            const float* xf = reinterpret_cast<const float*>(X) + off;
+            if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) {
+              rw[j][0] = *reinterpret_cast<const f32x4*>(xf);
+              rw[j][1] = *reinterpret_cast<const f32x4*>(xf + 4);
+            } else {
+              rw[j][0] = rw[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          } else {
+            if (pval[j] && HZ_DCHECK(off + 8 <= xlim)) b[j] = ld_act(X, off);
+            else b[j] = bf16x8{};
+          }
         }
       } else {
         const int uoff = cb * HW + r * p.W + s;  // wave-uniform part of the pixel offset
@@ -425,9 +435,10 @@ int launch(const HzConvParams& p, hipStream_t st) {
   const bool fast = (p.C % 32) == 0;
   dim3 grid(q.tiles_n * tiles_m), block(64 * kw);
   const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
-  if (p.x_f32) {  // a seam consumer: 3x3 (or strided) channel-blocked convs only
-    if (p.x_rowmajor || is1x1 || !fast) return -1;
-    hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false, true>), grid, block, lds, st, q);
+  if (p.x_f32) {  // a seam / K-split-conv consumer: channel-blocked convs only
+    if (p.x_rowmajor || !fast) return -1;
+    if (is1x1) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false, true>), grid, block, lds, st, q);
+    else hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false, true>), grid, block, lds, st, q);
   } else if (p.x_rowmajor) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
   else if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false>), grid, block, lds, st, q);
   else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false>), grid, block, lds, st, q);

@@ -439,18 +439,40 @@ typedef struct HzSeamParams {
   const unsigned short* w1;   // next conv1 weights [CM/16][4CM/32][64][8]
   float* z;                   // next conv1 accumulator [N][CM/32][HW][32] fp32, preset to its bias
   int N, HW, CM, cs;          // cs: slice width (64 or 128)
-  int tiles, pad_;            // pixel tiles per image (launcher: ceil(HW / 32))
+  int tiles, t2_f32;          // tiles: pixel tiles per image (launcher: ceil(HW / 32)); t2_f32: t2 is the
+                              //   fp32 accumulator of a K-split 3x3 conv (ReLU applied at the load)
+  float* zinit;               // or NULL: afterwards filled with zbias per channel ([N][z_C/32][z_HW][32]):
+  const float* zbias;         //   the next K-split 3x3 conv's accumulator
+  int z_C, z_HW;
 } HzSeamParams;
+// K-split 3x3 conv (stride 1, pad 1, H = W <= 14) into an fp32 accumulator (block.hip kconv_kernel):
+// a workgroup owns (image, 32 output channels, a slice of ck input channels): it stages that slice of
+// the whole image (+ zero halo) in LDS once -- bf16, or fp32 with the ReLU applied (x_f32: a seam's
+// conv1 sum) -- multiplies all 9 taps from LDS (mfma 32x32x16, pixels on the A rows) and adds its
+// partial into `out` by float atomics (out preset to the conv's bias by the launch before; the
+// consumer applies the ReLU when it loads out). Each input byte is read from L2 once per workgroup
+// instead of once per tap; the weight stream is split over C/ck workgroups per channel tile.
+typedef struct HzKconvParams {
+  const void* x;              // [N][C/32][H][W][32] fp32 (x_f32) or bf16
+  const unsigned short* w;    // packed as the per-conv kernels: [Cout/16][9C/32][64][8], k = (r*3 + s)*C + c
+  float* out;                 // [N][Cout/32][H][W][32] fp32, preset to the bias
+  float* zinit;               // or NULL: filled with zbias per channel afterwards, as HzConvParams.zinit
+  const float* zbias;
+  int z_C, z_HW;
+  int N, H, W, C, Cout, x_f32;
+  int ck, pad_;               // input channels per workgroup: 32, 64 or 128
+} HzKconvParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);
 int hz_seam_launch(const HzSeamParams* p, hipStream_t st);
+int hz_kconv_launch(const HzKconvParams* p, hipStream_t st);
 int hz_block_code_warm(void);
 
 // generic program op: kind selects the launcher, params are copied into the program
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
-       HZ_K_LMB_ADMIT = 16, /* 17: removed */ HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20 };
+       HZ_K_LMB_ADMIT = 16, /* 17: removed */ HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20, HZ_K_KCONV = 21 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_experiments(void);  // 1: built with HZ_EXPERIMENTS (measured-negative kernel variants)
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind

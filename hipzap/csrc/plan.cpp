@@ -154,7 +154,8 @@ struct Plan {
             case HZ_K_POOL_FC: u |= kUnitVision; break;
             case HZ_K_STEM:
             case HZ_K_BNECK:
-            case HZ_K_SEAM: u |= kUnitBlock; break;
+            case HZ_K_SEAM:
+            case HZ_K_KCONV: u |= kUnitBlock; break;
             default: break;
           }
           break;
@@ -469,6 +470,7 @@ uint64_t hz_abi_version(void) {
                             sizeof(HzStemParams),
                             sizeof(HzBneckParams),
                             sizeof(HzSeamParams),
+                            sizeof(HzKconvParams),
                             HZ_ABI_EPOCH};
   uint64_t x = 1469598103934665603ull;
   for (uint64_t v : parts) {

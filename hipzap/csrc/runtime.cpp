@@ -299,6 +299,7 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_STEM: return hz_stem_launch(static_cast<const HzStemParams*>(prm), st);
     case HZ_K_BNECK: return hz_bneck_launch(static_cast<const HzBneckParams*>(prm), st);
     case HZ_K_SEAM: return hz_seam_launch(static_cast<const HzSeamParams*>(prm), st);
+    case HZ_K_KCONV: return hz_kconv_launch(static_cast<const HzKconvParams*>(prm), st);
     default: return -100;
   }
 }
@@ -324,6 +325,7 @@ extern "C" size_t hz_kernel_param_size(int kind) {
     case HZ_K_STEM: return sizeof(HzStemParams);
     case HZ_K_BNECK: return sizeof(HzBneckParams);
     case HZ_K_SEAM: return sizeof(HzSeamParams);
+    case HZ_K_KCONV: return sizeof(HzKconvParams);
     default: return 0;
   }
 }

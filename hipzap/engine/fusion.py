@@ -37,8 +37,8 @@ import numpy as np
 
 from .. import _native as N
 
-HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM = 18, 19, 20
-KINDS = ("stem", "convpool", "bneck", "bneck2", "seam")
+HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
+KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box)
 DEFAULT = "convpool,bneck,bneck2"
 
@@ -60,7 +60,15 @@ class BneckParams(C.Structure):  # HzBneckParams
 class SeamParams(C.Structure):  # HzSeamParams
     _fields_ = [("t2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("res", C.c_void_p),
                 ("y", C.c_void_p), ("w1", C.c_void_p), ("z", C.c_void_p), ("N", C.c_int), ("HW", C.c_int),
-                ("CM", C.c_int), ("cs", C.c_int), ("tiles", C.c_int), ("pad_", C.c_int)]
+                ("CM", C.c_int), ("cs", C.c_int), ("tiles", C.c_int), ("t2_f32", C.c_int), ("zinit", C.c_void_p),
+                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int)]
+
+
+class KconvParams(C.Structure):  # HzKconvParams
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
+                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
+                ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
+                ("pad_", C.c_int)]
 
 
 @dataclass
@@ -71,6 +79,12 @@ class Fused:
     nodes: list   # the graph nodes it replaces
     init: int | None = None      # seam: the conv that presets the accumulator (block i's 3x3 conv)
     consumer: int | None = None  # seam: the conv that reads it (block i+1's 3x3 conv)
+    # kconv (a seam's consumer bound as the K-split 3x3 kernel): the seam that presets its fp32 output,
+    # the seam whose accumulator it presets (or None), the 1x1 conv that reads its output when that
+    # conv is not in a seam (the last block of a stage)
+    seam: int | None = None
+    next_seam: int | None = None
+    reader: int | None = None
 
 
 def enabled_kinds(spec: str | None = None) -> set:
@@ -266,15 +280,49 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
             if f is not None and not covered & set(range(f.init, f.consumer + 1)):
                 seams[i] = f
         out.update(seams)
+        if "kconv" in kinds:
+            out.update(match_kconvs(g, params, seams))
         out = dict(sorted(out.items()))
     return out
 
 
+def match_kconvs(g, params, seams: dict) -> dict:
+    """Each seam's consumer (block i+1's 3x3 conv, stride 1, 14 x 14 / 7 x 7) as a K-split 3x3
+    launch whose output is an fp32 accumulator: preset by that seam, read with the ReLU at the load
+    by the next seam's conv3 half (or, at a stage's last block, by a plain 1x1 conv3 with x_f32)."""
+    out = {}
+    by_init = {f.init: s for s, f in seams.items()}
+    for s, f in seams.items():
+        k = f.consumer
+        n = g.nodes[k]
+        pk = params.get(n.attrs.get("w"))
+        nb, h, w, c = g.shape(n.inputs[0])
+        if pk is None or not _geom(pk, c, c, 3, 1, 1) or c not in (256, 512) or h * w > (196 if c == 256 else 64):
+            continue
+        if k + 1 >= len(g.nodes):
+            continue
+        c3 = g.nodes[k + 1]
+        a = n.outputs[0]
+        if not _conv(c3) or c3.inputs[0] != a or a in g.outputs:
+            continue
+        if any(a in m.inputs for j, m in enumerate(g.nodes) if j != k + 1):
+            continue
+        nxt = by_init.get(k)  # the seam this conv presets (its own block's conv3 + the next conv1)
+        if nxt is not None and nxt != k + 1:
+            continue
+        p3 = params.get(c3.attrs.get("w"))
+        if nxt is None and (p3 is None or not _geom(p3, c, 4 * c, 1, 1, 0)):
+            continue
+        out[k] = Fused("kconv", k, k + 1, [n], seam=s, next_seam=nxt, reader=None if nxt is not None else k + 1)
+    return out
+
+
 def planning_graph(g, fused: dict):
-    """The graph the arena planner sees: a seam's accumulator (conv1's output) is fp32, and it is
-    live from the 3x3 conv that presets it (an extra output of that node)."""
-    seams = [f for f in fused.values() if f.kind == "seam"]
-    if not seams:
+    """The graph the arena planner sees: a seam's accumulator (conv1's output) and a K-split 3x3
+    conv's output are fp32, and each is live from the launch that presets it (an extra output of
+    that launch's node: the 3x3 conv before a seam, the seam before a K-split conv)."""
+    accs = [f for f in fused.values() if f.kind in ("seam", "kconv")]
+    if not accs:
         return g
     import copy
 
@@ -282,12 +330,24 @@ def planning_graph(g, fused: dict):
     gp = copy.copy(g)
     gp.tensors = list(g.tensors)
     gp.nodes = list(g.nodes)
-    for f in seams:
-        t1 = f.nodes[1].outputs[0]
-        spec = g.tensors[t1]
-        gp.tensors[t1] = type(spec)(spec.shape, torch.float32, spec.name, spec.external)
-        n = g.nodes[f.init]
-        gp.nodes[f.init] = type(n)(n.kind, list(n.inputs), list(n.outputs) + [t1], n.slot, n.attrs)
+
+    def fp32(t):
+        spec = g.tensors[t]
+        gp.tensors[t] = type(spec)(spec.shape, torch.float32, spec.name, spec.external)
+
+    def preset_by(j, t):
+        n = gp.nodes[j]
+        gp.nodes[j] = type(n)(n.kind, list(n.inputs), list(n.outputs) + [t], n.slot, n.attrs)
+
+    for f in accs:
+        if f.kind == "seam":
+            t1 = f.nodes[1].outputs[0]
+            fp32(t1)
+            preset_by(f.init, t1)
+        else:
+            a = f.nodes[0].outputs[0]
+            fp32(a)
+            preset_by(f.seam + 1, a)  # the seam's second node (its conv1 half) is the presetting launch
     return gp
 
 
@@ -297,7 +357,7 @@ def seam_cs(cm: int) -> int:
     return v[0] if cm == 256 else v[-1]
 
 
-def seam_params(g, params, f: Fused, addr) -> SeamParams:
+def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamParams:
     c3, c1 = f.nodes
     p3, p1 = params[c3.attrs["w"]], params[c1.attrs["w"]]
     p = SeamParams()
@@ -306,6 +366,38 @@ def seam_params(g, params, f: Fused, addr) -> SeamParams:
     nb, h, w, _ = g.shape(c3.outputs[0])
     p.N, p.HW, p.CM = nb, h * w, p1.cout
     p.cs = seam_cs(p.CM)
+    fused = fused or {}
+    kc = fused.get(f.start - 1)  # t2 is a K-split conv's fp32 accumulator
+    p.t2_f32 = int(kc is not None and kc.kind == "kconv")
+    kn = fused.get(f.consumer)  # this seam presets its consumer's accumulator
+    if kn is not None and kn.kind == "kconv":
+        kcv = kn.nodes[0]
+        _, kh, kw_, kcout = g.shape(kcv.outputs[0])
+        p.zinit, p.zbias = addr(kcv.outputs[0]), params[kcv.attrs["w"]].bias.data_ptr()
+        p.z_C, p.z_HW = kcout, kh * kw_
+    return p
+
+
+def kconv_ck(c: int) -> int:
+    """Input-channel slice of the K-split 3x3 conv (HIPZAP_KCONV_CK="<ck for C 256>,<ck for C 512>";
+    the microbenchmark's fastest, scripts/bench_kconv.py)."""
+    v = [int(x) for x in os.environ.get("HIPZAP_KCONV_CK", "32,64").split(",")]
+    return v[0] if c == 256 else v[-1]
+
+
+def kconv_params(g, params, f: Fused, addr, fused: dict) -> KconvParams:
+    n = f.nodes[0]
+    pk = params[n.attrs["w"]]
+    p = KconvParams()
+    nb, h, w, c = g.shape(n.inputs[0])
+    p.x, p.w, p.out = addr(n.inputs[0]), pk.wf.data_ptr(), addr(n.outputs[0])
+    p.N, p.H, p.W, p.C, p.Cout, p.x_f32, p.ck = nb, h, w, c, pk.cout, 1, kconv_ck(c)
+    if f.next_seam is not None:  # preset the next seam's conv1 accumulator
+        nf = fused[f.next_seam]
+        t1 = nf.nodes[1].outputs[0]
+        _, th, tw, tc = g.shape(t1)
+        p.zinit, p.zbias = addr(t1), params[nf.nodes[1].attrs["w"]].bias.data_ptr()
+        p.z_C, p.z_HW = tc, th * tw
     return p
 
 
@@ -366,12 +458,14 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
     return p
 
 
-def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
+def add_fused(prog, g, params, f: Fused, addr, lib, fused: dict | None = None) -> tuple:
     """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
     if f.kind in ("stem", "convpool"):
         prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
     elif f.kind == "seam":
-        prm, kind = seam_params(g, params, f, addr), HZ_K_SEAM
+        prm, kind = seam_params(g, params, f, addr, fused), HZ_K_SEAM
+    elif f.kind == "kconv":
+        prm, kind = kconv_params(g, params, f, addr, fused or {}), HZ_K_KCONV
     else:
         prm, kind = bneck_params(g, params, f, addr), HZ_K_BNECK
     N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(prm), C.sizeof(prm), f.nodes[0].slot), f"add_{f.kind}")
@@ -381,5 +475,5 @@ def add_fused(prog, g, params, f: Fused, addr, lib) -> tuple:
 
 def launch(kind: str, prm, stream=None) -> None:
     """Eager launch of a fused kernel (tests)."""
-    k = HZ_K_STEM if kind == "stem" else HZ_K_SEAM if kind == "seam" else HZ_K_BNECK
+    k = {"stem": HZ_K_STEM, "seam": HZ_K_SEAM, "kconv": HZ_K_KCONV}.get(kind, HZ_K_BNECK)
     N.check(N.lib().hz_launch_kernel(k, C.byref(prm), N.stream_ptr(stream)), f"launch_{kind}")

@@ -75,8 +75,12 @@ class ExecContext:
         self.fused = {k: f for k, f in self.fused.items() if f.kind != "seam" or (
             f.init not in paired and f.consumer not in paired and conv_plans[f.init][0] < 16
             and conv_plans[f.consumer][0] < 16)}
+        # a K-split 3x3 conv needs the seam that presets its output and, when it presets one, the next
+        self.fused = {k: f for k, f in self.fused.items() if f.kind != "kconv" or (
+            f.seam in self.fused and (f.next_seam is None or f.next_seam in self.fused))}
         self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
         self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}
+        self.f32_readers = {id(g.nodes[f.reader]) for f in self.fused.values() if f.kind == "kconv" and f.reader}
         offsets, arena_bytes = plan_memory(fusion.planning_graph(g, self.fused),
                                            groups=[(f.start, f.end) for f in self.fused.values()])
         self.arena_bytes = arena_bytes
@@ -125,7 +129,7 @@ class ExecContext:
             n = g.nodes[i]
             if i in self.fused:
                 f = self.fused[i]
-                self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib))
+                self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib, self.fused))
                 i = f.end
                 continue
             if i in self.pairs:
@@ -255,8 +259,8 @@ class ExecContext:
             prm, _, _ = conv_ops.make_params(
                 addr(n.inputs[0]), pc, nb, h, w, addr(n.outputs[0]), addr(res), n.attrs.get("act", "relu"),
                 n.attrs.get("out_f32", False), cfg, kw, out_rowmajor=n.attrs.get("rowmajor", False))
-            if id(n) in self.seam_consumer:  # reads a seam's fp32 conv1 sum (ReLU at the load)
-                prm.x_f32 = 1
+            if id(n) in self.seam_consumer or id(n) in self.f32_readers:  # reads an fp32 accumulator
+                prm.x_f32 = 1  # (a seam's conv1 sum or a K-split 3x3 conv's output; ReLU at the load)
             if id(n) in self.seam_init:  # presets the next seam's accumulator to conv1's bias
                 f = self.seam_init[id(n)]
                 t1 = f.nodes[1].outputs[0]

@@ -40,6 +40,7 @@ STUB(hz_lmb_admit_launch, HzLmbAdmitParams, 16, Bp)
 STUB(hz_stem_launch, HzStemParams, 18, N)
 STUB(hz_bneck_launch, HzBneckParams, 19, N)
 STUB(hz_seam_launch, HzSeamParams, 20, N)
+STUB(hz_kconv_launch, HzKconvParams, 21, N)
 extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
   g_calls.push_back(18);
   g_vals.push_back(n);

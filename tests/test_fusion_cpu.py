@@ -184,3 +184,34 @@ def test_seams_need_the_layer3_layer4_geometry(r50):
     p18, kw18 = r18.pack(randomize_bn(r18.make_model()).eval().state_dict(), "cpu")
     _, fz18 = _plan(r18, p18, kw18, "seam", batch=1, input_uint8=True)
     assert fz18 == {}  # basic blocks: no 1x1 -> 1x1 seam
+
+
+def test_resnet50_kconvs(r50):
+    """With ``kconv`` every seam's consumer 3x3 conv becomes a K-split launch: layer3 blocks 1-5 and
+    layer4 blocks 1-2; each is preset by the seam before it, the interior ones preset the next seam,
+    the last one of a stage is read by a plain conv3."""
+    from hipzap.engine.graph import plan_memory
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam,kconv", batch=1, input_uint8=True)
+    kc = [f for f in fz.values() if f.kind == "kconv"]
+    assert [f.nodes[0].attrs["name"] for f in kc] == [f"layer3.{b}.conv2" for b in range(1, 6)] + \
+        [f"layer4.{b}.conv2" for b in range(1, 3)]
+    assert [f.next_seam is None for f in kc] == [False] * 4 + [True] + [False, True]
+    for f in kc:
+        assert fz[f.seam].kind == "seam" and fz[f.seam].consumer == f.start
+        if f.next_seam is not None:
+            assert fz[f.next_seam].init == f.start and f.reader is None
+        else:
+            assert g.nodes[f.reader].attrs["name"].endswith("conv3")
+    gp = fusion.planning_graph(g, fz)
+    offsets, _ = plan_memory(gp, groups=[(f.start, f.end) for f in fz.values()])
+    for f in kc:
+        a_t = f.nodes[0].outputs[0]
+        assert gp.tensors[a_t].dtype == torch.float32 and a_t in gp.nodes[f.seam + 1].outputs
+        z0, z1 = offsets[a_t], offsets[a_t] + gp.tensors[a_t].nbytes
+        for j in range(f.seam, f.start + 2):  # presetting seam .. the reader
+            for t in g.nodes[j].inputs + g.nodes[j].outputs:
+                if t == a_t or t is None or g.tensors[t].external:
+                    continue
+                o0, o1 = offsets[t], offsets[t] + gp.tensors[t].nbytes
+                assert o1 <= z0 or z1 <= o0, (g.nodes[j].attrs.get("name"), g.tensors[t].name)

@@ -117,17 +117,22 @@ def _run(ctx, x):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("batch,noreuse", [(1, True), (1, False), (2, True)])
-def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, monkeypatch):
+KCONV = SEAMS + ",kconv"
+
+
+@pytest.mark.parametrize("batch,noreuse,spec", [(1, True, SEAMS), (1, False, SEAMS), (2, True, SEAMS),
+                                                (1, True, KCONV), (1, False, KCONV), (2, False, KCONV)])
+def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, monkeypatch):
     if noreuse:
         monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
     else:
         monkeypatch.delenv("HIPZAP_ARENA_NOREUSE", raising=False)
     a, params, params_cpu, kw = r50
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=True))
-    seam = ExecContext(g, params, torch.device(DEV), fuse=SEAMS)
+    seam = ExecContext(g, params, torch.device(DEV), fuse=spec)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     assert sum(f.kind == "seam" for f in seam.fused.values()) == 7
+    assert sum(f.kind == "kconv" for f in seam.fused.values()) == (7 if "kconv" in spec else 0)
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
     _run(seam, x)
     _run(plain, x)
@@ -146,11 +151,12 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, monkeypat
     assert torch.equal(ls.argmax(1), lp.argmax(1))
 
 
-def test_resnet50_seam_dispatches_and_replay(r50):
+@pytest.mark.parametrize("spec", [SEAMS, KCONV])
+def test_resnet50_seam_dispatches_and_replay(r50, spec):
     a, params, _, kw = r50
     g = a.build_graph(batch=1, **dict(kw, input_uint8=True))
     base = ExecContext(g, params, torch.device(DEV), fuse="convpool,bneck,bneck2")
-    ctx = ExecContext(g, params, torch.device(DEV), fuse=SEAMS)
+    ctx = ExecContext(g, params, torch.device(DEV), fuse=spec)
     assert base.num_ops() - ctx.num_ops() == 7
     assert ctx.num_ops() <= 31
     s = torch.cuda.Stream()
@@ -164,3 +170,52 @@ def test_resnet50_seam_dispatches_and_replay(r50):
         torch.cuda.synchronize()
         lb, lc = base.output.float().cpu(), ctx.output.float().cpu()
         assert _rel(lc, lb) < 2e-2 and torch.equal(lc.argmax(-1), lb.argmax(-1))
+
+
+class KconvParams(C.Structure):  # HzKconvParams (csrc/hipzap.h)
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
+                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
+                ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
+                ("pad_", C.c_int)]
+
+
+HZ_K_KCONV = 21
+
+
+@pytest.mark.parametrize("c,h,ck,xf32,n", [(256, 14, 64, True, 1), (256, 14, 32, True, 1), (256, 14, 64, False, 2),
+                                           (512, 7, 128, True, 1), (512, 7, 64, True, 2), (512, 7, 128, False, 1)])
+def test_kconv_vs_fp32(c, h, ck, xf32, n):
+    """K-split 3x3 conv: out = preset bias + conv3x3(relu(z) in bf16) by atomics; also presets the
+    next accumulator."""
+    g = torch.Generator().manual_seed(c + ck + n)
+    x = torch.randn(n, h, h, c, generator=g)
+    pc = CV.pack_conv(torch.randn(c, c, 3, 3, generator=g) * (2.0 / (9 * c)) ** 0.5, 0.1 * torch.randn(c, generator=g),
+                      None, 1, 1)
+    xin = (torch.relu(x) if xf32 else x).to(torch.bfloat16).float()
+    wref = pc.dense().reshape(c, 3, 3, c).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xin.permute(0, 3, 1, 2), wref, pc.bias, padding=1).permute(0, 2, 3, 1)
+    pcd = pc.to(DEV)
+    xd = _blk(x) if xf32 else _blk(x.to(torch.bfloat16))
+    out = pcd.bias.view(1, c // 32, 1, 1, 32).expand(n, c // 32, h, h, 32).contiguous()
+    nxt = torch.full((n, 8, h, h, 32), float("nan"), device=DEV)
+    zb = torch.randn(256, generator=g).to(DEV)
+    prm = KconvParams()
+    prm.x, prm.w, prm.out, prm.zinit, prm.zbias = xd.data_ptr(), pcd.wf.data_ptr(), out.data_ptr(), nxt.data_ptr(), \
+        zb.data_ptr()
+    prm.z_C, prm.z_HW, prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.x_f32, prm.ck = 256, h * h, n, h, h, c, c, int(xf32), ck
+    N.check(N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), N.stream_ptr()), "kconv")
+    torch.cuda.synchronize()
+    got = CV.from_blocked(out.cpu(), (n, h, h, c))
+    assert _rel(got, ref) < 1e-3, _rel(got, ref)
+    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, h, h, 256)), zb.cpu().expand(n, h, h, 256))
+
+
+def test_kconv_refuses_bad_geometry():
+    prm = KconvParams()
+    buf = torch.zeros(1 << 20, device=DEV)
+    prm.x, prm.w, prm.out = buf.data_ptr(), buf.data_ptr(), buf.data_ptr()
+    prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.ck = 1, 28, 28, 256, 256, 64  # 784 pixels: no kernel for that
+    assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
+    prm.H = prm.W = 14
+    prm.ck = 96
+    assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
