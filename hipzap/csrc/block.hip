@@ -1069,7 +1069,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // 32 consecutive channels = a 128-B row of the channel-blocked output: the no-return float atomics
 // go out as full 128-B segments (MI355X_MICROARCH.md § Global float atomics). k-parts > 1 are summed
 // through LDS first.
-template <int CK, int PG, bool XF32>
+template <int CK, int PG, bool XF32, int ST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void kconv_kernel(const HzKconvParams p) {
   constexpr int QK = 8 / PG;         // k-parts per pixel group
   constexpr int T = 9 * CK / 16;     // 32x32x16 k-steps of the slice
@@ -1079,7 +1079,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   extern __shared__ __attribute__((aligned(16))) char kc_smem[];
   bf16_t* X = reinterpret_cast<bf16_t*>(kc_smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int H = p.H, W = p.W, HW = H * W, W2 = W + 2, NPOS = (H + 2) * W2;
+  const int H = p.H, W = p.W, W2 = W + 2, NPOS = (H + 2) * W2;  // input (+ halo)
+  const int Q = W / ST, HW = (H / ST) * Q, HWI = H * W;          // output pixels
   const int nct = p.Cout >> 5, nsl = p.C / CK;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids: one input slice, all channel tiles
   const int ct = lid % nct, rest = lid / nct, slice = rest % nsl, n = rest / nsl;
@@ -1092,7 +1093,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // the staging is issued first (a fixed, unrolled count per thread; out-of-image entries read the
   // pixel at 0 and are written as zeros), then the weight ring behind them, so the wait before the
   // LDS writes covers the staging loads only (vmcnt retires in issue order) ----
-  constexpr int NPMAX = PG == 7 ? 256 : 100;       // padded pixels: (14+2)^2 / (8+2)^2
+  // padded input pixels: (14+2)^2 / (8+2)^2 at stride 1, (28+2)^2 / (14+2)^2 at stride 2
+  constexpr int NPMAX = ST == 1 ? (PG == 7 ? 256 : 100) : (PG == 7 ? 900 : 256);
   constexpr int NST = ((CK / 8) * NPMAX + 511) / 512;
   const int nent = (CK / 8) * NPOS;
   u32x4 sv[NST];
@@ -1107,7 +1109,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const int py = pos / W2, px = pos - py * W2;
     const bool in = (unsigned)(py - 1) < (unsigned)H && (unsigned)(px - 1) < (unsigned)W;
     sdst[i] = tid + 512 * i >= nent ? -1 : in ? ((cb * 4 + sub) * NPOS + pos) * 8 : -2 - ((cb * 4 + sub) * NPOS + pos) * 8;
-    const long off = ((((long)n * (p.C >> 5) + (c0 >> 5) + cb) * HW) + (in ? (py - 1) * W + (px - 1) : 0)) * 32 + sub * 8;
+    const long off = ((((long)n * (p.C >> 5) + (c0 >> 5) + cb) * HWI) + (in ? (py - 1) * W + (px - 1) : 0)) * 32 + sub * 8;
     if constexpr (XF32) {
       const float* xf = static_cast<const float*>(p.x) + off;
       sf[i][0] = *reinterpret_cast<const f32x4*>(xf);
@@ -1148,7 +1150,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int pix = min(pg * 32 + l32, HW - 1);  // (padding rows re-read the last pixel; never stored)
-  const int oy = pix / W, ox = pix - oy * W, base = oy * W2 + ox;
+  const int oy = pix / Q, ox = pix - oy * Q, base = ST * oy * W2 + ST * ox;
   if (active) {
 #pragma unroll
     for (int u = 0; u < TW; ++u) {
@@ -1266,7 +1268,10 @@ extern "C" int hz_kconv_launch(const HzKconvParams* pp, hipStream_t st) {
   const HzKconvParams& p = *pp;
   if (!p.x || !p.w || !p.out || (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1))) return -1;
   if (p.N < 1 || p.H < 1 || p.W < 1 || p.C % 32 || p.Cout % 32 || p.C % p.ck) return -1;
-  const int HW = p.H * p.W;
+  const int st_ = p.stride == 2 ? 2 : 1;
+  if (p.stride < 0 || p.stride > 2) return -1;  // (0 reads as 1)
+  if (st_ == 2 && (p.H % 2 || p.W % 2)) return -1;
+  const int HW = (p.H / st_) * (p.W / st_);
   const int pg = (HW + 31) / 32;
   const dim3 grid(p.N * (p.Cout / 32) * (p.C / p.ck));
   const size_t stage = (size_t)(p.ck / 8) * (p.H + 2) * (p.W + 2) * 16;
@@ -1275,12 +1280,14 @@ extern "C" int hz_kconv_launch(const HzKconvParams* pp, hipStream_t st) {
     const size_t red = (8 / PG) > 1 ? (size_t)PG * (8 / PG) * 16 * 64 * 4 : 0;                       \
     const size_t lds = stage > red ? stage : red;                                                    \
     if (lds > 160 * 1024) return -1;                                                                 \
-    hipLaunchKernelGGL((kconv_kernel<CK, PG, XF>), grid, dim3(512), lds, st, p);                     \
+    if (st_ == 1) hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 1>), grid, dim3(512), lds, st, p);    \
+    else hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 2>), grid, dim3(512), lds, st, p);             \
   } while (0)
 #define HZ_KC_X(CK, PG)              \
   if (p.x_f32) HZ_KC(CK, PG, true);  \
   else HZ_KC(CK, PG, false);
-  if ((pg == 7 && (p.H + 2) * (p.W + 2) > 256) || (pg == 2 && (p.H + 2) * (p.W + 2) > 100)) return -1;  // NPMAX
+  const int npmax = st_ == 1 ? (pg == 7 ? 256 : 100) : (pg == 7 ? 900 : 256);
+  if ((pg != 7 && pg != 2) || (p.H + 2) * (p.W + 2) > npmax) return -1;  // the kernel's NPMAX
   if (pg == 7 && p.ck == 64) { HZ_KC_X(64, 7) }        // 14 x 14 (layer3)
   else if (pg == 7 && p.ck == 32) { HZ_KC_X(32, 7) }
   else if (pg == 2 && p.ck == 128) { HZ_KC_X(128, 2) }  // 7 x 7 (layer4)

@@ -389,6 +389,7 @@ __global__ __launch_bounds__(conv_max_threads(FC * FP)) void conv2_kernel(const 
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   if (lid < split) conv_tile<FC, FP, FAST, IS1X1, false>(p0, lid);
   else conv_tile<FC, FP, FAST, IS1X1, false>(p1, lid - split);
+  if (p0.zinit) zfill(p0);  // preset the K-split 3x3 conv that follows the pair
 }
 
 int check_params(const HzConvParams& p) {
@@ -471,7 +472,7 @@ extern "C" int hz_conv_launch(const HzConvParams* pp, int cfg, hipStream_t st) {
 // Grouped launch of two independent convs sharing one (cfg, kw); see conv2_kernel.
 extern "C" int hz_conv2_launch(const HzConvParams* a, const HzConvParams* b, int cfg, hipStream_t st) {
   if (check_params(*a) || check_params(*b)) return -1;
-  if (a->x_f32 || b->x_f32 || a->zinit || b->zinit) return -1;  // (seams bind single convs)
+  if (a->x_f32 || b->x_f32 || b->zinit) return -1;  // (the pair's preset rides on its first conv)
   switch (cfg) {
     case 0: return launch2<1, 1>(*a, *b, st);
     case 1: return launch2<1, 2>(*a, *b, st);

@@ -445,7 +445,8 @@ typedef struct HzSeamParams {
   const float* zbias;         //   the next K-split 3x3 conv's accumulator
   int z_C, z_HW;
 } HzSeamParams;
-// K-split 3x3 conv (stride 1, pad 1, H = W <= 14) into an fp32 accumulator (block.hip kconv_kernel):
+// K-split 3x3 conv (pad 1, stride 1 at <= 14 x 14 or stride 2 from <= 28 x 28) into an fp32
+// accumulator (block.hip kconv_kernel):
 // a workgroup owns (image, 32 output channels, a slice of ck input channels): it stages that slice of
 // the whole image (+ zero halo) in LDS once -- bf16, or fp32 with the ReLU applied (x_f32: a seam's
 // conv1 sum) -- multiplies all 9 taps from LDS (mfma 32x32x16, pixels on the A rows) and adds its
@@ -459,8 +460,8 @@ typedef struct HzKconvParams {
   float* zinit;               // or NULL: filled with zbias per channel afterwards, as HzConvParams.zinit
   const float* zbias;
   int z_C, z_HW;
-  int N, H, W, C, Cout, x_f32;
-  int ck, pad_;               // input channels per workgroup: 32, 64 or 128
+  int N, H, W, C, Cout, x_f32;  // H, W: the INPUT size (the output is H/stride x W/stride)
+  int ck, stride;             // input channels per workgroup: 32, 64 or 128; stride 1 or 2
 } HzKconvParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);

@@ -39,8 +39,9 @@ from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
 KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv")
-# measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box)
-DEFAULT = "convpool,bneck,bneck2"
+# measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box; round 5
+# adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, profiles/r5_seam)
+DEFAULT = "convpool,bneck,bneck2,seam,kconv"
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -68,7 +69,7 @@ class KconvParams(C.Structure):  # HzKconvParams
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
                 ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
                 ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("pad_", C.c_int)]
+                ("stride", C.c_int)]
 
 
 @dataclass
@@ -85,6 +86,7 @@ class Fused:
     seam: int | None = None
     next_seam: int | None = None
     reader: int | None = None
+    preset: int | None = None  # kconv: node whose launch presets its accumulator (a seam's conv1, or conv1 of a pair)
 
 
 def enabled_kinds(spec: str | None = None) -> set:
@@ -281,17 +283,36 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
                 seams[i] = f
         out.update(seams)
         if "kconv" in kinds:
-            out.update(match_kconvs(g, params, seams))
+            out.update(match_kconvs(g, params, seams, covered))
         out = dict(sorted(out.items()))
     return out
 
 
-def match_kconvs(g, params, seams: dict) -> dict:
+def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
     """Each seam's consumer (block i+1's 3x3 conv, stride 1, 14 x 14 / 7 x 7) as a K-split 3x3
     launch whose output is an fp32 accumulator: preset by that seam, read with the ReLU at the load
-    by the next seam's conv3 half (or, at a stage's last block, by a plain 1x1 conv3 with x_f32)."""
+    by the next seam's conv3 half (or, at a stage's last block, by a plain 1x1 conv3 with x_f32).
+    Also a stage's first 3x3 conv (stride 2, 28 x 28 -> 14 x 14 / 14 x 14 -> 7 x 7) when it is the
+    first seam's init: preset by the launch before it (its block's conv1, usually paired with the
+    downsample), read by that seam's conv3 half."""
     out = {}
     by_init = {f.init: s for s, f in seams.items()}
+    for s, f in seams.items():  # the first block of a stage: its stride-2 3x3 conv
+        k = f.init
+        n = g.nodes[k]
+        pk = params.get(n.attrs.get("w"))
+        if pk is None or k < 1 or not _conv(n) or k - 1 in covered:
+            continue
+        nb, h, w, c = g.shape(n.inputs[0])
+        prev = g.nodes[k - 1]
+        if not (_geom(pk, c, c, 3, 2, 1) and c in (256, 512) and h % 2 == 0 and w % 2 == 0
+                and (h + 2) * (w + 2) <= (900 if c == 256 else 256)):
+            continue
+        if not _conv(prev) or prev.outputs[0] != n.inputs[0] or prev.attrs.get("act", "relu") != "relu":
+            continue
+        if any(s2 != s and f2.consumer == k for s2, f2 in seams.items()):
+            continue  # (a seam consumer: handled below)
+        out[k] = Fused("kconv", k, k + 1, [n], seam=None, next_seam=s, reader=None, preset=k - 1)
     for s, f in seams.items():
         k = f.consumer
         n = g.nodes[k]
@@ -313,7 +334,8 @@ def match_kconvs(g, params, seams: dict) -> dict:
         p3 = params.get(c3.attrs.get("w"))
         if nxt is None and (p3 is None or not _geom(p3, c, 4 * c, 1, 1, 0)):
             continue
-        out[k] = Fused("kconv", k, k + 1, [n], seam=s, next_seam=nxt, reader=None if nxt is not None else k + 1)
+        out[k] = Fused("kconv", k, k + 1, [n], seam=s, next_seam=nxt, reader=None if nxt is not None else k + 1,
+                       preset=s + 1)
     return out
 
 
@@ -347,13 +369,13 @@ def planning_graph(g, fused: dict):
         else:
             a = f.nodes[0].outputs[0]
             fp32(a)
-            preset_by(f.seam + 1, a)  # the seam's second node (its conv1 half) is the presetting launch
+            preset_by(f.preset, a)  # a seam's conv1 half, or the conv before a stage's stride-2 3x3
     return gp
 
 
 def seam_cs(cm: int) -> int:
     """Slice width of the seam kernel per geometry (HIPZAP_SEAM_CS="<cs for CM 256>,<cs for CM 512>")."""
-    v = [int(x) for x in os.environ.get("HIPZAP_SEAM_CS", "128,64").split(",")]
+    v = [int(x) for x in os.environ.get("HIPZAP_SEAM_CS", "128,128").split(",")]
     return v[0] if cm == 256 else v[-1]
 
 
@@ -378,11 +400,14 @@ def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamPar
     return p
 
 
-def kconv_ck(c: int) -> int:
-    """Input-channel slice of the K-split 3x3 conv (HIPZAP_KCONV_CK="<ck for C 256>,<ck for C 512>";
-    the microbenchmark's fastest, scripts/bench_kconv.py)."""
+def kconv_ck(c: int, stride: int = 1) -> int:
+    """Input-channel slice of the K-split 3x3 conv: HIPZAP_KCONV_CK="<C 256>,<C 512>[,<C 256 stride 2>,
+    <C 512 stride 2>]" (stride-2 entries default to the stride-1 ones); defaults from the microbenchmark
+    (scripts/bench_kconv.py) and the served A/B (profiles/r5_seam)."""
     v = [int(x) for x in os.environ.get("HIPZAP_KCONV_CK", "32,64").split(",")]
-    return v[0] if c == 256 else v[-1]
+    if stride == 2 and len(v) >= 4:
+        return v[2] if c == 256 else v[3]
+    return v[0] if c == 256 else v[1 if len(v) > 1 else 0]
 
 
 def kconv_params(g, params, f: Fused, addr, fused: dict) -> KconvParams:
@@ -391,7 +416,8 @@ def kconv_params(g, params, f: Fused, addr, fused: dict) -> KconvParams:
     p = KconvParams()
     nb, h, w, c = g.shape(n.inputs[0])
     p.x, p.w, p.out = addr(n.inputs[0]), pk.wf.data_ptr(), addr(n.outputs[0])
-    p.N, p.H, p.W, p.C, p.Cout, p.x_f32, p.ck = nb, h, w, c, pk.cout, 1, kconv_ck(c)
+    p.N, p.H, p.W, p.C, p.Cout, p.ck, p.stride = nb, h, w, c, pk.cout, kconv_ck(c, pk.stride), pk.stride
+    p.x_f32 = int(f.seam is not None)  # a seam's fp32 conv1 sum; a stage's first 3x3 reads bf16
     if f.next_seam is not None:  # preset the next seam's conv1 accumulator
         nf = fused[f.next_seam]
         t1 = nf.nodes[1].outputs[0]

@@ -77,10 +77,14 @@ class ExecContext:
             and conv_plans[f.consumer][0] < 16)}
         # a K-split 3x3 conv needs the seam that presets its output and, when it presets one, the next
         self.fused = {k: f for k, f in self.fused.items() if f.kind != "kconv" or (
-            f.seam in self.fused and (f.next_seam is None or f.next_seam in self.fused))}
+            (f.seam is None or f.seam in self.fused) and (f.next_seam is None or f.next_seam in self.fused)
+            and (f.seam is not None or conv_plans[f.preset][0] < 16))}
         self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
         self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}
         self.f32_readers = {id(g.nodes[f.reader]) for f in self.fused.values() if f.kind == "kconv" and f.reader}
+        # K-split 3x3 convs preset by a plain (or paired) conv launch: a stage's first block
+        self.kconv_preset = {id(g.nodes[f.preset]): f for f in self.fused.values()
+                             if f.kind == "kconv" and f.seam is None}
         offsets, arena_bytes = plan_memory(fusion.planning_graph(g, self.fused),
                                            groups=[(f.start, f.end) for f in self.fused.values()])
         self.arena_bytes = arena_bytes
@@ -211,6 +215,9 @@ class ExecContext:
             fa = self._conv_flops(a)
             cfg, kw = (plan_a if fa >= self._conv_flops(b) else plan_b)[:2]
         pa, pb = self._conv_params(a, cfg, kw), self._conv_params(b, cfg, kw)
+        kf = self.kconv_preset.get(id(a)) or self.kconv_preset.get(id(b))
+        if kf is not None:  # the pair presets the stage's first K-split 3x3 conv's accumulator
+            self._set_kconv_preset(pa, kf)
         self.configs.append((a.attrs.get("name", "") + "+" + b.attrs.get("name", ""), key, cfg, kw))
         N.check(lib.hz_prog_add_conv2(self.prog, C.byref(pa), C.byref(pb), cfg, a.slot), "add_conv2")
 
@@ -244,6 +251,12 @@ class ExecContext:
         self._keep.append(buf)
         return buf.data_ptr()
 
+    def _set_kconv_preset(self, prm, f) -> None:
+        k = f.nodes[0]
+        _, h, w, c = self.graph.shape(k.outputs[0])
+        prm.zinit, prm.zbias = self._addr(k.outputs[0]), self.params[k.attrs["w"]].bias.data_ptr()
+        prm.z_C, prm.z_HW = c, h * w
+
     def _conv_flops(self, n) -> int:
         pc = self.params[n.attrs["w"]]
         nb, p, q, _ = self.graph.shape(n.outputs[0])
@@ -261,6 +274,8 @@ class ExecContext:
                 n.attrs.get("out_f32", False), cfg, kw, out_rowmajor=n.attrs.get("rowmajor", False))
             if id(n) in self.seam_consumer or id(n) in self.f32_readers:  # reads an fp32 accumulator
                 prm.x_f32 = 1  # (a seam's conv1 sum or a K-split 3x3 conv's output; ReLU at the load)
+            if id(n) in self.kconv_preset:
+                self._set_kconv_preset(prm, self.kconv_preset[id(n)])
             if id(n) in self.seam_init:  # presets the next seam's accumulator to conv1's bias
                 f = self.seam_init[id(n)]
                 t1 = f.nodes[1].outputs[0]

@@ -28,7 +28,7 @@ class KconvParams(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
                 ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
                 ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("pad_", C.c_int)]
+                ("stride", C.c_int)]
 
 
 def prog_of(add, reps=REPS):

@@ -3,6 +3,8 @@ discipline (replay == eager, new input picked up), concurrent contexts."""
 import pytest
 import torch
 
+from conftest import logits_match
+
 from hipzap.engine.engine import Engine
 from hipzap.engine.program import ExecContext
 from hipzap.engine.reference import run_graph_reference
@@ -58,7 +60,7 @@ def test_graph_replay_equals_eager_and_tracks_input(model_sd):
             ctx_g.input.copy_(x)
             ctx_g.replay(s)
         torch.cuda.synchronize()
-        assert torch.equal(ctx_e.output, ctx_g.output)  # deterministic kernels: bitwise
+        assert logits_match(ctx_g.output, ctx_e.output)  # bitwise unless the program has seams
 
 
 def test_concurrent_contexts(model_sd):
@@ -67,7 +69,7 @@ def test_concurrent_contexts(model_sd):
     xs = [torch.randn(1, 3, 224, 224) for _ in range(4)]
     singles = [eng.infer(x) for x in xs] + [eng.infer(x) for x in xs]
     for i in range(4):
-        assert torch.equal(singles[i], singles[i + 4])
+        assert logits_match(singles[i + 4], singles[i])
     secs = eng.bench(20)
     assert secs > 0
 
@@ -83,7 +85,7 @@ def test_deferred_contexts(model_sd):
     assert eng.ensure_contexts() > 0 and len(eng.contexts) == len(eng.streams) == len(eng._locks) == 3
     assert eng.ensure_contexts() == 0.0
     for _ in range(3):
-        assert torch.equal(eng.infer(x), y0)
+        assert logits_match(eng.infer(x), y0)
     assert eng.bench(5) > 0
 
 
@@ -125,7 +127,7 @@ def test_zero_copy_host_io(model_sd, zc):
     eng = Engine.from_state_dict(name, sd, DEV, batch=1, zero_copy=zc)
     for seed in range(3):
         x = torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(seed))
-        assert torch.equal(eng.infer(x), base.infer(x))
+        assert logits_match(eng.infer(x), base.infer(x))
 
 
 def test_dynamic_batching_backend(model_sd):
@@ -152,7 +154,7 @@ def test_dynamic_batching_backend(model_sd):
     for t in th:
         t.join(timeout=60)
     for a, b in zip(out, solo):
-        assert torch.equal(a, b)  # rows are independent: same kernels, same result per row
+        assert logits_match(a, b)  # rows are independent: same kernels, same result per row
     assert be.batcher.batches < 4  # at least two requests shared a replay
     be.batcher.close()
 
@@ -171,7 +173,7 @@ def test_checkpoint_packed_fast_path(model_sd, tmp_path):
     fast = Engine.from_checkpoint(name, ck, DEV, batch=1)
     assert "load_packed_ms" in fast.timings and "pack_ms" not in fast.timings
     x = torch.randn(1, 3, 224, 224)
-    assert torch.equal(first.infer(x), fast.infer(x))
+    assert logits_match(first.infer(x), fast.infer(x))
 
 
 def test_shared_context_streams_bitwise(monkeypatch):
@@ -188,7 +190,7 @@ def test_shared_context_streams_bitwise(monkeypatch):
     eng.ensure_contexts()
     assert len({s.cuda_stream for s in eng.streams}) == 2
     outs = [eng.infer(x) for _ in range(12)]
-    assert all(torch.equal(o, ref) for o in outs)
+    assert all(logits_match(o, ref) for o in outs)
 
 
 @pytest.mark.parametrize("arch,dtype", [("resnet50", torch.float32), ("resnet18", torch.float32),

@@ -194,11 +194,14 @@ def test_resnet50_kconvs(r50):
     a, params, kw = r50
     g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam,kconv", batch=1, input_uint8=True)
     kc = [f for f in fz.values() if f.kind == "kconv"]
-    assert [f.nodes[0].attrs["name"] for f in kc] == [f"layer3.{b}.conv2" for b in range(1, 6)] + \
-        [f"layer4.{b}.conv2" for b in range(1, 3)]
-    assert [f.next_seam is None for f in kc] == [False] * 4 + [True] + [False, True]
+    assert [f.nodes[0].attrs["name"] for f in kc] == [f"layer3.{b}.conv2" for b in range(0, 6)] + \
+        [f"layer4.{b}.conv2" for b in range(0, 3)]
+    assert [f.next_seam is None for f in kc] == [False] * 5 + [True] + [False] * 2 + [True]
     for f in kc:
-        assert fz[f.seam].kind == "seam" and fz[f.seam].consumer == f.start
+        if f.seam is None:  # a stage's first block: stride 2, preset by its conv1 (paired with the downsample)
+            assert f.nodes[0].attrs["name"].endswith(".0.conv2") and g.nodes[f.preset].attrs["name"].endswith(".0.conv1")
+        else:
+            assert fz[f.seam].kind == "seam" and fz[f.seam].consumer == f.start and f.preset == f.seam + 1
         if f.next_seam is not None:
             assert fz[f.next_seam].init == f.start and f.reader is None
         else:
@@ -207,9 +210,9 @@ def test_resnet50_kconvs(r50):
     offsets, _ = plan_memory(gp, groups=[(f.start, f.end) for f in fz.values()])
     for f in kc:
         a_t = f.nodes[0].outputs[0]
-        assert gp.tensors[a_t].dtype == torch.float32 and a_t in gp.nodes[f.seam + 1].outputs
+        assert gp.tensors[a_t].dtype == torch.float32 and a_t in gp.nodes[f.preset].outputs
         z0, z1 = offsets[a_t], offsets[a_t] + gp.tensors[a_t].nbytes
-        for j in range(f.seam, f.start + 2):  # presetting seam .. the reader
+        for j in range(f.preset, f.start + 2):  # presetting launch .. the reader
             for t in g.nodes[j].inputs + g.nodes[j].outputs:
                 if t == a_t or t is None or g.tensors[t].external:
                     continue

@@ -132,7 +132,7 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     seam = ExecContext(g, params, torch.device(DEV), fuse=spec)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     assert sum(f.kind == "seam" for f in seam.fused.values()) == 7
-    assert sum(f.kind == "kconv" for f in seam.fused.values()) == (7 if "kconv" in spec else 0)
+    assert sum(f.kind == "kconv" for f in seam.fused.values()) == (9 if "kconv" in spec else 0)
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
     _run(seam, x)
     _run(plain, x)
@@ -176,46 +176,54 @@ class KconvParams(C.Structure):  # HzKconvParams (csrc/hipzap.h)
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
                 ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
                 ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("pad_", C.c_int)]
+                ("stride", C.c_int)]
 
 
 HZ_K_KCONV = 21
 
 
-@pytest.mark.parametrize("c,h,ck,xf32,n", [(256, 14, 64, True, 1), (256, 14, 32, True, 1), (256, 14, 64, False, 2),
-                                           (512, 7, 128, True, 1), (512, 7, 64, True, 2), (512, 7, 128, False, 1)])
-def test_kconv_vs_fp32(c, h, ck, xf32, n):
-    """K-split 3x3 conv: out = preset bias + conv3x3(relu(z) in bf16) by atomics; also presets the
-    next accumulator."""
-    g = torch.Generator().manual_seed(c + ck + n)
+@pytest.mark.parametrize("c,h,ck,xf32,n,st", [(256, 14, 64, True, 1, 1), (256, 14, 32, True, 1, 1),
+                                              (256, 14, 64, False, 2, 1), (512, 7, 128, True, 1, 1),
+                                              (512, 7, 64, True, 2, 1), (512, 7, 128, False, 1, 1),
+                                              (256, 28, 32, False, 1, 2), (256, 28, 64, False, 2, 2),
+                                              (512, 14, 64, False, 1, 2), (512, 14, 128, True, 1, 2)])
+def test_kconv_vs_fp32(c, h, ck, xf32, n, st):
+    """K-split 3x3 conv (stride 1 or 2, pad 1): out = preset bias + conv3x3(x, or relu(z) in bf16)
+    by atomics; also presets the next accumulator."""
+    g = torch.Generator().manual_seed(c + ck + n + st)
     x = torch.randn(n, h, h, c, generator=g)
     pc = CV.pack_conv(torch.randn(c, c, 3, 3, generator=g) * (2.0 / (9 * c)) ** 0.5, 0.1 * torch.randn(c, generator=g),
-                      None, 1, 1)
+                      None, st, 1)
     xin = (torch.relu(x) if xf32 else x).to(torch.bfloat16).float()
     wref = pc.dense().reshape(c, 3, 3, c).permute(0, 3, 1, 2)
-    ref = torch.nn.functional.conv2d(xin.permute(0, 3, 1, 2), wref, pc.bias, padding=1).permute(0, 2, 3, 1)
+    ref = torch.nn.functional.conv2d(xin.permute(0, 3, 1, 2), wref, pc.bias, stride=st, padding=1).permute(0, 2, 3, 1)
+    ho = h // st
     pcd = pc.to(DEV)
     xd = _blk(x) if xf32 else _blk(x.to(torch.bfloat16))
-    out = pcd.bias.view(1, c // 32, 1, 1, 32).expand(n, c // 32, h, h, 32).contiguous()
-    nxt = torch.full((n, 8, h, h, 32), float("nan"), device=DEV)
+    out = pcd.bias.view(1, c // 32, 1, 1, 32).expand(n, c // 32, ho, ho, 32).contiguous()
+    nxt = torch.full((n, 8, ho, ho, 32), float("nan"), device=DEV)
     zb = torch.randn(256, generator=g).to(DEV)
     prm = KconvParams()
     prm.x, prm.w, prm.out, prm.zinit, prm.zbias = xd.data_ptr(), pcd.wf.data_ptr(), out.data_ptr(), nxt.data_ptr(), \
         zb.data_ptr()
-    prm.z_C, prm.z_HW, prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.x_f32, prm.ck = 256, h * h, n, h, h, c, c, int(xf32), ck
+    prm.z_C, prm.z_HW, prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.x_f32, prm.ck, prm.stride = \
+        256, ho * ho, n, h, h, c, c, int(xf32), ck, st
     N.check(N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), N.stream_ptr()), "kconv")
     torch.cuda.synchronize()
-    got = CV.from_blocked(out.cpu(), (n, h, h, c))
+    got = CV.from_blocked(out.cpu(), (n, ho, ho, c))
     assert _rel(got, ref) < 1e-3, _rel(got, ref)
-    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, h, h, 256)), zb.cpu().expand(n, h, h, 256))
+    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, ho, ho, 256)), zb.cpu().expand(n, ho, ho, 256))
 
 
 def test_kconv_refuses_bad_geometry():
     prm = KconvParams()
     buf = torch.zeros(1 << 20, device=DEV)
     prm.x, prm.w, prm.out = buf.data_ptr(), buf.data_ptr(), buf.data_ptr()
-    prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.ck = 1, 28, 28, 256, 256, 64  # 784 pixels: no kernel for that
+    prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.ck = 1, 28, 28, 256, 256, 64  # 784 pixels at stride 1: none
     assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
+    prm.stride = 3
+    assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
+    prm.stride = 1
     prm.H = prm.W = 14
     prm.ck = 96
     assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
