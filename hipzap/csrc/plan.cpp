@@ -570,15 +570,16 @@ void* hz_plan_open(const char* path, int device, int read_blob, double* timings)
   // Joined before returning: left running into the caller's context setup (stream creation,
   // hipMemsetAsync), it crashed the runtime in a process that already held RCCL communicators
   // (tests/test_cluster_gpu.py, profiles/r3_warm3/README.md).
-  // Order (HIPZAP_PLAN_WARM_ORDER): "stream" (default) starts the thread once the upload stream
-  // exists, so the process's first hipStreamCreate (HIP's lazy queue setup) never runs beside the
-  // code-object loads -- the driver's round-4 box showed the first stream finishing only when the
-  // warm thread did (stream 161 ms, warm 163 ms); "init": right after HIP init
-  // (rounds 3-4).
+  // Order (HIPZAP_PLAN_WARM_ORDER): "init" (default) starts the thread right after HIP init;
+  // "stream" waits until the upload stream exists, so the process's first hipStreamCreate (HIP's
+  // lazy queue setup) never runs beside the code-object loads (the driver's round-4 box showed the
+  // first stream finishing only when the warm thread did). Measured negative:
+  // 10 interleaved trials each (profiles/r5_cold) gave p50 228.1 ms "init" vs 238.8 ms "stream"
+  // -- the stream took ~20.7 ms either way and "stream" added a 6.7 ms wait for the warm thread.
   const char* cw = getenv("HIPZAP_PLAN_CODE_WARM");
   const char* wo = getenv("HIPZAP_PLAN_WARM_ORDER");
   const bool warm_on = !(cw && cw[0] == '0');
-  const bool warm_early = wo && std::strcmp(wo, "init") == 0;
+  const bool warm_early = !(wo && std::strcmp(wo, "stream") == 0);
   auto start_warm = [&]() {
     const unsigned units = p->code_units() | ((p->h.flags & kFlagWeightless) ? kUnitPack : 0u);
     double* t_warm = &p->t[HZ_PLAN_T_WARM_THREAD];  // written by the thread, read after the join

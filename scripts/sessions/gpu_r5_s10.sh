@@ -1,11 +1,11 @@
 #!/bin/bash
-# r5 s9: the full GPU suite with seam + kconv as the default fusion (which bitwise tests notice the
+# r5 s10 (s9 re-run after the test fixes): the full GPU suite with seam + kconv as the default fusion (which bitwise tests notice the
 # atomics), then the headline A/B of the new defaults (seam CS 128,128; 16-B preprocess loads) and
 # the stride-2 kconv slice variants
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r5_s9; mkdir -p $O
+O=gpurun_out/r5_s10; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/ > $O/pytest.log 2>&1
 echo "pytest rc=$?"
 grep -E 'FAILED|ERROR|passed|failed' $O/pytest.log | tail -25

@@ -122,7 +122,7 @@ def _mx_decode(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
     return q8.view(torch.float8_e4m3fn).float() * sc
 
 
-@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 43, 44, 45])
+@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33])
 @pytest.mark.parametrize("mx_in,mx_out", [(True, False), (False, True), (True, True)])
 def test_gemm_mx8_activations(cfg, mx_in, mx_out):
     """MX8 (e4m3 + E8M0 per 32 k) activations into the block-scaled MFMA, and MX8 output from
