@@ -904,24 +904,30 @@ __device__ __forceinline__ int seam_lds(int row, int chunk) {  // bf16 offset of
 
 // (one workgroup per CU is the design point -- 56-128 workgroups -- so the register budget is 256:
 // with hipcc's default occupancy target its scheduler sinks the ring's loads next to their MFMAs)
-template <int CM, int CS, bool T2F32>
+//
+// TAIL (the network's last block, HzSeamParams.tail): phase 1 only, over ONE 64-pixel tile per image
+// (HW <= 64), and instead of storing y the workgroup averages its slice over the pixels -- the global
+// average pool of the classifier head, complete inside the workgroup (no atomics): fp32 [N][4CM] into
+// y's buffer, which the FC launch after it reads as-is (HzPoolFcParams.pooled).
+template <int CM, int CS, bool T2F32, bool TAIL = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void seam_kernel(const HzSeamParams p) {
   constexpr int CO = 4 * CM;
   constexpr int KS3 = CM / 32;     // conv3 k-steps
   constexpr int RG = CS / 16;      // conv3 row groups in the slice (4 or 8)
-  constexpr int PGW = 2 * RG / 8;  // 16-pixel groups per wave (1 or 2)
+  constexpr int PT = TAIL ? 64 : 32;   // pixel tile
+  constexpr int PGW = (PT / 16) * RG / 8;  // 16-pixel groups per wave (1 or 2; tail 2 or 4)
   constexpr int ZB = CM / 32;      // conv1 output column blocks (8 or 16)
   constexpr int ZBW = ZB / 8;      // per wave
   constexpr int KS1 = CS / 16;     // conv1 k-steps over the slice (32x32x16)
   constexpr int KSW1 = CO / 32;    // conv1 weight k-steps (its packing)
   constexpr int D = KS3;  // conv3 weight k-steps in flight
-  __shared__ __attribute__((aligned(16))) bf16_t Y[32 * CS];
+  __shared__ __attribute__((aligned(16))) bf16_t Y[TAIL ? 8 : 32 * CS];
   // the tile's t2 (32 pixels x CM) is staged ONCE per workgroup in LDS as bf16 (fp32 t2: with the
   // ReLU applied), [CM/8 chunks][32 pixels][8]: every wave's B fragment is then one conflict-free
   // ds_read_b128 (16 consecutive pixels of one chunk) instead of every wave re-reading the tile from
   // L1/L2 -- fp32 t2 read that way took 2x the seam's time, and staging also took the bf16 seam
   // from 7.1 to ~6 us (profiles/r5_seam)
-  __shared__ __attribute__((aligned(16))) bf16_t T2S[CM * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t T2S[CM * PT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4, l16 = lane & 15;
   const int h = lane >> 5, l32 = lane & 31;
@@ -929,20 +935,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int lid = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids (one XCD) share a weight slice
   const int slice = lid / nt, rem = lid - slice * nt;
   const int n = rem / p.tiles, t = rem - n * p.tiles;
-  const int hw0 = t * HW / p.tiles, cnt = (t + 1) * HW / p.tiles - hw0;  // <= 32 (launcher)
+  const int hw0 = t * HW / p.tiles, cnt = (t + 1) * HW / p.tiles - hw0;  // <= PT (launcher)
   const int c0 = slice * CS;
   const int rg = wave % RG, pg0 = (wave / RG) * PGW;
   const int ch = c0 + 16 * rg + 4 * g4;  // this lane's 4 conv3 output channels
 
   // ---- the staging loads first of all (the wait before the LDS writes then covers them only)
-  constexpr int NSE = CM * 32 / 8 / 512;
+  constexpr int NSE = CM * PT / 8 / 512;
   f32x4 sf[T2F32 ? NSE : 1][2];
   u32x4 sb[T2F32 ? 1 : NSE];
 #pragma unroll
   for (int i = 0; i < NSE; ++i) {
     // entry e -> (32-channel block cb, pixel px, 8-channel sub-chunk): consecutive threads read
     // consecutive 16 / 32 B of one pixel's line, then the next pixel's
-    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & (PT - 1), cb = e / (4 * PT);
     const long off = (((long)n * KS3 + cb) * HW + hw0 + min(px, cnt - 1)) * 32 + sub * 8;
     if constexpr (T2F32) {
       const float* xf = reinterpret_cast<const float*>(p.t2) + off;
@@ -975,7 +981,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // ---- conv1 weights of this wave's column blocks (phase 2's B operands), behind the ring ----
   bf16x8 fw[ZBW][KS1];
 #pragma unroll
-  for (int i = 0; i < ZBW; ++i) {
+  for (int i = 0; i < (TAIL ? 0 : ZBW); ++i) {
     const int zc = 32 * (wave * ZBW + i) + l32;
 #pragma unroll
     for (int u = 0; u < KS1; ++u) {
@@ -987,7 +993,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   asm volatile("" ::: "memory");  // keep those loads here: hipcc otherwise sinks them below phase 1
 #pragma unroll
   for (int i = 0; i < NSE; ++i) {
-    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & (PT - 1), cb = e / (4 * PT);
     u32x4 v;
     if constexpr (T2F32) {
       const f32x4 a = sf[i][0], b = sf[i][1];
@@ -996,7 +1002,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     } else {
       v = sb[i];
     }
-    *reinterpret_cast<u32x4*>(T2S + ((cb * 4 + sub) * 32 + px) * 8) = v;
+    *reinterpret_cast<u32x4*>(T2S + ((cb * 4 + sub) * PT + px) * 8) = v;
   }
   lds_sync();
   f32x4 acc[PGW];
@@ -1006,10 +1012,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   for (int s = 0; s < KS3; ++s) {
 #pragma unroll
     for (int q = 0; q < PGW; ++q) {
-      fb[s][q] = *reinterpret_cast<const bf16x8*>(T2S + ((s * 4 + g4) * 32 + 16 * (pg0 + q) + l16) * 8);
+      fb[s][q] = *reinterpret_cast<const bf16x8*>(T2S + ((s * 4 + g4) * PT + 16 * (pg0 + q) + l16) * 8);
       acc[q] = mfma16(fa[s], fb[s][q], acc[q]);
     }
     if (s + D < KS3) load(s + D);
+  }
+  if constexpr (TAIL) {  // ---- pooled epilogue: mean over the image's pixels of ReLU(conv3 + bias + res)
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < PGW; ++q) {
+      const float v[4] = {acc[q][0] + bias[0] + __uint_as_float(rr[q][0] << 16),
+                          acc[q][1] + bias[1] + __uint_as_float(rr[q][0] & 0xffff0000u),
+                          acc[q][2] + bias[2] + __uint_as_float(rr[q][1] << 16),
+                          acc[q][3] + bias[3] + __uint_as_float(rr[q][1] & 0xffff0000u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sm[e] += yv[q] ? fmaxf(v[e], 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1)  // the 16 lanes of a g4 group hold 16 pixels of the same 4 channels
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sm[e] += __shfl_xor(sm[e], m);
+    const float inv = 1.f / HW;
+    float* po = reinterpret_cast<float*>(p.y) + (long)n * CO + ch;
+    if constexpr (RG == 8) {  // one wave per row group: its sums are complete
+      if (l16 == 0) *reinterpret_cast<f32x4*>(po) = f32x4{sm[0] * inv, sm[1] * inv, sm[2] * inv, sm[3] * inv};
+    } else {  // two waves per row group (pixel halves): the second hands its sums over through LDS
+      __shared__ f32x4 PR[RG][4];
+      if (wave >= RG && l16 == 0) PR[rg][g4] = f32x4{sm[0], sm[1], sm[2], sm[3]};
+      __syncthreads();
+      if (wave < RG && l16 == 0) {
+        const f32x4 o = PR[rg][g4];
+        *reinterpret_cast<f32x4*>(po) =
+            f32x4{(sm[0] + o[0]) * inv, (sm[1] + o[1]) * inv, (sm[2] + o[2]) * inv, (sm[3] + o[3]) * inv};
+      }
+    }
+    return;
   }
   // ---- phase-1 epilogue: y slice -> global (bf16) and LDS ----
   const int cl = 16 * rg + 4 * g4;  // local channel in the slice
@@ -1247,8 +1284,22 @@ extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
 
 extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
   const HzSeamParams& p = *pp;
-  if (!p.t2 || !p.w3 || !p.b3 || !p.res || !p.y || !p.w1 || !p.z) return -1;
+  if (!p.t2 || !p.w3 || !p.b3 || !p.res || !p.y) return -1;
   if (p.N < 1 || p.HW < 1 || (p.CM != 256 && p.CM != 512) || (p.cs != 64 && p.cs != 128)) return -1;
+  if (p.tail) {  // conv3 + pool of the last block: one 64-pixel tile per image, no conv1 half
+    if (p.HW > 64 || p.CM != 512 || p.zinit) return -1;
+    HzSeamParams q = p;
+    q.tiles = 1;
+    const dim3 grid(p.N * (4 * p.CM / p.cs));
+#define HZ_TAIL(CS)                                                                                        \
+  if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<512, CS, true, true>), grid, dim3(512), 0, st, q);        \
+  else hipLaunchKernelGGL((seam_kernel<512, CS, false, true>), grid, dim3(512), 0, st, q);
+    if (p.cs == 128) { HZ_TAIL(128) }
+    else { HZ_TAIL(64) }
+#undef HZ_TAIL
+    return (int)hipGetLastError();
+  }
+  if (!p.w1 || !p.z) return -1;
   HzSeamParams q = p;
   q.tiles = (p.HW + 31) / 32;  // balanced tiles of <= 32 pixels
   const dim3 grid(q.tiles * p.N * (4 * p.CM / p.cs));

@@ -80,6 +80,7 @@ typedef struct HzPoolFcParams {
   const float* bias;        // [N]
   float* out;               // fp32 [B][ldo]
   int B, C, HW, N, ldo;
+  int pooled, pad_;         // pooled: x is already the fp32 [B][C] channel means (a tail seam's output)
 } HzPoolFcParams;
 int hz_pool_fc_launch(const HzPoolFcParams* p, hipStream_t st);
 
@@ -444,6 +445,8 @@ typedef struct HzSeamParams {
   float* zinit;               // or NULL: afterwards filled with zbias per channel ([N][z_C/32][z_HW][32]):
   const float* zbias;         //   the next K-split 3x3 conv's accumulator
   int z_C, z_HW;
+  int tail, pad_;             // tail: the last block -- conv3 + global average pool, no conv1 half (w1, z
+                              //   unused): fp32 [N][4CM] means into y's buffer (HW <= 64, CM 512)
 } HzSeamParams;
 // K-split 3x3 conv (pad 1, stride 1 at <= 14 x 14 or stride 2 from <= 28 x 28) into an fp32
 // accumulator (block.hip kconv_kernel):

@@ -129,7 +129,12 @@ __global__ __launch_bounds__(256) void pool_fc_kernel(const HzPoolFcParams p) {
   u32x4 wv[WB];
 #pragma unroll
   for (int j = 0; j < WB; ++j) wv[j] = *reinterpret_cast<const u32x4*>(wg + (long)min(cb_lo + j, cb_hi - 1) * 512);
-  for (int cb0 = cb_lo; cb0 < cb_hi; cb0 += 16) {
+  if (p.pooled) {  // x = the fp32 channel means already (a tail seam, block.hip): copy the wave's slice
+    const float* xp = reinterpret_cast<const float*>(p.x) + (long)b * p.C;
+    for (int c = cb_lo * 32 + lane * 4; c < cb_hi * 32; c += 256)
+      *reinterpret_cast<f32x4*>(pooled + c) = *reinterpret_cast<const f32x4*>(xp + c);
+  }
+  for (int cb0 = cb_lo; cb0 < (p.pooled ? cb_lo : cb_hi); cb0 += 16) {
     const int cb = cb0 + (lane >> 2), sub = lane & 3;
     if (cb < cb_hi) {
       const bf16_t* src = p.x + (((long)b * ncb + cb) * p.HW) * 32 + sub * 8;

@@ -20,6 +20,10 @@ bind as ONE fused kernel instead:
   at its operand load (``HzConvParams.x_f32``). The accumulator is conv1's output tensor, planned
   as fp32 (:func:`planning_graph`). Atomic accumulation order varies run to run: a seam program is
   numerically equal to the per-conv one within fp32 rounding, not bitwise reproducible.
+* ``kconv``: a seam's 3x3 neighbours as K-split 3x3 launches into fp32 accumulators
+  (``kconv_kernel``; :func:`match_kconvs`).
+* ``tail``: the last block's conv3 + the global average pool (the seam kernel's tail mode): the
+  classifier's ``pool_fc`` then reads fp32 channel means (``HzPoolFcParams.pooled``).
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
@@ -38,10 +42,11 @@ import numpy as np
 from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
-KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv")
+KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box; round 5
-# adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, profiles/r5_seam)
-DEFAULT = "convpool,bneck,bneck2,seam,kconv"
+# adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, and the pooling
+# tail: pool_fc 7.5 -> 4.6 us, sustained 13.2-13.9k -> 14.4k same box, profiles/r5_seam)
+DEFAULT = "convpool,bneck,bneck2,seam,kconv,tail"
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -62,7 +67,7 @@ class SeamParams(C.Structure):  # HzSeamParams
     _fields_ = [("t2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("res", C.c_void_p),
                 ("y", C.c_void_p), ("w1", C.c_void_p), ("z", C.c_void_p), ("N", C.c_int), ("HW", C.c_int),
                 ("CM", C.c_int), ("cs", C.c_int), ("tiles", C.c_int), ("t2_f32", C.c_int), ("zinit", C.c_void_p),
-                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int)]
+                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("tail", C.c_int), ("pad_", C.c_int)]
 
 
 class KconvParams(C.Structure):  # HzKconvParams
@@ -252,6 +257,31 @@ def match_seam(g, params, i: int) -> Fused | None:
     return Fused("seam", i, i + 2, [c3, c1], init=i - 1, consumer=i + 2)
 
 
+def match_tail(g, params, i: int) -> Fused | None:
+    """nodes[i] = conv3 of the network's last bottleneck (1x1 512 -> 2048 + residual, <= 64 pixels),
+    nodes[i+1] = the pooled classifier (``pool_fc``) reading its output alone: conv3 binds as the
+    seam kernel's tail mode, which writes the channel means instead of the block output, and the
+    pool_fc launch reads them (``reader``)."""
+    nodes = g.nodes
+    if i + 2 > len(nodes):
+        return None
+    c3, pf = nodes[i:i + 2]
+    if not _conv(c3) or pf.kind != "pool_fc" or pf.inputs != [c3.outputs[0]] or c3.slot != pf.slot:
+        return None
+    if c3.attrs.get("out_f32") or c3.attrs.get("rowmajor") or c3.attrs.get("act", "relu") != "relu":
+        return None
+    p3 = params.get(c3.attrs.get("w"))
+    if p3 is None or not _geom(p3, 512, 2048, 1, 1, 0) or len(c3.inputs) != 2:
+        return None
+    y = c3.outputs[0]
+    if y in g.outputs or g.tensors[y].external or any(y in n.inputs for j, n in enumerate(nodes) if j != i + 1):
+        return None
+    sh = g.shape(y)
+    if len(sh) != 4 or sh[1] * sh[2] > 64 or g.shape(c3.inputs[1]) != sh:
+        return None
+    return Fused("tail", i, i + 1, [c3], reader=i + 1)
+
+
 def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
     """{first node index: Fused} for every fusible run of ``g`` (non-overlapping, in order)."""
     kinds = enabled_kinds() if kinds is None else kinds
@@ -284,8 +314,13 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
         out.update(seams)
         if "kconv" in kinds:
             out.update(match_kconvs(g, params, seams, covered))
-        out = dict(sorted(out.items()))
-    return out
+    if "tail" in kinds:
+        covered = {j for f in out.values() for j in range(f.start, f.end)}
+        for i in range(len(g.nodes)):
+            f = match_tail(g, params, i)
+            if f is not None and i not in covered and i + 1 not in covered:
+                out[i] = f
+    return dict(sorted(out.items()))
 
 
 def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
@@ -380,6 +415,19 @@ def seam_cs(cm: int) -> int:
 
 
 def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamParams:
+    fused = fused or {}
+    kc = fused.get(f.start - 1)  # t2 is a K-split conv's fp32 accumulator
+    if f.kind == "tail":
+        c3 = f.nodes[0]
+        p3 = params[c3.attrs["w"]]
+        p = SeamParams()
+        p.t2, p.res, p.y = addr(c3.inputs[0]), addr(c3.inputs[1]), addr(c3.outputs[0])
+        p.w3, p.b3 = p3.wf.data_ptr(), p3.bias.data_ptr()
+        nb, h, w, _ = g.shape(c3.outputs[0])
+        p.N, p.HW, p.CM, p.tail = nb, h * w, p3.cin, 1
+        p.cs = int(os.environ.get("HIPZAP_TAIL_CS", "64"))  # 32 workgroups at bs=1 (128: 16, measured slower)
+        p.t2_f32 = int(kc is not None and kc.kind == "kconv")
+        return p
     c3, c1 = f.nodes
     p3, p1 = params[c3.attrs["w"]], params[c1.attrs["w"]]
     p = SeamParams()
@@ -388,8 +436,6 @@ def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamPar
     nb, h, w, _ = g.shape(c3.outputs[0])
     p.N, p.HW, p.CM = nb, h * w, p1.cout
     p.cs = seam_cs(p.CM)
-    fused = fused or {}
-    kc = fused.get(f.start - 1)  # t2 is a K-split conv's fp32 accumulator
     p.t2_f32 = int(kc is not None and kc.kind == "kconv")
     kn = fused.get(f.consumer)  # this seam presets its consumer's accumulator
     if kn is not None and kn.kind == "kconv":
@@ -488,7 +534,7 @@ def add_fused(prog, g, params, f: Fused, addr, lib, fused: dict | None = None) -
     """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
     if f.kind in ("stem", "convpool"):
         prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
-    elif f.kind == "seam":
+    elif f.kind in ("seam", "tail"):
         prm, kind = seam_params(g, params, f, addr, fused), HZ_K_SEAM
     elif f.kind == "kconv":
         prm, kind = kconv_params(g, params, f, addr, fused or {}), HZ_K_KCONV
@@ -501,5 +547,5 @@ def add_fused(prog, g, params, f: Fused, addr, lib, fused: dict | None = None) -
 
 def launch(kind: str, prm, stream=None) -> None:
     """Eager launch of a fused kernel (tests)."""
-    k = {"stem": HZ_K_STEM, "seam": HZ_K_SEAM, "kconv": HZ_K_KCONV}.get(kind, HZ_K_BNECK)
+    k = {"stem": HZ_K_STEM, "seam": HZ_K_SEAM, "tail": HZ_K_SEAM, "kconv": HZ_K_KCONV}.get(kind, HZ_K_BNECK)
     N.check(N.lib().hz_launch_kernel(k, C.byref(prm), N.stream_ptr(stream)), f"launch_{kind}")

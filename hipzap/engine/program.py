@@ -82,6 +82,8 @@ class ExecContext:
         self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
         self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}
         self.f32_readers = {id(g.nodes[f.reader]) for f in self.fused.values() if f.kind == "kconv" and f.reader}
+        # a kconv's reader bound as a tail seam instead reads its accumulator through HzSeamParams.t2_f32
+        self.pooled_readers = {id(g.nodes[f.reader]) for f in self.fused.values() if f.kind == "tail"}
         # K-split 3x3 convs preset by a plain (or paired) conv launch: a stage's first block
         self.kconv_preset = {id(g.nodes[f.preset]): f for f in self.fused.values()
                              if f.kind == "kconv" and f.seam is None}
@@ -386,7 +388,8 @@ class ExecContext:
             nb, h, w, c = g.shape(n.inputs[0])
             assert conv_ops.is_blocked(c) and pc.K == c and pc.ksteps * 32 == c
             prm = vision.PoolFcParams(addr(n.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), addr(n.outputs[0]),
-                                      nb, c, h * w, pc.cout, g.shape(n.outputs[0])[-1])
+                                      nb, c, h * w, pc.cout, g.shape(n.outputs[0])[-1],
+                                      int(id(n) in self.pooled_readers))
             tx.prog_add(self.prog, vision.K_POOL_FC, prm, n.slot, lib=lib)
         elif n.kind == "softmax":
             ishape = g.shape(n.inputs[0])

@@ -12,7 +12,8 @@ K_POOL_FC = 13
 
 class PoolFcParams(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("out", C.c_void_p), ("B", C.c_int),
-                ("C", C.c_int), ("HW", C.c_int), ("N", C.c_int), ("ldo", C.c_int)]
+                ("C", C.c_int), ("HW", C.c_int), ("N", C.c_int), ("ldo", C.c_int),
+                ("pooled", C.c_int), ("pad_", C.c_int)]
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)

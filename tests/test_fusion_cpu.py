@@ -218,3 +218,22 @@ def test_resnet50_kconvs(r50):
                     continue
                 o0, o1 = offsets[t], offsets[t] + gp.tensors[t].nbytes
                 assert o1 <= z0 or z1 <= o0, (g.nodes[j].attrs.get("name"), g.tensors[t].name)
+
+
+def test_resnet50_tail(r50):
+    """``tail``: the last block's conv3 (1x1 512 -> 2048 + residual, 7 x 7) next to the pooled
+    classifier becomes the seam kernel's pooling tail; the pool_fc node stays and reads the means.
+    Not matched when the block output is read elsewhere, nor on a larger final feature map."""
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam,kconv,tail", batch=1, input_uint8=True)
+    tails = [f for f in fz.values() if f.kind == "tail"]
+    assert len(tails) == 1
+    f = tails[0]
+    assert f.nodes[0].attrs["name"] == "layer4.2.conv3" and g.nodes[f.reader].kind == "pool_fc"
+    assert f.end == f.start + 1 and fz[f.start - 1].kind == "kconv"  # t2 is a K-split conv's fp32 sum
+    g2 = a.build_graph(**dict(kw, batch=1, input_uint8=True))
+    g2.outputs.append(f.nodes[0].outputs[0])  # a tap on the block output
+    assert not any(x.kind == "tail" for x in fusion.plan(g2, params, fusion.enabled_kinds("tail")).values())
+    from hipzap.models.resnet import build_graph
+    g3 = build_graph("resnet50", 1, 1000, 288, True)  # 9 x 9 = 81 pixels
+    assert not any(x.kind == "tail" for x in fusion.plan(g3, params, fusion.enabled_kinds("tail")).values())

@@ -7,7 +7,8 @@
   accumulator (HzConvParams.zinit) against the same conv on relu(z) in bf16;
 * ResNet-50 with seams against the per-conv program and the fp32 graph oracle: every block output
   a seam writes, the logits, with the arena's default reuse and without, eager and graph replay;
-  7 dispatches fewer.
+  7 dispatches fewer;
+* the tail (the last block's conv3 + global average pool, the classifier reading the means).
 Atomic accumulation order varies run to run, so comparisons are within fp32/bf16 rounding, not
 bitwise."""
 import ctypes as C
@@ -67,6 +68,35 @@ def test_seam_kernel_vs_fp32(cm, cs, n, h):
     assert _rel(z_got, z_ref) < 2e-3, _rel(z_got, z_ref)
 
 
+@pytest.mark.parametrize("cs,n,h,t2f32", [(128, 1, 7, False), (128, 1, 7, True), (64, 1, 7, True), (64, 3, 7, False),
+                                          (128, 2, 5, True), (128, 1, 8, False)])
+def test_tail_kernel_vs_fp32(cs, n, h, t2f32):
+    """Tail mode (the last block): pooled[n][c] = mean_hw relu(W3 t2 + b3 + res), fp32 into y's buffer;
+    t2 bf16, or fp32 with the ReLU at the load (a K-split conv's accumulator)."""
+    g = torch.Generator().manual_seed(cs + n + h + int(t2f32))
+    cm, co = 512, 2048
+    w3 = torch.randn(co, cm, 1, 1, generator=g) * (2.0 / cm) ** 0.5
+    p3 = CV.pack_conv(w3, 0.1 * torch.randn(co, generator=g))
+    t2 = torch.randn(n, h, h, cm, generator=g)
+    t2in = torch.relu(t2).to(torch.bfloat16)  # what the kernel multiplies either way
+    res = torch.randn(n, h, h, co, generator=g).to(torch.bfloat16)
+    ref = torch.relu(t2in.float() @ p3.dense().t() + p3.bias + res.float()).mean(dim=(1, 2))
+    p3d = p3.to(DEV)
+    t2d = _blk(t2) if t2f32 else _blk(t2in)
+    resd = _blk(res)
+    y = torch.full((n * co * h * h // 2,), float("nan"), device=DEV)  # y's bf16 buffer, as fp32 words
+    prm = fusion.SeamParams()
+    prm.t2, prm.w3, prm.b3, prm.res, prm.y = t2d.data_ptr(), p3d.wf.data_ptr(), p3d.bias.data_ptr(), resd.data_ptr(), \
+        y.data_ptr()
+    prm.N, prm.HW, prm.CM, prm.cs, prm.t2_f32, prm.tail = n, h * h, cm, cs, int(t2f32), 1
+    fusion.launch("tail", prm)
+    torch.cuda.synchronize()
+    got = y[: n * co].view(n, co).cpu()
+    assert _rel(got, ref) < 1e-2, _rel(got, ref)
+    prm.HW = 81  # > one 64-pixel tile
+    assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
+
+
 def test_seam_launch_refuses_bad_geometry():
     prm = fusion.SeamParams()
     buf = torch.zeros(1 << 20, device=DEV)
@@ -118,10 +148,12 @@ def _run(ctx, x):
 
 
 KCONV = SEAMS + ",kconv"
+TAIL = KCONV + ",tail"
 
 
 @pytest.mark.parametrize("batch,noreuse,spec", [(1, True, SEAMS), (1, False, SEAMS), (2, True, SEAMS),
-                                                (1, True, KCONV), (1, False, KCONV), (2, False, KCONV)])
+                                                (1, True, KCONV), (1, False, KCONV), (2, False, KCONV),
+                                                (1, False, TAIL), (2, True, TAIL)])
 def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, monkeypatch):
     if noreuse:
         monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
@@ -133,6 +165,7 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     assert sum(f.kind == "seam" for f in seam.fused.values()) == 7
     assert sum(f.kind == "kconv" for f in seam.fused.values()) == (9 if "kconv" in spec else 0)
+    assert sum(f.kind == "tail" for f in seam.fused.values()) == (1 if "tail" in spec else 0)
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
     _run(seam, x)
     _run(plain, x)
@@ -151,7 +184,7 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     assert torch.equal(ls.argmax(1), lp.argmax(1))
 
 
-@pytest.mark.parametrize("spec", [SEAMS, KCONV])
+@pytest.mark.parametrize("spec", [SEAMS, KCONV, TAIL])
 def test_resnet50_seam_dispatches_and_replay(r50, spec):
     a, params, _, kw = r50
     g = a.build_graph(batch=1, **dict(kw, input_uint8=True))

@@ -132,6 +132,25 @@ def test_pool_fc(B, H, C, N):
     assert ((y.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-2
 
 
+@pytest.mark.parametrize("B,C,N", [(1, 2048, 1000), (3, 512, 10)])
+def test_pool_fc_pooled_input(B, C, N):
+    """HzPoolFcParams.pooled: x is already the fp32 channel means (a tail seam's output) -> FC only."""
+    import ctypes
+    from hipzap import _native as NN
+    from hipzap.ops import conv as Cv
+    from hipzap.ops import vision as V
+    g = torch.Generator().manual_seed(12)
+    m = torch.randn(B, C, generator=g)
+    pc = Cv.pack_linear(torch.randn(N, C, generator=g) * 0.05, torch.randn(N, generator=g))
+    pcd, md = pc.to(DEV), m.to(DEV)
+    out = torch.empty(B, N, device=DEV)
+    prm = V.PoolFcParams(md.data_ptr(), pcd.wf.data_ptr(), pcd.bias.data_ptr(), out.data_ptr(), B, C, 49, N, N, 1)
+    NN.check(NN.lib().hz_launch_kernel(V.K_POOL_FC, ctypes.byref(prm), NN.stream_ptr()), "pool_fc")
+    torch.cuda.synchronize()
+    ref = m.to(torch.bfloat16).float() @ pc.dense().float().t() + pc.bias.float()  # the kernel's bf16 MFMA operands
+    assert ((out.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
 @pytest.mark.parametrize("cfg,kw", [(3, 2), (0, 4), (4, 1)])
 @pytest.mark.parametrize("stride2", [False, True])
 def test_conv_pair_grouped_launch(cfg, kw, stride2):
