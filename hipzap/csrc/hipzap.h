@@ -380,6 +380,18 @@ typedef struct HzVitTokensParams {
 int hz_layernorm_launch(const HzLayerNormParams* p, hipStream_t st);
 int hz_embed_ln_launch(const HzEmbedParams* p, hipStream_t st);
 int hz_attention_launch(const HzAttentionParams* p, hipStream_t st);
+// QKV projection + self-attention in one launch (transformer.hip qkvatt_kernel): one workgroup per
+// (sequence, head), L <= 128, head_dim 64; the QKV GEMM's own weight packing and bias
+typedef struct HzQkvAttParams {
+  const unsigned short* x;    // [B*L][ldx] bf16 (the layer input)
+  const unsigned short* w;    // packed QKV weights [3D/16][D/32][64][8] (rows: Q 0..D-1, K D.., V 2D..)
+  const float* bias;          // [3D]
+  const float* mask;          // additive per-key mask [B][L] or NULL
+  unsigned short* out;        // [B*L][ldo] context, head h at column h*64
+  int B, L, heads, D, ksteps, ldx, ldo;
+  float scale;
+} HzQkvAttParams;
+int hz_qkvatt_launch(const HzQkvAttParams* p, hipStream_t st);
 int hz_vit_tokens_launch(const HzVitTokensParams* p, hipStream_t st);
 
 // row softmax: out[r][i] = exp(s*x[r][i] + mask[i] - m_r) / sum_i(...), i < D
@@ -476,7 +488,8 @@ int hz_block_code_warm(void);
 enum { HZ_K_CONV = 1, HZ_K_LAYERNORM = 2, HZ_K_EMBED = 3, HZ_K_ATTENTION = 4, HZ_K_VIT_TOKENS = 5,
        HZ_K_LSTM = 6, HZ_K_DECODER = 7, HZ_K_SAMPLER = 8, HZ_K_MAXPOOL = 9, HZ_K_QUANT = 10, HZ_K_GEMM_FP8 = 11,
        HZ_K_SOFTMAX = 12, HZ_K_POOL_FC = 13, HZ_K_LMB_LAYER = 14, HZ_K_LMB_DEC = 15,
-       HZ_K_LMB_ADMIT = 16, /* 17: removed */ HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20, HZ_K_KCONV = 21 };
+       HZ_K_LMB_ADMIT = 16, /* 17: removed */ HZ_K_STEM = 18, HZ_K_BNECK = 19, HZ_K_SEAM = 20, HZ_K_KCONV = 21,
+       HZ_K_QKVATT = 22 };
 int hz_launch_kernel(int kind, const void* params, hipStream_t st);
 int hz_experiments(void);  // 1: built with HZ_EXPERIMENTS (measured-negative kernel variants)
 size_t hz_kernel_param_size(int kind);  // 0: unknown kind

@@ -146,6 +146,7 @@ struct Plan {
             case HZ_K_LAYERNORM:
             case HZ_K_EMBED:
             case HZ_K_ATTENTION:
+            case HZ_K_QKVATT:
             case HZ_K_VIT_TOKENS:
             case HZ_K_SOFTMAX: u |= kUnitTransformer; break;
             case HZ_K_GEMM_FP8:
@@ -471,6 +472,7 @@ uint64_t hz_abi_version(void) {
                             sizeof(HzBneckParams),
                             sizeof(HzSeamParams),
                             sizeof(HzKconvParams),
+                            sizeof(HzQkvAttParams),
                             HZ_ABI_EPOCH};
   uint64_t x = 1469598103934665603ull;
   for (uint64_t v : parts) {

@@ -296,6 +296,7 @@ extern "C" int hz_launch_kernel(int kind, const void* prm, hipStream_t st) {
     case HZ_K_LMB_LAYER: return hz_lmb_layer_launch(static_cast<const HzLmbLayerParams*>(prm), st);
     case HZ_K_LMB_DEC: return hz_lmb_dec_launch(static_cast<const HzLmbDecParams*>(prm), st);
     case HZ_K_LMB_ADMIT: return hz_lmb_admit_launch(static_cast<const HzLmbAdmitParams*>(prm), st);
+    case HZ_K_QKVATT: return hz_qkvatt_launch(static_cast<const HzQkvAttParams*>(prm), st);
     case HZ_K_STEM: return hz_stem_launch(static_cast<const HzStemParams*>(prm), st);
     case HZ_K_BNECK: return hz_bneck_launch(static_cast<const HzBneckParams*>(prm), st);
     case HZ_K_SEAM: return hz_seam_launch(static_cast<const HzSeamParams*>(prm), st);
@@ -322,6 +323,7 @@ extern "C" size_t hz_kernel_param_size(int kind) {
     case HZ_K_LMB_LAYER: return sizeof(HzLmbLayerParams);
     case HZ_K_LMB_DEC: return sizeof(HzLmbDecParams);
     case HZ_K_LMB_ADMIT: return sizeof(HzLmbAdmitParams);
+    case HZ_K_QKVATT: return sizeof(HzQkvAttParams);
     case HZ_K_STEM: return sizeof(HzStemParams);
     case HZ_K_BNECK: return sizeof(HzBneckParams);
     case HZ_K_SEAM: return sizeof(HzSeamParams);

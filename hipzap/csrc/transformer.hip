@@ -352,6 +352,216 @@ __global__ __launch_bounds__(64 * NW) void attention_kernel(const HzAttentionPar
   }
 }
 
+// --------------------------------------------------------------------------- QKV + attention
+// A BERT-class self-attention block in ONE launch (HzQkvAttParams; VERDICT r4 "next round" 4). A
+// workgroup per (sequence b, head h) computes its head's Q, K and V for the sequence's L <= 128
+// tokens as one 128 x 192 LDS-tiled GEMM tile over K = D (the tile and pipeline of gemm.hip's
+// gemm_lds_kernel<128, 192, NS, .., 2, 4>: 2 x 4 waves, 64-deep stages, swizzled 128-B activation
+// lines, fragment-major weights through global_load_lds) -- the packed QKV weight rows of head h
+// are the three 64-row spans h*64, D + h*64 and 2D + h*64, picked per weight fragment, so the
+// standalone GEMM's packing serves unchanged. The epilogue adds the bias and writes Q, K, V as bf16
+// images into the LDS the stages used; the attention (attention_kernel's math: S^T = K Q^T,
+// softmax over the lane's keys + 2 shuffles, O^T = V^T P^T with transposed V reads) then runs from
+// there. The QKV activations never go to memory, and the attention's launch and its kernel
+// boundary are gone: 6 kernels per encoder layer instead of 7.
+__device__ __forceinline__ void qa_glds16(const void* g, char* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void qa_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+constexpr int QA_BM = 128, QA_NWG = 12, QA_XBYTES = QA_BM * 128, QA_SBYTES = QA_XBYTES + QA_NWG * 2 * 1024;
+constexpr int QA_IMG = QA_BM * ATT_KST;  // bf16 elements of one Q / K / V image (row stride ATT_KST)
+static_assert(3 * QA_IMG * 2 + QA_BM * 4 <= 2 * QA_SBYTES, "the attention images alias the GEMM stages");
+
+template <int NS>
+__global__ __launch_bounds__(512) void qkvatt_kernel(const HzQkvAttParams p) {
+  constexpr int G = 2 + 3;  // global_load_lds per wave per stage: 2 activation pieces, 3 weight fragments
+  __shared__ __attribute__((aligned(16))) char smem[NS * QA_SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wm = wave >> 2;
+  // consecutive workgroups (one XCD) are the heads of one sequence: its 128 x D activations hit L2
+  const int bh = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bh / p.heads, h = bh - b * p.heads;
+  const int L = p.L, nst = p.ksteps >> 1;
+  const long row0 = (long)b * L;
+  // activation piece q = wave + 8i: tile rows 8q .. 8q+7, lane -> row 8q + (lane >> 3), 16-B chunk
+  // (lane & 7) of the row XOR-swizzled as gemm_lds_kernel's image; rows past L repeat token L-1
+  const bf16_t* xsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave + 8 * i;
+    const int row = min(q * 8 + (lane >> 3), L - 1);
+    const int chunk = (lane & 7) ^ (((q & 1) << 2) + (lane >> 4));
+    xsrc[i] = p.x + (row0 + row) * p.ldx + chunk * 8;
+  }
+  // weight piece f = wave + 8i (f = ks * 12 + g): tile fragment g = packed fragment (g/4) * D/16 + 4h + g%4
+  const bf16_t* wsrc[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int f = wave + 8 * i, ks = f / QA_NWG, g = f - ks * QA_NWG;
+    const int frag = (g >> 2) * (p.D >> 4) + 4 * h + (g & 3);
+    wsrc[i] = p.w + (((long)frag * p.ksteps + ks) * 64 + lane) * 8;
+  }
+  auto stage = [&](int buf, int st) {
+    char* base = smem + buf * QA_SBYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) qa_glds16(xsrc[i] + st * 64, base + (wave + 8 * i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) qa_glds16(wsrc[i] + st * 2 * 512, base + QA_XBYTES + (wave + 8 * i) * 1024);
+  };
+  // the epilogue's operands go out first (independent of the GEMM): bias of this lane's features,
+  // the additive key mask (threads < 128)
+  f32x4 bias[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int fl = wn * 48 + 16 * i + 4 * (lane >> 4);
+    bias[i] = *reinterpret_cast<const f32x4*>(p.bias + (fl >> 6) * p.D + h * ATT_D + (fl & 63));
+  }
+  const int Lp = (L + 31) & ~31;
+  float mk = 0.f;
+  if (tid < Lp) mk = tid < L ? (p.mask ? p.mask[row0 + tid] : 0.f) : -INFINITY;
+  // ---- the 128 x 192 x D GEMM (gemm_lds_kernel's schedule) ----
+  const int lr = lane & 15, sw = (lane >> 1) & 7;
+  const int boff0 = (wm * 64 + lr) * 128 + ((lane >> 4) ^ sw) * 16;
+  const int boff1 = (wm * 64 + lr) * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
+  const int aoff = QA_XBYTES + (wn * 3) * 1024 + lane * 16;
+  f32x4 acc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < nst) stage(s0, s0);
+  int cur = 0;
+  for (int st = 0; st < nst; ++st) {
+    const int ahead = min(NS - 2, nst - 1 - st);
+    if (NS > 2 && ahead >= 1) qa_wait_vm<(NS > 2 ? G : 0)>();
+    else qa_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NS - 1 < nst) stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
+    const char* base = smem + cur * QA_SBYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[3], bb[4];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) a[i] = *reinterpret_cast<const bf16x8*>(base + aoff + (ks * QA_NWG + i) * 1024);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(base + (ks ? boff1 : boff0) + j * 16 * 128);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+    }
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  // ---- Q, K, V (+ bias, bf16) into LDS images over the stages: lane holds features
+  // wn*48 + 16i + 4(lane>>4) + e of token wm*64 + 16j + (lane&15) ----
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave is done reading the stages
+  bf16_t* img = reinterpret_cast<bf16_t*>(smem);  // [3][QA_BM][ATT_KST]: Q, K, V
+  float* Ms = reinterpret_cast<float*>(smem + 3 * QA_IMG * 2);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int fl = wn * 48 + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tok = wm * 64 + 16 * j + lr;
+      const f32x4 v = acc[i][j] + bias[i];
+      *reinterpret_cast<u32x2*>(img + (fl >> 6) * QA_IMG + tok * ATT_KST + (fl & 63)) =
+          u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+    }
+  }
+  if (tid < Lp) Ms[tid] = mk;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bf16_t* Qs = img;
+  const bf16_t* Ks = img + QA_IMG;
+  const bf16_t* Vs = img + 2 * QA_IMG;
+  // ---- attention for queries q0 .. q0+15 of this wave (attention_kernel's math) ----
+  const int q0 = wave * 16;
+  if (q0 >= L) return;  // whole waves only (the transposed reads need full EXEC); no barrier follows
+  const int lq = lane & 15, g = lane >> 4;
+  bf16x8 qb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qb[ks] = *reinterpret_cast<const bf16x8*>(Qs + (q0 + lq) * ATT_KST + ks * 32 + g * 8);
+  const int nkt = Lp / 16;
+  f32x4 s[QA_BM / 16];
+#pragma unroll
+  for (int kt = 0; kt < QA_BM / 16; ++kt) {
+    s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kt < nkt) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(Ks + (kt * 16 + lq) * ATT_KST + ks * 32 + g * 8);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qb[ks], s[kt], 0, 0, 0);
+      }
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < QA_BM / 16; ++kt) {
+    if (kt < nkt) {
+      const f32x4 madd = *reinterpret_cast<const f32x4*>(Ms + kt * 16 + 4 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[kt][i] = s[kt][i] * p.scale + madd[i];
+        mx = fmaxf(mx, s[kt][i]);
+      }
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < QA_BM / 16; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = __expf(s[kt][i] - mx);
+        s[kt][i] = e;
+        sum += e;
+      }
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tr_row = (lane & 15) >> 2, tr_col = (lane & 3) * 4;
+#pragma unroll
+  for (int c = 0; c < QA_BM / 32; ++c) {
+    if (c < Lp / 32) {
+      const f32x4 pa = s[2 * c], pb = s[2 * c + 1];
+      const u32x4 pw = u32x4{pack_bf16x2(pa[0] * inv, pa[1] * inv), pack_bf16x2(pa[2] * inv, pa[3] * inv),
+                             pack_bf16x2(pb[0] * inv, pb[1] * inv), pack_bf16x2(pb[2] * inv, pb[3] * inv)};
+      const bf16x8 pfrag = *reinterpret_cast<const bf16x8*>(&pw);
+      const int r_lo = 32 * c + 4 * g + tr_row, r_hi = r_lo + 16;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(Vs + r_lo * ATT_VST + dt * 16 + tr_col));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(Vs + r_hi * ATT_VST + dt * 16 + tr_col));
+        const short vv8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(vv8);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pfrag, o[dt], 0, 0, 0);
+      }
+    }
+  }
+  const int q = q0 + lq;
+  if (q < L) {
+    bf16_t* out = p.out + (row0 + q) * p.ldo + h * ATT_D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      *reinterpret_cast<u32x2*>(out + dt * 16) = u32x2{pack_bf16x2(o[dt][0], o[dt][1]), pack_bf16x2(o[dt][2], o[dt][3])};
+  }
+}
+
 // --------------------------------------------------------------------------- ViT tokens
 // out[b][0] = cls + pos[0]; out[b][1+i] = patches[b*np + i] + pos[1+i]   (bf16, D % 8 == 0)
 __global__ __launch_bounds__(256) void vit_tokens_kernel(const HzVitTokensParams p) {
@@ -437,6 +647,18 @@ extern "C" int hz_attention_launch(const HzAttentionParams* pp, hipStream_t st) 
   if (nw16 && p.L > 128) hipLaunchKernelGGL(attention_kernel<16>, dim3(p.B * p.heads, 1), dim3(1024), lds, st, p);
   else if (p.L > nw8_minl) hipLaunchKernelGGL(attention_kernel<8>, dim3(p.B * p.heads, (p.L + 127) / 128), dim3(512), lds, st, p);
   else hipLaunchKernelGGL(attention_kernel<4>, dim3(p.B * p.heads, (p.L + 63) / 64), dim3(256), lds, st, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_qkvatt_launch(const HzQkvAttParams* pp, hipStream_t st) {
+  const HzQkvAttParams& p = *pp;
+  if (!p.x || !p.w || !p.bias || !p.out || p.B < 1 || p.heads < 1) return -1;
+  if (p.L < 1 || p.L > QA_BM || p.D != p.heads * ATT_D || p.ksteps * 32 != p.D || p.ksteps % 2) return -1;
+  if (p.ldx % 8 || p.ldx < p.D || p.ldo % 4 || p.ldo < p.D) return -1;
+  // stages: HIPZAP_QKVATT_NS = 2 (default: 80 KiB of LDS, two workgroups per CU) or 3
+  static const int ns = getenv("HIPZAP_QKVATT_NS") && atoi(getenv("HIPZAP_QKVATT_NS")) == 3 ? 3 : 2;
+  if (ns == 3) hipLaunchKernelGGL(qkvatt_kernel<3>, dim3(p.B * p.heads), dim3(512), 0, st, p);
+  else hipLaunchKernelGGL(qkvatt_kernel<2>, dim3(p.B * p.heads), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 

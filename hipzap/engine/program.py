@@ -42,6 +42,39 @@ def conv_pairs(g: Graph) -> dict:
     return out
 
 
+def qkvatt_pairs(g: Graph, params: dict) -> dict:
+    """{index of a QKV gemm node: its attention node} for every (QKV projection, attention) pair
+    that binds as ONE qkvatt launch: bf16 in / out, head_dim 64, L <= 128, the projection's output
+    read by the attention alone. ``HIPZAP_QKVATT=0``: never."""
+    if os.environ.get("HIPZAP_QKVATT", "1") == "0":
+        return {}
+    out = {}
+    nodes = g.nodes
+    for i in range(len(nodes) - 1):
+        gm, att = nodes[i], nodes[i + 1]
+        if gm.kind != "gemm" or att.kind != "attention" or att.inputs[0] != gm.outputs[0] or gm.slot != att.slot:
+            continue
+        if len(att.outputs) != 1 or _ln_folded(gm) or len(gm.outputs) != 1:
+            continue
+        a = gm.attrs
+        if a.get("act", "none") != "none" or a.get("out_f32") or a.get("has_res", len(gm.inputs) > 1):
+            continue
+        L, heads, B = att.attrs["L"], att.attrs["heads"], att.attrs["B"]
+        pc = params.get(a.get("w"))
+        D = heads * 64
+        if pc is None or L > 128 or pc.cout != 3 * D or pc.ksteps * 32 != D or pc.bias is None:
+            continue
+        qkv = gm.outputs[0]
+        if qkv in g.outputs or g.shape(qkv) != (B * L, 3 * D) or (a.get("ldx") or g.shape(gm.inputs[0])[-1]) % 8:
+            continue
+        if any(qkv in n.inputs for j, n in enumerate(nodes) if j != i + 1):
+            continue
+        if g.tensors[att.outputs[0]].dtype != torch.bfloat16 or g.tensors[gm.inputs[0]].dtype != torch.bfloat16:
+            continue
+        out[i] = att
+    return out
+
+
 def _ln_folded(n) -> bool:
     a = n.attrs
     return n.kind == "gemm" and bool(a.get("ln_in") or a.get("res_ln") or a.get("stats_out") is not None)
@@ -87,8 +120,11 @@ class ExecContext:
         # K-split 3x3 convs preset by a plain (or paired) conv launch: a stage's first block
         self.kconv_preset = {id(g.nodes[f.preset]): f for f in self.fused.values()
                              if f.kind == "kconv" and f.seam is None}
+        # QKV projection + attention as one launch (HIPZAP_QKVATT, csrc/transformer.hip qkvatt_kernel)
+        self.qkvatt = qkvatt_pairs(g, params)
         offsets, arena_bytes = plan_memory(fusion.planning_graph(g, self.fused),
-                                           groups=[(f.start, f.end) for f in self.fused.values()])
+                                           groups=[(f.start, f.end) for f in self.fused.values()] +
+                                           [(i, i + 2) for i in self.qkvatt])
         self.arena_bytes = arena_bytes
         self.arena = torch.empty(max(arena_bytes, 256), dtype=torch.uint8, device=self.device)
         base = self.arena.data_ptr()
@@ -138,6 +174,10 @@ class ExecContext:
                 self.configs.append(fusion.add_fused(self.prog, g, params, f, addr, lib, self.fused))
                 i = f.end
                 continue
+            if i in self.qkvatt:
+                self._add_qkvatt(lib, n, g.nodes[i + 1])
+                i += 2
+                continue
             if i in self.pairs:
                 self._add_conv_pair(lib, n, g.nodes[i + 1], conv_plans[i], conv_plans[i + 1], tuned)
                 i += 2
@@ -149,6 +189,17 @@ class ExecContext:
                                            self.output.numel() * self.output.element_size(), 0), "d2h")
 
     # ------------------------------------------------------------------
+    def _add_qkvatt(self, lib, gm, att) -> None:
+        g, a = self.graph, att.attrs
+        pc = self.params[gm.attrs["w"]]
+        mask = att.inputs[1] if len(att.inputs) > 1 else None
+        D = a["heads"] * 64
+        prm = tx.QkvAttParams(self._addr(gm.inputs[0]), pc.wf.data_ptr(), pc.bias.data_ptr(), self._addr(mask),
+                              self._addr(att.outputs[0]), a["B"], a["L"], a["heads"], D, pc.ksteps,
+                              gm.attrs.get("ldx") or g.shape(gm.inputs[0])[-1], g.shape(att.outputs[0])[-1], 0.125)
+        self.configs.append((f"{gm.attrs.get('name', '')}+attention", "fused:qkvatt", -1, 0))
+        tx.prog_add(self.prog, tx.K_QKVATT, prm, gm.slot, lib=lib)
+
     def _conv_plans(self, g: Graph, params: dict, tuned: dict | None) -> list:
         """(cfg, kw, tuning key) of every conv / GEMM node, None for other nodes."""
         conv_plans = []

@@ -12,6 +12,7 @@ from .. import _native as N
 
 K_LAYERNORM, K_EMBED, K_ATTENTION, K_VIT_TOKENS = 2, 3, 4, 5
 K_SOFTMAX = 12
+K_QKVATT = 22
 
 
 class SoftmaxParams(C.Structure):
@@ -37,6 +38,12 @@ class AttentionParams(C.Structure):
                 ("heads", C.c_int), ("head_dim", C.c_int), ("ldqkv", C.c_int), ("k_off", C.c_int),
                 ("v_off", C.c_int), ("ldo", C.c_int), ("scale", C.c_float), ("out8", C.c_void_p),
                 ("os8", C.c_void_p)]
+
+
+class QkvAttParams(C.Structure):  # HzQkvAttParams: QKV projection + attention in one launch
+    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("mask", C.c_void_p), ("out", C.c_void_p),
+                ("B", C.c_int), ("L", C.c_int), ("heads", C.c_int), ("D", C.c_int), ("ksteps", C.c_int),
+                ("ldx", C.c_int), ("ldo", C.c_int), ("scale", C.c_float)]
 
 
 class VitTokensParams(C.Structure):

@@ -41,6 +41,7 @@ STUB(hz_stem_launch, HzStemParams, 18, N)
 STUB(hz_bneck_launch, HzBneckParams, 19, N)
 STUB(hz_seam_launch, HzSeamParams, 20, N)
 STUB(hz_kconv_launch, HzKconvParams, 21, N)
+STUB(hz_qkvatt_launch, HzQkvAttParams, 22, B)
 extern "C" int hz_step_bump_launch(int*, int n, hipStream_t) {
   g_calls.push_back(18);
   g_vals.push_back(n);

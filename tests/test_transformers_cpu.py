@@ -155,3 +155,24 @@ def test_bert_fp8_graph_oracle_vs_hf():
     with torch.no_grad():
         ref = m(input_ids=ids).logits
     assert ((out - ref).abs().max() / ref.abs().max()).item() < 0.25
+
+
+def test_qkvatt_pairs(monkeypatch):
+    """Every (QKV projection, attention) pair of BERT-base at L = 128 binds as one qkvatt launch
+    (engine/program.py qkvatt_pairs); not ViT (L = 197 > 128), not a projection that reads folded
+    LayerNorm statistics, not with HIPZAP_QKVATT=0."""
+    from hipzap.engine.program import qkvatt_pairs
+    a = registry.get("bert-base")
+    meta, cfg = a.meta_params()
+    g = a.build_graph(batch=16, **dict(cfg, ln_fold=False))
+    pairs = qkvatt_pairs(g, meta)
+    assert len(pairs) == 12
+    for i, att in pairs.items():
+        assert g.nodes[i].kind == "gemm" and g.nodes[i].attrs["w"].endswith("qkv") and att is g.nodes[i + 1]
+    # with the fold only the first layer's projection (it reads the embedding LayerNorm's output)
+    assert list(qkvatt_pairs(a.build_graph(batch=16, **dict(cfg, ln_fold=True)), meta)) == [1]
+    v = registry.get("vit-b16")
+    vmeta, vcfg = v.meta_params()
+    assert not qkvatt_pairs(v.build_graph(batch=4, **vcfg), vmeta)
+    monkeypatch.setenv("HIPZAP_QKVATT", "0")
+    assert not qkvatt_pairs(g, meta)

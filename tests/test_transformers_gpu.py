@@ -42,6 +42,57 @@ def test_attention(B, L, heads):
     assert _rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,L,heads,masked", [(2, 128, 12, True), (3, 7, 2, False), (1, 33, 4, True),
+                                              (2, 100, 12, True), (1, 128, 1, False)])
+def test_qkvatt_kernel_vs_fp32(B, L, heads, masked):
+    """QKV projection + attention in one launch (csrc/transformer.hip qkvatt_kernel) vs fp32: the
+    QKV GEMM in fp32 on the bf16 operands, rounded to bf16 as the kernel's LDS images hold it, then
+    the fp32 attention oracle."""
+    import ctypes
+    g = torch.Generator().manual_seed(B * 100 + L + heads)
+    D = heads * 64
+    x = torch.randn(B * L, D, generator=g).to(torch.bfloat16)
+    w = torch.randn(3 * D, D, generator=g) * D ** -0.5
+    b = 0.1 * torch.randn(3 * D, generator=g)
+    mask = torch.zeros(B, L)
+    if masked:
+        mask[-1, L // 2:] = -1e9
+    pc = C.pack_linear(w, b)
+    qkv = (x.float() @ pc.dense().float().t() + b).to(torch.bfloat16)
+    ref = T.attention_ref(qkv, B, L, heads, mask)
+    pcd, xd, md = pc.to(DEV), x.to(DEV), mask.to(DEV)
+    out = torch.full((B * L, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+    prm = T.QkvAttParams(xd.data_ptr(), pcd.wf.data_ptr(), pcd.bias.data_ptr(), md.data_ptr(), out.data_ptr(), B, L,
+                         heads, D, pcd.ksteps, D, D, 0.125)
+    NN.check(NN.lib().hz_launch_kernel(T.K_QKVATT, ctypes.byref(prm), NN.stream_ptr()), "qkvatt")
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    prm.L = 129  # > one 128-token tile
+    assert NN.lib().hz_launch_kernel(T.K_QKVATT, ctypes.byref(prm), None) != 0
+
+
+def test_bert_qkvatt_matches_unfused(monkeypatch):
+    """The BERT engine with the fused QKV + attention launch (the default) vs HIPZAP_QKVATT=0: 12
+    fewer launches, logits equal to bf16 rounding of the QKV activations."""
+    torch.manual_seed(0)
+    m = bert.make_model(num_labels=2)
+    sd = m.state_dict()
+    B, L = 4, 128
+    ids = torch.randint(0, 30000, (B, L))
+    am = torch.ones(B, L, dtype=torch.long)
+    am[1, 70:] = 0
+    inputs = bert.encode_inputs(ids, None, am)
+    outs, nops = [], []
+    for v in ("0", "1"):
+        monkeypatch.setenv("HIPZAP_QKVATT", v)
+        eng = Engine.from_state_dict("bert-base", sd, DEV, batch=B)
+        outs.append(eng.infer(inputs).float().cpu())
+        nops.append(eng.contexts[0].num_ops() if hasattr(eng, "contexts") else None)
+    assert _rel(outs[1], outs[0]) < 2e-2 and torch.equal(outs[1].argmax(1), outs[0].argmax(1))
+    if nops[0] is not None:
+        assert nops[0] - nops[1] == 12
+
+
 @pytest.mark.parametrize("M,N,K,act", [(2048, 2304, 768, "none"), (16, 768, 768, "tanh"), (197, 3072, 768, "gelu"),
                                         (5, 4, 768, "none")])
 def test_linear_gemm(M, N, K, act):
