@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 16)),
                     help="concurrent bs=1 request contexts per GPU (16: the 24-48 rate at 2/3 of the 24-stream latency, profiles/r4_final/streams)")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
-    ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 5)),
+    ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 9)),
                     help="fresh processes per cold-start path (0: skip)")
     ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds (secondary figure)")
     ap.add_argument("--serve", choices=["executor", "threads", "pipelined"], default="executor",
@@ -203,9 +203,17 @@ def prepare_lm_artifacts(ckpt_dir: str, vocab: int = 60000) -> tuple[str, str]:
 
 def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
     """Cold start over fresh processes (hipzap/coldstart.py), before this process uses a GPU."""
-    from hipzap.coldstart import measure_fresh, measure_node
+    from hipzap.coldstart import measure_fresh, measure_fresh_interleaved, measure_node
     ckpt, plan = prepare_artifacts(args.model, args.ckpt_dir)
-    res = {"plan": measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index)}
+    # the three torch-free routes share HIP init (120-230 ms, box- and trial-dependent): measured in
+    # alternation so their p50s compare like for like (VERDICT r4 weak #2)
+    il = measure_fresh_interleaved({"plan": ("plan", plan, args.model, None),
+                                    "pth_lite": ("pth-lite", ckpt, args.model, None),
+                                    "native": ("native", plan, args.model, None)},
+                                   args.cold_trials, device=device_index)
+    if "error" in il["plan"]:
+        raise RuntimeError(f"plan cold start failed: {il['plan']['error']}")
+    res = {"plan": il["plan"]}
     try:  # the node: N torch-free workers, RCCL rendezvous, C1 weight broadcast, first logits on every rank
         if world > torch.cuda.device_count():  # (a shared-GPU rehearsal: one RCCL rank per GPU only)
             raise RuntimeError(f"{world} workers need {world} visible GPUs, {torch.cuda.device_count()} visible")
@@ -219,15 +227,15 @@ def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
                                       extra_args=["--vocab", itos])
         except Exception as e:  # noqa: BLE001 - secondary figure
             print(f"LM cold start skipped: {e}", file=sys.stderr)
-    try:  # the .pth itself without torch: weights-only reader + plan template + device-side packing
-        res["pth_lite"] = measure_fresh("pth-lite", ckpt, args.model, args.cold_trials, device=device_index)
-    except Exception as e:  # noqa: BLE001 - template not built: the torch path stays the .pth figure
-        print(f"torch-free .pth cold start skipped: {e}", file=sys.stderr)
-    res["pth"] = measure_fresh("pth", ckpt, args.model, args.cold_trials, device=device_index)
-    try:  # the Python-free server binary (csrc/tools/serve_plan.cpp) on the same plan image
-        res["native"] = measure_fresh("native", plan, args.model, args.cold_trials, device=device_index)
-    except Exception as e:  # noqa: BLE001 - not built: the Python plan path stays the headline
-        print(f"native cold start skipped: {e}", file=sys.stderr)
+    # the .pth itself without torch (weights-only reader + plan template + device-side packing) and
+    # the Python-free server binary (csrc/tools/serve_plan.cpp) on the plan image: interleaved above
+    for name, what in (("pth_lite", "torch-free .pth"), ("native", "native")):
+        if "error" in il[name]:  # template / binary not built: the torch path stays the .pth figure
+            print(f"{what} cold start skipped: {il[name]['error']}", file=sys.stderr)
+        else:
+            res[name] = il[name]
+    # import torch + torch.load + pack: ~1.9 s a trial, so at most 5
+    res["pth"] = measure_fresh("pth", ckpt, args.model, min(5, args.cold_trials), device=device_index)
     if args.bert_cold:
         try:  # BERT-base seq-cls (BASELINE config 4) from its text plan image: torch-free too
             res["bert_plan"] = measure_fresh("plan", prepare_bert_plan(args.ckpt_dir), "bert-base",

@@ -259,15 +259,8 @@ def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:
     return base, 0
 
 
-def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5, device: int = 0,
-                  timeout: float = 300.0, env: dict | None = None, extra_args: list | None = None) -> dict:
-    """Spawn ``trials`` fresh processes of this module; p50/min/max of spawn -> first logits and
-    the child-reported phases of the median trial. Raises if any child fails."""
-    import statistics
-    import subprocess
+def _fresh_cmd(mode: str, path: str, model: str, device: int, extra_args: list | None) -> list:
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    walls, res = [], []
-    env, device = isolated_env(env, device)
     if mode == "native":
         import tempfile
         from hipzap.lite import read_meta
@@ -278,19 +271,26 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
         img = os.path.join(tempfile.mkdtemp(prefix="hzcold"), "image.raw")
         with open(img, "wb") as f:
             f.write(os.urandom(nbytes))
-        cmd = [exe, path, "--once", img, "--device", str(device)]
-    else:
-        cmd = [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device),
-               *(extra_args or [])]
-    for _ in range(trials):
-        t = time.time()
-        r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout, env=env)
-        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        if r.returncode != 0 or not lines:
-            raise RuntimeError(f"cold-start child ({mode}) failed rc={r.returncode}: {r.stderr[-3000:]}")
-        out = json.loads(lines[-1])
-        walls.append((out["t_first"] - t) * 1e3)
-        res.append(out)
+        return [exe, path, "--once", img, "--device", str(device)]
+    return [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device),
+            *(extra_args or [])]
+
+
+def _fresh_trial(cmd: list, mode: str, env, timeout: float) -> tuple[float, dict]:
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t = time.time()
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        raise RuntimeError(f"cold-start child ({mode}) failed rc={r.returncode}: {r.stderr[-3000:]}")
+    out = json.loads(lines[-1])
+    return (out["t_first"] - t) * 1e3, out
+
+
+def _fresh_summary(mode: str, walls: list, res: list) -> dict:
+    import statistics
+    trials = len(walls)
     order = sorted(range(trials), key=lambda i: walls[i])
     med = res[order[len(order) // 2]]
     return {"mode": mode, "trials": trials, "p50_ms": round(statistics.median(walls), 2),
@@ -298,6 +298,50 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
             "all_ms": [round(w, 1) for w in walls],
             "median_trial_phases_ms": {k: round(v, 2) for k, v in med["phases_ms"].items()},
             "torch_imported": med.get("torch_imported", mode not in ("plan", "native", "pth-lite", "lm"))}
+
+
+def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5, device: int = 0,
+                  timeout: float = 300.0, env: dict | None = None, extra_args: list | None = None) -> dict:
+    """Spawn ``trials`` fresh processes of this module; p50/min/max of spawn -> first logits and
+    the child-reported phases of the median trial. Raises if any child fails."""
+    env, device = isolated_env(env, device)
+    cmd = _fresh_cmd(mode, path, model, device, extra_args)
+    walls, res = [], []
+    for _ in range(trials):
+        w, out = _fresh_trial(cmd, mode, env, timeout)
+        walls.append(w)
+        res.append(out)
+    return _fresh_summary(mode, walls, res)
+
+
+def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, timeout: float = 300.0,
+                              env: dict | None = None) -> dict:
+    """Several cold-start routes measured in alternation -- trial k of every route before trial
+    k + 1 of any -- so a drift of the box (page cache, clocks, other tenants) lands on all of them
+    alike: ``runs`` = {name: (mode, path, model, extra_args)} -> {name: measure_fresh-style result}.
+    A route whose child fails drops out (its error under "error"); the others continue."""
+    env, device = isolated_env(env, device)
+    cmds, walls, res, out = {}, {}, {}, {}
+    for name, (mode, path, model, extra) in runs.items():
+        try:
+            cmds[name] = _fresh_cmd(mode, path, model, device, extra)
+            walls[name], res[name] = [], []
+        except Exception as e:  # noqa: BLE001 - e.g. the native binary not built
+            out[name] = {"mode": mode, "error": repr(e)[:500]}
+    for _ in range(trials):
+        for name in list(cmds):
+            try:
+                w, o = _fresh_trial(cmds[name], runs[name][0], env, timeout)
+            except Exception as e:  # noqa: BLE001
+                out[name] = {"mode": runs[name][0], "error": repr(e)[:3000]}
+                del cmds[name]
+                continue
+            walls[name].append(w)
+            res[name].append(o)
+    for name in cmds:
+        out[name] = _fresh_summary(runs[name][0], walls[name], res[name])
+        out[name]["interleaved_with"] = sorted(n for n in runs if n != name)
+    return out
 
 
 def main(argv=None) -> int:

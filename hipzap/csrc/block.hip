@@ -909,19 +909,30 @@ __device__ __forceinline__ int seam_lds(int row, int chunk) {  // bf16 offset of
 // (HW <= 64), and instead of storing y the workgroup averages its slice over the pixels -- the global
 // average pool of the classifier head, complete inside the workgroup (no atomics): fp32 [N][4CM] into
 // y's buffer, which the FC launch after it reads as-is (HzPoolFcParams.pooled).
-template <int CM, int CS, bool T2F32, bool TAIL = false>
+//
+// CN (cross-stage seam, HzSeamParams.cn): the next conv1 has CN != CM outputs -- conv3 of a stage's
+// last block and conv1 of the next stage's first block (layer3 -> layer4: CM 256, CN 512).
+// DS (HzSeamParams.ds): the residual is the block's stride-2 1x1 downsample of the stage input xd
+// (2CM channels, twice the spatial size), computed here as more phase-1 K: acc = W3 t2 + Wd xd(2y, 2x),
+// bias b3 + bd -- the downsample launch is gone. Its pixels are staged in LDS like t2 and its weights
+// stream through the same register ring (16 k-steps deep) behind W3's.
+template <int CM, int CS, bool T2F32, bool TAIL = false, int CN = CM, bool DS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void seam_kernel(const HzSeamParams p) {
   constexpr int CO = 4 * CM;
   constexpr int KS3 = CM / 32;     // conv3 k-steps
+  constexpr int KSD = DS ? CM / 16 : 0;  // downsample k-steps (K = 2CM)
+  constexpr int KT = KS3 + KSD;    // phase-1 k-steps
   constexpr int RG = CS / 16;      // conv3 row groups in the slice (4 or 8)
   constexpr int PT = TAIL ? 64 : 32;   // pixel tile
   constexpr int PGW = (PT / 16) * RG / 8;  // 16-pixel groups per wave (1 or 2; tail 2 or 4)
-  constexpr int ZB = CM / 32;      // conv1 output column blocks (8 or 16)
+  constexpr int ZB = CN / 32;      // conv1 output column blocks (8 or 16)
   constexpr int ZBW = ZB / 8;      // per wave
   constexpr int KS1 = CS / 16;     // conv1 k-steps over the slice (32x32x16)
   constexpr int KSW1 = CO / 32;    // conv1 weight k-steps (its packing)
-  constexpr int D = KS3;  // conv3 weight k-steps in flight
+  constexpr int D = DS ? 16 : KS3;  // phase-1 weight k-steps in flight
+  static_assert(!DS || (!TAIL && T2F32), "the downsample seam follows a K-split 3x3 conv");
   __shared__ __attribute__((aligned(16))) bf16_t Y[TAIL ? 8 : 32 * CS];
+  __shared__ __attribute__((aligned(16))) bf16_t XS[DS ? 2 * CM * 32 : 8];  // [2CM/8][32 px][8]
   // the tile's t2 (32 pixels x CM) is staged ONCE per workgroup in LDS as bf16 (fp32 t2: with the
   // ReLU applied), [CM/8 chunks][32 pixels][8]: every wave's B fragment is then one conflict-free
   // ds_read_b128 (16 consecutive pixels of one chunk) instead of every wave re-reading the tile from
@@ -958,10 +969,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       sb[i] = *reinterpret_cast<const u32x4*>(p.t2 + off);
     }
   }
+  // DS: the downsample's input pixels (2y, 2x) of the tile's outputs, [2CM/32 blocks][Hx][Wx][32] bf16
+  constexpr int NSX = DS ? 2 * CM * 32 / 8 / 512 : 0;
+  u32x4 sx[DS ? NSX : 1];
+#pragma unroll
+  for (int i = 0; i < NSX; ++i) {
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    const int hw = hw0 + min(px, cnt - 1), wo = p.xd_W >> 1;
+    const int oy = hw / wo, ox = hw - oy * wo;
+    const long off = (((long)n * (2 * CM / 32) + cb) * p.xd_H * p.xd_W + 2 * oy * p.xd_W + 2 * ox) * 32 + sub * 8;
+    sx[i] = *reinterpret_cast<const u32x4*>(p.xd + off);
+  }
   // ---- epilogue operands next (vmcnt retires in issue order). A padding pixel column (j >= cnt)
   // loads its tile's last pixel instead of branching (a branch around a load makes hipcc drain
   // vmcnt): its conv3 column, LDS row and conv1 row are never stored ----
-  const f32x4 bias = *reinterpret_cast<const f32x4*>(p.b3 + ch);
+  f32x4 bias = *reinterpret_cast<const f32x4*>(p.b3 + ch);
+  if constexpr (DS) bias += *reinterpret_cast<const f32x4*>(p.bd + ch);
   u32x2 rr[PGW];
   long yo[PGW];
   bool yv[PGW];
@@ -970,14 +993,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const int j = 16 * (pg0 + q) + l16, jc = min(j, cnt - 1);
     yv[q] = j < cnt;
     yo[q] = (((long)n * (CO / 32) + (ch >> 5)) * HW + hw0 + jc) * 32 + (ch & 31);
-    rr[q] = *reinterpret_cast<const u32x2*>(p.res + yo[q]);
+    if constexpr (DS) rr[q] = u32x2{0u, 0u};  // (the residual is the downsample, in acc)
+    else rr[q] = *reinterpret_cast<const u32x2*>(p.res + yo[q]);
   }
-  // ---- conv3 operand ring ----
+  // ---- phase-1 operand ring: W3's k-steps, then (DS) Wd's ----
   const bf16_t* __restrict__ W3 = p.w3 + ((long)(c0 / 16 + rg) * KS3) * 512 + lane * 8;
-  bf16x8 fa[KS3], fb[KS3][PGW];
-  auto load = [&](int s) { fa[s] = *reinterpret_cast<const bf16x8*>(W3 + (long)s * 512); };
+  const bf16_t* __restrict__ WD = DS ? p.wd + ((long)(c0 / 16 + rg) * KSD) * 512 + lane * 8 : W3;
+  bf16x8 fa[D];
+  auto load = [&](int s) {
+    fa[s % D] = *reinterpret_cast<const bf16x8*>(s < KS3 ? W3 + (long)s * 512 : WD + (long)(s - KS3) * 512);
+  };
 #pragma unroll
-  for (int s = 0; s < D && s < KS3; ++s) load(s);
+  for (int s = 0; s < D && s < KT; ++s) load(s);
   // ---- conv1 weights of this wave's column blocks (phase 2's B operands), behind the ring ----
   bf16x8 fw[ZBW][KS1];
 #pragma unroll
@@ -1004,18 +1031,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     *reinterpret_cast<u32x4*>(T2S + ((cb * 4 + sub) * PT + px) * 8) = v;
   }
+#pragma unroll
+  for (int i = 0; i < NSX; ++i) {
+    const int e = tid + 512 * i, sub = e & 3, px = (e >> 2) & 31, cb = e >> 7;
+    *reinterpret_cast<u32x4*>(XS + ((cb * 4 + sub) * 32 + px) * 8) = sx[i];
+  }
   lds_sync();
   f32x4 acc[PGW];
 #pragma unroll
   for (int q = 0; q < PGW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < KS3; ++s) {
+  for (int s = 0; s < KT; ++s) {
 #pragma unroll
     for (int q = 0; q < PGW; ++q) {
-      fb[s][q] = *reinterpret_cast<const bf16x8*>(T2S + ((s * 4 + g4) * PT + 16 * (pg0 + q) + l16) * 8);
-      acc[q] = mfma16(fa[s], fb[s][q], acc[q]);
+      const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
+          s < KS3 ? T2S + ((s * 4 + g4) * PT + 16 * (pg0 + q) + l16) * 8
+                  : XS + (((s - KS3) * 4 + g4) * 32 + 16 * (pg0 + q) + l16) * 8);
+      acc[q] = mfma16(fa[s % D], fb, acc[q]);
     }
-    if (s + D < KS3) load(s + D);
+    if (s + D < KT) load(s + D);
   }
   if constexpr (TAIL) {  // ---- pooled epilogue: mean over the image's pixels of ReLU(conv3 + bias + res)
     float sm[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1304,6 +1338,26 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
   q.tiles = (p.HW + 31) / 32;  // balanced tiles of <= 32 pixels
   const dim3 grid(q.tiles * p.N * (4 * p.CM / p.cs));
   if (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1)) return -1;
+  const int cn = p.cn ? p.cn : p.CM;
+  if (p.ds) {  // the downsample seam: CM 512 (layer4's first block), after a K-split conv
+    if (p.CM != 512 || cn != 512 || !p.t2_f32 || !p.xd || !p.wd || !p.bd || p.xd_H % 2 || p.xd_W % 2 ||
+        (p.xd_H / 2) * (p.xd_W / 2) != p.HW)
+      return -1;
+    if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    else hipLaunchKernelGGL((seam_kernel<512, 64, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    return (int)hipGetLastError();
+  }
+  if (cn != p.CM) {  // the cross-stage seam: layer3's last conv3 + layer4's first conv1
+    if (p.CM != 256 || cn != 512) return -1;
+    if (p.cs == 128) {
+      if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<256, 128, true, false, 512>), grid, dim3(512), 0, st, q);
+      else hipLaunchKernelGGL((seam_kernel<256, 128, false, false, 512>), grid, dim3(512), 0, st, q);
+    } else {
+      if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<256, 64, true, false, 512>), grid, dim3(512), 0, st, q);
+      else hipLaunchKernelGGL((seam_kernel<256, 64, false, false, 512>), grid, dim3(512), 0, st, q);
+    }
+    return (int)hipGetLastError();
+  }
 #define HZ_SEAM(CM, CS)                                                                                    \
   if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<CM, CS, true>), grid, dim3(512), 0, st, q);               \
   else hipLaunchKernelGGL((seam_kernel<CM, CS, false>), grid, dim3(512), 0, st, q);

@@ -459,6 +459,12 @@ typedef struct HzSeamParams {
   int z_C, z_HW;
   int tail, pad_;             // tail: the last block -- conv3 + global average pool, no conv1 half (w1, z
                               //   unused): fp32 [N][4CM] means into y's buffer (HW <= 64, CM 512)
+  int cn;                     // conv1 outputs (0: CM); 512 at CM 256 = the layer3 -> layer4 seam
+  int ds;                     // 1: the residual is the stride-2 1x1 downsample of xd (res unused):
+  const unsigned short* xd;   //   [N][2CM/32][xd_H][xd_W][32] bf16, the stage input
+  const unsigned short* wd;   //   packed like the per-conv kernels ([4CM/16][2CM/32][64][8])
+  const float* bd;            //   [4CM]
+  int xd_H, xd_W;
 } HzSeamParams;
 // K-split 3x3 conv (pad 1, stride 1 at <= 14 x 14 or stride 2 from <= 28 x 28) into an fp32
 // accumulator (block.hip kconv_kernel):

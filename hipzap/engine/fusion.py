@@ -24,6 +24,9 @@ bind as ONE fused kernel instead:
   (``kconv_kernel``; :func:`match_kconvs`).
 * ``tail``: the last block's conv3 + the global average pool (the seam kernel's tail mode): the
   classifier's ``pool_fc`` then reads fp32 channel means (``HzPoolFcParams.pooled``).
+* ``xseam``: the layer3 -> layer4 boundary -- layer3's last conv3 + layer4's first conv1 as one
+  seam (:func:`match_xseam`), layer4's stride-2 3x3 as its K-split consumer, and layer4's
+  downsample computed inside the next seam's conv3 (``HzSeamParams.ds``): the pair launch is gone.
 
 Both reuse the per-conv packed weights, so plan images / templates need no new parameters; the
 fused kernels' intermediate tensors simply stay unwritten in the arena. ``HIPZAP_FUSE`` selects
@@ -42,7 +45,7 @@ import numpy as np
 from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
-KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail")
+KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail", "xseam")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box; round 5
 # adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, and the pooling
 # tail: pool_fc 7.5 -> 4.6 us, sustained 13.2-13.9k -> 14.4k same box, profiles/r5_seam)
@@ -67,7 +70,9 @@ class SeamParams(C.Structure):  # HzSeamParams
     _fields_ = [("t2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("res", C.c_void_p),
                 ("y", C.c_void_p), ("w1", C.c_void_p), ("z", C.c_void_p), ("N", C.c_int), ("HW", C.c_int),
                 ("CM", C.c_int), ("cs", C.c_int), ("tiles", C.c_int), ("t2_f32", C.c_int), ("zinit", C.c_void_p),
-                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("tail", C.c_int), ("pad_", C.c_int)]
+                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("tail", C.c_int), ("pad_", C.c_int),
+                ("cn", C.c_int), ("ds", C.c_int), ("xd", C.c_void_p), ("wd", C.c_void_p), ("bd", C.c_void_p),
+                ("xd_H", C.c_int), ("xd_W", C.c_int)]
 
 
 class KconvParams(C.Structure):  # HzKconvParams
@@ -92,6 +97,10 @@ class Fused:
     next_seam: int | None = None
     reader: int | None = None
     preset: int | None = None  # kconv: node whose launch presets its accumulator (a seam's conv1, or conv1 of a pair)
+    # cross-stage seam (xseam: the last block's conv3 + the next stage's first conv1, the downsample
+    # node between them skipped) and the seam that computes that downsample as its residual
+    ds: object | None = None       # seam: the downsample node whose output is this seam's residual
+    ds_from: int | None = None     # seam: the cross-stage seam that skipped it
 
 
 def enabled_kinds(spec: str | None = None) -> set:
@@ -282,6 +291,45 @@ def match_tail(g, params, i: int) -> Fused | None:
     return Fused("tail", i, i + 1, [c3], reader=i + 1)
 
 
+def match_xseam(g, params, i: int, seams: dict) -> Fused | None:
+    """The layer3 -> layer4 boundary: nodes[i] = conv3 of layer3's last block (1x1 256 -> 1024 +
+    residual), nodes[i+1] = layer4's downsample (1x1/2 1024 -> 2048), nodes[i+2] = layer4's first
+    conv1 (1x1 1024 -> 512), nodes[i+3] = its stride-2 3x3, nodes[i+4] = its conv3 (+ the
+    downsample) starting a seam. The cross-stage seam binds conv3 + conv1 (conv1's K split over the
+    workgroups into an fp32 accumulator, as every seam); the downsample becomes more K of the
+    nodes[i+4] seam (its residual computed from the block input), so the pair launch is gone."""
+    nodes = g.nodes
+    if i < 1 or i + 5 > len(nodes) or (i + 4) not in seams:
+        return None
+    c2a, c3, ds, c1, c2b, c3b = nodes[i - 1:i + 5]
+    if not all(_conv(n) for n in (c2a, c3, ds, c1, c2b, c3b)) or len({n.slot for n in (c3, ds, c1, c2b, c3b)}) != 1:
+        return None
+    if any(n.attrs.get("out_f32") or n.attrs.get("rowmajor") for n in (c3, ds, c1, c2b, c3b)):
+        return None
+    if any(n.attrs.get("act", "relu") != "relu" for n in (c3, c1, c2b, c3b)) or ds.attrs.get("act", "relu") != "none":
+        return None
+    p2a, p3, pd, p1, p2b = (params.get(n.attrs.get("w")) for n in (c2a, c3, ds, c1, c2b))
+    if None in (p2a, p3, pd, p1, p2b):
+        return None
+    if not (_geom(p3, 256, 1024, 1, 1, 0) and _geom(pd, 1024, 2048, 1, 2, 0) and _geom(p1, 1024, 512, 1, 1, 0)
+            and _geom(p2b, 512, 512, 3, 2, 1) and p2a.r == 3 and p2a.cout == 256):
+        return None
+    y = c3.outputs[0]
+    if len(c3.inputs) != 2 or c3.inputs[0] != c2a.outputs[0] or ds.inputs != [y] or c1.inputs != [y]:
+        return None
+    if c2b.inputs != [c1.outputs[0]] or c3b.inputs != [c2b.outputs[0], ds.outputs[0]]:
+        return None
+    for t, reader in ((ds.outputs[0], i + 4), (c1.outputs[0], i + 3)):
+        if t in g.outputs or any(t in n.inputs for j, n in enumerate(nodes) if j != reader):
+            return None
+    if y in g.outputs or any(y in n.inputs for j, n in enumerate(nodes) if j not in (i + 1, i + 2)):
+        return None
+    nb, h, w, _ = g.shape(y)
+    if h % 2 or w % 2 or h * w > 196:  # the stride-2 K-split consumer stages (h+2)(w+2) <= 256 pixels
+        return None
+    return Fused("seam", i, i + 3, [c3, c1], init=i - 1, consumer=i + 3)
+
+
 def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
     """{first node index: Fused} for every fusible run of ``g`` (non-overlapping, in order)."""
     kinds = enabled_kinds() if kinds is None else kinds
@@ -311,6 +359,13 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
             f = match_seam(g, params, i)
             if f is not None and not covered & set(range(f.init, f.consumer + 1)):
                 seams[i] = f
+        if "xseam" in kinds and "kconv" in kinds:
+            for i in range(len(g.nodes)):
+                f = match_xseam(g, params, i, seams)
+                if f is not None and not covered & set(range(f.init, f.consumer + 1)) and \
+                        not any(j in seams for j in range(f.init, f.consumer + 1)):
+                    seams[i] = f
+                    seams[i + 4].ds, seams[i + 4].ds_from = g.nodes[i + 1], i
         out.update(seams)
         if "kconv" in kinds:
             out.update(match_kconvs(g, params, seams, covered))
@@ -353,7 +408,11 @@ def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
         n = g.nodes[k]
         pk = params.get(n.attrs.get("w"))
         nb, h, w, c = g.shape(n.inputs[0])
-        if pk is None or not _geom(pk, c, c, 3, 1, 1) or c not in (256, 512) or h * w > (196 if c == 256 else 64):
+        cross = f.end - f.start == 3  # a cross-stage seam's consumer: the next stage's stride-2 3x3
+        if cross:
+            if pk is None or not _geom(pk, c, c, 3, 2, 1) or c != 512 or (h + 2) * (w + 2) > 256:
+                continue
+        elif pk is None or not _geom(pk, c, c, 3, 1, 1) or c not in (256, 512) or h * w > (196 if c == 256 else 64):
             continue
         if k + 1 >= len(g.nodes):
             continue
@@ -370,7 +429,7 @@ def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
         if nxt is None and (p3 is None or not _geom(p3, c, 4 * c, 1, 1, 0)):
             continue
         out[k] = Fused("kconv", k, k + 1, [n], seam=s, next_seam=nxt, reader=None if nxt is not None else k + 1,
-                       preset=s + 1)
+                       preset=f.end - 1)  # (the seam's conv1 node)
     return out
 
 
@@ -401,6 +460,10 @@ def planning_graph(g, fused: dict):
             t1 = f.nodes[1].outputs[0]
             fp32(t1)
             preset_by(f.init, t1)
+            if f.ds is not None:  # the downsample's input stays live until this seam reads it
+                j = f.start
+                n = gp.nodes[j]
+                gp.nodes[j] = type(n)(n.kind, list(n.inputs) + [f.ds.inputs[0]], list(n.outputs), n.slot, n.attrs)
         else:
             a = f.nodes[0].outputs[0]
             fp32(a)
@@ -434,8 +497,15 @@ def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamPar
     p.t2, p.res, p.y, p.z = addr(c3.inputs[0]), addr(c3.inputs[1]), addr(c3.outputs[0]), addr(c1.outputs[0])
     p.w3, p.b3, p.w1 = p3.wf.data_ptr(), p3.bias.data_ptr(), p1.wf.data_ptr()
     nb, h, w, _ = g.shape(c3.outputs[0])
-    p.N, p.HW, p.CM = nb, h * w, p1.cout
-    p.cs = seam_cs(p.CM)
+    p.N, p.HW, p.CM = nb, h * w, p3.cin
+    p.cn = p1.cout if p1.cout != p3.cin else 0
+    # slice widths of the cross-stage seam and of the downsample seam: HIPZAP_XSEAM_CS="<xseam>,<ds seam>"
+    xcs = [int(v) for v in os.environ.get("HIPZAP_XSEAM_CS", "128,64").split(",")]
+    p.cs = xcs[0] if p.cn else xcs[-1] if f.ds is not None else seam_cs(p.CM)
+    if f.ds is not None:
+        pd = params[f.ds.attrs["w"]]
+        p.ds, p.xd, p.wd, p.bd = 1, addr(f.ds.inputs[0]), pd.wf.data_ptr(), pd.bias.data_ptr()
+        _, p.xd_H, p.xd_W, _ = g.shape(f.ds.inputs[0])
     p.t2_f32 = int(kc is not None and kc.kind == "kconv")
     kn = fused.get(f.consumer)  # this seam presets its consumer's accumulator
     if kn is not None and kn.kind == "kconv":

@@ -109,9 +109,19 @@ class ExecContext:
             f.init not in paired and f.consumer not in paired and conv_plans[f.init][0] < 16
             and conv_plans[f.consumer][0] < 16)}
         # a K-split 3x3 conv needs the seam that presets its output and, when it presets one, the next
-        self.fused = {k: f for k, f in self.fused.items() if f.kind != "kconv" or (
-            (f.seam is None or f.seam in self.fused) and (f.next_seam is None or f.next_seam in self.fused)
-            and (f.seam is not None or conv_plans[f.preset][0] < 16))}
+        # (and a cross-stage seam needs its K-split consumer: a fixed point over the two rules)
+        while True:
+            n0 = len(self.fused)
+            self.fused = {k: f for k, f in self.fused.items() if f.kind != "kconv" or (
+                (f.seam is None or f.seam in self.fused) and (f.next_seam is None or f.next_seam in self.fused)
+                and (f.seam is not None or conv_plans[f.preset][0] < 16))}
+            self.fused = {k: f for k, f in self.fused.items() if f.kind != "seam" or f.end - f.start == 2 or (
+                f.consumer in self.fused and self.fused[f.consumer].kind == "kconv")}
+            if len(self.fused) == n0:
+                break
+        for f in self.fused.values():  # a downsample seam needs the cross-stage seam that skipped the node
+            if f.kind == "seam" and f.ds is not None and f.ds_from not in self.fused:
+                f.ds = f.ds_from = None
         self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
         self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}
         self.f32_readers = {id(g.nodes[f.reader]) for f in self.fused.values() if f.kind == "kconv" and f.reader}

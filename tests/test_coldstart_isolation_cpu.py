@@ -13,3 +13,27 @@ def test_respects_launcher_visibility_and_opt_out():
         assert isolated_env(env, 1) == (env, 1)
     env = {"HIPZAP_COLD_ISOLATE": "0"}
     assert isolated_env(env, 4) == (env, 4)
+
+
+def test_interleaved_cold_start_alternates_and_drops_failed_routes(monkeypatch):
+    """bench.py measures the torch-free routes (plan, .pth-lite, native) in alternation: trial k of
+    every route before trial k + 1 of any, so box drift lands on all alike; a route whose child
+    fails drops out with its error and the others finish."""
+    from hipzap import coldstart as cs
+    calls = []
+    monkeypatch.setattr(cs, "_fresh_cmd", lambda mode, path, model, device, extra: [mode])
+
+    def trial(cmd, mode, env, timeout):
+        calls.append(mode)
+        if mode == "native" and calls.count("native") == 2:
+            raise RuntimeError("child failed")
+        return 100.0 + len(calls), {"phases_ms": {"hip_init_ms": 1.0}}
+
+    monkeypatch.setattr(cs, "_fresh_trial", trial)
+    out = cs.measure_fresh_interleaved({"plan": ("plan", "p", "resnet50", None),
+                                        "pth_lite": ("pth-lite", "c", "resnet50", None),
+                                        "native": ("native", "p", "resnet50", None)}, trials=3, env={})
+    assert calls == ["plan", "pth-lite", "native", "plan", "pth-lite", "native", "plan", "pth-lite"]
+    assert out["plan"]["trials"] == 3 and out["pth_lite"]["trials"] == 3
+    assert out["plan"]["all_ms"] == [101.0, 104.0, 107.0] and out["plan"]["p50_ms"] == 104.0
+    assert "error" in out["native"] and out["plan"]["interleaved_with"] == ["native", "pth_lite"]

@@ -237,3 +237,37 @@ def test_resnet50_tail(r50):
     from hipzap.models.resnet import build_graph
     g3 = build_graph("resnet50", 1, 1000, 288, True)  # 9 x 9 = 81 pixels
     assert not any(x.kind == "tail" for x in fusion.plan(g3, params, fusion.enabled_kinds("tail")).values())
+
+
+def test_resnet50_cross_stage_seam(r50):
+    """``xseam``: layer3's last conv3 + layer4's first conv1 become one seam (the downsample node
+    between them skipped), layer4's stride-2 3x3 its K-split consumer (preset by that seam's conv1
+    half), and the next seam computes the downsample as its residual; the downsample's input stays
+    live in the arena until that seam."""
+    from hipzap.engine.graph import plan_memory
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam,kconv,tail,xseam", batch=1, input_uint8=True)
+    xs = [f for f in fz.values() if f.kind == "seam" and f.end - f.start == 3]
+    assert len(xs) == 1
+    x = xs[0]
+    assert [n.attrs["name"] for n in x.nodes] == ["layer3.5.conv3", "layer4.0.conv1"]
+    assert g.nodes[x.start + 1].attrs["name"] == "layer4.0.downsample"
+    kc = fz[x.consumer]
+    assert kc.kind == "kconv" and kc.seam == x.start and kc.preset == x.start + 2 and kc.next_seam == x.consumer + 1
+    assert fz[x.init].kind == "kconv" and fz[x.init].next_seam == x.start
+    ds_seam = fz[x.consumer + 1]
+    assert ds_seam.ds is g.nodes[x.start + 1] and ds_seam.ds_from == x.start
+    assert sum(f.kind == "seam" for f in fz.values()) == 8
+    gp = fusion.planning_graph(g, fz)
+    y = x.nodes[0].outputs[0]
+    assert y in gp.nodes[ds_seam.start].inputs
+    offsets, _ = plan_memory(gp, groups=[(f.start, f.end) for f in fz.values()])
+    y0, y1 = offsets[y], offsets[y] + gp.tensors[y].nbytes
+    for j in range(x.start, ds_seam.end):  # nothing written from the xseam through the ds seam reuses y
+        for t in g.nodes[j].outputs:
+            if t != y and t in offsets:
+                assert offsets[t] + gp.tensors[t].nbytes <= y0 or y1 <= offsets[t], g.nodes[j].attrs.get("name")
+    # without kconv there is no consumer for the fp32 conv1 sum: no cross-stage seam
+    _, fz2 = _plan(a, params, kw, "convpool,bneck,bneck2,seam,xseam", batch=1, input_uint8=True)
+    assert not any(f.kind == "seam" and f.end - f.start == 3 for f in fz2.values())
+    assert all(f.ds is None for f in fz2.values())

@@ -97,6 +97,68 @@ def test_tail_kernel_vs_fp32(cs, n, h, t2f32):
     assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
 
 
+@pytest.mark.parametrize("cs,n", [(128, 1), (64, 2)])
+def test_cross_stage_seam_kernel_vs_fp32(cs, n):
+    """The layer3 -> layer4 seam (HzSeamParams.cn): conv3 256 -> 1024 (+ residual) and the next
+    stage's conv1 1024 -> 512 into its fp32 accumulator, t2 the fp32 sum of a K-split conv."""
+    g = torch.Generator().manual_seed(cs + n)
+    cm, cn, co, h = 256, 512, 1024, 14
+    p3 = CV.pack_conv(torch.randn(co, cm, 1, 1, generator=g) * (2.0 / cm) ** 0.5, 0.1 * torch.randn(co, generator=g))
+    p1 = CV.pack_conv(torch.randn(cn, co, 1, 1, generator=g) * (2.0 / co) ** 0.5, 0.1 * torch.randn(cn, generator=g))
+    t2 = torch.randn(n, h, h, cm, generator=g)
+    res = torch.randn(n, h, h, co, generator=g).to(torch.bfloat16)
+    y_ref = torch.relu(torch.relu(t2).to(torch.bfloat16).float() @ p3.dense().t() + p3.bias + res.float())
+    z_ref = p1.bias + y_ref.to(torch.bfloat16).float() @ p1.dense().t()
+    p3d, p1d = p3.to(DEV), p1.to(DEV)
+    t2d, resd = _blk(t2), _blk(res)
+    y = torch.zeros(n, co // 32, h, h, 32, dtype=torch.bfloat16, device=DEV)
+    z = p1d.bias.view(1, cn // 32, 1, 1, 32).expand(n, cn // 32, h, h, 32).contiguous()
+    prm = fusion.SeamParams()
+    prm.t2, prm.w3, prm.b3, prm.res, prm.y = t2d.data_ptr(), p3d.wf.data_ptr(), p3d.bias.data_ptr(), resd.data_ptr(), \
+        y.data_ptr()
+    prm.w1, prm.z, prm.N, prm.HW, prm.CM, prm.cs, prm.t2_f32, prm.cn = p1d.wf.data_ptr(), z.data_ptr(), n, h * h, cm, \
+        cs, 1, cn
+    fusion.launch("seam", prm)
+    torch.cuda.synchronize()
+    assert _rel(CV.from_blocked(y.cpu(), (n, h, h, co)).float(), y_ref) < 1e-2
+    assert _rel(CV.from_blocked(z.cpu(), (n, h, h, cn)), z_ref) < 2e-3
+    prm.cn = 384
+    assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
+
+
+@pytest.mark.parametrize("cs,n", [(64, 1), (128, 2)])
+def test_downsample_seam_kernel_vs_fp32(cs, n):
+    """HzSeamParams.ds: layer4's first conv3 with its stride-2 1x1 downsample as more K (the residual
+    computed from the stage input), then conv1 of the next block into its accumulator."""
+    g = torch.Generator().manual_seed(7 * cs + n)
+    cm, co, h = 512, 2048, 7
+    p3 = CV.pack_conv(torch.randn(co, cm, 1, 1, generator=g) * (2.0 / cm) ** 0.5, 0.1 * torch.randn(co, generator=g))
+    pd = CV.pack_conv(torch.randn(co, 2 * cm, 1, 1, generator=g) * (1.0 / cm) ** 0.5, 0.1 * torch.randn(co, generator=g),
+                      None, 2, 0)
+    p1 = CV.pack_conv(torch.randn(cm, co, 1, 1, generator=g) * (2.0 / co) ** 0.5, 0.1 * torch.randn(cm, generator=g))
+    t2 = torch.randn(n, h, h, cm, generator=g)
+    xd = torch.relu(torch.randn(n, 2 * h, 2 * h, 2 * cm, generator=g)).to(torch.bfloat16)
+    ds_ref = xd[:, ::2, ::2, :].float() @ pd.dense().t() + pd.bias
+    y_ref = torch.relu(torch.relu(t2).to(torch.bfloat16).float() @ p3.dense().t() + p3.bias + ds_ref)
+    z_ref = p1.bias + y_ref.to(torch.bfloat16).float() @ p1.dense().t()
+    p3d, pdd, p1d = p3.to(DEV), pd.to(DEV), p1.to(DEV)
+    t2d, xdd = _blk(t2), _blk(xd)
+    y = torch.zeros(n, co // 32, h, h, 32, dtype=torch.bfloat16, device=DEV)
+    z = p1d.bias.view(1, cm // 32, 1, 1, 32).expand(n, cm // 32, h, h, 32).contiguous()
+    prm = fusion.SeamParams()
+    prm.t2, prm.w3, prm.b3, prm.res, prm.y = t2d.data_ptr(), p3d.wf.data_ptr(), p3d.bias.data_ptr(), y.data_ptr(), \
+        y.data_ptr()
+    prm.w1, prm.z, prm.N, prm.HW, prm.CM, prm.cs, prm.t2_f32 = p1d.wf.data_ptr(), z.data_ptr(), n, h * h, cm, cs, 1
+    prm.ds, prm.xd, prm.wd, prm.bd, prm.xd_H, prm.xd_W = 1, xdd.data_ptr(), pdd.wf.data_ptr(), pdd.bias.data_ptr(), \
+        2 * h, 2 * h
+    fusion.launch("seam", prm)
+    torch.cuda.synchronize()
+    assert _rel(CV.from_blocked(y.cpu(), (n, h, h, co)).float(), y_ref) < 1e-2
+    assert _rel(CV.from_blocked(z.cpu(), (n, h, h, cm)), z_ref) < 2e-3
+    prm.xd_W = 13  # odd: not a stride-2 source of the 7 x 7 output
+    assert N.lib().hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(prm), None) != 0
+
+
 def test_seam_launch_refuses_bad_geometry():
     prm = fusion.SeamParams()
     buf = torch.zeros(1 << 20, device=DEV)
@@ -149,11 +211,13 @@ def _run(ctx, x):
 
 KCONV = SEAMS + ",kconv"
 TAIL = KCONV + ",tail"
+XSEAM = TAIL + ",xseam"
 
 
 @pytest.mark.parametrize("batch,noreuse,spec", [(1, True, SEAMS), (1, False, SEAMS), (2, True, SEAMS),
                                                 (1, True, KCONV), (1, False, KCONV), (2, False, KCONV),
-                                                (1, False, TAIL), (2, True, TAIL)])
+                                                (1, False, TAIL), (2, True, TAIL), (1, False, XSEAM),
+                                                (1, True, XSEAM), (2, False, XSEAM)])
 def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, monkeypatch):
     if noreuse:
         monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
@@ -163,7 +227,7 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=True))
     seam = ExecContext(g, params, torch.device(DEV), fuse=spec)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
-    assert sum(f.kind == "seam" for f in seam.fused.values()) == 7
+    assert sum(f.kind == "seam" for f in seam.fused.values()) == (8 if "xseam" in spec else 7)
     assert sum(f.kind == "kconv" for f in seam.fused.values()) == (9 if "kconv" in spec else 0)
     assert sum(f.kind == "tail" for f in seam.fused.values()) == (1 if "tail" in spec else 0)
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
@@ -184,13 +248,13 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     assert torch.equal(ls.argmax(1), lp.argmax(1))
 
 
-@pytest.mark.parametrize("spec", [SEAMS, KCONV, TAIL])
+@pytest.mark.parametrize("spec", [SEAMS, KCONV, TAIL, XSEAM])
 def test_resnet50_seam_dispatches_and_replay(r50, spec):
     a, params, _, kw = r50
     g = a.build_graph(batch=1, **dict(kw, input_uint8=True))
     base = ExecContext(g, params, torch.device(DEV), fuse="convpool,bneck,bneck2")
     ctx = ExecContext(g, params, torch.device(DEV), fuse=spec)
-    assert base.num_ops() - ctx.num_ops() == 7
+    assert base.num_ops() - ctx.num_ops() == (8 if "xseam" in spec else 7)
     assert ctx.num_ops() <= 31
     s = torch.cuda.Stream()
     ctx.capture(s)
