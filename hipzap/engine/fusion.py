@@ -48,8 +48,9 @@ HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
 KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail", "xseam")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box; round 5
 # adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, and the pooling
-# tail: pool_fc 7.5 -> 4.6 us, sustained 13.2-13.9k -> 14.4k same box, profiles/r5_seam)
-DEFAULT = "convpool,bneck,bneck2,seam,kconv,tail"
+# tail: pool_fc 7.5 -> 4.6 us, sustained 13.2-13.9k -> 14.4k same box; the layer3 -> layer4
+# cross-stage + downsample seams: 29 dispatches, 14.36-14.41k -> 14.51-14.57k, profiles/r5_seam)
+DEFAULT = "convpool,bneck,bneck2,seam,kconv,tail,xseam"
 
 
 class StemParams(C.Structure):  # HzStemParams (csrc/hipzap.h)
@@ -500,7 +501,7 @@ def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamPar
     p.N, p.HW, p.CM = nb, h * w, p3.cin
     p.cn = p1.cout if p1.cout != p3.cin else 0
     # slice widths of the cross-stage seam and of the downsample seam: HIPZAP_XSEAM_CS="<xseam>,<ds seam>"
-    xcs = [int(v) for v in os.environ.get("HIPZAP_XSEAM_CS", "128,64").split(",")]
+    xcs = [int(v) for v in os.environ.get("HIPZAP_XSEAM_CS", "128,128").split(",")]
     p.cs = xcs[0] if p.cn else xcs[-1] if f.ds is not None else seam_cs(p.CM)
     if f.ds is not None:
         pd = params[f.ds.attrs["w"]]
