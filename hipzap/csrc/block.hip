@@ -1140,6 +1140,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // 32 consecutive channels = a 128-B row of the channel-blocked output: the no-return float atomics
 // go out as full 128-B segments (MI355X_MICROARCH.md § Global float atomics). k-parts > 1 are summed
 // through LDS first.
+// The downsample job of a K-split launch (HzKconvParams.dso): workgroup = (image, 64 output
+// channels, 16 output pixels); wave w = 16 channels (w & 3) x one half of K (w >> 2), every one of
+// its weight and input fragments issued before the first MFMA (16x16x32, A = weights, B = the input
+// pixels (2y, 2x) straight from L2: consecutive lanes read 16 B of one pixel's 32-channel line); the
+// two K halves meet in LDS. One round of load latency per workgroup, so it hides under the K-split
+// workgroups' staging + MFMAs (r5_s16: a 32-channel x 64-pixel tile with a 16-deep ring over all
+// of K made the launch 13.5 us).
+__device__ __forceinline__ void kconv_ds_tile(const HzKconvParams& p, int bid, char* smem) {
+  constexpr int KH = 16;  // k-steps per wave (K <= 1024)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4, l16 = lane & 15;
+  const int Wo = p.ds_W >> 1, HWo = (p.ds_H >> 1) * Wo, npg = (HWo + 15) >> 4, n64 = p.ds_Cout >> 6;
+  const int pgi = bid % npg, rest = bid / npg, c64 = rest % n64, n = rest / n64;
+  const int px = pgi * 16 + l16, pix = min(px, HWo - 1);
+  const int oy = pix / Wo, ox = pix - oy * Wo;
+  const int cq = wave & 3, kh = wave >> 2;
+  const int co16 = c64 * 4 + cq;  // this wave's 16-channel weight row group
+  const int KS = p.ds_C >> 5, k0 = kh * (KS >> 1);
+  const bf16_t* __restrict__ wsrc = p.dsw + ((long)co16 * KS + k0) * 512 + lane * 8;
+  const long xstep = (long)p.ds_H * p.ds_W * 32;  // one 32-channel block
+  const bf16_t* __restrict__ xsrc =
+      p.dsx + (((long)n * KS + k0) * xstep) + ((long)2 * oy * p.ds_W + 2 * ox) * 32 + g4 * 8;
+  bf16x8 wa[KH], xb[KH];
+#pragma unroll
+  for (int s = 0; s < KH; ++s) {
+    wa[s] = *reinterpret_cast<const bf16x8*>(wsrc + (long)s * 512);
+    xb[s] = *reinterpret_cast<const bf16x8*>(xsrc + s * xstep);
+  }
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KH; ++s) acc = mfma16(wa[s], xb[s], acc);
+  f32x4* red = reinterpret_cast<f32x4*>(smem);  // [4 channel groups][64 lanes]
+  if (kh == 1) red[cq * 64 + lane] = acc;
+  __syncthreads();
+  if (kh == 0 && px < HWo) {  // lane: channels co16 * 16 + 4 g4 .. +3 of output pixel px
+    const int co = co16 * 16 + 4 * g4;
+    const f32x4 v = acc + red[cq * 64 + lane] + *reinterpret_cast<const f32x4*>(p.dsb + co);
+    *reinterpret_cast<u32x2*>(p.dso + (((long)n * (p.ds_Cout >> 5) + (co >> 5)) * HWo + px) * 32 + (co & 31)) =
+        u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  }
+}
+
 template <int CK, int PG, bool XF32, int ST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void kconv_kernel(const HzKconvParams p) {
   constexpr int QK = 8 / PG;         // k-parts per pixel group
@@ -1153,7 +1194,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int H = p.H, W = p.W, W2 = W + 2, NPOS = (H + 2) * W2;  // input (+ halo)
   const int Q = W / ST, HW = (H / ST) * Q, HWI = H * W;          // output pixels
   const int nct = p.Cout >> 5, nsl = p.C / CK;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids: one input slice, all channel tiles
+  // the downsample job's workgroups come first (dispatched first: they are the longer chains)
+  const int nds = p.dso ? p.N * (p.ds_Cout >> 6) * (((p.ds_H >> 1) * (p.ds_W >> 1) + 15) >> 4) : 0;
+  if ((int)blockIdx.x < nds) {
+    kconv_ds_tile(p, blockIdx.x, kc_smem);
+    return;
+  }
+  const int lid = xcd_remap(blockIdx.x - nds, gridDim.x - nds);  // consecutive ids: one input slice, all channel tiles
   const int ct = lid % nct, rest = lid / nct, slice = rest % nsl, n = rest / nsl;
   const int c0 = slice * CK;
   const int pg = wave % PG, q = wave / PG;
@@ -1264,7 +1311,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   if (p.zinit) {  // preset the next accumulator (HzConvParams.zinit)
     const long n4 = (long)p.N * p.z_C * p.z_HW / 4;
     const int cbz = p.z_C >> 5;
-    for (long i = (long)blockIdx.x * 512 + tid; i < n4; i += (long)gridDim.x * 512) {
+    for (long i = (long)(blockIdx.x - nds) * 512 + tid; i < n4; i += (long)(gridDim.x - nds) * 512) {
       const long e = i * 4;
       const int c = (int)((e / (32L * p.z_HW)) % cbz) * 32 + (int)(e & 31);
       *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
@@ -1339,12 +1386,14 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
   const dim3 grid(q.tiles * p.N * (4 * p.CM / p.cs));
   if (p.zinit && (!p.zbias || p.z_C % 32 || p.z_HW < 1)) return -1;
   const int cn = p.cn ? p.cn : p.CM;
-  if (p.ds) {  // the downsample seam: CM 512 (layer4's first block), after a K-split conv
-    if (p.CM != 512 || cn != 512 || !p.t2_f32 || !p.xd || !p.wd || !p.bd || p.xd_H % 2 || p.xd_W % 2 ||
+  if (p.ds) {  // the downsample seam: a stage's first block (layer3: CM 256, layer4: 512), after a K-split conv
+    if (cn != p.CM || !p.t2_f32 || !p.xd || !p.wd || !p.bd || p.xd_H % 2 || p.xd_W % 2 ||
         (p.xd_H / 2) * (p.xd_W / 2) != p.HW)
       return -1;
-    if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128, true, false, 512, true>), grid, dim3(512), 0, st, q);
-    else hipLaunchKernelGGL((seam_kernel<512, 64, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    if (p.CM == 512 && p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    else if (p.CM == 512) hipLaunchKernelGGL((seam_kernel<512, 64, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    else if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<256, 128, true, false, 256, true>), grid, dim3(512), 0, st, q);
+    else hipLaunchKernelGGL((seam_kernel<256, 64, true, false, 256, true>), grid, dim3(512), 0, st, q);
     return (int)hipGetLastError();
   }
   if (cn != p.CM) {  // the cross-stage seam: layer3's last conv3 + layer4's first conv1
@@ -1378,12 +1427,19 @@ extern "C" int hz_kconv_launch(const HzKconvParams* pp, hipStream_t st) {
   if (st_ == 2 && (p.H % 2 || p.W % 2)) return -1;
   const int HW = (p.H / st_) * (p.W / st_);
   const int pg = (HW + 31) / 32;
-  const dim3 grid(p.N * (p.Cout / 32) * (p.C / p.ck));
+  int nds = 0;
+  if (p.dso) {  // the downsample job: K = 1024 (two waves x 16 k-steps), 64-channel groups
+    if (!p.dsx || !p.dsw || !p.dsb || p.ds_C != 1024 || p.ds_Cout % 64 || p.ds_H % 2 || p.ds_W % 2 ||
+        (p.ds_H / 2) * (p.ds_W / 2) > 64)
+      return -1;
+    nds = p.N * (p.ds_Cout / 64) * (((p.ds_H / 2) * (p.ds_W / 2) + 15) / 16);
+  }
+  const dim3 grid(p.N * (p.Cout / 32) * (p.C / p.ck) + nds);
   const size_t stage = (size_t)(p.ck / 8) * (p.H + 2) * (p.W + 2) * 16;
 #define HZ_KC(CK, PG, XF)                                                                            \
   do {                                                                                               \
     const size_t red = (8 / PG) > 1 ? (size_t)PG * (8 / PG) * 16 * 64 * 4 : 0;                       \
-    const size_t lds = stage > red ? stage : red;                                                    \
+    const size_t lds0 = stage > red ? stage : red, lds = p.dso && lds0 < 4096 ? 4096 : lds0;        \
     if (lds > 160 * 1024) return -1;                                                                 \
     if (st_ == 1) hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 1>), grid, dim3(512), lds, st, p);    \
     else hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 2>), grid, dim3(512), lds, st, p);             \

@@ -483,6 +483,13 @@ typedef struct HzKconvParams {
   int z_C, z_HW;
   int N, H, W, C, Cout, x_f32;  // H, W: the INPUT size (the output is H/stride x W/stride)
   int ck, stride;             // input channels per workgroup: 32, 64 or 128; stride 1 or 2
+  // optional second job of the launch (dso != NULL): the block's stride-2 1x1 downsample, in its
+  // own workgroups (32 output channels x <= 64 output pixels, full K): dso = dsw dsx(2y, 2x) + dsb
+  const unsigned short* dsx;  // [N][ds_C/32][ds_H][ds_W][32] bf16
+  const unsigned short* dsw;  // packed [ds_Cout/16][ds_C/32][64][8]
+  const float* dsb;           // [ds_Cout]
+  unsigned short* dso;        // [N][ds_Cout/32][ds_H/2][ds_W/2][32] bf16
+  int ds_C, ds_Cout, ds_H, ds_W;
 } HzKconvParams;
 int hz_stem_launch(const HzStemParams* p, hipStream_t st);
 int hz_bneck_launch(const HzBneckParams* p, hipStream_t st);

@@ -24,6 +24,8 @@ bind as ONE fused kernel instead:
   (``kconv_kernel``; :func:`match_kconvs`).
 * ``tail``: the last block's conv3 + the global average pool (the seam kernel's tail mode): the
   classifier's ``pool_fc`` then reads fp32 channel means (``HzPoolFcParams.pooled``).
+* ``dsseam``: layer3's downsample as more K of layer3's first seam (its node skipped), so the
+  stage's downsample + conv1 pair launch becomes conv1 alone (:func:`match_dsseam`).
 * ``xseam``: the layer3 -> layer4 boundary -- layer3's last conv3 + layer4's first conv1 as one
   seam (:func:`match_xseam`), layer4's stride-2 3x3 as its K-split consumer, and layer4's
   downsample computed inside the next seam's conv3 (``HzSeamParams.ds``): the pair launch is gone.
@@ -45,7 +47,7 @@ import numpy as np
 from .. import _native as N
 
 HZ_K_STEM, HZ_K_BNECK, HZ_K_SEAM, HZ_K_KCONV = 18, 19, 20, 21
-KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail", "xseam")
+KINDS = ("stem", "convpool", "bneck", "bneck2", "seam", "kconv", "tail", "xseam", "dsseam")
 # measured default (profiles/r4_fuse/README.md: served 11.3k -> 13.4k inf/s on one box; round 5
 # adds the layer3/layer4 seams + K-split 3x3 convs: 13.5-13.6k -> 14.2k same box, and the pooling
 # tail: pool_fc 7.5 -> 4.6 us, sustained 13.2-13.9k -> 14.4k same box; the layer3 -> layer4
@@ -80,7 +82,8 @@ class KconvParams(C.Structure):  # HzKconvParams
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
                 ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
                 ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("stride", C.c_int)]
+                ("stride", C.c_int), ("dsx", C.c_void_p), ("dsw", C.c_void_p), ("dsb", C.c_void_p), ("dso", C.c_void_p),
+                ("ds_C", C.c_int), ("ds_Cout", C.c_int), ("ds_H", C.c_int), ("ds_W", C.c_int)]
 
 
 @dataclass
@@ -331,6 +334,31 @@ def match_xseam(g, params, i: int, seams: dict) -> Fused | None:
     return Fused("seam", i, i + 3, [c3, c1], init=i - 1, consumer=i + 3)
 
 
+def match_dsseam(g, params, f: Fused, covered: set) -> Fused | None:
+    """A stage's first block whose conv3 opens a seam (layer3: 1x1 256 -> 1024 + the downsample
+    1x1/2 512 -> 1024 of the stage input): nodes [ds, conv1, 3x3/2, conv3 ...]. The downsample then
+    runs inside that seam (HzSeamParams.ds, more phase-1 K from the stage input) and its own node is
+    skipped (a ``skip`` run: no launch), so layer3's downsample + conv1 pair becomes conv1 alone.
+    Returns the skip run."""
+    nodes = g.nodes
+    c3 = f.nodes[0]
+    if f.end - f.start != 2 or len(c3.inputs) != 2 or f.init is None or f.init < 2:
+        return None
+    d, c1, c2 = nodes[f.init - 2], nodes[f.init - 1], nodes[f.init]
+    if not all(_conv(n) for n in (d, c1, c2)) or f.init - 2 in covered or c3.inputs[1] != d.outputs[0]:
+        return None
+    if d.attrs.get("act", "relu") != "none" or d.attrs.get("out_f32") or d.slot != c3.slot:
+        return None
+    pd, p3 = params.get(d.attrs.get("w")), params.get(c3.attrs.get("w"))
+    if pd is None or p3 is None or p3.cin != 256 or not _geom(pd, 2 * p3.cin, p3.cout, 1, 2, 0):
+        return None
+    if d.outputs[0] in g.outputs or any(d.outputs[0] in n.inputs for n in nodes if n is not c3):
+        return None
+    if c1.inputs != d.inputs or c2.inputs != [c1.outputs[0]]:
+        return None
+    return Fused("skip", f.init - 2, f.init - 1, [d], seam=f.start)
+
+
 def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
     """{first node index: Fused} for every fusible run of ``g`` (non-overlapping, in order)."""
     kinds = enabled_kinds() if kinds is None else kinds
@@ -368,8 +396,24 @@ def plan(g, params, kinds: set | None = None) -> dict[int, Fused]:
                     seams[i] = f
                     seams[i + 4].ds, seams[i + 4].ds_from = g.nodes[i + 1], i
         out.update(seams)
+        if "dsseam" in kinds and "kconv" in kinds:  # layer3's downsample inside its first seam
+            for s0, f in seams.items():
+                sk = match_dsseam(g, params, f, covered | set(out) | {j for x in seams.values()
+                                                                     for j in range(x.start, x.end)})
+                if sk is not None:
+                    out[sk.start] = sk
+                    f.ds, f.ds_from = g.nodes[sk.start], sk.start
         if "kconv" in kinds:
             out.update(match_kconvs(g, params, seams, covered))
+            # where layer4's downsample runs (HIPZAP_XSEAM_DS): "seam" (default) = more K of the next
+            # seam; "kconv" = extra workgroups of the stride-2 K-split launch (measured slower served:
+            # the full-chip launch costs CU-time, profiles/r5_seam)
+            if os.environ.get("HIPZAP_XSEAM_DS", "seam") == "kconv":
+                for f in seams.values():
+                    kc = out.get(f.start - 1)
+                    if f.ds is not None and seams.get(f.ds_from) is not None and kc is not None and \
+                            kc.kind == "kconv" and kc.start == f.init:
+                        kc.ds, kc.ds_from, f.ds, f.ds_from = f.ds, f.ds_from, None, None
     if "tail" in kinds:
         covered = {j for f in out.values() for j in range(f.start, f.end)}
         for i in range(len(g.nodes)):
@@ -469,6 +513,10 @@ def planning_graph(g, fused: dict):
             a = f.nodes[0].outputs[0]
             fp32(a)
             preset_by(f.preset, a)  # a seam's conv1 half, or the conv before a stage's stride-2 3x3
+            if f.ds is not None:  # the launch also computes the downsample: its input and output
+                n = gp.nodes[f.start]
+                gp.nodes[f.start] = type(n)(n.kind, list(n.inputs) + [f.ds.inputs[0]],
+                                            list(n.outputs) + [f.ds.outputs[0]], n.slot, n.attrs)
     return gp
 
 
@@ -535,6 +583,11 @@ def kconv_params(g, params, f: Fused, addr, fused: dict) -> KconvParams:
     p.x, p.w, p.out = addr(n.inputs[0]), pk.wf.data_ptr(), addr(n.outputs[0])
     p.N, p.H, p.W, p.C, p.Cout, p.ck, p.stride = nb, h, w, c, pk.cout, kconv_ck(c, pk.stride), pk.stride
     p.x_f32 = int(f.seam is not None)  # a seam's fp32 conv1 sum; a stage's first 3x3 reads bf16
+    if f.ds is not None:  # layer4's downsample in extra workgroups of this launch
+        pd = params[f.ds.attrs["w"]]
+        p.dsx, p.dsw, p.dsb, p.dso = addr(f.ds.inputs[0]), pd.wf.data_ptr(), pd.bias.data_ptr(), addr(f.ds.outputs[0])
+        _, p.ds_H, p.ds_W, p.ds_C = g.shape(f.ds.inputs[0])
+        p.ds_Cout = pd.cout
     if f.next_seam is not None:  # preset the next seam's conv1 accumulator
         nf = fused[f.next_seam]
         t1 = nf.nodes[1].outputs[0]
@@ -603,6 +656,8 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
 
 def add_fused(prog, g, params, f: Fused, addr, lib, fused: dict | None = None) -> tuple:
     """Bind ``f`` as one program op; returns the (name, key, cfg, kw) record ExecContext.configs keeps."""
+    if f.kind == "skip":  # computed inside another launch (a downsample seam): no op of its own
+        return (str(f.nodes[0].attrs.get("name", "")), "fused:skip", -1, 0)
     if f.kind in ("stem", "convpool"):
         prm, kind = stem_params(g, params, f, addr), HZ_K_STEM
     elif f.kind in ("seam", "tail"):

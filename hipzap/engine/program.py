@@ -117,10 +117,15 @@ class ExecContext:
                 and (f.seam is not None or conv_plans[f.preset][0] < 16))}
             self.fused = {k: f for k, f in self.fused.items() if f.kind != "seam" or f.end - f.start == 2 or (
                 f.consumer in self.fused and self.fused[f.consumer].kind == "kconv")}
+            # a skipped downsample node needs the seam that computes it (and a K-split conv before that
+            # seam: the downsample seam reads an fp32 t2)
+            self.fused = {k: f for k, f in self.fused.items() if f.kind != "skip" or (
+                f.seam in self.fused and self.fused.get(self.fused[f.seam].init) is not None
+                and self.fused[self.fused[f.seam].init].kind == "kconv")}
             if len(self.fused) == n0:
                 break
-        for f in self.fused.values():  # a downsample seam needs the cross-stage seam that skipped the node
-            if f.kind == "seam" and f.ds is not None and f.ds_from not in self.fused:
+        for f in self.fused.values():  # a launch computing the downsample needs the seam that skipped its node
+            if f.ds is not None and f.ds_from not in self.fused:
                 f.ds = f.ds_from = None
         self.seam_init = {id(g.nodes[f.init]): f for f in self.fused.values() if f.kind == "seam"}
         self.seam_consumer = {id(g.nodes[f.consumer]) for f in self.fused.values() if f.kind == "seam"}

@@ -21,14 +21,7 @@ from hipzap import _native as N  # noqa: E402
 from hipzap.ops import conv as CV  # noqa: E402
 
 REPS = 64
-HZ_K_KCONV = 21
-
-
-class KconvParams(C.Structure):
-    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
-                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
-                ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("stride", C.c_int)]
+from hipzap.engine.fusion import HZ_K_KCONV, KconvParams  # noqa: E402  (the struct the launcher reads)
 
 
 def prog_of(add, reps=REPS):

@@ -239,13 +239,15 @@ def test_resnet50_tail(r50):
     assert not any(x.kind == "tail" for x in fusion.plan(g3, params, fusion.enabled_kinds("tail")).values())
 
 
-def test_resnet50_cross_stage_seam(r50):
+@pytest.mark.parametrize("ds_at", ["kconv", "seam"])  # HIPZAP_XSEAM_DS
+def test_resnet50_cross_stage_seam(r50, ds_at, monkeypatch):
     """``xseam``: layer3's last conv3 + layer4's first conv1 become one seam (the downsample node
     between them skipped), layer4's stride-2 3x3 its K-split consumer (preset by that seam's conv1
     half), and the next seam computes the downsample as its residual; the downsample's input stays
     live in the arena until that seam."""
     from hipzap.engine.graph import plan_memory
     a, params, kw = r50
+    monkeypatch.setenv("HIPZAP_XSEAM_DS", ds_at)
     g, fz = _plan(a, params, kw, "convpool,bneck,bneck2,seam,kconv,tail,xseam", batch=1, input_uint8=True)
     xs = [f for f in fz.values() if f.kind == "seam" and f.end - f.start == 3]
     assert len(xs) == 1
@@ -255,15 +257,20 @@ def test_resnet50_cross_stage_seam(r50):
     kc = fz[x.consumer]
     assert kc.kind == "kconv" and kc.seam == x.start and kc.preset == x.start + 2 and kc.next_seam == x.consumer + 1
     assert fz[x.init].kind == "kconv" and fz[x.init].next_seam == x.start
+    ds_node = g.nodes[x.start + 1]
     ds_seam = fz[x.consumer + 1]
-    assert ds_seam.ds is g.nodes[x.start + 1] and ds_seam.ds_from == x.start
+    owner = kc if ds_at == "kconv" else ds_seam  # the launch that computes layer4's downsample
+    other = ds_seam if ds_at == "kconv" else kc
+    assert owner.ds is ds_node and owner.ds_from == x.start and other.ds is None
     assert sum(f.kind == "seam" for f in fz.values()) == 8
     gp = fusion.planning_graph(g, fz)
     y = x.nodes[0].outputs[0]
-    assert y in gp.nodes[ds_seam.start].inputs
+    assert y in gp.nodes[owner.start].inputs
+    if ds_at == "kconv":
+        assert ds_node.outputs[0] in gp.nodes[owner.start].outputs
     offsets, _ = plan_memory(gp, groups=[(f.start, f.end) for f in fz.values()])
     y0, y1 = offsets[y], offsets[y] + gp.tensors[y].nbytes
-    for j in range(x.start, ds_seam.end):  # nothing written from the xseam through the ds seam reuses y
+    for j in range(x.start, owner.end):  # nothing written from the xseam through the downsample's launch reuses y
         for t in g.nodes[j].outputs:
             if t != y and t in offsets:
                 assert offsets[t] + gp.tensors[t].nbytes <= y0 or y1 <= offsets[t], g.nodes[j].attrs.get("name")
@@ -271,3 +278,19 @@ def test_resnet50_cross_stage_seam(r50):
     _, fz2 = _plan(a, params, kw, "convpool,bneck,bneck2,seam,xseam", batch=1, input_uint8=True)
     assert not any(f.kind == "seam" and f.end - f.start == 3 for f in fz2.values())
     assert all(f.ds is None for f in fz2.values())
+
+
+def test_resnet50_layer3_downsample_seam(r50):
+    """``dsseam``: layer3's downsample node is skipped (no launch of its own) and computed inside
+    layer3's first seam, whose t2 is the stride-2 K-split conv's fp32 sum; conv1 then binds alone.
+    Its input (layer2's output) stays live until that seam."""
+    a, params, kw = r50
+    g, fz = _plan(a, params, kw, fusion.DEFAULT + ",dsseam", batch=1, input_uint8=True)
+    sk = [f for f in fz.values() if f.kind == "skip"]
+    assert len(sk) == 1 and sk[0].nodes[0].attrs["name"] == "layer3.0.downsample"
+    s0 = fz[sk[0].seam]
+    assert s0.ds is sk[0].nodes[0] and s0.ds_from == sk[0].start
+    assert [n.attrs["name"] for n in s0.nodes] == ["layer3.0.conv3", "layer3.1.conv1"]
+    assert fz[s0.init].kind == "kconv" and fz[s0.init].preset == s0.init - 1  # conv1 alone presets it
+    gp = fusion.planning_graph(g, fz)
+    assert sk[0].nodes[0].inputs[0] in gp.nodes[s0.start].inputs

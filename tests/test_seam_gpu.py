@@ -217,8 +217,12 @@ XSEAM = TAIL + ",xseam"
 @pytest.mark.parametrize("batch,noreuse,spec", [(1, True, SEAMS), (1, False, SEAMS), (2, True, SEAMS),
                                                 (1, True, KCONV), (1, False, KCONV), (2, False, KCONV),
                                                 (1, False, TAIL), (2, True, TAIL), (1, False, XSEAM),
-                                                (1, True, XSEAM), (2, False, XSEAM)])
+                                                (1, True, XSEAM), (2, False, XSEAM), (1, False, XSEAM + ":kconv"),
+                                                (2, True, XSEAM + ":kconv"), (1, False, XSEAM + ",dsseam"),
+                                                (1, True, XSEAM + ",dsseam"), (2, False, XSEAM + ",dsseam")])
 def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, monkeypatch):
+    spec, _, ds_at = spec.partition(":")  # where layer4's downsample runs (HIPZAP_XSEAM_DS)
+    monkeypatch.setenv("HIPZAP_XSEAM_DS", ds_at or "seam")
     if noreuse:
         monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
     else:
@@ -228,6 +232,7 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     seam = ExecContext(g, params, torch.device(DEV), fuse=spec)
     plain = ExecContext(g, params, torch.device(DEV), fuse="none")
     assert sum(f.kind == "seam" for f in seam.fused.values()) == (8 if "xseam" in spec else 7)
+    assert sum(f.kind == "skip" for f in seam.fused.values()) == (1 if "dsseam" in spec else 0)
     assert sum(f.kind == "kconv" for f in seam.fused.values()) == (9 if "kconv" in spec else 0)
     assert sum(f.kind == "tail" for f in seam.fused.values()) == (1 if "tail" in spec else 0)
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
@@ -248,13 +253,13 @@ def test_resnet50_seams_match_per_conv_and_oracle(r50, batch, noreuse, spec, mon
     assert torch.equal(ls.argmax(1), lp.argmax(1))
 
 
-@pytest.mark.parametrize("spec", [SEAMS, KCONV, TAIL, XSEAM])
+@pytest.mark.parametrize("spec", [SEAMS, KCONV, TAIL, XSEAM, XSEAM + ",dsseam"])
 def test_resnet50_seam_dispatches_and_replay(r50, spec):
     a, params, _, kw = r50
     g = a.build_graph(batch=1, **dict(kw, input_uint8=True))
     base = ExecContext(g, params, torch.device(DEV), fuse="convpool,bneck,bneck2")
     ctx = ExecContext(g, params, torch.device(DEV), fuse=spec)
-    assert base.num_ops() - ctx.num_ops() == (8 if "xseam" in spec else 7)
+    assert base.num_ops() - ctx.num_ops() == (8 if "xseam" in spec else 7)  # (dsseam: the pair becomes one conv)
     assert ctx.num_ops() <= 31
     s = torch.cuda.Stream()
     ctx.capture(s)
@@ -269,14 +274,8 @@ def test_resnet50_seam_dispatches_and_replay(r50, spec):
         assert _rel(lc, lb) < 2e-2 and torch.equal(lc.argmax(-1), lb.argmax(-1))
 
 
-class KconvParams(C.Structure):  # HzKconvParams (csrc/hipzap.h)
-    _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("out", C.c_void_p), ("zinit", C.c_void_p),
-                ("zbias", C.c_void_p), ("z_C", C.c_int), ("z_HW", C.c_int), ("N", C.c_int), ("H", C.c_int),
-                ("W", C.c_int), ("C", C.c_int), ("Cout", C.c_int), ("x_f32", C.c_int), ("ck", C.c_int),
-                ("stride", C.c_int)]
-
-
-HZ_K_KCONV = 21
+KconvParams = fusion.KconvParams
+HZ_K_KCONV = fusion.HZ_K_KCONV
 
 
 @pytest.mark.parametrize("c,h,ck,xf32,n,st", [(256, 14, 64, True, 1, 1), (256, 14, 32, True, 1, 1),
@@ -310,6 +309,40 @@ def test_kconv_vs_fp32(c, h, ck, xf32, n, st):
     got = CV.from_blocked(out.cpu(), (n, ho, ho, c))
     assert _rel(got, ref) < 1e-3, _rel(got, ref)
     assert torch.equal(CV.from_blocked(nxt.cpu(), (n, ho, ho, 256)), zb.cpu().expand(n, ho, ho, 256))
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_kconv_with_downsample_job(n):
+    """HzKconvParams.dso: layer4's stride-2 3x3 (fp32 input, ReLU at the load) and, in extra
+    workgroups of the same launch, the block's stride-2 1x1 downsample 1024 -> 2048 (bf16 out)."""
+    g = torch.Generator().manual_seed(40 + n)
+    c, h, cd, cdo = 512, 14, 1024, 2048
+    x = torch.randn(n, h, h, c, generator=g)
+    pc = CV.pack_conv(torch.randn(c, c, 3, 3, generator=g) * (2.0 / (9 * c)) ** 0.5, 0.1 * torch.randn(c, generator=g),
+                      None, 2, 1)
+    pd = CV.pack_conv(torch.randn(cdo, cd, 1, 1, generator=g) * cd ** -0.5, 0.1 * torch.randn(cdo, generator=g),
+                      None, 2, 0)
+    xd = torch.relu(torch.randn(n, h, h, cd, generator=g)).to(torch.bfloat16)
+    wref = pc.dense().reshape(c, 3, 3, c).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(torch.relu(x).to(torch.bfloat16).float().permute(0, 3, 1, 2), wref, pc.bias,
+                                     stride=2, padding=1).permute(0, 2, 3, 1)
+    ds_ref = xd[:, ::2, ::2, :].float() @ pd.dense().t() + pd.bias
+    ho = h // 2
+    pcd, pdd = pc.to(DEV), pd.to(DEV)
+    xdev, xdd = _blk(x), _blk(xd)
+    out = pcd.bias.view(1, c // 32, 1, 1, 32).expand(n, c // 32, ho, ho, 32).contiguous()
+    dso = torch.full((n, cdo // 32, ho, ho, 32), float("nan"), dtype=torch.bfloat16, device=DEV)
+    prm = KconvParams()
+    prm.x, prm.w, prm.out = xdev.data_ptr(), pcd.wf.data_ptr(), out.data_ptr()
+    prm.N, prm.H, prm.W, prm.C, prm.Cout, prm.x_f32, prm.ck, prm.stride = n, h, h, c, c, 1, 64, 2
+    prm.dsx, prm.dsw, prm.dsb, prm.dso = xdd.data_ptr(), pdd.wf.data_ptr(), pdd.bias.data_ptr(), dso.data_ptr()
+    prm.ds_C, prm.ds_Cout, prm.ds_H, prm.ds_W = cd, cdo, h, h
+    N.check(N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), N.stream_ptr()), "kconv+ds")
+    torch.cuda.synchronize()
+    assert _rel(CV.from_blocked(out.cpu(), (n, ho, ho, c)), ref) < 1e-3
+    assert _rel(CV.from_blocked(dso.cpu(), (n, ho, ho, cdo)).float(), ds_ref) < 1e-2
+    prm.ds_H = 13  # odd: not a stride-2 source
+    assert N.lib().hz_launch_kernel(HZ_K_KCONV, C.byref(prm), None) != 0
 
 
 def test_kconv_refuses_bad_geometry():
