@@ -18,94 +18,125 @@ HZ_DEBUG_UNIT(transformer)
 namespace {
 
 // --------------------------------------------------------------------------- LayerNorm
-// rows x D (D % 8 == 0, D <= 64*8*4): each lane holds up to 4 16-B chunks of its row.
+// rows x D (D % 8 == 0, D <= 64*8*NC): each lane holds up to NC 16-B chunks of its row (NC sized
+// to D at launch: at D = 768 two, so the kernel holds ~100 instead of 174 VGPRs). A wave owns
+// RPW consecutive rows: gamma / beta are loaded once per wave (not once per row: 6 KB a row at
+// D = 768), and row i+1's loads are issued before row i's reductions, so a wave pays one memory
+// latency for its RPW rows (RPW = 1: a wave per row, the round-1..4 kernel). Same per-row math in
+// the same order: bitwise the same outputs for every RPW.
+template <int NC, int RPW>
 __global__ __launch_bounds__(256) void layernorm_kernel(const HzLayerNormParams p) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= p.rows) return;
-  if (!HZ_DCHECK(p.D <= 4 * 64 * 8 && p.ldx >= p.D && (!p.res || p.ldr >= p.D))) return;
-  const bf16_t* x = p.x + (long)row * p.ldx;
-  const bf16_t* r = p.res ? p.res + (long)row * p.ldr : nullptr;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= p.rows) return;
+  if (!HZ_DCHECK(p.D <= NC * 64 * 8 && p.ldx >= p.D && (!p.res || p.ldr >= p.D))) return;
   const int nch = p.D >> 3;
-  // every load of the row first -- x, residual, gamma, beta -- so the kernel pays ONE memory
-  // latency before the two reductions instead of a second one for gamma/beta after them
-  u32x4 xr[4], rr4[4];
-  f32x4 g4[4][2], b4[4][2];
+  u32x4 xr[NC], rr4[NC];
+  auto load_row = [&](int row, u32x4 (&xo)[NC], u32x4 (&ro)[NC]) {
+    const bf16_t* x = p.x + (long)row * p.ldx;
+    const bf16_t* r = p.res ? p.res + (long)row * p.ldr : nullptr;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
+      const int ch = c * 64 + lane;
+      if (ch < nch) {
+        xo[c] = *reinterpret_cast<const u32x4*>(x + ch * 8);
+        if (r) ro[c] = *reinterpret_cast<const u32x4*>(r + ch * 8);
+      }
+    }
+  };
+  // every load of the first row first -- x, residual, then gamma, beta -- so the wave pays ONE
+  // memory latency before the reductions
+  load_row(row0, xr, rr4);
+  f32x4 g4[NC][2], b4[NC][2];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
     const int ch = c * 64 + lane;
     if (ch < nch) {
-      xr[c] = *reinterpret_cast<const u32x4*>(x + ch * 8);
-      if (r) rr4[c] = *reinterpret_cast<const u32x4*>(r + ch * 8);
       g4[c][0] = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8);
       g4[c][1] = *reinterpret_cast<const f32x4*>(p.gamma + ch * 8 + 4);
       b4[c][0] = *reinterpret_cast<const f32x4*>(p.beta + ch * 8);
       b4[c][1] = *reinterpret_cast<const f32x4*>(p.beta + ch * 8 + 4);
     }
   }
-  float v[4][8];
-  float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int ch = c * 64 + lane;
-    if (ch < nch) {
-      unpack8(xr[c], v[c]);
-      if (r) {
-        float rr[8];
-        unpack8(rr4[c], rr);
+  for (int i = 0; i < RPW; ++i) {
+    const int row = row0 + i;
+    if (row >= p.rows) break;  // wave-uniform
+    u32x4 xn[NC], rn[NC];
+    if (RPW > 1 && i + 1 < RPW && row + 1 < p.rows) load_row(row + 1, xn, rn);  // in flight over this row
+    float v[NC][8];
+    float s = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[c][e] += rr[e];
-      }
+    for (int c = 0; c < NC; ++c) {
+      const int ch = c * 64 + lane;
+      if (ch < nch) {
+        unpack8(xr[c], v[c]);
+        if (p.res) {
+          float rr[8];
+          unpack8(rr4[c], rr);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[c][e];
-    }
-  }
-  const float mean = warp_sum(s) / p.D;
-  float q = 0.f;
+          for (int e = 0; e < 8; ++e) v[c][e] += rr[e];
+        }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int ch = c * 64 + lane;
-    if (ch < nch) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = v[c][e] - mean;
-        q += d * d;
+        for (int e = 0; e < 8; ++e) s += v[c][e];
       }
     }
-  }
-  const float rstd = rsqrtf(warp_sum(q) / p.D + p.eps);
-  float amax = 0.f;
+    const float mean = warp_sum(s) / p.D;
+    float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int ch = c * 64 + lane;
-    if (ch < nch) {
-      const f32x4 g0 = g4[c][0], g1 = g4[c][1], b0 = b4[c][0], b1 = b4[c][1];
+    for (int c = 0; c < NC; ++c) {
+      const int ch = c * 64 + lane;
+      if (ch < nch) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[c][e] = (v[c][e] - mean) * rstd * g0[e] + b0[e];
-        v[c][e + 4] = (v[c][e + 4] - mean) * rstd * g1[e] + b1[e];
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[c][e] - mean;
+          q += d * d;
+        }
       }
-      if (p.out) *reinterpret_cast<u32x4*>(p.out + (long)row * p.ldo + ch * 8) = pack8(v[c]);
+    }
+    const float rstd = rsqrtf(warp_sum(q) / p.D + p.eps);
+    float amax = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
+    for (int c = 0; c < NC; ++c) {
+      const int ch = c * 64 + lane;
+      if (ch < nch) {
+        const f32x4 g0 = g4[c][0], g1 = g4[c][1], b0 = b4[c][0], b1 = b4[c][1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[c][e] = (v[c][e] - mean) * rstd * g0[e] + b0[e];
+          v[c][e + 4] = (v[c][e + 4] - mean) * rstd * g1[e] + b1[e];
+        }
+        if (p.out) *reinterpret_cast<u32x4*>(p.out + (long)row * p.ldo + ch * 8) = pack8(v[c]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
+      }
+    }
+    if (p.out8) {
+      // fused fp8 quantisation (same rule as fp8.hip quant_rows: s = amax / 448, e4m3fn)
+      amax = warp_max(amax);
+      const float scale = fmaxf(amax, 1e-12f) / 448.f, inv = 1.f / scale;
+      unsigned char* o8 = p.out8 + (long)row * p.D;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = c * 64 + lane;
+        if (ch < nch) {
+          float q8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q8[e] = fminf(fmaxf(v[c][e] * inv, -448.f), 448.f);
+          *reinterpret_cast<u32x2*>(o8 + ch * 8) =
+              u32x2{pack4_fp8(q8[0], q8[1], q8[2], q8[3]), pack4_fp8(q8[4], q8[5], q8[6], q8[7])};
+        }
+      }
+      if (lane == 0) p.scale8[row] = scale;
+    }
+    if constexpr (RPW > 1) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        xr[c] = xn[c];
+        rr4[c] = rn[c];
+      }
     }
   }
-  if (!p.out8) return;
-  // fused fp8 quantisation (same rule as fp8.hip quant_rows: s = amax / 448, e4m3fn)
-  amax = warp_max(amax);
-  const float scale = fmaxf(amax, 1e-12f) / 448.f, inv = 1.f / scale;
-  unsigned char* o8 = p.out8 + (long)row * p.D;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int ch = c * 64 + lane;
-    if (ch < nch) {
-      float q[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = fminf(fmaxf(v[c][e] * inv, -448.f), 448.f);
-      *reinterpret_cast<u32x2*>(o8 + ch * 8) = u32x2{pack4_fp8(q[0], q[1], q[2], q[3]), pack4_fp8(q[4], q[5], q[6], q[7])};
-    }
-  }
-  if (lane == 0) p.scale8[row] = scale;
 }
 
 // --------------------------------------------------------------------------- BERT embeddings
@@ -619,7 +650,24 @@ extern "C" int hz_layernorm_launch(const HzLayerNormParams* pp, hipStream_t st) 
   if (p.D % 8 || p.D > 2048) return -1;
   // (a half-wave-per-row variant, 3 chunks per lane at D = 768 and 8 rows per workgroup, measured
   // equal end to end on BERT / ViT: profiles/r2_transformers/layernorm_halfwave_ab)
-  hipLaunchKernelGGL(layernorm_kernel, dim3((p.rows + 3) / 4), dim3(256), 0, st, p);
+  // rows per wave: HIPZAP_LN_RPW = 1 (default), 2 or 4. Measured (profiles/r5_tx/ln_ab.jsonl):
+  // BERT bs16 16.70k / 16.45k / 15.34k seq/s, ViT fp8 bs64 16.1k / 16.0k / 15.5k img/s -- with the
+  // kernel sized to D, one row per wave already keeps 7 waves per SIMD resident
+  static const int rpw_env = getenv("HIPZAP_LN_RPW") ? atoi(getenv("HIPZAP_LN_RPW")) : 1;
+  const int rpw = rpw_env == 2 || rpw_env == 4 ? rpw_env : 1;
+  const dim3 grid((p.rows + 4 * rpw - 1) / (4 * rpw));
+  const int nc = (p.D / 8 + 63) / 64;
+#define HZ_LN(NC)                                                                           \
+  if (rpw == 4) hipLaunchKernelGGL((layernorm_kernel<NC, 4>), grid, dim3(256), 0, st, p);   \
+  else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<NC, 2>), grid, dim3(256), 0, st, p); \
+  else hipLaunchKernelGGL((layernorm_kernel<NC, 1>), grid, dim3(256), 0, st, p);
+  switch (nc) {
+    case 1: HZ_LN(1) break;
+    case 2: HZ_LN(2) break;
+    case 3: HZ_LN(3) break;
+    default: HZ_LN(4) break;
+  }
+#undef HZ_LN
   return (int)hipGetLastError();
 }
 
