@@ -51,5 +51,13 @@ def logits_match(a, b, rel: float = 2e-2) -> bool:
         return True
     a2 = a.reshape(-1, a.shape[-1]) if a.ndim > 1 else a.reshape(1, -1)
     b2 = b.reshape(-1, b.shape[-1]) if b.ndim > 1 else b.reshape(1, -1)
-    err = float(np.abs(a - b).max()) / max(float(np.abs(b).max()), 1e-6)
-    return err < rel and bool((a2.argmax(-1) == b2.argmax(-1)).all())
+    scale = max(float(np.abs(b).max()), 1e-6)
+    err = float(np.abs(a - b).max()) / scale
+    if err >= rel:
+        return False
+    # the same top class per row -- unless the reference's top two are closer than the difference
+    # between the runs (random-init logits have near-ties; a rounding-level reorder may flip them)
+    ia, ib = a2.argmax(-1), b2.argmax(-1)
+    rows = np.arange(len(ib))
+    tie = b2[rows, ib] - b2[rows, ia] <= 2 * float(np.abs(a - b).max())
+    return bool(((ia == ib) | tie).all())
