@@ -86,50 +86,15 @@ __device__ __forceinline__ void rows_stats(const float* __restrict__ st, int nsl
   }
 }
 
-// 4 consecutive output features at element offset o: + bias, + residual, activation, store
-// (the epilogue of the M32 tiles; the 16x16 loop below inlines the same steps around the LN fold)
-__device__ __forceinline__ void epilogue4(const HzConvParams& p, int n, long o, float (&v)[4]) {
-  if (p.bias) {
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] += bb[e];
-  }
-  if (p.res) {
-    const u32x2 rr = *reinterpret_cast<const u32x2*>(p.res + o);
-    v[0] += __uint_as_float(rr[0] << 16);
-    v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-    v[2] += __uint_as_float(rr[1] << 16);
-    v[3] += __uint_as_float(rr[1] & 0xffff0000u);
-  }
-  if (p.act == HZ_ACT_RELU) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-  } else if (p.act == HZ_ACT_GELU) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-  } else if (p.act == HZ_ACT_TANH) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-  }
-  if (p.out_f32) {
-    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + o) = f32x4{v[0], v[1], v[2], v[3]};
-  } else {
-    *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(p.out) + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-  }
-}
-
 // LNF: folded-LayerNorm variant (p.lnf != NULL); a separate instantiation so the plain GEMM keeps
 // its register budget (the fold's statistics cost ~60 VGPRs, which halves occupancy)
 // WM x WN waves (4 or 8): wave (wm, wn) owns rows wm*BM/WM.. and features wn*BN/WN..
-// M32: the same LDS image read as 32x32x16 operands (mfma_f32_32x32x16_bf16: one instruction per
-// 32x32 block and 16-deep sub-step, half the instructions of 16x16x32 for the same MACs; the
-// r2 issue-rate probe: 2.3 vs 1.4-2.0 PF/s). Needs 32-aligned wave sub-tiles; no LNF.
-template <int BM, int BN, int NS, bool LNF, int WM, int WN, bool CV = false, bool M32 = false>
+// (a variant reading the same LDS image as 32x32x16 operands, cfg 64-77, was a measured negative,
+// profiles/r3_m32, deleted in round 5)
+template <int BM, int BN, int NS, bool LNF, int WM, int WN, bool CV = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvParams p, int group_m) {
   constexpr int NW = WM * WN;
   constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;  // 16x16 fragments per wave
-  static_assert(!M32 || (!LNF && FCW % 2 == 0 && FPW % 2 == 0), "M32: 32-aligned wave tiles, no LN fold");
-  constexpr int FI = M32 ? FCW / 2 : 1, FJ = M32 ? FPW / 2 : 1;  // 32x32 blocks per wave (M32)
   constexpr int NWG = BN / 16;                 // weight fragments per 32-deep k-step
   constexpr int XBYTES = BM * 128;             // activation bytes per stage (BK = 64 bf16 = 128 B)
   constexpr int SBYTES = XBYTES + BN * 128;    // + 2 k-steps x NWG fragments x 1 KiB
@@ -221,25 +186,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   const int boff0 = (wm * (BM / WM) + lr) * 128 + (((lane >> 4)) ^ sw) * 16;
   const int boff1 = (wm * (BM / WM) + lr) * 128 + ((4 + (lane >> 4)) ^ sw) * 16;
   const int aoff = XBYTES + (wn * FCW) * 1024 + lane * 16;
-  // M32 readers (lane: r = lane & 31, h = lane >> 5 holds A[r][8h..8h+7], B[8h..8h+7][r]): feature
-  // r of a 32-block is row r & 15 of 16-fragment (r >> 4); sub-step t (16 deep) of k-step t >> 1 is
-  // lane slot (r & 15) + 16 (2 (t & 1) + h) of that fragment. Token r reads chunk 2t + h of its row.
-  const int r32 = lane & 31, h32 = lane >> 5;
-  const int aoff32 = XBYTES + (wn * FCW + (r32 >> 4)) * 1024 + ((r32 & 15) + 16 * h32) * 16;
-  const int brow32 = (wm * (BM / WM) + r32) * 128, sw32 = (r32 >> 1) & 7;
 
   f32x4 acc[FCW][FPW];
 #pragma unroll
   for (int i = 0; i < FCW; ++i)
 #pragma unroll
     for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x16 acc32[FI][FJ];
-#pragma unroll
-  for (int i = 0; i < FI; ++i)
-#pragma unroll
-    for (int j = 0; j < FJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -267,30 +219,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
     __builtin_amdgcn_s_barrier();
     if (st + NS - 1 < nst) stage(cur == 0 ? NS - 1 : cur - 1, st + NS - 1);
     const char* base = smem + cur * SBYTES;
-    if constexpr (M32) {
-      // every operand read of the 64-deep stage goes out first (counted lgkmcnt waits let the
-      // MFMAs of sub-step t start while the reads of t+1.. are still in flight)
-      bf16x8 a[4][FI], b[4][FJ];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-          a[t][i] = *reinterpret_cast<const bf16x8*>(base + aoff32 + (t >> 1) * NWG * 1024 + i * 2048 + (t & 1) * 512);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j)
-          b[t][j] = *reinterpret_cast<const bf16x8*>(base + brow32 + (((2 * t + h32) ^ sw32) << 4) + j * 32 * 128);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise re-serialises them)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-#pragma unroll
-          for (int j = 0; j < FJ; ++j)
-            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t][i], b[t][j], acc32[i][j], 0, 0, 0);
-      cur = cur == NS - 1 ? 0 : cur + 1;
-      continue;
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 a[FCW], b[FPW];
@@ -310,30 +238,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   // ---- fused epilogue (row-major out) ----
   // Optional folded LayerNorm (HzLnFold, hipzap.h): input-side correction rstd*(acc - mean*c1),
   // normalised residual, and per-row (sum, sumsq) partials of the stored bf16 output.
-  if constexpr (M32) {  // lane: token r32 of each 32-block, features 8q + 4 h32 + (0..3) of register group q
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int m = m0 + wm * (BM / WM) + j * 32 + r32;
-      const bool mval = m < p.M;
-      int ni_m = 0, hw_m = 0;
-      if constexpr (CV) {
-        ni_m = fdiv(mval ? m : 0, PQ);
-        hw_m = m - ni_m * PQ;
-      }
-#pragma unroll
-      for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const int n = n0 + wn * (BN / WN) + i * 32 + q4 * 8 + h32 * 4;
-          const long o = CV ? (((long)ni_m * (p.Cout >> 5) + (n >> 5)) * PQ + hw_m) * 32 + (n & 31) : (long)m * p.ldo + n;
-          const long olim = CV ? (long)p.N * p.Cout * PQ : (long)(p.M - 1) * p.ldo + p.Cout;
-          if (!mval || n >= p.Cout || !HZ_DCHECK(o + 4 <= olim)) continue;
-          float v[4] = {acc32[i][j][4 * q4], acc32[i][j][4 * q4 + 1], acc32[i][j][4 * q4 + 2], acc32[i][j][4 * q4 + 3]};
-          epilogue4(p, n, o, v);
-        }
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
     const int m = m0 + wm * (BM / WM) + j * 16 + lrow;
@@ -409,7 +313,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_lds_kernel(const HzConvPara
   }
 }
 
-template <int BM, int BN, int NS, int WM = 2, int WN = 2, bool CVOK = false, bool M32 = false>
+template <int BM, int BN, int NS, int WM = 2, int WN = 2, bool CVOK = false>
 int launch_lds(const HzConvParams& p, hipStream_t st) {
   // the last feature tile must stay inside the 128-row padded weight packing (BN = 96 / 192 / 288
   // tiles fit only some widths: every BERT / ViT projection, not arbitrary N)
@@ -425,20 +329,20 @@ int launch_lds(const HzConvParams& p, hipStream_t st) {
       if (p.out_rowmajor || p.lnf || p.C % 64 || p.Cout % BN || p.Cout % 32 || p.K != p.R * p.S * p.C ||
           (long)p.N * p.C * p.H * p.W * 2 >= (1L << 31))
         return -1;
-      hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, true, M32>), dim3(tiles), block, 0, st, p, group_m);
+      hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, true>), dim3(tiles), block, 0, st, p, group_m);
       return (int)hipGetLastError();
     } else {
       return -1;
     }
   }
   if (p.lnf) {  // the folded-LayerNorm statistics slabs assume 2 feature halves per tile
-    if constexpr (WN != 2 || M32 || !HZ_EXPERIMENTS) {
+    if constexpr (WN != 2 || !HZ_EXPERIMENTS) {
       return -3;  // (the LN-fold epilogue is an experiment: not in the product library)
     } else {
       hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, true, WM, 2>), dim3(tiles), block, 0, st, p, group_m);
     }
   } else {
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, false, M32>), dim3(tiles), block, 0, st, p, group_m);
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, NS, false, WM, WN, false>), dim3(tiles), block, 0, st, p, group_m);
   }
   return (int)hipGetLastError();
 }
@@ -469,17 +373,6 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
       case 31: return launch_lds<128, 64, 3, 4, 2, true>(p, st);
       case 32: return launch_lds<64, 128, 3, 2, 4, true>(p, st);
       case 33: return launch_lds<256, 64, 2, 4, 2, true>(p, st);
-#if HZ_EXPERIMENTS
-      // 64-77: mfma_f32_32x32x16_bf16 tiles (M32)
-      case 64: return launch_lds<128, 128, 2, 2, 2, true, true>(p, st);
-      case 65: return launch_lds<128, 128, 3, 2, 2, true, true>(p, st);
-      case 66: return launch_lds<128, 128, 2, 2, 4, true, true>(p, st);
-      case 67: return launch_lds<256, 128, 2, 4, 2, true, true>(p, st);
-      case 69: return launch_lds<64, 64, 2, 2, 2, true, true>(p, st);
-      case 71: return launch_lds<128, 64, 3, 4, 2, true, true>(p, st);
-      case 72: return launch_lds<64, 128, 2, 2, 2, true, true>(p, st);
-      case 76: return launch_lds<128, 64, 2, 2, 2, true, true>(p, st);
-#endif
       default: return -2;
     }
   }
@@ -513,23 +406,6 @@ extern "C" int hz_gemm_lds_launch(const HzConvParams* pp, int cfg, hipStream_t s
     case 38: return launch_lds<64, 288, 3, 2, 2>(p, st);
     case 39: return launch_lds<256, 96, 2, 2, 2>(p, st);
     case 40: return launch_lds<64, 96, 4, 2, 2>(p, st);
-#if HZ_EXPERIMENTS
-    // 64-77: the LDS image read as mfma_f32_32x32x16_bf16 operands (32-aligned wave tiles)
-    case 64: return launch_lds<128, 128, 2, 2, 2, false, true>(p, st);
-    case 65: return launch_lds<128, 128, 3, 2, 2, false, true>(p, st);
-    case 66: return launch_lds<128, 128, 2, 2, 4, false, true>(p, st);
-    case 67: return launch_lds<256, 128, 2, 4, 2, false, true>(p, st);
-    case 68: return launch_lds<128, 256, 2, 2, 4, false, true>(p, st);
-    case 69: return launch_lds<64, 64, 2, 2, 2, false, true>(p, st);
-    case 70: return launch_lds<64, 64, 3, 2, 2, false, true>(p, st);
-    case 71: return launch_lds<128, 64, 3, 4, 2, false, true>(p, st);
-    case 72: return launch_lds<64, 128, 2, 2, 2, false, true>(p, st);
-    case 73: return launch_lds<64, 128, 3, 2, 2, false, true>(p, st);
-    case 74: return launch_lds<128, 192, 2, 4, 2, false, true>(p, st);
-    case 75: return launch_lds<64, 192, 2, 2, 2, false, true>(p, st);
-    case 76: return launch_lds<128, 64, 2, 2, 2, false, true>(p, st);
-    case 77: return launch_lds<256, 256, 2, 4, 2, false, true>(p, st);
-#endif
     default: return -2;
   }
 }

@@ -244,15 +244,15 @@ class ExecContext:
                 # a conv with row-major output (ViT patch embedding) never runs as the LDS implicit GEMM
                 lds_pc = None if n.kind == "conv" and n.attrs.get("rowmajor") else pc
                 cfg, kw = conv_ops.choose_config(M, pc.cout, pc.K, tuned, key, rowmajor=n.kind == "gemm", pc=lds_pc)
-            # HzLnFold lives in the 16x16 LDS GEMM epilogue with 2 wave columns (not in the
-            # 32x32x16 M32 tiles), and only in the experiments build
+            # HzLnFold lives in the LDS GEMM epilogue with 2 wave columns, and only in the
+            # experiments build
             if _ln_folded(n):
                 if not self.recording and not N.experiments():
                     raise RuntimeError("the folded-LayerNorm GEMMs (HIPZAP_LN_FOLD=1) are a measured negative "
                                        "built only into the experiments library: python -m hipzap.build "
                                        "--experiments, HIPZAP_LIB=hipzap/_lib/libhipzap_exp.so")
                 cfg = conv_ops.LNF_REMAP.get(cfg, cfg)
-                if cfg not in conv_ops.LDS_TILES or cfg in conv_ops.M32_CFGS:
+                if cfg not in conv_ops.LDS_TILES:
                     if not conv_ops.lds_ok(M, pc.K, True, pc):
                         raise ValueError(f"{n.attrs.get('name')}: folded LayerNorm needs the LDS GEMM (M={M} < 64?)")
                     cfg, kw = 19, 1

@@ -29,19 +29,16 @@ LDS_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
              28: (128, 128), 29: (128, 128), 30: (256, 128), 31: (128, 64), 32: (64, 128),
              33: (256, 64),  # 28-33: 8-wave workgroups
              34: (64, 96), 35: (128, 192), 36: (128, 192), 37: (64, 288), 38: (64, 288), 39: (256, 96),
-             40: (64, 96),  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
-             # 64-77: the same LDS image read as mfma_f32_32x32x16_bf16 operands (csrc/gemm.hip M32)
-             64: (128, 128), 65: (128, 128), 66: (128, 128), 67: (256, 128), 68: (128, 256), 69: (64, 64),
-             70: (64, 64), 71: (128, 64), 72: (64, 128), 73: (64, 128), 74: (128, 192), 75: (64, 192),
-             76: (128, 64), 77: (256, 256)}
-M32_CFGS = tuple(range(64, 78))
+             40: (64, 96)}  # 34-40: one tile per CU at M = 2048 (BERT) projection widths
+# (cfg 64-77, the same LDS image read as 32x32x16 MFMA operands, were a measured negative,
+# profiles/r3_m32, and were deleted in round 5; source: git history)
 # the folded-LayerNorm epilogue (HzLnFold, experiments build) writes its statistics slabs per
 # (feature tile, wave column) of a 2-column wave grid: LDS tiles with 4 wave columns map to the
 # same tile with 2 (128x192 has none: 128x128)
 LNF_REMAP = {28: 16, 29: 20, 32: 17, 35: 16, 36: 16}
 # LDS tiles that also run as an implicit-GEMM conv on channel-blocked activations (csrc/gemm.hip CV
 # mode; ResNet at batch >= 4): C % 64 == 0, Cout % BN == 0
-LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 64, 65, 66, 67, 69, 71, 72, 76)
+LDS_CONV_CFGS = (16, 17, 18, 19, 20, 21, 22, 23, 28, 29, 30, 31, 32, 33)
 LDS_CONV_MIN_M = 4096  # heuristic: below this the register-ring conv kernel (bs=1 shapes) stays
 ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 NUM_CUS = 256
@@ -200,11 +197,10 @@ def candidates(M: int, cout: int, K: int, rowmajor: bool = False, pc: PackedConv
     """All legal (cfg, kw) launch choices worth timing for one conv / GEMM shape."""
     steps = max(1, math.ceil(K / 32))
     out = []
-    exp = N.experiments()  # the 32x32 (M32) tiles exist only in the HZ_EXPERIMENTS library
     if lds_ok(M, K, rowmajor, pc):
-        out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout) and (exp or cfg not in M32_CFGS)]
+        out += [(cfg, 1) for cfg in LDS_TILES if lds_fits(cfg, cout)]
     elif not rowmajor and lds_conv_ok(M, pc):
-        out += [(cfg, 1) for cfg in LDS_CONV_CFGS if lds_conv_fits(cfg, cout) and (exp or cfg not in M32_CFGS)]
+        out += [(cfg, 1) for cfg in LDS_CONV_CFGS if lds_conv_fits(cfg, cout)]
     for cfg, (fc, fp) in enumerate(TILES):
         if (fc > 1 and fc * 16 > cout) or (fp > 1 and fp * 16 > M):
             continue

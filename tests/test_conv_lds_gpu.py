@@ -24,8 +24,6 @@ SHAPES = [
 
 @pytest.mark.parametrize("cfg", C.LDS_CONV_CFGS)
 def test_lds_conv_every_tile(cfg):
-    if cfg in C.M32_CFGS and not N.experiments():
-        pytest.skip("M32 tiles are a measured negative, built only with --experiments")
     for n, cin, h, cout, k, stride, pad, res in SHAPES:
         if not C.lds_conv_fits(cfg, cout):
             continue

@@ -114,8 +114,6 @@ def test_linear_gemm(M, N, K, act):
                                             (64, 132, 64, "none", False)])
 def test_lds_gemm(cfg, M, N, K, act, res):
     """LDS-tiled GEMM (csrc/gemm.hip) vs fp32: ragged M and N tails, all tiles."""
-    if cfg in C.M32_CFGS and not NN.experiments():
-        pytest.skip("M32 tiles are a measured negative, built only with --experiments")
     g = torch.Generator().manual_seed(3)
     w = torch.randn(N, K, generator=g) * 0.03
     b = torch.randn(N, generator=g)
@@ -129,24 +127,6 @@ def test_lds_gemm(cfg, M, N, K, act, res):
     ref = x.float() @ w.to(torch.bfloat16).float().t() + b + (r.float() if res else 0)
     ref = {"gelu": torch.nn.functional.gelu, "relu": torch.relu}.get(act, lambda t: t)(ref)
     assert _rel(y, ref) < 2e-2
-
-
-@pytest.mark.parametrize("m32,base", [(64, 20), (65, 16), (66, 29), (67, 30), (69, 23), (71, 31), (72, 21), (77, 16)])
-def test_lds_gemm_m32_matches_16x16(m32, base):
-    """The 32x32x16-MFMA tiles (csrc/gemm.hip M32) read the same LDS image through a different
-    lane map: against the 16x16x32 kernel in fp32 output they agree to summation-order rounding,
-    so a wrong operand or accumulator map (even one that permutes a few k) cannot hide."""
-    from hipzap import _native as NN
-    if not NN.experiments():
-        pytest.skip("M32 tiles are a measured negative: python -m hipzap.build --experiments")
-    M, N, K = 520, 768, 1024
-    g = torch.Generator().manual_seed(5)
-    w = torch.randn(N, K, generator=g) * 0.03
-    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
-    pc = C.pack_linear(w, torch.randn(N, generator=g)).to(DEV)
-    ya = C.linear(x, pc, act="gelu", cfg=m32, kw=1, out_f32=True)
-    yb = C.linear(x, pc, act="gelu", cfg=base, kw=1, out_f32=True)
-    assert _rel(ya, yb) < 1e-5
 
 
 @pytest.mark.parametrize("ln_fold", ["1", "0"])
