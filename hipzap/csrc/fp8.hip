@@ -457,129 +457,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
-// Deeper prefetch at cfg 24's residency (cfg 48 / 49): cfg 24 waits on memory
-// (PMC: waves waiting 54 % of their cycles, MFMA busy 0.20 per SIMD, LDS active 15 %,
-// profiles/r5_mx) with one 32-KB stage in flight per workgroup, and a deeper LDS ring would cost
-// its second workgroup per CU (cfg 27 / 30, 3 / 4 stages at one workgroup: slower). Here only the
-// activations go through LDS (D+1 stages of 16 KB) and each wave loads its own weight fragments
-// straight from L2 into a register ring D k-steps ahead (the lane holds exactly the 2 x 16 B the
-// LDS read of cfg 24 gave it: same operands, same MFMA order -> bitwise equal to cfg 24). D = 2:
-// 48 KB of LDS, two k-steps of both operands in flight per workgroup, two workgroups per CU.
-template <int BM, int BN, int D, bool XS, int WM = 2, int WN = 4>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_mxr_kernel(const HzGemmFp8Params p, int group_m) {
-  constexpr int NW = WM * WN;
-  constexpr int NS = D + 1;  // activation stages in LDS = weight slots in registers
-  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;
-  constexpr int XBYTES = BM * 128;
-  constexpr int SBYTES = XBYTES + (XS ? NW * 256 : 0);
-  constexpr int XPW = BM / 8 / NW;
-  static_assert(XPW * 8 * NW == BM && FCW >= 1 && FPW >= 1 && BM / 64 <= NW, "tile / wave split");
-  constexpr int G = XPW + (XS ? 1 : 0) + 2 * FCW;  // vector-memory ops per wave per k-step
-  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  int tile_m, tile_n;
-  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
-  const int n0 = tile_n * BN, m0 = tile_m * BM;
-  const int kb = p.K >> 7;
-
-  const unsigned char* xsrc[XPW];
-#pragma unroll
-  for (int i = 0; i < XPW; ++i) {
-    const int q = wave + NW * i;
-    const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
-    const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
-    xsrc[i] = p.x + (long)row * p.ldx + chunk * 16;
-  }
-  const unsigned char* ssrc = XS ? p.xs + (long)min(m0 + (wave % (BM / 64)) * 64 + lane, p.M - 1) * (p.K >> 5) : nullptr;
-  // this wave's weight fragments (features n0 + wn*BN/WN + 16i): the lane's 16 B of each 1-KiB half
-  const unsigned char* wsrc[FCW];
-#pragma unroll
-  for (int i = 0; i < FCW; ++i) wsrc[i] = p.wmx + (long)((n0 + wn * (BN / WN)) / 16 + i) * kb * 2048 + lane * 16;
-  i32x8 wa[NS][FCW];
-  auto issue = [&](int buf, int st) {  // k-step st: activations (+ scales) -> LDS buffer buf, weights -> slot buf
-    char* base = smem + buf * SBYTES;
-    if constexpr (XS) glds4_8(ssrc + st * 4, base + XBYTES + wave * 256);
-#pragma unroll
-    for (int i = 0; i < XPW; ++i) glds16_8(xsrc[i] + st * 128, base + (wave + NW * i) * 1024);
-#pragma unroll
-    for (int i = 0; i < FCW; ++i) {
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(wsrc[i] + (long)st * 2048);
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(wsrc[i] + (long)st * 2048 + 1024);
-      wa[buf][i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-  };
-
-  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
-  const int brow = (wm * (BM / WM) + lr) * 128;
-  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
-  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
-
-  f32x4 acc[FCW][FPW];
-#pragma unroll
-  for (int i = 0; i < FCW; ++i)
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s0 = 0; s0 < D; ++s0)
-    if (s0 < kb) issue(s0, s0);
-  for (int st0 = 0; st0 < kb; st0 += NS) {
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {  // slot / buffer j: compile-time (st0 is a multiple of NS)
-      const int st = st0 + j;
-      if (st >= kb) break;
-      // k-steps issued after st: min(D - 1, kb - 1 - st), G ops each (vmcnt retires in issue order)
-      const int ahead = min(D - 1, kb - 1 - st);
-      if (D > 2 && ahead >= 2) wait_vm8<(D > 2 ? 2 * G : 0)>();
-      else if (D > 1 && ahead >= 1) wait_vm8<(D > 1 ? G : 0)>();
-      else wait_vm8<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (st + D < kb) issue((j + D) % NS, st + D);  // into the buffer / slot k-step st - 1 used
-      const char* base = smem + j * SBYTES;
-      i32x8 b[FPW];
-#pragma unroll
-      for (int jj = 0; jj < FPW; ++jj) {
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(base + boff0 + jj * 16 * 128);
-        const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + jj * 16 * 128);
-        b[jj] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-      }
-      int sb[FPW];
-#pragma unroll
-      for (int jj = 0; jj < FPW; ++jj) {
-        if constexpr (XS) {
-          const int r = wm * (BM / WM) + jj * 16 + (lane & 15);
-          sb[jj] = *reinterpret_cast<const unsigned char*>(base + XBYTES + (r >> 6) * 256 + (r & 63) * 4 + (lane >> 4));
-        } else {
-          sb[jj] = 0x7f7f7f7f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < FCW; ++i)
-#pragma unroll
-        for (int jj = 0; jj < FPW; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[j][i], b[jj], acc[i][jj], 0, 0, 0, 0x7f7f7f7f,
-                                                                       0, sb[jj]);
-    }
-  }
-  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
-}
-
-template <int BM, int BN, int D, int WM = 2, int WN = 4>
-int launch_mxr(const HzGemmFp8Params& p, hipStream_t st) {
-  if (p.N % BN) return -4;  // every wave's weight fragments exist
-  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
-  const int group_m = group_env < 1 ? 1 : group_env;
-  const dim3 block(64 * WM * WN);
-  if (p.xs) hipLaunchKernelGGL((gemm_mxr_kernel<BM, BN, D, true, WM, WN>), dim3(tiles), block, 0, st, p, group_m);
-  else hipLaunchKernelGGL((gemm_mxr_kernel<BM, BN, D, false, WM, WN>), dim3(tiles), block, 0, st, p, group_m);
-  return (int)hipGetLastError();
-}
-
 // Measured-negative MX schedules removed in round 5, their numbers committed: the
 // ping-pong 128x128 tile with two wave groups a phase apart (cfg 34-36, 1.4x slower than cfg 24,
 // profiles/r4_mx), the 256-row tiles with a branch-free main loop (cfg 43-45) and the ring-pipelined
@@ -629,10 +506,6 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
-      // activations through LDS, weights through a register ring (cfg 24's tile and wave map)
-      case 48: return launch_mxr<128, 128, 2>(p, st);
-      case 49: return launch_mxr<128, 128, 1>(p, st);
-      case 50: return launch_mxr<128, 128, 3>(p, st);
       default: return -2;
     }
   }

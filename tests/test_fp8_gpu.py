@@ -122,7 +122,7 @@ def _mx_decode(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
     return q8.view(torch.float8_e4m3fn).float() * sc
 
 
-@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 48, 49, 50])
+@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33])
 @pytest.mark.parametrize("mx_in,mx_out", [(True, False), (False, True), (True, True)])
 def test_gemm_mx8_activations(cfg, mx_in, mx_out):
     """MX8 (e4m3 + E8M0 per 32 k) activations into the block-scaled MFMA, and MX8 output from
@@ -161,15 +161,14 @@ def test_gemm_mx8_activations(cfg, mx_in, mx_out):
         assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-2
 
 
-@pytest.mark.parametrize("cfg", [33, 48, 49, 50])
-@pytest.mark.parametrize("mx_in,mx_out", [(False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("cfg", [33])
+@pytest.mark.parametrize("mx_in,mx_out", [(False, False), (True, True)])
 def test_gemm_mx256_bitwise_vs_128(cfg, mx_in, mx_out):
     """The plain 256x256 MX tile (cfg 33) sums every output over the same k-steps in the same order
     with the same instruction and epilogue as the 8-wave 128x128 kernel (cfg 24): results are
     BITWISE equal, over several row tiles (one partial) and column tiles, bf16 or MX8 output.
-    The register-ring tiles (cfg 48-50: weights straight into registers, activations through LDS)
-    feed the same operands to the same MFMAs in the same order: bitwise too. (The 256-row /
-    ping-pong variants 34-36 and 43-47 were removed in round 5; their bitwise tests with them.)"""
+    (The 256-row / ping-pong variants 34-36 and 43-47 were removed in round 5; their bitwise tests
+    with them.)"""
     _need_exp(cfg)
     import ctypes
     from hipzap import _native as N
