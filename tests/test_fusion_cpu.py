@@ -294,3 +294,46 @@ def test_resnet50_layer3_downsample_seam(r50):
     assert fz[s0.init].kind == "kconv" and fz[s0.init].preset == s0.init - 1  # conv1 alone presets it
     gp = fusion.planning_graph(g, fz)
     assert sk[0].nodes[0].inputs[0] in gp.nodes[s0.start].inputs
+
+
+def test_round5_launchers_refuse_malformed_params_before_any_hip_call():
+    """The seam (tail, cross-stage, downsample), K-split (+ downsample job) and fused QKV +
+    attention launchers validate geometry on the host and return before any HIP call (so this runs
+    without a GPU): a shape their tiles do not assume would read out of bounds."""
+    import ctypes as C
+    from hipzap import _native as N
+    from hipzap.ops import transformer as T
+    lib = N.lib()
+    fake = 1 << 20  # never dereferenced
+
+    def seam(**kw):
+        p = fusion.SeamParams(t2=fake, w3=fake, b3=fake, res=fake, y=fake, w1=fake, z=fake, N=1, HW=49, CM=512, cs=128)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return lib.hz_launch_kernel(fusion.HZ_K_SEAM, C.byref(p), None)
+
+    assert seam(CM=384) != 0 and seam(cs=96) != 0
+    assert seam(tail=1, HW=81) != 0                       # the pooling tail: one 64-pixel tile per image
+    assert seam(tail=1, CM=256, HW=49) != 0
+    assert seam(cn=384, CM=256, HW=196) != 0              # cross-stage seam: CM 256 -> conv1 512 only
+    assert seam(ds=1, t2_f32=0) != 0                      # the downsample seam follows a K-split conv
+    assert seam(ds=1, t2_f32=1, xd=fake, wd=fake, bd=fake, xd_H=13, xd_W=13) != 0
+    assert seam(ds=1, t2_f32=1, xd=fake, wd=fake, bd=fake, xd_H=16, xd_W=16) != 0  # 8x8 != 49 pixels
+
+    def kconv(**kw):
+        p = fusion.KconvParams(x=fake, w=fake, out=fake, N=1, H=14, W=14, C=512, Cout=512, x_f32=1, ck=64, stride=2)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return lib.hz_launch_kernel(fusion.HZ_K_KCONV, C.byref(p), None)
+
+    assert kconv(ck=48) != 0 and kconv(stride=3) != 0 and kconv(H=13) != 0
+    assert kconv(dso=fake, dsx=fake, dsw=fake, dsb=fake, ds_C=512, ds_Cout=2048, ds_H=14, ds_W=14) != 0
+    assert kconv(dso=fake, dsx=fake, dsw=fake, dsb=fake, ds_C=1024, ds_Cout=2048, ds_H=18, ds_W=18) != 0
+
+    def qa(**kw):
+        p = T.QkvAttParams(fake, fake, fake, 0, fake, 2, 128, 12, 768, 24, 768, 768, 0.125)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return lib.hz_launch_kernel(T.K_QKVATT, C.byref(p), None)
+
+    assert qa(L=129) != 0 and qa(D=700) != 0 and qa(ksteps=23) != 0 and qa(ldx=770) != 0 and qa(w=None) != 0
