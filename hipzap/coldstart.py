@@ -168,7 +168,7 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
         logs = [(tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")) for _ in range(world)]
         t = time.time()
         for r in range(world):
-            cmd = [sys.executable, "-m", "hipzap.coldstart", "node", plan, "--device", str(r), "--rank", str(r),
+            cmd = [*python_cmd(), "-m", "hipzap.coldstart", "node", plan, "--device", str(r), "--rank", str(r),
                    "--world", str(world), "--rdzv", rdzv] + (["--dry"] if dry else [])
             procs.append(subprocess.Popen(cmd, cwd=root, env=env, stdout=logs[r][0], stderr=logs[r][1], text=True))
 
@@ -259,6 +259,16 @@ def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:
     return base, 0
 
 
+def python_cmd(torch_free: bool = True) -> list:
+    """The interpreter command of a fresh worker. A torch-free worker (plan, .pth-lite, LM-lite,
+    node) needs only the standard library and this package, so it starts with ``-S``: no
+    site-packages scan (on these images ~50 ms of the bare interpreter start, with dozens of .pth
+    hooks; `python -S -c pass` ~13 ms). ``HIPZAP_COLD_SITE=1`` keeps the site scan (A/B)."""
+    if torch_free and os.environ.get("HIPZAP_COLD_SITE", "0") != "1":
+        return [sys.executable, "-S"]
+    return [sys.executable]
+
+
 def _fresh_cmd(mode: str, path: str, model: str, device: int, extra_args: list | None) -> list:
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if mode == "native":
@@ -272,7 +282,8 @@ def _fresh_cmd(mode: str, path: str, model: str, device: int, extra_args: list |
         with open(img, "wb") as f:
             f.write(os.urandom(nbytes))
         return [exe, path, "--once", img, "--device", str(device)]
-    return [sys.executable, "-m", "hipzap.coldstart", mode, path, "--model", model, "--device", str(device),
+    return [*python_cmd(mode in ("plan", "pth-lite", "lm")), "-m", "hipzap.coldstart", mode, path, "--model", model,
+            "--device", str(device),
             *(extra_args or [])]
 
 
@@ -285,6 +296,8 @@ def _fresh_trial(cmd: list, mode: str, env, timeout: float) -> tuple[float, dict
     if r.returncode != 0 or not lines:
         raise RuntimeError(f"cold-start child ({mode}) failed rc={r.returncode}: {r.stderr[-3000:]}")
     out = json.loads(lines[-1])
+    if "t_interp" in out and isinstance(out.get("phases_ms"), dict):  # process spawn -> this module's first line
+        out["phases_ms"] = {"spawn_to_interp": (out["t_interp"] - t) * 1e3, **out["phases_ms"]}
     return (out["t_first"] - t) * 1e3, out
 
 
@@ -369,6 +382,7 @@ def main(argv=None) -> int:
     else:
         res = run_torch(a.path, a.model, a.device, packed=a.mode == "hzpack")
     res["t_interp"] = T0
+    res["no_site"] = bool(sys.flags.no_site)
     print(json.dumps(res), flush=True)
     return 0 if res["ok"] else 1
 
