@@ -84,7 +84,9 @@ typedef struct HzPoolFcParams {
 } HzPoolFcParams;
 int hz_pool_fc_launch(const HzPoolFcParams* p, hipStream_t st);
 
-// image pre-processing: src NCHW fp32 (mode 0) or NHWC uint8 (mode 1) -> NHWC bf16 with Cpad channels
+// image pre-processing: src NCHW fp32 (mode 0) or NHWC uint8 (mode 1) -> NHWC bf16 with Cpad channels;
+// mode 2: src NCHW fp32 -> bf16 patch rows [N * H/P * W/P][Cin * P * P] in (c, ky, kx) order, with
+// P = Cpad (16; the ViT patch embedding as a row-major GEMM)
 int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
                          int mode, const float* mean, const float* inv_std, hipStream_t st);
 

@@ -287,6 +287,46 @@ __global__ __launch_bounds__(256) void preprocess_u8c3_kernel(const unsigned* __
   }
 }
 
+// mode 2 (ViT patch embedding as a plain GEMM): src fp32 NCHW -> bf16 patch rows
+// [N * (H/P) * (W/P)][Cin * P * P], column (c, ky, kx) = the flattened [D][Cin][P][P] conv weight's
+// K order, so the patch projection is a row-major GEMM with K = Cin * P * P (768 at P = 16, Cin = 3)
+// instead of an implicit-GEMM conv over 8-channel padded pixels (K 2048). A thread owns one
+// (patch, c, ky) run of P pixels: P / 4 16-B loads, P / 8 16-B stores.
+template <int P>
+__global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                       int N, int Cin, int H, int W,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ inv_std) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (patch row, c, ky)
+  const int px = W / P, py = H / P;
+  const long runs = (long)N * py * px * Cin * P;
+  if (i >= runs) return;
+  const int ky = (int)(i % P);
+  const long t = i / P;
+  const int c = (int)(t % Cin);
+  const long row = t / Cin;  // n * py * px + pyi * px + pxi
+  const int pxi = (int)(row % px);
+  const long t2 = row / px;
+  const int pyi = (int)(t2 % py);
+  const long n = t2 / py;
+  const float* s = src + ((n * Cin + c) * H + (long)pyi * P + ky) * W + (long)pxi * P;
+  float v[P];
+#pragma unroll
+  for (int q = 0; q < P / 4; ++q) {
+    const f32x4 f = *reinterpret_cast<const f32x4*>(s + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * q + e] = f[e];
+  }
+  if (mean) {
+    const float mu = mean[c], is = inv_std[c];
+#pragma unroll
+    for (int e = 0; e < P; ++e) v[e] = (v[e] - mu) * is;
+  }
+  bf16_t* o = dst + row * ((long)Cin * P * P) + (c * P + ky) * P;
+#pragma unroll
+  for (int q = 0; q < P / 8; ++q) *reinterpret_cast<u32x4*>(o + 8 * q) = pack8(v + 8 * q);
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i + 3 < n) {
@@ -344,6 +384,14 @@ extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
 #endif
 extern "C" int hz_preprocess_launch(const void* src, unsigned short* dst, int N, int Cin, int H, int W, int Cpad,
                                     int mode, const float* mean, const float* inv_std, hipStream_t st) {
+  if (mode == 2) {  // patch rows; Cpad carries the patch size
+    if (Cpad != 16 || H % 16 || W % 16 || Cin < 1 || Cin > 8 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+      return -1;
+    const long runs = (long)N * (H / 16) * (W / 16) * Cin * 16;
+    hipLaunchKernelGGL(patchify_kernel<16>, dim3((runs + 255) / 256), dim3(256), 0, st,
+                       static_cast<const float*>(src), reinterpret_cast<bf16_t*>(dst), N, Cin, H, W, mean, inv_std);
+    return (int)hipGetLastError();
+  }
   if (Cpad % 8 || Cin > 8) return -1;
   const long total = (long)N * H * W;
   if (mode == 1 && Cin == 3 && total % 4 == 0 && ((uintptr_t)src & 15) == 0 && !HZ_PREPROC_GENERIC) {

@@ -381,6 +381,15 @@ class ExecContext:
                 self._keep += [mean, std]
             N.check(lib.hz_prog_add_preprocess(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, cin, h, w,
                                                cpad, mode, N.ptr(mean), N.ptr(std), n.slot), "add_preprocess")
+        elif n.kind == "patchify":  # preprocess mode 2: fp32 NCHW -> bf16 patch rows (Cpad = patch)
+            nb, cin, h, w = g.tensors[n.inputs[0]].shape
+            mean = std = None
+            if n.attrs.get("mean") is not None:
+                mean = torch.tensor(n.attrs["mean"], dtype=torch.float32, device=self.device)
+                std = 1.0 / torch.tensor(n.attrs["std"], dtype=torch.float32, device=self.device)
+                self._keep += [mean, std]
+            N.check(lib.hz_prog_add_preprocess(self.prog, addr(n.inputs[0]), addr(n.outputs[0]), nb, cin, h, w,
+                                               n.attrs["patch"], 2, N.ptr(mean), N.ptr(std), n.slot), "add_patchify")
         elif n.kind == "gemm":
             pc = self.params[n.attrs["w"]]
             cfg, kw, key = plan

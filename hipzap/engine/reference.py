@@ -54,6 +54,14 @@ def run_graph_reference(g: Graph, params: dict, inputs: list, bf16_acts: bool = 
             if n.attrs.get("mean") is not None:
                 x = (x - torch.tensor(n.attrs["mean"])) / torch.tensor(n.attrs["std"])
             store(n.outputs[0], F.pad(x, (0, cpad - x.shape[-1])))
+        elif k == "patchify":
+            x = vals[n.inputs[0]].float()
+            if n.attrs.get("mean") is not None:
+                x = (x - torch.tensor(n.attrs["mean"])[:, None, None]) / torch.tensor(n.attrs["std"])[:, None, None]
+            P = n.attrs["patch"]
+            nb, c, h, w = x.shape
+            x = x.reshape(nb, c, h // P, P, w // P, P).permute(0, 2, 4, 1, 3, 5)  # n, py, px, c, ky, kx
+            store(n.outputs[0], x.reshape(nb * (h // P) * (w // P), c * P * P))
         elif k == "conv":
             pc = params[n.attrs["w"]]
             res = vals[n.inputs[1]] if len(n.inputs) > 1 else None

@@ -8,18 +8,28 @@ Not in the reference.
   ``ViTConfig``). Both the transformers-5 key names (``vit.layers.{i}.attention.q_proj``,
   ``layernorm_before``, ``mlp.fc1``) and the classic ones
   (``vit.encoder.layer.{i}.attention.attention.query``, ``intermediate.dense``, ...) load.
-* Lowering: preprocess (fp32 NCHW -> bf16 NHWC8) -> patch-embed as a 16x16/16 implicit-GEMM
-  conv writing row-major tokens -> CLS + position add -> 12 pre-LN blocks (LN -> QKV GEMM ->
+* Lowering: patchify (fp32 NCHW -> bf16 patch rows [B*196][3*16*16], the flattened conv weight's
+  K order) -> patch-embed as a plain row-major GEMM (K 768; the round-1..5 implicit-GEMM conv over
+  8-channel padded pixels ran K 2048 at 112 us per bs64 forward) -> CLS + position add -> 12
+  pre-LN blocks (LN -> QKV GEMM ->
   fused attention (L=197) -> O-proj GEMM + residual -> LN -> FC1 + GELU -> FC2 + residual)
   -> LN on the CLS rows only -> classifier GEMM (fp32 logits).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from ..engine.graph import Graph
 from ..ops.conv import pack_conv
 from ._tx import TxBuilder, norm, pack_linear_padded, pack_qkv
+
+
+def _patch_conv() -> bool:
+    """HIPZAP_VIT_PATCH=conv: the patch embedding as the implicit-GEMM conv over 8-channel padded
+    pixels (rounds 1-5) instead of patchify + row-major GEMM; for A/B runs."""
+    return os.environ.get("HIPZAP_VIT_PATCH", "gemm") == "conv"
 
 
 def make_model(num_labels: int = 1000, **cfg):
@@ -59,8 +69,9 @@ def pack_vit(sd: dict, device="cpu", eps: float = 1e-12, weights: str = "bf16") 
     sd = {k: v.to(device) for k, v in sd.items()}
     cfg = config_from_sd(sd)
     pw = sd["vit.embeddings.patch_embeddings.projection.weight"]
-    P = {"patch": pack_conv(pw, sd["vit.embeddings.patch_embeddings.projection.bias"], None, stride=cfg["patch"],
-                            pad=0, cin_pad=8),
+    pb = sd["vit.embeddings.patch_embeddings.projection.bias"]
+    P = {"patch": (pack_conv(pw, pb, None, stride=cfg["patch"], pad=0, cin_pad=8) if _patch_conv()
+                   else pack_linear_padded(pw.reshape(pw.shape[0], -1), pb)),
          "cls_token": sd["vit.embeddings.cls_token"].reshape(-1).to(torch.bfloat16).contiguous(),
          "pos": sd["vit.embeddings.position_embeddings"].reshape(-1, cfg["hidden"]).to(torch.bfloat16).contiguous(),
          "final_ln": norm(sd, "vit.layernorm", eps),
@@ -90,13 +101,18 @@ def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12
     g = Graph(f"vit_bs{B}")
     x_in = g.tensor((B, 3, image, image), torch.float32, "input", external=True)
     g.inputs.append(x_in)
-    nhwc = g.tensor((B, image, image, 8), name="nhwc")
-    g.add("preprocess", [x_in], [nhwc], mean=None, std=None)
-    patches = g.tensor((B * npch, D), torch.bfloat16, "patches")
-    g.add("conv", [nhwc], [patches], w="patch", act="none", rowmajor=True, name="patch_embed")
+    tb = TxBuilder(g)
+    if _patch_conv():  # the round-1..5 lowering (A/B only)
+        nhwc = g.tensor((B, image, image, 8), name="nhwc")
+        g.add("preprocess", [x_in], [nhwc], mean=None, std=None)
+        patches = g.tensor((B * npch, D), torch.bfloat16, "patches")
+        g.add("conv", [nhwc], [patches], w="patch", act="none", rowmajor=True, name="patch_embed")
+    else:
+        prow = g.tensor((B * npch, 3 * patch * patch), torch.bfloat16, "patch_rows")
+        g.add("patchify", [x_in], [prow], patch=patch, mean=None, std=None)
+        patches = tb.gemm(prow, "patch", D, name="patch_embed")
     tok = g.tensor((B * T, D), torch.bfloat16, "tokens")
     g.add("vit_tokens", [patches], [tok], cls="cls_token", pos="pos", B=B, np=npch)
-    tb = TxBuilder(g)
     f8 = weights == "fp8"
     x = tok
     for i in range(layers):

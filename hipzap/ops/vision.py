@@ -77,6 +77,26 @@ def preprocess(src: torch.Tensor, cpad: int = 8, mean=None, std=None) -> torch.T
     return out
 
 
+def patchify(src: torch.Tensor, patch: int = 16, mean=None, std=None) -> torch.Tensor:
+    """fp32 NCHW -> bf16 patch rows [N*(H/P)*(W/P)][C*P*P], columns in (c, ky, kx) order (preprocess
+    mode 2, csrc/vision.hip patchify_kernel: the ViT patch embedding's GEMM operand)."""
+    n, cin, h, w = src.shape
+    out = torch.empty(n * (h // patch) * (w // patch), cin * patch * patch, device=src.device, dtype=torch.bfloat16)
+    mean_t = inv_t = None
+    if mean is not None:
+        mean_t = torch.tensor(mean, dtype=torch.float32, device=src.device)
+        inv_t = 1.0 / torch.tensor(std, dtype=torch.float32, device=src.device)
+    N.check(N.lib().hz_preprocess_launch(src.data_ptr(), out.data_ptr(), n, cin, h, w, patch, 2,
+                                         N.ptr(mean_t), N.ptr(inv_t), N.stream_ptr()), "patchify")
+    return out
+
+
+def patchify_reference(src: torch.Tensor, patch: int = 16) -> torch.Tensor:
+    n, c, h, w = src.shape
+    x = src.float().reshape(n, c, h // patch, patch, w // patch, patch).permute(0, 2, 4, 1, 3, 5)
+    return x.reshape(n * (h // patch) * (w // patch), c * patch * patch).to(torch.bfloat16)
+
+
 def preprocess_reference(src: torch.Tensor, cpad: int = 8, mean=None, std=None) -> torch.Tensor:
     if src.dtype == torch.uint8:
         x = src.float() / 255.0

@@ -170,6 +170,21 @@ def test_vit_engine_matches_hf():
     assert (out.argmax(1) == ref.argmax(1)).all()
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 64, 96)])
+def test_patchify_bitwise(n, h, w):
+    """ViT patch rows (preprocess mode 2): the fp32 -> bf16 rounding and (c, ky, kx) column order of
+    the flattened conv weight, bitwise the torch reshape / permute / cast."""
+    from hipzap.ops import vision as V
+    x = torch.randn(n, 3, h, w, generator=torch.Generator().manual_seed(3))
+    got = V.patchify(x.to(DEV)).cpu()
+    assert torch.equal(got, V.patchify_reference(x))
+    # and the product with the flattened weight IS the conv
+    wt = torch.randn(16, 3, 16, 16, generator=torch.Generator().manual_seed(4))
+    conv = torch.nn.functional.conv2d(x, wt, stride=16).permute(0, 2, 3, 1).reshape(-1, 16)
+    mm = V.patchify_reference(x).float() @ wt.reshape(16, -1).t()
+    assert (conv - mm).abs().max() / conv.abs().max() < 1e-2
+
+
 @pytest.mark.parametrize("rows,D,ld,dtype", [(8, 1000, 1000, torch.float32), (37, 197, 200, torch.bfloat16),
                                               (1, 5, 8, torch.float32)])
 def test_softmax_rows(rows, D, ld, dtype):
