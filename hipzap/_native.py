@@ -9,14 +9,16 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
-from pathlib import Path
 
 # HIPZAP_DEBUG=1 selects the HZ_DEBUG variant (device-side contract checks, csrc/common.h HZ_DCHECK;
 # build it with `python -m hipzap.build --debug`); failures are read with hipzap.utils.kcheck
 DEBUG = os.environ.get("HIPZAP_DEBUG") == "1"
-_LIB_PATH = Path(__file__).resolve().parent / "_lib" / ("libhipzap_debug.so" if DEBUG else "libhipzap.so")
+# plain os.path (no pathlib): this module is on the torch-free cold-start path, where pathlib's
+# imports (urllib.parse, ipaddress, ...) are a few ms of the measured window
+_LIB_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), "_lib",
+                         "libhipzap_debug.so" if DEBUG else "libhipzap.so")
 if os.environ.get("HIPZAP_LIB"):  # same-box A/B of two builds (scripts/ab_lib.sh)
-    _LIB_PATH = Path(os.environ["HIPZAP_LIB"]).resolve()
+    _LIB_PATH = os.path.realpath(os.environ["HIPZAP_LIB"])
 DEBUG_UNITS = ("conv", "gemm", "vision", "transformer", "lstm", "lmbatch", "pack", "block")
 _lock = threading.Lock()
 _lib = None
@@ -132,7 +134,7 @@ def _sig(lib, name, res, *args):
 
 
 def _load():
-    lib = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(_LIB_PATH, mode=C.RTLD_GLOBAL)
     P = c_void_p
     _sig(lib, "hz_conv_launch", c_int, C.POINTER(ConvParams), c_int, P)
     _sig(lib, "hz_conv2_launch", c_int, C.POINTER(ConvParams), C.POINTER(ConvParams), c_int, P)
@@ -240,7 +242,7 @@ _EXTRA_SIGS: list = []
 
 
 def available() -> bool:
-    return _LIB_PATH.exists()
+    return os.path.exists(_LIB_PATH)
 
 
 def lib():
@@ -250,7 +252,7 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            if not _LIB_PATH.exists():
+            if not os.path.exists(_LIB_PATH):
                 if os.environ.get("HIPZAP_NO_AUTOBUILD"):
                     raise RuntimeError(f"hipzap native library missing: {_LIB_PATH} (run python -m hipzap.build)")
                 from . import build as _b

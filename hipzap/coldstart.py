@@ -28,7 +28,6 @@ import time
 
 T0 = time.time()
 
-import json  # noqa: E402
 import os  # noqa: E402
 import sys  # noqa: E402
 
@@ -205,6 +204,7 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
             if p.returncode != 0 or not lines:
                 err = err or f"rank {r} rc={p.returncode}: {se[-2000:]}"
                 continue
+            import json
             outs.append(json.loads(lines[-1]))
         for fo, fe in logs:
             fo.close()
@@ -295,6 +295,7 @@ def _fresh_trial(cmd: list, mode: str, env, timeout: float) -> tuple[float, dict
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         raise RuntimeError(f"cold-start child ({mode}) failed rc={r.returncode}: {r.stderr[-3000:]}")
+    import json
     out = json.loads(lines[-1])
     if "t_interp" in out and isinstance(out.get("phases_ms"), dict):  # process spawn -> this module's first line
         out["phases_ms"] = {"spawn_to_interp": (out["t_interp"] - t) * 1e3, **out["phases_ms"]}
@@ -357,20 +358,48 @@ def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, time
     return out
 
 
+_OPTS = {"--model": str, "--device": int, "--vocab": str, "--words": int, "--rank": int, "--world": int,
+         "--rdzv": str}
+_MODES = ("plan", "pth", "hzpack", "pth-lite", "lm", "node")
+
+
+def _parse(argv):
+    """``mode path [--model M] [--device D] [--vocab V] [--words W] [--rank R] [--world N] [--rdzv DIR]
+    [--dry]`` by hand: argparse's import and parser construction cost ~6-10 ms of every cold start
+    (profiles/r5_cold), inside the measured window."""
+    a = {"model": "resnet50", "device": 0, "vocab": None, "words": 200, "rank": 0, "world": 1, "rdzv": None,
+         "dry": False}
+    pos, i = [], 0
+    while i < len(argv):
+        t = argv[i]
+        key, eq, val = t.partition("=")
+        if t == "--dry":
+            a["dry"] = True
+        elif key in _OPTS:
+            if not eq:
+                i += 1
+                if i >= len(argv):
+                    raise SystemExit(f"coldstart: {t} needs a value")
+                val = argv[i]
+            a[key[2:]] = _OPTS[key](val)
+        elif t.startswith("-"):
+            raise SystemExit(f"coldstart: unknown option {t}")
+        else:
+            pos.append(t)
+        i += 1
+    if len(pos) != 2 or pos[0] not in _MODES:
+        raise SystemExit(f"usage: python -m hipzap.coldstart {{{','.join(_MODES)}}} PATH [options]")
+    a["mode"], a["path"] = pos
+
+    class _A:
+        pass
+    ns = _A()
+    ns.__dict__.update(a)
+    return ns
+
+
 def main(argv=None) -> int:
-    import argparse
-    ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["plan", "pth", "hzpack", "pth-lite", "lm", "node"])
-    ap.add_argument("path")
-    ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--vocab", default=None, help="lm mode: the pickled itos list")
-    ap.add_argument("--words", type=int, default=200, help="lm mode: words to generate")
-    ap.add_argument("--rank", type=int, default=0, help="node mode")
-    ap.add_argument("--world", type=int, default=1, help="node mode")
-    ap.add_argument("--rdzv", default=None, help="node mode: rendezvous directory")
-    ap.add_argument("--dry", action="store_true", help="node mode: launcher/rendezvous only, no GPU")
-    a = ap.parse_args(argv)
+    a = _parse(sys.argv[1:] if argv is None else argv)
     if a.mode == "plan":
         res = run_plan(a.path, a.device)
     elif a.mode == "pth-lite":
@@ -383,6 +412,7 @@ def main(argv=None) -> int:
         res = run_torch(a.path, a.model, a.device, packed=a.mode == "hzpack")
     res["t_interp"] = T0
     res["no_site"] = bool(sys.flags.no_site)
+    import json  # after t_first: not part of the measured cold start
     print(json.dumps(res), flush=True)
     return 0 if res["ok"] else 1
 
