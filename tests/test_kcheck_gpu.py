@@ -26,7 +26,8 @@ from hipzap.models.resnet import randomize_bn
 from hipzap.ops import conv as cv
 from hipzap.utils import kcheck
 
-assert N.DEBUG and N._LIB_PATH.name == "libhipzap_debug.so", N._LIB_PATH
+import os
+assert N.DEBUG and os.path.basename(N._LIB_PATH) == "libhipzap_debug.so", N._LIB_PATH
 res = {}
 torch.manual_seed(0)
 dev = "cuda:0"
