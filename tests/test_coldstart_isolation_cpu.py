@@ -37,3 +37,19 @@ def test_interleaved_cold_start_alternates_and_drops_failed_routes(monkeypatch):
     assert out["plan"]["trials"] == 3 and out["pth_lite"]["trials"] == 3
     assert out["plan"]["all_ms"] == [101.0, 104.0, 107.0] and out["plan"]["p50_ms"] == 104.0
     assert "error" in out["native"] and out["plan"]["interleaved_with"] == ["native", "pth_lite"]
+
+
+def test_child_argv_parser():
+    """The cold-start child parses its argv by hand (no argparse in the measured window)."""
+    import pytest
+    from hipzap import coldstart as cs
+    a = cs._parse(["node", "x.hzplan", "--rank", "1", "--world=2", "--rdzv", "/tmp/r", "--dry"])
+    assert (a.mode, a.path, a.rank, a.world, a.rdzv, a.dry, a.device, a.model) == \
+        ("node", "x.hzplan", 1, 2, "/tmp/r", True, 0, "resnet50")
+    a = cs._parse(["lm", "ck.pth", "--vocab", "itos.pkl", "--words", "20", "--device", "3"])
+    assert (a.mode, a.vocab, a.words, a.device, a.dry) == ("lm", "itos.pkl", 20, 3, False)
+    a = cs._parse(["plan", "a=b.hzplan"])  # '=' in a positional is a path, not an option
+    assert a.path == "a=b.hzplan"
+    for bad in (["plan"], ["bogus", "p"], ["plan", "p", "--nope"], ["plan", "p", "--rank"], ["plan", "p", "q"]):
+        with pytest.raises(SystemExit):
+            cs._parse(bad)
