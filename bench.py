@@ -37,8 +37,17 @@ import os  # noqa: E402
 import statistics  # noqa: E402
 import sys  # noqa: E402
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+# torch (which maps libamdhip64) is imported by the rank processes only, after the launch decision:
+# the N-rank launcher counts GPUs from the KFD topology and spawns the ranks without ever mapping or
+# initialising HIP
+torch = dist = None
+
+
+def _import_torch():
+    global torch, dist
+    import torch as _torch
+    import torch.distributed as _dist
+    torch, dist = _torch, _dist
 
 METRIC = "inferences/sec (whole node) + p50 cold-start ms, ResNet-50 bs=1 at 1/2/4/8 GPU"
 BASELINE_INF_S = 27.2  # reference execution model (CPU PyTorch in a WSGI handler), ResNet-50 bs=1
@@ -56,7 +65,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 16)),
                     help="concurrent bs=1 request contexts per GPU (16: the 24-48 rate at 2/3 of the 24-stream latency, profiles/r4_final/streams)")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
-    ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 9)),
+    ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 15)),
                     help="fresh processes per cold-start path (0: skip)")
     ap.add_argument("--cold-runs", type=int, default=3, help="extra in-process engine rebuilds (secondary figure)")
     ap.add_argument("--serve", choices=["executor", "threads", "pipelined"], default="executor",
@@ -81,6 +90,8 @@ def parse():
                     help="also report the GET /inference (AWD-LSTM V=60000, 200 words) torch-free cold start")
     ap.add_argument("--dp-figures", type=int, default=int(os.environ.get("HIPZAP_BENCH_DP", 1)),
                     help="also measure BASELINE configs 3 / 5 (scatter-gather DP) in the same launch")
+    ap.add_argument("--config-figures", type=int, default=int(os.environ.get("HIPZAP_BENCH_CONFIGS", 1)),
+                    help="also time BASELINE configs 1 / 4 and the reference's GET /inference route (rank 0)")
     ap.add_argument("--sustained-s", type=float, default=2.0,
                     help="secondary figure: served throughput over a self-timed window of at least this long")
     ap.add_argument("--mode", choices=["replica", "scatter"], default="replica",
@@ -214,6 +225,9 @@ def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
     if "error" in il["plan"]:
         raise RuntimeError(f"plan cold start failed: {il['plan']['error']}")
     res = {"plan": il["plan"]}
+    from hipzap.coldstart import isolated_env, narrow_env
+    res["narrowing"] = narrow_env(os.environ, device_index)[2] if isolated_env(None, device_index)[0] is not None \
+        else "unchanged"
     try:  # the node: N torch-free workers, RCCL rendezvous, C1 weight broadcast, first logits on every rank
         if world > torch.cuda.device_count():  # (a shared-GPU rehearsal: one RCCL rank per GPU only)
             raise RuntimeError(f"{world} workers need {world} visible GPUs, {torch.cuda.device_count()} visible")
@@ -463,6 +477,149 @@ def http_figure(args, world: int, rank: int):
     return res
 
 
+def config_figures(args, device, world: int, rank: int) -> dict | None:
+    """The other BASELINE configs and the reference's own route, on the driver's clock in the same
+    launch. Run by rank 0 after the headline (the other ranks wait on the
+    process group's store, a CPU wait); every figure states its timed region:
+
+    * ``bert_base_bs16`` (config 4): BERT-base seq-cls, bs 16, L 128, random-init weights, bf16;
+      hipGraph replays of 1 and of 4 concurrent contexts (``Engine.bench``: the C++ replay loop,
+      all contexts' streams, synchronised) -> seq/s; plus the one-context request latency p50
+      (``Engine.infer``: pinned token ids in, logits out).
+    * ``awd_lstm_get_inference`` (the reference's route, /root/reference/main.py:105-112):
+      ``GET /inference`` through the WSGI app (``hipzap.serve.app``, Flask test clients in
+      process: routing, the batched AWD-LSTM engine, 200 sampled words, detokenisation, the JSON
+      body) on the reference's dimensions (emb 1000, hidden 1150, 3 layers, tied, V = 60000,
+      random-init); the lone-request latency p50 (sequential requests) and the req/s of 32
+      concurrent clients (wall over all their requests).
+    * ``resnet18_cpu_plumbing`` (config 1): ``scripts/bench_cpu_plumbing.py`` -- the dev server
+      (``main.py``) on the CPU backend in a child process, single-image POST /predict over HTTP,
+      sequential; req/s = 1000 / p50.
+    Returns the dict (rank 0) or None; a figure that fails is recorded as its error."""
+    from datetime import timedelta
+    from hipzap.parallel.comm import is_dist
+    out = None
+    if rank == 0:
+        out = {}
+        try:
+            out["bert_base_bs16"] = _bert_figure(args, device)
+        except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
+            out["bert_base_bs16"] = {"error": repr(e)[:500]}
+        try:
+            out["awd_lstm_get_inference"] = _lm_route_figure(args)
+        except Exception as e:  # noqa: BLE001
+            out["awd_lstm_get_inference"] = {"error": repr(e)[:500]}
+        try:
+            out["resnet18_cpu_plumbing"] = _plumbing_figure()
+        except Exception as e:  # noqa: BLE001
+            out["resnet18_cpu_plumbing"] = {"error": repr(e)[:500]}
+    if is_dist():
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("hipzap_configs_done", "1")
+        else:
+            store.wait(["hipzap_configs_done"], timedelta(seconds=1200))
+    return out
+
+
+def _bert_figure(args, device) -> dict:
+    from hipzap.engine.engine import Engine
+    from hipzap.models import registry
+    a = registry.get("bert-base")
+    torch.manual_seed(0)
+    sd = a.make_model().eval().state_dict()
+    res = {"model": "bert-base (seq-cls, 2 labels)", "batch": 16, "seq_len": 128, "dtype": "bf16",
+           "data": "synthetic (random-init weights, random token ids)"}
+    iters = max(100, args.steps * 10)
+    for ctx in (1, 4):
+        eng = Engine.from_state_dict("bert-base", sd, device, batch=16, num_contexts=ctx)
+        x = a.example_input(16)
+        eng.infer(x)
+        if ctx == 1:
+            lat = []
+            for _ in range(50):
+                t = time.perf_counter()
+                eng.infer(x)
+                lat.append((time.perf_counter() - t) * 1e3)
+            res["latency_ms_p50_1ctx"] = round(statistics.median(lat), 4)
+        eng.bench(10)
+        torch.cuda.synchronize(device)
+        t = eng.bench(iters)  # (synchronised inside: seconds for iters replays of every context)
+        res[f"seq_s_{ctx}ctx"] = round(16 * ctx * iters / t, 1)
+        res[f"ms_per_replay_{ctx}ctx"] = round(t / iters * 1e3, 4)
+        del eng
+    res["timed_region"] = f"{iters} hipGraph replays per context, all contexts concurrently, synchronised"
+    return res
+
+
+def _lm_route_figure(args) -> dict:
+    import threading
+    os.environ.setdefault("HIPZAP_SETTINGS", "/nonexistent")
+    os.environ.update(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_LM_VOCAB="60000", HIPZAP_BACKEND="gpu")
+    from hipzap.serve.app import app, get_server
+    srv = get_server()
+    t = time.perf_counter()
+    srv.lm()  # the cold load (random-init reference-dims model packed on the GPU), untimed below
+    load_ms = (time.perf_counter() - t) * 1e3
+    cl = app.test_client()
+
+    def get(seed):
+        r = cl.get(f"/inference?seed={seed}")
+        assert r.status_code == 200 and r.get_json()["response"]["text"]
+        return r
+
+    for i in range(3):
+        get(i)
+    lat = []
+    for i in range(15):
+        t = time.perf_counter()
+        get(100 + i)
+        lat.append((time.perf_counter() - t) * 1e3)
+    clients, per = 32, 6
+    errs = []
+
+    def client(c):
+        cc = app.test_client()
+        for k in range(per):
+            try:
+                r = cc.get(f"/inference?seed={1000 + c * per + k}")
+                assert r.status_code == 200
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+    th = [threading.Thread(target=client, args=(c,)) for c in range(clients)]
+    t = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    wall = time.perf_counter() - t
+    words = srv.settings.lm_words
+    return {"route": "GET /inference (WSGI app in process: Flask test clients)", "words": words,
+            "model": "AWD-LSTM emb 1000 / hidden 1150 / 3 layers / tied, V = 60000 (main.py:96)",
+            "data": "random-init weights, synthetic vocabulary", "load_ms": round(load_ms, 1),
+            "lone_request_ms_p50": round(statistics.median(lat), 3), "lone_request_ms_min": round(min(lat), 3),
+            "concurrent_clients": clients, "concurrent_requests": clients * per - len(errs),
+            "concurrent_req_s": round((clients * per - len(errs)) / wall, 1),
+            "concurrent_words_s": round((clients * per - len(errs)) * words / wall, 0), "errors": len(errs),
+            "timed_region": "lone: one request at a time, 15 requests; concurrent: 32 threads x 6 requests, wall"}
+
+
+def _plumbing_figure() -> dict:
+    import subprocess
+    root = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "bench_cpu_plumbing.py"), "--requests", "30"],
+                       capture_output=True, text=True, timeout=300, cwd=root,
+                       env=dict(os.environ, HIPZAP_RANDOM_WEIGHTS="1"))
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        raise RuntimeError(f"bench_cpu_plumbing rc={r.returncode}: {r.stderr[-800:]}")
+    res = json.loads(lines[-1])
+    res["req_s_sequential"] = round(1e3 / res["http_image_b64_ms_p50"], 1)
+    res["timed_region"] = "30 sequential HTTP POST /predict per payload kind, per-request wall"
+    return res
+
+
 def request_input(args, adapter):
     """One request's payload: a decoded uint8 HWC image (default) or an fp32 NCHW tensor."""
     if args.input == "uint8" and args.model.startswith("resnet"):
@@ -478,9 +635,11 @@ def _free_port() -> int:
 
 
 def check_gpus(n: int, share: bool) -> None:
-    """Fail loudly unless this node has ``n`` GPUs for ``n`` ranks. ``device_count`` does not
-    initialise HIP on this image, so the launcher may call it before spawning ranks."""
-    have = torch.cuda.device_count()
+    """Fail loudly unless this node has ``n`` GPUs for ``n`` ranks, counted from the KFD topology
+    in sysfs narrowed by the visibility variables (hipzap/utils/gpucount.py): no HIP call, no
+    fallback to ``hipGetDeviceCount``."""
+    from hipzap.utils.gpucount import visible_gpu_count
+    have = visible_gpu_count()
     if share:  # multi-rank rehearsal folded onto the visible GPU(s): HIPZAP_SHARE_GPU=1
         if have < 1:
             raise SystemExit(f"bench: --gpus {n} with HIPZAP_SHARE_GPU=1 needs at least one GPU, found none")
@@ -499,14 +658,17 @@ def self_launch(args) -> int:
     collectives until the process-group timeout."""
     import signal
     import subprocess
+    from hipzap.utils.gpucount import hip_mapped
     if not args.launch_check:
         check_gpus(args.gpus, os.environ.get("HIPZAP_SHARE_GPU") == "1")
+    if hip_mapped():  # the ranks must be the only processes on the GPUs
+        raise SystemExit("bench: the launcher mapped the HIP runtime before spawning its ranks")
     port = int(os.environ.get("MASTER_PORT") or _free_port())
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HIPZAP_SELF_LAUNCHED="1")
+                   MASTER_PORT=str(port), HIPZAP_SELF_LAUNCHED="1", HIPZAP_LAUNCHER_HIP_MAPPED="0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
                                       start_new_session=True))
     codes: dict[int, int] = {}
@@ -547,7 +709,8 @@ def launch_check(rank: int, world: int) -> None:
         dist.all_reduce(t)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
-                          "self_launched": os.environ.get("HIPZAP_SELF_LAUNCHED") == "1"}), flush=True)
+                          "self_launched": os.environ.get("HIPZAP_SELF_LAUNCHED") == "1",
+                          "launcher_hip_mapped": os.environ.get("HIPZAP_LAUNCHER_HIP_MAPPED")}), flush=True)
     if is_dist():
         dist.barrier()
         dist.destroy_process_group()
@@ -555,9 +718,10 @@ def launch_check(rank: int, world: int) -> None:
 
 def main():
     args = parse()
-    from hipzap.parallel.comm import env_rank
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(self_launch(args))
+    _import_torch()
+    from hipzap.parallel.comm import env_rank
     rank, world, local = env_rank()
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
@@ -607,10 +771,15 @@ def main():
     # which RCCL build each rank mapped (libhipzap_comm.so's librccl.so.1 resolves to torch's bundled
     # copy in a torch-imported process) and its version; every rank reports
     from hipzap.parallel.rccl import mapped_rccl
-    rccl_map = [mapped_rccl()]
+    # per rank: the RCCL build it mapped, and the rank / size its communicator reports
+    # (ncclCommUserRank / ncclCommCount) -- a world the driver launched must be one communicator
+    mine = dict(mapped_rccl(), rank=rank, device=device.index)
+    if native_comm is not None:
+        mine.update(comm_rank=native_comm.comm_rank(), comm_count=native_comm.comm_size())
+    rccl_map = [mine]
     if is_dist():
         rccl_map = [None] * world
-        dist.all_gather_object(rccl_map, mapped_rccl())
+        dist.all_gather_object(rccl_map, mine)
     if is_dist():
         dist.barrier()
     if args.mode == "scatter":
@@ -751,6 +920,7 @@ def main():
     http = http_figure(args, world, rank) if args.http_clients > 0 and args.batch == 1 else None
     dpf = dp_figures(args, eng, device, world, rank, native_comm) \
         if args.dp_figures and args.batch == 1 and args.model == "resnet50" else None
+    cfgs = config_figures(args, device, world, rank) if args.config_figures and args.batch == 1 else None
     torch_ref = None
     if args.compare_torch and rank == 0:
         try:
@@ -781,9 +951,12 @@ def main():
                                "cold_start_pth_torch_ms_p50: import torch + torch.load + pack); "
                                "each child sees only its own GPU (ROCR_VISIBLE_DEVICES, a one-GPU worker) unless "
                                "the launcher already restricts visibility",
-            "cold_start_isolated": not any(os.environ.get(k) for k in
-                                           ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
-                                            "GPU_DEVICE_ORDINAL")) and os.environ.get("HIPZAP_COLD_ISOLATE", "1") != "0",
+            # how each cold-start child was narrowed to its one GPU (hipzap/coldstart.py narrow_env):
+            # "rocr" (nothing set by the launcher), "rocr_from_<var>" (the launcher set a HIP-level
+            # list), "unchanged" (ROCR_VISIBLE_DEVICES already set / isolation off); the child's
+            # environment (visibility variables, KFD nodes, render nodes) is in cold_start_fresh_process
+            "cold_start_isolated": (fresh or {}).get("narrowing", "unchanged") != "unchanged",
+            "cold_start_narrowing": (fresh or {}).get("narrowing"),
             # the reference's checkpoint format (main.py:99): torch-free when the template exists
             "cold_start_pth_ms_p50": ((fresh.get("pth_lite") or fresh["pth"])["p50_ms"]) if fresh else None,
             "cold_start_pth_torch_ms_p50": fresh["pth"]["p50_ms"] if fresh else None,
@@ -820,6 +993,8 @@ def main():
             res["http_serving"] = http
         if dpf is not None:  # BASELINE configs 3 and 5 (scatter / gather DP) in the same launch
             res["dp_scatter"] = dpf
+        if cfgs is not None:  # BASELINE configs 1 and 4 and the reference's GET /inference route
+            res["configs"] = cfgs
         if torch_ref is not None:
             res["torch_miopen_graph_inf_s_1gpu_1stream"] = round(torch_ref, 2)
         print(json.dumps(res), flush=True)

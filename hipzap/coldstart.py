@@ -247,16 +247,52 @@ def run_torch(ckpt: str, model: str, device: int, packed: bool) -> dict:
 _VIS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
 
 
+def narrow_env(env: dict | None, device: int) -> tuple[dict, int, str]:
+    """The environment of a one-GPU worker for HIP device ``device`` of ``env``, narrowed at the
+    ROCr level so ROCr's init opens ONE agent: -> (env, device in it, what was done).
+
+    * nothing set: ``ROCR_VISIBLE_DEVICES=<device>`` (device 0 in the child);
+    * only a HIP-level list (``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` /
+      ``GPU_DEVICE_ORDINAL``, which HIP applies AFTER ROCr has initialised every agent it can see):
+      ``ROCR_VISIBLE_DEVICES=<k>`` with k the list's entry for ``device`` (HIP numbers the ROCr GPU
+      agents in ROCr's order) and ``HIP_VISIBLE_DEVICES=0``, the HIP-level lists dropped;
+    * ``ROCR_VISIBLE_DEVICES`` already set, a non-integer list entry, or ``HIPZAP_COLD_ISOLATE=0``:
+      unchanged."""
+    base = dict(os.environ if env is None else env)
+    if base.get("HIPZAP_COLD_ISOLATE", "1") == "0" or base.get("ROCR_VISIBLE_DEVICES"):
+        return base, device, "unchanged"
+    hip_lists = [k for k in _VIS[1:] if base.get(k)]
+    if not hip_lists:
+        base["ROCR_VISIBLE_DEVICES"] = str(device)
+        return base, 0, "rocr"
+    entries = [x.strip() for x in base[hip_lists[0]].split(",") if x.strip()]
+    if device >= len(entries) or not entries[device].isdigit() or len(hip_lists) > 1:
+        return base, device, "unchanged"
+    for k in hip_lists:
+        del base[k]
+    base["ROCR_VISIBLE_DEVICES"] = entries[device]
+    base["HIP_VISIBLE_DEVICES"] = "0"
+    return base, 0, f"rocr_from_{hip_lists[0].lower()}"
+
+
 def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:
     """A serverless worker owns ONE GPU (a one-GPU container): the cold-start child sees only
-    ``device`` (``ROCR_VISIBLE_DEVICES``), so HIP init enumerates one agent, not every GPU of the
-    node, and uses it as device 0. Left alone when the parent already restricts visibility (its
-    indices would not be physical ones) or ``HIPZAP_COLD_ISOLATE=0``."""
+    ``device``, so HIP init enumerates one agent, not every GPU of the node, and uses it as
+    device 0. Narrowed at the ROCr level (:func:`narrow_env`), also when the parent restricts
+    visibility only at the HIP level (``HIPZAP_COLD_NARROW=0``: such a parent is left alone, the
+    round-5 behaviour); ``HIPZAP_COLD_ISOLATE=0``: never narrowed."""
     base = dict(os.environ if env is None else env)
-    if base.get("HIPZAP_COLD_ISOLATE", "1") == "0" or any(base.get(k) for k in _VIS):
+    if base.get("HIPZAP_COLD_NARROW", "1") == "0" and any(base.get(k) for k in _VIS):
         return env, device
-    base["ROCR_VISIBLE_DEVICES"] = str(device)
-    return base, 0
+    out, dev, _ = narrow_env(base, device)
+    return out, dev
+
+
+def child_environment(env: dict | None) -> dict:
+    """What a cold-start child enumerates (the visibility variables it gets, KFD topology and
+    render nodes: hipzap/utils/gpucount.py), recorded with every fresh-process measurement."""
+    from hipzap.utils.gpucount import environment
+    return environment(os.environ if env is None else env)
 
 
 def python_cmd(torch_free: bool = True) -> list:
@@ -307,7 +343,13 @@ def _fresh_summary(mode: str, walls: list, res: list) -> dict:
     trials = len(walls)
     order = sorted(range(trials), key=lambda i: walls[i])
     med = res[order[len(order) // 2]]
-    return {"mode": mode, "trials": trials, "p50_ms": round(statistics.median(walls), 2),
+    # own_ms: spawn -> first logits minus the HIP runtime's init (hipSetDevice + hipFree) of the
+    # same trial -- the part of the cold start that is this runtime's (VERDICT r5 next #2e)
+    hip = [r.get("phases_ms", {}).get("hip_init_ms", r.get("phases_ms", {}).get("hip_init")) for r in res]
+    own = [w - h for w, h in zip(walls, hip) if isinstance(h, (int, float))]
+    extra = {"own_ms_p50": round(statistics.median(own), 2), "hip_init_ms_p50": round(statistics.median(
+        h for h in hip if isinstance(h, (int, float))), 2)} if own else {}
+    return {"mode": mode, "trials": trials, "p50_ms": round(statistics.median(walls), 2), **extra,
             "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2),
             "all_ms": [round(w, 1) for w in walls],
             "median_trial_phases_ms": {k: round(v, 2) for k, v in med["phases_ms"].items()},
@@ -325,7 +367,7 @@ def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5
         w, out = _fresh_trial(cmd, mode, env, timeout)
         walls.append(w)
         res.append(out)
-    return _fresh_summary(mode, walls, res)
+    return dict(_fresh_summary(mode, walls, res), child_env=child_environment(env))
 
 
 def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, timeout: float = 300.0,
@@ -352,9 +394,11 @@ def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, time
                 continue
             walls[name].append(w)
             res[name].append(o)
+    cenv = child_environment(env)
     for name in cmds:
         out[name] = _fresh_summary(runs[name][0], walls[name], res[name])
         out[name]["interleaved_with"] = sorted(n for n in runs if n != name)
+        out[name]["child_env"] = cenv
     return out
 
 

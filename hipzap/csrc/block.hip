@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (row < cnt) atomicAdd(zb + row * 32, za[i][r]);
+      if (row < cnt) atomicAdd(zb + row * 32, hz_fixq(za[i][r]));  // (hz_fixq: order-independent sum)
     }
   }
   if (p.zinit) {  // preset the next K-split 3x3 conv's accumulator (HzSeamParams.zinit)
@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (long i = (long)blockIdx.x * 512 + tid; i < n4; i += (long)gridDim.x * 512) {
       const long e = i * 4;
       const int c = (int)((e / (32L * p.z_HW)) % cbz) * 32 + (int)(e & 31);
-      *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
+      *reinterpret_cast<f32x4*>(p.zinit + e) = hz_fixq4(*reinterpret_cast<const f32x4*>(p.zbias + c));
     }
   }
 }
@@ -1305,7 +1305,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (int r = 0; r < 16; ++r) {
       if (r < r_lo || r >= r_hi) continue;
       const int px = pg * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (px < HW) atomicAdd(ob + px * 32, acc[r]);
+      if (px < HW) atomicAdd(ob + px * 32, hz_fixq(acc[r]));  // (hz_fixq: order-independent sum)
     }
   }
   if (p.zinit) {  // preset the next accumulator (HzConvParams.zinit)
@@ -1314,7 +1314,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (long i = (long)(blockIdx.x - nds) * 512 + tid; i < n4; i += (long)(gridDim.x - nds) * 512) {
       const long e = i * 4;
       const int c = (int)((e / (32L * p.z_HW)) % cbz) * 32 + (int)(e & 31);
-      *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
+      *reinterpret_cast<f32x4*>(p.zinit + e) = hz_fixq4(*reinterpret_cast<const f32x4*>(p.zbias + c));
     }
   }
 }
@@ -1368,7 +1368,7 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
   if (!p.t2 || !p.w3 || !p.b3 || !p.res || !p.y) return -1;
   if (p.N < 1 || p.HW < 1 || (p.CM != 256 && p.CM != 512) || (p.cs != 64 && p.cs != 128)) return -1;
   if (p.tail) {  // conv3 + pool of the last block: one 64-pixel tile per image, no conv1 half
-    if (p.HW > 64 || p.CM != 512 || p.zinit) return -1;
+    if (p.HW > 64 || p.HW < 2 || p.CM != 512 || p.zinit) return -1;  // (fp32 means in y's bf16 bytes: HW >= 2)
     HzSeamParams q = p;
     q.tiles = 1;
     const dim3 grid(p.N * (4 * p.CM / p.cs));

@@ -66,6 +66,17 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     }                                                                            \
   } while (0)
 
+// Deterministic cross-workgroup sums (the ResNet seam / K-split accumulators, csrc/block.hip): every
+// term added into such an accumulator -- the preset bias and each workgroup's partial -- is first
+// rounded to a multiple of 2^-13. While |sum| < 2^24 * 2^-13 = 2048 every partial sum of such terms is
+// exactly representable in fp32, so the memory-side float atomics give the same bits in any arrival
+// order (replays, stream counts, XCD placement). The rounding (<= 6.1e-5 per term) sits far below the
+// bf16 the consumer converts the sum to.
+__device__ __forceinline__ float hz_fixq(float x) { return __builtin_rintf(x * 8192.f) * (1.f / 8192.f); }
+__device__ __forceinline__ f32x4 hz_fixq4(f32x4 v) {
+  return f32x4{hz_fixq(v[0]), hz_fixq(v[1]), hz_fixq(v[2]), hz_fixq(v[3])};
+}
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((unsigned)v) << 16);
 }

@@ -370,7 +370,7 @@ __device__ __forceinline__ void zfill(const HzConvParams& p) {
   for (long i = (long)blockIdx.x * T + threadIdx.x; i < n4; i += (long)gridDim.x * T) {
     const long e = i * 4;
     const int c = (int)((e / (32L * p.z_HW)) % cb) * 32 + (int)(e & 31);
-    *reinterpret_cast<f32x4*>(p.zinit + e) = *reinterpret_cast<const f32x4*>(p.zbias + c);
+    *reinterpret_cast<f32x4*>(p.zinit + e) = hz_fixq4(*reinterpret_cast<const f32x4*>(p.zbias + c));
   }
 }
 

@@ -290,7 +290,8 @@ def match_tail(g, params, i: int) -> Fused | None:
     if y in g.outputs or g.tensors[y].external or any(y in n.inputs for j, n in enumerate(nodes) if j != i + 1):
         return None
     sh = g.shape(y)
-    if len(sh) != 4 or sh[1] * sh[2] > 64 or g.shape(c3.inputs[1]) != sh:
+    # (>= 2 pixels: the fp32 channel means must fit the block output's bf16 buffer they are written to)
+    if len(sh) != 4 or not 2 <= sh[1] * sh[2] <= 64 or g.shape(c3.inputs[1]) != sh:
         return None
     return Fused("tail", i, i + 1, [c3], reader=i + 1)
 
@@ -447,6 +448,8 @@ def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
             continue
         if any(s2 != s and f2.consumer == k for s2, f2 in seams.items()):
             continue  # (a seam consumer: handled below)
+        if not kconv_launchable(h, w, c, 2):
+            continue
         out[k] = Fused("kconv", k, k + 1, [n], seam=None, next_seam=s, reader=None, preset=k - 1)
     for s, f in seams.items():
         k = f.consumer
@@ -458,6 +461,8 @@ def match_kconvs(g, params, seams: dict, covered: set = frozenset()) -> dict:
             if pk is None or not _geom(pk, c, c, 3, 2, 1) or c != 512 or (h + 2) * (w + 2) > 256:
                 continue
         elif pk is None or not _geom(pk, c, c, 3, 1, 1) or c not in (256, 512) or h * w > (196 if c == 256 else 64):
+            continue
+        if not kconv_launchable(h, w, c, pk.stride):
             continue
         if k + 1 >= len(g.nodes):
             continue
@@ -563,6 +568,24 @@ def seam_params(g, params, f: Fused, addr, fused: dict | None = None) -> SeamPar
         p.zinit, p.zbias = addr(kcv.outputs[0]), params[kcv.attrs["w"]].bias.data_ptr()
         p.z_C, p.z_HW = kcout, kh * kw_
     return p
+
+
+def kconv_launchable(h: int, w: int, c: int, stride: int) -> bool:
+    """The geometry ``hz_kconv_launch`` (csrc/block.hip) accepts, mirrored on the host so a graph at
+    another image size binds its 3x3 convs per conv instead of failing at the first replay: an
+    output of 7 (14 x 14) or 2 (<= 64 px) 32-pixel groups, a channel slice the kernel is
+    instantiated for at that group count, and the padded input within the kernel's LDS image."""
+    st = 2 if stride == 2 else 1
+    if st == 2 and (h % 2 or w % 2):
+        return False
+    pg = ((h // st) * (w // st) + 31) // 32
+    ck = kconv_ck(c, st)
+    if c % 32 or ck <= 0 or c % ck:
+        return False
+    if not ((pg == 7 and ck in (32, 64)) or (pg == 2 and ck in (64, 128))):
+        return False
+    npmax = (256 if pg == 7 else 100) if st == 1 else (900 if pg == 7 else 256)
+    return (h + 2) * (w + 2) <= npmax
 
 
 def kconv_ck(c: int, stride: int = 1) -> int:

@@ -144,7 +144,7 @@ class ImageTransformerAdapter(VisionAdapter):
         with torch.device("meta"):
             m = make_model(num_labels or num_classes or self.num_classes,
                            **_hf_arch(arch, patch="patch_size", image="image_size"))
-        return pack_vit(m.state_dict(), "meta", weights=self.weights)
+        return pack_vit(m.state_dict(), "meta", weights=self.weights, patch_lowering=arch.get("patch_lowering"))
 
     def build_graph(self, batch=1, **kw):
         from .vit import build_graph

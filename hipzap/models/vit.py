@@ -26,10 +26,15 @@ from ..ops.conv import pack_conv
 from ._tx import TxBuilder, norm, pack_linear_padded, pack_qkv
 
 
-def _patch_conv() -> bool:
-    """HIPZAP_VIT_PATCH=conv: the patch embedding as the implicit-GEMM conv over 8-channel padded
-    pixels (rounds 1-5) instead of patchify + row-major GEMM; for A/B runs."""
-    return os.environ.get("HIPZAP_VIT_PATCH", "gemm") == "conv"
+def _patch_lowering(patch: int = 16, image: int = 224) -> str:
+    """How the patch embedding lowers: "gemm" (patchify + a row-major GEMM; the patchify kernel is
+    built for 16 x 16 patches tiling the image) or "conv" (the implicit-GEMM conv over 8-channel
+    padded pixels, rounds 1-5: any patch size). HIPZAP_VIT_PATCH=conv forces the conv (A/B runs).
+    Chosen ONCE at pack time and recorded in the packed config (``patch_lowering``), which the
+    graph builder follows, so packed weights and the graph cannot disagree."""
+    if os.environ.get("HIPZAP_VIT_PATCH", "gemm") == "conv" or patch != 16 or image % patch:
+        return "conv"
+    return "gemm"
 
 
 def make_model(num_labels: int = 1000, **cfg):
@@ -65,12 +70,15 @@ def config_from_sd(sd: dict) -> dict:
             "ffn": sd[f"{fc1}.weight"].shape[0], "num_labels": sd["classifier.weight"].shape[0]}
 
 
-def pack_vit(sd: dict, device="cpu", eps: float = 1e-12, weights: str = "bf16") -> tuple[dict, dict]:
+def pack_vit(sd: dict, device="cpu", eps: float = 1e-12, weights: str = "bf16",
+             patch_lowering: str | None = None) -> tuple[dict, dict]:
+    """``patch_lowering``: the source rank's choice (broadcast metadata); default: decided here."""
     sd = {k: v.to(device) for k, v in sd.items()}
     cfg = config_from_sd(sd)
     pw = sd["vit.embeddings.patch_embeddings.projection.weight"]
     pb = sd["vit.embeddings.patch_embeddings.projection.bias"]
-    P = {"patch": (pack_conv(pw, pb, None, stride=cfg["patch"], pad=0, cin_pad=8) if _patch_conv()
+    cfg["patch_lowering"] = patch_lowering or _patch_lowering(cfg["patch"], cfg["image"])
+    P = {"patch": (pack_conv(pw, pb, None, stride=cfg["patch"], pad=0, cin_pad=8) if cfg["patch_lowering"] == "conv"
                    else pack_linear_padded(pw.reshape(pw.shape[0], -1), pb)),
          "cls_token": sd["vit.embeddings.cls_token"].reshape(-1).to(torch.bfloat16).contiguous(),
          "pos": sd["vit.embeddings.position_embeddings"].reshape(-1, cfg["hidden"]).to(torch.bfloat16).contiguous(),
@@ -93,7 +101,8 @@ def pack_vit(sd: dict, device="cpu", eps: float = 1e-12, weights: str = "bf16") 
 
 
 def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
-                patch: int = 16, image: int = 224, num_labels: int = 1000, weights: str = "bf16", **_) -> Graph:
+                patch: int = 16, image: int = 224, num_labels: int = 1000, weights: str = "bf16",
+                patch_lowering: str | None = None, **_) -> Graph:
     B, D = batch, hidden
     n_side = image // patch
     npch = n_side * n_side
@@ -102,7 +111,7 @@ def build_graph(batch: int, layers: int = 12, hidden: int = 768, heads: int = 12
     x_in = g.tensor((B, 3, image, image), torch.float32, "input", external=True)
     g.inputs.append(x_in)
     tb = TxBuilder(g)
-    if _patch_conv():  # the round-1..5 lowering (A/B only)
+    if (patch_lowering or _patch_lowering(patch, image)) == "conv":  # any patch size; the A/B lowering
         nhwc = g.tensor((B, image, image, 8), name="nhwc")
         g.add("preprocess", [x_in], [nhwc], mean=None, std=None)
         patches = g.tensor((B * npch, D), torch.bfloat16, "patches")

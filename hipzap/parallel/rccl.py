@@ -183,6 +183,14 @@ class RcclComm(Comm):
             kind = "timeout" if rc == TIMEOUT else "aborted" if rc == ABORTED else f"error {rc}"
             raise CommError(f"rank {self.rank}: {what} {kind}: {lib().hz_comm_last_error().decode()}")
 
+    def comm_rank(self) -> int:
+        """This member's rank as RCCL reports it (ncclCommUserRank)."""
+        return int(lib().hz_comm_rank(self._h))
+
+    def comm_size(self) -> int:
+        """The communicator's size as RCCL reports it (ncclCommCount)."""
+        return int(lib().hz_comm_size(self._h))
+
     @property
     def stream(self) -> int:
         return lib().hz_comm_stream(self._h)

@@ -30,11 +30,14 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
-def logits_match(a, b, rel: float = 2e-2) -> bool:
-    """Two runs of the same ResNet program agree: bitwise when it is deterministic; with the default
-    layer3/layer4 seams and K-split 3x3 convs (float atomics: the summation order varies run to run,
-    engine/fusion.py) to within fp32/bf16 rounding -- max |a - b| / max |b| < ``rel`` and the same
-    argmax per row. Accepts torch tensors, numpy arrays, lists or raw float32 bytes."""
+def logits_match(a, b, rel: float = 1e-4) -> bool:
+    """Two runs of the same ResNet program agree. Every program is deterministic now (the seam /
+    K-split float atomics add terms on a fixed 2^-13 grid, csrc/common.h hz_fixq, so their sums do
+    not depend on arrival order; tests/test_determinism_gpu.py checks bitwise replays), so this is
+    bitwise in practice; the tolerance (max |a - b| / max |b| < ``rel``, 1e-4 = fp32-rounding level,
+    ADVICE r5) only keeps a comparison of two differently tiled programs meaningful, and it is far
+    below what a stale accumulator preset or a race would produce. Also the same argmax per row.
+    Accepts torch tensors, numpy arrays, lists or raw float32 bytes."""
     import numpy as np
 
     def arr(x):

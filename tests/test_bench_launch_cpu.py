@@ -28,6 +28,20 @@ def test_self_launch_spawns_n_ranks():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # only rank 0 reports
     assert lines[0]["n_gpus"] == 3 and lines[0]["ranks_seen"] == 3 and lines[0]["self_launched"]
+    # the launcher spawned its ranks without mapping the HIP runtime (it never imports torch)
+    assert lines[0]["launcher_hip_mapped"] == "0"
+
+
+def test_launcher_path_imports_no_torch():
+    """bench.py's N-rank launcher decision and GPU count run before (and without) ``import torch``:
+    torch maps libamdhip64, and the launcher must not hold the HIP runtime while its ranks run."""
+    code = ("import sys, runpy; sys.argv = ['bench.py', '--gpus', '2']; import bench, os; "
+            "from hipzap.utils.gpucount import hip_mapped, visible_gpu_count; "
+            "bench.check_gpus.__globals__; print('torch' in sys.modules, hip_mapped())")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env=_env())
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["False", "False"]
 
 
 def test_torchrun_world_mismatch_fails_loudly():

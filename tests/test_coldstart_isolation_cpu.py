@@ -8,11 +8,30 @@ def test_isolates_to_one_physical_gpu():
 
 
 def test_respects_launcher_visibility_and_opt_out():
-    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        env = {k: "2,3"}
-        assert isolated_env(env, 1) == (env, 1)
+    env = {"ROCR_VISIBLE_DEVICES": "2,3"}  # already narrowed at the ROCr level: left alone
+    assert isolated_env(env, 1) == (env, 1)
     env = {"HIPZAP_COLD_ISOLATE": "0"}
     assert isolated_env(env, 4) == (env, 4)
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):  # round-5 behaviour on request
+        env = {k: "2,3", "HIPZAP_COLD_NARROW": "0"}
+        assert isolated_env(env, 1) == (env, 1)
+
+
+def test_a_hip_level_list_is_narrowed_at_the_rocr_level():
+    """A launcher that sets only HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES leaves ROCr opening
+    every agent it can see; the one-GPU child gets ROCR_VISIBLE_DEVICES=<physical index> and
+    HIP_VISIBLE_DEVICES=0 (VERDICT r5 next #2c)."""
+    from hipzap.coldstart import narrow_env
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"):
+        env, dev = isolated_env({k: "2,3", "PATH": "/bin"}, 1)
+        assert dev == 0 and env["ROCR_VISIBLE_DEVICES"] == "3" and env["HIP_VISIBLE_DEVICES"] == "0"
+        assert env["PATH"] == "/bin" and (k == "HIP_VISIBLE_DEVICES" or k not in env)
+    assert narrow_env({"HIP_VISIBLE_DEVICES": "4"}, 0)[2] == "rocr_from_hip_visible_devices"
+    assert narrow_env({}, 2)[:2] == ({"ROCR_VISIBLE_DEVICES": "2"}, 0)
+    # an index the list does not have, a UUID entry, or two disagreeing lists: unchanged
+    for env, d in (({"HIP_VISIBLE_DEVICES": "0"}, 3), ({"HIP_VISIBLE_DEVICES": "GPU-abc"}, 0),
+                   ({"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "0"}, 0)):
+        assert narrow_env(env, d) == (env, d, "unchanged")
 
 
 def test_interleaved_cold_start_alternates_and_drops_failed_routes(monkeypatch):

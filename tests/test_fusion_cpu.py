@@ -337,3 +337,53 @@ def test_round5_launchers_refuse_malformed_params_before_any_hip_call():
         return lib.hz_launch_kernel(T.K_QKVATT, C.byref(p), None)
 
     assert qa(L=129) != 0 and qa(D=700) != 0 and qa(ksteps=23) != 0 and qa(ldx=770) != 0 and qa(w=None) != 0
+
+
+@pytest.mark.parametrize("image", [112, 128, 160, 192, 224, 288])
+def test_kconv_and_tail_only_bind_geometries_the_launchers_accept(r50, image):
+    """at another image size the default fusion set must not bind a K-split 3x3 conv the
+    launcher refuses (pixel-group counts other than 7 / 2, a channel slice the kernel has no
+    instantiation for, a padded image over its LDS bound) nor a pooling tail over a 1-pixel map
+    (whose fp32 means would overrun the block output's bf16 buffer); those runs bind per conv."""
+    from hipzap.models.resnet import build_graph
+    a, params, kw = r50
+    g = build_graph("resnet50", 1, 1000, image, True)
+    fz = fusion.plan(g, params, fusion.enabled_kinds(fusion.DEFAULT))
+    for f in fz.values():
+        if f.kind == "kconv":
+            n = f.nodes[0]
+            _, h, w, c = g.shape(n.inputs[0])
+            assert fusion.kconv_launchable(h, w, c, params[n.attrs["w"]].stride), (image, n.attrs["name"])
+        if f.kind == "tail":
+            _, h, w, _ = g.shape(f.nodes[0].outputs[0])
+            assert 2 <= h * w <= 64
+    if image == 224:  # the served geometry keeps every fused launch
+        assert sum(f.kind == "kconv" for f in fz.values()) == 9
+    if image in (160, 192):  # layer3 at 10x10 / 12x12: pixel-group counts 4 / 5 -> per-conv 3x3s
+        assert not any(f.kind == "kconv" and g.shape(f.nodes[0].inputs[0])[3] == 256 and
+                       params[f.nodes[0].attrs["w"]].stride == 1 for f in fz.values())
+
+
+def test_kconv_launchable_mirrors_the_launcher_refusals():
+    """Every geometry the host predicate rejects is refused by hz_kconv_launch before any HIP call
+    (so the predicate is never looser than the launcher's own checks)."""
+    import ctypes as C
+    from hipzap import _native as N
+    lib = N.lib()
+    fake = 1 << 20
+    for c in (256, 512):
+        for stride in (1, 2):
+            for h in range(4, 31, 2):
+                if fusion.kconv_launchable(h, h, c, stride):
+                    continue
+                p = fusion.KconvParams(x=fake, w=fake, out=fake, N=1, H=h, W=h, C=c, Cout=c,
+                                       ck=fusion.kconv_ck(c, stride), stride=stride)
+                assert lib.hz_kconv_launch(C.byref(p), None) < 0, (c, stride, h)
+
+
+def test_tail_refuses_a_one_pixel_map():
+    import ctypes as C
+    from hipzap import _native as N
+    fake = 1 << 20
+    p = fusion.SeamParams(t2=fake, w3=fake, b3=fake, res=fake, y=fake, N=1, HW=1, CM=512, cs=64, tail=1)
+    assert N.lib().hz_seam_launch(C.byref(p), None) == -1

@@ -21,19 +21,29 @@ import torch
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NDEV = torch.cuda.device_count()  # does not initialise HIP on this image
-WORLD = min(NDEV, 4)
+WORLD = NDEV  # the whole node (8 on an MI355X node): what the driver's scaling run will use
 multi = pytest.mark.skipif(NDEV < 2, reason=f"needs >= 2 GPUs (this box has {NDEV})")
 
 
 def _run_ranks(mode: str, world: int, timeout: float = 240.0) -> list:
+    """One fresh process per rank; each rank's stdout / stderr go to its own file (a rank blocked
+    on a full pipe while the test waits on another rank would deadlock the collective)."""
+    import time
     rdzv = tempfile.mkdtemp(prefix="hz_selftest_")
+    files = [(open(os.path.join(rdzv, f"r{r}.out"), "w+"), open(os.path.join(rdzv, f"r{r}.err"), "w+"))
+             for r in range(world)]
     procs = [subprocess.Popen([sys.executable, "-m", "hipzap.parallel.selftest", "--mode", mode, "--rank", str(r),
-                               "--world", str(world), "--rdzv", rdzv], cwd=ROOT, stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+                               "--world", str(world), "--rdzv", rdzv], cwd=ROOT, stdout=fo, stderr=fe, text=True)
+             for r, (fo, fe) in enumerate(files)]
     outs = []
     try:
-        for r, p in enumerate(procs):
-            so, se = p.communicate(timeout=timeout)
+        deadline = time.time() + timeout
+        for p in procs:  # every rank runs concurrently; wait for all within one deadline
+            p.wait(timeout=max(1.0, deadline - time.time()))
+        for r, (p, (fo, fe)) in enumerate(zip(procs, files)):
+            fo.seek(0)
+            fe.seek(0)
+            so, se = fo.read(), fe.read()
             lines = [ln for ln in so.splitlines() if ln.startswith("{")]
             assert lines, f"rank {r} printed nothing (rc {p.returncode}): {se[-3000:]}"
             outs.append(json.loads(lines[-1]))
@@ -41,6 +51,10 @@ def _run_ranks(mode: str, world: int, timeout: float = 240.0) -> list:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+                p.wait()
+        for fo, fe in files:
+            fo.close()
+            fe.close()
     return outs
 
 
