@@ -560,34 +560,43 @@ __device__ __forceinline__ int b2_t1(int hy, int hx) { return (hy * kB2T1Row + h
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// NI (batched programs): one workgroup owns the same 4 x 4 tile of NI consecutive images and
+// multiplies every streamed weight fragment by all NI images' operands, so the 544 KB stream is paid
+// once per NI images (bs >= 2: config 3 shards, dynamic-batching replays). Per image the arithmetic
+// and its order are those of NI = 1, so the outputs are bitwise the same.
+template <int NI>
 __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
   constexpr int XCH = kB2CI / 8, NQ = kB2NP * XCH, NL = (NQ + 511) / 512;
-  __shared__ __attribute__((aligned(16))) bf16_t X[16 * kB2NF1 * kB2CI];          // 48 pixel slots
-  __shared__ __attribute__((aligned(16))) bf16_t T1[(5 * kB2T1Row + 6) * kB2T1Pix];
-  __shared__ __attribute__((aligned(16))) bf16_t T2[16 * kB2CM];
+  constexpr int XSZ = 16 * kB2NF1 * kB2CI, T1SZ = (5 * kB2T1Row + 6) * kB2T1Pix, T2SZ = 16 * kB2CM;
+  __shared__ __attribute__((aligned(16))) bf16_t X[NI * XSZ];          // 48 pixel slots per image
+  __shared__ __attribute__((aligned(16))) bf16_t T1[NI * T1SZ];
+  __shared__ __attribute__((aligned(16))) bf16_t T2[NI * T2SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
   const int tx_n = p.W / kB2T, ty_n = p.H / kB2T, per_img = tx_n * ty_n;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int n = b / per_img, rem = b - n * per_img;
+  const int n0 = (b / per_img) * NI, rem = b - (b / per_img) * per_img;
   const int ty = rem / tx_n, tx = rem - ty * tx_n;
   const int y0 = ty * kB2T, x0 = tx * kB2T;
   HZ_BSTAMP_DECL
   HZ_BSTAMP(0);
-  // ---- input patch loads (6 x 6 x 512, zero outside the image) ----
-  u32x4 xv[NL];
+  // ---- input patch loads (6 x 6 x 512 per image, zero outside the image) ----
+  u32x4 xv[NI][NL];
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int q = tid + 512 * i;
-    xv[i] = u32x4{0u, 0u, 0u, 0u};
-    if (q < NQ) {
-      const int sub = q & 3, pc = q >> 2;
-      const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
-      const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
-      const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
-      if ((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)
-        xv[i] = *reinterpret_cast<const u32x4*>(p.x + ((((long)n * (kB2CI / 32) + cb) * p.H + gy) * p.W + gx) * 32 + sub * 8);
+  for (int m = 0; m < NI; ++m)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      xv[m][i] = u32x4{0u, 0u, 0u, 0u};
+      if (q < NQ) {
+        const int sub = q & 3, pc = q >> 2;
+        const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
+        const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
+        const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+        if ((unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W)
+          xv[m][i] = *reinterpret_cast<const u32x4*>(
+              p.x + ((((long)(n0 + m) * (kB2CI / 32) + cb) * p.H + gy) * p.W + gx) * 32 + sub * 8);
+      }
     }
-  }
   // ---- folded-BN biases ----
   const f32x4 bias1 = *reinterpret_cast<const f32x4*>(p.b1 + 16 * wave + 4 * g);
   const f32x4 bias2 = *reinterpret_cast<const f32x4*>(p.b2 + 16 * wave + 4 * g);
@@ -610,43 +619,54 @@ __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
 #pragma unroll
   for (int i = 0; i < kB2D; ++i) fetch(i);
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int q = tid + 512 * i;
-    if (q < NQ) {
-      const int sub = q & 3, pc = q >> 2;
-      const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
-      *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
+  for (int m = 0; m < NI; ++m)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      if (q < NQ) {
+        const int sub = q & 3, pc = q >> 2;
+        const int cb = pc / kB2NP, pp = pc - cb * kB2NP;
+        *reinterpret_cast<u32x4*>(X + m * XSZ + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[m][i];
+      }
     }
-  }
   lds_sync();
   HZ_BSTAMP(1);
   // ---- conv1 (1x1, 512 -> 128) over the 36 halo pixels (3 fragments; slots 36..47 are computed
   // from unwritten LDS and discarded) ----
   {
-    f32x4 acc[kB2NF1];
+    f32x4 acc[NI][kB2NF1];
 #pragma unroll
-    for (int f = 0; f < kB2NF1; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < NI; ++m)
+#pragma unroll
+      for (int f = 0; f < kB2NF1; ++f) acc[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kB2KS1; ++s) {
-      bf16x8 bv[kB2NF1];
+      bf16x8 bv[NI][kB2NF1];
 #pragma unroll
-      for (int f = 0; f < kB2NF1; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+      for (int m = 0; m < NI; ++m)
 #pragma unroll
-      for (int f = 0; f < kB2NF1; ++f) acc[f] = mfma16(wr[s], bv[f], acc[f]);
+        for (int f = 0; f < kB2NF1; ++f)
+          bv[m][f] = *reinterpret_cast<const bf16x8*>(X + m * XSZ + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+#pragma unroll
+      for (int m = 0; m < NI; ++m)
+#pragma unroll
+        for (int f = 0; f < kB2NF1; ++f) acc[m][f] = mfma16(wr[s], bv[m][f], acc[m][f]);
       consumed(s);
     }
     const int ch = 16 * wave + 4 * g;
 #pragma unroll
-    for (int f = 0; f < kB2NF1; ++f) {
-      const int pp = 16 * f + l16;
-      if (pp >= kB2NP) continue;
-      const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
-      const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)p.H && (unsigned)(x0 - 1 + hx) < (unsigned)p.W;
-      float v[4];
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[f][e] + bias1[e], 0.f) : 0.f;  // conv2's zero padding
-      *reinterpret_cast<u32x2*>(T1 + b2_t1(hy, hx) + ch) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
+      for (int f = 0; f < kB2NF1; ++f) {
+        const int pp = 16 * f + l16;
+        if (pp >= kB2NP) continue;
+        const int hy = pp / kB2HW, hx = pp - hy * kB2HW;
+        const bool in = (unsigned)(y0 - 1 + hy) < (unsigned)p.H && (unsigned)(x0 - 1 + hx) < (unsigned)p.W;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[m][f][e] + bias1[e], 0.f) : 0.f;  // conv2's zero padding
+        *reinterpret_cast<u32x2*>(T1 + m * T1SZ + b2_t1(hy, hx) + ch) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
   }
   lds_sync();
   HZ_BSTAMP(2);
@@ -654,19 +674,28 @@ __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
   // quarter ks % 4; the tap offset is an immediate ----
   {
     const int j = l16, base = b2_t1(j >> 2, j & 3) + 8 * g;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[NI];
+#pragma unroll
+    for (int m = 0; m < NI; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < kB2KS2; ++ks) {
       const int tap = ks >> 2, r = tap / 3, c = tap % 3;
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + base + b2_t1(r, c) + (ks & 3) * 32);
-      acc = mfma16(wr[kB2KS1 + ks], bv, acc);
+#pragma unroll
+      for (int m = 0; m < NI; ++m) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + m * T1SZ + base + b2_t1(r, c) + (ks & 3) * 32);
+        acc[m] = mfma16(wr[kB2KS1 + ks], bv, acc[m]);
+      }
       consumed(kB2KS1 + ks);
     }
     const int ch = 16 * wave + 4 * g;
-    float v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[e] + bias2[e], 0.f);
-    *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    for (int m = 0; m < NI; ++m) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[m][e] + bias2[e], 0.f);
+      *reinterpret_cast<u32x2*>(T2 + m * T2SZ + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) =
+          u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
   }
   lds_sync();
   HZ_BSTAMP(3);
@@ -674,37 +703,49 @@ __global__ __launch_bounds__(512) void bneck2_kernel(const HzBneckParams p) {
   // output fragments 4w .. 4w+3 ----
   {
     const int j = l16, jy = j >> 2, jx = j & 3, cp = (jy + 1) * kB2HW + jx + 1;
-    bf16x8 b3[kB2KS3];
+    bf16x8 b3[NI][kB2KS3];
 #pragma unroll
-    for (int s = 0; s < kB2KS3; ++s) b3[s] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 16) * 8);
-    u32x2 rr[4];
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ch = 16 * (4 * wave + i) + 4 * g;
-      rr[i] = *reinterpret_cast<const u32x2*>(X + x_chunk(cp, ch >> 3, XCH) * 8 + (ch & 4));
-    }
-    f32x4 acc[4];
+      for (int s = 0; s < kB2KS3; ++s)
+        b3[m][s] = *reinterpret_cast<const bf16x8*>(T2 + m * T2SZ + x_chunk(j, 4 * s + g, 16) * 8);
+    u32x2 rr[NI][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = bias3[i];
+    for (int m = 0; m < NI; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ch = 16 * (4 * wave + i) + 4 * g;
+        rr[m][i] = *reinterpret_cast<const u32x2*>(X + m * XSZ + x_chunk(cp, ch >> 3, XCH) * 8 + (ch & 4));
+      }
+    f32x4 acc[NI][4];
+#pragma unroll
+    for (int m = 0; m < NI; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[m][i] = bias3[i];
 #pragma unroll
     for (int s = 0; s < kB2KS3; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        acc[i] = mfma16(wr[kB2KS1 + kB2KS2 + 4 * s + i], b3[s], acc[i]);
+#pragma unroll
+        for (int m = 0; m < NI; ++m) acc[m][i] = mfma16(wr[kB2KS1 + kB2KS2 + 4 * s + i], b3[m][s], acc[m][i]);
         consumed(kB2KS1 + kB2KS2 + 4 * s + i);
       }
     HZ_BSTAMP(4);
     const int CO32 = kB2CO / 32;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ch = 16 * (4 * wave + i) + 4 * g;
-      float v[4] = {acc[i][0] + __uint_as_float(rr[i][0] << 16), acc[i][1] + __uint_as_float(rr[i][0] & 0xffff0000u),
-                    acc[i][2] + __uint_as_float(rr[i][1] << 16), acc[i][3] + __uint_as_float(rr[i][1] & 0xffff0000u)};
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      const long o = ((((long)n * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
-      *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int ch = 16 * (4 * wave + i) + 4 * g;
+        float v[4] = {acc[m][i][0] + __uint_as_float(rr[m][i][0] << 16),
+                      acc[m][i][1] + __uint_as_float(rr[m][i][0] & 0xffff0000u),
+                      acc[m][i][2] + __uint_as_float(rr[m][i][1] << 16),
+                      acc[m][i][3] + __uint_as_float(rr[m][i][1] & 0xffff0000u)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        const long o = ((((long)(n0 + m) * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
+        *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
   }
   HZ_BSTAMP(5);
   HZ_BSTAMP_FLUSH(3);
@@ -727,35 +768,40 @@ __device__ __forceinline__ int b2d_t1(int hy, int hx, int chunk) {
   return (hy * kB2dRow + hx) * kB2dPix + ((chunk ^ (hx & 15)) << 3);
 }
 
+template <int NI>  // images per workgroup, as bneck2_kernel
 __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
   constexpr int XCH = kB2dCI / 8, NQ = kB2dNP * XCH, NL = (NQ + 511) / 512;
-  __shared__ __attribute__((aligned(16))) bf16_t X[16 * kB2dNF1 * kB2dCI];        // 96 pixel slots
-  __shared__ __attribute__((aligned(16))) bf16_t T1[(8 * kB2dRow + 9) * kB2dPix];
-  __shared__ __attribute__((aligned(16))) bf16_t T2[16 * kB2CM];
+  constexpr int XSZ = 16 * kB2dNF1 * kB2dCI, T1SZ = (8 * kB2dRow + 9) * kB2dPix, T2SZ = 16 * kB2CM;
+  __shared__ __attribute__((aligned(16))) bf16_t X[NI * XSZ];        // 96 pixel slots per image
+  __shared__ __attribute__((aligned(16))) bf16_t T1[NI * T1SZ];
+  __shared__ __attribute__((aligned(16))) bf16_t T2[NI * T2SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
   const int tx_n = p.W / kB2T, ty_n = p.H / kB2T, per_img = tx_n * ty_n;  // OUTPUT geometry (28 x 28)
   const int IH = 2 * p.H, IW = 2 * p.W;                                   // input 56 x 56
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int n = b / per_img, rem = b - n * per_img;
+  const int n0 = (b / per_img) * NI, rem = b - (b / per_img) * per_img;
   const int ty = rem / tx_n, tx = rem - ty * tx_n;
   const int y0 = ty * kB2T, x0 = tx * kB2T;
   const int iy0 = 2 * y0 - 1, ix0 = 2 * x0 - 1;  // halo origin in the input
   HZ_BSTAMP_DECL
   HZ_BSTAMP(0);
-  u32x4 xv[NL];
+  u32x4 xv[NI][NL];
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int q = tid + 512 * i;
-    xv[i] = u32x4{0u, 0u, 0u, 0u};
-    if (q < NQ) {
-      const int sub = q & 3, pc = q >> 2;
-      const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
-      const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
-      const int gy = iy0 + hy, gx = ix0 + hx;
-      if ((unsigned)gy < (unsigned)IH && (unsigned)gx < (unsigned)IW)
-        xv[i] = *reinterpret_cast<const u32x4*>(p.x + ((((long)n * (kB2dCI / 32) + cb) * IH + gy) * IW + gx) * 32 + sub * 8);
+  for (int m = 0; m < NI; ++m)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      xv[m][i] = u32x4{0u, 0u, 0u, 0u};
+      if (q < NQ) {
+        const int sub = q & 3, pc = q >> 2;
+        const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
+        const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
+        const int gy = iy0 + hy, gx = ix0 + hx;
+        if ((unsigned)gy < (unsigned)IH && (unsigned)gx < (unsigned)IW)
+          xv[m][i] = *reinterpret_cast<const u32x4*>(
+              p.x + ((((long)(n0 + m) * (kB2dCI / 32) + cb) * IH + gy) * IW + gx) * 32 + sub * 8);
+      }
     }
-  }
   const f32x4 bias1 = *reinterpret_cast<const f32x4*>(p.b1 + 16 * wave + 4 * g);
   const f32x4 bias2 = *reinterpret_cast<const f32x4*>(p.b2 + 16 * wave + 4 * g);
   f32x4 bias3[4];
@@ -777,100 +823,138 @@ __global__ __launch_bounds__(512) void bneck2d_kernel(const HzBneckParams p) {
 #pragma unroll
   for (int i = 0; i < kB2D; ++i) fetch(i);
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int q = tid + 512 * i;
-    if (q < NQ) {
-      const int sub = q & 3, pc = q >> 2;
-      const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
-      *reinterpret_cast<u32x4*>(X + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[i];
+  for (int m = 0; m < NI; ++m)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int q = tid + 512 * i;
+      if (q < NQ) {
+        const int sub = q & 3, pc = q >> 2;
+        const int cb = pc / kB2dNP, pp = pc - cb * kB2dNP;
+        *reinterpret_cast<u32x4*>(X + m * XSZ + x_chunk(pp, cb * 4 + sub, XCH) * 8) = xv[m][i];
+      }
     }
-  }
   lds_sync();
   HZ_BSTAMP(1);
   // ---- conv1 (1x1, 256 -> 128) over the 81 halo pixels ----
   {
-    f32x4 acc[kB2dNF1];
+    f32x4 acc[NI][kB2dNF1];
 #pragma unroll
-    for (int f = 0; f < kB2dNF1; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < NI; ++m)
+#pragma unroll
+      for (int f = 0; f < kB2dNF1; ++f) acc[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kB2dKS1; ++s) {
-      bf16x8 bv[kB2dNF1];
 #pragma unroll
-      for (int f = 0; f < kB2dNF1; ++f) bv[f] = *reinterpret_cast<const bf16x8*>(X + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+      for (int m = 0; m < NI; ++m) {
+        bf16x8 bv[kB2dNF1];
 #pragma unroll
-      for (int f = 0; f < kB2dNF1; ++f) acc[f] = mfma16(wr[s], bv[f], acc[f]);
+        for (int f = 0; f < kB2dNF1; ++f)
+          bv[f] = *reinterpret_cast<const bf16x8*>(X + m * XSZ + x_chunk(16 * f + l16, 4 * s + g, XCH) * 8);
+#pragma unroll
+        for (int f = 0; f < kB2dNF1; ++f) acc[m][f] = mfma16(wr[s], bv[f], acc[m][f]);
+      }
       consumed(s);
     }
     const int ch = 16 * wave + 4 * g;
 #pragma unroll
-    for (int f = 0; f < kB2dNF1; ++f) {
-      const int pp = 16 * f + l16;
-      if (pp >= kB2dNP) continue;
-      const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
-      const bool in = (unsigned)(iy0 + hy) < (unsigned)IH && (unsigned)(ix0 + hx) < (unsigned)IW;
-      float v[4];
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[f][e] + bias1[e], 0.f) : 0.f;
-      *reinterpret_cast<u32x2*>(T1 + b2d_t1(hy, hx, ch >> 3) + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
+      for (int f = 0; f < kB2dNF1; ++f) {
+        const int pp = 16 * f + l16;
+        if (pp >= kB2dNP) continue;
+        const int hy = pp / kB2dHW, hx = pp - hy * kB2dHW;
+        const bool in = (unsigned)(iy0 + hy) < (unsigned)IH && (unsigned)(ix0 + hx) < (unsigned)IW;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = in ? fmaxf(acc[m][f][e] + bias1[e], 0.f) : 0.f;
+        *reinterpret_cast<u32x2*>(T1 + m * T1SZ + b2d_t1(hy, hx, ch >> 3) + (ch & 4)) =
+            u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
   }
   lds_sync();
   HZ_BSTAMP(2);
   // ---- conv2 (3x3 stride 2, 128 -> 128): output (jy, jx) reads halo (2jy + r, 2jx + c) ----
   {
     const int j = l16, jy = j >> 2, jx = j & 3;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[NI];
+#pragma unroll
+    for (int m = 0; m < NI; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < kB2KS2; ++ks) {
       const int tap = ks >> 2, r = tap / 3, c = tap % 3;
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(T1 + b2d_t1(2 * jy + r, 2 * jx + c, 4 * (ks & 3) + g));
-      acc = mfma16(wr[O2 + ks], bv, acc);
+#pragma unroll
+      for (int m = 0; m < NI; ++m) {
+        const bf16x8 bv =
+            *reinterpret_cast<const bf16x8*>(T1 + m * T1SZ + b2d_t1(2 * jy + r, 2 * jx + c, 4 * (ks & 3) + g));
+        acc[m] = mfma16(wr[O2 + ks], bv, acc[m]);
+      }
       consumed(O2 + ks);
     }
     const int ch = 16 * wave + 4 * g;
-    float v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[e] + bias2[e], 0.f);
-    *reinterpret_cast<u32x2*>(T2 + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    for (int m = 0; m < NI; ++m) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[m][e] + bias2[e], 0.f);
+      *reinterpret_cast<u32x2*>(T2 + m * T2SZ + x_chunk(j, ch >> 3, 16) * 8 + (ch & 4)) =
+          u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
   }
   lds_sync();
   HZ_BSTAMP(3);
   // ---- conv3 (1x1, 128 -> 512) + downsample (1x1 stride 2, 256 -> 512) + ReLU ----
   {
     const int j = l16, jy = j >> 2, jx = j & 3, dp = (2 * jy + 1) * kB2dHW + 2 * jx + 1;
-    bf16x8 b3[kB2KS3], bd[kB2dKSD];
+    f32x4 acc[NI][4];
 #pragma unroll
-    for (int s = 0; s < kB2KS3; ++s) b3[s] = *reinterpret_cast<const bf16x8*>(T2 + x_chunk(j, 4 * s + g, 16) * 8);
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-    for (int s = 0; s < kB2dKSD; ++s) bd[s] = *reinterpret_cast<const bf16x8*>(X + x_chunk(dp, 4 * s + g, XCH) * 8);
-    f32x4 acc[4];
+      for (int i = 0; i < 4; ++i) acc[m][i] = bias3[i];
+    {
+      bf16x8 b3[NI][kB2KS3];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = bias3[i];
+      for (int m = 0; m < NI; ++m)
 #pragma unroll
-    for (int s = 0; s < kB2KS3; ++s)
+        for (int s = 0; s < kB2KS3; ++s)
+          b3[m][s] = *reinterpret_cast<const bf16x8*>(T2 + m * T2SZ + x_chunk(j, 4 * s + g, 16) * 8);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i] = mfma16(wr[O3 + 4 * s + i], b3[s], acc[i]);
-        consumed(O3 + 4 * s + i);
-      }
+      for (int s = 0; s < kB2KS3; ++s)
 #pragma unroll
-    for (int s = 0; s < kB2dKSD; ++s)
+        for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i] = mfma16(wr[OD + 4 * s + i], bd[s], acc[i]);
-        consumed(OD + 4 * s + i);
-      }
+          for (int m = 0; m < NI; ++m) acc[m][i] = mfma16(wr[O3 + 4 * s + i], b3[m][s], acc[m][i]);
+          consumed(O3 + 4 * s + i);
+        }
+    }
+    {
+      bf16x8 bd[NI][kB2dKSD];
+#pragma unroll
+      for (int m = 0; m < NI; ++m)
+#pragma unroll
+        for (int s = 0; s < kB2dKSD; ++s)
+          bd[m][s] = *reinterpret_cast<const bf16x8*>(X + m * XSZ + x_chunk(dp, 4 * s + g, XCH) * 8);
+#pragma unroll
+      for (int s = 0; s < kB2dKSD; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int m = 0; m < NI; ++m) acc[m][i] = mfma16(wr[OD + 4 * s + i], bd[m][s], acc[m][i]);
+          consumed(OD + 4 * s + i);
+        }
+    }
     HZ_BSTAMP(4);
     const int CO32 = kB2CO / 32;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ch = 16 * (4 * wave + i) + 4 * g;
-      float v[4];
+    for (int m = 0; m < NI; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[i][e], 0.f);
-      const long o = ((((long)n * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
-      *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int ch = 16 * (4 * wave + i) + 4 * g;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[m][i][e], 0.f);
+        const long o = ((((long)(n0 + m) * CO32 + (ch >> 5)) * p.H + y0 + jy) * p.W + x0 + jx) * 32 + (ch & 31);
+        *reinterpret_cast<u32x2*>(p.out + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
   }
   HZ_BSTAMP(5);
   HZ_BSTAMP_FLUSH(4);
@@ -1330,7 +1414,7 @@ extern "C" int hz_stem_launch(const HzStemParams* pp, hipStream_t st) {
   if (p.mode == 1 && ((long)p.H * p.W * 3) % 4) return -1;  // whole-dword image rows (see the kernel)
   if (p.mode == 1 && ((uintptr_t)p.src & 3)) return -1;
   const int tiles = ((p.PW + kStemPW - 1) / kStemPW) * ((p.PH + kStemPH - 1) / kStemPH) * p.N;
-  hipLaunchKernelGGL(stem_kernel, dim3(tiles), dim3(512), 0, st, p);
+  HZ_LAUNCH(stem_kernel, dim3(tiles), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -1340,18 +1424,27 @@ extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   if (p.N < 1 || p.H < 1 || p.W < 1) return -1;
   if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles (H, W: the block's OUTPUT size)
     if (p.N < 1 || p.Cout != kB2CO || p.H % kB2T || p.W % kB2T) return -1;
-    const dim3 grid((p.H / kB2T) * (p.W / kB2T) * p.N);
-    if (p.Cin == kB2CI && !p.wd) hipLaunchKernelGGL(bneck2_kernel, grid, dim3(512), 0, st, p);
-    else if (p.Cin == kB2dCI && p.wd && p.bd) hipLaunchKernelGGL(bneck2d_kernel, grid, dim3(512), 0, st, p);
-    else return -1;
+    // images per workgroup (HzBneckParams.imgs; auto: two when the batch is even; bitwise either way)
+    if (p.imgs < 0 || p.imgs > 2 || (p.imgs == 2 && p.N % 2)) return -1;
+    const int ni = p.imgs ? p.imgs : (p.N % 2 == 0 ? 2 : 1);
+    const dim3 grid((p.H / kB2T) * (p.W / kB2T) * (p.N / ni));
+    if (p.Cin == kB2CI && !p.wd) {
+      if (ni == 2) HZ_LAUNCH(bneck2_kernel<2>, grid, dim3(512), 0, st, p);
+      else HZ_LAUNCH(bneck2_kernel<1>, grid, dim3(512), 0, st, p);
+    } else if (p.Cin == kB2dCI && p.wd && p.bd) {
+      if (ni == 2) HZ_LAUNCH(bneck2d_kernel<2>, grid, dim3(512), 0, st, p);
+      else HZ_LAUNCH(bneck2d_kernel<1>, grid, dim3(512), 0, st, p);
+    } else {
+      return -1;
+    }
     return (int)hipGetLastError();
   }
   const int th = p.tile_h ? p.tile_h : 8;
   if (p.N < 1 || (th != 8 && th != 4) || p.H % th || p.W % kBnTW || p.Cmid != kBnCM || p.Cout != kBnCO) return -1;
   const int tiles = (p.H / th) * (p.W / kBnTW) * p.N;
 #define HZ_BNL(CIN, DS)                                                                               \
-  if (th == 8) hipLaunchKernelGGL((bneck_kernel<CIN, DS, 8>), dim3(tiles), dim3(512), 0, st, p);     \
-  else hipLaunchKernelGGL((bneck_kernel<CIN, DS, 4>), dim3(tiles), dim3(512), 0, st, p);
+  if (th == 8) HZ_LAUNCH((bneck_kernel<CIN, DS, 8>), dim3(tiles), dim3(512), 0, st, p);     \
+  else HZ_LAUNCH((bneck_kernel<CIN, DS, 4>), dim3(tiles), dim3(512), 0, st, p);
   if (p.Cin == 64 && p.wd && p.bd) {
     HZ_BNL(64, true)
   } else if (p.Cin == 256 && !p.wd) {
@@ -1373,8 +1466,8 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
     q.tiles = 1;
     const dim3 grid(p.N * (4 * p.CM / p.cs));
 #define HZ_TAIL(CS)                                                                                        \
-  if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<512, CS, true, true>), grid, dim3(512), 0, st, q);        \
-  else hipLaunchKernelGGL((seam_kernel<512, CS, false, true>), grid, dim3(512), 0, st, q);
+  if (p.t2_f32) HZ_LAUNCH((seam_kernel<512, CS, true, true>), grid, dim3(512), 0, st, q);        \
+  else HZ_LAUNCH((seam_kernel<512, CS, false, true>), grid, dim3(512), 0, st, q);
     if (p.cs == 128) { HZ_TAIL(128) }
     else { HZ_TAIL(64) }
 #undef HZ_TAIL
@@ -1390,26 +1483,26 @@ extern "C" int hz_seam_launch(const HzSeamParams* pp, hipStream_t st) {
     if (cn != p.CM || !p.t2_f32 || !p.xd || !p.wd || !p.bd || p.xd_H % 2 || p.xd_W % 2 ||
         (p.xd_H / 2) * (p.xd_W / 2) != p.HW)
       return -1;
-    if (p.CM == 512 && p.cs == 128) hipLaunchKernelGGL((seam_kernel<512, 128, true, false, 512, true>), grid, dim3(512), 0, st, q);
-    else if (p.CM == 512) hipLaunchKernelGGL((seam_kernel<512, 64, true, false, 512, true>), grid, dim3(512), 0, st, q);
-    else if (p.cs == 128) hipLaunchKernelGGL((seam_kernel<256, 128, true, false, 256, true>), grid, dim3(512), 0, st, q);
-    else hipLaunchKernelGGL((seam_kernel<256, 64, true, false, 256, true>), grid, dim3(512), 0, st, q);
+    if (p.CM == 512 && p.cs == 128) HZ_LAUNCH((seam_kernel<512, 128, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    else if (p.CM == 512) HZ_LAUNCH((seam_kernel<512, 64, true, false, 512, true>), grid, dim3(512), 0, st, q);
+    else if (p.cs == 128) HZ_LAUNCH((seam_kernel<256, 128, true, false, 256, true>), grid, dim3(512), 0, st, q);
+    else HZ_LAUNCH((seam_kernel<256, 64, true, false, 256, true>), grid, dim3(512), 0, st, q);
     return (int)hipGetLastError();
   }
   if (cn != p.CM) {  // the cross-stage seam: layer3's last conv3 + layer4's first conv1
     if (p.CM != 256 || cn != 512) return -1;
     if (p.cs == 128) {
-      if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<256, 128, true, false, 512>), grid, dim3(512), 0, st, q);
-      else hipLaunchKernelGGL((seam_kernel<256, 128, false, false, 512>), grid, dim3(512), 0, st, q);
+      if (p.t2_f32) HZ_LAUNCH((seam_kernel<256, 128, true, false, 512>), grid, dim3(512), 0, st, q);
+      else HZ_LAUNCH((seam_kernel<256, 128, false, false, 512>), grid, dim3(512), 0, st, q);
     } else {
-      if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<256, 64, true, false, 512>), grid, dim3(512), 0, st, q);
-      else hipLaunchKernelGGL((seam_kernel<256, 64, false, false, 512>), grid, dim3(512), 0, st, q);
+      if (p.t2_f32) HZ_LAUNCH((seam_kernel<256, 64, true, false, 512>), grid, dim3(512), 0, st, q);
+      else HZ_LAUNCH((seam_kernel<256, 64, false, false, 512>), grid, dim3(512), 0, st, q);
     }
     return (int)hipGetLastError();
   }
 #define HZ_SEAM(CM, CS)                                                                                    \
-  if (p.t2_f32) hipLaunchKernelGGL((seam_kernel<CM, CS, true>), grid, dim3(512), 0, st, q);               \
-  else hipLaunchKernelGGL((seam_kernel<CM, CS, false>), grid, dim3(512), 0, st, q);
+  if (p.t2_f32) HZ_LAUNCH((seam_kernel<CM, CS, true>), grid, dim3(512), 0, st, q);               \
+  else HZ_LAUNCH((seam_kernel<CM, CS, false>), grid, dim3(512), 0, st, q);
   if (p.CM == 256 && p.cs == 128) { HZ_SEAM(256, 128) }
   else if (p.CM == 256) { HZ_SEAM(256, 64) }
   else if (p.cs == 128) { HZ_SEAM(512, 128) }
@@ -1441,8 +1534,8 @@ extern "C" int hz_kconv_launch(const HzKconvParams* pp, hipStream_t st) {
     const size_t red = (8 / PG) > 1 ? (size_t)PG * (8 / PG) * 16 * 64 * 4 : 0;                       \
     const size_t lds0 = stage > red ? stage : red, lds = p.dso && lds0 < 4096 ? 4096 : lds0;        \
     if (lds > 160 * 1024) return -1;                                                                 \
-    if (st_ == 1) hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 1>), grid, dim3(512), lds, st, p);    \
-    else hipLaunchKernelGGL((kconv_kernel<CK, PG, XF, 2>), grid, dim3(512), lds, st, p);             \
+    if (st_ == 1) HZ_LAUNCH((kconv_kernel<CK, PG, XF, 1>), grid, dim3(512), lds, st, p);    \
+    else HZ_LAUNCH((kconv_kernel<CK, PG, XF, 2>), grid, dim3(512), lds, st, p);             \
   } while (0)
 #define HZ_KC_X(CK, PG)              \
   if (p.x_f32) HZ_KC(CK, PG, true);  \

@@ -3,6 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Exclusive-CU launches (A/B switch HIPZAP_EXCL_LDS=<bytes>, csrc/runtime.cpp hz_excl_pad): every
+// HZ_LAUNCH asks for at least that much LDS (static + dynamic), so two workgroups -- of this kernel
+// or of a concurrent request's -- never share a CU when it exceeds half of the 160 KiB. Off (0) by
+// default: the dynamic LDS argument is passed through unchanged.
+size_t hz_excl_pad(const void* fn, size_t dyn_lds);
+#define HZ_LAUNCH(K, GRID, BLOCK, LDS, ST, ...) \
+  hipLaunchKernelGGL(K, GRID, BLOCK, hz_excl_pad(reinterpret_cast<const void*>(&(K)), (LDS)), ST, __VA_ARGS__)
+
 typedef unsigned short bf16_t;                                   // storage type
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));       // MFMA A/B fragment (4 VGPR)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -68,11 +76,17 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // Deterministic cross-workgroup sums (the ResNet seam / K-split accumulators, csrc/block.hip): every
 // term added into such an accumulator -- the preset bias and each workgroup's partial -- is first
-// rounded to a multiple of 2^-13. While |sum| < 2^24 * 2^-13 = 2048 every partial sum of such terms is
-// exactly representable in fp32, so the memory-side float atomics give the same bits in any arrival
-// order (replays, stream counts, XCD placement). The rounding (<= 6.1e-5 per term) sits far below the
-// bf16 the consumer converts the sum to.
-__device__ __forceinline__ float hz_fixq(float x) { return __builtin_rintf(x * 8192.f) * (1.f / 8192.f); }
+// rounded to a multiple of 2^-10. While |sum| < 2^24 * 2^-10 = 16384 every partial sum of such terms
+// is exactly representable in fp32, so the memory-side float atomics give the same bits in any
+// arrival order (replays, stream counts, XCD placement). 16384 leaves 2x headroom over the largest
+// accumulator of the random-init benchmark model (7,520 in layer4; trained ResNets stay in the tens);
+// the rounding (<= 4.9e-4 per term) sits below the bf16 the consumer converts the sum to for the
+// activations that matter (|x| >~ 0.1).
+#ifdef HZ_NO_FIXQ  // (A/B build only: HIPZAP_CFLAGS=-DHZ_NO_FIXQ python -m hipzap.build --experiments)
+__device__ __forceinline__ float hz_fixq(float x) { return x; }
+#else
+__device__ __forceinline__ float hz_fixq(float x) { return __builtin_rintf(x * 1024.f) * (1.f / 1024.f); }
+#endif
 __device__ __forceinline__ f32x4 hz_fixq4(f32x4 v) {
   return f32x4{hz_fixq(v[0]), hz_fixq(v[1]), hz_fixq(v[2]), hz_fixq(v[3])};
 }

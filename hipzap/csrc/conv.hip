@@ -418,9 +418,9 @@ int launch2(const HzConvParams& a, const HzConvParams& b, hipStream_t st) {
   const bool fast = (a.C % 32) == 0 && (b.C % 32) == 0;
   dim3 grid(t0 + t1), block(64 * kw);
   const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
-  if (fast && one(a) && one(b)) hipLaunchKernelGGL((conv2_kernel<FC, FP, true, true>), grid, block, lds, st, q0, q1, t0);
-  else if (fast) hipLaunchKernelGGL((conv2_kernel<FC, FP, true, false>), grid, block, lds, st, q0, q1, t0);
-  else hipLaunchKernelGGL((conv2_kernel<FC, FP, false, false>), grid, block, lds, st, q0, q1, t0);
+  if (fast && one(a) && one(b)) HZ_LAUNCH((conv2_kernel<FC, FP, true, true>), grid, block, lds, st, q0, q1, t0);
+  else if (fast) HZ_LAUNCH((conv2_kernel<FC, FP, true, false>), grid, block, lds, st, q0, q1, t0);
+  else HZ_LAUNCH((conv2_kernel<FC, FP, false, false>), grid, block, lds, st, q0, q1, t0);
   return (int)hipGetLastError();
 }
 
@@ -438,12 +438,12 @@ int launch(const HzConvParams& p, hipStream_t st) {
   const size_t lds = kw > 1 ? (size_t)kw * FC * FP * 64 * 16 : 0;
   if (p.x_f32) {  // a seam / K-split-conv consumer: channel-blocked convs only
     if (p.x_rowmajor || !fast) return -1;
-    if (is1x1) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false, true>), grid, block, lds, st, q);
-    else hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false, true>), grid, block, lds, st, q);
-  } else if (p.x_rowmajor) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
-  else if (is1x1 && fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, true, false>), grid, block, lds, st, q);
-  else if (fast) hipLaunchKernelGGL((conv_kernel<FC, FP, true, false, false>), grid, block, lds, st, q);
-  else hipLaunchKernelGGL((conv_kernel<FC, FP, false, false, false>), grid, block, lds, st, q);
+    if (is1x1) HZ_LAUNCH((conv_kernel<FC, FP, true, true, false, true>), grid, block, lds, st, q);
+    else HZ_LAUNCH((conv_kernel<FC, FP, true, false, false, true>), grid, block, lds, st, q);
+  } else if (p.x_rowmajor) HZ_LAUNCH((conv_kernel<FC, FP, true, true, true>), grid, block, lds, st, q);
+  else if (is1x1 && fast) HZ_LAUNCH((conv_kernel<FC, FP, true, true, false>), grid, block, lds, st, q);
+  else if (fast) HZ_LAUNCH((conv_kernel<FC, FP, true, false, false>), grid, block, lds, st, q);
+  else HZ_LAUNCH((conv_kernel<FC, FP, false, false, false>), grid, block, lds, st, q);
   return (int)hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -88,6 +89,18 @@ struct Program {
 };
 
 }  // namespace
+
+size_t hz_excl_pad(const void* fn, size_t dyn) {
+  static const size_t target = [] {
+    const char* e = getenv("HIPZAP_EXCL_LDS");
+    return e ? (size_t)strtoul(e, nullptr, 10) : (size_t)0;
+  }();
+  if (!target || target > 160 * 1024) return dyn;
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, fn) != hipSuccess) return dyn;
+  const size_t tot = a.sharedSizeBytes + dyn;
+  return tot >= target ? dyn : dyn + (target - tot);
+}
 
 extern "C" {
 

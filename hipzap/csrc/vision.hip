@@ -348,15 +348,15 @@ extern "C" int hz_maxpool_launch(const HzPoolParams* pp, hipStream_t st) {
   if (p.C % 8) return -1;
   const long total = (long)p.N * p.P * p.Q * (p.C / 8);
   // clamped taps are only inside the window when the padding is smaller than the window
-  if (p.k == 3 && p.pad < 3) hipLaunchKernelGGL(maxpool_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL(maxpool_kernel<0>, dim3((total + 255) / 256), dim3(256), 0, st, p);
+  if (p.k == 3 && p.pad < 3) HZ_LAUNCH(maxpool_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, p);
+  else HZ_LAUNCH(maxpool_kernel<0>, dim3((total + 255) / 256), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
 extern "C" int hz_avgpool_launch(const unsigned short* x, unsigned short* out, int N, int HW, int C, int blocked,
                                  hipStream_t st) {
   if (C % 64) return -1;
-  hipLaunchKernelGGL(avgpool_kernel, dim3(N * (C / 64)), dim3(256), 0, st, x, out, N, HW, C, blocked);
+  HZ_LAUNCH(avgpool_kernel, dim3(N * (C / 64)), dim3(256), 0, st, x, out, N, HW, C, blocked);
   return (int)hipGetLastError();
 }
 
@@ -370,11 +370,11 @@ extern "C" int hz_pool_fc_launch(const HzPoolFcParams* pp, hipStream_t st) {
 #define HZ_POOLFC_STATIC 0  // 1: measured -1.5 % at 8 streams (384 VGPRs, one workgroup per CU)
 #endif
   switch (HZ_POOLFC_STATIC ? (p.HW + 7) / 8 : 0) {  // compile-time pixel batches: every pooling load in flight
-    case 1: hipLaunchKernelGGL(pool_fc_kernel<1>, grid, dim3(256), lds, st, p); break;
-    case 2: hipLaunchKernelGGL(pool_fc_kernel<2>, grid, dim3(256), lds, st, p); break;
-    case 4: hipLaunchKernelGGL(pool_fc_kernel<4>, grid, dim3(256), lds, st, p); break;
-    case 7: hipLaunchKernelGGL(pool_fc_kernel<7>, grid, dim3(256), lds, st, p); break;  // 7x7 (ResNet @224)
-    default: hipLaunchKernelGGL(pool_fc_kernel<0>, grid, dim3(256), lds, st, p); break;
+    case 1: HZ_LAUNCH(pool_fc_kernel<1>, grid, dim3(256), lds, st, p); break;
+    case 2: HZ_LAUNCH(pool_fc_kernel<2>, grid, dim3(256), lds, st, p); break;
+    case 4: HZ_LAUNCH(pool_fc_kernel<4>, grid, dim3(256), lds, st, p); break;
+    case 7: HZ_LAUNCH(pool_fc_kernel<7>, grid, dim3(256), lds, st, p); break;  // 7x7 (ResNet @224)
+    default: HZ_LAUNCH(pool_fc_kernel<0>, grid, dim3(256), lds, st, p); break;
   }
   return (int)hipGetLastError();
 }
@@ -388,29 +388,29 @@ extern "C" int hz_preprocess_launch(const void* src, unsigned short* dst, int N,
     if (Cpad != 16 || H % 16 || W % 16 || Cin < 1 || Cin > 8 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
       return -1;
     const long runs = (long)N * (H / 16) * (W / 16) * Cin * 16;
-    hipLaunchKernelGGL(patchify_kernel<16>, dim3((runs + 255) / 256), dim3(256), 0, st,
+    HZ_LAUNCH(patchify_kernel<16>, dim3((runs + 255) / 256), dim3(256), 0, st,
                        static_cast<const float*>(src), reinterpret_cast<bf16_t*>(dst), N, Cin, H, W, mean, inv_std);
     return (int)hipGetLastError();
   }
   if (Cpad % 8 || Cin > 8) return -1;
   const long total = (long)N * H * W;
   if (mode == 1 && Cin == 3 && total % 4 == 0 && ((uintptr_t)src & 15) == 0 && !HZ_PREPROC_GENERIC) {
-    hipLaunchKernelGGL(preprocess_u8c3_kernel, dim3((total + 1023) / 1024), dim3(256), 0, st,
+    HZ_LAUNCH(preprocess_u8c3_kernel, dim3((total + 1023) / 1024), dim3(256), 0, st,
                        static_cast<const unsigned*>(src), dst, total, Cpad, mean, inv_std);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(preprocess_kernel, dim3((total + 255) / 256), dim3(256), 0, st, src, dst, N, Cin, H, W, Cpad,
+  HZ_LAUNCH(preprocess_kernel, dim3((total + 255) / 256), dim3(256), 0, st, src, dst, N, Cin, H, W, Cpad,
                      mode, mean, inv_std);
   return (int)hipGetLastError();
 }
 
 extern "C" int hz_cast_f32_bf16(const float* x, unsigned short* y, long n, hipStream_t st) {
   const long threads = (n + 3) / 4;
-  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, x, y, n);
+  HZ_LAUNCH(cast_f32_bf16_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, x, y, n);
   return (int)hipGetLastError();
 }
 extern "C" int hz_cast_bf16_f32(const unsigned short* x, float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, y, n);
+  HZ_LAUNCH(cast_bf16_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, y, n);
   return (int)hipGetLastError();
 }
 

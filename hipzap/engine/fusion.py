@@ -66,7 +66,7 @@ class BneckParams(C.Structure):  # HzBneckParams
     _fields_ = [("x", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p),
                 ("b2", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("wd", C.c_void_p),
                 ("bd", C.c_void_p), ("out", C.c_void_p), ("N", C.c_int), ("H", C.c_int), ("W", C.c_int),
-                ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int), ("tile_h", C.c_int), ("pad_", C.c_int)]
+                ("Cin", C.c_int), ("Cmid", C.c_int), ("Cout", C.c_int), ("tile_h", C.c_int), ("imgs", C.c_int)]
 
 
 class SeamParams(C.Structure):  # HzSeamParams
@@ -674,6 +674,9 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
     if p.Cmid == 128:  # layer2 kernels take the block's OUTPUT size (the first block halves it)
         _, p.H, p.W, _ = g.shape(c3.outputs[0])
     p.tile_h = 0 if p.Cmid == 128 else int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # layer1 tile rows
+    # layer2 images per workgroup (batched programs): 0 = 2 when the batch is even (the weight stream
+    # is paid once per image pair, bitwise the one-image kernel), HIPZAP_B2_IMG=1: one
+    p.imgs = int(os.environ.get("HIPZAP_B2_IMG", "0")) if p.Cmid == 128 else 0
     return p
 
 

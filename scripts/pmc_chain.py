@@ -5,8 +5,9 @@ Merges several ``rocprofv3 --pmc ... --output-format csv`` passes (one directory
 same served program into one row per chain position. A position is (kernel name, grid size):
 the 29 launches of one request are distinct by name except the repeated seam / kconv launches,
 which share their shapes, so their counters are averaged per dispatch. Besides the counters each
-row carries the per-workgroup resources from the dispatch record (arch VGPRs, AGPRs, LDS bytes)
-and the workgroups per CU they allow.
+row carries the per-workgroup resources from the dispatch record (its VGPR count is not in
+registers: take VGPRs from the compiler, profiles/r6_chain/kernel_resources.txt). GRBM_GUI_ACTIVE
+under counter collection is mostly profiler overhead per dispatch: no durations here.
 
 Usage: pmc_chain.py <out.json> <pass_dir>... ; prints a text table too.
 """
@@ -51,14 +52,6 @@ def load(dirs):
     return rows, meta, disp
 
 
-def wg_per_cu(m):
-    waves = max(1, m["wg_threads"] // 64)
-    regs = m["vgpr"] + m["agpr"]
-    by_regs = (512 // max(1, regs)) * 4 // waves if regs else 8  # 512 unified regs per SIMD lane, 4 SIMDs
-    by_lds = (160 * 1024) // m["lds_bytes"] if m["lds_bytes"] else 32
-    return max(0, min(by_regs, by_lds, 32 // waves))
-
-
 def main():
     out, dirs = sys.argv[1], sys.argv[2:]
     rows, meta, disp = load(dirs)
@@ -68,7 +61,7 @@ def main():
         avg = {k: v / n[k] for k, v in c.items()}  # per dispatch
         name, wgs = key
         m = meta[key]
-        r = {"kernel": name, "workgroups": wgs, "dispatches": max(n.values()), **m, "wg_per_cu_max": wg_per_cu(m)}
+        r = {"kernel": name, "workgroups": wgs, "dispatches": max(n.values()), "lds_bytes": m["lds_bytes"]}
         if avg.get("SQ_BUSY_CU_CYCLES"):
             r["mfma_busy_per_cu_busy"] = round(avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / avg["SQ_BUSY_CU_CYCLES"], 4)
         if avg.get("SQ_WAVE_CYCLES"):
@@ -96,10 +89,10 @@ def main():
         if avg.get("GRBM_GUI_ACTIVE"):
             r["gpu_active_cycles"] = int(avg["GRBM_GUI_ACTIVE"])
         table.append(r)
-    table.sort(key=lambda r: -r.get("gpu_active_cycles", 0))
+    table.sort(key=lambda r: -r.get("wave_wait_frac", 0))
     with open(out, "w") as f:
         json.dump(table, f, indent=1)
-    cols = ["workgroups", "vgpr", "agpr", "lds_bytes", "wg_per_cu_max", "gpu_active_cycles", "mfma_busy_per_cu_busy",
+    cols = ["workgroups", "lds_bytes", "mfma_busy_per_cu_busy",
             "wave_wait_frac", "wave_issue_stall_frac", "l2_hit", "ta_busy_frac", "td_busy_frac",
             "lds_bank_conflict_ratio", "fetch_KB_per_wg", "write_KB"]
     print(f"{'kernel':48s} " + " ".join(f"{c[:9]:>9s}" for c in cols))

@@ -1,6 +1,6 @@
 """Deterministic served logits. The default ResNet-50 program's layer3 /
 layer4 seams and K-split 3x3 convs sum partial products across workgroups with memory-side float
-atomics; every term they add is first rounded to a multiple of 2^-13 (csrc/common.h hz_fixq), so
+atomics; every term they add is first rounded to a multiple of 2^-10 (csrc/common.h hz_fixq), so
 the sums are exact and independent of arrival order. 1,008 replays of one image spread over 16
 concurrent request contexts (the bench's serving shape, through the native request executor) and
 a second, independently built engine all return the same bits."""

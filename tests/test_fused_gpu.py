@@ -123,3 +123,29 @@ def test_fused_zero_copy_request(r50):
         c.run()
     torch.cuda.synchronize()
     assert torch.equal(zc.host_output, cp.host_output)
+
+
+@pytest.mark.parametrize("batch", [2, 4])
+def test_layer2_two_images_per_workgroup_is_bitwise_one_image(r50, batch, monkeypatch):
+    """Batched programs run the layer2 kernels with two images per workgroup (HzBneckParams.imgs:
+    each weight fragment streamed once for both images); per image the arithmetic and its order are
+    the one-image kernel's, so every layer2 output and the logits are bitwise equal, and half the
+    workgroups are launched."""
+    monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
+    a, params, params_cpu, kw = r50
+    g = a.build_graph(batch=batch, **dict(kw, input_uint8=True))
+    monkeypatch.setenv("HIPZAP_B2_IMG", "0")  # auto: two per workgroup at an even batch
+    two = ExecContext(g, params, torch.device(DEV))
+    monkeypatch.setenv("HIPZAP_B2_IMG", "1")
+    one = ExecContext(g, params, torch.device(DEV))
+    x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(11))
+    _run(two, x)
+    _run(one, x)
+    b2 = [f for f in two.fused.values() if f.kind == "bneck2"]
+    assert len(b2) == 4
+    for f in b2:
+        tid = f.nodes[-1].outputs[0]
+        assert torch.equal(two.view(tid), one.view(tid)), f.nodes[-1].attrs.get("name")
+    assert torch.equal(two.output, one.output)
+    ref = run_graph_reference(g, params_cpu, [x])[g.outputs[0]].reshape(batch, -1)
+    assert _rel(two.output.float().cpu().reshape(batch, -1), ref) < 3e-2

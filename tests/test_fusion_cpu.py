@@ -116,6 +116,7 @@ def test_launchers_refuse_malformed_params_before_any_hip_call():
     assert bneck(Cout=256) == -1
     assert bneck(Cmid=64, Cin=256, Cout=256, H=56, W=56, tile_h=6) == -1
     assert bneck(Cmid=64, Cin=64, Cout=256, H=56, W=56) == -1  # layer1 first block without downsample
+    assert bneck(imgs=2, N=3) == -1 and bneck(imgs=3, N=4) == -1  # layer2 image pairs need an even batch
 
     def stem(**kw):
         p = fusion.StemParams(src=fake, w=fake, bias=fake, out=fake, N=1, H=224, W=224, mode=1,

@@ -33,6 +33,10 @@ def _rel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
 
 
+def _fixq(t):  # csrc/common.h hz_fixq: the 2^-10 grid every accumulator term (and preset) is rounded to
+    return torch.round(t * 1024.0) / 1024.0
+
+
 def _blk(x_nhwc):  # logical NHWC -> channel-blocked device layout
     return CV.to_blocked(x_nhwc).to(DEV)
 
@@ -190,7 +194,7 @@ def test_conv_fp32_relu_input_and_zinit(cfg, kw):
     torch.cuda.synchronize()
     got = CV.from_blocked(out.cpu(), (n, h, h, cm))
     assert torch.equal(got, want.cpu())  # same bf16 operands, same kernel, same K order
-    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, h, h, cm)), zb.cpu().expand(n, h, h, cm))
+    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, h, h, cm)), _fixq(zb.cpu()).expand(n, h, h, cm))
 
 
 @pytest.fixture(scope="module")
@@ -308,7 +312,7 @@ def test_kconv_vs_fp32(c, h, ck, xf32, n, st):
     torch.cuda.synchronize()
     got = CV.from_blocked(out.cpu(), (n, ho, ho, c))
     assert _rel(got, ref) < 1e-3, _rel(got, ref)
-    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, ho, ho, 256)), zb.cpu().expand(n, ho, ho, 256))
+    assert torch.equal(CV.from_blocked(nxt.cpu(), (n, ho, ho, 256)), _fixq(zb.cpu()).expand(n, ho, ho, 256))
 
 
 @pytest.mark.parametrize("n", [1, 2])
