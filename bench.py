@@ -480,21 +480,12 @@ def http_figure(args, world: int, rank: int):
 def config_figures(args, device, world: int, rank: int) -> dict | None:
     """The other BASELINE configs and the reference's own route, on the driver's clock in the same
     launch. Run by rank 0 after the headline (the other ranks wait on the
-    process group's store, a CPU wait); every figure states its timed region:
-
-    * ``bert_base_bs16`` (config 4): BERT-base seq-cls, bs 16, L 128, random-init weights, bf16;
-      hipGraph replays of 1 and of 4 concurrent contexts (``Engine.bench``: the C++ replay loop,
-      all contexts' streams, synchronised) -> seq/s; plus the one-context request latency p50
-      (``Engine.infer``: pinned token ids in, logits out).
-    * ``awd_lstm_get_inference`` (the reference's route, /root/reference/main.py:105-112):
-      ``GET /inference`` through the WSGI app (``hipzap.serve.app``, Flask test clients in
-      process: routing, the batched AWD-LSTM engine, 200 sampled words, detokenisation, the JSON
-      body) on the reference's dimensions (emb 1000, hidden 1150, 3 layers, tied, V = 60000,
-      random-init); the lone-request latency p50 (sequential requests) and the req/s of 32
-      concurrent clients (wall over all their requests).
-    * ``resnet18_cpu_plumbing`` (config 1): ``scripts/bench_cpu_plumbing.py`` -- the dev server
-      (``main.py``) on the CPU backend in a child process, single-image POST /predict over HTTP,
-      sequential; req/s = 1000 / p50.
+    process group's store, a CPU wait), each in a FRESH child process on rank 0's GPU: this process
+    already holds dozens of streams over HIP's 4 hardware queues, which would fold a figure's
+    concurrent contexts onto shared queues (BERT 4 contexts measured 24.4k seq/s in-process vs
+    29.2k fresh). Figures and their timed regions: ``scripts/bench_configs.py`` (config 4: BERT-base
+    bs16 at 1 and 4 contexts; the reference's ``GET /inference`` route through the WSGI app) and
+    ``scripts/bench_cpu_plumbing.py`` (config 1: ResNet-18 POST through the CPU Flask handler).
     Returns the dict (rank 0) or None; a figure that fails is recorded as its error."""
     from datetime import timedelta
     from hipzap.parallel.comm import is_dist
@@ -502,13 +493,10 @@ def config_figures(args, device, world: int, rank: int) -> dict | None:
     if rank == 0:
         out = {}
         try:
-            out["bert_base_bs16"] = _bert_figure(args, device)
+            out.update(_child_json(["scripts/bench_configs.py", "--device", str(device.index or 0),
+                                    "--steps", str(args.steps)], timeout=600))
         except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
-            out["bert_base_bs16"] = {"error": repr(e)[:500]}
-        try:
-            out["awd_lstm_get_inference"] = _lm_route_figure(args)
-        except Exception as e:  # noqa: BLE001
-            out["awd_lstm_get_inference"] = {"error": repr(e)[:500]}
+            out["bert_base_bs16"] = out["awd_lstm_get_inference"] = {"error": repr(e)[:500]}
         try:
             out["resnet18_cpu_plumbing"] = _plumbing_figure()
         except Exception as e:  # noqa: BLE001
@@ -522,99 +510,20 @@ def config_figures(args, device, world: int, rank: int) -> dict | None:
     return out
 
 
-def _bert_figure(args, device) -> dict:
-    from hipzap.engine.engine import Engine
-    from hipzap.models import registry
-    a = registry.get("bert-base")
-    torch.manual_seed(0)
-    sd = a.make_model().eval().state_dict()
-    res = {"model": "bert-base (seq-cls, 2 labels)", "batch": 16, "seq_len": 128, "dtype": "bf16",
-           "data": "synthetic (random-init weights, random token ids)"}
-    iters = max(100, args.steps * 10)
-    for ctx in (1, 4):
-        eng = Engine.from_state_dict("bert-base", sd, device, batch=16, num_contexts=ctx)
-        x = a.example_input(16)
-        eng.infer(x)
-        if ctx == 1:
-            lat = []
-            for _ in range(50):
-                t = time.perf_counter()
-                eng.infer(x)
-                lat.append((time.perf_counter() - t) * 1e3)
-            res["latency_ms_p50_1ctx"] = round(statistics.median(lat), 4)
-        eng.bench(10)
-        torch.cuda.synchronize(device)
-        t = eng.bench(iters)  # (synchronised inside: seconds for iters replays of every context)
-        res[f"seq_s_{ctx}ctx"] = round(16 * ctx * iters / t, 1)
-        res[f"ms_per_replay_{ctx}ctx"] = round(t / iters * 1e3, 4)
-        del eng
-    res["timed_region"] = f"{iters} hipGraph replays per context, all contexts concurrently, synchronised"
-    return res
-
-
-def _lm_route_figure(args) -> dict:
-    import threading
-    os.environ.setdefault("HIPZAP_SETTINGS", "/nonexistent")
-    os.environ.update(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_LM_VOCAB="60000", HIPZAP_BACKEND="gpu")
-    from hipzap.serve.app import app, get_server
-    srv = get_server()
-    t = time.perf_counter()
-    srv.lm()  # the cold load (random-init reference-dims model packed on the GPU), untimed below
-    load_ms = (time.perf_counter() - t) * 1e3
-    cl = app.test_client()
-
-    def get(seed):
-        r = cl.get(f"/inference?seed={seed}")
-        assert r.status_code == 200 and r.get_json()["response"]["text"]
-        return r
-
-    for i in range(3):
-        get(i)
-    lat = []
-    for i in range(15):
-        t = time.perf_counter()
-        get(100 + i)
-        lat.append((time.perf_counter() - t) * 1e3)
-    clients, per = 32, 6
-    errs = []
-
-    def client(c):
-        cc = app.test_client()
-        for k in range(per):
-            try:
-                r = cc.get(f"/inference?seed={1000 + c * per + k}")
-                assert r.status_code == 200
-            except Exception as e:  # noqa: BLE001
-                errs.append(repr(e))
-
-    th = [threading.Thread(target=client, args=(c,)) for c in range(clients)]
-    t = time.perf_counter()
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
-    wall = time.perf_counter() - t
-    words = srv.settings.lm_words
-    return {"route": "GET /inference (WSGI app in process: Flask test clients)", "words": words,
-            "model": "AWD-LSTM emb 1000 / hidden 1150 / 3 layers / tied, V = 60000 (main.py:96)",
-            "data": "random-init weights, synthetic vocabulary", "load_ms": round(load_ms, 1),
-            "lone_request_ms_p50": round(statistics.median(lat), 3), "lone_request_ms_min": round(min(lat), 3),
-            "concurrent_clients": clients, "concurrent_requests": clients * per - len(errs),
-            "concurrent_req_s": round((clients * per - len(errs)) / wall, 1),
-            "concurrent_words_s": round((clients * per - len(errs)) * words / wall, 0), "errors": len(errs),
-            "timed_region": "lone: one request at a time, 15 requests; concurrent: 32 threads x 6 requests, wall"}
+def _child_json(argv: list, timeout: float, env: dict | None = None) -> dict:
+    import subprocess
+    root = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(root, argv[0]), *argv[1:]], capture_output=True, text=True,
+                       timeout=timeout, cwd=root, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        raise RuntimeError(f"{argv[0]} rc={r.returncode}: {r.stderr[-800:]}")
+    return json.loads(lines[-1])
 
 
 def _plumbing_figure() -> dict:
-    import subprocess
-    root = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "bench_cpu_plumbing.py"), "--requests", "30"],
-                       capture_output=True, text=True, timeout=300, cwd=root,
-                       env=dict(os.environ, HIPZAP_RANDOM_WEIGHTS="1"))
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    if r.returncode != 0 or not lines:
-        raise RuntimeError(f"bench_cpu_plumbing rc={r.returncode}: {r.stderr[-800:]}")
-    res = json.loads(lines[-1])
+    res = _child_json(["scripts/bench_cpu_plumbing.py", "--requests", "30"], timeout=300,
+                      env=dict(os.environ, HIPZAP_RANDOM_WEIGHTS="1"))
     res["req_s_sequential"] = round(1e3 / res["http_image_b64_ms_p50"], 1)
     res["timed_region"] = "30 sequential HTTP POST /predict per payload kind, per-request wall"
     return res

@@ -1424,9 +1424,12 @@ extern "C" int hz_bneck_launch(const HzBneckParams* pp, hipStream_t st) {
   if (p.N < 1 || p.H < 1 || p.W < 1) return -1;
   if (p.Cmid == kB2CM) {  // layer2 geometry: 4 x 4 output tiles (H, W: the block's OUTPUT size)
     if (p.N < 1 || p.Cout != kB2CO || p.H % kB2T || p.W % kB2T) return -1;
-    // images per workgroup (HzBneckParams.imgs; auto: two when the batch is even; bitwise either way)
+    // images per workgroup (HzBneckParams.imgs; bitwise either way). auto: two from batch 8 up,
+    // where the launch is throughput-bound (bs16 / bs32 +4.5-5.6 %); one below, where the program
+    // is a latency chain and twice the workgroups at half the work each finish sooner (bs4 -2.8 %
+    // with pairs, profiles/r6_batched)
     if (p.imgs < 0 || p.imgs > 2 || (p.imgs == 2 && p.N % 2)) return -1;
-    const int ni = p.imgs ? p.imgs : (p.N % 2 == 0 ? 2 : 1);
+    const int ni = p.imgs ? p.imgs : (p.N % 2 == 0 && p.N >= 8 ? 2 : 1);
     const dim3 grid((p.H / kB2T) * (p.W / kB2T) * (p.N / ni));
     if (p.Cin == kB2CI && !p.wd) {
       if (ni == 2) HZ_LAUNCH(bneck2_kernel<2>, grid, dim3(512), 0, st, p);

@@ -437,7 +437,7 @@ typedef struct HzBneckParams {
   int N, H, W, Cin, Cmid, Cout;  // H, W: the block's OUTPUT size (the input is 2H x 2W for the
                                  //   stride-2 first block of layer2)
   int tile_h;                 // layer1 output tile rows: 8 (default when 0) or 4 (twice the workgroups)
-  int imgs;                   // layer2 images per workgroup: 0 auto (2 when N is even), 1, 2
+  int imgs;                   // layer2 images per workgroup: 0 auto (2 at an even N >= 8), 1, 2
 } HzBneckParams;
 // ResNet 1x1 -> 1x1 seam at 14x14 / 7x7 (layer3 / layer4, bs=1): conv3 of block i (1x1 CM -> 4CM,
 // + residual + ReLU) and the K-split conv1 of block i+1 (1x1 4CM -> CM) in ONE launch. A workgroup

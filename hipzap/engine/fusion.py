@@ -674,8 +674,8 @@ def bneck_params(g, params, f: Fused, addr) -> BneckParams:
     if p.Cmid == 128:  # layer2 kernels take the block's OUTPUT size (the first block halves it)
         _, p.H, p.W, _ = g.shape(c3.outputs[0])
     p.tile_h = 0 if p.Cmid == 128 else int(os.environ.get("HIPZAP_BNECK_TH", "8"))  # layer1 tile rows
-    # layer2 images per workgroup (batched programs): 0 = 2 when the batch is even (the weight stream
-    # is paid once per image pair, bitwise the one-image kernel), HIPZAP_B2_IMG=1: one
+    # layer2 images per workgroup (batched programs): 0 = auto (2 at an even batch >= 8: the weight
+    # stream is paid once per image pair, bitwise the one-image kernel), HIPZAP_B2_IMG=1 / 2: forced
     p.imgs = int(os.environ.get("HIPZAP_B2_IMG", "0")) if p.Cmid == 128 else 0
     return p
 

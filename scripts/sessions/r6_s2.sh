@@ -37,3 +37,5 @@ grep '^{' $OUT/bench_full.log > $OUT/bench_full.json
 summ $OUT/bench_full.log
 python3 -c "
 import json; d=json.load(open('$OUT/bench_full.json')); print(json.dumps(d.get('configs'), indent=1)[:3000]); print('cold', d['cold_start_ms_p50'], d.get('cold_start_narrowing'), d['cold_start_pth_ms_p50'])"
+timeout -k 10 300 python3 scripts/diag_lmb_vocab.py 8000 20000 40000 60000 90000 > $OUT/lmb_vocab.log 2>&1
+rc=$?; echo "lmb vocab rc=$rc"; grep '^{' $OUT/lmb_vocab.log

@@ -125,7 +125,7 @@ def test_fused_zero_copy_request(r50):
     assert torch.equal(zc.host_output, cp.host_output)
 
 
-@pytest.mark.parametrize("batch", [2, 4])
+@pytest.mark.parametrize("batch", [2, 8])
 def test_layer2_two_images_per_workgroup_is_bitwise_one_image(r50, batch, monkeypatch):
     """Batched programs run the layer2 kernels with two images per workgroup (HzBneckParams.imgs:
     each weight fragment streamed once for both images); per image the arithmetic and its order are
@@ -134,7 +134,7 @@ def test_layer2_two_images_per_workgroup_is_bitwise_one_image(r50, batch, monkey
     monkeypatch.setenv("HIPZAP_ARENA_NOREUSE", "1")
     a, params, params_cpu, kw = r50
     g = a.build_graph(batch=batch, **dict(kw, input_uint8=True))
-    monkeypatch.setenv("HIPZAP_B2_IMG", "0")  # auto: two per workgroup at an even batch
+    monkeypatch.setenv("HIPZAP_B2_IMG", "2")  # two per workgroup (auto picks two from batch 8)
     two = ExecContext(g, params, torch.device(DEV))
     monkeypatch.setenv("HIPZAP_B2_IMG", "1")
     one = ExecContext(g, params, torch.device(DEV))
