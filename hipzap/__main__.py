@@ -33,9 +33,12 @@ def cmd_serve(a):
         from .serve.native_http import NativeHTTPServer, listening_socket
         be = srv.vision(st.default_model)  # cold start before the port opens
         fast = be if isinstance(be, PlanVisionBackend) else None
+        if os.environ.get("HIPZAP_LM_PRELOAD", "0") == "1":
+            srv.lm()  # GET /inference backend before the port opens (else on its first request)
+        http = NativeHTTPServer(app, listening_socket(host, port), fast=fast, server=srv)
         print(f"hipzap serving stage {st.stage} on {host}:{port} (native http, fast route: "
-              f"{fast.name if fast else None})", flush=True)
-        NativeHTTPServer(app, listening_socket(host, port), fast=fast).serve_forever()
+              f"{fast.name if fast else None}, native GET /inference: {http.lm_native})", flush=True)
+        http.serve_forever()
         return
     from werkzeug.serving import WSGIRequestHandler
     WSGIRequestHandler.protocol_version = "HTTP/1.1"  # keep-alive: no TCP handshake per request

@@ -210,6 +210,7 @@ def _load():
     _sig(lib, "hz_exec_bench", c_int, P, c_int, c_int, PP_, C.POINTER(D), C.POINTER(D))
     _sig(lib, "hz_http_start", P, c_int, P)
     _sig(lib, "hz_http_set_fast", c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, C.c_char_p)
+    _sig(lib, "hz_http_set_lm", c_int, P, P, c_int, c_int, c_int, c_int, C.c_char_p, U64, C.c_char_p)
     _sig(lib, "hz_http_respond", None, P, c_int, C.c_char_p, U64, C.c_char_p, U64)
     _sig(lib, "hz_http_stats", None, P, C.POINTER(U64))
     _sig(lib, "hz_http_stop", C.c_int, P)

@@ -251,28 +251,49 @@ def narrow_env(env: dict | None, device: int) -> tuple[dict, int, str]:
     """The environment of a one-GPU worker for HIP device ``device`` of ``env``, narrowed at the
     ROCr level so ROCr's init opens ONE agent: -> (env, device in it, what was done).
 
-    * nothing set: ``ROCR_VISIBLE_DEVICES=<device>`` (device 0 in the child);
-    * only a HIP-level list (``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` /
-      ``GPU_DEVICE_ORDINAL``, which HIP applies AFTER ROCr has initialised every agent it can see):
-      ``ROCR_VISIBLE_DEVICES=<k>`` with k the list's entry for ``device`` (HIP numbers the ROCr GPU
-      agents in ROCr's order) and ``HIP_VISIBLE_DEVICES=0``, the HIP-level lists dropped;
-    * ``ROCR_VISIBLE_DEVICES`` already set, a non-integer list entry, or ``HIPZAP_COLD_ISOLATE=0``:
-      unchanged."""
+    HIP device k is the k-th entry of the HIP-level list (``HIP_VISIBLE_DEVICES`` /
+    ``CUDA_VISIBLE_DEVICES`` / ``GPU_DEVICE_ORDINAL``, which HIP applies after ROCr has initialised
+    every agent it can see) if one is set, else k; that indexes the GPUs ROCr exposes, i.e. the
+    entries of ``ROCR_VISIBLE_DEVICES`` if set, else the physical GPUs. The child gets
+    ``ROCR_VISIBLE_DEVICES=<that entry>`` (+ ``HIP_VISIBLE_DEVICES=0`` when a HIP-level list was
+    set; those lists are dropped) and uses device 0. Kinds: ``rocr`` (nothing was set),
+    ``rocr_from_<var>`` (narrowed from a multi-GPU list), ``unchanged`` (already one ROCr agent, a
+    non-integer HIP-level entry, two disagreeing HIP-level lists, an index past a list, or
+    ``HIPZAP_COLD_ISOLATE=0``)."""
     base = dict(os.environ if env is None else env)
-    if base.get("HIPZAP_COLD_ISOLATE", "1") == "0" or base.get("ROCR_VISIBLE_DEVICES"):
+    if base.get("HIPZAP_COLD_ISOLATE", "1") == "0":
         return base, device, "unchanged"
-    hip_lists = [k for k in _VIS[1:] if base.get(k)]
-    if not hip_lists:
-        base["ROCR_VISIBLE_DEVICES"] = str(device)
-        return base, 0, "rocr"
-    entries = [x.strip() for x in base[hip_lists[0]].split(",") if x.strip()]
-    if device >= len(entries) or not entries[device].isdigit() or len(hip_lists) > 1:
+
+    def entries(var):
+        return [x.strip() for x in base[var].split(",") if x.strip()] if base.get(var) else None
+
+    rocr = entries("ROCR_VISIBLE_DEVICES")
+    hip_vars = [k for k in _VIS[1:] if base.get(k)]
+    if len({base[k] for k in hip_vars}) > 1:
         return base, device, "unchanged"
-    for k in hip_lists:
+    hip = entries(hip_vars[0]) if hip_vars else None
+    if hip is not None:
+        if device >= len(hip) or not hip[device].isdigit():
+            return base, device, "unchanged"
+        idx = int(hip[device])
+    else:
+        idx = device
+    if rocr is not None:
+        if idx >= len(rocr):
+            return base, device, "unchanged"
+        if len(rocr) == 1 and (hip is None or hip == ["0"]):
+            return base, device, "unchanged"  # one ROCr agent already
+        phys = rocr[idx]
+    else:
+        phys = str(idx)
+    for k in hip_vars:
         del base[k]
-    base["ROCR_VISIBLE_DEVICES"] = entries[device]
-    base["HIP_VISIBLE_DEVICES"] = "0"
-    return base, 0, f"rocr_from_{hip_lists[0].lower()}"
+    base["ROCR_VISIBLE_DEVICES"] = phys
+    if hip_vars:
+        base["HIP_VISIBLE_DEVICES"] = "0"
+    kind = "rocr" if rocr is None and not hip_vars else \
+        "rocr_from_" + ("rocr_visible_devices" if rocr is not None else hip_vars[0].lower())
+    return base, 0, kind
 
 
 def isolated_env(env: dict | None, device: int) -> tuple[dict | None, int]:

@@ -619,6 +619,9 @@ typedef void (*HzHttpPyHandler)(void* req, const char* method, const char* targe
 void* hz_http_start(int listen_fd, HzHttpPyHandler py);
 int hz_http_set_fast(void* srv, void* exec, int H, int W, int C, int out_floats, int classes, int probs,
                      const char* model);
+// the native GET /inference route (csrc/http.cpp try_lm); sched = NULL removes it
+int hz_http_set_lm(void* srv, void* sched, int V, int maxn, int dflt, int empty_id, const char* blob, uint64_t blen,
+                   const uint8_t* flags);
 void hz_http_respond(void* req, int status, const char* headers, uint64_t hlen, const char* body, uint64_t blen);
 void hz_http_stats(void* srv, uint64_t* out4);
 int hz_http_stop(void* srv);  // 1: all connections ended; 0: some still live (state leaked)

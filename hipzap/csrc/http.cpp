@@ -8,6 +8,12 @@
 //   [, "model"]} or as an .npy body -> base64/npy decode -> the request executor
 //   (csrc/executor.cpp: pinned input, hipGraph replay, wait) -> softmax + top-5 -> the same
 //   JSON schema as the Flask route (hipzap/serve/app.py predict()).
+// And, once the AWD-LSTM backend is loaded (hz_http_set_lm), the reference's own route:
+//   GET /inference [?seed=<int>][&words=<int>] (no prompt: the reference's request,
+//   /root/reference/main.py:105-112) -> the continuous-batching decode scheduler
+//   (csrc/lmserve.cpp hz_lmb_submit, blocking) -> the reference's detokenizer over a vocabulary
+//   table whose per-word JSON fragments, capitalised forms and spacing flags Python computed
+//   (serve/native_http.py set_lm: byte-identical to the Flask route's body) -> JSON.
 // Anything else (other routes, batches, other keys or dtypes, query flags) goes to a Python
 // callback that runs the WSGI app and answers through hz_http_respond(). One thread per
 // keep-alive connection, blocking I/O; the GIL is only taken on the fallback path.
@@ -22,7 +28,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,6 +48,15 @@ struct Fast {
   std::string model;
 };
 
+// The GET /inference route: the decode scheduler and the detokenizer's vocabulary table.
+struct Lm {
+  void* sched = nullptr;     // csrc/lmserve.cpp scheduler
+  int V = 0, maxn = 0, dflt = 200, empty_id = 0;
+  std::vector<std::string> w, wc;  // JSON-escaped word / its capitalised form (no quotes)
+  std::vector<uint8_t> fl;         // bit0 word in NO_SPACE, bit1 capitalised in NO_SPACE,
+                                   // bit2 word in CAPITALIZE_AFTER, bit3 capitalised in CAPITALIZE_AFTER
+};
+
 struct Server {
   int lfd = -1;
   std::atomic<bool> stop{false};
@@ -50,6 +67,8 @@ struct Server {
   std::atomic<bool> has_fast{false};
   std::mutex fast_mu;
   std::atomic<uint64_t> n_fast{0}, n_py{0}, n_bad{0};
+  std::shared_ptr<const Lm> lm;  // (replaced whole under lm_mu; a request keeps its copy alive)
+  std::mutex lm_mu;
 };
 
 struct PyReq {
@@ -371,6 +390,108 @@ bool try_fast(Server* S, const std::string& method, const std::string& target, c
   return true;
 }
 
+// ---------------------------------------------------------------- GET /inference
+// an integer query value as Python's int() reads the plain forms ("[+-]digits"), reduced mod 2^64
+// (what the engine keeps: seed & (2^62 - 1) depends only on the value mod 2^62); false otherwise
+bool parse_int(const std::string& v, unsigned long long* out, bool* neg) {
+  size_t i = 0;
+  *neg = false;
+  if (i < v.size() && (v[i] == '+' || v[i] == '-')) *neg = v[i++] == '-';
+  if (i == v.size() || v.size() - i > 40) return false;
+  unsigned long long x = 0;
+  for (; i < v.size(); ++i) {
+    if (v[i] < '0' || v[i] > '9') return false;
+    x = x * 10 + (unsigned long long)(v[i] - '0');
+  }
+  *out = *neg ? 0ull - x : x;
+  return true;
+}
+
+bool try_lm(Server* S, const std::string& method, const std::string& target, bool keep, std::string& out) {
+  if (method != "GET") return false;
+  const size_t qpos = target.find('?');
+  if (target.compare(0, qpos == std::string::npos ? target.size() : qpos, "/inference") != 0) return false;
+  std::shared_ptr<const Lm> lm;
+  {
+    std::lock_guard<std::mutex> g(S->lm_mu);
+    lm = S->lm;
+  }
+  if (!lm) return false;
+  // only seed= / words= with plain integers; a prompt or anything else goes to the Flask route
+  bool have_seed = false, have_words = false;
+  unsigned long long seed = 0;
+  int n = lm->dflt;
+  if (qpos != std::string::npos) {
+    const std::string q = target.substr(qpos + 1);
+    size_t p = 0;
+    while (p <= q.size()) {
+      size_t e = q.find('&', p);
+      if (e == std::string::npos) e = q.size();
+      const std::string kv = q.substr(p, e - p);
+      p = e + 1;
+      if (kv.empty()) continue;
+      const size_t eq = kv.find('=');
+      if (eq == std::string::npos) return false;
+      const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+      unsigned long long x;
+      bool neg;
+      if (!parse_int(v, &x, &neg)) return false;
+      if (k == "seed" && !have_seed) {
+        have_seed = true;
+        seed = x;
+      } else if (k == "words" && !have_words && !neg && v.size() <= 9 && x >= 1 && x <= (unsigned long long)lm->maxn) {
+        have_words = true;
+        n = (int)x;
+      } else {
+        return false;  // (a repeated key, an out-of-range word count: the Flask route answers)
+      }
+    }
+  }
+  if (n < 1 || n > lm->maxn) return false;
+  if (!have_seed) {
+    thread_local std::mt19937_64 rng{std::random_device{}()};
+    seed = rng();
+  }
+  seed &= (1ull << 62) - 1;
+  const double t0 = now_ms();
+  thread_local std::vector<int> ids;
+  ids.resize(n);
+  const int prompt = lm->empty_id;  // words = [""] (main.py:103)
+  double lat = 0;
+  const int rc = hz_lmb_submit(lm->sched, &prompt, 1, n, seed, ids.data(), nullptr, &lat);
+  const double t1 = now_ms();
+  if (rc) {
+    out = simple(500, "{\"error\": \"RuntimeError\", \"message\": \"batched decode request failed\"}", keep);
+    return true;
+  }
+  // the reference's detokenizer (serve/text.py Detokenizer, main.py:73-78): the prompt word "" adds
+  // " "; a word after ".", "!" or a newline is capitalised; NO_SPACE words attach without a space
+  std::string js = "{\"response\": {\"text\": \" ";
+  js.reserve(16 + (size_t)n * 12);
+  bool cap = false;
+  for (int i = 0; i < n; ++i) {
+    const int t = ids[i];
+    if (t < 0 || t >= lm->V) {
+      out = simple(500, "{\"error\": \"RuntimeError\", \"message\": \"token out of range\"}", keep);
+      return true;
+    }
+    const uint8_t f = lm->fl[t];
+    if (!(f & (cap ? 2 : 1))) js += ' ';
+    js += cap ? lm->wc[t] : lm->w[t];
+    cap = f & (cap ? 8 : 4);
+  }
+  js += "\"}}";
+  const double t2 = now_ms();
+  char h[400];
+  snprintf(h, sizeof(h),
+           "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n"
+           "Access-Control-Allow-Origin: *\r\nAccess-Control-Expose-Headers: X-Timing\r\n"
+           "X-Timing: generate=%.3f;detok=%.3f;total=%.3f\r\nX-Hipzap-Path: native\r\nConnection: %s\r\n\r\n",
+           js.size(), t1 - t0, t2 - t1, t2 - t0, keep ? "keep-alive" : "close");
+  out = std::string(h) + js;
+  return true;
+}
+
 // ---------------------------------------------------------------- connections
 // S->live was incremented by the spawner BEFORE this thread exists (hz_http_stop frees the server
 // once it reads live == 0: a count taken here could come after that read)
@@ -466,7 +587,7 @@ void serve_conn(Server* S, int fd) {
     }
     if (!open) break;
     const char* body = buf.data() + hend + 4;
-    if (try_fast(S, method, target, ctype, body, (size_t)clen, keep, resp)) {
+    if (try_fast(S, method, target, ctype, body, (size_t)clen, keep, resp) || try_lm(S, method, target, keep, resp)) {
       S->n_fast++;
     } else if (S->py) {
       S->n_py++;
@@ -519,6 +640,43 @@ int hz_http_set_fast(void* h, void* exec, int H, int W, int C, int out_floats, i
   std::lock_guard<std::mutex> g(S->fast_mu);
   S->fast = Fast{exec, H, W, C, out_floats, classes, probs, model ? model : ""};
   S->has_fast.store(true, std::memory_order_release);
+  return 0;
+}
+
+// the native GET /inference route over a decode scheduler (see hipzap/serve/native_http.py set_lm):
+// blob = V entries of <JSON-escaped word>\0<JSON-escaped capitalised word>\0, flags[V] as struct Lm;
+// sched = NULL removes the route
+int hz_http_set_lm(void* h, void* sched, int V, int maxn, int dflt, int empty_id, const char* blob, uint64_t blen,
+                   const uint8_t* flags) {
+  Server* S = static_cast<Server*>(h);
+  if (!sched) {
+    std::lock_guard<std::mutex> g(S->lm_mu);
+    S->lm.reset();
+    return 0;
+  }
+  if (V < 1 || maxn < 1 || dflt < 1 || empty_id < 0 || empty_id >= V || !blob || !flags) return -1;
+  auto lm = std::make_shared<Lm>();
+  lm->sched = sched;
+  lm->V = V;
+  lm->maxn = maxn;
+  lm->dflt = dflt;
+  lm->empty_id = empty_id;
+  lm->w.reserve(V);
+  lm->wc.reserve(V);
+  uint64_t p = 0;
+  for (int i = 0; i < V; ++i) {
+    for (int k = 0; k < 2; ++k) {
+      const void* z = memchr(blob + p, 0, blen - p);
+      if (p >= blen || !z) return -2;
+      const uint64_t e = (uint64_t)(static_cast<const char*>(z) - blob);
+      (k ? lm->wc : lm->w).emplace_back(blob + p, e - p);
+      p = e + 1;
+    }
+  }
+  if (p != blen) return -2;
+  lm->fl.assign(flags, flags + V);
+  std::lock_guard<std::mutex> g(S->lm_mu);
+  S->lm = std::move(lm);
   return 0;
 }
 

@@ -615,7 +615,9 @@ def worker_main() -> int:
         from .native_http import NativeHTTPServer
         from .server import PlanVisionBackend
         fast = backend if isinstance(backend, PlanVisionBackend) else None
-        srv_http = NativeHTTPServer(app_mod.app, socket.socket(fileno=fd), fast=fast)
+        if os.environ.get("HIPZAP_LM_PRELOAD", "0") == "1":
+            srv.lm()  # GET /inference backend before the port opens (else on its first request)
+        srv_http = NativeHTTPServer(app_mod.app, socket.socket(fileno=fd), fast=fast, server=srv)
         app_mod.CLUSTER["http"] = srv_http
         srv_http.serve_forever()
         return 0

@@ -53,12 +53,43 @@ def _environ(method: str, target: str, headers: str, body: bytes, server_port: s
     return env
 
 
+def lm_route_table(itos) -> tuple[bytes, bytes]:
+    """The native GET /inference detokenizer table (csrc/http.cpp ``Lm``): per word its JSON-escaped
+    form and that of its ``str.capitalize()`` (the Flask route's encoder, ``json.dumps``), NUL
+    separated, and a flag byte: bit0 word in NO_SPACE, bit1 capitalised form in NO_SPACE, bit2 word
+    in CAPITALIZE_AFTER, bit3 capitalised form in CAPITALIZE_AFTER (serve/text.py Detokenizer)."""
+    import json
+    from .text import CAPITALIZE_AFTER, NO_SPACE
+    ns, ca = set(NO_SPACE), set(CAPITALIZE_AFTER)
+    parts, flags = [], bytearray(len(itos))
+    for i, w in enumerate(itos):
+        c = w.capitalize()
+        parts.append(json.dumps(w)[1:-1].encode() + b"\0" + json.dumps(c)[1:-1].encode() + b"\0")
+        flags[i] = (w in ns) | ((c in ns) << 1) | ((w in ca) << 2) | ((c in ca) << 3)
+    return b"".join(parts), bytes(flags)
+
+
+def render_with_table(blob: bytes, flags: bytes, ids) -> str:
+    """What csrc/http.cpp try_lm writes inside ``"text": "..."`` for the empty prompt (a Python
+    mirror of its loop, for the CPU test against the Detokenizer)."""
+    ents = blob.split(b"\0")[:-1]
+    w, wc = ents[0::2], ents[1::2]
+    out, cap = [b" "], False
+    for t in ids:
+        f = flags[t]
+        if not f & (2 if cap else 1):
+            out.append(b" ")
+        out.append(wc[t] if cap else w[t])
+        cap = bool(f & (8 if cap else 4))
+    return b"".join(out).decode()
+
+
 class NativeHTTPServer:
     """``app``: any WSGI app (the Flask app). ``sock``: a listening socket (shared by cluster
     workers). ``fast``: a :class:`~hipzap.serve.server.PlanVisionBackend` whose model gets the
     native ``POST /predict`` route (its contexts are built first so the executor covers them)."""
 
-    def __init__(self, app, sock: socket.socket, fast=None):
+    def __init__(self, app, sock: socket.socket, fast=None, server=None):
         from .lambda_handler import call_wsgi
         self.app, self.sock = app, sock
         self._call_wsgi = call_wsgi
@@ -75,6 +106,12 @@ class NativeHTTPServer:
             raise RuntimeError("hz_http_start failed")
         if fast is not None:
             self._route_fast(fast, ex)
+        self.lm_native = False
+        if server is not None:  # GET /inference goes native once the LM backend exists
+            server.lm_listeners.append(self.set_lm)
+            loaded = server._models.get("__lm__")
+            if loaded is not None:
+                self.set_lm(loaded)
 
     @staticmethod
     def _prepare_fast(backend):
@@ -101,6 +138,34 @@ class NativeHTTPServer:
         if rc:
             raise RuntimeError(f"native /predict route rejected (rc={rc}, plan batch {b})")
         self.fast_model = backend.name
+
+    def set_lm(self, backend) -> bool:
+        """Route ``GET /inference`` natively (csrc/http.cpp try_lm) over ``backend``'s batched
+        decode scheduler. The detokenizer's table is computed here from the backend's own
+        vocabulary with the Flask route's rules and its JSON encoder, so the native body is
+        byte-for-byte the WSGI one for the same seed: per word its JSON-escaped form and that of
+        its ``str.capitalize()`` (serve/text.py Detokenizer), and whether each form is in
+        ``NO_SPACE`` / ``CAPITALIZE_AFTER``. Backends without a batched scheduler (the CPU model,
+        the context pool) stay on the WSGI route. Returns whether the route is native."""
+        core = getattr(getattr(backend, "engine", None), "core", None)
+        sched = getattr(core, "_sched", None)
+        if not sched or not getattr(self, "_h", None):
+            return False
+        itos, stoi = backend.itos, backend.stoi
+        V = int(core.V)
+        if len(itos) < V:
+            return False
+        blob, flags = lm_route_table(itos[:V])
+        from .app import get_server
+        dflt = int(get_server().settings.lm_words)
+        rc = N.lib().hz_http_set_lm(self._h, sched, V, int(core.max_words), dflt, int(stoi.get("", 0)), blob,
+                                    len(blob), bytes(flags))
+        if rc:
+            log.warning("native GET /inference route rejected (rc=%d)", rc)
+            return False
+        self._lm_backend = backend  # keep its scheduler alive while the route points at it
+        self.lm_native = True
+        return True
 
     def _handle(self, req, method, target, headers, hlen, body_ptr, blen):
         try:

@@ -242,6 +242,7 @@ class ModelServer:
         self._watchdog = None
         self.comm = None  # set by a DP cluster worker (serve/cluster.py): plan weights arrive by RCCL broadcast
         self.stats = {"requests": 0, "errors": 0, "cold_loads": 0}
+        self.lm_listeners: list = []  # called with the GET /inference backend once it is loaded
 
     def spec(self, name: str) -> ModelSpec:
         return self.settings.models.get(name) or ModelSpec(name=name)
@@ -373,6 +374,11 @@ class ModelServer:
                         be = LMBackend(load_checkpoint(ckpt), load_itos(vocab), self.backend, self.device)
                 self._models[key] = be
                 self.stats["cold_loads"] += 1
+                for cb in list(self.lm_listeners):  # e.g. the native HTTP front end's GET /inference route
+                    try:
+                        cb(be)
+                    except Exception:  # noqa: BLE001 - the WSGI route keeps serving
+                        log.exception("GET /inference listener failed")
             return self._models[key]
 
     def loaded(self) -> dict:

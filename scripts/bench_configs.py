@@ -12,6 +12,9 @@ on rank 0's GPU after the headline). One JSON line:
   dimensions (emb 1000, hidden 1150, 3 layers, tied, V = 60000, random-init); the lone-request
   latency p50 (one request at a time) and the req/s of 32 concurrent clients (wall over all their
   requests).
+* ``awd_lstm_get_inference_http``: the same route over HTTP through the native front end (the
+  request is answered in C++: scheduler submit + detokenizer table + JSON, no GIL), keep-alive
+  client connections.
 
     python scripts/bench_configs.py [--device D] [--steps K]
 """
@@ -108,6 +111,67 @@ def lm_route_figure() -> dict:
                             "requests, wall"}
 
 
+def lm_http_figure() -> dict:
+    """The same route over HTTP through the native front end (``hipzap serve``'s server:
+    csrc/http.cpp answers GET /inference in C++ once the LM backend exists, no GIL on the request
+    path); keep-alive client connections from threads of this process."""
+    import http.client
+    from hipzap.serve.app import app, get_server
+    from hipzap.serve.native_http import NativeHTTPServer, listening_socket
+    srv = get_server()
+    srv.lm()
+    sock = listening_socket("127.0.0.1", 0)
+    port = sock.getsockname()[1]
+    hs = NativeHTTPServer(app, sock, server=srv)
+    try:
+        def conn():
+            return http.client.HTTPConnection("127.0.0.1", port, timeout=120)
+
+        def get(c, seed):
+            c.request("GET", f"/inference?seed={seed}")
+            r = c.getresponse()
+            b = r.read()
+            assert r.status == 200 and b.startswith(b'{"response": {"text": ')
+            return r.getheader("X-Hipzap-Path")
+
+        c = conn()
+        paths = {get(c, i) for i in range(3)}
+        lat = []
+        for i in range(15):
+            t = time.perf_counter()
+            get(c, 100 + i)
+            lat.append((time.perf_counter() - t) * 1e3)
+        c.close()
+        clients, per = 32, 12
+        errs = []
+
+        def client(k):
+            cc = conn()
+            for j in range(per):
+                try:
+                    get(cc, 5000 + k * per + j)
+                except Exception as e:  # noqa: BLE001
+                    errs.append(repr(e))
+            cc.close()
+
+        th = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
+        t = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        wall = time.perf_counter() - t
+        done = clients * per - len(errs)
+        return {"route": "GET /inference over HTTP/1.1 (native front end, csrc/http.cpp)",
+                "native": paths == {"native"}, "lone_request_ms_p50": round(statistics.median(lat), 3),
+                "lone_request_ms_min": round(min(lat), 3), "concurrent_clients": clients,
+                "concurrent_requests": done, "concurrent_req_s": round(done / wall, 1), "errors": len(errs),
+                "timed_region": f"lone: 15 sequential keep-alive requests; concurrent: {clients} keep-alive "
+                                f"connections x {per} requests, wall"}
+    finally:
+        hs.stop()
+
+
 def main():
     dev = int(sys.argv[sys.argv.index("--device") + 1]) if "--device" in sys.argv else 0
     steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 20
@@ -115,7 +179,8 @@ def main():
     torch.cuda.set_device(dev)
     out = {}
     for name, fn in (("bert_base_bs16", lambda: bert_figure(f"cuda:{dev}", steps)),
-                     ("awd_lstm_get_inference", lm_route_figure)):
+                     ("awd_lstm_get_inference", lm_route_figure),
+                     ("awd_lstm_get_inference_http", lm_http_figure)):
         try:
             out[name] = fn()
         except Exception as e:  # noqa: BLE001 - each figure on its own

@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/r6_s3
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_gpu.py -k "two_images" > $OUT/tests.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_gpu.py tests/test_native_lm_gpu.py -k "two_images or native" > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python3 scripts/bench_configs.py --device 0 > $OUT/configs.log 2>&1

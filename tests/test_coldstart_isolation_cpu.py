@@ -8,8 +8,10 @@ def test_isolates_to_one_physical_gpu():
 
 
 def test_respects_launcher_visibility_and_opt_out():
-    env = {"ROCR_VISIBLE_DEVICES": "2,3"}  # already narrowed at the ROCr level: left alone
-    assert isolated_env(env, 1) == (env, 1)
+    env = {"ROCR_VISIBLE_DEVICES": "3"}  # already one ROCr agent: left alone
+    assert isolated_env(env, 0) == (env, 0)
+    env = {"ROCR_VISIBLE_DEVICES": "3", "HIP_VISIBLE_DEVICES": "0"}  # (the serving lease's pair)
+    assert isolated_env(env, 0) == (env, 0)
     env = {"HIPZAP_COLD_ISOLATE": "0"}
     assert isolated_env(env, 4) == (env, 4)
     for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):  # round-5 behaviour on request
@@ -28,6 +30,13 @@ def test_a_hip_level_list_is_narrowed_at_the_rocr_level():
         assert env["PATH"] == "/bin" and (k == "HIP_VISIBLE_DEVICES" or k not in env)
     assert narrow_env({"HIP_VISIBLE_DEVICES": "4"}, 0)[2] == "rocr_from_hip_visible_devices"
     assert narrow_env({}, 2)[:2] == ({"ROCR_VISIBLE_DEVICES": "2"}, 0)
+    # a multi-GPU ROCr list (an 8-GPU node's launcher): narrowed to the rank's entry
+    env, dev = isolated_env({"ROCR_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}, 5)
+    assert env == {"ROCR_VISIBLE_DEVICES": "5"} and dev == 0
+    env, dev = isolated_env({"ROCR_VISIBLE_DEVICES": "4,5,6,7", "HIP_VISIBLE_DEVICES": "3,2"}, 1)
+    assert env == {"ROCR_VISIBLE_DEVICES": "6", "HIP_VISIBLE_DEVICES": "0"} and dev == 0
+    assert narrow_env({"ROCR_VISIBLE_DEVICES": "GPU-a,GPU-b"}, 1)[:2] == ({"ROCR_VISIBLE_DEVICES": "GPU-b"}, 0)
+    assert narrow_env({"ROCR_VISIBLE_DEVICES": "0,1"}, 1)[2] == "rocr_from_rocr_visible_devices"
     # an index the list does not have, a UUID entry, or two disagreeing lists: unchanged
     for env, d in (({"HIP_VISIBLE_DEVICES": "0"}, 3), ({"HIP_VISIBLE_DEVICES": "GPU-abc"}, 0),
                    ({"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "0"}, 0)):
