@@ -18,6 +18,14 @@
 #include <random>
 
 extern "C" int hz_exec_submit(void*, const void* const*, void*, double*) { return 1; }
+// the decode scheduler of the GET /inference route: deterministic token ids from the seed
+extern "C" int hz_lmb_submit(void*, const int* prompt, int P, int n, unsigned long long seed, int* out, float*,
+                             double* lat) {
+  if (!prompt || P != 1 || n < 1 || !out) return -1;
+  for (int i = 0; i < n; ++i) out[i] = (int)((seed * 2654435761ull + (unsigned long long)i * 7) % 6);
+  if (lat) *lat = 1.0;
+  return 0;
+}
 
 namespace {
 
@@ -111,6 +119,52 @@ void fuzz_framing() {
   }
 }
 
+// the GET /inference route: query strings fuzzed (seed / words / other keys, signs, overflow,
+// repeats) through try_lm against a 6-word table; a request the route takes must produce a body
+// of exactly n words from the table, and anything else must fall back (return false)
+void fuzz_lm_route() {
+  Server S;
+  // words: "a", "B", ".", "n't", "q\"t", "\n" (JSON-escaped forms as Python writes them)
+  const char* w[6] = {"a", "b", ".", "n't", "q\\\"t", "\\n"};
+  const char* wc[6] = {"A", "B", ".", "N't", "Q\\\"t", "\\n"};
+  std::string blob;
+  for (int i = 0; i < 6; ++i) {
+    blob += w[i];
+    blob.push_back('\0');
+    blob += wc[i];
+    blob.push_back('\0');
+  }
+  const uint8_t fl[6] = {0, 0, 1 | 2 | 4 | 8, 1, 0, 4 | 8};
+  int dummy = 0;
+  if (hz_http_set_lm(&S, &dummy, 6, 50, 20, 0, blob.data(), blob.size(), fl) != 0) abort();
+  if (hz_http_set_lm(&S, &dummy, 6, 50, 20, 7, blob.data(), blob.size(), fl) != -1) abort();  // empty id past V
+  if (hz_http_set_lm(&S, &dummy, 7, 50, 20, 0, blob.data(), blob.size(), fl) != -2) abort();  // short blob
+  const std::string seeds[] = {"/inference", "/inference?seed=5", "/inference?seed=-5&words=7",
+                               "/inference?words=50&seed=18446744073709551621", "/inference?words=0",
+                               "/inference?prompt=a&seed=1", "/inference?seed=1&seed=2", "/inference?words=9999999999"};
+  int native = 0;
+  for (int it = 0; it < 20000; ++it) {
+    std::string t = it % 3 == 0 ? mutate(seeds[rng() % 8]) : seeds[rng() % 8];
+    std::string out;
+    if (try_lm(&S, "GET", t, true, out)) {
+      ++native;
+      const size_t b = out.find("\r\n\r\n");
+      if (b == std::string::npos || out.compare(0, 15, "HTTP/1.1 200 OK") != 0) abort();
+      const std::string body = out.substr(b + 4);
+      if (body.compare(0, 23, "{\"response\": {\"text\": \"") != 0 || body.compare(body.size() - 3, 3, "\"}}") != 0)
+        abort();
+    }
+  }
+  std::string out;
+  if (!try_lm(&S, "GET", "/inference?seed=3&words=4", true, out) || try_lm(&S, "POST", "/inference", true, out) ||
+      try_lm(&S, "GET", "/inference?words=51", true, out) || try_lm(&S, "GET", "/inference?seed=1&x=2", true, out) ||
+      try_lm(&S, "GET", "/inferencex", true, out))
+    abort();
+  if (hz_http_set_lm(&S, nullptr, 0, 0, 0, 0, nullptr, 0, nullptr) != 0 || try_lm(&S, "GET", "/inference", true, out))
+    abort();  // route removed
+  printf("lm route fuzz: %d native\n", native);
+}
+
 extern "C" void echo_handler(void* req, const char*, const char* target, const char*, uint64_t, const char*,
                              uint64_t blen) {
   const std::string body = std::string("{\"target\": \"") + target + "\", \"n\": " + std::to_string(blen) + "}";
@@ -172,6 +226,7 @@ void server_rounds() {
 int main() {
   fuzz_parsers();
   fuzz_framing();
+  fuzz_lm_route();
   server_rounds();
   printf("http parse fuzz: ok\n");
   return 0;
