@@ -391,13 +391,15 @@ bool try_fast(Server* S, const std::string& method, const std::string& target, c
 }
 
 // ---------------------------------------------------------------- GET /inference
-// an integer query value as Python's int() reads the plain forms ("[+-]digits"), reduced mod 2^64
-// (what the engine keeps: seed & (2^62 - 1) depends only on the value mod 2^62); false otherwise
+// an integer query value as Python's int() reads the plain forms ("[+-]digits"), at most 18
+// digits (|x| < 2^63: the range the Flask route's engine call accepts; beyond it the Flask route
+// answers, with its error), as two's complement mod 2^64 (the engine keeps seed & (2^62 - 1),
+// which depends only on the value mod 2^62); false otherwise
 bool parse_int(const std::string& v, unsigned long long* out, bool* neg) {
   size_t i = 0;
   *neg = false;
   if (i < v.size() && (v[i] == '+' || v[i] == '-')) *neg = v[i++] == '-';
-  if (i == v.size() || v.size() - i > 40) return false;
+  if (i == v.size() || v.size() - i > 18) return false;
   unsigned long long x = 0;
   for (; i < v.size(); ++i) {
     if (v[i] < '0' || v[i] > '9') return false;

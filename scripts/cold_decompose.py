@@ -30,7 +30,7 @@ def main():
     trials = int(sys.argv[sys.argv.index("--trials") + 1]) if "--trials" in sys.argv else 12
     out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else "gpurun_out/cold_decompose.json"
     base = dict(os.environ)
-    arms = {"hip": ([PROBE, "--hip-only"], base), "hsa": ([PROBE], base),
+    arms = {"hip": ([PROBE, "--hip-only"], base), "hsa": ([PROBE], base), "null_first": ([PROBE, "--null-first"], base),
             "hip_narrow": ([PROBE, "--hip-only"], narrowed(base)), "hsa_narrow": ([PROBE], narrowed(base))}
     res = {"environment": environment(base),
            "env_vars": {k: v for k, v in base.items() if any(s in k for s in ("VISIBLE", "ROCR", "HSA_", "HIP_", "GPU_"))},
@@ -45,10 +45,10 @@ def main():
     summ = {}
     for a, rows in res["arms"].items():
         ok = [r for r in rows if "total_ms" in r]
-        summ[a] = {k: round(statistics.median(r[k] for r in ok), 2) for k in
-                   ("hsa_init_ms", "agents_pools_ms", "queue_create_ms", "hip_init_ms", "first_stream_ms",
-                    "first_op_ms", "total_ms")} if ok else {"error": rows[-1]}
-        if ok:
+        summ[a] = {k: round(statistics.median(r[k] for r in ok), 2) for k in ok[0] if k not in
+                   ("rc", "hip_only", "null_first", "agents", "gpu_agents", "pools", "hip_devices")} \
+            if ok else {"error": rows[-1]}
+        if ok and "gpu_agents" in ok[0]:
             summ[a].update(gpu_agents=ok[0]["gpu_agents"], agents=ok[0]["agents"], hip_devices=ok[0]["hip_devices"],
                            total_min=round(min(r["total_ms"] for r in ok), 2),
                            total_max=round(max(r["total_ms"] for r in ok), 2))

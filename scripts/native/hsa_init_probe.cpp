@@ -44,10 +44,33 @@ static hsa_status_t agent_cb(hsa_agent_t a, void* d) {
 
 int main(int argc, char** argv) {
   const bool hip_only = argc > 1 && std::strcmp(argv[1], "--hip-only") == 0;
+  // --null-first: HIP alone, then the first operation on the NULL stream before any stream exists
+  // (is the default stream's hardware queue made at init, or lazily like a created stream's?)
+  const bool null_first = argc > 1 && std::strcmp(argv[1], "--null-first") == 0;
   const double t0 = now_ms();
   Census c;
   double t_init = t0, t_enum = t0, t_queue = t0;
   hsa_queue_t* q = nullptr;
+  if (null_first) {
+    hipError_t e = hipSetDevice(0);
+    if (e == hipSuccess) e = hipFree(nullptr);
+    const double t_init_ = now_ms();
+    void* p = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&p, 4096);
+    const double t_mal = now_ms();
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, 4096, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    const double t_null = now_ms();
+    hipStream_t st = nullptr;
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    const double t_stream = now_ms();
+    std::printf("{\"null_first\": true, \"hip_init_ms\": %.2f, \"malloc_ms\": %.2f, \"null_first_op_ms\": %.2f, "
+                "\"then_stream_ms\": %.2f, \"total_ms\": %.2f, \"rc\": %d}\n",
+                t_init_ - t0, t_mal - t_init_, t_null - t_mal, t_stream - t_null, t_stream - t0, (int)e);
+    if (st) (void)hipStreamDestroy(st);
+    if (p) (void)hipFree(p);
+    return e == hipSuccess ? 0 : 1;
+  }
   if (!hip_only) {
     if (hsa_init() != HSA_STATUS_SUCCESS) {
       std::printf("{\"error\": \"hsa_init failed\"}\n");

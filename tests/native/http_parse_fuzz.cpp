@@ -140,7 +140,7 @@ void fuzz_lm_route() {
   if (hz_http_set_lm(&S, &dummy, 6, 50, 20, 7, blob.data(), blob.size(), fl) != -1) abort();  // empty id past V
   if (hz_http_set_lm(&S, &dummy, 7, 50, 20, 0, blob.data(), blob.size(), fl) != -2) abort();  // short blob
   const std::string seeds[] = {"/inference", "/inference?seed=5", "/inference?seed=-5&words=7",
-                               "/inference?words=50&seed=18446744073709551621", "/inference?words=0",
+                               "/inference?words=50&seed=999999999999999999", "/inference?words=0",
                                "/inference?prompt=a&seed=1", "/inference?seed=1&seed=2", "/inference?words=9999999999"};
   int native = 0;
   for (int it = 0; it < 20000; ++it) {

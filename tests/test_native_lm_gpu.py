@@ -44,7 +44,7 @@ def test_native_route_is_byte_identical_to_the_flask_route(served):
     assert st == 200 and h.get("X-Hipzap-Path") != "native"
     assert http_srv.lm_native
     cl = app_mod.app.test_client()
-    for q in ("seed=7", "seed=12345&words=37", "words=200&seed=3", "seed=-5", "seed=18446744073709551621"):
+    for q in ("seed=7", "seed=12345&words=37", "words=200&seed=3", "seed=-5", "seed=999999999999999999"):
         st, h, nb = _get(port, f"/inference?{q}")
         assert st == 200 and h.get("X-Hipzap-Path") == "native", q
         fb = cl.get(f"/inference?{q}").get_data()  # the WSGI route, same engine
@@ -62,5 +62,7 @@ def test_requests_the_native_route_does_not_take_reach_flask(served):
     assert json.loads(body)["response"]["text"].startswith(" the cat")
     st, h, _ = _get(port, "/inference?words=0")
     assert st >= 400 and h.get("X-Hipzap-Path") != "native"
+    st, h, _ = _get(port, "/inference?seed=18446744073709551621")  # past 2^63: the Flask route's answer
+    assert h.get("X-Hipzap-Path") != "native"
     st, h, body = _get(port, "/inference")  # no seed: a random one, natively
     assert st == 200 and h.get("X-Hipzap-Path") == "native" and json.loads(body)["response"]["text"]
