@@ -13,8 +13,9 @@ on rank 0's GPU after the headline). One JSON line:
   latency p50 (one request at a time) and the req/s of 32 concurrent clients (wall over all their
   requests).
 * ``awd_lstm_get_inference_http``: the same route over HTTP through the native front end (the
-  request is answered in C++: scheduler submit + detokenizer table + JSON, no GIL), keep-alive
-  client connections.
+  request is answered in C++: scheduler submit + detokenizer table + JSON, no GIL), 32 client
+  PROCESSES (scripts/lm_http_client.py; 32 Python client threads in one process were the
+  bottleneck: 1.4k req/s against the engine's 2.76k), one keep-alive connection each.
 
     python scripts/bench_configs.py [--device D] [--steps K]
 """
@@ -114,7 +115,7 @@ def lm_route_figure() -> dict:
 def lm_http_figure() -> dict:
     """The same route over HTTP through the native front end (``hipzap serve``'s server:
     csrc/http.cpp answers GET /inference in C++ once the LM backend exists, no GIL on the request
-    path); keep-alive client connections from threads of this process."""
+    path); the lone request from this process, the concurrent load from client processes."""
     import http.client
     from hipzap.serve.app import app, get_server
     from hipzap.serve.native_http import NativeHTTPServer, listening_socket
@@ -143,31 +144,30 @@ def lm_http_figure() -> dict:
             lat.append((time.perf_counter() - t) * 1e3)
         c.close()
         clients, per = 32, 12
-        errs = []
-
-        def client(k):
-            cc = conn()
-            for j in range(per):
-                try:
-                    get(cc, 5000 + k * per + j)
-                except Exception as e:  # noqa: BLE001
-                    errs.append(repr(e))
-            cc.close()
-
-        th = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
-        t = time.perf_counter()
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        wall = time.perf_counter() - t
-        done = clients * per - len(errs)
+        import subprocess
+        import tempfile
+        go = os.path.join(tempfile.mkdtemp(prefix="hz_lmgo_"), "go")
+        procs = [subprocess.Popen([sys.executable, "-S", os.path.join(ROOT, "scripts", "lm_http_client.py"), str(port),
+                                   str(per), str(5000 + k * per), go], stdout=subprocess.PIPE, text=True)
+                 for k in range(clients)]
+        time.sleep(1.0)  # every client process started and connected
+        t_go = time.time()
+        open(go, "w").close()
+        outs = [json.loads(p.communicate(timeout=300)[0].strip().splitlines()[-1]) for p in procs]
+        wall = max(o["t_end"] for o in outs) - t_go  # go signal -> the last client's last response
+        errs = [o["errors"] for o in outs if o["errors"]]
+        done = clients * per - sum(errs)
+        lat_all = sorted(x for o in outs for x in o["lat"])
+        paths |= {p for o in outs for p in o["paths"]}
         return {"route": "GET /inference over HTTP/1.1 (native front end, csrc/http.cpp)",
                 "native": paths == {"native"}, "lone_request_ms_p50": round(statistics.median(lat), 3),
                 "lone_request_ms_min": round(min(lat), 3), "concurrent_clients": clients,
-                "concurrent_requests": done, "concurrent_req_s": round(done / wall, 1), "errors": len(errs),
-                "timed_region": f"lone: 15 sequential keep-alive requests; concurrent: {clients} keep-alive "
-                                f"connections x {per} requests, wall"}
+                "concurrent_requests": done, "concurrent_req_s": round(done / wall, 1), "errors": sum(errs),
+                "concurrent_latency_ms_p50": round(lat_all[len(lat_all) // 2], 3),
+                "concurrent_latency_ms_p99": round(lat_all[int(0.99 * (len(lat_all) - 1))], 3),
+                "timed_region": f"lone: 15 sequential keep-alive requests; concurrent: {clients} client processes "
+                                f"(scripts/lm_http_client.py), one keep-alive connection x {per} requests each, "
+                                "wall from the go signal to the last client's last response"}
     finally:
         hs.stop()
 
