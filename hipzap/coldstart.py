@@ -344,9 +344,19 @@ def _fresh_cmd(mode: str, path: str, model: str, device: int, extra_args: list |
             *(extra_args or [])]
 
 
+def trial_gap_s() -> float:
+    """Idle time before each fresh-process trial (``HIPZAP_COLD_GAP_MS``, default 0): back to back,
+    a child's HIP init overlaps the kernel driver's teardown of the previous child's GPU process
+    state, which a serverless cold start (no process just exited on that GPU) does not pay."""
+    return max(0.0, float(os.environ.get("HIPZAP_COLD_GAP_MS", "0"))) / 1e3
+
+
 def _fresh_trial(cmd: list, mode: str, env, timeout: float) -> tuple[float, dict]:
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gap = trial_gap_s()
+    if gap:
+        time.sleep(gap)
     t = time.time()
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout, env=env)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
