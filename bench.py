@@ -354,17 +354,21 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
     (``parallel/dp.py`` DPExecutor), images/s over the whole job = global batch x K / the slowest
     rank's wall. ResNet-50 at global batch 32 (uint8 images, the headline's broadcast weights)
     and ViT-B/16 fp8 at global batch 64 (random-init weights packed on every rank from the same
-    seed). Collectives run on the native RCCL communicator when the headline uses it (bounded
+    seed). ``img_s``: ``dp_depth()`` steps in flight (``parallel/dp.py`` DPPipeline: one captured
+    context and stream per in-flight step, collectives in pipelined order on the caller's
+    stream; every step's gather issued and completed inside the timed region);
+    ``img_s_one_in_flight``: each step alone, back to back. Collectives run on the native RCCL communicator when the headline uses it (bounded
     waits: a stuck collective raises instead of hanging the launch), else torch.distributed.
     Every rank builds first and all agree before the first collective; a failure skips the
     figure (None), never the headline."""
     from hipzap.engine.engine import Engine
     from hipzap.models import registry
     from hipzap.parallel.comm import is_dist, max_over_ranks
-    from hipzap.parallel.dp import DPExecutor
+    from hipzap.parallel.dp import DPPipeline
+    depth = dp_depth()
     out = {}
     for name, model, gb in (("resnet50_gb32", args.model, 32), ("vit_b16_fp8_gb64", "vit-b16-fp8", 64)):
-        ok, ex, xg = 1.0, None, None
+        ok, seng, xg = 1.0, None, None
         try:
             shard = gb // world
             if shard * world != gb:
@@ -375,13 +379,8 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
                 a = registry.get(model)
                 torch.manual_seed(0)
                 params, arch_kw = a.pack(a.make_model().eval().state_dict(), device)
-            seng = Engine(model, params, device, batch=shard, num_contexts=1, arch_kw=arch_kw, host_io=False)
+            seng = Engine(model, params, device, batch=shard, num_contexts=depth, arch_kw=arch_kw, host_io=False)
             cin, cout = seng.contexts[0].input, seng.contexts[0].output
-            # the scatter writes each shard straight into the captured context's input; the gather reads its
-            # output in place; the returned logits are a view of the gather buffer (no per-step clone)
-            ex = DPExecutor(lambda xs, e=seng: e.infer_device(xs), shard, tuple(cin.shape[1:]), tuple(cout.shape[1:]),
-                            device, in_dtype=cin.dtype, out_dtype=cout.dtype, comm=native_comm, in_buf=cin,
-                            copy_out=False)
             if rank == 0:
                 xg = (torch.randint(0, 256, (gb,) + tuple(cin.shape[1:]), dtype=torch.uint8, device=device)
                       if cin.dtype == torch.uint8 else torch.randn((gb,) + tuple(cin.shape[1:]), device=device).to(cin.dtype))
@@ -391,30 +390,51 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
         if -max_over_ranks(-ok, device) < 1.0:
             out[name] = None
             continue
-        try:
-            for _ in range(max(1, args.warmup)):
-                ex.step(xg)
-            torch.cuda.synchronize(device)
-            if is_dist():
-                dist.barrier()
-            t0 = time.perf_counter()
-            for i in range(args.steps):  # one bounded host sync per 8 steps (DPExecutor.step docstring)
-                ex.step(xg, sync=i % 8 == 7)
-            ex.sync()
-            torch.cuda.synchronize(device)
-            dt = time.perf_counter() - t0
-        except Exception as e:  # noqa: BLE001
-            print(f"dp figure {name} failed: {e!r}", file=sys.stderr)
-            dt = float("inf")
-        dt = max_over_ranks(dt, device)
-        out[name] = None if dt == float("inf") else {
-            "img_s": round(gb * args.steps / dt, 2), "global_batch": gb, "per_rank_batch": gb // world,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "steps": args.steps, "model": model,
-            "comm": "native-rccl" if native_comm is not None else ("torch.distributed" if world > 1 else None),
-            "dtype": "fp8" if "fp8" in model else "bf16"}
-        del ex
+        res = {"global_batch": gb, "per_rank_batch": gb // world, "steps": args.steps, "model": model,
+               "comm": "native-rccl" if native_comm is not None else ("torch.distributed" if world > 1 else None),
+               "dtype": "fp8" if "fp8" in model else "bf16"}
+        # the scatter writes each shard straight into a captured context's input, the gather reads its output
+        # in place; D steps in flight (DPPipeline): the rank keeps D batches moving, one per context / stream
+        for d in sorted({1, depth}):
+            pipe = DPPipeline(seng.pipeline_slots()[:d], gb // world, tuple(cout.shape[1:]), device,
+                              out_dtype=cout.dtype, comm=native_comm)
+            try:
+                for _ in range(max(1, args.warmup)):
+                    pipe.submit(xg)
+                pipe.flush()
+                pipe.sync()
+                torch.cuda.synchronize(device)
+                if is_dist():
+                    dist.barrier()
+                t0 = time.perf_counter()
+                for i in range(args.steps):  # one bounded host sync per 8 steps
+                    pipe.submit(xg)
+                    if i % 8 == 7:
+                        pipe.sync()
+                pipe.flush()  # every step's gather issued: all K steps complete inside the timed region
+                pipe.sync()
+                torch.cuda.synchronize(device)
+                dt = time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001
+                print(f"dp figure {name} (in flight {d}) failed: {e!r}", file=sys.stderr)
+                dt = float("inf")
+            dt = max_over_ranks(dt, device)
+            if dt == float("inf"):
+                continue
+            key = "" if d == depth else "_one_in_flight"
+            res[f"img_s{key}"] = round(gb * args.steps / dt, 2)
+            res[f"ms_per_step{key}"] = round(dt / args.steps * 1e3, 4)
+            del pipe
+        res["in_flight"] = depth
+        out[name] = res if "img_s" in res else None
+        del seng
     out["dp_shard_w8"] = dp_shard_figures(args, eng, device)
     return out
+
+
+def dp_depth() -> int:
+    """DP steps in flight per rank for the config 3 / 5 figures (``HIPZAP_DP_DEPTH``, 1-8)."""
+    return max(1, min(8, int(os.environ.get("HIPZAP_DP_DEPTH", "3"))))
 
 
 def dp_shard_figures(args, eng, device) -> dict:
@@ -440,6 +460,14 @@ def dp_shard_figures(args, eng, device) -> dict:
             res[name] = {"img_s": round(shard * iters / t, 2), "ms_per_batch": round(t / iters * 1e3, 4),
                          "batch": shard, "node_upper_img_s": round(8 * shard * iters / t, 2), "model": model}
             del seng
+            depth = dp_depth()
+            if depth > 1:  # the same shard program with D batches in flight (DPPipeline's compute side)
+                seng = Engine(model, params, device, batch=shard, num_contexts=depth, arch_kw=arch_kw, host_io=False)
+                seng.bench(max(5, args.warmup))
+                t = seng.bench(iters)  # iters replays of every context, concurrently, synchronised
+                res[name].update(in_flight=depth, img_s_in_flight=round(shard * depth * iters / t, 2),
+                                 node_upper_img_s_in_flight=round(8 * shard * depth * iters / t, 2))
+                del seng
         except Exception as e:  # noqa: BLE001 - a secondary figure must not take the headline down
             print(f"dp shard figure {name} skipped: {e!r}", file=sys.stderr)
             res[name] = None

@@ -308,6 +308,12 @@ class Engine:
             x.record_stream(s)
         return ctx.output
 
+    def pipeline_slots(self) -> list:
+        """One ``parallel.dp.DPPipeline`` slot per captured context (its static input / output and
+        its own stream): DP steps in flight on this rank, one per context."""
+        self.ensure_contexts()
+        return [_EngineSlot(self, i) for i in range(len(self.contexts))]
+
     def bench(self, iters: int) -> float:
         """Replay all contexts concurrently ``iters`` times (C++ loop); returns seconds."""
         self.ensure_contexts()
@@ -354,3 +360,25 @@ class Engine:
         return {"model": self.model, "batch": self.batch, "contexts": len(self.contexts),
                 "ops": c.num_ops(), "arena_MB": round(c.arena_bytes / 2**20, 2),
                 "captured": c.captured, "timings_ms": {k: round(v, 2) for k, v in self.timings.items()}}
+
+
+class _EngineSlot:
+    """``DPPipeline`` slot over one captured context: ``launch`` orders the context's stream after
+    the caller's current stream and replays; ``join`` orders the caller after the replay."""
+
+    def __init__(self, eng: Engine, i: int):
+        self.eng, self.i = eng, i
+        self.input = eng.contexts[i].input
+        self.output = eng.contexts[i].output
+
+    def launch(self) -> None:
+        ctx, s = self.eng.contexts[self.i], self.eng.streams[self.i]
+        with torch.cuda.device(self.eng.device):
+            s.wait_stream(torch.cuda.current_stream(self.eng.device))
+            with torch.cuda.stream(s):
+                ctx.replay(s)
+
+    def join(self) -> torch.Tensor:
+        with torch.cuda.device(self.eng.device):
+            torch.cuda.current_stream(self.eng.device).wait_stream(self.eng.streams[self.i])
+        return self.output

@@ -13,6 +13,7 @@ Two DP modes:
 """
 from __future__ import annotations
 
+from collections import deque
 from typing import Callable
 
 import torch
@@ -115,6 +116,130 @@ class DPExecutor:
     def sync(self) -> None:
         """Wait for the steps left in flight by ``step(sync=False)`` (bounded on RCCL)."""
         if getattr(self.comm, "supports_async", False) and self.world > 1:
+            self.comm.sync(torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else None)
+        elif self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+
+class FnSlot:
+    """A pipeline slot over a plain function (CPU ranks, tests): ``launch`` computes at once."""
+
+    def __init__(self, fn: Callable[[torch.Tensor], torch.Tensor], shard_batch: int, in_shape: tuple,
+                 dtype=torch.float32, device="cpu"):
+        self.fn = fn
+        self.input = torch.zeros((shard_batch,) + tuple(in_shape), dtype=dtype, device=device)
+        self.output = None
+
+    def launch(self) -> None:
+        self.output = self.fn(self.input)
+
+    def join(self) -> torch.Tensor:
+        return self.output
+
+
+class DPPipeline:
+    """The scatter -> shard replay -> gather step with ``len(slots)`` steps in flight.
+
+    Each slot is one captured context of the rank's shard program (``Engine.pipeline_slots``: its
+    own static input / output and its own stream; ``FnSlot`` on the CPU): ``slot.input`` is where
+    the scatter lands, ``slot.launch()`` enqueues the shard's compute after the caller's current
+    stream, ``slot.join()`` makes the caller's current stream wait for it and returns the output.
+
+    Every collective stays on the caller's current stream, in the same order on every rank:
+    ``submit`` of step i issues scatter(i), launches i on its slot, and -- once ``depth`` steps are
+    pending -- gather(i - depth + 1). So with depth D the issue order is sc0 .. sc(D-1), g0, scD,
+    g1, ...: the scatters of the next D - 1 steps are queued before the oldest step's gather
+    waits for its compute, and D shard programs run concurrently on their own streams. A slot is
+    reused only after its previous step's gather (which waited for that step's compute) was
+    issued on the same stream, so no buffer is overwritten while in use. Depth 1 is exactly
+    ``DPExecutor.step``.
+
+    ``submit`` returns the oldest pending step's logits once D are pending (else None); ``flush``
+    retires every pending step (in order). Rank 0's results are views of per-slot gather buffers,
+    valid for the next D - 1 submits. Config 3 as a serving load: one rank keeps D batches moving
+    instead of running each one's latency chain alone (``bench.py`` dp figures, ``in_flight``)."""
+
+    def __init__(self, slots: list, shard_batch: int, out_shape: tuple, device, out_dtype=torch.float32,
+                 group=None, comm: Comm | None = None):
+        if not slots:
+            raise ValueError("a pipeline needs at least one slot")
+        self.slots = list(slots)
+        self.depth = len(self.slots)
+        self.shard = shard_batch
+        self.device = torch.device(device)
+        self.comm = comm or default_comm(group)
+        self.world, self.rank = self.comm.world, self.comm.rank
+        self.global_batch = shard_batch * self.world
+        for s in self.slots:
+            if tuple(s.input.shape[:1]) != (shard_batch,) or not s.input.is_contiguous():
+                raise ValueError("every slot's input must be a contiguous [shard, ...] tensor")
+        self.out_shape = (shard_batch,) + tuple(out_shape)
+        self._pad = None
+        self.y_all = None
+        if self.rank == 0 and self.world > 1:
+            self.y_all = [torch.zeros((self.global_batch,) + tuple(out_shape), dtype=out_dtype, device=self.device)
+                          for _ in self.slots]
+        self._aio = bool(getattr(self.comm, "supports_async", False)) and self.world > 1
+        self._kw = {"wait": False} if self._aio else {}
+        self._pending: deque = deque()
+        self._i = 0
+
+    def _send_buffer(self, x: torch.Tensor) -> torch.Tensor:
+        n = x.shape[0]
+        if n == self.global_batch and x.is_contiguous() and x.dtype == self.slots[0].input.dtype \
+                and x.device == self.device:
+            return x
+        if self._pad is None:
+            self._pad = torch.zeros((self.global_batch,) + tuple(self.slots[0].input.shape[1:]),
+                                    dtype=self.slots[0].input.dtype, device=self.device)
+        self._pad[:n].copy_(x, non_blocking=True)
+        if n < self.global_batch:
+            self._pad[n:].zero_()
+        return self._pad
+
+    def submit(self, x: torch.Tensor | None = None) -> torch.Tensor | None:
+        """Collective: every rank calls it once per step; rank 0 passes the global batch."""
+        k = self._i % self.depth
+        slot = self.slots[k]
+        n = 0
+        if self.rank == 0:
+            n = x.shape[0]
+            if n > self.global_batch:
+                raise ValueError(f"batch {n} exceeds world*shard = {self.global_batch}")
+            if self.world == 1:
+                if x.data_ptr() != slot.input.data_ptr():
+                    slot.input[:n].copy_(x, non_blocking=True)
+                if n < self.shard:
+                    slot.input[n:].zero_()
+            else:
+                send = self._send_buffer(x)
+                self.comm.scatter(slot.input, list(send.chunk(self.world)), src=0, **self._kw)
+        elif self.world > 1:
+            self.comm.scatter(slot.input, None, src=0, **self._kw)
+        slot.launch()
+        self._pending.append((k, n))
+        self._i += 1
+        return self._retire() if len(self._pending) == self.depth else None
+
+    def _retire(self) -> torch.Tensor | None:
+        k, n = self._pending.popleft()
+        y = self.slots[k].join().reshape(self.out_shape)
+        if self.world == 1:
+            return y[:n]
+        outs = list(self.y_all[k].chunk(self.world)) if self.rank == 0 else None
+        self.comm.gather(y if y.is_contiguous() else y.contiguous(), outs, dst=0, **self._kw)
+        return self.y_all[k][:n] if self.rank == 0 else None
+
+    def flush(self) -> list:
+        """Retire every pending step, oldest first (their gathers are issued now)."""
+        out = []
+        while self._pending:
+            out.append(self._retire())
+        return out
+
+    def sync(self) -> None:
+        """Host wait for everything issued so far (bounded on the native RCCL communicator)."""
+        if self._aio:
             self.comm.sync(torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else None)
         elif self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()

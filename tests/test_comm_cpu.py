@@ -110,3 +110,39 @@ def test_mapped_rccl_report_parses_maps():
     assert mapped_rccl("7f00-7f10 r-xp 00000000 08:01 1 /opt/rocm/lib/librccl.so.1")["torch_bundled"] is False
     live = mapped_rccl()  # this process: whatever is mapped, a well-formed report
     assert set(live) == {"paths", "version", "torch_bundled", "has_comm_shrink"}
+
+
+def _pipe_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipzap.parallel.dp import DPPipeline, FnSlot
+    runner = lambda x: x.sum(dim=1) + 1000 * rank  # noqa: E731
+    pipe = DPPipeline([FnSlot(runner, 2, (4,)) for _ in range(3)], 2, (), "cpu")
+    outs = []
+    for i in range(5):
+        x = torch.arange(4 * 4, dtype=torch.float32).reshape(4, 4) * (i + 1) if rank == 0 else None
+        y = pipe.submit(x)
+        if y is not None:
+            outs.append(y.tolist())
+    outs += [y.tolist() for y in pipe.flush() if y is not None]
+    if rank == 0:
+        q.put(outs)
+    dist.destroy_process_group()
+
+
+def test_dp_pipeline_world2_gloo():
+    """Three DP steps in flight over torch.distributed (gloo, two processes): the five steps'
+    logits come back in order, each row tagged by the rank that computed it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+    assert len(outs) == 5
+    for i, y in enumerate(outs):
+        x = torch.arange(16, dtype=torch.float32).reshape(4, 4) * (i + 1)
+        assert y == (x.sum(dim=1) + torch.tensor([0, 0, 1000, 1000])).tolist()

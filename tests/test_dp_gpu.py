@@ -78,3 +78,28 @@ def test_dp_loopback_world4_with_gpu_replicas(sd):
         assert not isinstance(r, BaseException), r
     assert torch.equal(res[0].reshape(ref.shape), ref)
     assert all(r is None for r in res[1:])
+
+
+def test_dp_pipeline_three_in_flight_matches_engine_bitwise(sd):
+    """DPPipeline over three captured contexts (three batch-8 steps in flight on their own streams,
+    issued from a non-default caller stream with no host sync): every step's logits equal the
+    host path's for its own images, bitwise and in order (the slot reuse and the stream waits)."""
+    from hipzap.parallel.dp import DPPipeline
+    eng = Engine.from_state_dict("resnet18", sd, DEV, batch=8, num_contexts=3, host_io=False)
+    pipe = DPPipeline(eng.pipeline_slots(), 8, tuple(eng.contexts[0].output.shape[1:]), DEV)
+    ref_eng = Engine.from_state_dict("resnet18", sd, DEV, batch=8, num_contexts=1)
+    xs = [_images(8 - (i % 3 == 2), 100 + i) for i in range(7)]
+    caller = torch.cuda.Stream(DEV)
+    outs = []
+    with torch.cuda.stream(caller):
+        for x in xs:
+            y = pipe.submit(x.to(DEV, non_blocking=True))
+            if y is not None:
+                outs.append(y.clone())
+        outs += [y.clone() for y in pipe.flush()]
+    caller.synchronize()
+    assert len(outs) == len(xs)
+    for x, y in zip(xs, outs):
+        full = torch.cat([x, torch.zeros(8 - x.shape[0], *x.shape[1:])]) if x.shape[0] < 8 else x
+        ref = ref_eng.infer(full)[:x.shape[0]]
+        assert torch.equal(y.cpu().reshape(ref.shape), ref)

@@ -125,3 +125,83 @@ def test_dp_step_one_host_sync_per_step():
         assert s3 == 3 and s4 == 3 and a == 8, (r, s3, s4, a)  # 1 sync per step; 2 async collectives per step
     for y in res[0][0]:
         assert torch.equal(y, runner(x))
+
+
+@pytest.mark.parametrize("world,depth", [(1, 1), (1, 3), (2, 2), (4, 3)])
+def test_dp_pipeline_results_and_collective_order(world, depth):
+    """DPPipeline with ``depth`` steps in flight returns every step's logits in order, equal to the
+    blocking one-step executor's (uneven batches included), and issues the collectives in the
+    pipelined order sc0 .. sc(D-1), g0, scD, g1, ... on every rank."""
+    from hipzap.parallel.dp import DPPipeline, FnSlot
+    shard, steps = 3, 7
+    sizes = [world * shard - (i % 2) for i in range(steps)]
+
+    def body(c):
+        log = []
+
+        class Logged:
+            rank, world = c.rank, c.world
+
+            def scatter(self, out, chunks, src=0):
+                log.append("s")
+                c.scatter(out, chunks, src)
+
+            def gather(self, t, outs, dst=0):
+                log.append("g")
+                c.gather(t, outs, dst)
+
+        def runner(x):  # row sums + 1000 * rank
+            return x.sum(dim=1) + 1000 * c.rank
+        slots = [FnSlot(runner, shard, (4,)) for _ in range(depth)]
+        pipe = DPPipeline(slots, shard, (), "cpu", comm=Logged() if world > 1 else c)
+        outs = []
+        for i, n in enumerate(sizes):
+            x = torch.arange(n * 4, dtype=torch.float32).reshape(n, 4) + i if c.rank == 0 else None
+            y = pipe.submit(x)
+            if y is not None:
+                outs.append(y.clone() if c.rank == 0 else None)
+            elif c.rank != 0 and len(log) and log[-1] == "g":
+                outs.append(None)
+        tail = pipe.flush()
+        outs += [t.clone() if t is not None else None for t in tail]
+        return outs, "".join(log)
+
+    res = run_ranks(world, body)
+    outs0, log0 = res[0]
+    assert len(outs0) == steps
+    for i, (n, y) in enumerate(zip(sizes, outs0)):
+        x = torch.arange(n * 4, dtype=torch.float32).reshape(n, 4) + i
+        assert torch.equal(y, x.sum(dim=1) + 1000 * (torch.arange(n) // shard)), i
+    if world > 1:
+        expect = "s" * depth + "gs" * (steps - depth) + "g" * depth
+        assert all(lg == expect for _, lg in res), [lg for _, lg in res]
+
+
+def test_dp_pipeline_depth1_is_the_executor():
+    from hipzap.parallel.dp import DPPipeline, FnSlot
+
+    def fn(c):
+        runner = lambda x: x * 2 + c.rank  # noqa: E731
+        ex = DPExecutor(runner, 2, (3,), (3,), "cpu", comm=c)
+        pipe = DPPipeline([FnSlot(runner, 2, (3,))], 2, (3,), "cpu", comm=c)
+        a, b = [], []
+        for i in range(3):
+            x = torch.randn(4, 3, generator=torch.Generator().manual_seed(i)) if c.rank == 0 else None
+            a.append(ex.step(x))
+            y = pipe.submit(x)  # a view of the gather buffer, valid until the next submit at depth 1
+            b.append(y.clone() if y is not None else None)
+        return a, b, pipe.flush()
+    for r, (a, b, rest) in enumerate(run_ranks(2, fn)):
+        assert rest == []
+        if r == 0:
+            assert all(torch.equal(p, q) for p, q in zip(a, b))
+        else:
+            assert a == b == [None] * 3
+
+
+def test_dp_pipeline_rejects_bad_slots():
+    from hipzap.parallel.dp import DPPipeline, FnSlot
+    with pytest.raises(ValueError):
+        DPPipeline([], 2, (1,), "cpu")
+    with pytest.raises(ValueError):
+        DPPipeline([FnSlot(lambda x: x, 3, (1,))], 2, (1,), "cpu")
