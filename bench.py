@@ -354,7 +354,7 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
     (``parallel/dp.py`` DPExecutor), images/s over the whole job = global batch x K / the slowest
     rank's wall. ResNet-50 at global batch 32 (uint8 images, the headline's broadcast weights)
     and ViT-B/16 fp8 at global batch 64 (random-init weights packed on every rank from the same
-    seed). ``img_s``: ``dp_depth()`` steps in flight (``parallel/dp.py`` DPPipeline: one captured
+    seed). ``img_s``: ``dp_depth(model, shard)`` steps in flight (``parallel/dp.py`` DPPipeline: one captured
     context and stream per in-flight step, collectives in pipelined order on the caller's
     stream; every step's gather issued and completed inside the timed region);
     ``img_s_one_in_flight``: each step alone, back to back. Collectives run on the native RCCL communicator when the headline uses it (bounded
@@ -365,10 +365,10 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
     from hipzap.models import registry
     from hipzap.parallel.comm import is_dist, max_over_ranks
     from hipzap.parallel.dp import DPPipeline
-    depth = dp_depth()
     out = {}
     for name, model, gb in (("resnet50_gb32", args.model, 32), ("vit_b16_fp8_gb64", "vit-b16-fp8", 64)):
         ok, seng, xg = 1.0, None, None
+        depth = dp_depth(model, gb // world)
         try:
             shard = gb // world
             if shard * world != gb:
@@ -432,9 +432,15 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
     return out
 
 
-def dp_depth() -> int:
-    """DP steps in flight per rank for the config 3 / 5 figures (``HIPZAP_DP_DEPTH``, 1-8)."""
-    return max(1, min(8, int(os.environ.get("HIPZAP_DP_DEPTH", "3"))))
+def dp_depth(model: str, shard: int) -> int:
+    """DP steps in flight per rank for the config 3 / 5 figures: ``HIPZAP_DP_DEPTH`` (1-8), else
+    by the measured optimum (profiles/r6_dp_pipeline): 4 for ResNet-50 at any shard and for small
+    ViT shards; 2 for ViT-B/16 fp8 shards of >= 32 images, whose per-step GEMMs already fill the
+    chip (gb64 on one GPU: 23.8k img/s at 2, 23.3k at 3, 22.3k at 4)."""
+    env = os.environ.get("HIPZAP_DP_DEPTH", "")
+    if env:
+        return max(1, min(8, int(env)))
+    return 2 if "vit" in model and shard >= 32 else 4
 
 
 def dp_shard_figures(args, eng, device) -> dict:
@@ -460,7 +466,7 @@ def dp_shard_figures(args, eng, device) -> dict:
             res[name] = {"img_s": round(shard * iters / t, 2), "ms_per_batch": round(t / iters * 1e3, 4),
                          "batch": shard, "node_upper_img_s": round(8 * shard * iters / t, 2), "model": model}
             del seng
-            depth = dp_depth()
+            depth = dp_depth(model, shard)
             if depth > 1:  # the same shard program with D batches in flight (DPPipeline's compute side)
                 seng = Engine(model, params, device, batch=shard, num_contexts=depth, arch_kw=arch_kw, host_io=False)
                 seng.bench(max(5, args.warmup))

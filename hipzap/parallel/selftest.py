@@ -126,6 +126,26 @@ def run_torch(rank: int, world: int, rdzv_dir: str) -> dict:
         torch.cuda.synchronize(dev)
         checks["dp_vs_shards_alone"] = torch.equal(y_sync.reshape(alone.shape), alone)
         checks["dp_async_equals_sync"] = torch.equal(y_sync, y_async)
+    # DPPipeline over RCCL: three steps in flight (three contexts), five different global batches;
+    # every step's gathered logits == its shards run alone
+    from .dp import DPPipeline
+    eng3 = Engine("resnet18", params, dev, batch=shard, num_contexts=3, arch_kw=kw, host_io=False)
+    pipe = DPPipeline(eng3.pipeline_slots(), shard, tuple(cout.shape[1:]), dev, out_dtype=cout.dtype, comm=comm)
+    xs = [xg * (0.5 + i) if rank == 0 else None for i in range(5)]
+    got = []
+    for x in xs:
+        y = pipe.submit(x)
+        if y is not None:
+            got.append(y.clone())
+    got += [y.clone() for y in pipe.flush() if y is not None]
+    pipe.sync()
+    if rank == 0:
+        ok = len(got) == len(xs)
+        for x, y in zip(xs, got):
+            alone = torch.cat([eng.infer_device(x[r * shard:(r + 1) * shard]).clone() for r in range(world)])
+            torch.cuda.synchronize(dev)
+            ok = ok and torch.equal(y.reshape(alone.shape), alone)
+        checks["dp_pipeline_vs_shards_alone"] = ok
     comm.close()
     return {"rank": rank, "world": world, "mode": "torch", "ok": all(checks.values()), "checks": checks}
 

@@ -5,7 +5,8 @@ multi-GPU node. Every rank is a FRESH process (hipzap/parallel/selftest.py), one
   returning N, over the native communicator (csrc/comm/comm.cpp);
 * torch-imported processes (bench.py's library mix): the same through the tensor interface, and
   DPExecutor over RCCL (ResNet-18 global batch scattered / run per shard / gathered) bitwise equal
-  to rank 0 running every shard alone, including the one-host-sync asynchronous step;
+  to rank 0 running every shard alone, including the one-host-sync asynchronous step, and
+  DPPipeline with three steps in flight (the collectives in pipelined order);
 * the node-level cold start (hipzap/coldstart.py measure_node): N torch-free plan workers, RCCL
   rendezvous, rank 0 broadcasts the weight blob, every rank serves a finite first request.
 """
@@ -72,6 +73,7 @@ def test_rccl_collectives_and_dp_with_torch_loaded():
     for o in outs:
         assert o["ok"], o
     assert outs[0]["checks"]["dp_vs_shards_alone"] and outs[0]["checks"]["dp_async_equals_sync"]
+    assert outs[0]["checks"]["dp_pipeline_vs_shards_alone"]
 
 
 @multi
