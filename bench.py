@@ -225,6 +225,13 @@ def fresh_cold_start(args, device_index: int, world: int = 1) -> dict:
     if "error" in il["plan"]:
         raise RuntimeError(f"plan cold start failed: {il['plan']['error']}")
     res = {"plan": il["plan"]}
+    # the same plan trials back to back (no idle gap): each child's HIP init then overlaps the driver's
+    # teardown of the previous child (hipzap/coldstart.py trial_gap_s, profiles/r6_cold)
+    try:
+        res["plan_back_to_back"] = measure_fresh("plan", plan, args.model, args.cold_trials, device=device_index,
+                                                 gap_s=0.0)
+    except Exception as e:  # noqa: BLE001 - secondary figure
+        print(f"back-to-back plan cold start skipped: {e}", file=sys.stderr)
     from hipzap.coldstart import isolated_env, narrow_env
     res["narrowing"] = narrow_env(os.environ, device_index)[2] if isolated_env(None, device_index)[0] is not None \
         else "unchanged"
@@ -888,8 +895,14 @@ def main():
                        ("torch.distributed" if world > 1 else None)},
             "rccl_mapped": rccl_map,
             "cold_start_ms_p50": fresh["plan"]["p50_ms"] if fresh else None,
+            # the same trials back to back (no idle gap before each child)
+            "cold_start_back_to_back_ms_p50": ((fresh or {}).get("plan_back_to_back") or {}).get("p50_ms"),
+            "cold_start_gap_ms": (fresh or {}).get("plan", {}).get("gap_ms"),
             "cold_start_note": "p50 over fresh processes, spawn -> first logits, from the .hzplan deploy artifact "
-                               "(torch-free runtime); cold_start_pth_ms_p50 = same from the .pth state_dict "
+                               "(torch-free runtime), each child started on an idle GPU (cold_start_gap_ms after "
+                               "the previous child exited: back to back, the driver's teardown of the previous "
+                               "process delays the next one's HIP init by ~130 ms, profiles/r6_cold; that set is "
+                               "cold_start_back_to_back_ms_p50); cold_start_pth_ms_p50 = same from the .pth state_dict "
                                "without torch (weights-only zip reader + plan template + device-side packing; "
                                "cold_start_pth_torch_ms_p50: import torch + torch.load + pack); "
                                "each child sees only its own GPU (ROCR_VISIBLE_DEVICES, a one-GPU worker) unless "

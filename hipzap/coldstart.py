@@ -344,17 +344,22 @@ def _fresh_cmd(mode: str, path: str, model: str, device: int, extra_args: list |
             *(extra_args or [])]
 
 
+COLD_GAP_MS_DEFAULT = 300.0
+
+
 def trial_gap_s() -> float:
-    """Idle time before each fresh-process trial (``HIPZAP_COLD_GAP_MS``, default 0): back to back,
-    a child's HIP init overlaps the kernel driver's teardown of the previous child's GPU process
-    state, which a serverless cold start (no process just exited on that GPU) does not pay."""
-    return max(0.0, float(os.environ.get("HIPZAP_COLD_GAP_MS", "0"))) / 1e3
+    """Idle time before each fresh-process trial (``HIPZAP_COLD_GAP_MS``, default 300 ms). Back to
+    back, a child's HIP init overlaps the kernel driver's asynchronous teardown of the previous
+    child's GPU process state (its ``hsa_init`` waits ~130 ms longer: profiles/r6_cold), which a
+    serverless cold start -- a new process on a GPU nobody just left -- does not pay. ``0``: back
+    to back (bench.py also reports that set for the plan image)."""
+    return max(0.0, float(os.environ.get("HIPZAP_COLD_GAP_MS", str(COLD_GAP_MS_DEFAULT)))) / 1e3
 
 
-def _fresh_trial(cmd: list, mode: str, env, timeout: float) -> tuple[float, dict]:
+def _fresh_trial(cmd: list, mode: str, env, timeout: float, gap_s: float | None = None) -> tuple[float, dict]:
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    gap = trial_gap_s()
+    gap = trial_gap_s() if gap_s is None else gap_s
     if gap:
         time.sleep(gap)
     t = time.time()
@@ -388,17 +393,20 @@ def _fresh_summary(mode: str, walls: list, res: list) -> dict:
 
 
 def measure_fresh(mode: str, path: str, model: str = "resnet50", trials: int = 5, device: int = 0,
-                  timeout: float = 300.0, env: dict | None = None, extra_args: list | None = None) -> dict:
+                  timeout: float = 300.0, env: dict | None = None, extra_args: list | None = None,
+                  gap_s: float | None = None) -> dict:
     """Spawn ``trials`` fresh processes of this module; p50/min/max of spawn -> first logits and
-    the child-reported phases of the median trial. Raises if any child fails."""
+    the child-reported phases of the median trial. Raises if any child fails. ``gap_s``: idle
+    time before each trial (default ``trial_gap_s()``)."""
     env, device = isolated_env(env, device)
     cmd = _fresh_cmd(mode, path, model, device, extra_args)
+    gap = trial_gap_s() if gap_s is None else gap_s
     walls, res = [], []
     for _ in range(trials):
-        w, out = _fresh_trial(cmd, mode, env, timeout)
+        w, out = _fresh_trial(cmd, mode, env, timeout, gap)
         walls.append(w)
         res.append(out)
-    return dict(_fresh_summary(mode, walls, res), child_env=child_environment(env))
+    return dict(_fresh_summary(mode, walls, res), child_env=child_environment(env), gap_ms=round(gap * 1e3, 1))
 
 
 def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, timeout: float = 300.0,
@@ -430,6 +438,7 @@ def measure_fresh_interleaved(runs: dict, trials: int = 5, device: int = 0, time
         out[name] = _fresh_summary(runs[name][0], walls[name], res[name])
         out[name]["interleaved_with"] = sorted(n for n in runs if n != name)
         out[name]["child_env"] = cenv
+        out[name]["gap_ms"] = round(trial_gap_s() * 1e3, 1)
     return out
 
 

@@ -27,6 +27,25 @@ def main():
     a = registry.get("bert-base")
     torch.manual_seed(0)
     sd = a.make_model().eval().state_dict()
+    mode = _arg("--mode", "")
+    if mode:  # process-state probe: one 4-context figure after a given history (run each in a fresh process)
+        if mode.startswith("after1"):
+            e1 = Engine.from_state_dict("bert-base", sd, "cuda:0", batch=16, num_contexts=1)
+            e1.bench(20)
+            del e1
+            torch.cuda.synchronize()
+        eng = Engine.from_state_dict("bert-base", sd, "cuda:0", batch=16, num_contexts=4)
+        if mode.endswith("infer"):
+            x = a.example_input(16)
+            for _ in range(21):
+                eng.infer(x)
+        eng.bench(10)
+        rates = []
+        for _ in range(3):
+            t = eng.bench(200)
+            rates.append(round(16 * 4 * 200 / t, 1))
+        print(json.dumps({"mode": mode, "contexts": 4, "seq_s": rates}), flush=True)
+        return
     for c in ctxs:
         eng = Engine.from_state_dict("bert-base", sd, "cuda:0", batch=16, num_contexts=c)
         eng.bench(10)

@@ -81,3 +81,24 @@ def test_child_argv_parser():
     for bad in (["plan"], ["bogus", "p"], ["plan", "p", "--nope"], ["plan", "p", "--rank"], ["plan", "p", "q"]):
         with pytest.raises(SystemExit):
             cs._parse(bad)
+
+
+def test_trial_gap_default_and_override(monkeypatch):
+    """Each fresh cold-start child starts on an idle GPU by default (300 ms after the previous one
+    exited); HIPZAP_COLD_GAP_MS=0 gives the back-to-back trials; a per-call gap wins over both."""
+    from hipzap import coldstart
+    monkeypatch.delenv("HIPZAP_COLD_GAP_MS", raising=False)
+    assert coldstart.trial_gap_s() == 0.3
+    monkeypatch.setenv("HIPZAP_COLD_GAP_MS", "0")
+    assert coldstart.trial_gap_s() == 0.0
+    slept = []
+    monkeypatch.setattr(coldstart.time, "sleep", slept.append)
+
+    class R:
+        returncode, stderr = 0, ""
+        stdout = '{"t_first": 1e12, "phases_ms": {}}\n'
+    import subprocess
+    monkeypatch.setattr(subprocess, "run", lambda *a, **k: R())
+    coldstart._fresh_trial(["x"], "plan", None, 1.0, 0.05)
+    coldstart._fresh_trial(["x"], "plan", None, 1.0)
+    assert slept == [0.05]
