@@ -107,7 +107,7 @@ class Engine:
             if k > 0 and idx >= k:
                 streams.append(pool[idx % k])
             else:
-                st = torch.cuda.Stream(device=self.device)
+                st = _context_stream(self.device)
                 pool.append(st)
                 streams.append(st)
         return ctxs, streams
@@ -360,6 +360,44 @@ class Engine:
         return {"model": self.model, "batch": self.batch, "contexts": len(self.contexts),
                 "ops": c.num_ops(), "arena_MB": round(c.arena_bytes / 2**20, 2),
                 "captured": c.captured, "timings_ms": {k: round(v, 2) for k, v in self.timings.items()}}
+
+
+def _context_stream(device):
+    """A request context's stream. ``HIPZAP_STREAM_KIND``: ``torch`` (default: torch's stream pool,
+    whose 32 streams per priority share the process's 4 hardware queues in creation order),
+    ``native`` (a fresh ``hipStreamCreateWithFlags`` stream) or ``cumask`` (a stream created with a
+    full CU mask: HIP gives a CU-masked stream a hardware queue of its own instead of sharing one)."""
+    kind = os.environ.get("HIPZAP_STREAM_KIND", "torch")
+    if kind == "torch":
+        return torch.cuda.Stream(device=device)
+    import ctypes as C
+    import weakref
+    from .. import hip as H
+    h = H.hip()
+    p = C.c_void_p()
+    with torch.cuda.device(device):
+        if kind == "cumask":
+            f = h.hipExtStreamCreateWithCUMask
+            f.restype, f.argtypes = C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+            ncu = torch.cuda.get_device_properties(device).multi_processor_count
+            words = (ncu + 31) // 32
+            mask = (C.c_uint32 * words)(*([0xFFFFFFFF] * words))
+            H.check(f(C.byref(p), words, mask), "hipExtStreamCreateWithCUMask")
+        elif kind == "native":
+            H.check(h.hipStreamCreateWithFlags(C.byref(p), 1), "hipStreamCreateWithFlags")
+        else:
+            raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: torch, native or cumask")
+    st = torch.cuda.ExternalStream(p.value, device=device)
+    destroy = h.hipStreamDestroy
+    destroy.restype, destroy.argtypes = C.c_int, [C.c_void_p]
+    try:
+        weakref.finalize(st, destroy, p.value)
+    except TypeError:  # not weak-referenceable on this torch: the stream lives as long as the process
+        _KEEP_STREAMS.append(p.value)
+    return st
+
+
+_KEEP_STREAMS: list = []
 
 
 class _EngineSlot:
