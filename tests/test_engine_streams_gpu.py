@@ -1,0 +1,45 @@
+"""Request-context streams (engine.py ``stream_kind``): an engine of 2-4 contexts gets one
+full-CU-mask stream per context (a hardware queue each), more contexts share torch's stream pool.
+The logits do not depend on which: every context of a dedicated-queue engine gives bitwise the
+pooled engine's output, and concurrent replays on the dedicated queues stay correct."""
+import pytest
+import torch
+
+from hipzap.engine.engine import Engine, stream_kind
+from hipzap.models import registry
+from hipzap.models.resnet import randomize_bn
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def test_stream_kind_policy(monkeypatch):
+    monkeypatch.delenv("HIPZAP_STREAM_KIND", raising=False)
+    assert [stream_kind(n) for n in (1, 2, 4, 5, 16)] == ["torch", "cumask", "cumask", "torch", "torch"]
+    monkeypatch.setenv("HIPZAP_STREAM_KIND", "native")
+    assert stream_kind(4) == "native"
+
+
+def test_dedicated_queue_contexts_match_pooled_bitwise(monkeypatch):
+    torch.manual_seed(0)
+    sd = randomize_bn(registry.get("resnet18").make_model()).eval().state_dict()
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(5))
+    monkeypatch.setenv("HIPZAP_STREAM_KIND", "torch")
+    ref_eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=1)
+    ref = ref_eng.infer(x)
+    monkeypatch.delenv("HIPZAP_STREAM_KIND")
+    eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=3, host_io=False)
+    assert all(getattr(s, "hz_raw", None) for s in eng.streams)  # dedicated (CU-masked) streams
+    xd = x.to(DEV)
+    outs = [eng.infer_device(xd, i).clone() for i in range(3)]
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o.cpu().reshape(ref.shape), ref)
+    eng.bench(20)  # every context replayed concurrently on its own queue
+    outs2 = [c.output.clone() for c in eng.contexts]
+    torch.cuda.synchronize()
+    for o in outs2:
+        assert torch.equal(o.cpu().reshape(ref.shape), ref)
+    del eng
+    import gc
+    gc.collect()  # the engine's own streams are destroyed with it
