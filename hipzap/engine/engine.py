@@ -107,20 +107,15 @@ class Engine:
             if k > 0 and idx >= k:
                 streams.append(pool[idx % k])
             else:
-                st = _context_stream(self.device, self.num_contexts)
-                if getattr(st, "hz_raw", None):
-                    if not hasattr(self, "_raw_streams"):
-                        import weakref
-                        self._raw_streams = []
-                        weakref.finalize(self, _destroy_streams, self._raw_streams)
-                    self._raw_streams.append(st.hz_raw)
+                st = _context_stream(self.device, self.num_contexts, idx)
                 pool.append(st)
                 streams.append(st)
         return ctxs, streams
 
     def _capture_all(self, ctxs, streams) -> None:
         if self._capture:
-            shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0
+            # the dedicated-queue streams are shared by every engine of <= 4 contexts in the process
+            shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0 or stream_kind(self.num_contexts) == "cumask"
             cap = torch.cuda.Stream(device=self.device) if shared else None
             for c, s in zip(ctxs, streams):
                 # a shared stream may carry other contexts' replays (other threads) that a capture
@@ -389,17 +384,37 @@ def stream_kind(num_contexts: int) -> str:
     return kind
 
 
-def _context_stream(device, num_contexts: int = 1):
-    """A request context's stream of the kind ``stream_kind(num_contexts)`` picks."""
+_DEDICATED: dict = {}  # device index -> the process's dedicated-queue streams (never destroyed)
+
+
+def _context_stream(device, num_contexts: int = 1, index: int = 0):
+    """Context ``index``'s stream, of the kind ``stream_kind(num_contexts)`` picks. The CU-masked
+    streams are a per-process pool of at most ``DEDICATED_QUEUE_MAX_CONTEXTS`` per device, shared by
+    every engine that takes them (context i gets stream i) and alive until the process ends: a
+    hardware queue per engine rebuild would pile up queues, and a destroyed stream may still be
+    recorded on a tensor the caching allocator frees later (``Tensor.record_stream``)."""
     kind = stream_kind(num_contexts)
     if kind == "torch":
         return torch.cuda.Stream(device=device)
+    if kind == "native":
+        return torch.cuda.ExternalStream(_new_hip_stream(device, False), device=device)
+    dev = torch.device(device)
+    dev_i = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = _DEDICATED.setdefault(dev_i, [])
+    while len(pool) <= index % DEDICATED_QUEUE_MAX_CONTEXTS:
+        pool.append(torch.cuda.ExternalStream(_new_hip_stream(dev, True), device=dev))
+    return pool[index % DEDICATED_QUEUE_MAX_CONTEXTS]
+
+
+def _new_hip_stream(device, cumask: bool) -> int:
+    """A new non-blocking HIP stream; ``cumask``: created with a full CU mask, which HIP backs with
+    a hardware queue of its own."""
     import ctypes as C
     from .. import hip as H
     h = H.hip()
     p = C.c_void_p()
     with torch.cuda.device(device):
-        if kind == "cumask":
+        if cumask:
             f = h.hipExtStreamCreateWithCUMask
             f.restype, f.argtypes = C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
             ncu = torch.cuda.get_device_properties(device).multi_processor_count
@@ -408,22 +423,7 @@ def _context_stream(device, num_contexts: int = 1):
             H.check(f(C.byref(p), words, mask), "hipExtStreamCreateWithCUMask")
         else:
             H.check(h.hipStreamCreateWithFlags(C.byref(p), 1), "hipStreamCreateWithFlags")
-    st = torch.cuda.ExternalStream(p.value, device=device)
-    st.hz_raw = p.value  # owned: the engine destroys it (_destroy_streams) when it is collected
-    return st
-
-
-def _destroy_streams(raw: list) -> None:
-    """hipStreamDestroy of an engine's own streams (work still queued on one completes first)."""
-    if not raw:
-        return
-    import ctypes as C
-    from .. import hip as H
-    f = H.hip().hipStreamDestroy
-    f.restype, f.argtypes = C.c_int, [C.c_void_p]
-    for ptr in raw:
-        f(ptr)
-    raw.clear()
+    return p.value
 
 
 class _EngineSlot:

@@ -29,7 +29,11 @@ def test_dedicated_queue_contexts_match_pooled_bitwise(monkeypatch):
     ref = ref_eng.infer(x)
     monkeypatch.delenv("HIPZAP_STREAM_KIND")
     eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=3, host_io=False)
-    assert all(getattr(s, "hz_raw", None) for s in eng.streams)  # dedicated (CU-masked) streams
+    # dedicated (CU-masked) streams from the process pool: a second engine gets the same ones
+    assert all(isinstance(s, torch.cuda.ExternalStream) for s in eng.streams)
+    eng_b = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=2, host_io=False)
+    assert [s.cuda_stream for s in eng_b.streams] == [s.cuda_stream for s in eng.streams[:2]]
+    del eng_b
     xd = x.to(DEV)
     outs = [eng.infer_device(xd, i).clone() for i in range(3)]
     torch.cuda.synchronize()
@@ -40,6 +44,10 @@ def test_dedicated_queue_contexts_match_pooled_bitwise(monkeypatch):
     torch.cuda.synchronize()
     for o in outs2:
         assert torch.equal(o.cpu().reshape(ref.shape), ref)
+    xd2 = x.to(DEV)
+    eng.infer_device(xd2, 1)  # a tensor recorded on a pooled stream, freed after the engine
     del eng
     import gc
-    gc.collect()  # the engine's own streams are destroyed with it
+    gc.collect()
+    del xd2
+    torch.cuda.synchronize()
