@@ -405,21 +405,27 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
         for d in sorted({1, depth}):
             pipe = DPPipeline(seng.pipeline_slots()[:d], gb // world, tuple(cout.shape[1:]), device,
                               out_dtype=cout.dtype, comm=native_comm)
+            # the steps are issued from a non-default stream: the dedicated-queue context streams
+            # (engine.py stream_kind) are blocking streams, which any NULL-stream command would
+            # serialise against
+            issue = torch.cuda.Stream(device)
             try:
-                for _ in range(max(1, args.warmup)):
-                    pipe.submit(xg)
-                pipe.flush()
-                pipe.sync()
+                with torch.cuda.stream(issue):
+                    for _ in range(max(1, args.warmup)):
+                        pipe.submit(xg)
+                    pipe.flush()
+                    pipe.sync()
                 torch.cuda.synchronize(device)
                 if is_dist():
                     dist.barrier()
                 t0 = time.perf_counter()
-                for i in range(args.steps):  # one bounded host sync per 8 steps
-                    pipe.submit(xg)
-                    if i % 8 == 7:
-                        pipe.sync()
-                pipe.flush()  # every step's gather issued: all K steps complete inside the timed region
-                pipe.sync()
+                with torch.cuda.stream(issue):
+                    for i in range(args.steps):  # one bounded host sync per 8 steps
+                        pipe.submit(xg)
+                        if i % 8 == 7:
+                            pipe.sync()
+                    pipe.flush()  # every step's gather issued: all K steps complete inside the timed region
+                    pipe.sync()
                 torch.cuda.synchronize(device)
                 dt = time.perf_counter() - t0
             except Exception as e:  # noqa: BLE001

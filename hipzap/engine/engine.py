@@ -372,7 +372,10 @@ def stream_kind(num_contexts: int) -> str:
     * ``torch``: torch's stream pool, whose streams share the process's 4 hardware queues
       (``GPU_MAX_HW_QUEUES``) in creation order -- two of four contexts can land on one queue;
     * ``native``: a fresh ``hipStreamCreateWithFlags`` stream (shares the same 4 queues);
-    * ``cumask``: a stream created with a full CU mask, which HIP gives a hardware queue of its own;
+    * ``cumask``: a stream created with a full CU mask, which HIP gives a hardware queue of its own.
+      HIP creates it as a BLOCKING stream (no flags argument): a command on the legacy NULL stream
+      waits for its work and vice versa, so drive such contexts from the native executor, the
+      replay loop or a non-default stream (``DPPipeline`` callers: ``bench.py dp_figures``);
     * ``auto``: ``cumask`` for an engine of 2-4 contexts (one queue per context: BERT bs16 with 4
       contexts 23.3k -> 29.0k seq/s), ``torch`` above (16 ResNet-50 bs=1 contexts on 16 dedicated
       queues halve the served rate, 14.3k -> 7.4k: profiles/r6_queues)."""

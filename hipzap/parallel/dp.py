@@ -157,7 +157,10 @@ class DPPipeline:
     ``submit`` returns the oldest pending step's logits once D are pending (else None); ``flush``
     retires every pending step (in order). Rank 0's results are views of per-slot gather buffers,
     valid for the next D - 1 submits. Config 3 as a serving load: one rank keeps D batches moving
-    instead of running each one's latency chain alone (``bench.py`` dp figures, ``in_flight``)."""
+    instead of running each one's latency chain alone (``bench.py`` dp figures, ``in_flight``).
+    Issue from a non-default stream: engines of 2-4 contexts replay on dedicated-queue streams,
+    which HIP creates blocking, so a step issued on the NULL stream would wait for every slot's
+    replay in flight (measured: 44k -> 20k img/s at global batch 32)."""
 
     def __init__(self, slots: list, shard_batch: int, out_shape: tuple, device, out_dtype=torch.float32,
                  group=None, comm: Comm | None = None):

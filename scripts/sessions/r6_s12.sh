@@ -28,3 +28,13 @@ import json,sys; d=json.loads(sys.stdin.read()); x=d.get('dynamic_batching') or 
 print('dyn $1 contexts $2 rep $rep', x.get('inf_s'), 'p50', x.get('latency_ms_p50'), 'p99', x.get('latency_ms_p99'))" | tee -a $OUT/summary.txt
   done
 done
+P="python3 bench.py --cold-trials 0 --lm-cold 0 --bert-cold 0 --dyn-batch 0 --http-clients 0 --dp-figures 1 --config-figures 0 --cold-runs 0 --steps 40 --warmup 5 --sustained-s 0"
+for rep in 1 2; do
+  for k in auto torch; do
+    HIPZAP_STREAM_KIND=$k timeout -k 10 300 $P > $OUT/dp_${k}_$rep.log 2>&1
+    rc=$?; [ $rc -eq 0 ] || { tail -5 $OUT/dp_${k}_$rep.log; exit $rc; }
+    grep '^{' $OUT/dp_${k}_$rep.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); dp=d.get('dp_scatter') or {}; sh=dp.get('dp_shard_w8') or {}
+print('dp $k rep $rep gb32', (dp.get('resnet50_gb32') or {}).get('img_s'), 'one', (dp.get('resnet50_gb32') or {}).get('img_s_one_in_flight'), 'vit', (dp.get('vit_b16_fp8_gb64') or {}).get('img_s'), 'bs4', (sh.get('resnet50_bs4') or {}).get('img_s_in_flight'), 'vit8', (sh.get('vit_b16_fp8_bs8') or {}).get('img_s_in_flight'))" | tee -a $OUT/summary.txt
+  done
+done
