@@ -382,8 +382,8 @@ def stream_kind(num_contexts: int) -> str:
     kind = os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
         return "cumask" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
-    if kind not in ("torch", "native", "cumask"):
-        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, native or cumask")
+    if kind not in ("torch", "hiprio", "native", "cumask"):
+        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, native or cumask")
     return kind
 
 
@@ -399,6 +399,8 @@ def _context_stream(device, num_contexts: int = 1, index: int = 0):
     kind = stream_kind(num_contexts)
     if kind == "torch":
         return torch.cuda.Stream(device=device)
+    if kind == "hiprio":  # torch's high-priority pool: HIP keeps a separate set of 4 queues per priority
+        return torch.cuda.Stream(device=device, priority=-1)
     if kind == "native":
         return torch.cuda.ExternalStream(_new_hip_stream(device, False), device=device)
     dev = torch.device(device)
