@@ -115,7 +115,8 @@ class Engine:
     def _capture_all(self, ctxs, streams) -> None:
         if self._capture:
             # the dedicated-queue streams are shared by every engine of <= 4 contexts in the process
-            shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0 or stream_kind(self.num_contexts) == "cumask"
+            shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0 or \
+                stream_kind(self.num_contexts) in ("cumask", "hiprio")
             cap = torch.cuda.Stream(device=self.device) if shared else None
             for c, s in zip(ctxs, streams):
                 # a shared stream may carry other contexts' replays (other threads) that a capture
@@ -382,8 +383,8 @@ def stream_kind(num_contexts: int) -> str:
     kind = os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
         return "cumask" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
-    if kind not in ("torch", "hiprio", "native", "cumask"):
-        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, native or cumask")
+    if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask"):
+        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native or cumask")
     return kind
 
 
@@ -399,27 +400,38 @@ def _context_stream(device, num_contexts: int = 1, index: int = 0):
     kind = stream_kind(num_contexts)
     if kind == "torch":
         return torch.cuda.Stream(device=device)
-    if kind == "hiprio":  # torch's high-priority pool: HIP keeps a separate set of 4 queues per priority
+    if kind == "hiprio_torch":  # torch's high-priority pool (its 32 streams share the 4 high-priority queues)
         return torch.cuda.Stream(device=device, priority=-1)
     if kind == "native":
-        return torch.cuda.ExternalStream(_new_hip_stream(device, False), device=device)
+        return torch.cuda.ExternalStream(_new_hip_stream(device, "native"), device=device)
     dev = torch.device(device)
     dev_i = dev.index if dev.index is not None else torch.cuda.current_device()
-    pool = _DEDICATED.setdefault(dev_i, [])
+    pool = _DEDICATED.setdefault((dev_i, kind), [])
     while len(pool) <= index % DEDICATED_QUEUE_MAX_CONTEXTS:
-        pool.append(torch.cuda.ExternalStream(_new_hip_stream(dev, True), device=dev))
+        pool.append(torch.cuda.ExternalStream(_new_hip_stream(dev, kind), device=dev))
     return pool[index % DEDICATED_QUEUE_MAX_CONTEXTS]
 
 
-def _new_hip_stream(device, cumask: bool) -> int:
-    """A new non-blocking HIP stream; ``cumask``: created with a full CU mask, which HIP backs with
-    a hardware queue of its own."""
+def _new_hip_stream(device, kind: str) -> int:
+    """A new HIP stream: ``cumask`` -- created with a full CU mask, which HIP backs with a hardware
+    queue of its own (a blocking stream: the API takes no flags); ``hiprio`` -- non-blocking at the
+    highest priority (HIP keeps a separate set of up to 4 queues per priority, and nothing else in
+    this process asks for high priority, so the pool's first four get four queues of their own);
+    ``native`` -- plain non-blocking."""
     import ctypes as C
     from .. import hip as H
     h = H.hip()
     p = C.c_void_p()
     with torch.cuda.device(device):
-        if cumask:
+        if kind == "hiprio":
+            lo, hi = C.c_int(0), C.c_int(0)
+            g = h.hipDeviceGetStreamPriorityRange
+            g.restype, g.argtypes = C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int)]
+            H.check(g(C.byref(lo), C.byref(hi)), "hipDeviceGetStreamPriorityRange")
+            f = h.hipStreamCreateWithPriority
+            f.restype, f.argtypes = C.c_int, [C.POINTER(C.c_void_p), C.c_uint, C.c_int]
+            H.check(f(C.byref(p), 1, hi.value), "hipStreamCreateWithPriority")
+        elif kind == "cumask":
             f = h.hipExtStreamCreateWithCUMask
             f.restype, f.argtypes = C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
             ncu = torch.cuda.get_device_properties(device).multi_processor_count

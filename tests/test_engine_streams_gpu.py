@@ -18,6 +18,9 @@ def test_stream_kind_policy(monkeypatch):
     assert [stream_kind(n) for n in (1, 2, 4, 5, 16)] == ["torch", "cumask", "cumask", "torch", "torch"]
     monkeypatch.setenv("HIPZAP_STREAM_KIND", "native")
     assert stream_kind(4) == "native"
+    monkeypatch.setenv("HIPZAP_STREAM_KIND", "bogus")
+    with pytest.raises(ValueError):
+        stream_kind(2)
 
 
 def test_dedicated_queue_contexts_match_pooled_bitwise(monkeypatch):
