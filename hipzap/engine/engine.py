@@ -116,7 +116,7 @@ class Engine:
         if self._capture:
             # the dedicated-queue streams are shared by every engine of <= 4 contexts in the process
             shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0 or \
-                stream_kind(self.num_contexts) in ("cumask", "hiprio")
+                stream_kind(self.num_contexts) == "cumask"
             cap = torch.cuda.Stream(device=self.device) if shared else None
             for c, s in zip(ctxs, streams):
                 # a shared stream may carry other contexts' replays (other threads) that a capture
@@ -382,7 +382,7 @@ def stream_kind(num_contexts: int) -> str:
       queues halve the served rate, 14.3k -> 7.4k: profiles/r6_queues)."""
     kind = os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
-        return "cumask" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
+        return "hiprio" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
     if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask"):
         raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native or cumask")
     return kind
@@ -402,8 +402,8 @@ def _context_stream(device, num_contexts: int = 1, index: int = 0):
         return torch.cuda.Stream(device=device)
     if kind == "hiprio_torch":  # torch's high-priority pool (its 32 streams share the 4 high-priority queues)
         return torch.cuda.Stream(device=device, priority=-1)
-    if kind == "native":
-        return torch.cuda.ExternalStream(_new_hip_stream(device, "native"), device=device)
+    if kind in ("native", "hiprio"):  # fresh streams for every engine (never destroyed: see above)
+        return torch.cuda.ExternalStream(_new_hip_stream(device, kind), device=device)
     dev = torch.device(device)
     dev_i = dev.index if dev.index is not None else torch.cuda.current_device()
     pool = _DEDICATED.setdefault((dev_i, kind), [])
