@@ -53,11 +53,12 @@ class Engine:
     def __init__(self, model: str, params: dict, device="cuda:0", batch: int = 1, num_contexts: int = 1,
                  capture: bool = True, tuned: dict | None = None, arch_kw: dict | None = None, timings=None,
                  host_io: bool = True, probs: bool = False, zero_copy: str | None = None,
-                 eager_contexts: int | None = None):
+                 eager_contexts: int | None = None, stream_kind: str | None = None):
         """``eager_contexts``: plan + capture only this many of the ``num_contexts`` request
         contexts before the engine is ready (cold start = time to the first served request); the
         rest are built by :meth:`ensure_contexts` (``bench`` calls it), e.g. after the first
-        request, the way a warm container scales up its concurrency. None: all up front."""
+        request, the way a warm container scales up its concurrency. None: all up front.
+        ``stream_kind``: the contexts' streams (module ``stream_kind``; None: ``HIPZAP_STREAM_KIND``)."""
         self.model = model
         self.adapter = registry.get(model)
         self.device = torch.device(device)
@@ -69,6 +70,7 @@ class Engine:
             tuned = load_tuning(model, batch, num_contexts)
         self.tuned = tuned
         self.num_contexts = num_contexts
+        self._stream_kind = stream_kind
         self._capture, self._zero_copy = capture, zero_copy
         n0 = num_contexts if eager_contexts is None else max(1, min(eager_contexts, num_contexts))
         t0 = time.perf_counter()
@@ -107,7 +109,7 @@ class Engine:
             if k > 0 and idx >= k:
                 streams.append(pool[idx % k])
             else:
-                st = _context_stream(self.device, self.num_contexts, idx)
+                st = _context_stream(self.device, self.num_contexts, idx, self._stream_kind)
                 pool.append(st)
                 streams.append(st)
         return ctxs, streams
@@ -116,7 +118,7 @@ class Engine:
         if self._capture:
             # the dedicated-queue streams are shared by every engine of <= 4 contexts in the process
             shared = int(os.environ.get("HIPZAP_CTX_STREAMS", "0")) > 0 or \
-                stream_kind(self.num_contexts) == "cumask"
+                stream_kind(self.num_contexts, self._stream_kind) == "cumask"
             cap = torch.cuda.Stream(device=self.device) if shared else None
             for c, s in zip(ctxs, streams):
                 # a shared stream may carry other contexts' replays (other threads) that a capture
@@ -367,20 +369,26 @@ class Engine:
 DEDICATED_QUEUE_MAX_CONTEXTS = 4
 
 
-def stream_kind(num_contexts: int) -> str:
-    """Which stream a request context gets (``HIPZAP_STREAM_KIND``, default ``auto``):
+def stream_kind(num_contexts: int, kind: str | None = None) -> str:
+    """Which stream a request context gets (``kind``, else ``HIPZAP_STREAM_KIND``, default ``auto``;
+    measurements in profiles/r6_queues):
 
-    * ``torch``: torch's stream pool, whose streams share the process's 4 hardware queues
-      (``GPU_MAX_HW_QUEUES``) in creation order -- two of four contexts can land on one queue;
-    * ``native``: a fresh ``hipStreamCreateWithFlags`` stream (shares the same 4 queues);
-    * ``cumask``: a stream created with a full CU mask, which HIP gives a hardware queue of its own.
-      HIP creates it as a BLOCKING stream (no flags argument): a command on the legacy NULL stream
-      waits for its work and vice versa, so drive such contexts from the native executor, the
-      replay loop or a non-default stream (``DPPipeline`` callers: ``bench.py dp_figures``);
-    * ``auto``: ``cumask`` for an engine of 2-4 contexts (one queue per context: BERT bs16 with 4
-      contexts 23.3k -> 29.0k seq/s), ``torch`` above (16 ResNet-50 bs=1 contexts on 16 dedicated
-      queues halve the served rate, 14.3k -> 7.4k: profiles/r6_queues)."""
-    kind = os.environ.get("HIPZAP_STREAM_KIND", "auto")
+    * ``torch``: torch's stream pool. Its streams share the process's 4 normal-priority hardware
+      queues (``GPU_MAX_HW_QUEUES``), and which queue a stream lands on depends on what else the
+      process created before it: the same 4-context BERT engine replays at 23.3k or 29.9k seq/s
+      from one process to the next, the batch-4 ResNet shard at 19.6k or 25.5k img/s.
+    * ``hiprio``: fresh non-blocking streams at the highest priority for every engine. HIP keeps a
+      separate set of queues per priority and nothing else here asks for high priority, so an
+      engine's 2-4 contexts land on distinct queues every time (BERT 4 contexts 28.1-28.6k seq/s
+      in any process history). Never destroyed (a destroyed stream may still be recorded on a
+      tensor the caching allocator frees later); an engine is built once per serving process.
+    * ``hiprio_torch``: torch's high-priority pool; ``native``: fresh normal-priority streams;
+      ``cumask``: a per-process pool of full-CU-mask streams (a queue each, but BLOCKING: a NULL-
+      stream command waits for their work). Measured, not defaults.
+    * ``auto``: ``hiprio`` for engines of 2-4 contexts, ``torch`` otherwise -- 16 ResNet-50 bs=1
+      contexts need the shared queues (16 queues of their own: 14.3k -> 7.4k inf/s), and a
+      DPPipeline over big batches does better on them too (``bench.py`` passes ``torch``)."""
+    kind = kind or os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
         return "hiprio" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
     if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask"):
@@ -391,13 +399,13 @@ def stream_kind(num_contexts: int) -> str:
 _DEDICATED: dict = {}  # device index -> the process's dedicated-queue streams (never destroyed)
 
 
-def _context_stream(device, num_contexts: int = 1, index: int = 0):
+def _context_stream(device, num_contexts: int = 1, index: int = 0, kind: str | None = None):
     """Context ``index``'s stream, of the kind ``stream_kind(num_contexts)`` picks. The CU-masked
     streams are a per-process pool of at most ``DEDICATED_QUEUE_MAX_CONTEXTS`` per device, shared by
     every engine that takes them (context i gets stream i) and alive until the process ends: a
     hardware queue per engine rebuild would pile up queues, and a destroyed stream may still be
     recorded on a tensor the caching allocator frees later (``Tensor.record_stream``)."""
-    kind = stream_kind(num_contexts)
+    kind = stream_kind(num_contexts, kind)
     if kind == "torch":
         return torch.cuda.Stream(device=device)
     if kind == "hiprio_torch":  # torch's high-priority pool (its 32 streams share the 4 high-priority queues)

@@ -17,6 +17,7 @@ DEV = torch.device("cuda:0")
 def test_stream_kind_policy(monkeypatch):
     monkeypatch.delenv("HIPZAP_STREAM_KIND", raising=False)
     assert [stream_kind(n) for n in (1, 2, 4, 5, 16)] == ["torch", "hiprio", "hiprio", "torch", "torch"]
+    assert stream_kind(4, "torch") == "torch"  # an engine's own choice wins over the default
     monkeypatch.setenv("HIPZAP_STREAM_KIND", "native")
     assert stream_kind(4) == "native"
     monkeypatch.setenv("HIPZAP_STREAM_KIND", "bogus")
