@@ -13,9 +13,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def served(tmp_path_factory):
-    import os
-    os.environ.update(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_LM_VOCAB="2000", HIPZAP_BACKEND="gpu",
-                      HIPZAP_SETTINGS=str(tmp_path_factory.mktemp("s") / "none.json"))
+    # the environment is restored after the module: later tests read HIPZAP_RANDOM_WEIGHTS etc.
+    mp = pytest.MonkeyPatch()
+    for k, v in dict(HIPZAP_RANDOM_WEIGHTS="1", HIPZAP_LM_VOCAB="2000", HIPZAP_BACKEND="gpu",
+                     HIPZAP_SETTINGS=str(tmp_path_factory.mktemp("s") / "none.json")).items():
+        mp.setenv(k, v)
     from hipzap.serve import app as app_mod
     from hipzap.serve.native_http import NativeHTTPServer, listening_socket
     from hipzap.serve.server import ModelServer
@@ -27,6 +29,7 @@ def served(tmp_path_factory):
     yield app_mod, srv, http_srv, sock.getsockname()[1]
     http_srv.stop()
     app_mod.set_server(None)
+    mp.undo()
 
 
 def _get(port, path):
