@@ -451,12 +451,12 @@ def dp_figures(args, eng, device, world: int, rank: int, native_comm):
 def dp_depth(model: str, shard: int) -> int:
     """DP steps in flight per rank for the config 3 / 5 figures: ``HIPZAP_DP_DEPTH`` (1-8), else
     by the measured optimum (profiles/r6_dp_pipeline): 4 for ResNet-50 at any shard and for small
-    ViT shards; 2 for ViT-B/16 fp8 shards of >= 32 images, whose per-step GEMMs already fill the
-    chip (gb64 on one GPU: 23.8k img/s at 2, 23.3k at 3, 22.3k at 4)."""
+    ViT shards; 3 for ViT-B/16 fp8 shards of >= 32 images, whose per-step GEMMs already fill the
+    chip (gb64 on one GPU over six runs: 22.5-23.3k img/s at 3, 20.0-23.8k at 2, 21.8-22.3k at 4)."""
     env = os.environ.get("HIPZAP_DP_DEPTH", "")
     if env:
         return max(1, min(8, int(env)))
-    return 2 if "vit" in model and shard >= 32 else 4
+    return 3 if "vit" in model and shard >= 32 else 4
 
 
 def dp_shard_figures(args, eng, device) -> dict:
