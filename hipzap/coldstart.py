@@ -159,7 +159,10 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
     import tempfile
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     walls, res = [], []
+    gap = trial_gap_s()  # every launch on idle GPUs, as the one-GPU trials (_fresh_trial)
     for _ in range(trials):
+        if gap:
+            time.sleep(gap)
         rdzv = tempfile.mkdtemp(prefix="hzcold_node_")
         procs = []
         # worker output goes to files, not pipes: a worker writing more than a pipe buffer (RCCL debug
@@ -217,7 +220,8 @@ def measure_node(plan: str, world: int, trials: int = 3, timeout: float = 300.0,
     order = sorted(range(trials), key=lambda i: walls[i])
     med = res[order[len(order) // 2]]
     slow = max(med, key=lambda o: o["t_first"])
-    return {"mode": "node", "world": world, "trials": trials, "p50_ms": round(statistics.median(walls), 2),
+    return {"mode": "node", "world": world, "trials": trials, "gap_ms": round(gap * 1e3, 1),
+            "p50_ms": round(statistics.median(walls), 2),
             "min_ms": round(min(walls), 2), "max_ms": round(max(walls), 2), "all_ms": [round(w, 1) for w in walls],
             "slowest_rank_phases_ms": {k: round(v, 2) for k, v in slow["phases_ms"].items()},
             "slowest_rank": slow["rank"], "torch_imported": any(o["torch_imported"] for o in med)}
