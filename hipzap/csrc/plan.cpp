@@ -88,6 +88,68 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// File byte ranges -> device memory through pinned staging buffers. One reader thread copies at
+// the page cache's single-core rate (~10-16 GB/s), below the host -> device DMA, so
+// HIPZAP_UPLOAD_THREADS (default 4) readers split the chunks round-robin, each with its own two
+// 2-MiB staging buffers: chunk j is read while the DMA of that thread's chunk j - T runs. Every
+// copy goes on `st` (distinct destinations, so their order does not matter).
+int staged_upload(int fd, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,
+                  hipStream_t st) {
+  const size_t chunk = size_t(2) << 20;
+  struct Chunk {
+    uint64_t f;
+    size_t m;
+    uint8_t* d;
+  };
+  std::vector<Chunk> cs;
+  for (int i = 0; i < n; ++i)
+    for (uint64_t off = 0; off < nbytes[i]; off += chunk)
+      cs.push_back({file_off[i] + off, (size_t)(nbytes[i] - off < chunk ? nbytes[i] - off : chunk),
+                    static_cast<uint8_t*>(dst[i]) + off});
+  if (cs.empty()) return 0;
+  const char* e = getenv("HIPZAP_UPLOAD_THREADS");
+  int T = e ? atoi(e) : 4;
+  T = T < 1 ? 1 : T > 8 ? 8 : T;
+  if ((size_t)T > cs.size()) T = (int)cs.size();
+  std::vector<int> ok(T, 1);
+  auto work = [&](int t) {
+    void* stage[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool good = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
+                hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
+                hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
+    int k = 0, issued = 0;
+    for (size_t j = (size_t)t; good && j < cs.size(); j += (size_t)T, k ^= 1, ++issued) {
+      if (issued >= 2) good = hipEventSynchronize(done[k]) == hipSuccess;  // staging buffer k free again
+      if (!good) break;
+      size_t got = 0;
+      while (got < cs[j].m) {
+        const ssize_t r = pread(fd, static_cast<uint8_t*>(stage[k]) + got, cs[j].m - got, (off_t)(cs[j].f + got));
+        if (r <= 0) break;
+        got += (size_t)r;
+      }
+      good = got == cs[j].m && hipMemcpyAsync(cs[j].d, stage[k], cs[j].m, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipEventRecord(done[k], st) == hipSuccess;
+    }
+    for (int i = 0; i < 2; ++i) {
+      if (done[i]) {
+        if (issued > i) good = hipEventSynchronize(done[i]) == hipSuccess && good;  // before its buffer is freed
+        (void)hipEventDestroy(done[i]);
+      }
+      if (stage[i]) (void)hipHostFree(stage[i]);
+    }
+    ok[t] = good;
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  for (int v : ok)
+    if (!v) return -1;
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+}
+
 struct Plan {
   int device = 0;
   int fd = -1;
@@ -220,7 +282,8 @@ struct Plan {
 
   // blob upload, HIPZAP_PLAN_UPLOAD selects (measured: profiles/r2_coldstart):
   //   register  pin the mmapped file pages in place (hipHostRegister) -> one DMA -> unpin
-  //   staged    read() chunks into two pinned staging buffers, DMA chunk i while reading i+1
+  //   staged    pread() chunks into pinned staging buffers on HIPZAP_UPLOAD_THREADS readers, the
+  //             DMA of each chunk overlapping the next reads (staged_upload)
   //   pageable  hipMemcpyAsync from the mapping (HIP stages pageable memory internally)
   //   kernel    pin the mapping in place, then a copy kernel reads it over PCIe (no DMA engine)
   int upload_blob(hipStream_t st) {
@@ -269,43 +332,9 @@ struct Plan {
       (void)hipGetLastError();  // fall through to the staged copy
     }
     if (m != "pageable") {
-      const size_t chunk = size_t(4) << 20;
-      void* stage[2] = {nullptr, nullptr};
-      hipEvent_t done[2] = {nullptr, nullptr};
-      double ph[5] = {0, 0, 0, 0, 0};  // diagnostics: host alloc, pread, buffer waits, final sync, free
-      double tp = now_ms();
-      bool ok = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
-                hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
-                hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
-      ph[0] = now_ms() - tp;
-      int k = 0;
-      for (size_t off = 0; ok && off < h.blob_len; off += chunk, k ^= 1) {
-        const size_t n = h.blob_len - off < chunk ? h.blob_len - off : chunk;
-        tp = now_ms();
-        if (off >= 2 * chunk) ok = hipEventSynchronize(done[k]) == hipSuccess;  // buffer k free again
-        ph[2] += now_ms() - tp;
-        if (!ok) break;
-        tp = now_ms();
-        ssize_t got = pread(fd, stage[k], n, (off_t)(h.blob_off + off));
-        ph[1] += now_ms() - tp;
-        ok = got == (ssize_t)n &&
-             hipMemcpyAsync(static_cast<uint8_t*>(blob) + off, stage[k], n, hipMemcpyHostToDevice, st) == hipSuccess &&
-             hipEventRecord(done[k], st) == hipSuccess;
-      }
-      tp = now_ms();
-      if (ok) ok = hipStreamSynchronize(st) == hipSuccess;
-      ph[3] = now_ms() - tp;
-      tp = now_ms();
-      for (int i = 0; i < 2; ++i) {
-        if (done[i]) (void)hipEventDestroy(done[i]);
-        if (stage[i]) (void)hipHostFree(stage[i]);
-      }
-      ph[4] = now_ms() - tp;
-      if (probe && probe[0] == '2')
-        std::fprintf(stderr, "hipzap plan upload: host_alloc %.2f pread %.2f waits %.2f sync %.2f free %.2f ms\n", ph[0],
-                     ph[1], ph[2], ph[3], ph[4]);
-      if (ok) return 0;
+      const uint64_t off = h.blob_off, len = h.blob_len;
+      void* d = blob;
+      if (staged_upload(fd, 1, &off, &len, &d, st) == 0) return 0;
       (void)hipGetLastError();
     }
     const uint8_t* src = map + h.blob_off;
@@ -484,46 +513,15 @@ uint64_t hz_abi_version(void) {
 
 const char* hz_plan_last_error(void) { return g_err.c_str(); }
 
-// file byte ranges -> device pointers: pread into two pinned 4-MiB staging buffers, the DMA of
-// chunk i overlapping the read of chunk i+1 (the plan blob upload's scheme); synchronous
+// file byte ranges -> device pointers (staged_upload: the plan blob upload's scheme); synchronous
 int hz_upload_file(const char* path, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,
                    void* stream) {
   g_err.clear();
-  hipStream_t st = static_cast<hipStream_t>(stream);
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return fail(std::string("upload: cannot open ") + path);
-  const size_t chunk = size_t(4) << 20;
-  void* stage[2] = {nullptr, nullptr};
-  hipEvent_t done[2] = {nullptr, nullptr};
-  bool ok = hipHostMalloc(&stage[0], chunk, hipHostMallocDefault) == hipSuccess &&
-            hipHostMalloc(&stage[1], chunk, hipHostMallocDefault) == hipSuccess &&
-            hipEventCreateWithFlags(&done[0], hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&done[1], hipEventDisableTiming) == hipSuccess;
-  int k = 0;
-  size_t issued = 0;
-  for (int i = 0; ok && i < n; ++i) {
-    for (uint64_t off = 0; ok && off < nbytes[i]; off += chunk, k ^= 1, ++issued) {
-      const size_t m = nbytes[i] - off < chunk ? nbytes[i] - off : chunk;
-      if (issued >= 2) ok = hipEventSynchronize(done[k]) == hipSuccess;  // staging buffer k free again
-      if (!ok) break;
-      size_t got = 0;
-      while (got < m) {
-        const ssize_t r = pread(fd, static_cast<uint8_t*>(stage[k]) + got, m - got, (off_t)(file_off[i] + off + got));
-        if (r <= 0) break;
-        got += (size_t)r;
-      }
-      ok = got == m &&
-           hipMemcpyAsync(static_cast<uint8_t*>(dst[i]) + off, stage[k], m, hipMemcpyHostToDevice, st) == hipSuccess &&
-           hipEventRecord(done[k], st) == hipSuccess;
-    }
-  }
-  if (ok) ok = hipStreamSynchronize(st) == hipSuccess;
-  for (int i = 0; i < 2; ++i) {
-    if (done[i]) (void)hipEventDestroy(done[i]);
-    if (stage[i]) (void)hipHostFree(stage[i]);
-  }
+  const int rc = staged_upload(fd, n, file_off, nbytes, dst, static_cast<hipStream_t>(stream));
   close(fd);
-  return ok ? 0 : fail("upload: read or copy failed");
+  return rc == 0 ? 0 : fail("upload: read or copy failed");
 }
 
 void* hz_plan_open(const char* path, int device, int read_blob, double* timings) {

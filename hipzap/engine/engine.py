@@ -391,8 +391,8 @@ def stream_kind(num_contexts: int, kind: str | None = None) -> str:
     kind = kind or os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
         return "hiprio" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
-    if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask"):
-        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native or cumask")
+    if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask", "mixed"):
+        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native, cumask or mixed")
     return kind
 
 
@@ -406,6 +406,8 @@ def _context_stream(device, num_contexts: int = 1, index: int = 0, kind: str | N
     hardware queue per engine rebuild would pile up queues, and a destroyed stream may still be
     recorded on a tensor the caching allocator frees later (``Tensor.record_stream``)."""
     kind = stream_kind(num_contexts, kind)
+    if kind == "mixed":  # experiment: alternate contexts between the normal- and high-priority queue sets
+        kind = "torch" if index % 2 == 0 else "hiprio"
     if kind == "torch":
         return torch.cuda.Stream(device=device)
     if kind == "hiprio_torch":  # torch's high-priority pool (its 32 streams share the 4 high-priority queues)
