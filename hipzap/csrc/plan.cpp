@@ -88,14 +88,18 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// File byte ranges -> device memory through pinned staging buffers. One reader thread copies at
-// the page cache's single-core rate (~10-16 GB/s), below the host -> device DMA, so
-// HIPZAP_UPLOAD_THREADS (default 4) readers split the chunks round-robin, each with its own two
-// 2-MiB staging buffers: chunk j is read while the DMA of that thread's chunk j - T runs. Every
-// copy goes on `st` (distinct destinations, so their order does not matter).
+// File byte ranges -> device memory through pinned staging buffers: each reader thread has two
+// staging buffers and reads chunk j while the DMA of its previous chunk runs; every copy goes on
+// `st` (distinct destinations, so their order does not matter). HIPZAP_UPLOAD_THREADS readers
+// (default 1, 4-MiB chunks) split the chunks round-robin (2-MiB chunks). Measured (r6 session 18,
+// profiles/r6_cold): 4 readers made the plan blob's DMA 4.3 -> 7.8-11.0 ms and the LM checkpoint's
+// 340-MB upload no faster (the extra pinned staging buffers cost more than the parallel reads save).
 int staged_upload(int fd, int n, const uint64_t* file_off, const uint64_t* nbytes, void* const* dst,
                   hipStream_t st) {
-  const size_t chunk = size_t(2) << 20;
+  const char* e = getenv("HIPZAP_UPLOAD_THREADS");
+  int T = e ? atoi(e) : 1;
+  T = T < 1 ? 1 : T > 8 ? 8 : T;
+  const size_t chunk = T == 1 ? size_t(4) << 20 : size_t(2) << 20;
   struct Chunk {
     uint64_t f;
     size_t m;
@@ -107,9 +111,6 @@ int staged_upload(int fd, int n, const uint64_t* file_off, const uint64_t* nbyte
       cs.push_back({file_off[i] + off, (size_t)(nbytes[i] - off < chunk ? nbytes[i] - off : chunk),
                     static_cast<uint8_t*>(dst[i]) + off});
   if (cs.empty()) return 0;
-  const char* e = getenv("HIPZAP_UPLOAD_THREADS");
-  int T = e ? atoi(e) : 4;
-  T = T < 1 ? 1 : T > 8 ? 8 : T;
   if ((size_t)T > cs.size()) T = (int)cs.size();
   std::vector<int> ok(T, 1);
   auto work = [&](int t) {

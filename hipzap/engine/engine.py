@@ -386,13 +386,14 @@ def stream_kind(num_contexts: int, kind: str | None = None) -> str:
       ``cumask``: a per-process pool of full-CU-mask streams (a queue each, but BLOCKING: a NULL-
       stream command waits for their work). Measured, not defaults.
     * ``auto``: ``hiprio`` for engines of 2-4 contexts, ``torch`` otherwise -- 16 ResNet-50 bs=1
-      contexts need the shared queues (16 queues of their own: 14.3k -> 7.4k inf/s), and a
+      contexts need the shared queues (16 queues of their own: 14.3k -> 7.4k inf/s; alternating
+      them over the normal- and high-priority sets, 8 queues: 6.7k), and a
       DPPipeline over big batches does better on them too (``bench.py`` passes ``torch``)."""
     kind = kind or os.environ.get("HIPZAP_STREAM_KIND", "auto")
     if kind == "auto":
         return "hiprio" if 2 <= num_contexts <= DEDICATED_QUEUE_MAX_CONTEXTS else "torch"
-    if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask", "mixed"):
-        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native, cumask or mixed")
+    if kind not in ("torch", "hiprio", "hiprio_torch", "native", "cumask"):
+        raise ValueError(f"HIPZAP_STREAM_KIND={kind!r}: auto, torch, hiprio, hiprio_torch, native or cumask")
     return kind
 
 
@@ -406,8 +407,6 @@ def _context_stream(device, num_contexts: int = 1, index: int = 0, kind: str | N
     hardware queue per engine rebuild would pile up queues, and a destroyed stream may still be
     recorded on a tensor the caching allocator frees later (``Tensor.record_stream``)."""
     kind = stream_kind(num_contexts, kind)
-    if kind == "mixed":  # experiment: alternate contexts between the normal- and high-priority queue sets
-        kind = "torch" if index % 2 == 0 else "hiprio"
     if kind == "torch":
         return torch.cuda.Stream(device=device)
     if kind == "hiprio_torch":  # torch's high-priority pool (its 32 streams share the 4 high-priority queues)
