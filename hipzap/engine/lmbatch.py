@@ -213,12 +213,13 @@ class LMBatchEngine:
 
     def __init__(self, packed: dict, device="cuda:0", rows: int = 32, unroll: int = 8, exclude_ids=(),
                  max_words: int = 1024, record_logits: bool = False, capture: bool = True,
-                 lowload: bool | None = None, embproj: bool | None = None, solo: bool | None = None):
+                 lowload: bool | None = None, embproj: bool | None = None, solo: bool | None = None,
+                 priority: int = 0):
         self.p = packed
         self.device = torch.device(device)
         self.V = packed["V"]
         with torch.cuda.device(self.device):
-            self.stream = torch.cuda.Stream(self.device)
+            self.stream = torch.cuda.Stream(self.device, priority=priority)
             self._alloc = _TorchAlloc(self.device)
             w = {"layers": [(ly["w"].data_ptr(), ly["bias"].data_ptr()) for ly in packed["layers"]],
                  "emb": packed["emb"].data_ptr(), "dec": packed["dec"].data_ptr(),

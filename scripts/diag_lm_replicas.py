@@ -22,25 +22,17 @@ def _arg(name, default):
 def main():
     import torch
     from bench_lm_batch import run_load
-    from hipzap.engine import lmbatch
     from hipzap.engine.lmbatch import LMBatchEngine, pack_lmb
     from hipzap.models.awd_lstm import reference_lm
     clients = [int(c) for c in _arg("--clients", "32,64,128").split(",")]
     requests = int(_arg("--requests", "6"))
     torch.manual_seed(0)
     packed = pack_lmb(reference_lm(60000).eval().state_dict(), "cuda:0")
-    for reps, hiprio in ((1, False), (2, False), (2, True)):
+    for reps, hiprio in ((2, True), (1, False), (2, False)):
         engines = []
-        for _ in range(reps):
-            if hiprio:  # the engine's stream at high priority (a queue of its own)
-                orig = torch.cuda.Stream
-                lmbatch.torch.cuda.Stream = lambda dev, _o=orig: _o(dev, priority=-1)
-                try:
-                    engines.append(LMBatchEngine(packed, "cuda:0", rows=32, exclude_ids=[2, 5, 6]))
-                finally:
-                    lmbatch.torch.cuda.Stream = orig
-            else:
-                engines.append(LMBatchEngine(packed, "cuda:0", rows=32, exclude_ids=[2, 5, 6]))
+        for i in range(reps):  # hiprio: the second engine's stream at high priority (a queue set of its own)
+            engines.append(LMBatchEngine(packed, "cuda:0", rows=32, exclude_ids=[2, 5, 6],
+                                         priority=-1 if hiprio and i else 0))
         for e in engines:
             e.run_tokens([0], 200, 1)
         ctr = [0]
