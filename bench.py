@@ -13,7 +13,7 @@ cold start (headline ``cold_start_ms_p50``): measured FIRST, before this process
   of the real ResNet-50 architecture, their plan image) are written untimed beforehand, on the
   CPU, as ``hipzap plan`` does at deploy time. In-process rebuilds inside this warm process are
   reported separately (``cold_start_inprocess_*``).
-warm path: every rank serves ``--streams`` (default 16: the rate of 24-48 streams at a third less latency under load, profiles/r4_final/streams16v24)
+warm path: every rank serves ``--streams`` (default 12: the rate of 16-24 streams at three quarters of the 16-stream latency under load, profiles/r6_final/streams_dyn_sweep_s20.txt)
   concurrent bs=1 request streams; each request is one hipGraph replay (zero-copy pinned uint8
   image -> preprocess -> 37 kernels: conv+maxpool, fused layer1/layer2 bottlenecks, layer3/layer4 convs -> pool+FC -> logits in pinned memory).
   ``--serve executor`` (default): one native client thread per stream sends requests back to
@@ -62,8 +62,9 @@ def parse():
                     help="requests per stream in one timed step (replica mode)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=1, help="per-request batch (headline: 1)")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 16)),
-                    help="concurrent bs=1 request contexts per GPU (16: the 24-48 rate at 2/3 of the 24-stream latency, profiles/r4_final/streams)")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("HIPZAP_STREAMS", 12)),
+                    help="concurrent bs=1 request contexts per GPU (12: the 16-24 rate, 14.24-14.35k, at p50 0.83 ms under "
+                         "load vs 1.11 at 16, profiles/r6_final/streams_dyn_sweep_s20.txt)")
     ap.add_argument("--ckpt-dir", default=os.environ.get("HIPZAP_BENCH_DIR", "/tmp/hipzap_bench"))
     ap.add_argument("--cold-trials", type=int, default=int(os.environ.get("HIPZAP_COLD_TRIALS", 15)),
                     help="fresh processes per cold-start path (0: skip)")
