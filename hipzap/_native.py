@@ -158,6 +158,7 @@ def _load():
     _sig(lib, "hz_prog_capture", c_int, P, P)
     _sig(lib, "hz_prog_replay", c_int, P, P)
     _sig(lib, "hz_prog_is_captured", c_int, P)
+    _sig(lib, "hz_prog_prepare", c_int, P)
     _sig(lib, "hz_prog_bench", c_double, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int)
     _sig(lib, "hz_prog_bench2", c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), c_int, c_int, c_int,
          C.POINTER(c_double))

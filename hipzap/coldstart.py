@@ -91,6 +91,7 @@ def run_lm(ckpt: str, device: int, vocab: str | None, words: int = 200) -> dict:
     t_ready = time.time()
     text = eng.generate([""], words, itos, stoi, seed=1)
     t_first = time.time()
+    eng.wait_captured()  # the deferred graph captures finish before this process exits (untimed)
     return {"mode": "lm", "t_first": t_first, "ok": len(text.split()) >= words // 2, "words": words,
             "torch_imported": "torch" in sys.modules, "numpy_imported": "numpy" in sys.modules,
             "vocab": eng.V, "decode_ms": eng.last_latency_ms,

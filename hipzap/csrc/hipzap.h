@@ -533,6 +533,8 @@ int hz_prog_run(HzProgram p, hipStream_t st);  // eager launch of every op
 int hz_prog_capture(HzProgram p, hipStream_t st);
 int hz_prog_replay(HzProgram p, hipStream_t st);
 int hz_prog_is_captured(HzProgram p);
+// make the side streams / fork events a run needs (before a lazy capture races a replay)
+int hz_prog_prepare(HzProgram p);
 int hz_prog_replay_n(HzProgram p, hipStream_t st, int n);  // n back-to-back replays, no sync
 // replay `n` programs round-robin on `n` streams `iters` times from C++ and synchronize;
 // returns elapsed microseconds (host wall, includes the final sync) or negative on error.

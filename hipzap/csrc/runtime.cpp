@@ -8,6 +8,7 @@
 // invocation captured as a hipGraph"). Nothing here allocates or synchronises inside the
 // launch sequence, so capture is always legal (cdna_hip_programming.md §6 Guideline 9).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,11 +34,13 @@ struct Program {
   std::vector<hipStream_t> side;     // side[k-1]
   std::vector<hipEvent_t> fork_ev;   // one per fork/join op (indexed by op)
   hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  // atomic: a program captured lazily (hz_prog_capture from one thread) may be replayed op by op
+  // (hz_prog_replay from another) until the instantiated graph is published
+  std::atomic<hipGraphExec_t> exec{nullptr};
   int max_slot = 0;
 
   ~Program() {
-    if (exec) (void)hipGraphExecDestroy(exec);
+    if (hipGraphExec_t x = exec.load()) (void)hipGraphExecDestroy(x);
     if (graph) (void)hipGraphDestroy(graph);
     for (auto s : side) (void)hipStreamDestroy(s);
     for (auto e : fork_ev)
@@ -186,22 +189,26 @@ int hz_prog_capture(HzProgram h, hipStream_t st) {
   }
   if (e != hipSuccess) return (int)e;
   P->graph = g;
-  e = hipGraphInstantiate(&P->exec, g, nullptr, nullptr, 0);
-  if (e != hipSuccess) {
-    P->exec = nullptr;
-    return (int)e;
-  }
-  // upload once so the first replay does not pay for it
-  (void)hipGraphUpload(P->exec, st);
+  hipGraphExec_t x = nullptr;
+  e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  if (e != hipSuccess) return (int)e;
+  // upload once so the first replay does not pay for it; then publish
+  (void)hipGraphUpload(x, st);
+  P->exec.store(x);
   return 0;
 }
 
-int hz_prog_is_captured(HzProgram h) { return static_cast<Program*>(h)->exec != nullptr; }
+int hz_prog_prepare(HzProgram h) {  // the side streams / events a run needs, made before any run
+  return static_cast<Program*>(h)->ensure_streams();
+}
+
+int hz_prog_is_captured(HzProgram h) { return static_cast<Program*>(h)->exec.load() != nullptr; }
 
 int hz_prog_replay(HzProgram h, hipStream_t st) {
   Program* P = static_cast<Program*>(h);
-  if (!P->exec) return P->run(st);
-  return (int)hipGraphLaunch(P->exec, st);
+  hipGraphExec_t x = P->exec.load();
+  if (!x) return P->run(st);
+  return (int)hipGraphLaunch(x, st);
 }
 
 double hz_prog_bench(HzProgram* progs, hipStream_t* streams, int n, int iters) {

@@ -252,8 +252,6 @@ class LmbCore:
                     if kind == N.HZ_K_LMB_DEC and self.logits_bufs:
                         q.logits = self.logits_bufs[k]
                     N.check(lib.hz_prog_add_kernel(prog, kind, C.byref(q), C.sizeof(q), 0), f"add lmb kernel {kind}")
-            if capture:
-                N.check(lib.hz_prog_capture(prog, stream), "capture lmb")
             return prog
 
         self._admit = a
@@ -266,6 +264,18 @@ class LmbCore:
         # one request (HIPZAP_LM_SOLO, default on): programs that read and write row 0's state only,
         # replayed while row 0 is the only busy row (a lone request always sits in row 0)
         self.progs_solo = [build(-1, k) for k in range(self.nprog)] if solo else []
+        # capture: True -- every program now; "lazy" -- only what a lone first request replays (the
+        # one-request programs, else the full ones), the rest by capture_pending() after the first
+        # response (until then they run launch by launch: same kernels, same results); False -- none
+        first = self.progs_solo or self.progs
+        now = [q for q in self.progs + self.progs_lo + self.progs_solo
+               if (capture and capture != "lazy") or (capture == "lazy" and q in first)]
+        self._pending = [q for q in self.progs + self.progs_lo + self.progs_solo if q not in now] \
+            if capture == "lazy" else []
+        for q in now:
+            N.check(lib.hz_prog_capture(q, stream), "capture lmb")
+        for q in self._pending:
+            N.check(lib.hz_prog_prepare(q), "prepare lmb")
         P2 = C.c_void_p * 2
         lg = P2(*(self.logits_bufs + [0] * (2 - len(self.logits_bufs)))) if self.logits_bufs else None
         self._sched = lib.hz_lmb_create(P2(*(self.progs + [0] * (2 - self.nprog))), self.nprog, stream,
@@ -280,6 +290,24 @@ class LmbCore:
             N.check(lib.hz_lmb_set_solo(self._sched, P2(*(self.progs_solo + [0] * (2 - self.nprog)))),
                     "hz_lmb_set_solo")
         self.last_latency_ms = None
+
+    def capture_pending(self, stream: int | None = None) -> float:
+        """Capture the programs a lazy engine left uncaptured, on a private stream (``stream``, or a
+        new one) while the scheduler keeps replaying on its own: a program is published to the
+        scheduler only once its graph is instantiated and uploaded (csrc/runtime.cpp). Returns ms."""
+        import time
+        if not self._pending:
+            return 0.0
+        t0 = time.perf_counter()
+        if stream is None:
+            from .. import hip as H
+            p = C.c_void_p()
+            H.check(H.hip().hipStreamCreateWithFlags(C.byref(p), 1), "hipStreamCreateWithFlags")
+            stream = self._cap_stream = p.value
+        while self._pending:
+            N.check(self.lib.hz_prog_capture(self._pending[0], stream), "capture lmb")
+            self._pending.pop(0)
+        return (time.perf_counter() - t0) * 1e3
 
     def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
         """Feed ``prompt_ids``, sample ``n_words`` tokens (blocking, thread-safe); the sampled ids,
@@ -314,6 +342,11 @@ class LmbCore:
         s, self._sched = getattr(self, "_sched", None), None
         if s:
             self.lib.hz_lmb_destroy(s)
+        cs, self._cap_stream = getattr(self, "_cap_stream", None), None
+        if cs:
+            from .. import hip as H
+            H.hip().hipStreamDestroy.argtypes = [C.c_void_p]
+            H.hip().hipStreamDestroy(cs)
         progs = (list(getattr(self, "progs", []) or []) + list(getattr(self, "progs_lo", []) or []) +
                  list(getattr(self, "progs_solo", []) or []))
         self.progs, self.progs_lo, self.progs_solo, self.prog = [], [], [], None

@@ -66,7 +66,12 @@ class LMLiteEngine:
     concurrent requests share decode steps); ``timings`` holds the cold-start phases (ms)."""
 
     def __init__(self, ckpt: str, device: int = 0, rows: int = 32, unroll: int = 8, exclude_ids=(),
-                 max_words: int = 1024, record_logits: bool = False, capture: bool = True):
+                 max_words: int = 1024, record_logits: bool = False, capture: bool | str | None = None):
+        """``capture="lazy"`` (default, ``HIPZAP_LM_CAPTURE``): the graphs a lone first request
+        replays are captured here, the others on a background thread after the first request
+        (``LmbCore.capture_pending``), off the cold start's critical path; ``True``: all now."""
+        if capture is None:
+            capture = "lazy" if os.environ.get("HIPZAP_LM_CAPTURE", "lazy") == "lazy" else True
         t0 = time.perf_counter()
         refs = scan(ckpt)
         enc, dec = refs.get("0.encoder.weight"), refs.get("1.decoder.weight")
@@ -134,13 +139,32 @@ class LMLiteEngine:
                         "program_ms": (t_ready - t_pack) * 1e3, "raw_MB": round(total / 2 ** 20, 1)}
         self._seed_lock = threading.Lock()
         self._seed_ctr = int.from_bytes(os.urandom(8), "little")
+        self._capturer = None
 
     @classmethod
     def for_vocab(cls, ckpt: str, stoi: dict, **kw) -> "LMLiteEngine":
         return cls(ckpt, exclude_ids=[stoi[w] for w in EXCLUDE_TOKENS if w in stoi], **kw)
 
     def run_tokens(self, prompt_ids, n_words: int, seed: int = 0, logits: bool = False):
-        return self.core.run_tokens(prompt_ids, n_words, seed, logits)
+        out = self.core.run_tokens(prompt_ids, n_words, seed, logits)
+        if self._capturer is None and self.core._pending:  # after the first response: the rest of the graphs
+            with self._seed_lock:
+                if self._capturer is None:
+                    self._capturer = threading.Thread(target=self._capture_rest, name="hz-lm-capture", daemon=True)
+                    self._capturer.start()
+        return out
+
+    def _capture_rest(self) -> None:
+        try:
+            self.timings["deferred_capture_ms"] = self.core.capture_pending()
+        except Exception as e:  # noqa: BLE001 - the uncaptured programs keep running launch by launch
+            self.timings["deferred_capture_error"] = repr(e)[:300]
+
+    def wait_captured(self, timeout: float | None = None) -> bool:
+        """Join the deferred capture (tests, shutdown); True when every program is captured."""
+        if self._capturer is not None:
+            self._capturer.join(timeout)
+        return not self.core._pending
 
     @property
     def last_latency_ms(self):
@@ -167,6 +191,8 @@ class LMLiteEngine:
         return self.core.stats()
 
     def close(self) -> None:
+        if getattr(self, "_capturer", None) is not None:
+            self._capturer.join()
         core = getattr(self, "core", None)
         if core is not None:
             core.close()

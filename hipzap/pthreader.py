@@ -23,7 +23,6 @@ import mmap
 import os
 import pickle
 import struct
-import zipfile
 from collections import OrderedDict
 
 # storage class -> (numpy dtype name, item size)
@@ -186,45 +185,105 @@ class _RestrictedUnpickler(pickle.Unpickler):
         return self._load_storage(str(key), st, int(numel))
 
 
-def _member_data_offset(mm, info: zipfile.ZipInfo) -> int:
+def _member_data_offset(mm, header_offset: int) -> int:
     """Byte offset of a stored member's data inside the archive (local header is 30 bytes +
     name + extra; the extra field is what torch uses to 64-byte-align the records)."""
-    hdr = mm[info.header_offset: info.header_offset + 30]
+    hdr = mm[header_offset: header_offset + 30]
     if hdr[:4] != b"PK\x03\x04":
         raise NotAZipCheckpoint("bad local file header")
     name_len, extra_len = struct.unpack("<HH", hdr[26:30])
-    return info.header_offset + 30 + name_len + extra_len
+    return header_offset + 30 + name_len + extra_len
+
+
+def _zip_index(mm) -> dict | None:
+    """{name: (method, compressed size, size, local header offset, flags)} from the archive's
+    central directory, read straight from the memory map (zip64 records included) -- importing
+    ``zipfile`` (pathlib, shutil, urllib.parse ...) cost ~1/3 of the torch-free cold-start
+    child's imports. None when the archive has anything this reader does not handle; the caller
+    then uses ``zipfile``."""
+    n = len(mm)
+    i = mm.rfind(b"PK\x05\x06", max(0, n - 22 - 65535))
+    if i < 0 or i + 22 > n:
+        return None
+    _, disk, cd_disk, _, count, cd_size, cd_off, _ = struct.unpack("<IHHHHIIH", mm[i:i + 22])
+    if disk != 0 or cd_disk != 0:
+        return None
+    if cd_off == 0xFFFFFFFF or count == 0xFFFF or cd_size == 0xFFFFFFFF:
+        j = i - 20
+        if j < 0 or mm[j:j + 4] != b"PK\x06\x07":
+            return None
+        eocd64 = struct.unpack("<IIQI", mm[j:j + 20])[2]
+        if eocd64 + 56 > n or mm[eocd64:eocd64 + 4] != b"PK\x06\x06":
+            return None
+        count, cd_size, cd_off = struct.unpack("<IQHHIIQQQQ", mm[eocd64:eocd64 + 56])[7:10]
+    members, p = {}, cd_off
+    for _ in range(count):
+        if p + 46 > n or mm[p:p + 4] != b"PK\x01\x02":
+            return None
+        f = struct.unpack("<IHHHHHHIIIHHHHHII", mm[p:p + 46])
+        flags, method, csize, usize, nlen, xlen, clen, hoff = f[3], f[4], f[8], f[9], f[10], f[11], f[12], f[16]
+        name = bytes(mm[p + 46:p + 46 + nlen]).decode("utf-8" if flags & 0x800 else "cp437")
+        if 0xFFFFFFFF in (csize, usize, hoff):  # zip64 extended information (header id 1)
+            extra, q, vals = mm[p + 46 + nlen:p + 46 + nlen + xlen], 0, None
+            while q + 4 <= len(extra):
+                hid, hlen = struct.unpack("<HH", extra[q:q + 4])
+                if hid == 1:
+                    vals = extra[q + 4:q + 4 + hlen]
+                    break
+                q += 4 + hlen
+            if vals is None:
+                return None
+            k = 0
+            if usize == 0xFFFFFFFF:
+                usize, k = struct.unpack("<Q", vals[k:k + 8])[0], k + 8
+            if csize == 0xFFFFFFFF:
+                csize, k = struct.unpack("<Q", vals[k:k + 8])[0], k + 8
+            if hoff == 0xFFFFFFFF:
+                hoff = struct.unpack("<Q", vals[k:k + 8])[0]
+        members[name] = (method, csize, usize, hoff, flags)
+        p += 46 + nlen + xlen + clen
+    return members
 
 
 def _read(path: str, with_arrays: bool):
-    if not zipfile.is_zipfile(path):
-        raise NotAZipCheckpoint(f"{path}: not a zip-format torch checkpoint")
     fd = os.open(path, os.O_RDONLY)
     try:
-        mm = mmap.mmap(fd, 0, access=mmap.ACCESS_READ)
+        mm = mmap.mmap(fd, 0, access=mmap.ACCESS_READ) if os.fstat(fd).st_size else None
     finally:
         os.close(fd)
-    zf = zipfile.ZipFile(path)
-    names = zf.namelist()
-    pkl = [n for n in names if n.endswith("/data.pkl") or n == "data.pkl"]
+    idx = _zip_index(mm) if mm is not None else None
+    if idx is None:  # not a zip, or a layout the direct reader does not handle: the zipfile module
+        import zipfile
+        if mm is None or not zipfile.is_zipfile(path):
+            raise NotAZipCheckpoint(f"{path}: not a zip-format torch checkpoint")
+        with zipfile.ZipFile(path) as zf:
+            idx = {i.filename: (i.compress_type, i.compress_size, i.file_size, i.header_offset, i.flag_bits)
+                   for i in zf.infolist()}
+    pkl = [n for n in idx if n.endswith("/data.pkl") or n == "data.pkl"]
     if len(pkl) != 1:
         raise NotAZipCheckpoint(f"{path}: expected one data.pkl, found {pkl}")
     prefix = pkl[0][: -len("data.pkl")]
-    infos = {i.filename: i for i in zf.infolist()}
-    bo = infos.get(prefix + "byteorder")
-    if bo is not None and zf.read(bo).strip() not in (b"little", b""):
+
+    def stored(name: str):  # (data offset, size) of an uncompressed, unencrypted member
+        m = idx.get(name)
+        if m is None or m[0] != 0 or m[4] & 1:
+            return None
+        return _member_data_offset(mm, m[3]), m[2]
+
+    bo = stored(prefix + "byteorder")
+    if bo is not None and bytes(mm[bo[0]:bo[0] + bo[1]]).strip() not in (b"little", b""):
         raise ValueError(f"{path}: big-endian checkpoint")
     cache: dict = {}
 
     def load_storage(key: str, st: _StorageType, numel: int) -> StorageRef:
         s = cache.get(key)
         if s is None:
-            info = infos.get(f"{prefix}data/{key}")
-            if info is None or info.compress_type != zipfile.ZIP_STORED:
+            rec = stored(f"{prefix}data/{key}")
+            if rec is None:
                 raise pickle.UnpicklingError(f"storage {key}: missing or compressed record")
-            if numel * st.itemsize > info.file_size:
+            if numel * st.itemsize > rec[1]:
                 raise pickle.UnpicklingError(f"storage {key}: record shorter than {numel} elements")
-            s = StorageRef(key, st, numel, _member_data_offset(mm, info))
+            s = StorageRef(key, st, numel, rec[0])
             if s.file_off + s.nbytes > len(mm):
                 raise pickle.UnpicklingError(f"storage {key}: record runs past the end of the file")
             cache[key] = s
@@ -233,9 +292,16 @@ def _read(path: str, with_arrays: bool):
                 s.array = np.frombuffer(mm, dtype=np.dtype(st.dtype), count=numel, offset=s.file_off)
         return s
 
-    with zf.open(pkl[0]) as f:
-        obj = _RestrictedUnpickler(f, load_storage).load()
-    zf.close()
+    rec = stored(pkl[0])
+    if rec is not None:
+        import io
+        data = io.BytesIO(mm[rec[0]:rec[0] + rec[1]])
+    else:  # a compressed data.pkl: let zipfile inflate it
+        import io
+        import zipfile
+        with zipfile.ZipFile(path) as zf:
+            data = io.BytesIO(zf.read(pkl[0]))
+    obj = _RestrictedUnpickler(data, load_storage).load()
     if not with_arrays:
         mm.close()
     if isinstance(obj, dict) and "state_dict" in obj and isinstance(obj["state_dict"], dict):

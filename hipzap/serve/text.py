@@ -17,12 +17,10 @@ multinomial-without-replacement on exp(logits), but computed in log space (the r
 from __future__ import annotations
 
 import io
-import json
 import pickle
-from typing import TYPE_CHECKING, Callable, Sequence
 
-if TYPE_CHECKING:  # torch-free at import: the plan / lite LM servers never load torch
-    import torch
+# (annotations only -- ``typing`` and ``json`` are imported where used: the torch-free LM cold-start
+# child imports this module on its critical path)
 
 NO_SPACE = ["'s", "'ll", ",", "?", ".", "'t", "'m", "n't", "!", "'", "'ve", ";", "http", ":", "/", "\\"]
 CAPITALIZE_AFTER = [".", "!", "\n"]
@@ -42,6 +40,7 @@ def load_itos(path: str) -> list[str]:
     with open(path, "rb") as f:
         data = f.read()
     if path.endswith(".json"):
+        import json
         itos = json.loads(data.decode("utf-8"))
     else:
         itos = _NoGlobalsUnpickler(io.BytesIO(data)).load()
@@ -53,6 +52,7 @@ def load_itos(path: str) -> list[str]:
 def save_itos(itos: Sequence[str], path: str) -> None:
     if path.endswith(".json"):
         with open(path, "w") as f:
+            import json
             json.dump(list(itos), f)
     else:
         with open(path, "wb") as f:

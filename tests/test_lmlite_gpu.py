@@ -96,3 +96,38 @@ def test_fresh_process_cold_start_is_torch_free(ckpt):
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["ok"] and r["torch_imported"] is False and r["numpy_imported"] is False and r["vocab"] == V
+
+
+def test_lazy_capture_is_bitwise_the_eager_engine_under_load(ckpt):
+    """capture="lazy" (the default): the lone first request replays the one-request graphs, the
+    other programs run launch by launch until the background capture publishes them -- while 12
+    concurrent requests run through them. Every request's tokens equal the eagerly captured
+    engine's for the same seed, and afterwards every program is captured."""
+    import threading
+    from hipzap import _native as N
+    p, _, _ = ckpt
+    eager = LMLiteEngine(p, rows=32, unroll=4, exclude_ids=[2, 3, 4], capture=True)
+    lazy = LMLiteEngine(p, rows=32, unroll=4, exclude_ids=[2, 3, 4])
+    try:
+        core = lazy.core
+        assert core._pending and all(N.lib().hz_prog_is_captured(q) for q in core.progs_solo)
+        first = lazy.run_tokens([0], 30, seed=5)  # starts the deferred capture
+        assert first == eager.run_tokens([0], 30, seed=5)
+        seeds = list(range(100, 112))
+        got = {}
+
+        def client(s):
+            got[s] = lazy.run_tokens([s % 50], 30, seed=s)
+        th = [threading.Thread(target=client, args=(s,)) for s in seeds]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+        assert lazy.wait_captured(120)
+        assert all(N.lib().hz_prog_is_captured(q) for q in core.progs + core.progs_lo + core.progs_solo)
+        for s in seeds:
+            assert got[s] == eager.run_tokens([s % 50], 30, seed=s), s
+        assert "deferred_capture_ms" in lazy.timings
+    finally:
+        eager.close()
+        lazy.close()

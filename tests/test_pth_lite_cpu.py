@@ -223,3 +223,40 @@ def test_from_checkpoint_refuses_short_vectors(tmp_path, key):
     torch.save(sd, p)
     with pytest.raises(lite.PlanError, match=key.replace(".", r"\.")):
         lite.PlanEngine.from_checkpoint(p)
+
+
+def _zipfile_index(path):
+    with zipfile.ZipFile(path) as zf:
+        return {i.filename: (i.compress_type, i.compress_size, i.file_size, i.header_offset, i.flag_bits)
+                for i in zf.infolist()}
+
+
+def test_direct_zip_index_matches_zipfile(tmp_path):
+    """The central-directory reader (no zipfile import on the cold-start path) sees exactly what
+    zipfile sees: a torch.save archive, and a zip64 archive (> 65535 members: zip64 end records)."""
+    import mmap
+    p = str(tmp_path / "m.pth")
+    torch.save(resnet18().state_dict(), p)
+    with open(p, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    assert pthreader._zip_index(mm) == _zipfile_index(p)
+    z = str(tmp_path / "many.zip")
+    with zipfile.ZipFile(z, "w", allowZip64=True) as zf:
+        for i in range(65540):
+            zf.writestr(f"a/{i}", b"x")
+    with open(z, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+        assert mm.rfind(b"PK\x06\x06") > 0  # the zip64 end record is there
+    assert pthreader._zip_index(mm) == _zipfile_index(z)
+    assert pthreader._zip_index(mmap.mmap(-1, 64)) is None  # not a zip: the caller falls back
+
+
+def test_reader_without_the_direct_index_is_unchanged(tmp_path, monkeypatch):
+    """With the direct index refused (None), the zipfile fallback reads the same state_dict."""
+    p = str(tmp_path / "m.pth")
+    sd = resnet18().state_dict()
+    torch.save(sd, p)
+    a = pthreader.load_state_dict(p)
+    monkeypatch.setattr(pthreader, "_zip_index", lambda mm: None)
+    b = pthreader.load_state_dict(p)
+    assert a.keys() == b.keys() and all(np.array_equal(a[k], b[k]) for k in a)
