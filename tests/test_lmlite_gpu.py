@@ -99,7 +99,7 @@ def test_fresh_process_cold_start_is_torch_free(ckpt):
 
 
 def test_lazy_capture_is_bitwise_the_eager_engine_under_load(ckpt):
-    """capture="lazy" (the default): the lone first request replays the one-request graphs, the
+    """capture="lazy": the lone first request replays the one-request graphs, the
     other programs run launch by launch until the background capture publishes them -- while 12
     concurrent requests run through them. Every request's tokens equal the eagerly captured
     engine's for the same seed, and afterwards every program is captured."""
@@ -107,7 +107,7 @@ def test_lazy_capture_is_bitwise_the_eager_engine_under_load(ckpt):
     from hipzap import _native as N
     p, _, _ = ckpt
     eager = LMLiteEngine(p, rows=32, unroll=4, exclude_ids=[2, 3, 4], capture=True)
-    lazy = LMLiteEngine(p, rows=32, unroll=4, exclude_ids=[2, 3, 4])
+    lazy = LMLiteEngine(p, rows=32, unroll=4, exclude_ids=[2, 3, 4], capture="lazy")
     try:
         core = lazy.core
         assert core._pending and all(N.lib().hz_prog_is_captured(q) for q in core.progs_solo)
