@@ -457,6 +457,172 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mx_kernel(const HzGemmFp8Pa
   mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
 }
 
+// Role-split MX GEMM (round 6; cfg 40 / 41): the 128 x 128 tile of cfg 24,
+// but its 8 MFMA waves never issue a global load and never meet at a workgroup barrier. Two loader
+// waves stage the k-steps into an NS-deep LDS ring with global_load_lds (wave 8: the activation
+// pieces and the block-scale pieces, wave 9: the weight pieces), keeping up to AH = NS - 2 stages
+// in flight, and publish each stage with an LDS counter once its loads have landed (vmcnt); an
+// MFMA wave waits for that count, reads its fragments exactly as cfg 24 does, and returns the slot
+// with a second counter once its ds_reads are in registers. Both counters only grow (the round
+// r = st / NS of a slot is part of the expected value), so no wave ever resets shared state.
+// Every wait is bounded (RS_SPIN polls): a broken handshake ends the kernel with wrong results
+// instead of a hang. Same MFMAs in the same order per accumulator as cfg 24: bitwise cfg 24.
+constexpr int RS_SPIN = 1 << 22;
+
+__device__ __forceinline__ int lds_load_relaxed(int* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void lds_add(int* a) {
+  __hip_atomic_fetch_add(a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wait until *a >= v (one lane polls; the value is wave-uniform through readfirstlane)
+__device__ __forceinline__ void lds_wait_ge(int* a, int v) {
+  for (int i = 0; i < RS_SPIN; ++i) {
+    if (__builtin_amdgcn_readfirstlane(lds_load_relaxed(a)) >= v) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int NS, bool XS>
+__global__ __launch_bounds__(64 * 10) void gemm_mx_rs_kernel(const HzGemmFp8Params p, int group_m) {
+  constexpr int BM = 128, BN = 128, WM = 2, WN = 4, MW = WM * WN;
+  constexpr int FCW = BN / WN / 16, FPW = BM / WM / 16;
+  constexpr int NWG = BN / 16;
+  constexpr int XBYTES = BM * 128, WBYTES = NWG * 2048, SCB = XS ? (BM / 64) * 256 : 0;
+  constexpr int SBYTES = XBYTES + WBYTES + SCB;
+  constexpr int XP = BM / 8, WP = NWG * 2, SP = XS ? BM / 64 : 0;
+  constexpr int AH = NS - 2;  // stages a loader keeps in flight behind the one it publishes
+  static_assert(NS >= 3 && AH * (XP + SP) < 64 && AH * WP < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
+  __shared__ int loaded[NS], consumed[NS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < NS) {
+    loaded[tid] = 0;
+    consumed[tid] = 0;
+  }
+  __syncthreads();  // the only workgroup barrier: the counters exist
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  grouped_tile(lid, tiles_m, tiles_n, group_m, tile_m, tile_n);
+  const int n0 = tile_n * BN, m0 = tile_m * BM;
+  const int kb = p.K >> 7;
+
+  if (wave >= MW) {  // ------------------------------------------------------------ loader waves
+    const bool xw = wave == MW;  // wave 8: activations (+ scales); wave 9: weights
+    const unsigned char* xsrc[XP];
+#pragma unroll
+    for (int q = 0; q < XP; ++q) {
+      const int row = min(m0 + q * 8 + (lane >> 3), p.M - 1);
+      const int chunk = (lane & 7) ^ mx_swz(((q & 1) << 2) + (lane >> 4));
+      xsrc[q] = p.x + (long)row * p.ldx + chunk * 16;
+    }
+    const unsigned char* wsrc = p.wmx + (long)(n0 >> 4) * kb * 2048 + lane * 16;
+    const unsigned char* ssrc[SP > 0 ? SP : 1];
+#pragma unroll
+    for (int q = 0; q < SP; ++q) ssrc[q] = p.xs + (long)min(m0 + q * 64 + lane, p.M - 1) * (p.K >> 5);
+    for (int st = 0; st < kb + AH; ++st) {
+      if (st < kb) {
+        const int buf = st % NS;
+        lds_wait_ge(&consumed[buf], MW * (st / NS));  // every MFMA wave is done with round st/NS - 1
+        char* base = smem + buf * SBYTES;
+        if (xw) {
+#pragma unroll
+          for (int q = 0; q < SP; ++q) glds4_8(ssrc[q] + st * 4, base + XBYTES + WBYTES + q * 256);
+#pragma unroll
+          for (int q = 0; q < XP; ++q) glds16_8(xsrc[q] + st * 128, base + q * 1024);
+        } else {
+#pragma unroll
+          for (int q = 0; q < WP; ++q)
+            glds16_8(wsrc + ((long)(q >> 1) * kb + st) * 2048 + (q & 1) * 1024, base + XBYTES + q * 1024);
+        }
+      }
+      const int done = st - AH;  // the stage whose loads must have landed now
+      if (done >= 0) {
+        // loads retire in issue order: with the later stages' pieces still allowed in flight
+        const int later = min(AH, kb - 1 - done);
+        if (xw) {
+          if (later >= 2) wait_vm8<2 * (XP + SP) < 64 ? 2 * (XP + SP) : 0>();
+          else if (later == 1) wait_vm8<XP + SP>();
+          else wait_vm8<0>();
+        } else {
+          if (later >= 2) wait_vm8<2 * WP < 64 ? 2 * WP : 0>();
+          else if (later == 1) wait_vm8<WP>();
+          else wait_vm8<0>();
+        }
+        if (lane == 0) lds_add(&loaded[done % NS]);
+      }
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------------------ MFMA waves
+  const int wn = wave % WN, wm = wave / WN;
+  const int lr = lane & 15, swz = mx_swz((lane >> 1) & 7);
+  const int brow = (wm * (BM / WM) + lr) * 128;
+  const int boff0 = brow + ((lane >> 4) ^ swz) * 16;
+  const int boff1 = brow + ((4 + (lane >> 4)) ^ swz) * 16;
+  const int aoff = XBYTES + (wn * FCW) * 2048 + lane * 16;
+  f32x4 acc[FCW][FPW];
+#pragma unroll
+  for (int i = 0; i < FCW; ++i)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int st = 0; st < kb; ++st) {
+    const int buf = st % NS;
+    lds_wait_ge(&loaded[buf], 2 * (st / NS + 1));  // both loader waves published stage st
+    const char* base = smem + buf * SBYTES;
+    i32x8 a[FCW], b[FPW];
+#pragma unroll
+    for (int i = 0; i < FCW; ++i) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + aoff + i * 2048 + 1024);
+      a[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(base + boff0 + j * 16 * 128);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(base + boff1 + j * 16 * 128);
+      b[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+    int sb[FPW];
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) {
+      if constexpr (XS) {
+        const int r = wm * (BM / WM) + j * 16 + (lane & 15);
+        sb[j] = *reinterpret_cast<const unsigned char*>(base + XBYTES + WBYTES + (r >> 6) * 256 + (r & 63) * 4 +
+                                                        (lane >> 4));
+      } else {
+        sb[j] = 0x7f7f7f7f;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the fragments are in registers: return the slot
+    if (lane == 0) lds_add(&consumed[buf]);
+#pragma unroll
+    for (int i = 0; i < FCW; ++i)
+#pragma unroll
+      for (int j = 0; j < FPW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                      sb[j]);
+  }
+  mx_epilogue<FCW, FPW>(p, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane);
+}
+
+template <int NS>
+int launch_mx_rs(const HzGemmFp8Params& p, hipStream_t st) {
+  if (p.N % 128) return -4;
+  const int tiles = (p.N / 128) * ((p.M + 127) / 128);
+  static const int group_env = getenv("HIPZAP_GEMM_GROUP") ? atoi(getenv("HIPZAP_GEMM_GROUP")) : 8;
+  const int group_m = group_env < 1 ? 1 : group_env;
+  if (p.xs) hipLaunchKernelGGL((gemm_mx_rs_kernel<NS, true>), dim3(tiles), dim3(640), 0, st, p, group_m);
+  else hipLaunchKernelGGL((gemm_mx_rs_kernel<NS, false>), dim3(tiles), dim3(640), 0, st, p, group_m);
+  return (int)hipGetLastError();
+}
+
 // Measured-negative MX schedules removed in round 5, their numbers committed: the
 // ping-pong 128x128 tile with two wave groups a phase apart (cfg 34-36, 1.4x slower than cfg 24,
 // profiles/r4_mx), the 256-row tiles with a branch-free main loop (cfg 43-45) and the ring-pipelined
@@ -506,6 +672,9 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       case 32: return launch_mx<128, 64, 4>(p, st);
       // 8-wave 256x256 tile of the plain kernel (all fragments read before the MFMAs)
       case 33: return launch_mx<256, 256, 2, 2, 4>(p, st);
+      // role-split 128x128 (8 MFMA waves + 2 loader waves, LDS FULL / FREE counters): 4 / 3 stages
+      case 40: return launch_mx_rs<4>(p, st);
+      case 41: return launch_mx_rs<3>(p, st);
       default: return -2;
     }
   }
