@@ -495,7 +495,7 @@ __global__ __launch_bounds__(64 * 10) void gemm_mx_rs_kernel(const HzGemmFp8Para
   constexpr int SBYTES = XBYTES + WBYTES + SCB;
   constexpr int XP = BM / 8, WP = NWG * 2, SP = XS ? BM / 64 : 0;
   constexpr int AH = NS - 2;  // stages a loader keeps in flight behind the one it publishes
-  static_assert(NS >= 3 && AH * (XP + SP) < 64 && AH * WP < 64, "vmcnt range");
+  static_assert(NS >= 2 && AH * (XP + SP) < 64 && AH * WP < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[NS * SBYTES];
   __shared__ int loaded[NS], consumed[NS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -675,6 +675,7 @@ extern "C" int hz_gemm_fp8_launch(const HzGemmFp8Params* pp, hipStream_t st) {
       // role-split 128x128 (8 MFMA waves + 2 loader waves, LDS FULL / FREE counters): 4 / 3 stages
       case 40: return launch_mx_rs<4>(p, st);
       case 41: return launch_mx_rs<3>(p, st);
+      case 42: return launch_mx_rs<2>(p, st);  // 66 KB of LDS: two workgroups (20 waves) per CU
       default: return -2;
     }
   }

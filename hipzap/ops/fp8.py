@@ -105,9 +105,10 @@ MX_TILES = {16: (128, 128), 17: (64, 128), 18: (128, 64), 19: (64, 64),
             # 33: 8-wave 256x256 (plain). Removed in round 5 with their negatives committed: 34-36
             # (ping-pong, profiles/r4_mx), 43-47 (256-row tiles, profiles/r3_mx256, r3_mxk)
             33: (256, 256),
-            # 40 / 41: role-split 128x128 (8 MFMA waves + 2 loader waves, LDS FULL / FREE counters), 4 / 3 stages
-            40: (128, 128), 41: (128, 128)}
-MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 40, 41)
+            # 40 / 41 / 42: role-split 128x128 (8 MFMA waves + 2 loader waves, LDS FULL / FREE counters), 4 / 3 / 2
+            # stages (profiles/r6_mx: 1.2-1.5x slower than cfg 24)
+            40: (128, 128), 41: (128, 128), 42: (128, 128)}
+MX_WIDE = (24, 25, 26, 27, 28, 29, 30, 33, 40, 41, 42)
 MX_PERROW_ONLY = ()
 MX_EXPERIMENTS = ()  # MX tiles that exist only in the HZ_EXPERIMENTS library: none left
 

@@ -122,7 +122,7 @@ def _mx_decode(q8: torch.Tensor, s8: torch.Tensor) -> torch.Tensor:
     return q8.view(torch.float8_e4m3fn).float() * sc
 
 
-@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 40, 41])
+@pytest.mark.parametrize("cfg", [16, 19, 21, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 40, 41, 42])
 @pytest.mark.parametrize("mx_in,mx_out", [(True, False), (False, True), (True, True)])
 def test_gemm_mx8_activations(cfg, mx_in, mx_out):
     """MX8 (e4m3 + E8M0 per 32 k) activations into the block-scaled MFMA, and MX8 output from
@@ -161,7 +161,7 @@ def test_gemm_mx8_activations(cfg, mx_in, mx_out):
         assert ((out.float().cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-2
 
 
-@pytest.mark.parametrize("cfg", [33, 40, 41])
+@pytest.mark.parametrize("cfg", [33, 40, 41, 42])
 @pytest.mark.parametrize("mx_in,mx_out", [(False, False), (True, True)])
 def test_gemm_mx256_bitwise_vs_128(cfg, mx_in, mx_out):
     """The plain 256x256 MX tile (cfg 33) sums every output over the same k-steps in the same order
@@ -304,7 +304,7 @@ def test_mfma_block_scale_kblock_map():
     assert all(m[(g, j)] == 2 * (j // 16) + g // 2 for g in range(4) for j in range(32)), m
 
 
-@pytest.mark.parametrize("cfg", [40, 41])
+@pytest.mark.parametrize("cfg", [40, 41, 42])
 @pytest.mark.parametrize("K", [128, 256, 384, 3072])
 def test_gemm_mx_role_split_short_and_long_k(cfg, K):
     """The role-split kernels' ring at fewer k-steps than stages (K 128 / 256 / 384: the loaders'
