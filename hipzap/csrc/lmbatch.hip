@@ -149,6 +149,19 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
       }
     }
   }
+  // the cell update's own operands (folded bias, previous cell state) need nothing computed here:
+  // the cell-update threads fetch them now, behind the weight and state loads, instead of after
+  // the MFMAs and the LDS reduction (one more memory round trip on the layer's critical path)
+  const bool upd = tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw && row_lane;
+  const int u_tt = tid / (NBW * 64), u_cb = (tid >> 6) % NBW, u_l = tid & 63;
+  const int u_j = (tile0 + u_tt) * 4 + (u_l >> 4), u_r = (cb0 + u_cb) * 16 + (u_l & 15);
+  const bool u_ok = upd && tile0 + u_tt < ntile && u_j < p.H;
+  f32x4 u_b = f32x4{0.f, 0.f, 0.f, 0.f};
+  float u_c = 0.f;
+  if (u_ok) {
+    u_b = *reinterpret_cast<const f32x4*>(p.bias + 4 * u_j);
+    u_c = p.c[(size_t)u_r * p.H + u_j];
+  }
   if constexpr (FIRST) {
     // ---- token of every row: the argmax of the acceptable keys of the last decoder (its
     // workgroups' atomic maxima, buffer of the other parity); the first workgroup clears this
@@ -218,23 +231,21 @@ __global__ __launch_bounds__(512) void lmb_layer_kernel(const HzLmbLayerParams p
   // ---- cell update: thread (tt, cb, l) owns unit 4*(tile0+tt) + (l >> 4) of request row
   // (cb0+cb)*16 + (l & 15); its 4 accumulator registers ARE the unit's gates i, f, g, o (C/D rows
   // 4(l>>4) .. +3)
-  if (tid < TPW * NBW * 64 && (tid >> 6) % NBW < nbw && row_lane) {
-    const int tt = tid / (NBW * 64), cb = (tid >> 6) % NBW, l = tid & 63;
+  if (upd) {
+    const int tt = u_tt, cb = u_cb, l = u_l;
     f32x4 g = part[0][tt][cb][l];
 #pragma unroll
     for (int w = 1; w < LW; ++w) g += part[w][tt][cb][l];  // fixed order: deterministic
-    const int j = (tile0 + tt) * 4 + (l >> 4), r = (cb0 + cb) * 16 + (l & 15);
-    if (tile0 + tt < ntile && j < p.H) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + 4 * j);
-      g += b;
+    const int j = u_j, r = u_r;
+    if (u_ok) {
+      g += u_b;
       if constexpr (EP) g += pe;
       const float si = 1.f / (1.f + __expf(-g[0]));
       const float sf = 1.f / (1.f + __expf(-g[1]));
       const float so = 1.f / (1.f + __expf(-g[3]));
-      float* cp = p.c + (size_t)r * p.H + j;
-      const float c_new = sf * *cp + si * tanhf(g[2]);
+      const float c_new = sf * u_c + si * tanhf(g[2]);
       const float h_new = so * tanhf(c_new);
-      *cp = c_new;
+      p.c[(size_t)r * p.H + j] = c_new;
       const __bf16 hi = (__bf16)h_new;
       const __bf16 lo = (__bf16)(h_new - (float)hi);
       bf16_t* dst = p.h + (size_t)((par ^ 1) * 2) * KSH * NB * 512 + st_off(j, r, NB);
@@ -338,6 +349,15 @@ __global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecP
   int woff[TW];
 #pragma unroll
   for (int t = 0; t < TW; ++t) woff[t] = (tile0 + t < t_hi ? (tile0 + t) * KS * 1024 : kOOB) + lane * 16;
+  // the epilogue's bias, fetched first (it needs nothing, and retiring first it never holds up the
+  // counted weight-chunk waits below): one memory round trip less after the last chunk
+  f32x4 bias_t[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int v0 = (tile0 + t) * 16 + (lane >> 4) * 4;
+    bias_t[t] = p.bias && tile0 + t < t_hi && v0 < p.V ? *reinterpret_cast<const f32x4*>(p.bias + v0)
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   u32x4 wr[TW][RR][CH];
   auto issue = [&](int slot, int c) {
 #pragma unroll
@@ -448,7 +468,7 @@ __global__ __launch_bounds__(64 * (16 / TW)) void lmb_dec_kernel(const HzLmbDecP
       const int v0 = (tile0 + t) * 16 + (lane >> 4) * 4;
       if (cb >= nba || tile0 + t >= t_hi || v0 >= p.V) continue;
       f32x4 lg = acc[t][cb];
-      if (p.bias) lg += *reinterpret_cast<const f32x4*>(p.bias + v0);
+      if (p.bias) lg += bias_t[t];
       if (p.logits && rec[cb])
 #pragma unroll
         for (int i = 0; i < 4; ++i)
