@@ -70,6 +70,13 @@ class Engine:
             tuned = load_tuning(model, batch, num_contexts)
         self.tuned = tuned
         self.num_contexts = num_contexts
+        # device-I/O engines are driven from their callers' streams (infer_device, DPPipeline): a
+        # wait between a caller's stream and a high-priority context stream is slow (the DP
+        # pipeline at shard 4: 11.1k vs 17.5-23.0k img/s, profiles/r6_queues), so under the
+        # default policy they keep torch's pooled streams; host-I/O engines (the request executor,
+        # the replay loop) take auto's choice
+        if stream_kind is None and not host_io and os.environ.get("HIPZAP_STREAM_KIND", "auto") == "auto":
+            stream_kind = "torch"
         self._stream_kind = stream_kind
         self._capture, self._zero_copy = capture, zero_copy
         n0 = num_contexts if eager_contexts is None else max(1, min(eager_contexts, num_contexts))
@@ -385,7 +392,9 @@ def stream_kind(num_contexts: int, kind: str | None = None) -> str:
     * ``hiprio_torch``: torch's high-priority pool; ``native``: fresh normal-priority streams;
       ``cumask``: a per-process pool of full-CU-mask streams (a queue each, but BLOCKING: a NULL-
       stream command waits for their work). Measured, not defaults.
-    * ``auto``: ``hiprio`` for engines of 2-4 contexts, ``torch`` otherwise -- 16 ResNet-50 bs=1
+    * ``auto``: ``hiprio`` for engines of 2-4 contexts (host-I/O engines only: ``Engine`` keeps a
+      device-I/O engine on ``torch``, whose callers' stream waits into a high-priority stream are
+      slow), ``torch`` otherwise -- 16 ResNet-50 bs=1
       contexts need the shared queues (16 queues of their own: 14.3k -> 7.4k inf/s; alternating
       them over the normal- and high-priority sets, 8 queues: 6.7k), and a
       DPPipeline over big batches does better on them too (``bench.py`` passes ``torch``)."""

@@ -33,7 +33,11 @@ def test_dedicated_queue_contexts_match_pooled_bitwise(monkeypatch):
     ref_eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=1)
     ref = ref_eng.infer(x)
     monkeypatch.delenv("HIPZAP_STREAM_KIND")
-    eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=3, host_io=False)
+    # a device-I/O engine keeps torch's pooled streams by default (its callers' stream waits)
+    eng_d = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=3, host_io=False)
+    assert not any(isinstance(s, torch.cuda.ExternalStream) for s in eng_d.streams)
+    del eng_d
+    eng = Engine.from_state_dict("resnet18", sd, DEV, batch=2, num_contexts=3, host_io=False, stream_kind="hiprio")
     # high-priority streams of its own (HIP's separate queue set for that priority)
     assert all(isinstance(s, torch.cuda.ExternalStream) for s in eng.streams)
     assert len({s.cuda_stream for s in eng.streams}) == 3
