@@ -187,6 +187,7 @@ def _load():
     _sig(lib, "hz_plan_open", P, C.c_char_p, c_int, c_int, C.POINTER(D))
     _sig(lib, "hz_plan_add_contexts", c_int, P, c_int, c_int)
     _sig(lib, "hz_plan_num_contexts", c_int, P)
+    _sig(lib, "hz_plan_set_stream_priority", None, P, c_int)
     _sig(lib, "hz_plan_timings", None, P, C.POINTER(D))
     _sig(lib, "hz_plan_blob", P, P, C.POINTER(U64))
     _sig(lib, "hz_plan_host", P, P, c_int)

@@ -586,6 +586,8 @@ const char* hz_plan_last_error(void);
 void* hz_plan_open(const char* path, int device, int read_blob, double* timings);
 int hz_plan_add_contexts(void* plan, int n, int capture);
 int hz_plan_num_contexts(void* plan);
+// contexts added after this call (except one on the upload stream) get highest-priority streams
+void hz_plan_set_stream_priority(void* plan, int high);
 void hz_plan_timings(void* plan, double* out);
 void* hz_plan_blob(void* plan, uint64_t* bytes);
 void* hz_plan_host(void* plan, int ctx);

@@ -166,6 +166,10 @@ struct Plan {
   hipStream_t spare = nullptr;  // the upload stream, handed to the first context (stream creation is
                                 // ~10-25 ms of lazy runtime work in a fresh process)
   hipStream_t cap_st = nullptr;  // private capture stream for contexts on borrowed streams
+  // hz_plan_set_stream_priority: contexts after the first get fresh highest-priority streams (HIP
+  // keeps a separate set of hardware queues per priority: 2-4 contexts land on distinct queues;
+  // engine.py stream_kind, profiles/r6_queues)
+  bool prio_high = false;
   std::mutex cap_mu;
   std::thread warm;  // device-code warm-up, joined before hz_plan_open returns
   void join_warm() {
@@ -423,6 +427,10 @@ struct Plan {
       } else if (spare) {
         c.st = spare;
         spare = nullptr;
+      } else if (prio_high) {
+        int lo = 0, hi = 0;
+        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&c.st, hipStreamNonBlocking, hi);
       } else {
         e = hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking);
       }
@@ -637,6 +645,8 @@ int hz_plan_add_contexts(void* h, int n, int capture) {
   if (hipSetDevice(P(h)->device) != hipSuccess) return fail("plan: hipSetDevice failed");
   return P(h)->add_contexts(n, capture);
 }
+
+void hz_plan_set_stream_priority(void* h, int high) { P(h)->prio_high = high != 0; }
 
 int hz_plan_num_contexts(void* h) {
   std::lock_guard<std::mutex> g(P(h)->mu);

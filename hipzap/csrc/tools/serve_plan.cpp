@@ -168,6 +168,11 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  {  // 2-4 request contexts on highest-priority streams: distinct hardware queues (engine.py stream_kind)
+    const char* k = std::getenv("HIPZAP_STREAM_KIND");
+    const std::string kind = k ? k : "auto";
+    if (kind == "hiprio" || (kind == "auto" && contexts >= 2 && contexts <= 4)) hz_plan_set_stream_priority(plan, 1);
+  }
   if (hz_plan_add_contexts(plan, contexts, 1)) return die("contexts");
   std::vector<HzProgram> progs(contexts);
   std::vector<hipStream_t> streams(contexts);
