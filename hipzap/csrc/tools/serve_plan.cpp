@@ -168,10 +168,10 @@ int main(int argc, char** argv) {
     return 0;
   }
 
-  {  // 2-4 request contexts on highest-priority streams: distinct hardware queues (engine.py stream_kind)
+  {  // HIPZAP_STREAM_KIND=hiprio: contexts after the first on highest-priority streams (opt-in: a
+     // mix of one normal- and several high-priority queues measured slower, profiles/r6_queues)
     const char* k = std::getenv("HIPZAP_STREAM_KIND");
-    const std::string kind = k ? k : "auto";
-    if (kind == "hiprio" || (kind == "auto" && contexts >= 2 && contexts <= 4)) hz_plan_set_stream_priority(plan, 1);
+    if (k && std::string(k) == "hiprio") hz_plan_set_stream_priority(plan, 1);
   }
   if (hz_plan_add_contexts(plan, contexts, 1)) return die("contexts");
   std::vector<HzProgram> progs(contexts);

@@ -169,10 +169,11 @@ class PlanEngine:
         self.num_contexts = contexts
         self._capture = bool(capture)
         self._lazy = capture == "lazy"
-        # the request contexts' streams, as engine.py stream_kind decides for a host-I/O engine
-        # (torch-free here): 2-4 contexts -> highest-priority streams, distinct hardware queues
-        kind = os.environ.get("HIPZAP_STREAM_KIND", "auto")
-        if kind == "hiprio" or (kind == "auto" and 2 <= contexts <= 4 and self.meta.get("host_io", True)):
+        # HIPZAP_STREAM_KIND=hiprio: the contexts after the first (which takes the upload stream)
+        # on highest-priority streams. Not the default here: with the first context on a
+        # normal-priority queue and the rest on high-priority ones, the BERT text plan's 4
+        # contexts replay at 16.3k seq/s against 22.5k on plain streams (profiles/r6_queues)
+        if os.environ.get("HIPZAP_STREAM_KIND", "auto") == "hiprio":
             L.hz_plan_set_stream_priority(h, 1)
         n0 = contexts if eager_contexts is None else max(1, min(eager_contexts, contexts))
         self._check(L.hz_plan_add_contexts(h, n0, 0 if self._lazy else int(bool(capture))), "add_contexts")
